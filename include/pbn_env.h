@@ -1,0 +1,151 @@
+/*
+ * pbn_env.h -- C-ABI of the MI355X batched PBN environment step (libpbn_env.so).
+ *
+ * This is the drop-in boundary for the gym-PBN state-transition hot path that
+ * jakub-zarzycki2022/pbn-rl drives.  The reference binds no native code: it
+ * calls the external Python package gym_PBN (requirements.txt:11,
+ * gym-PBN[vis]==1.1.1 + an unpublished fork) through gymnasium:
+ *
+ *   gym.make("gym-PBN/PBNEnv", N=, genes=, logic_functions=[, min_attractors=])
+ *        train_assa_BQN.py:121-124, model_tester.py:409-413     -> pbn_net_create
+ *   env.reset() -> ((state, target), info)
+ *        bdq_model/__init__.py:161,204                         -> pbn_reset
+ *   env.step(actions) -> (obs, reward, terminated, truncated, info)
+ *        bdq_model/__init__.py:177, graph_classifier/__init__.py:148,
+ *        model_tester.py:561,624, ddqn_per/__init__.py:354     -> pbn_step
+ *   env.close()  train_BDQ.py:116                              -> pbn_net_destroy
+ *
+ * The Python facade (pbn_rl_amd.env.PBNEnv / pbn_rl_amd.vector_env.VectorPBNEnv)
+ * keeps that gym surface and calls these entry points through ctypes;
+ * INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - every entry point returns 0 or a negative PBN_E* code; pbn_last_error()
+ *     returns a thread-local message for the last failure on the calling thread;
+ *   - the caller owns every device buffer (plain device pointers, e.g. from
+ *     torch tensors); a pbn_net owns only its device-resident tables;
+ *   - calls are asynchronous on the caller's HIP stream (hipStream_t passed as
+ *     void*; NULL = the default stream); no entry point synchronises, allocates
+ *     or frees inside pbn_reset/pbn_step, so both can be captured in a hipGraph;
+ *   - a pbn_net is bound to the device that was current at create time and is
+ *     not thread-safe: use one per GPU / process;
+ *   - envs are processed in groups of 32 consecutive envs (bit-sliced layout):
+ *     n_envs and env_offset must be multiples of 32.  Randomness depends only
+ *     on (seed, global env id = env_offset + local id, step), so sharding envs
+ *     across GPUs gives bit-identical results.
+ *
+ * Device data layout for n envs with W = ceil(n_nodes / 32) state words:
+ *   state, flipmask          uint32 [W][n]   (SoA word planes; bit i of word w = node 32w+i)
+ *   target                   uint8  [n]      (attractor id; 0xFF = none)
+ *   t                        uint8  [n]      (steps taken in the current episode)
+ *   reward                   float  [n]
+ *   flags                    uint8  [n]      (PBN_FLAG_* bits)
+ *
+ * Step semantics: DESIGN.md "Step semantics" (frozen; gym_PBN is unavailable).
+ */
+#ifndef PBN_ENV_H
+#define PBN_ENV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PBN_ABI_VERSION 1
+
+#define PBN_MAX_NODES 128
+#define PBN_MAX_ARITY 4
+#define PBN_MAX_FUNCS_PER_NODE 16
+#define PBN_MAX_ATTRACTORS 254
+#define PBN_NO_TARGET 0xFF
+
+/* error codes */
+#define PBN_OK 0
+#define PBN_EINVAL (-22)
+#define PBN_ENOMEM (-12)
+#define PBN_EDEVICE (-5)
+
+/* pbn_step mode bits */
+#define PBN_MODE_AUTORESET 1u      /* done envs restart: state_out/target/t hold the new episode */
+#define PBN_MODE_RANDOM_ACTIONS 2u /* actions drawn in-kernel (3 uniform ints in [0,N], 0 = no-op,
+                                      bdq_model/__init__.py:76); flipmask is an OUTPUT */
+
+/* flags bits */
+#define PBN_FLAG_TERMINATED 1u     /* s' is a state of the env's target attractor */
+#define PBN_FLAG_TRUNCATED 2u      /* t' == horizon */
+#define PBN_FLAG_IN_ATTRACTOR 4u   /* s' is a state of some attractor */
+#define PBN_FLAG_PERTURBED 8u      /* a perturbation fired this step */
+#define PBN_FLAG_RESET 16u         /* autoreset happened: state_out is a fresh start */
+
+/*
+ * Network description (semantic form; the library derives its kernel encodings).
+ * Function f of node i (node_func_start[i] <= f < node_func_start[i+1]) has
+ * func_arity[f] <= 4 inputs func_inputs[4f..4f+arity) (node indices) and truth
+ * table func_table[f]: bit m = value when input j = bit j of m.
+ * func_threshold[f] is the cumulative selection threshold c_f in units of
+ * 2^-prob_bits (strictly: c_{f-1} <= c_f, last of a node == 2^prob_bits).
+ * perturb_cdf[m-1] = floor(2^32 * (1 - (1-p)^m)), m = 1..n_nodes.
+ * Attractor a owns states attractor_start[a] .. attractor_start[a+1]-1; state k
+ * is words attractor_states[k*W .. k*W+W).  reward_table[(2*term + wrong)*(N+1) + k]
+ * with k = popcount(flipmask), wrong = in some non-target attractor.
+ */
+typedef struct pbn_net_desc {
+  int32_t n_nodes;
+  int32_t n_funcs;
+  int32_t prob_bits;     /* 4, 8, 12 or 16 */
+  int32_t horizon;       /* 0 = no truncation, else 1..255 */
+  const int32_t* node_func_start;   /* [n_nodes + 1] */
+  const int32_t* func_arity;        /* [n_funcs] */
+  const int32_t* func_inputs;       /* [n_funcs * 4], unused slots -1 */
+  const uint32_t* func_table;       /* [n_funcs] */
+  const uint32_t* func_threshold;   /* [n_funcs] */
+  const uint32_t* perturb_cdf;      /* [n_nodes] */
+  int32_t n_attractors;             /* 0..254 */
+  int32_t n_attractor_states;
+  const int32_t* attractor_start;   /* [n_attractors + 1] */
+  const uint32_t* attractor_states; /* [n_attractor_states * W] */
+  const float* reward_table;        /* [4 * (n_nodes + 1)] */
+} pbn_net_desc;
+
+typedef struct pbn_net pbn_net;
+
+/* Compile + upload the tables to the current device. */
+int pbn_net_create(const pbn_net_desc* desc, pbn_net** out);
+int pbn_net_destroy(pbn_net* net);
+/* W = state words per env. */
+int pbn_net_words(const pbn_net* net);
+
+/*
+ * Start episodes for envs [env_offset, env_offset + n_envs): state uniform over
+ * the states of a uniformly drawn attractor, target a different attractor
+ * (or a uniform random state and PBN_NO_TARGET when there are no attractors),
+ * t = 0.  Draws are keyed by (seed, global env id, step).
+ */
+int pbn_reset(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs,
+              uint32_t* d_state, uint8_t* d_target, uint8_t* d_t, void* stream);
+
+/*
+ * One synchronous PBN transition of every env (the hot path).
+ *   d_state        in   [W][n]  current observation s
+ *   d_flipmask     in   [W][n]  intervention flips (bit a-1 for action a > 0);
+ *                  out  with PBN_MODE_RANDOM_ACTIONS (the actions drawn)
+ *   d_target       in/out [n]   rewritten only for envs that autoreset
+ *   d_t            in/out [n]
+ *   d_state_out    out  [W][n]  next observation (reset state for autoreset envs)
+ *   d_final_state  out  [W][n]  s' (the transition result) -- may be NULL
+ *   d_reward, d_flags  out [n]
+ * d_state_out must not alias d_state.
+ */
+int pbn_step(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs,
+             uint32_t mode, const uint32_t* d_state, uint32_t* d_flipmask, uint8_t* d_target,
+             uint8_t* d_t, uint32_t* d_state_out, uint32_t* d_final_state, float* d_reward,
+             uint8_t* d_flags, void* stream);
+
+const char* pbn_last_error(void);
+int pbn_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PBN_ENV_H */

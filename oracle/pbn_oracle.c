@@ -1,0 +1,257 @@
+/*
+ * pbn_oracle.c -- CPU restatement of the batched PBN env step.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity checker for the HIP path
+ * in pbn_rl_amd/csrc: only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it.  The product path never links or calls it.
+ *
+ * What it restates.  The reference's env step lives in the external package
+ * gym_PBN (requirements.txt:11), which is absent from /root/reference and not
+ * installed, so the transition itself is PARITY-UNPINNED by the reference; it
+ * follows the frozen semantics of DESIGN.md "Step semantics" (SURVEY.md
+ * Appendix C).  The parts that are pinned by the reference are cited inline:
+ *   - action encoding 0 = no-op, a > 0 flips node a-1, duplicates removed
+ *     (bdq_model/__init__.py:76-84,176);
+ *   - per-node probabilistic rule selection among weighted functions
+ *     (weights as passed at train_assa_BQN.py:109,121-124);
+ *   - truncation at horizon (train_BDQ.py:50, counted at bdq_model/__init__.py:179-180);
+ *   - termination = s' in the target attractor (model_tester.py:616 in_target);
+ *   - wildcard '*' -> 0 in attractor states (model_tester.py:609), applied by
+ *     the Python side before it builds the descriptor.
+ * Philox4x32-10 follows the Random123 definition (Salmon et al., SC'11); it is
+ * pinned by known-answer vectors and by rocRAND's philox4x32_10 engine in
+ * tests/test_philox.py.
+ *
+ * Written for clarity: scalar per env, the group selection words recomputed
+ * per group of 32 envs (the unit the semantics defines), OpenMP over groups.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "../include/pbn_env.h"
+
+enum { STREAM_SEL = 0, STREAM_ENV = 1, STREAM_PERT = 2, STREAM_RESET = 3 };
+
+static void philox4x32_10(const uint32_t ctr_in[4], uint32_t k0, uint32_t k1, uint32_t out[4]) {
+  uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+  for (int r = 0; r < 10; ++r) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    uint32_t n1 = (uint32_t)p1;
+    uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    uint32_t n3 = (uint32_t)p0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  philox4x32_10(ctr, key[0], key[1], out);
+}
+
+static void draw(uint64_t seed, uint64_t id, uint64_t step, uint32_t stream, uint32_t idx,
+                 uint32_t out[4]) {
+  uint32_t ctr[4];
+  ctr[0] = (uint32_t)id;
+  ctr[1] = (uint32_t)step;
+  ctr[2] = (stream << 28) | (idx & 0x0FFFFFFFu);
+  ctr[3] = (uint32_t)((id >> 32) & 0xFFFFu) | (uint32_t)(((step >> 32) & 0xFFFFu) << 16);
+  philox4x32_10(ctr, (uint32_t)seed, (uint32_t)(seed >> 32), out);
+}
+
+static int words_of(int n) { return (n + 31) / 32; }
+
+static int gap_of(const pbn_net_desc* d, uint32_t u) {
+  /* smallest m in 1..N with u < C[m]; N+1 if none */
+  for (int m = 1; m <= d->n_nodes; ++m)
+    if (u < d->perturb_cdf[m - 1]) return m;
+  return d->n_nodes + 1;
+}
+
+static int eval_func(const pbn_net_desc* d, int f, const uint32_t* s) {
+  int k = d->func_arity[f];
+  uint32_t m = 0;
+  for (int j = 0; j < k; ++j) {
+    int g = d->func_inputs[4 * f + j];
+    m |= ((s[g >> 5] >> (g & 31)) & 1u) << j;
+  }
+  return (int)((d->func_table[f] >> m) & 1u);
+}
+
+/* attractor id of state s, or -1 */
+static int attractor_of(const pbn_net_desc* d, const uint32_t* s, int W) {
+  for (int a = 0; a < d->n_attractors; ++a) {
+    for (int k = d->attractor_start[a]; k < d->attractor_start[a + 1]; ++k) {
+      int eq = 1;
+      for (int w = 0; w < W; ++w)
+        if (d->attractor_states[(size_t)k * W + w] != s[w]) { eq = 0; break; }
+      if (eq) return a;
+    }
+  }
+  return -1;
+}
+
+static void valid_mask(int n, int W, uint32_t* m) {
+  for (int w = 0; w < W; ++w) {
+    int bits = n - 32 * w;
+    m[w] = bits >= 32 ? 0xFFFFFFFFu : (bits <= 0 ? 0u : ((1u << bits) - 1u));
+  }
+}
+
+/* reset formula shared by pbn_reset (word from STREAM_RESET call 0) and autoreset (E2) */
+static void reset_one(const pbn_net_desc* d, uint64_t seed, uint64_t e, uint64_t step, uint32_t R,
+                      uint32_t* state, uint8_t* target) {
+  int N = d->n_nodes, W = words_of(N), A = d->n_attractors;
+  uint32_t vm[4];
+  valid_mask(N, W, vm);
+  if (A >= 1) {
+    uint32_t as = (uint32_t)(((uint64_t)(R & 1023u) * (uint32_t)A) >> 10);
+    int start = d->attractor_start[as];
+    uint32_t size = (uint32_t)(d->attractor_start[as + 1] - start);
+    uint32_t idx = (uint32_t)(((uint64_t)((R >> 20) & 4095u) * size) >> 12);
+    for (int w = 0; w < W; ++w) state[w] = d->attractor_states[(size_t)(start + idx) * W + w];
+    uint32_t at = as;
+    if (A >= 2) {
+      at = (uint32_t)(((uint64_t)((R >> 10) & 1023u) * (uint32_t)(A - 1)) >> 10);
+      at += (at >= as);
+    }
+    *target = (uint8_t)at;
+  } else {
+    uint32_t r[4];
+    draw(seed, e, step, STREAM_RESET, 1, r);
+    for (int w = 0; w < W; ++w) state[w] = r[w] & vm[w];
+    *target = PBN_NO_TARGET;
+  }
+}
+
+int oracle_reset(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t env_offset,
+                 int64_t n, uint32_t* state, uint8_t* target, uint8_t* t) {
+  int W = words_of(d->n_nodes);
+  for (int64_t i = 0; i < n; ++i) {
+    uint64_t e = env_offset + (uint64_t)i;
+    uint32_t r[4], s[4];
+    draw(seed, e, step, STREAM_RESET, 0, r);
+    reset_one(d, seed, e, step, r[0], s, &target[i]);
+    for (int w = 0; w < W; ++w) state[(size_t)w * n + i] = s[w];
+    t[i] = 0;
+  }
+  return 0;
+}
+
+int oracle_step(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n,
+                uint32_t mode, const uint32_t* state, uint32_t* flipmask, uint8_t* target, uint8_t* t,
+                uint32_t* state_out, uint32_t* final_state, float* reward, uint8_t* flags,
+                int n_threads) {
+  const int N = d->n_nodes, W = words_of(N), B = d->prob_bits;
+  if ((env_offset & 31u) || (n & 31)) return PBN_EINVAL;
+  const int64_t n_groups = n / 32;
+#ifdef _OPENMP
+  if (n_threads > 0) omp_set_num_threads(n_threads);
+#pragma omp parallel for schedule(static)
+#endif
+  for (int64_t g = 0; g < n_groups; ++g) {
+    const uint64_t G = (env_offset >> 5) + (uint64_t)g;
+    /* selection digit words of this group: D[i][d], digit d = 0 is the MSB of u */
+    uint32_t D[PBN_MAX_NODES][16];
+    for (int i = 0; i < N; ++i) {
+      int nf = d->node_func_start[i + 1] - d->node_func_start[i];
+      if (nf < 2) continue;
+      for (int c = 0; c < B / 4; ++c) draw(seed, G, step, STREAM_SEL, (uint32_t)(4 * i + c), &D[i][4 * c]);
+    }
+    for (int b = 0; b < 32; ++b) {
+      const int64_t li = g * 32 + b;
+      const uint64_t e = env_offset + (uint64_t)li;
+      uint32_t vm[4], s[4] = {0, 0, 0, 0}, m[4] = {0, 0, 0, 0}, s1[4], gam[4] = {0, 0, 0, 0},
+               sp[4] = {0, 0, 0, 0};
+      valid_mask(N, W, vm);
+      uint32_t E[4];
+      draw(seed, e, step, STREAM_ENV, 0, E);
+      for (int w = 0; w < W; ++w) s[w] = state[(size_t)w * n + li] & vm[w];
+      /* 1-2. interventions: 0 = no-op, a > 0 flips node a-1, each distinct node once
+       *      (bdq_model/__init__.py:76-84 explore branch, :176 action.unique()) */
+      if (mode & PBN_MODE_RANDOM_ACTIONS) {
+        for (int k = 0; k < 3; ++k) {
+          uint32_t a = (uint32_t)(((uint64_t)((E[3] >> (10 * k)) & 1023u) * (uint32_t)(N + 1)) >> 10);
+          if (a > 0) m[(a - 1) >> 5] |= 1u << ((a - 1) & 31);
+        }
+        for (int w = 0; w < W; ++w) flipmask[(size_t)w * n + li] = m[w];
+      } else {
+        for (int w = 0; w < W; ++w) m[w] = flipmask[(size_t)w * n + li] & vm[w];
+      }
+      for (int w = 0; w < W; ++w) s1[w] = s[w] ^ m[w];
+      /* 3. perturbation: gaps between flipped nodes are geometric(p) draws */
+      {
+        int pos = -1, k = 0;
+        uint32_t P[4];
+        while (pos < N - 1) {
+          uint32_t u;
+          if (k == 0) u = E[0];
+          else if (k == 1) u = E[1];
+          else {
+            if (((k - 2) & 3) == 0) draw(seed, e, step, STREAM_PERT, (uint32_t)((k - 2) >> 2), P);
+            u = P[(k - 2) & 3];
+          }
+          ++k;
+          pos += gap_of(d, u);
+          if (pos >= N) break;
+          gam[pos >> 5] |= 1u << (pos & 31);
+        }
+      }
+      int perturbed = 0;
+      for (int w = 0; w < W; ++w) perturbed |= gam[w] != 0;
+      /* 4. transition */
+      if (perturbed) {
+        for (int w = 0; w < W; ++w) sp[w] = s1[w] ^ gam[w];
+      } else {
+        for (int i = 0; i < N; ++i) {
+          int f0 = d->node_func_start[i], nf = d->node_func_start[i + 1] - f0, x;
+          if (nf == 1) {
+            x = eval_func(d, f0, s1);
+          } else {
+            uint32_t u = 0;
+            for (int dd = 0; dd < B; ++dd) u |= ((D[i][dd] >> b) & 1u) << (B - 1 - dd);
+            int j = 0;
+            while (j < nf - 1 && !(u < d->func_threshold[f0 + j])) ++j;
+            x = eval_func(d, f0 + j, s1);
+          }
+          if (x) sp[i >> 5] |= 1u << (i & 31);
+        }
+      }
+      /* 5. reward / termination */
+      int a = attractor_of(d, sp, W);
+      int in_attr = a >= 0;
+      int term = in_attr && (uint32_t)a == target[li];
+      int tt = t[li] + 1;
+      if (tt > 255) tt = 255;
+      int trunc = d->horizon > 0 && tt >= d->horizon;
+      int wrong = in_attr && !term;
+      int pc = 0;
+      for (int w = 0; w < W; ++w) pc += __builtin_popcount(m[w]);
+      reward[li] = d->reward_table[(2 * term + wrong) * (N + 1) + pc];
+      uint8_t fl = (uint8_t)(term | (trunc << 1) | (in_attr << 2) | (perturbed << 3));
+      if (final_state)
+        for (int w = 0; w < W; ++w) final_state[(size_t)w * n + li] = sp[w];
+      if ((mode & PBN_MODE_AUTORESET) && (term || trunc)) {
+        uint32_t ns[4];
+        uint8_t tg;
+        reset_one(d, seed, e, step, E[2], ns, &tg);
+        for (int w = 0; w < W; ++w) state_out[(size_t)w * n + li] = ns[w];
+        target[li] = tg;
+        t[li] = 0;
+        fl |= PBN_FLAG_RESET;
+      } else {
+        for (int w = 0; w < W; ++w) state_out[(size_t)w * n + li] = sp[w];
+        t[li] = (uint8_t)tt;
+      }
+      flags[li] = fl;
+    }
+  }
+  return 0;
+}

@@ -1,0 +1,140 @@
+"""Pure-Python, one-env-at-a-time restatement of the step (gym-PBN style).
+
+TEST INFRASTRUCTURE ONLY.  Second, independent restatement of DESIGN.md
+"Step semantics": it works from the compiled ``Network`` objects (per-node
+function lists, boolean tables) rather than from the C descriptor, so agreement
+with oracle/pbn_oracle.c also checks the descriptor encoding.  It is slow by
+construction (per-node Python loop, like the external gym_PBN step the
+reference calls at bdq_model/__init__.py:177) and doubles as the
+"reference-style Python" CPU baseline in bench.py.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Sequence, Tuple
+
+M0, M1 = 0xD2511F53, 0xCD9E8D57
+W0, W1 = 0x9E3779B9, 0xBB67AE85
+MASK32 = 0xFFFFFFFF
+SEL, ENV, PERT, RESET = 0, 1, 2, 3
+MODE_AUTORESET, MODE_RANDOM_ACTIONS = 1, 2
+
+
+def philox4x32_10(ctr: Sequence[int], key: Sequence[int]) -> Tuple[int, int, int, int]:
+    c0, c1, c2, c3 = (int(x) & MASK32 for x in ctr)
+    k0, k1 = int(key[0]) & MASK32, int(key[1]) & MASK32
+    for _ in range(10):
+        p0 = M0 * c0
+        p1 = M1 * c2
+        c0, c1, c2, c3 = ((p1 >> 32) ^ c1 ^ k0) & MASK32, p1 & MASK32, ((p0 >> 32) ^ c3 ^ k1) & MASK32, p0 & MASK32
+        k0 = (k0 + W0) & MASK32
+        k1 = (k1 + W1) & MASK32
+    return c0, c1, c2, c3
+
+
+def draw(seed: int, ident: int, step: int, stream: int, idx: int):
+    ctr = (ident & MASK32, step & MASK32, (stream << 28) | (idx & 0x0FFFFFFF),
+           ((ident >> 32) & 0xFFFF) | (((step >> 32) & 0xFFFF) << 16))
+    return philox4x32_10(ctr, (seed & MASK32, (seed >> 32) & MASK32))
+
+
+class PyPBN:
+    """Scalar env semantics over an EnvSpec (network + attractors + constants)."""
+
+    def __init__(self, spec):
+        self.spec = spec
+        self.net = spec.network
+        self.n = self.net.n
+        self.thr = self.net.thresholds(spec.prob_bits)
+        self.cdf = [int(x) for x in spec.arrays["perturb_cdf"]]
+        self.att_of: Dict[Tuple[int, ...], int] = {}
+        for a, att in enumerate(spec.attractors):
+            for s in att:
+                self.att_of[tuple(s)] = a
+
+    def gap(self, u: int) -> int:
+        for m in range(1, self.n + 1):
+            if u < self.cdf[m - 1]:
+                return m
+        return self.n + 1
+
+    def reset_from_word(self, seed: int, e: int, step: int, R: int):
+        A = len(self.spec.attractors)
+        if A >= 1:
+            a_s = ((R & 1023) * A) >> 10
+            att = self.spec.attractors[a_s]
+            idx = (((R >> 20) & 4095) * len(att)) >> 12
+            state = list(att[idx])
+            a_t = a_s
+            if A >= 2:
+                a_t = (((R >> 10) & 1023) * (A - 1)) >> 10
+                a_t += a_t >= a_s
+            return state, a_t
+        r = draw(seed, e, step, RESET, 1)
+        bits = [(r[i >> 5] >> (i & 31)) & 1 for i in range(self.n)]
+        return bits, 0xFF
+
+    def reset(self, seed: int, step: int, e: int):
+        R = draw(seed, e, step, RESET, 0)[0]
+        state, tgt = self.reset_from_word(seed, e, step, R)
+        return state, tgt, 0
+
+    def step(self, seed: int, step: int, e: int, state: List[int], flip: List[int], target: int, t: int,
+             mode: int):
+        n, B = self.n, self.spec.prob_bits
+        G, b = e >> 5, e & 31
+        E = draw(seed, e, step, ENV, 0)
+        if mode & MODE_RANDOM_ACTIONS:
+            flip = [0] * n
+            for k in range(3):
+                a = (((E[3] >> (10 * k)) & 1023) * (n + 1)) >> 10
+                if a > 0:
+                    flip[a - 1] = 1  # each distinct node once (bdq_model/__init__.py:81-84,176)
+        s1 = [state[i] ^ flip[i] for i in range(n)]
+        gamma = [0] * n
+        pos, k, P = -1, 0, None
+        while pos < n - 1:
+            if k == 0:
+                u = E[0]
+            elif k == 1:
+                u = E[1]
+            else:
+                if (k - 2) % 4 == 0:
+                    P = draw(seed, e, step, PERT, (k - 2) // 4)
+                u = P[(k - 2) % 4]
+            k += 1
+            pos += self.gap(u)
+            if pos >= n:
+                break
+            gamma[pos] = 1
+        perturbed = any(gamma)
+        if perturbed:
+            sp = [s1[i] ^ gamma[i] for i in range(n)]
+        else:
+            sp = []
+            for i, fl in enumerate(self.net.nodes):
+                if len(fl) == 1:
+                    j = 0
+                else:
+                    u = 0
+                    for d in range(B):
+                        word = draw(seed, G, step, SEL, 4 * i + (d >> 2))[d & 3]
+                        u |= ((word >> b) & 1) << (B - 1 - d)
+                    j = 0
+                    while j < len(fl) - 1 and not (u < self.thr[i][j]):
+                        j += 1
+                sp.append(fl[j](s1))
+        a = self.att_of.get(tuple(sp), -1)
+        in_attr = a >= 0
+        term = in_attr and a == target
+        tt = min(t + 1, 255)
+        trunc = self.spec.horizon > 0 and tt >= self.spec.horizon
+        wrong = in_attr and not term
+        reward = self.spec.reward_value(term, wrong, sum(flip))
+        flags = int(term) | (int(trunc) << 1) | (int(in_attr) << 2) | (int(perturbed) << 3)
+        out = {"final_state": sp, "reward": reward, "flipmask": flip, "target": target}
+        if (mode & MODE_AUTORESET) and (term or trunc):
+            ns, tg = self.reset_from_word(seed, e, step, E[2])
+            out.update(state_out=ns, target=tg, t=0, flags=flags | 16)
+        else:
+            out.update(state_out=sp, t=tt, flags=flags)
+        return out

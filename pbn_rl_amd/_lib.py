@@ -1,0 +1,100 @@
+"""ctypes binding of libpbn_env.so (include/pbn_env.h).
+
+The HIP library is the only compute path: if it is missing or fails to load,
+every entry point raises -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from typing import Optional
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpbn_env.so")
+SRC_DIR = os.path.join(HERE, "csrc")
+INCLUDE_DIR = os.path.join(HERE, "..", "include")
+
+MODE_AUTORESET = 1
+MODE_RANDOM_ACTIONS = 2
+FLAG_TERMINATED = 1
+FLAG_TRUNCATED = 2
+FLAG_IN_ATTRACTOR = 4
+FLAG_PERTURBED = 8
+FLAG_RESET = 16
+
+EXPORTS = ["pbn_net_create", "pbn_net_destroy", "pbn_net_words", "pbn_reset", "pbn_step",
+           "pbn_last_error", "pbn_abi_version"]
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+class PbnError(RuntimeError):
+    pass
+
+
+def build(verbose: bool = False) -> str:
+    """Compile csrc/pbn_env.hip for gfx950 into pbn_rl_amd/libpbn_env.so (in-tree)."""
+    src = os.path.join(SRC_DIR, "pbn_env.hip")
+    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wno-unused-result", "-o", LIB_PATH + ".tmp", src]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    return LIB_PATH
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise PbnError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u64, i64, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64, ctypes.c_uint32
+    L.pbn_net_create.argtypes = [vp, ctypes.POINTER(vp)]
+    L.pbn_net_create.restype = ctypes.c_int
+    L.pbn_net_destroy.argtypes = [vp]
+    L.pbn_net_destroy.restype = ctypes.c_int
+    L.pbn_net_words.argtypes = [vp]
+    L.pbn_net_words.restype = ctypes.c_int
+    L.pbn_reset.argtypes = [vp, u64, u64, u64, i64, vp, vp, vp, vp]
+    L.pbn_reset.restype = ctypes.c_int
+    L.pbn_step.argtypes = [vp, u64, u64, u64, i64, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.pbn_step.restype = ctypes.c_int
+    L.pbn_last_error.argtypes = []
+    L.pbn_last_error.restype = ctypes.c_char_p
+    L.pbn_abi_version.argtypes = []
+    L.pbn_abi_version.restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().pbn_last_error().decode(errors="replace")
+        raise PbnError(f"{what} failed ({rc}): {msg}")
+
+
+class NetHandle:
+    """Owns one pbn_net (device tables) on the current device."""
+
+    def __init__(self, spec):
+        L = load()
+        self.spec = spec
+        h = ctypes.c_void_p()
+        check(L.pbn_net_create(ctypes.addressof(spec.desc), ctypes.byref(h)), "pbn_net_create")
+        self.handle = h
+        self.words = L.pbn_net_words(h)
+
+    def close(self) -> None:
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            load().pbn_net_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,45 @@
+// philox.h -- Philox4x32-10 (Salmon et al., SC'11 / Random123) for gfx950.
+//
+// One round: two 32x32->64 products (v_mad_u64_u32), two 3-input xors
+// (v_xor3_b32); the key schedule is wave-uniform and lives in SGPRs.
+// Counter map (DESIGN.md "RNG stream map"):
+//   ctr = (lo32(id), lo32(step), stream << 28 | idx, hi16(id) | hi16(step) << 16)
+//   key = (lo32(seed), hi32(seed))
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pbn {
+
+enum : uint32_t { kStreamSel = 0, kStreamEnv = 1, kStreamPert = 2, kStreamReset = 3 };
+
+struct Word4 {
+  uint32_t x, y, z, w;
+};
+
+__host__ __device__ __forceinline__ Word4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2,
+                                                         uint32_t c3, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return Word4{c0, c1, c2, c3};
+}
+
+__host__ __device__ __forceinline__ Word4 draw(uint64_t seed, uint64_t id, uint64_t step,
+                                                uint32_t stream, uint32_t idx) {
+  return philox4x32_10((uint32_t)id, (uint32_t)step, (stream << 28) | (idx & 0x0FFFFFFFu),
+                       (uint32_t)((id >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16),
+                       (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+}  // namespace pbn

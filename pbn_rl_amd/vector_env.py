@@ -1,0 +1,166 @@
+"""VectorPBNEnv: a batch of PBN envs resident in HBM, stepped by libpbn_env.so.
+
+This is the batched form of the gym-PBN env the reference steps one frame at
+a time (bdq_model/__init__.py:172-177).  All buffers are torch tensors on one
+GPU in the SoA layout of include/pbn_env.h (uint32 words stored as int32);
+every step is one ``pbn_step`` launch on the current torch stream, with no
+host synchronisation.  Buffers are padded to a multiple of 32 envs (the
+kernel's group size); the padding envs are real envs nobody reads.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence, Tuple, Union
+
+import torch
+
+from . import _lib
+from .spec import EnvSpec
+
+__all__ = ["VectorPBNEnv", "actions_to_flipmask", "unpack_states", "pack_states"]
+
+
+def _round32(n: int) -> int:
+    return (n + 31) // 32 * 32
+
+
+def actions_to_flipmask(actions: torch.Tensor, n_nodes: int) -> torch.Tensor:
+    """(n, k) ints in [0, N] -> (W, n) int32 flip masks; 0 = no-op, a > 0 flips node a-1
+    once however often it is repeated (bdq_model/__init__.py:81-84,176)."""
+    if actions.dim() == 1:
+        actions = actions[:, None]
+    n = actions.shape[0]
+    W = (n_nodes + 31) // 32
+    a = actions.to(torch.int64)
+    if bool(((a < 0) | (a > n_nodes)).any()):
+        raise ValueError(f"actions must be in [0, {n_nodes}]")
+    node = torch.arange(1, n_nodes + 1, device=a.device)
+    hit = (a[:, :, None] == node[None, None, :]).any(dim=1)          # (n, N)
+    pad = torch.zeros(n, 32 * W, dtype=torch.int64, device=a.device)
+    pad[:, :n_nodes] = hit.to(torch.int64)
+    weights = (torch.ones(32, dtype=torch.int64, device=a.device) << torch.arange(32, device=a.device))
+    words = (pad.view(n, W, 32) * weights).sum(dim=2)                  # (n, W) in [0, 2^32)
+    words = torch.where(words >= 2 ** 31, words - 2 ** 32, words)
+    return words.to(torch.int32).t().contiguous()
+
+
+def unpack_states(words: torch.Tensor, n_nodes: int) -> torch.Tensor:
+    """(W, n) int32 words -> (n, N) uint8 bits (node i = bit i)."""
+    W, n = words.shape
+    shifts = torch.arange(32, device=words.device, dtype=torch.int32)
+    bits = (words.t()[:, :, None] >> shifts[None, None, :]) & 1     # (n, W, 32)
+    return bits.reshape(n, 32 * W)[:, :n_nodes].to(torch.uint8)
+
+
+def pack_states(bits: torch.Tensor, n_nodes: int) -> torch.Tensor:
+    """(n, N) 0/1 -> (W, n) int32 words."""
+    n = bits.shape[0]
+    W = (n_nodes + 31) // 32
+    pad = torch.zeros(n, 32 * W, dtype=torch.int64, device=bits.device)
+    pad[:, :n_nodes] = bits.to(torch.int64) & 1
+    weights = torch.ones(32, dtype=torch.int64, device=bits.device) << torch.arange(32, device=bits.device)
+    words = (pad.view(n, W, 32) * weights).sum(dim=2)
+    words = torch.where(words >= 2 ** 31, words - 2 ** 32, words)
+    return words.to(torch.int32).t().contiguous()
+
+
+class VectorPBNEnv:
+    """``num_envs`` PBN envs on ``device``; env ids ``env_offset .. env_offset+num_envs``.
+
+    step() consumes either a (W, n) flip-mask tensor, an (n, k) action tensor,
+    or nothing (``random_actions=True``: 3 uniform actions per env drawn in-kernel,
+    the synthetic explore policy of bdq_model/__init__.py:76).
+    """
+
+    def __init__(self, spec: EnvSpec, num_envs: int, *, seed: int = 0, device: Union[str, torch.device, None] = None,
+                 env_offset: int = 0, autoreset: bool = True, keep_final_state: bool = True):
+        if not torch.cuda.is_available():
+            raise _lib.PbnError("VectorPBNEnv needs a ROCm GPU (libpbn_env.so has no CPU path)")
+        if env_offset % 32:
+            raise ValueError("env_offset must be a multiple of 32")
+        self.spec = spec
+        self.device = torch.device(device if device is not None else f"cuda:{torch.cuda.current_device()}")
+        self.num_envs = int(num_envs)
+        self.n_alloc = _round32(self.num_envs)
+        self.env_offset = int(env_offset)
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.autoreset = autoreset
+        self.keep_final_state = keep_final_state
+        self.n_nodes = spec.n
+        self.words = spec.words
+        with torch.cuda.device(self.device):
+            self.net = _lib.NetHandle(spec)
+        W, n = self.words, self.n_alloc
+        dev = self.device
+        z32 = lambda *s: torch.zeros(*s, dtype=torch.int32, device=dev)  # noqa: E731
+        self.state = z32(W, n)
+        self._state_next = z32(W, n)
+        self.flipmask = z32(W, n)
+        self.final_state = z32(W, n) if keep_final_state else None
+        self.target = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.t = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.reward = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.flags = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.step_index = 0      # global step counter: the RNG's time coordinate
+
+    # ------------------------------------------------------------ internals
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def reset(self, seed: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        if seed is not None:
+            self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        L = _lib.load()
+        with torch.cuda.device(self.device):
+            _lib.check(L.pbn_reset(self.net.handle, self.seed, self.step_index, self.env_offset, self.n_alloc,
+                                   self.state.data_ptr(), self.target.data_ptr(), self.t.data_ptr(),
+                                   self._stream()), "pbn_reset")
+        self.step_index += 1
+        return self.state[:, : self.num_envs], self.target[: self.num_envs]
+
+    def step_flipmask(self, flipmask: Optional[torch.Tensor] = None, random_actions: bool = False):
+        """One transition for every env; returns views (state', reward, flags)."""
+        L = _lib.load()
+        mode = _lib.MODE_AUTORESET if self.autoreset else 0
+        if random_actions:
+            mode |= _lib.MODE_RANDOM_ACTIONS
+        elif flipmask is not None:
+            if flipmask.shape != (self.words, self.num_envs):
+                raise ValueError(f"flipmask must have shape {(self.words, self.num_envs)}")
+            self.flipmask[:, : self.num_envs].copy_(flipmask)
+            if self.n_alloc > self.num_envs:
+                self.flipmask[:, self.num_envs:].zero_()
+        else:
+            self.flipmask.zero_()
+        fs = self.final_state.data_ptr() if self.final_state is not None else None
+        with torch.cuda.device(self.device):
+            _lib.check(L.pbn_step(self.net.handle, self.seed, self.step_index, self.env_offset, self.n_alloc, mode,
+                                  self.state.data_ptr(), self.flipmask.data_ptr(), self.target.data_ptr(),
+                                  self.t.data_ptr(), self._state_next.data_ptr(), fs, self.reward.data_ptr(),
+                                  self.flags.data_ptr(), self._stream()), "pbn_step")
+        self.step_index += 1
+        self.state, self._state_next = self._state_next, self.state
+        k = self.num_envs
+        return self.state[:, :k], self.reward[:k], self.flags[:k]
+
+    def step(self, actions: Optional[torch.Tensor] = None):
+        """gymnasium-vector style: actions (n, k) in [0, N] (or None = no intervention).
+        Returns (state_words, reward, terminated, truncated, info)."""
+        fm = None if actions is None else actions_to_flipmask(actions.to(self.device), self.n_nodes)
+        state, reward, flags = self.step_flipmask(fm)
+        terminated = (flags & _lib.FLAG_TERMINATED) != 0
+        truncated = (flags & _lib.FLAG_TRUNCATED) != 0
+        info = {"flags": flags}
+        if self.final_state is not None:
+            info["final_state"] = self.final_state[:, : self.num_envs]
+        return state, reward, terminated, truncated, info
+
+    def set_state(self, words: torch.Tensor, target: Optional[torch.Tensor] = None,
+                  t: Optional[torch.Tensor] = None) -> None:
+        self.state[:, : self.num_envs].copy_(words)
+        if target is not None:
+            self.target[: self.num_envs].copy_(target)
+        if t is not None:
+            self.t[: self.num_envs].copy_(t)
+
+    def close(self) -> None:
+        self.net.close()

@@ -1,0 +1,144 @@
+"""HIP kernel == CPU oracle, bit for bit, through the C-ABI (libpbn_env.so).
+
+Every output of pbn_step (state_out, final_state, reward, flags, target, t,
+and the in-kernel actions) is compared exactly against oracle/pbn_oracle.c on
+the same seeded inputs, for every bundled network and configuration axis:
+interventions from a buffer / drawn in-kernel, autoreset on / off, selection
+resolution (prob_bits), perturbation rate (including a high rate that drives
+the rare multi-flip path), env offsets (sharding) and batch sizes up to the
+BASELINE sizes.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle
+from pbn_rl_amd import _lib
+from pbn_rl_amd.attractors import load_attractors
+from pbn_rl_amd.network import load_network
+from pbn_rl_amd.spec import EnvSpec
+from pbn_rl_amd.vector_env import VectorPBNEnv
+
+pytestmark = pytest.mark.gpu
+
+NETS = ["pbn7", "pbn10", "pbn28", "pbn70"]
+
+
+def make_spec(name, **kw):
+    return EnvSpec(load_network(name), load_attractors(name), **kw)
+
+
+def u32(x: torch.Tensor) -> np.ndarray:
+    return x.cpu().numpy().view(np.uint32)
+
+
+def run_pair(spec, n, steps, *, seed=12345, env_offset=0, mode=3, flip_density=0.1, rng_seed=0,
+             start_random=False):
+    """Step the GPU env and the oracle side by side; assert equality every step."""
+    env = VectorPBNEnv(spec, n, seed=seed, env_offset=env_offset, autoreset=bool(mode & 1))
+    env.reset()
+    st, tg, t = oracle.reset(spec, seed, 0, env_offset, n)
+    assert np.array_equal(u32(env.state), st), "reset state"
+    assert np.array_equal(env.target.cpu().numpy(), tg)
+    assert np.array_equal(env.t.cpu().numpy(), t)
+    rng = np.random.default_rng(rng_seed)
+    W = spec.words
+    if start_random:
+        st = rng.integers(0, 2 ** 32, size=(W, n), dtype=np.uint64).astype(np.uint32)
+        if spec.n % 32:
+            st[W - 1] &= np.uint32((1 << (spec.n % 32)) - 1)
+        env.set_state(torch.from_numpy(st.view(np.int32)).to(env.device))
+    for k in range(steps):
+        random_actions = bool(mode & _lib.MODE_RANDOM_ACTIONS)
+        if random_actions:
+            flip = np.zeros((W, n), dtype=np.uint32)
+            fm = None
+        else:
+            bits = (rng.random((W, n, 32)) < flip_density).astype(np.uint64)
+            flip = (bits << np.arange(32, dtype=np.uint64)).sum(axis=2).astype(np.uint32)
+            fm = torch.from_numpy(flip.view(np.int32)).to(env.device)
+        step_idx = env.step_index
+        state, reward, flags = env.step_flipmask(fm, random_actions=random_actions)
+        ref = oracle.step(spec, seed, step_idx, env_offset, st, flip, tg, t, mode)
+        tag = f"step {k}"
+        assert np.array_equal(u32(env.final_state), ref["final_state"]), tag + " final_state"
+        assert np.array_equal(u32(state), ref["state_out"]), tag + " state_out"
+        assert np.array_equal(flags.cpu().numpy(), ref["flags"]), tag + " flags"
+        assert np.array_equal(reward.cpu().numpy().view(np.uint32), ref["reward"].view(np.uint32)), tag + " reward"
+        assert np.array_equal(env.target.cpu().numpy(), ref["target"]), tag + " target"
+        assert np.array_equal(env.t.cpu().numpy(), ref["t"]), tag + " t"
+        if random_actions:
+            assert np.array_equal(u32(env.flipmask), ref["flipmask"]), tag + " in-kernel actions"
+        st, tg, t = ref["state_out"], ref["target"], ref["t"]
+    env.close()
+    return ref
+
+
+@pytest.mark.parametrize("name", NETS)
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_step_matches_oracle(name, mode):
+    spec = make_spec(name, perturbation=0.02)
+    run_pair(spec, 2048, 12, mode=mode, env_offset=0 if mode < 2 else 4096)
+
+
+@pytest.mark.parametrize("name", ["pbn28", "pbn70"])
+def test_high_perturbation_multi_flip_path(name):
+    ref = run_pair(make_spec(name, perturbation=0.3), 1024, 6, mode=3)
+    assert (ref["flags"] & _lib.FLAG_PERTURBED).mean() > 0.9
+
+
+@pytest.mark.parametrize("bits", [4, 8, 12, 16])
+def test_prob_bits(bits):
+    run_pair(make_spec("pbn28", prob_bits=bits, perturbation=0.0), 1024, 6, mode=1, start_random=True)
+
+
+@pytest.mark.parametrize("name", NETS)
+def test_from_random_states_no_perturbation(name):
+    run_pair(make_spec(name, perturbation=0.0, horizon=0), 2048, 5, mode=0, start_random=True)
+
+
+def test_no_attractors_autoreset():
+    spec = EnvSpec(load_network("pbn28"), [], perturbation=0.01, horizon=3)
+    run_pair(spec, 1024, 8, mode=3)
+
+
+def test_baseline_size_bittner28():
+    """BASELINE config 2 size: 65,536 envs, in-kernel actions, autoreset."""
+    run_pair(make_spec("pbn28"), 65536, 30, mode=3, seed=0)
+
+
+def test_baseline_size_pbn70():
+    """BASELINE config 3 size: 1,048,576 envs (2-word+ state path)."""
+    run_pair(make_spec("pbn70"), 1 << 20, 2, mode=3, seed=1)
+
+
+def test_shard_invariance():
+    """Concatenated shards == one run (env ids keep their RNG streams)."""
+    spec = make_spec("pbn28")
+    n, steps = 4096, 5
+    whole = VectorPBNEnv(spec, n, seed=7)
+    whole.reset()
+    parts = [VectorPBNEnv(spec, n // 2, seed=7, env_offset=r * (n // 2)) for r in range(2)]
+    for p in parts:
+        p.step_index = 0
+        p.reset()
+    for _ in range(steps):
+        a = whole.step_flipmask(random_actions=True)
+        b = [p.step_flipmask(random_actions=True) for p in parts]
+        for i in range(3):
+            cat = torch.cat([b[0][i], b[1][i]], dim=-1)
+            assert torch.equal(a[i], cat)
+
+
+def test_abi_rejects_bad_arguments():
+    spec = make_spec("pbn28")
+    env = VectorPBNEnv(spec, 64)
+    L = _lib.load()
+    rc = L.pbn_step(env.net.handle, 0, 0, 16, 64, 3, env.state.data_ptr(), env.flipmask.data_ptr(),
+                    env.target.data_ptr(), env.t.data_ptr(), env._state_next.data_ptr(), None,
+                    env.reward.data_ptr(), env.flags.data_ptr(), None)
+    assert rc == -22 and b"multiples of 32" in L.pbn_last_error()
+    rc = L.pbn_step(env.net.handle, 0, 0, 0, 64, 3, env.state.data_ptr(), env.flipmask.data_ptr(),
+                    env.target.data_ptr(), env.t.data_ptr(), env.state.data_ptr(), None,
+                    env.reward.data_ptr(), env.flags.data_ptr(), None)
+    assert rc == -22
