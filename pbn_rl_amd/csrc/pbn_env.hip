@@ -20,6 +20,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <string>
@@ -70,6 +71,8 @@ struct StepArgs {
   int hash_bits;     // 0 = no attractors
   int hash_probes;   // max probe count (>= 1 when attractors exist)
   int tab_words;     // words of the LDS table image
+  int prob_bits;
+  int n_funcs;
   uint32_t hash_mult[4];
 };
 
@@ -105,22 +108,23 @@ __device__ __forceinline__ uint32_t eval_func(const FuncRec* __restrict__ fr,
   return bfi(x3, y1, y0);
 }
 
-// lanes-of-32-envs bit mask of (u < c), u = digits dig[0..B) MSB first.
-template <int B>
-__device__ __forceinline__ uint32_t less_than(const uint32_t (&dig)[16], uint32_t c) {
+// lanes-of-32-envs bit mask of (u < c), u = digits dig[0..B) MSB first (B = prob_bits).
+__device__ __forceinline__ uint32_t less_than(const uint32_t (&dig)[16], uint32_t c, int B) {
   uint32_t lt = 0;
 #pragma unroll
-  for (int d = B - 1; d >= 0; --d) {
-    const uint32_t C = ((c >> (B - 1 - d)) & 1u) ? 0xFFFFFFFFu : 0u;
-    const uint32_t m = dig[d] ^ ~C;
-    lt = bfi(m, lt, C);
+  for (int d = 15; d >= 0; --d) {
+    if (d < B) {
+      const uint32_t C = ((c >> (B - 1 - d)) & 1u) ? 0xFFFFFFFFu : 0u;
+      const uint32_t m = dig[d] ^ ~C;
+      lt = bfi(m, lt, C);
+    }
   }
   return lt;
 }
 
-// ---------------------------------------------------------------- step kernel
-template <int W, int B>
-__global__ void __launch_bounds__(128) pbn_step_kernel(StepArgs a) {
+// ------------------------------------------------- step kernel, one thread per group
+template <int W>
+__global__ void __launch_bounds__(128) pbn_step_lane(StepArgs a) {
   extern __shared__ uint32_t smem[];
   for (int i = threadIdx.x; i < a.tab_words; i += blockDim.x) smem[i] = a.tab[i];
   __syncthreads();
@@ -303,7 +307,8 @@ __global__ void __launch_bounds__(128) pbn_step_kernel(StepArgs a) {
     uint32_t dig[16];
     if (nf > 1) {
 #pragma unroll
-      for (int c = 0; c < B / 4; ++c) {
+      for (int c = 0; c < 4; ++c) {
+        if (4 * c >= a.prob_bits) break;
         const Word4 d = pbn::philox4x32_10((uint32_t)G, st_lo,
                                            (pbn::kStreamSel << 28) | (uint32_t)(4 * i + c),
                                            (uint32_t)((G >> 32) & 0xFFFFu) | st_hi, k0, k1);
@@ -317,7 +322,7 @@ __global__ void __launch_bounds__(128) pbn_step_kernel(StepArgs a) {
     for (int j = nf - 2; j >= 0; --j) {
       const FuncRec* fr = a.funcs + f0 + j;
       const uint32_t fj = eval_func(fr, S);
-      const uint32_t lt = less_than<B>(dig, fr->thr);
+      const uint32_t lt = less_than(dig, fr->thr, a.prob_bits);
       x = bfi(lt, fj, x);
     }
     R[i * 64] = bfi(pmask, R[i * 64], x);
@@ -442,6 +447,273 @@ __global__ void __launch_bounds__(128) pbn_step_kernel(StepArgs a) {
   }
 }
 
+// ------------------------------------------- step kernel, a team of T threads per group
+//
+// For batches too small to fill 256 CUs with one thread per 32-env group, T
+// lanes of one wave share a group: each lane runs the per-env work of 32/T envs
+// and the node loop of nodes i = j, j+T, ...; the group's state planes are
+// exchanged through LDS.  Per-group LDS: S[32W] planes of s1, R[32W] planes of
+// s1^gamma (then of s'), WS/WR[32][W] per-env words, P (perturbed mask).
+// FuncRecs and node ranges are staged in LDS because each lane evaluates a
+// different node.
+
+// eval of a lane-varying function: record in LDS, planes in LDS
+__device__ __forceinline__ uint32_t eval_func_lds(const uint32_t* __restrict__ fr,
+                                                  const uint32_t* __restrict__ S) {
+  const uint4 in = *reinterpret_cast<const uint4*>(fr);
+  const uint32_t x0 = S[in.x], x1 = S[in.y], x2 = S[in.z], x3 = S[in.w];
+  const uint4 d0 = *reinterpret_cast<const uint4*>(fr + 4);
+  const uint4 d1 = *reinterpret_cast<const uint4*>(fr + 8);
+  const uint4 b0 = *reinterpret_cast<const uint4*>(fr + 12);
+  const uint4 b1 = *reinterpret_cast<const uint4*>(fr + 16);
+  const uint32_t v0 = (x0 & d0.x) ^ b0.x, v1 = (x0 & d0.y) ^ b0.y, v2 = (x0 & d0.z) ^ b0.z,
+                 v3 = (x0 & d0.w) ^ b0.w, v4 = (x0 & d1.x) ^ b1.x, v5 = (x0 & d1.y) ^ b1.y,
+                 v6 = (x0 & d1.z) ^ b1.z, v7 = (x0 & d1.w) ^ b1.w;
+  const uint32_t w0 = bfi(x1, v1, v0), w1 = bfi(x1, v3, v2), w2 = bfi(x1, v5, v4), w3 = bfi(x1, v7, v6);
+  return bfi(x3, bfi(x2, w3, w2), bfi(x2, w1, w0));
+}
+
+template <int W, int T>
+__global__ void __launch_bounds__(256) pbn_step_team(StepArgs a) {
+  constexpr int GPB = 256 / T;        // groups per block
+  constexpr int EPT = 32 / T;         // envs per thread
+  constexpr int GW = 32 * W;          // planes per group
+  constexpr int GSTRIDE = 4 * GW + 4; // LDS words per group
+  extern __shared__ uint32_t smem[];
+  const int N = a.n_nodes;
+  const int fwords = a.n_funcs * kFuncRecWords;
+  uint32_t* funcs_l = smem + a.tab_words;
+  int32_t* nodefs_l = reinterpret_cast<int32_t*>(funcs_l + fwords);
+  uint32_t* groups_l = funcs_l + fwords + ((N + 1 + 3) & ~3);
+  for (int i = threadIdx.x; i < a.tab_words; i += 256) smem[i] = a.tab[i];
+  for (int i = threadIdx.x; i < fwords; i += 256) funcs_l[i] = reinterpret_cast<const uint32_t*>(a.funcs)[i];
+  for (int i = threadIdx.x; i <= N; i += 256) nodefs_l[i] = a.node_fs[i];
+  const int team = threadIdx.x / T, j = threadIdx.x % T;
+  uint32_t* S = groups_l + team * GSTRIDE;
+  uint32_t* R = S + GW;
+  uint32_t* WS = R + GW;
+  uint32_t* WR = WS + GW;
+  uint32_t* P = WR + GW;
+  if (j == 0) *P = 0;
+  __syncthreads();
+
+  const uint32_t* cdf = smem;
+  const float* rtab = reinterpret_cast<const float*>(smem + a.cdf_len);
+  const uint32_t* htab = smem + a.cdf_len + 4 * (N + 1);
+  const int64_t n = a.n_envs;
+  int64_t g = (int64_t)blockIdx.x * GPB + team;
+  const bool live = g < a.n_groups;
+  if (!live) g = a.n_groups - 1;  // dead teams mirror the last group, store nothing
+  const int64_t e0 = g * 32;
+  const uint64_t ge0 = a.env_offset + (uint64_t)e0;
+  const uint64_t G = ge0 >> 5;
+  const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+  const uint32_t st_lo = (uint32_t)a.step;
+  const uint32_t st_hi = (uint32_t)((a.step >> 32) & 0xFFFFu) << 16;
+  const bool random_actions = (a.mode & PBN_MODE_RANDOM_ACTIONS) != 0;
+
+  // ---- per env: interventions, perturbation, reset word
+  uint32_t tt_[EPT], tg_[EPT], pc_[EPT], rw_[EPT];
+  bool pert_[EPT];
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int b = j + k * T;
+    const int64_t le = e0 + b;
+    const uint64_t ge = ge0 + (uint64_t)b;
+    const uint32_t ghi = (uint32_t)((ge >> 32) & 0xFFFFu) | st_hi;
+    const Word4 E = pbn::philox4x32_10((uint32_t)ge, st_lo, pbn::kStreamEnv << 28, ghi, k0, k1);
+    uint32_t s1[W], m[W], gam[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      s1[w] = a.state[(size_t)w * n + le] & valid_word_mask(N, w);
+      m[w] = 0;
+      gam[w] = 0;
+    }
+    tt_[k] = a.t[le];
+    tg_[k] = a.target[le];
+    if (random_actions) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const uint32_t act = (((E.w >> (10 * q)) & 1023u) * (uint32_t)(N + 1)) >> 10;
+        if (act > 0) {
+#pragma unroll
+          for (int w = 0; w < W; ++w)
+            if ((int)((act - 1) >> 5) == w) m[w] |= 1u << ((act - 1) & 31);
+        }
+      }
+      if (live) {
+#pragma unroll
+        for (int w = 0; w < W; ++w) a.flipmask[(size_t)w * n + le] = m[w];
+      }
+    } else {
+#pragma unroll
+      for (int w = 0; w < W; ++w) m[w] = a.flipmask[(size_t)w * n + le] & valid_word_mask(N, w);
+    }
+    uint32_t pc = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      pc += __builtin_popcount(m[w]);
+      s1[w] ^= m[w];
+    }
+    // perturbation: flip positions are partial sums of geometric gaps
+    int pos = -1;
+    uint32_t P4[4] = {0, 0, 0, 0};
+    for (int kk = 0; pos < N - 1; ++kk) {
+      uint32_t u;
+      if (kk == 0) {
+        u = E.x;
+      } else if (kk == 1) {
+        u = E.y;
+      } else {
+        if (((kk - 2) & 3) == 0) {
+          const Word4 pw = pbn::philox4x32_10((uint32_t)ge, st_lo,
+                                              (pbn::kStreamPert << 28) | (uint32_t)((kk - 2) >> 2), ghi, k0, k1);
+          P4[0] = pw.x; P4[1] = pw.y; P4[2] = pw.z; P4[3] = pw.w;
+        }
+        u = P4[(kk - 2) & 3];
+      }
+      pos += gap_of(cdf, a.cdf_len, u);
+      if (pos >= N) break;
+#pragma unroll
+      for (int w = 0; w < W; ++w)
+        if ((pos >> 5) == w) gam[w] |= 1u << (pos & 31);
+    }
+    bool pert = false;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      pert = pert || gam[w] != 0;
+      WS[b * W + w] = s1[w];
+      WR[b * W + w] = s1[w] ^ gam[w];
+    }
+    if (pert) atomicOr(P, 1u << b);
+    pc_[k] = pc;
+    rw_[k] = E.z;
+    pert_[k] = pert;
+  }
+  __syncthreads();
+
+  // ---- bit-slice the group: plane p = bit p of every env word
+  for (int p = j; p < GW; p += T) {
+    const int w = p >> 5, c = p & 31;
+    uint32_t sa = 0, ra = 0;
+#pragma unroll
+    for (int e = 0; e < 32; ++e) {
+      sa |= ((WS[e * W + w] >> c) & 1u) << e;
+      ra |= ((WR[e * W + w] >> c) & 1u) << e;
+    }
+    S[p] = sa;
+    R[p] = ra;
+  }
+  __syncthreads();
+
+  // ---- node loop: lane j owns nodes j, j+T, ...
+  const uint32_t pmask = *P;
+  for (int i = j; i < N; i += T) {
+    const int f0 = nodefs_l[i];
+    const int nf = nodefs_l[i + 1] - f0;
+    uint32_t dig[16];
+    if (nf > 1) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (4 * c >= a.prob_bits) break;
+        const Word4 d = pbn::philox4x32_10((uint32_t)G, st_lo, (pbn::kStreamSel << 28) | (uint32_t)(4 * i + c),
+                                           (uint32_t)((G >> 32) & 0xFFFFu) | st_hi, k0, k1);
+        dig[4 * c + 0] = d.x;
+        dig[4 * c + 1] = d.y;
+        dig[4 * c + 2] = d.z;
+        dig[4 * c + 3] = d.w;
+      }
+    }
+    const uint32_t* fr = funcs_l + (size_t)(f0 + nf - 1) * kFuncRecWords;
+    uint32_t x = eval_func_lds(fr, S);
+    for (int jj = nf - 2; jj >= 0; --jj) {
+      fr = funcs_l + (size_t)(f0 + jj) * kFuncRecWords;
+      const uint32_t fj = eval_func_lds(fr, S);
+      x = bfi(less_than(dig, fr[20], a.prob_bits), fj, x);
+    }
+    R[i] = bfi(pmask, R[i], x);
+  }
+  __syncthreads();
+
+  // ---- per env: back to words, reward, termination, autoreset, stores
+  const int hmask = (1 << a.hash_bits) - 1;
+  const uint32_t* hid = htab + (size_t)W * (hmask + 1);
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int b = j + k * T;
+    const int64_t le = e0 + b;
+    const uint64_t ge = ge0 + (uint64_t)b;
+    uint32_t sp[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      uint32_t acc = 0;
+#pragma unroll
+      for (int c = 0; c < 32; ++c) acc |= ((R[32 * w + c] >> b) & 1u) << c;
+      sp[w] = acc;
+    }
+    if (!live) continue;
+    if (a.final_state) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) a.final_state[(size_t)w * n + le] = sp[w];
+    }
+    int att = -1;
+    if (a.hash_bits > 0) {
+      uint32_t h = 0;
+#pragma unroll
+      for (int w = 0; w < W; ++w) h += sp[w] * a.hash_mult[w];
+      h >>= (32 - a.hash_bits);
+      for (int pr = 0; pr < a.hash_probes; ++pr) {
+        const uint32_t slot = (h + pr) & hmask;
+        bool eq = true;
+#pragma unroll
+        for (int w = 0; w < W; ++w) eq = eq && (htab[(size_t)w * (hmask + 1) + slot] == sp[w]);
+        const uint32_t id = hid[slot];
+        if (eq && id != 0xFFFFFFFFu) att = (int)id;
+      }
+    }
+    const bool in_attr = att >= 0;
+    const bool term = in_attr && (uint32_t)att == tg_[k];
+    const bool wrong = in_attr && !term;
+    int tt = (int)tt_[k] + 1;
+    tt = tt > 255 ? 255 : tt;
+    const bool trunc = a.horizon > 0 && tt >= a.horizon;
+    a.reward[le] = rtab[(2 * (int)term + (int)wrong) * (N + 1) + (int)pc_[k]];
+    uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) | ((uint32_t)pert_[k] << 3);
+    if ((a.mode & PBN_MODE_AUTORESET) && (term || trunc)) {
+      const uint32_t Rw = rw_[k];
+      uint32_t nt;
+      if (a.n_attr >= 1) {
+        const uint32_t A = (uint32_t)a.n_attr;
+        const uint32_t as = ((Rw & 1023u) * A) >> 10;
+        const int st0 = a.att_start[as];
+        const uint32_t size = (uint32_t)(a.att_start[as + 1] - st0);
+        const uint32_t idx = (((Rw >> 20) & 4095u) * size) >> 12;
+#pragma unroll
+        for (int w = 0; w < W; ++w) sp[w] = a.att_states[(size_t)(st0 + idx) * W + w];
+        nt = as;
+        if (A >= 2) {
+          nt = (((Rw >> 10) & 1023u) * (A - 1)) >> 10;
+          nt += (nt >= as) ? 1u : 0u;
+        }
+      } else {
+        const Word4 rr = pbn::philox4x32_10((uint32_t)ge, st_lo, (pbn::kStreamReset << 28) | 1u,
+                                            (uint32_t)((ge >> 32) & 0xFFFFu) | st_hi, k0, k1);
+        const uint32_t rw4[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+        for (int w = 0; w < W; ++w) sp[w] = rw4[w] & valid_word_mask(N, w);
+        nt = PBN_NO_TARGET;
+      }
+      a.target[le] = (uint8_t)nt;
+      tt = 0;
+      fl |= PBN_FLAG_RESET;
+    }
+#pragma unroll
+    for (int w = 0; w < W; ++w) a.state_out[(size_t)w * n + le] = sp[w];
+    a.t[le] = (uint8_t)tt;
+    a.flags[le] = (uint8_t)fl;
+  }
+}
+
 // ---------------------------------------------------------------- reset kernel
 template <int W>
 __global__ void __launch_bounds__(256) pbn_reset_kernel(const int32_t* __restrict__ att_start,
@@ -497,16 +769,37 @@ int fail(int code, const std::string& msg) {
 
 using StepFn = void (*)(StepArgs);
 
-template <int W, int B>
-StepFn step_fn() { return pbn_step_kernel<W, B>; }
+constexpr int kTeamSizes[5] = {2, 4, 8, 16, 32};
 
-StepFn pick_step(int W, int B) {
-#define PBN_CASE(w, b) if (W == w && B == b) return step_fn<w, b>();
-  PBN_CASE(1, 4) PBN_CASE(1, 8) PBN_CASE(1, 12) PBN_CASE(1, 16)
-  PBN_CASE(2, 4) PBN_CASE(2, 8) PBN_CASE(2, 12) PBN_CASE(2, 16)
-  PBN_CASE(3, 4) PBN_CASE(3, 8) PBN_CASE(3, 12) PBN_CASE(3, 16)
-  PBN_CASE(4, 4) PBN_CASE(4, 8) PBN_CASE(4, 12) PBN_CASE(4, 16)
-#undef PBN_CASE
+StepFn pick_lane(int W) {
+  switch (W) {
+    case 1: return pbn_step_lane<1>;
+    case 2: return pbn_step_lane<2>;
+    case 3: return pbn_step_lane<3>;
+    case 4: return pbn_step_lane<4>;
+  }
+  return nullptr;
+}
+
+template <int W>
+StepFn pick_team_w(int T) {
+  switch (T) {
+    case 2: return pbn_step_team<W, 2>;
+    case 4: return pbn_step_team<W, 4>;
+    case 8: return pbn_step_team<W, 8>;
+    case 16: return pbn_step_team<W, 16>;
+    case 32: return pbn_step_team<W, 32>;
+  }
+  return nullptr;
+}
+
+StepFn pick_team(int W, int T) {
+  switch (W) {
+    case 1: return pick_team_w<1>(T);
+    case 2: return pick_team_w<2>(T);
+    case 3: return pick_team_w<3>(T);
+    case 4: return pick_team_w<4>(T);
+  }
   return nullptr;
 }
 
@@ -529,9 +822,13 @@ struct pbn_net {
   int n_nodes = 0, W = 0, B = 0, horizon = 0, n_attr = 0, n_states = 0;
   int cdf_len = 0, hash_bits = 0, hash_probes = 0, tab_words = 0;
   uint32_t hash_mult[4] = {0, 0, 0, 0};
-  int waves_per_block = 1;
-  size_t lds_bytes = 0;
-  StepFn step = nullptr;
+  int n_funcs = 0;
+  int waves_per_block = 1;   // lane kernel
+  size_t lds_lane = 0;
+  size_t lds_team[5] = {0, 0, 0, 0, 0};
+  StepFn lane = nullptr;
+  StepFn team[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  int force_team = -1;       // PBN_TEAM env override (1 = lane kernel)
   ResetFn reset = nullptr;
   FuncRec* d_funcs = nullptr;
   int32_t* d_node_fs = nullptr;
@@ -724,15 +1021,21 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     tab.push_back(u);
   }
   tab.insert(tab.end(), hash_img.begin(), hash_img.end());
+  while (tab.size() & 3) tab.push_back(0u);  // keep the FuncRec image 16-byte aligned in LDS
   net->tab_words = (int)tab.size();
+  net->n_funcs = d->n_funcs;
   net->waves_per_block = (W == 1) ? 2 : 1;
-  net->lds_bytes = (size_t)net->tab_words * 4 + (size_t)net->waves_per_block * 2 * 32 * W * 64 * 4;
-  if (net->lds_bytes > 160 * 1024) {
-    free_net(net);
-    return fail(PBN_EINVAL, "LDS budget exceeded");
+  net->lds_lane = (size_t)net->tab_words * 4 + (size_t)net->waves_per_block * 2 * 32 * W * 64 * 4;
+  const size_t team_fixed =
+      ((size_t)net->tab_words + (size_t)d->n_funcs * kFuncRecWords + (size_t)((N + 1 + 3) & ~3)) * 4;
+  for (int ti = 0; ti < 5; ++ti) {
+    const int T = kTeamSizes[ti];
+    net->lds_team[ti] = team_fixed + (size_t)(256 / T) * (4 * 32 * W + 4) * 4;
+    net->team[ti] = pick_team(W, T);
   }
-  net->step = pick_step(W, d->prob_bits);
+  net->lane = pick_lane(W);
   net->reset = pick_reset(W);
+  if (const char* env = getenv("PBN_TEAM")) net->force_team = atoi(env);
   int rc;
   if (hipGetDevice(&net->device) != hipSuccess) {
     free_net(net);
@@ -746,10 +1049,19 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     free_net(net);
     return rc;
   }
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(net->step),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)net->lds_bytes) != hipSuccess) {
+  for (int ti = -1; ti < 5; ++ti) {
+    const StepFn fn = ti < 0 ? net->lane : net->team[ti];
+    const size_t bytes = ti < 0 ? net->lds_lane : net->lds_team[ti];
+    if (bytes > 160 * 1024) continue;  // variant unusable for this net; never picked
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)bytes) != hipSuccess) {
+      free_net(net);
+      return fail(PBN_EDEVICE, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+    }
+  }
+  if (net->lds_lane > 160 * 1024 && net->lds_team[4] > 160 * 1024) {
     free_net(net);
-    return fail(PBN_EDEVICE, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+    return fail(PBN_EINVAL, "LDS budget exceeded");
   }
   *out = net;
   return PBN_OK;
@@ -833,9 +1145,28 @@ int pbn_step(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, in
   a.hash_probes = net->hash_probes;
   a.tab_words = net->tab_words;
   memcpy(a.hash_mult, net->hash_mult, sizeof a.hash_mult);
-  const int threads = 64 * net->waves_per_block;
-  const unsigned blocks = (unsigned)((a.n_groups + threads - 1) / threads);
-  hipLaunchKernelGGL(net->step, dim3(blocks), dim3(threads), net->lds_bytes, (hipStream_t)stream, a);
+  a.prob_bits = net->B;
+  a.n_funcs = net->n_funcs;
+  // launch shape: one thread per 32-env group when that fills the chip, else a
+  // team of T lanes per group (smallest T reaching ~4 waves per SIMD, max 32)
+  int T = 1;
+  const int64_t target_threads = 256 * 4 * 4 * 64;
+  while (T < 32 && a.n_groups * T < target_threads) T <<= 1;
+  if (net->force_team > 0) T = net->force_team;
+  int ti = -1;
+  for (int k = 0; k < 5; ++k)
+    if (kTeamSizes[k] == T) ti = k;
+  if (T != 1 && (ti < 0 || net->lds_team[ti] > 160 * 1024)) T = 1, ti = -1;
+  if (T == 1 && net->lds_lane > 160 * 1024) ti = 4;
+  if (ti < 0) {
+    const int threads = 64 * net->waves_per_block;
+    const unsigned blocks = (unsigned)((a.n_groups + threads - 1) / threads);
+    hipLaunchKernelGGL(net->lane, dim3(blocks), dim3(threads), net->lds_lane, (hipStream_t)stream, a);
+  } else {
+    const int gpb = 256 / kTeamSizes[ti];
+    const unsigned blocks = (unsigned)((a.n_groups + gpb - 1) / gpb);
+    hipLaunchKernelGGL(net->team[ti], dim3(blocks), dim3(256), net->lds_team[ti], (hipStream_t)stream, a);
+  }
   HIP_OK(hipGetLastError());
   return PBN_OK;
 }

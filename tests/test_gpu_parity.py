@@ -142,3 +142,13 @@ def test_abi_rejects_bad_arguments():
                     env.target.data_ptr(), env.t.data_ptr(), env.state.data_ptr(), None,
                     env.reward.data_ptr(), env.flags.data_ptr(), None)
     assert rc == -22
+
+
+@pytest.mark.parametrize("team", [1, 2, 4, 8, 16, 32])
+@pytest.mark.parametrize("name", ["pbn7", "pbn28", "pbn70"])
+def test_every_launch_shape(name, team, monkeypatch):
+    """Each kernel variant (one thread per group, or a team of T lanes per group)
+    gives the oracle's results; PBN_TEAM forces the variant at pbn_net_create."""
+    monkeypatch.setenv("PBN_TEAM", str(team))
+    run_pair(make_spec(name, perturbation=0.05), 4096, 6, mode=3, env_offset=1024)
+    run_pair(make_spec(name, perturbation=0.05), 2048, 4, mode=0)
