@@ -1,0 +1,274 @@
+"""PBNEnv: the gym-PBN environment surface, backed by the HIP step.
+
+Drop-in for the env the reference builds with
+``gym.make("gym-PBN/PBNEnv", N=, genes=, logic_functions=[, min_attractors=])``
+(train_assa_BQN.py:121-124, model_tester.py:409-413) or
+``gym.make("gym-PBN/BittnerMultiGeneral", N=28, horizon=20, min_attractors=7)``
+(train_BDQ.py:50), exposing the attribute surface its callers use
+(SURVEY.md Appendix A):
+
+  reset() -> ((state, target), info)              bdq_model/__init__.py:161,204
+  step(actions) -> (obs, reward, term, trunc, info)  bdq_model/__init__.py:177
+      actions: list of ints / 0-d (CUDA) tensors, a tensor, an int, or []
+      (0 = no-op, a > 0 flips node a-1, duplicates count once: bdq_model/__init__.py:76-84,176)
+  observation_space.shape[0]                      train_BDQ.py:82
+  attracting_states, all_attractors, real_attractors      bdq_model/__init__.py:60,182
+  state_attractor_id, target_attractor_id         bdq_model/__init__.py:180
+  rework_probas(ep_len=None)                      bdq_model/__init__.py:203
+  is_attracting_state(s), in_target(s), setTarget(a), render()   model_tester.py:611-625,
+                                                  graph_classifier/__init__.py:129
+  graph.setState(s), graph.nodes[i].index / .predictors, graph.getNodeByID(id)
+                                                  gbdq_model/__init__.py:264-274
+  env.env.env chain, close()                      train_pbn_BQN.py:90, train_BDQ.py:116
+
+One PBNEnv is one env (gym semantics: no autoreset; callers call reset()).  It
+runs on the GPU as a 32-env group of which env 0 is the visible one; every
+step is one pbn_step launch plus a tiny device->host copy.  Use VectorPBNEnv
+for batched rollouts.
+"""
+from __future__ import annotations
+
+import warnings
+from typing import List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+import torch
+
+from . import _lib
+from .attractors import Attractors, clean_state, find_attractors, load_attractors
+from .network import Network, load_network
+from .spec import NO_TARGET, EnvSpec
+from .vector_env import VectorPBNEnv
+
+__all__ = ["PBNEnv", "make", "Box", "MultiDiscrete"]
+
+
+class Box:
+    def __init__(self, low, high, shape, dtype=np.int8):
+        self.low, self.high, self.shape, self.dtype = low, high, tuple(shape), dtype
+
+    def sample(self, rng=None):
+        rng = rng or np.random.default_rng()
+        return rng.integers(self.low, self.high + 1, size=self.shape).astype(self.dtype)
+
+
+class MultiDiscrete:
+    def __init__(self, nvec):
+        self.nvec = np.asarray(nvec)
+        self.shape = self.nvec.shape
+
+    def sample(self, rng=None):
+        rng = rng or np.random.default_rng()
+        return rng.integers(0, self.nvec)
+
+
+class _Node:
+    """gym-PBN style node: ``index``, ``ID`` and ``predictors = [(IDs, A, COD)]``."""
+
+    def __init__(self, index: int, name: str, predictors):
+        self.index = index
+        self.ID = name
+        self.name = name
+        self.predictors = predictors
+
+
+class _Graph:
+    def __init__(self, env: "PBNEnv"):
+        self._env = env
+        net = env.spec.network
+        thr = net.thresholds(env.spec.prob_bits)
+        self.nodes: List[_Node] = []
+        for i, fl in enumerate(net.nodes):
+            preds, prev = [], 0
+            for f, c in zip(fl, thr[i]):
+                A = np.array([(f.table >> m) & 1 for m in range(1 << f.arity)], dtype=np.int8)
+                preds.append((tuple(net.genes[g] for g in f.inputs), A, (c - prev) / float(1 << env.spec.prob_bits)))
+                prev = c
+            self.nodes.append(_Node(i, net.genes[i], preds))
+        self._by_id = {n.ID: n for n in self.nodes}
+
+    def getNodeByID(self, ident):
+        return self._by_id[ident]
+
+    def setState(self, state: Sequence) -> None:
+        self._env._set_state(clean_state(state))
+
+    def getState(self):
+        return self._env.render()
+
+    def genSTG(self):
+        """State-transition graph {state: set(successor states)} for small networks."""
+        from .attractors import _successor_options  # exhaustive, N <= 20
+        net = self._env.spec.network
+        if net.n > 20:
+            raise ValueError("genSTG is exhaustive; limited to 20 nodes")
+        stg = {}
+        for s in range(1 << net.n):
+            opts = _successor_options(net, s)
+            nexts = [0]
+            for i, vals in enumerate(opts):
+                nexts = [x | (v << i) for x in nexts for v in vals]
+            stg[tuple(net.unpack([s]))] = {tuple(net.unpack([x])) for x in nexts}
+        return stg
+
+
+class PBNEnv:
+    metadata = {"render_modes": ["human", "PBN"]}
+
+    def __init__(self, N: Optional[int] = None, genes: Optional[Sequence[str]] = None, logic_functions=None,
+                 min_attractors: Optional[int] = None, *, network: Union[str, Network, None] = None,
+                 attractors: Optional[Attractors] = None, horizon: int = 20, perturbation: float = 0.01,
+                 prob_bits: int = 16, seed: Optional[int] = None, device=None, render_mode=None,
+                 success_reward: float = 5.0, wrong_attractor_cost: float = 2.0, action_cost: float = 1.0,
+                 step_cost: float = 0.0, name: Optional[str] = None):
+        if isinstance(network, str):
+            if attractors is None:
+                attractors = load_attractors(network)
+            network = load_network(network)
+        elif network is None:
+            if genes is None or logic_functions is None:
+                raise ValueError("give network= or genes= and logic_functions=")
+            network = Network.from_logic_functions(genes, logic_functions, name=name or "pbn")
+        if N is not None and N != network.n:
+            raise ValueError(f"N={N} but the network has {network.n} nodes")
+        if attractors is None:
+            attractors = find_attractors(network) if network.n <= 20 else []
+        if min_attractors is not None and len(attractors) < min_attractors:
+            warnings.warn(f"network has {len(attractors)} attractors < min_attractors={min_attractors}")
+        self.spec = EnvSpec(network, attractors, perturbation=perturbation, prob_bits=prob_bits, horizon=horizon,
+                            success_reward=success_reward, wrong_attractor_cost=wrong_attractor_cost,
+                            action_cost=action_cost, step_cost=step_cost)
+        self.N = network.n
+        self.render_mode = render_mode
+        self._seed = int(seed if seed is not None else np.random.SeedSequence().entropy % (1 << 63))
+        self._venv = VectorPBNEnv(self.spec, 1, seed=self._seed, device=device, autoreset=False)
+        self.observation_space = Box(0, 1, (self.N,))
+        self.action_space = MultiDiscrete([self.N + 1] * 3)
+        self.discrete_action_space = self.action_space
+        self.graph = _Graph(self)
+        self.all_attractors: List[List[Tuple[int, ...]]] = [list(a) for a in self.spec.attractors]
+        self.real_attractors = self.all_attractors
+        self.attracting_states = [s for a in self.all_attractors for s in a]
+        self.state_attractor_id = -1
+        self.target_attractor_id = -1
+        self.target = None
+        self.n_steps = 0
+        self.target_nodes: List[int] = []
+        self.control_nodes = list(range(self.N))
+        self._ep_lens: List[int] = []
+
+    # gymnasium wrapper chain compatibility (env.env.env, env.unwrapped)
+    @property
+    def env(self):
+        return self
+
+    @property
+    def unwrapped(self):
+        return self
+
+    # ---------------------------------------------------------------- core
+    def _read_state(self) -> np.ndarray:
+        w = self._venv.state[:, 0].cpu().numpy().view(np.uint32)
+        return np.array(self.spec.network.unpack(list(w)), dtype=np.int64)
+
+    def _set_state(self, bits: Tuple[int, ...]) -> None:
+        words = torch.tensor(np.array(self.spec.network.pack(bits), dtype=np.uint32).view(np.int32)[:, None],
+                             device=self._venv.device)
+        self._venv.state[:, :1].copy_(words)
+
+    def reset(self, seed: Optional[int] = None, options=None):
+        if seed is not None:
+            self._seed = int(seed)
+        self._venv.reset(seed=self._seed)
+        state = self._read_state()
+        tgt = int(self._venv.target[0].item())
+        self.target_attractor_id = tgt if tgt != NO_TARGET else -1
+        self.state_attractor_id = self.spec.attractor_id(state)
+        self.target = list(self.all_attractors[tgt][0]) if tgt != NO_TARGET else None
+        target_vec = np.array(self.target if self.target is not None else [0] * self.N, dtype=np.int64)
+        self.n_steps = 0
+        return (state, target_vec), {"target_attractor": self.target_attractor_id,
+                                     "state_attractor": self.state_attractor_id}
+
+    @staticmethod
+    def _actions(action) -> List[int]:
+        if action is None:
+            return []
+        if isinstance(action, torch.Tensor):
+            return [int(x) for x in action.reshape(-1).tolist()]
+        if isinstance(action, np.ndarray):
+            return [int(x) for x in action.reshape(-1)]
+        if isinstance(action, (int, np.integer)):
+            return [int(action)]
+        return [int(x.item()) if isinstance(x, torch.Tensor) else int(x) for x in action]
+
+    def step(self, action):
+        acts = self._actions(action)
+        bits = [0] * self.N
+        for a in acts:
+            if not 0 <= a <= self.N:
+                raise ValueError(f"action {a} outside [0, {self.N}]")
+            if a > 0:
+                bits[a - 1] = 1
+        fm = torch.tensor(np.array(self.spec.network.pack(bits), dtype=np.uint32).view(np.int32)[:, None],
+                          device=self._venv.device)
+        state_w, reward, flags = self._venv.step_flipmask(fm)
+        fl = int(flags[0].item())
+        r = float(reward[0].item())
+        obs = self._read_state()
+        self.n_steps += 1
+        info = {"perturbed": bool(fl & _lib.FLAG_PERTURBED), "in_attractor": bool(fl & _lib.FLAG_IN_ATTRACTOR),
+                "flags": fl}
+        return obs, r, bool(fl & _lib.FLAG_TERMINATED), bool(fl & _lib.FLAG_TRUNCATED), info
+
+    # ------------------------------------------------------ attribute surface
+    def render(self):
+        return list(self._read_state())
+
+    def is_attracting_state(self, state) -> bool:
+        return self.spec.attractor_id(clean_state(state)) >= 0
+
+    def in_target(self, state) -> bool:
+        if self.target_attractor_id < 0:
+            return False
+        return tuple(clean_state(state)) in set(self.all_attractors[self.target_attractor_id])
+
+    def setTarget(self, target) -> None:
+        """target: an attractor (list of states), one state, or an attractor index."""
+        if isinstance(target, (int, np.integer)):
+            idx = int(target)
+        else:
+            first = target[0] if len(target) and isinstance(target[0], (list, tuple, np.ndarray)) else target
+            idx = self.spec.attractor_id(clean_state(first))
+            if idx < 0:
+                raise ValueError("target is not a state of a known attractor")
+        self.target_attractor_id = idx
+        self.target = list(self.all_attractors[idx][0])
+        self._venv.target[:1].fill_(idx)
+
+    def rework_probas(self, ep_len: Optional[int] = None) -> None:
+        """The fork of gym-PBN reweights future (start, target) draws after each episode
+        (bdq_model/__init__.py:203); that rule is unavailable.  Reset draws
+        here are uniform and keyed by (seed, env, step); episode lengths are only recorded."""
+        if ep_len is not None:
+            self._ep_lens.append(int(ep_len))
+
+    def close(self) -> None:
+        self._venv.close()
+
+
+def make(env_id: str, **kwargs):
+    """Minimal stand-in for gymnasium.make over the env ids the reference uses."""
+    key = env_id.split("/")[-1]
+    if key == "PBNEnv":
+        return PBNEnv(**kwargs)
+    if key.startswith("BittnerMultiGeneral") or key.startswith("BittnerMulti-") or key.startswith("Bittner-"):
+        n = kwargs.pop("N", None)
+        if n is None:
+            digits = "".join(c for c in key.split("-")[-1] if c.isdigit())
+            n = int(digits) if digits else 28
+        bundled = {7: "pbn7", 10: "pbn10", 28: "pbn28", 70: "pbn70"}
+        if n not in bundled:
+            raise ValueError(f"no bundled Bittner network with {n} nodes (have {sorted(bundled)})")
+        return PBNEnv(network=bundled[n], **kwargs)
+    raise ValueError(f"unknown env id {env_id!r}")

@@ -1,0 +1,30 @@
+"""Test helper: an oracle-backed stand-in for VectorPBNEnv on CPU tensors (used to
+exercise the multi-rank sharding / gather logic with gloo, without a GPU)."""
+import numpy as np
+import torch
+
+from oracle import oracle
+
+
+class OracleVectorEnv:
+    def __init__(self, spec, env_offset, count, seed=0):
+        self.spec, self.env_offset, self.count, self.seed = spec, env_offset, count, seed
+        self.words = spec.words
+        st, tg, t = oracle.reset(spec, seed, 0, env_offset, count)
+        self._st, self._tg, self._t = st, tg, t
+        self.step_index = 1
+        self.state = torch.from_numpy(st.view(np.int32).copy())
+        self.flipmask = torch.zeros_like(self.state)
+        self.final_state = torch.zeros_like(self.state)
+
+    def step_flipmask(self, flipmask=None, random_actions=False):
+        flip = np.zeros_like(self._st) if flipmask is None else flipmask.numpy().view(np.uint32)
+        mode = 1 | (2 if random_actions else 0)
+        out = oracle.step(self.spec, self.seed, self.step_index, self.env_offset, self._st, flip, self._tg,
+                          self._t, mode)
+        self.step_index += 1
+        self._st, self._tg, self._t = out["state_out"], out["target"], out["t"]
+        self.state = torch.from_numpy(out["state_out"].view(np.int32).copy())
+        self.flipmask = torch.from_numpy(out["flipmask"].view(np.int32).copy())
+        self.final_state = torch.from_numpy(out["final_state"].view(np.int32).copy())
+        return self.state, torch.from_numpy(out["reward"]), torch.from_numpy(out["flags"])

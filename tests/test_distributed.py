@@ -1,0 +1,63 @@
+"""Env sharding + the per-rollout gather, world_size 2 over gloo on CPU.
+The union of the shards' transitions must equal a single-process run."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from pbn_rl_amd.distributed import ShardedRollout, record_rows, shard_range
+
+
+def test_shard_range_partitions():
+    for n, w in [(256, 2), (64 * 7, 3), (32, 1), (1 << 20, 8)]:
+        parts = [shard_range(n, w, r) for r in range(w)]
+        assert parts[0][0] == 0
+        for (o, c), (o2, _) in zip(parts, parts[1:]):
+            assert o + c == o2 and o % 32 == 0 and c % 32 == 0
+        assert sum(c for _, c in parts) == n
+    with pytest.raises(ValueError):
+        shard_range(100, 2, 0)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, n_total, steps, result_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pbn_rl_amd.attractors import load_attractors
+    from pbn_rl_amd.network import load_network
+    from pbn_rl_amd.spec import EnvSpec
+    from tests.oracle_env import OracleVectorEnv
+
+    spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.05)
+    ro = ShardedRollout(n_total, lambda off, cnt: OracleVectorEnv(spec, off, cnt, seed=11))
+    rec = ro.rollout(steps)
+    glob = ShardedRollout.to_global(ro.gather(rec))
+    if rank == 0:
+        torch.save(glob, result_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gather_equals_single_run(tmp_path):
+    from pbn_rl_amd.attractors import load_attractors
+    from pbn_rl_amd.network import load_network
+    from pbn_rl_amd.spec import EnvSpec
+    from tests.oracle_env import OracleVectorEnv
+
+    n_total, steps = 256, 4
+    out = str(tmp_path / "gathered.pt")
+    mp.spawn(_worker, args=(2, _free_port(), n_total, steps, out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.05)
+    single = ShardedRollout(n_total, lambda off, cnt: OracleVectorEnv(spec, off, cnt, seed=11))
+    want = single.rollout(steps)
+    assert got.shape == (steps, record_rows(1), n_total)
+    assert torch.equal(got, want)

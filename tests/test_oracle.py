@@ -1,0 +1,135 @@
+"""The CPU oracle: golden vectors, C == Python restatements, and the laws the
+reference's data pins independently of the RNG (per-node marginals, fixture
+self-loop probabilities, perturbation rate)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle, pyoracle
+from pbn_rl_amd.attractors import load_attractors
+from pbn_rl_amd.network import load_network
+from pbn_rl_amd.spec import EnvSpec
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def spec_for(name, **kw):
+    return EnvSpec(load_network(name), load_attractors(name), **kw)
+
+
+@pytest.mark.parametrize("name", ["pbn7", "pbn28", "pbn70"])
+def test_golden_vectors(name):
+    g = np.load(os.path.join(GOLDEN, f"steps_{name}.npz"))
+    spec = spec_for(name, perturbation=float(g["perturbation"]))
+    seed, off = int(g["seed"]), int(g["env_offset"])
+    n = g["reset_state"].shape[1]
+    st, tg, t = oracle.reset(spec, seed, 0, off, n)
+    assert np.array_equal(st, g["reset_state"]) and np.array_equal(tg, g["reset_target"])
+    for k in range(8):
+        mode = 3 if k % 2 == 0 else 1
+        out = oracle.step(spec, seed, k + 1, off, g[f"in_state_{k}"], g[f"in_flip_{k}"],
+                          g[f"in_target_{k}"], g[f"in_t_{k}"], mode)
+        for key in ("state_out", "final_state", "reward", "flags", "target", "t", "flipmask"):
+            assert np.array_equal(out[key], g[f"out_{key}_{k}"]), (name, k, key)
+
+
+@pytest.mark.parametrize("name", ["pbn7", "pbn10", "pbn28", "pbn70"])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_c_oracle_equals_python_oracle(name, mode):
+    spec = spec_for(name, perturbation=0.08, horizon=4)
+    net = spec.network
+    n, seed, off = 64, 31337, 64
+    W = spec.words
+    py = pyoracle.PyPBN(spec)
+    rng = np.random.default_rng(5)
+    st, tg, t = oracle.reset(spec, seed, 0, off, n)
+    for i in range(n):
+        s, a, tt = py.reset(seed, 0, off + i)
+        assert net.pack(s) == [int(st[w, i]) for w in range(W)] and a == tg[i] and tt == 0
+    for step in range(1, 5):
+        flip = rng.integers(0, 2 ** 32, size=(W, n), dtype=np.uint64).astype(np.uint32) & np.uint32(0x00100201)
+        res = oracle.step(spec, seed, step, off, st, flip, tg, t, mode)
+        for i in range(n):
+            bits = net.unpack([int(st[w, i]) for w in range(W)])
+            fb = net.unpack([int(flip[w, i]) for w in range(W)])
+            r = py.step(seed, step, off + i, bits, fb, int(tg[i]), int(t[i]), mode)
+            assert net.pack(r["final_state"]) == [int(res["final_state"][w, i]) for w in range(W)]
+            assert net.pack(r["state_out"]) == [int(res["state_out"][w, i]) for w in range(W)]
+            assert r["flags"] == res["flags"][i] and r["t"] == res["t"][i] and r["target"] == res["target"][i]
+            assert np.float32(r["reward"]) == res["reward"][i]
+        st, tg, t = res["state_out"], res["target"], res["t"]
+
+
+def _one_step_from(spec, state_bits, n, seed=99, mode=0):
+    net = spec.network
+    W = spec.words
+    words = np.array(net.pack(state_bits), dtype=np.uint32)
+    st = np.repeat(words[:, None], n, axis=1)
+    zeros = np.zeros((W, n), dtype=np.uint32)
+    out = oracle.step(spec, seed, 1, 0, st, zeros, np.full(n, 255, np.uint8), np.zeros(n, np.uint8), mode,
+                      n_threads=8)
+    return out
+
+
+def test_per_node_marginal_law():
+    """P(x'_i = 1 | s) = sum of the weights of functions true at s (quantised), per node."""
+    spec = spec_for("pbn28", perturbation=0.0, horizon=0)
+    net = spec.network
+    rng = np.random.default_rng(2)
+    n = 1 << 16
+    for _ in range(3):
+        s = list(rng.integers(0, 2, size=net.n))
+        out = _one_step_from(spec, s, n)
+        bits = (out["final_state"][0][None, :] >> np.arange(net.n, dtype=np.uint32)[:, None]) & 1
+        emp = bits.mean(axis=1)
+        want = np.array(net.marginal_one(s, 16))
+        sigma = np.sqrt(np.maximum(want * (1 - want), 1e-12) / n)
+        assert np.all(np.abs(emp - want) <= 5 * sigma + 1e-12), np.abs(emp - want) / (sigma + 1e-12)
+
+
+def test_fixture_self_loop_probabilities():
+    """SURVEY.md 8(c) fixture 1: P(s -> s) at the 14 Bittner-28 attractor states."""
+    spec = spec_for("pbn28", perturbation=0.0, horizon=0)
+    net = spec.network
+    n = 1 << 15
+    for att in load_attractors("pbn28")[:6]:
+        s = list(att[0])
+        out = _one_step_from(spec, s, n)
+        emp = (out["final_state"][0] == net.pack(s)[0]).mean()
+        want = net.self_loop_probability(s, 16)
+        assert abs(emp - want) < 5 * np.sqrt(want * (1 - want) / n)
+        # an attracting state is flagged; with target == its own attractor, staying terminates
+        assert (out["flags"][out["final_state"][0] == net.pack(s)[0]] & 4).all()
+
+
+def test_perturbation_statistics():
+    p = 0.05
+    spec = spec_for("pbn28", perturbation=p, horizon=0)
+    n = 1 << 16
+    s = [0] * 28
+    out = _one_step_from(spec, s, n)
+    pert = (out["flags"] & 8) != 0
+    want = 1 - (1 - p) ** 28
+    assert abs(pert.mean() - want) < 5 * np.sqrt(want * (1 - want) / n)
+    # perturbed envs: s' = s ^ gamma, E[|gamma|] = N p / P(any)
+    pc = np.array([bin(int(x)).count("1") for x in out["final_state"][0][pert]])
+    assert abs(pc.mean() - 28 * p / want) < 0.03
+
+
+def test_group_alignment_required():
+    spec = spec_for("pbn7")
+    st = np.zeros((1, 48), np.uint32)
+    with pytest.raises(ValueError):
+        oracle.step(spec, 1, 1, 0, st, st, np.zeros(48, np.uint8), np.zeros(48, np.uint8), 0)
+
+
+def test_shard_invariance_oracle():
+    spec = spec_for("pbn28")
+    n = 256
+    st, tg, t = oracle.reset(spec, 5, 0, 0, n)
+    full = oracle.step(spec, 5, 1, 0, st, np.zeros_like(st), tg, t, 3)
+    a = oracle.step(spec, 5, 1, 0, st[:, :128], np.zeros_like(st[:, :128]), tg[:128], t[:128], 3)
+    b = oracle.step(spec, 5, 1, 128, st[:, 128:], np.zeros_like(st[:, 128:]), tg[128:], t[128:], 3)
+    for key in ("state_out", "reward", "flags", "target", "t", "flipmask"):
+        assert np.array_equal(full[key], np.concatenate([a[key], b[key]], axis=-1)), key
