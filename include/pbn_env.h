@@ -14,6 +14,7 @@
  *        bdq_model/__init__.py:177, graph_classifier/__init__.py:148,
  *        model_tester.py:561,624, ddqn_per/__init__.py:354     -> pbn_step
  *   env.close()  train_BDQ.py:116                              -> pbn_net_destroy
+ *   T frames of the frame loop bdq_model/__init__.py:172-213     -> pbn_rollout
  *
  * The Python facade (pbn_rl_amd.env.PBNEnv / pbn_rl_amd.vector_env.VectorPBNEnv)
  * keeps that gym surface and calls these entry points through ctypes;
@@ -141,6 +142,20 @@ int pbn_step(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, in
              uint32_t mode, const uint32_t* d_state, uint32_t* d_flipmask, uint8_t* d_target,
              uint8_t* d_t, uint32_t* d_state_out, uint32_t* d_final_state, float* d_reward,
              uint8_t* d_flags, void* stream);
+
+/*
+ * n_steps synchronous transitions in one launch (steps step .. step+n_steps-1), with the
+ * envs' state kept on chip between steps.  Bit-identical to n_steps successive pbn_step
+ * calls that ping-pong d_state.  State, target and t are updated in place.
+ *   d_flipmask     [n_steps][W][n]  in, or out with PBN_MODE_RANDOM_ACTIONS
+ *   d_obs          [n_steps][W][n]  out: observation before each step (nullable)
+ *   d_final_state  [n_steps][W][n]  out: s' of each step (nullable)
+ *   d_reward, d_flags  [n_steps][n] out
+ */
+int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs,
+                int32_t n_steps, uint32_t mode, uint32_t* d_state, uint32_t* d_flipmask, uint8_t* d_target,
+                uint8_t* d_t, uint32_t* d_obs, uint32_t* d_final_state, float* d_reward, uint8_t* d_flags,
+                void* stream);
 
 const char* pbn_last_error(void);
 int pbn_abi_version(void);

@@ -23,7 +23,7 @@ FLAG_IN_ATTRACTOR = 4
 FLAG_PERTURBED = 8
 FLAG_RESET = 16
 
-EXPORTS = ["pbn_net_create", "pbn_net_destroy", "pbn_net_words", "pbn_reset", "pbn_step",
+EXPORTS = ["pbn_net_create", "pbn_net_destroy", "pbn_net_words", "pbn_reset", "pbn_step", "pbn_rollout",
            "pbn_last_error", "pbn_abi_version"]
 
 _lib: Optional[ctypes.CDLL] = None
@@ -33,25 +33,27 @@ class PbnError(RuntimeError):
     pass
 
 
-def build(verbose: bool = False) -> str:
-    """Compile csrc/pbn_env.hip for gfx950 into pbn_rl_amd/libpbn_env.so (in-tree)."""
+def build(verbose: bool = False, out: str = LIB_PATH, defines=()) -> str:
+    """Compile csrc/pbn_env.hip for gfx950 into pbn_rl_amd/libpbn_env.so (in-tree).
+    ``defines`` builds a diagnostic variant (e.g. PBN_STAMPS) into another path."""
     src = os.path.join(SRC_DIR, "pbn_env.hip")
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-unused-result", "-o", LIB_PATH + ".tmp", src]
+           "-Wno-unused-result", *[f"-D{d}" for d in defines], "-o", out + ".tmp", src]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(LIB_PATH + ".tmp", LIB_PATH)
-    return LIB_PATH
+    os.replace(out + ".tmp", out)
+    return out
 
 
 def load() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise PbnError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
-    L = ctypes.CDLL(LIB_PATH)
+    path = os.environ.get("PBN_LIB", LIB_PATH)  # diagnostic builds only
+    if not os.path.exists(path):
+        raise PbnError(f"{path} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(path)
     vp, u64, i64, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64, ctypes.c_uint32
     L.pbn_net_create.argtypes = [vp, ctypes.POINTER(vp)]
     L.pbn_net_create.restype = ctypes.c_int
@@ -63,6 +65,8 @@ def load() -> ctypes.CDLL:
     L.pbn_reset.restype = ctypes.c_int
     L.pbn_step.argtypes = [vp, u64, u64, u64, i64, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.pbn_step.restype = ctypes.c_int
+    L.pbn_rollout.argtypes = [vp, u64, u64, u64, i64, ctypes.c_int32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.pbn_rollout.restype = ctypes.c_int
     L.pbn_last_error.argtypes = []
     L.pbn_last_error.restype = ctypes.c_char_p
     L.pbn_abi_version.argtypes = []

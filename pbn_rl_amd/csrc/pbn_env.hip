@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <math.h>
 #include <stdio.h>
 #include <string.h>
 #include <stdlib.h>
@@ -36,6 +37,7 @@ using pbn::Word4;
 namespace {
 
 constexpr int kFuncRecWords = 24;  // in[4], leaf[16], thr, pad[3]
+constexpr int kNodeRecs = 4;       // compact records prefetched per node by the wave kernel
 constexpr int kMaxHashBits = 12;
 
 struct FuncRec {
@@ -73,8 +75,32 @@ struct StepArgs {
   int tab_words;     // words of the LDS table image
   int prob_bits;
   int n_funcs;
+  int wave_words;    // wave kernel: per-wave LDS words (tables + S planes)
+  int gap_exact;     // 1: binary search for gaps (p == 0 or tiny); 0: log estimate + fix-up
+  float inv_log2q;   // 1 / log2(1 - p)
+  const uint4* fcompact;   // [n_funcs] {inputs (4 x u8), truth table, threshold, 0}
+  const uint4* nrec;       // [N * kNodeRecs] node-major copy of the first records (+ nf, f0 in .w)
   uint32_t hash_mult[4];
+  unsigned long long* stamps;  // diagnostic builds (-DPBN_STAMPS) only: per-wave phase clocks
+  int n_steps;       // steps per launch (wave kernel); outputs are [n_steps][...] arrays
+  uint32_t* obs;     // [n_steps][W][n] observation before each step (nullable)
 };
+
+// In-kernel phase clocks (cdna_hip_programming.md section 7, "In-kernel stamps"):
+// compiled only into the diagnostic library (-DPBN_STAMPS), never the product.
+#ifdef PBN_STAMPS
+#define PBN_STAMP(k)                                                                          \
+  do {                                                                                        \
+    unsigned long long t_;                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    if (a.stamps && (threadIdx.x & 63) == 0)                                                  \
+      a.stamps[(size_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + (k)] = t_; \
+  } while (0)
+#else
+#define PBN_STAMP(k) do {} while (0)
+#endif
 
 // ---------------------------------------------------------------- helpers
 __device__ __forceinline__ uint32_t valid_word_mask(int n, int w) {
@@ -109,14 +135,15 @@ __device__ __forceinline__ uint32_t eval_func(const FuncRec* __restrict__ fr,
 }
 
 // lanes-of-32-envs bit mask of (u < c), u = digits dig[0..B) MSB first (B = prob_bits).
+// From the least significant digit up: lt' = c_d ? (u_d ? lt : 1) : (u_d ? 0 : lt),
+// one v_bitop3_b32 per digit over (u_d, lt, C_d) with LUT 0x8E.
 __device__ __forceinline__ uint32_t less_than(const uint32_t (&dig)[16], uint32_t c, int B) {
   uint32_t lt = 0;
 #pragma unroll
   for (int d = 15; d >= 0; --d) {
     if (d < B) {
-      const uint32_t C = ((c >> (B - 1 - d)) & 1u) ? 0xFFFFFFFFu : 0u;
-      const uint32_t m = dig[d] ^ ~C;
-      lt = bfi(m, lt, C);
+      const uint32_t C = (uint32_t)__builtin_amdgcn_sbfe((int)c, B - 1 - d, 1);
+      lt = __builtin_amdgcn_bitop3_b32(dig[d], lt, C, 0x8E);
     }
   }
   return lt;
@@ -447,16 +474,6 @@ __global__ void __launch_bounds__(128) pbn_step_lane(StepArgs a) {
   }
 }
 
-// ------------------------------------------- step kernel, a team of T threads per group
-//
-// For batches too small to fill 256 CUs with one thread per 32-env group, T
-// lanes of one wave share a group: each lane runs the per-env work of 32/T envs
-// and the node loop of nodes i = j, j+T, ...; the group's state planes are
-// exchanged through LDS.  Per-group LDS: S[32W] planes of s1, R[32W] planes of
-// s1^gamma (then of s'), WS/WR[32][W] per-env words, P (perturbed mask).
-// FuncRecs and node ranges are staged in LDS because each lane evaluates a
-// different node.
-
 // eval of a lane-varying function: record in LDS, planes in LDS
 __device__ __forceinline__ uint32_t eval_func_lds(const uint32_t* __restrict__ fr,
                                                   const uint32_t* __restrict__ S) {
@@ -473,64 +490,246 @@ __device__ __forceinline__ uint32_t eval_func_lds(const uint32_t* __restrict__ f
   return bfi(x3, bfi(x2, w3, w2), bfi(x2, w1, w0));
 }
 
-template <int W, int T>
-__global__ void __launch_bounds__(256) pbn_step_team(StepArgs a) {
-  constexpr int GPB = 256 / T;        // groups per block
-  constexpr int EPT = 32 / T;         // envs per thread
-  constexpr int GW = 32 * W;          // planes per group
-  constexpr int GSTRIDE = 4 * GW + 4; // LDS words per group
+// ------------------------------------------- step kernel, one wave per 32-env group
+//
+// For batches too small to fill the chip with one thread per group.  Lane j of
+// the wave is env j (lanes 0-31) for the per-env work and node j (+32r) for the
+// node work, so the node loop runs in parallel across lanes.  No block barrier:
+// every wave stages its own copy of the small tables + FuncRecs in LDS, and all
+// global loads are issued before the Philox batch so their latency hides under it.
+//   1. Philox: the lower half computes each env's ENV call and the first half of
+//      its node's selection calls, the upper half the other selection calls plus
+//      each env's first continuation-gap call; results meet via lane swaps;
+//   2. per env (lower lanes): interventions, perturbation (gap = linear count
+//      against the CDF in SGPRs for N <= 32), reset word;
+//   3. 32x32 bit transposes as 5-stage cross-lane butterflies on DPP
+//      (quad_perm, row_ror) and v_permlane16_swap: lane p ends up holding plane p;
+//   4. lane i evaluates node i; selection digits stay in its registers;
+//   5. butterfly back to per-env words, reward/termination/autoreset, stores.
+
+// y = a of lane ^ J (J in 1, 2, 4, 8, 16), within 32-lane halves, without LDS
+template <int J>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t a, int lane) {
+  if constexpr (J == 1) {
+    return __builtin_amdgcn_update_dpp(0u, a, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  } else if constexpr (J == 2) {
+    return __builtin_amdgcn_update_dpp(0u, a, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  } else if constexpr (J == 4) {
+    const uint32_t r4 = __builtin_amdgcn_update_dpp(0u, a, 0x124, 0xF, 0xF, false);   // row_ror:4
+    const uint32_t r12 = __builtin_amdgcn_update_dpp(0u, a, 0x12C, 0xF, 0xF, false);  // row_ror:12
+    return (lane & 4) ? r4 : r12;
+  } else if constexpr (J == 8) {
+    return __builtin_amdgcn_update_dpp(0u, a, 0x128, 0xF, 0xF, false);  // row_ror:8
+  } else {
+    const auto r = __builtin_amdgcn_permlane16_swap(a, a, false, false);
+    return (lane & 16) ? r[0] : r[1];
+  }
+}
+
+template <int J>
+__device__ __forceinline__ uint32_t transpose_step(uint32_t a, int lane) {
+  constexpr uint32_t M = J == 16 ? 0x0000FFFFu : (J == 8 ? 0x00FF00FFu : (J == 4 ? 0x0F0F0F0Fu : (J == 2 ? 0x33333333u : 0x55555555u)));
+  const uint32_t y = xor_lane<J>(a, lane);
+  return (lane & J) ? bfi(M, y >> J, a) : bfi(M, a, y << J);
+}
+
+// lane k holds row k of a 32x32 bit matrix (per 32-lane half); afterwards lane c holds column c
+__device__ __forceinline__ uint32_t lane_transpose32(uint32_t a, int lane) {
+  a = transpose_step<16>(a, lane);
+  a = transpose_step<8>(a, lane);
+  a = transpose_step<4>(a, lane);
+  a = transpose_step<2>(a, lane);
+  a = transpose_step<1>(a, lane);
+  return a;
+}
+
+// eval of a lane-varying function from its compact record: 4 input planes, 16-bit
+// truth table T; leaf masks are sign-extended table bits (v_bfe_i32).
+__device__ __forceinline__ uint32_t eval_compact(uint32_t ins, uint32_t T, const uint32_t* __restrict__ S) {
+  const uint32_t x0 = S[ins & 0xFFu], x1 = S[(ins >> 8) & 0xFFu], x2 = S[(ins >> 16) & 0xFFu], x3 = S[ins >> 24];
+  uint32_t v[8];
+#pragma unroll
+  for (int mm = 0; mm < 8; ++mm) {
+    const uint32_t l0 = (uint32_t)__builtin_amdgcn_sbfe((int)T, 2 * mm, 1);
+    const uint32_t l1 = (uint32_t)__builtin_amdgcn_sbfe((int)T, 2 * mm + 1, 1);
+    v[mm] = bfi(x0, l1, l0);
+  }
+  const uint32_t w0 = bfi(x1, v[1], v[0]), w1 = bfi(x1, v[3], v[2]), w2 = bfi(x1, v[5], v[4]), w3 = bfi(x1, v[7], v[6]);
+  return bfi(x3, bfi(x2, w3, w2), bfi(x2, w1, w0));
+}
+
+// gap(u) = min{m : u < C[m-1]} from a float estimate of log(1-x)/log(1-p) corrected
+// exactly (+-1) against the integer CDF in LDS; C padded with 0xFFFFFFFF.
+__device__ __forceinline__ int gap_est(const uint32_t* __restrict__ cdf, int len, float inv_log2q, uint32_t u) {
+  const float x = (float)u * 2.3283064365386963e-10f;   // u / 2^32
+  const float l2 = __builtin_amdgcn_logf(1.0f - x);     // v_log_f32: log2
+  float est = floorf(l2 * inv_log2q) + 1.0f;
+  est = fminf(fmaxf(est, 1.0f), (float)len);
+  int g = (int)est;
+  const uint32_t hi = cdf[g - 1];                       // C[g-1]
+  const uint32_t lo = g >= 2 ? cdf[g - 2] : 0u;         // C[g-2]
+  g += (u >= hi) ? 1 : 0;
+  g -= (g >= 2 && u < lo) ? 1 : 0;
+  return g;
+}
+
+// VARIANT 0: rollout, loop invariants hoisted (small batches, few waves per SIMD);
+// 1: exactly one step (pbn_step; no loop, lowest VGPR count);
+// 2: rollout with invariants recomputed per step (large batches, occupancy first).
+template <int W, int B, int VARIANT>
+__global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
+  constexpr bool LEAN = VARIANT == 2;
+  constexpr int CPN = B / 4;               // selection calls per node
+  constexpr int H = (CPN + 1) / 2;         // of which the lower half computes H
+  constexpr int NLO = 1 + W * H;           // lower list: ENV, SEL(c < H)
+  constexpr int NUP = W * (CPN - H) + 1;   // upper list: SEL(c >= H), PERT call 0
+  constexpr int IT = NLO > NUP ? NLO : NUP;
+  constexpr int UPC = (CPN - H) > 0 ? (CPN - H) : 1;  // divisor guard (B = 4: no upper calls)
   extern __shared__ uint32_t smem[];
+  PBN_STAMP(0);
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int64_t g = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  if (g >= a.n_groups) return;  // whole wave; the kernel has no block barrier
   const int N = a.n_nodes;
-  const int fwords = a.n_funcs * kFuncRecWords;
-  uint32_t* funcs_l = smem + a.tab_words;
-  int32_t* nodefs_l = reinterpret_cast<int32_t*>(funcs_l + fwords);
-  uint32_t* groups_l = funcs_l + fwords + ((N + 1 + 3) & ~3);
-  for (int i = threadIdx.x; i < a.tab_words; i += 256) smem[i] = a.tab[i];
-  for (int i = threadIdx.x; i < fwords; i += 256) funcs_l[i] = reinterpret_cast<const uint32_t*>(a.funcs)[i];
-  for (int i = threadIdx.x; i <= N; i += 256) nodefs_l[i] = a.node_fs[i];
-  const int team = threadIdx.x / T, j = threadIdx.x % T;
-  uint32_t* S = groups_l + team * GSTRIDE;
-  uint32_t* R = S + GW;
-  uint32_t* WS = R + GW;
-  uint32_t* WR = WS + GW;
-  uint32_t* P = WR + GW;
-  if (j == 0) *P = 0;
-  __syncthreads();
-
-  const uint32_t* cdf = smem;
-  const float* rtab = reinterpret_cast<const float*>(smem + a.cdf_len);
-  const uint32_t* htab = smem + a.cdf_len + 4 * (N + 1);
+  // per-wave LDS: [cdf | reward | hash] image, then S planes
+  uint32_t* L = smem + (size_t)wv * a.wave_words;
+  uint32_t* S = L + a.tab_words;
+  const uint32_t* cdf = L;
+  const float* rtab = reinterpret_cast<const float*>(L + a.cdf_len);
+  const uint32_t* htab = L + a.cdf_len + 4 * (N + 1);
   const int64_t n = a.n_envs;
-  int64_t g = (int64_t)blockIdx.x * GPB + team;
-  const bool live = g < a.n_groups;
-  if (!live) g = a.n_groups - 1;  // dead teams mirror the last group, store nothing
-  const int64_t e0 = g * 32;
-  const uint64_t ge0 = a.env_offset + (uint64_t)e0;
-  const uint64_t G = ge0 >> 5;
+  const bool lo = lane < 32;
+  const int l32 = lane & 31;
+  const int64_t le = g * 32 + l32;
+  const uint64_t ge = a.env_offset + (uint64_t)le;
+  const uint64_t G = ge >> 5;
   const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
-  const uint32_t st_lo = (uint32_t)a.step;
-  const uint32_t st_hi = (uint32_t)((a.step >> 32) & 0xFFFFu) << 16;
   const bool random_actions = (a.mode & PBN_MODE_RANDOM_ACTIONS) != 0;
+  const size_t plane = (size_t)W * n;   // words per step of a [steps][W][n] output
 
-  // ---- per env: interventions, perturbation, reset word
-  uint32_t tt_[EPT], tg_[EPT], pc_[EPT], rw_[EPT];
-  bool pert_[EPT];
+  // ---- 0. issue the one-time global loads: env state, node records, tables
+  uint32_t st[W];      // current observation s of env l32 (lower lanes), carried across steps
+  uint32_t tt0 = 0, tg0 = 0;
 #pragma unroll
-  for (int k = 0; k < EPT; ++k) {
-    const int b = j + k * T;
-    const int64_t le = e0 + b;
-    const uint64_t ge = ge0 + (uint64_t)b;
-    const uint32_t ghi = (uint32_t)((ge >> 32) & 0xFFFFu) | st_hi;
-    const Word4 E = pbn::philox4x32_10((uint32_t)ge, st_lo, pbn::kStreamEnv << 28, ghi, k0, k1);
-    uint32_t s1[W], m[W], gam[W];
+  for (int w = 0; w < W; ++w) st[w] = 0;
+  if (lo) {
 #pragma unroll
-    for (int w = 0; w < W; ++w) {
-      s1[w] = a.state[(size_t)w * n + le] & valid_word_mask(N, w);
-      m[w] = 0;
-      gam[w] = 0;
+    for (int w = 0; w < W; ++w) st[w] = a.state[(size_t)w * n + le] & valid_word_mask(N, w);
+    tt0 = a.t[le];
+    tg0 = a.target[le];
+  }
+  // node l32 + 32r: its first kNodeRecs compact records {inputs, table, threshold, meta}
+  // (node-major, fixed stride: no dependent load); meta of record 0 = nf, of record 1 = f0
+  uint4 rec_[W][kNodeRecs];
+#pragma unroll
+  for (int r = 0; r < W; ++r) {
+    const int i = l32 + 32 * r;
+    const int ic = i < N ? i : 0;
+#pragma unroll
+    for (int q = 0; q < kNodeRecs; ++q) rec_[r][q] = a.nrec[(size_t)ic * kNodeRecs + q];
+  }
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(a.tab);
+    uint4* dst = reinterpret_cast<uint4*>(L);
+    for (int k = lane; k < (a.tab_words >> 2); k += 64) dst[k] = src[k];
+  }
+  __builtin_amdgcn_wave_barrier();
+
+  const int n_steps = VARIANT == 1 ? 1 : a.n_steps;
+  for (int ks = 0; ks < n_steps; ++ks) {
+  if constexpr (LEAN) {
+    // LEAN (large batches): keep loop-invariant expansions (leaf masks, threshold digits,
+    // key schedule, first-round products) inside the loop so VGPRs stay low and
+    // occupancy high; the default variant lets the compiler hoist them (small batches).
+#pragma unroll
+    for (int r = 0; r < W; ++r) {
+#pragma unroll
+      for (int q = 0; q < kNodeRecs; ++q) {
+        asm volatile("" : "+v"(rec_[r][q].x), "+v"(rec_[r][q].y), "+v"(rec_[r][q].z));
+      }
     }
-    tt_[k] = a.t[le];
-    tg_[k] = a.target[le];
+  }
+  const uint32_t kk0 = k0, kk1 = k1, ge_lo = (uint32_t)ge, G_lo = (uint32_t)G;
+  const uint64_t step = a.step + (uint64_t)ks;
+  const uint32_t st_lo = (uint32_t)step;
+  const uint32_t st_hi = (uint32_t)((step >> 32) & 0xFFFFu) << 16;
+  const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | st_hi;
+  const uint32_t G_hi = (uint32_t)((G >> 32) & 0xFFFFu) | st_hi;
+  uint32_t m[W], s1[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) { m[w] = 0; s1[w] = st[w]; }
+  if (lo && !random_actions) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) m[w] = a.flipmask[ks * plane + (size_t)w * n + le];
+  }
+  if (lo && a.obs) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) a.obs[ks * plane + (size_t)w * n + le] = st[w];
+  }
+
+  // ---- 1. all Philox calls of the group, two half-wave work lists
+  PBN_STAMP(1);
+  Word4 out[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    uint32_t lc0, lc2, lc3, uc0, uc2, uc3;
+    if (it == 0) {
+      lc0 = ge_lo; lc2 = pbn::kStreamEnv << 28; lc3 = ge_hi;
+    } else {
+      const int idx = it - 1;
+      const int r = (idx / H) < W ? idx / H : W - 1;
+      const int c = idx % H;
+      lc0 = G_lo; lc2 = (pbn::kStreamSel << 28) | (uint32_t)(4 * (l32 + 32 * r) + c); lc3 = G_hi;
+    }
+    if (it < W * (CPN - H)) {
+      const int r = it / UPC;
+      const int c = H + it % UPC;
+      uc0 = G_lo; uc2 = (pbn::kStreamSel << 28) | (uint32_t)(4 * (l32 + 32 * r) + c); uc3 = G_hi;
+    } else {
+      uc0 = ge_lo; uc2 = pbn::kStreamPert << 28; uc3 = ge_hi;
+    }
+    out[it] = pbn::philox4x32_10(lo ? lc0 : uc0, st_lo, lo ? lc2 : uc2, lo ? lc3 : uc3, kk0, kk1);
+  }
+  // digits of node l32 + 32r: calls c < H from this lane, c >= H from lane + 32
+  uint32_t dig[W][16];
+#pragma unroll
+  for (int r = 0; r < W; ++r) {
+#pragma unroll
+    for (int c = 0; c < CPN; ++c) {
+      Word4 d;
+      if (c < H) {
+        d = out[(1 + r * H + c) < IT ? (1 + r * H + c) : 0];
+      } else {
+        const Word4 src = out[r * (CPN - H) + (c - H)];
+        const auto sx = __builtin_amdgcn_permlane32_swap(src.x, src.x, false, false);
+        const auto sy = __builtin_amdgcn_permlane32_swap(src.y, src.y, false, false);
+        const auto sz = __builtin_amdgcn_permlane32_swap(src.z, src.z, false, false);
+        const auto sw = __builtin_amdgcn_permlane32_swap(src.w, src.w, false, false);
+        d.x = sx[1]; d.y = sy[1]; d.z = sz[1]; d.w = sw[1];   // lower lanes: value of lane + 32
+      }
+      dig[r][4 * c + 0] = d.x; dig[r][4 * c + 1] = d.y; dig[r][4 * c + 2] = d.z; dig[r][4 * c + 3] = d.w;
+    }
+  }
+  uint32_t P4[4];
+  {
+    const Word4 src = out[W * (CPN - H)];
+    const auto sx = __builtin_amdgcn_permlane32_swap(src.x, src.x, false, false);
+    const auto sy = __builtin_amdgcn_permlane32_swap(src.y, src.y, false, false);
+    const auto sz = __builtin_amdgcn_permlane32_swap(src.z, src.z, false, false);
+    const auto sw = __builtin_amdgcn_permlane32_swap(src.w, src.w, false, false);
+    P4[0] = sx[1]; P4[1] = sy[1]; P4[2] = sz[1]; P4[3] = sw[1];
+  }
+  const Word4 E = out[0];
+
+  // ---- 2. per env (lower lanes): interventions, perturbation, reset word
+  PBN_STAMP(2);
+  uint32_t gam[W];
+  uint32_t pc = 0;
+  bool pert = false;
+#pragma unroll
+  for (int w = 0; w < W; ++w) gam[w] = 0;
+  if (lo) {
     if (random_actions) {
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
@@ -541,23 +740,16 @@ __global__ void __launch_bounds__(256) pbn_step_team(StepArgs a) {
             if ((int)((act - 1) >> 5) == w) m[w] |= 1u << ((act - 1) & 31);
         }
       }
-      if (live) {
 #pragma unroll
-        for (int w = 0; w < W; ++w) a.flipmask[(size_t)w * n + le] = m[w];
-      }
-    } else {
-#pragma unroll
-      for (int w = 0; w < W; ++w) m[w] = a.flipmask[(size_t)w * n + le] & valid_word_mask(N, w);
+      for (int w = 0; w < W; ++w) a.flipmask[ks * plane + (size_t)w * n + le] = m[w];
     }
-    uint32_t pc = 0;
 #pragma unroll
     for (int w = 0; w < W; ++w) {
+      m[w] &= valid_word_mask(N, w);
       pc += __builtin_popcount(m[w]);
       s1[w] ^= m[w];
     }
-    // perturbation: flip positions are partial sums of geometric gaps
     int pos = -1;
-    uint32_t P4[4] = {0, 0, 0, 0};
     for (int kk = 0; pos < N - 1; ++kk) {
       uint32_t u;
       if (kk == 0) {
@@ -565,152 +757,139 @@ __global__ void __launch_bounds__(256) pbn_step_team(StepArgs a) {
       } else if (kk == 1) {
         u = E.y;
       } else {
-        if (((kk - 2) & 3) == 0) {
-          const Word4 pw = pbn::philox4x32_10((uint32_t)ge, st_lo,
-                                              (pbn::kStreamPert << 28) | (uint32_t)((kk - 2) >> 2), ghi, k0, k1);
+        if (kk >= 6 && ((kk - 2) & 3) == 0) {
+          const Word4 pw = pbn::philox4x32_10(ge_lo, st_lo,
+                                              (pbn::kStreamPert << 28) | (uint32_t)((kk - 2) >> 2), ge_hi, kk0, kk1);
           P4[0] = pw.x; P4[1] = pw.y; P4[2] = pw.z; P4[3] = pw.w;
         }
-        u = P4[(kk - 2) & 3];
+        const int j4 = (kk - 2) & 3;
+        u = j4 == 0 ? P4[0] : (j4 == 1 ? P4[1] : (j4 == 2 ? P4[2] : P4[3]));
       }
-      pos += gap_of(cdf, a.cdf_len, u);
+      pos += a.gap_exact ? gap_of(cdf, a.cdf_len, u) : gap_est(cdf, a.cdf_len, a.inv_log2q, u);
       if (pos >= N) break;
 #pragma unroll
       for (int w = 0; w < W; ++w)
         if ((pos >> 5) == w) gam[w] |= 1u << (pos & 31);
     }
-    bool pert = false;
 #pragma unroll
-    for (int w = 0; w < W; ++w) {
-      pert = pert || gam[w] != 0;
-      WS[b * W + w] = s1[w];
-      WR[b * W + w] = s1[w] ^ gam[w];
-    }
-    if (pert) atomicOr(P, 1u << b);
-    pc_[k] = pc;
-    rw_[k] = E.z;
-    pert_[k] = pert;
+    for (int w = 0; w < W; ++w) pert = pert || gam[w] != 0;
   }
-  __syncthreads();
+  const uint32_t pmask = (uint32_t)__ballot(pert);
 
-  // ---- bit-slice the group: plane p = bit p of every env word
-  for (int p = j; p < GW; p += T) {
-    const int w = p >> 5, c = p & 31;
-    uint32_t sa = 0, ra = 0;
+  // ---- 3. bit-slice: lane p <- plane p of s1 (to LDS) and of s1 ^ gamma (register)
+  PBN_STAMP(3);
+  uint32_t R[W];
 #pragma unroll
-    for (int e = 0; e < 32; ++e) {
-      sa |= ((WS[e * W + w] >> c) & 1u) << e;
-      ra |= ((WR[e * W + w] >> c) & 1u) << e;
-    }
-    S[p] = sa;
-    R[p] = ra;
+  for (int w = 0; w < W; ++w) {
+    const uint32_t sp = lane_transpose32(s1[w], lane);
+    R[w] = lane_transpose32(s1[w] ^ gam[w], lane);
+    if (lo) S[32 * w + l32] = sp;
   }
-  __syncthreads();
+  __builtin_amdgcn_wave_barrier();
 
-  // ---- node loop: lane j owns nodes j, j+T, ...
-  const uint32_t pmask = *P;
-  for (int i = j; i < N; i += T) {
-    const int f0 = nodefs_l[i];
-    const int nf = nodefs_l[i + 1] - f0;
-    uint32_t dig[16];
-    if (nf > 1) {
+  // ---- 4. node l32 + 32r on lane l32
+  PBN_STAMP(4);
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        if (4 * c >= a.prob_bits) break;
-        const Word4 d = pbn::philox4x32_10((uint32_t)G, st_lo, (pbn::kStreamSel << 28) | (uint32_t)(4 * i + c),
-                                           (uint32_t)((G >> 32) & 0xFFFFu) | st_hi, k0, k1);
-        dig[4 * c + 0] = d.x;
-        dig[4 * c + 1] = d.y;
-        dig[4 * c + 2] = d.z;
-        dig[4 * c + 3] = d.w;
+  for (int r = 0; r < W; ++r) {
+    const int i = l32 + 32 * r;
+    const int nf = (lo && i < N) ? (int)rec_[r][0].w : 0;
+    if (nf > 0) {
+      const int f0 = (int)rec_[r][1].w;
+      // selection chain from the last function down: x = F_{nf-1}; x = lt_j ? F_j : x
+      uint32_t x = 0;
+      for (int j = nf - 1; j >= kNodeRecs; --j) {   // nodes with more than kNodeRecs functions (slow path)
+        const uint4 rc = a.fcompact[f0 + j];
+        const uint32_t fj = eval_compact(rc.x, rc.y, S);
+        x = (j == nf - 1) ? fj : bfi(less_than(dig[r], rc.z, B), fj, x);
       }
+#pragma unroll
+      for (int q = kNodeRecs - 1; q >= 0; --q) {
+        if (q < nf) {
+          const uint4 rc = rec_[r][q];
+          const uint32_t fj = eval_compact(rc.x, rc.y, S);
+          x = (q == nf - 1) ? fj : bfi(less_than(dig[r], rc.z, B), fj, x);
+        }
+      }
+      R[r] = bfi(pmask, R[r], x);
     }
-    const uint32_t* fr = funcs_l + (size_t)(f0 + nf - 1) * kFuncRecWords;
-    uint32_t x = eval_func_lds(fr, S);
-    for (int jj = nf - 2; jj >= 0; --jj) {
-      fr = funcs_l + (size_t)(f0 + jj) * kFuncRecWords;
-      const uint32_t fj = eval_func_lds(fr, S);
-      x = bfi(less_than(dig, fr[20], a.prob_bits), fj, x);
-    }
-    R[i] = bfi(pmask, R[i], x);
   }
-  __syncthreads();
 
-  // ---- per env: back to words, reward, termination, autoreset, stores
+  // ---- 5. back to per-env words, reward, termination, autoreset, stores
+  PBN_STAMP(5);
+  uint32_t sp[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) sp[w] = lane_transpose32(R[w], lane);
+  PBN_STAMP(6);
+  if (lo) {
+  if (a.final_state) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) a.final_state[ks * plane + (size_t)w * n + le] = sp[w];
+  }
   const int hmask = (1 << a.hash_bits) - 1;
   const uint32_t* hid = htab + (size_t)W * (hmask + 1);
+  int att = -1;
+  if (a.hash_bits > 0) {
+    uint32_t h = 0;
 #pragma unroll
-  for (int k = 0; k < EPT; ++k) {
-    const int b = j + k * T;
-    const int64_t le = e0 + b;
-    const uint64_t ge = ge0 + (uint64_t)b;
-    uint32_t sp[W];
+    for (int w = 0; w < W; ++w) h += sp[w] * a.hash_mult[w];
+    h >>= (32 - a.hash_bits);
+    for (int pr = 0; pr < a.hash_probes; ++pr) {
+      const uint32_t slot = (h + pr) & hmask;
+      bool eq = true;
 #pragma unroll
-    for (int w = 0; w < W; ++w) {
-      uint32_t acc = 0;
-#pragma unroll
-      for (int c = 0; c < 32; ++c) acc |= ((R[32 * w + c] >> b) & 1u) << c;
-      sp[w] = acc;
+      for (int w = 0; w < W; ++w) eq = eq && (htab[(size_t)w * (hmask + 1) + slot] == sp[w]);
+      const uint32_t id = hid[slot];
+      if (eq && id != 0xFFFFFFFFu) att = (int)id;
     }
-    if (!live) continue;
-    if (a.final_state) {
+  }
+  const bool in_attr = att >= 0;
+  const bool term = in_attr && (uint32_t)att == tg0;
+  const bool wrong = in_attr && !term;
+  int tt = (int)tt0 + 1;
+  tt = tt > 255 ? 255 : tt;
+  const bool trunc = a.horizon > 0 && tt >= a.horizon;
+  a.reward[ks * n + le] = rtab[(2 * (int)term + (int)wrong) * (N + 1) + (int)pc];
+  uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) | ((uint32_t)pert << 3);
+  if ((a.mode & PBN_MODE_AUTORESET) && (term || trunc)) {
+    const uint32_t Rw = E.z;
+    uint32_t nt;
+    if (a.n_attr >= 1) {
+      const uint32_t A = (uint32_t)a.n_attr;
+      const uint32_t as = ((Rw & 1023u) * A) >> 10;
+      const int st0 = a.att_start[as];
+      const uint32_t size = (uint32_t)(a.att_start[as + 1] - st0);
+      const uint32_t idx = (((Rw >> 20) & 4095u) * size) >> 12;
 #pragma unroll
-      for (int w = 0; w < W; ++w) a.final_state[(size_t)w * n + le] = sp[w];
-    }
-    int att = -1;
-    if (a.hash_bits > 0) {
-      uint32_t h = 0;
-#pragma unroll
-      for (int w = 0; w < W; ++w) h += sp[w] * a.hash_mult[w];
-      h >>= (32 - a.hash_bits);
-      for (int pr = 0; pr < a.hash_probes; ++pr) {
-        const uint32_t slot = (h + pr) & hmask;
-        bool eq = true;
-#pragma unroll
-        for (int w = 0; w < W; ++w) eq = eq && (htab[(size_t)w * (hmask + 1) + slot] == sp[w]);
-        const uint32_t id = hid[slot];
-        if (eq && id != 0xFFFFFFFFu) att = (int)id;
+      for (int w = 0; w < W; ++w) sp[w] = a.att_states[(size_t)(st0 + idx) * W + w];
+      nt = as;
+      if (A >= 2) {
+        nt = (((Rw >> 10) & 1023u) * (A - 1)) >> 10;
+        nt += (nt >= as) ? 1u : 0u;
       }
+    } else {
+      const Word4 rr = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamReset << 28) | 1u, ge_hi, kk0, kk1);
+      const uint32_t rw4[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+      for (int w = 0; w < W; ++w) sp[w] = rw4[w] & valid_word_mask(N, w);
+      nt = PBN_NO_TARGET;
     }
-    const bool in_attr = att >= 0;
-    const bool term = in_attr && (uint32_t)att == tg_[k];
-    const bool wrong = in_attr && !term;
-    int tt = (int)tt_[k] + 1;
-    tt = tt > 255 ? 255 : tt;
-    const bool trunc = a.horizon > 0 && tt >= a.horizon;
-    a.reward[le] = rtab[(2 * (int)term + (int)wrong) * (N + 1) + (int)pc_[k]];
-    uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) | ((uint32_t)pert_[k] << 3);
-    if ((a.mode & PBN_MODE_AUTORESET) && (term || trunc)) {
-      const uint32_t Rw = rw_[k];
-      uint32_t nt;
-      if (a.n_attr >= 1) {
-        const uint32_t A = (uint32_t)a.n_attr;
-        const uint32_t as = ((Rw & 1023u) * A) >> 10;
-        const int st0 = a.att_start[as];
-        const uint32_t size = (uint32_t)(a.att_start[as + 1] - st0);
-        const uint32_t idx = (((Rw >> 20) & 4095u) * size) >> 12;
+    tg0 = nt;
+    tt = 0;
+    fl |= PBN_FLAG_RESET;
+  }
+  a.flags[ks * n + le] = (uint8_t)fl;
+  tt0 = (uint32_t)tt;
 #pragma unroll
-        for (int w = 0; w < W; ++w) sp[w] = a.att_states[(size_t)(st0 + idx) * W + w];
-        nt = as;
-        if (A >= 2) {
-          nt = (((Rw >> 10) & 1023u) * (A - 1)) >> 10;
-          nt += (nt >= as) ? 1u : 0u;
-        }
-      } else {
-        const Word4 rr = pbn::philox4x32_10((uint32_t)ge, st_lo, (pbn::kStreamReset << 28) | 1u,
-                                            (uint32_t)((ge >> 32) & 0xFFFFu) | st_hi, k0, k1);
-        const uint32_t rw4[4] = {rr.x, rr.y, rr.z, rr.w};
+  for (int w = 0; w < W; ++w) st[w] = sp[w];
+  }  // lo
+  PBN_STAMP(7);
+  }  // steps
+
+  if (lo) {
 #pragma unroll
-        for (int w = 0; w < W; ++w) sp[w] = rw4[w] & valid_word_mask(N, w);
-        nt = PBN_NO_TARGET;
-      }
-      a.target[le] = (uint8_t)nt;
-      tt = 0;
-      fl |= PBN_FLAG_RESET;
-    }
-#pragma unroll
-    for (int w = 0; w < W; ++w) a.state_out[(size_t)w * n + le] = sp[w];
-    a.t[le] = (uint8_t)tt;
-    a.flags[le] = (uint8_t)fl;
+    for (int w = 0; w < W; ++w) a.state_out[(size_t)w * n + le] = st[w];
+    a.t[le] = (uint8_t)tt0;
+    a.target[le] = (uint8_t)tg0;
   }
 }
 
@@ -769,7 +948,6 @@ int fail(int code, const std::string& msg) {
 
 using StepFn = void (*)(StepArgs);
 
-constexpr int kTeamSizes[5] = {2, 4, 8, 16, 32};
 
 StepFn pick_lane(int W) {
   switch (W) {
@@ -781,24 +959,24 @@ StepFn pick_lane(int W) {
   return nullptr;
 }
 
-template <int W>
-StepFn pick_team_w(int T) {
-  switch (T) {
-    case 2: return pbn_step_team<W, 2>;
-    case 4: return pbn_step_team<W, 4>;
-    case 8: return pbn_step_team<W, 8>;
-    case 16: return pbn_step_team<W, 16>;
-    case 32: return pbn_step_team<W, 32>;
+template <int W, int V>
+StepFn pick_wave_w(int B) {
+  switch (B) {
+    case 4: return pbn_step_wave<W, 4, V>;
+    case 8: return pbn_step_wave<W, 8, V>;
+    case 12: return pbn_step_wave<W, 12, V>;
+    case 16: return pbn_step_wave<W, 16, V>;
   }
   return nullptr;
 }
 
-StepFn pick_team(int W, int T) {
+template <int V>
+StepFn pick_wave(int W, int B) {
   switch (W) {
-    case 1: return pick_team_w<1>(T);
-    case 2: return pick_team_w<2>(T);
-    case 3: return pick_team_w<3>(T);
-    case 4: return pick_team_w<4>(T);
+    case 1: return pick_wave_w<1, V>(B);
+    case 2: return pick_wave_w<2, V>(B);
+    case 3: return pick_wave_w<3, V>(B);
+    case 4: return pick_wave_w<4, V>(B);
   }
   return nullptr;
 }
@@ -822,13 +1000,22 @@ struct pbn_net {
   int n_nodes = 0, W = 0, B = 0, horizon = 0, n_attr = 0, n_states = 0;
   int cdf_len = 0, hash_bits = 0, hash_probes = 0, tab_words = 0;
   uint32_t hash_mult[4] = {0, 0, 0, 0};
+  int wave_words = 0;
+  int gap_exact = 1;
+  float inv_log2q = 0.f;
+  uint4* d_fcompact = nullptr;
+  uint4* d_nrec = nullptr;
   int n_funcs = 0;
   int waves_per_block = 1;   // lane kernel
   size_t lds_lane = 0;
-  size_t lds_team[5] = {0, 0, 0, 0, 0};
+  size_t lds_wave = 0;
   StepFn lane = nullptr;
-  StepFn team[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
-  int force_team = -1;       // PBN_TEAM env override (1 = lane kernel)
+  StepFn wave = nullptr;        // rollout, loop invariants hoisted (small batches)
+  StepFn wave1 = nullptr;       // single step (pbn_step)
+  StepFn wave_lean = nullptr;   // rollout with low VGPR count (large batches)
+  int force = 0;             // PBN_KERNEL env override: 1 = lane, 2 = wave
+  int force_roll = 0;        // PBN_ROLL env override: 1 = hoist, 2 = lean
+  int64_t roll_lean_groups = 1 << 16;  // rollouts above this many 32-env groups use the lean variant
   ResetFn reset = nullptr;
   FuncRec* d_funcs = nullptr;
   int32_t* d_node_fs = nullptr;
@@ -843,6 +1030,8 @@ void free_net(pbn_net* net) {
   if (!net) return;
   (void)hipFree(net->d_funcs);
   (void)hipFree(net->d_node_fs);
+  (void)hipFree(net->d_fcompact);
+  (void)hipFree(net->d_nrec);
   (void)hipFree(net->d_tab);
   (void)hipFree(net->d_att_start);
   (void)hipFree(net->d_att_states);
@@ -1024,18 +1213,47 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   while (tab.size() & 3) tab.push_back(0u);  // keep the FuncRec image 16-byte aligned in LDS
   net->tab_words = (int)tab.size();
   net->n_funcs = d->n_funcs;
+  net->wave_words = net->tab_words + ((32 * W + 3) & ~3);
+  {
+    const double p = (double)d->perturb_cdf[0] / 4294967296.0;
+    net->gap_exact = (p < 1e-6 || p > 0.5) ? 1 : 0;
+    net->inv_log2q = net->gap_exact ? 0.f : (float)(1.0 / log2(1.0 - p));
+  }
   net->waves_per_block = (W == 1) ? 2 : 1;
   net->lds_lane = (size_t)net->tab_words * 4 + (size_t)net->waves_per_block * 2 * 32 * W * 64 * 4;
-  const size_t team_fixed =
-      ((size_t)net->tab_words + (size_t)d->n_funcs * kFuncRecWords + (size_t)((N + 1 + 3) & ~3)) * 4;
-  for (int ti = 0; ti < 5; ++ti) {
-    const int T = kTeamSizes[ti];
-    net->lds_team[ti] = team_fixed + (size_t)(256 / T) * (4 * 32 * W + 4) * 4;
-    net->team[ti] = pick_team(W, T);
+  net->lds_wave = (size_t)net->wave_words * 4;
+  // compact records for the wave kernel: {inputs as bytes, 4-input truth table, threshold, 0}
+  std::vector<uint4> fcomp(d->n_funcs);
+  for (int f = 0; f < d->n_funcs; ++f) {
+    const FuncRec& r = recs[f];
+    uint32_t T4 = 0;
+    for (int mm = 0; mm < 8; ++mm) {
+      const uint32_t b0 = r.leaf[8 + mm] & 1u;               // value at x0 = 0
+      const uint32_t b1 = (r.leaf[8 + mm] ^ r.leaf[mm]) & 1u; // value at x0 = 1
+      T4 |= (b0 << (2 * mm)) | (b1 << (2 * mm + 1));
+    }
+    fcomp[f] = make_uint4(r.in[0] | (r.in[1] << 8) | (r.in[2] << 16) | (r.in[3] << 24), T4, r.thr, 0u);
   }
+  std::vector<uint4> nrec((size_t)N * kNodeRecs, make_uint4(0, 0, 0, 0));
+  for (int i = 0; i < N; ++i) {
+    const int f0 = d->node_func_start[i], nf = d->node_func_start[i + 1] - f0;
+    for (int q = 0; q < kNodeRecs && q < nf; ++q) nrec[(size_t)i * kNodeRecs + q] = fcomp[f0 + q];
+    nrec[(size_t)i * kNodeRecs + 0].w = (uint32_t)nf;
+    nrec[(size_t)i * kNodeRecs + 1].w = (uint32_t)f0;
+  }
+  net->wave = pick_wave<0>(W, d->prob_bits);
+  net->wave1 = pick_wave<1>(W, d->prob_bits);
+  net->wave_lean = pick_wave<2>(W, d->prob_bits);
   net->lane = pick_lane(W);
   net->reset = pick_reset(W);
-  if (const char* env = getenv("PBN_TEAM")) net->force_team = atoi(env);
+  if (const char* env = getenv("PBN_ROLL")) {
+    if (!strcmp(env, "hoist")) net->force_roll = 1;
+    if (!strcmp(env, "lean")) net->force_roll = 2;
+  }
+  if (const char* env = getenv("PBN_KERNEL")) {
+    if (!strcmp(env, "lane")) net->force = 1;
+    if (!strcmp(env, "wave")) net->force = 2;
+  }
   int rc;
   if (hipGetDevice(&net->device) != hipSuccess) {
     free_net(net);
@@ -1043,15 +1261,17 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   }
   if ((rc = upload(&net->d_funcs, recs.data(), recs.size())) ||
       (rc = upload(&net->d_node_fs, d->node_func_start, (size_t)N + 1)) ||
+      (rc = upload(&net->d_fcompact, fcomp.data(), fcomp.size())) ||
+      (rc = upload(&net->d_nrec, nrec.data(), nrec.size())) ||
       (rc = upload(&net->d_tab, tab.data(), tab.size())) ||
       (rc = upload(&net->d_att_start, A ? d->attractor_start : nullptr, (size_t)A + 1)) ||
       (rc = upload(&net->d_att_states, S ? d->attractor_states : nullptr, (size_t)S * W))) {
     free_net(net);
     return rc;
   }
-  for (int ti = -1; ti < 5; ++ti) {
-    const StepFn fn = ti < 0 ? net->lane : net->team[ti];
-    const size_t bytes = ti < 0 ? net->lds_lane : net->lds_team[ti];
+  for (int ti = 0; ti < 4; ++ti) {
+    const StepFn fn = ti == 0 ? net->lane : (ti == 1 ? net->wave : (ti == 2 ? net->wave_lean : net->wave1));
+    const size_t bytes = ti == 0 ? net->lds_lane : net->lds_wave;
     if (bytes > 160 * 1024) continue;  // variant unusable for this net; never picked
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)bytes) != hipSuccess) {
@@ -1059,13 +1279,21 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
       return fail(PBN_EDEVICE, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
     }
   }
-  if (net->lds_lane > 160 * 1024 && net->lds_team[4] > 160 * 1024) {
+  if (net->lds_lane > 160 * 1024 && net->lds_wave > 160 * 1024) {
     free_net(net);
     return fail(PBN_EINVAL, "LDS budget exceeded");
   }
   *out = net;
   return PBN_OK;
 }
+
+#ifdef PBN_STAMPS
+static unsigned long long* g_stamps = nullptr;
+int pbn_debug_set_stamps(unsigned long long* d_buf) {
+  g_stamps = d_buf;
+  return 0;
+}
+#endif
 
 int pbn_net_destroy(pbn_net* net) {
   if (!net) return PBN_OK;
@@ -1145,28 +1373,96 @@ int pbn_step(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, in
   a.hash_probes = net->hash_probes;
   a.tab_words = net->tab_words;
   memcpy(a.hash_mult, net->hash_mult, sizeof a.hash_mult);
+#ifdef PBN_STAMPS
+  a.stamps = g_stamps;
+#endif
   a.prob_bits = net->B;
   a.n_funcs = net->n_funcs;
-  // launch shape: one thread per 32-env group when that fills the chip, else a
-  // team of T lanes per group (smallest T reaching ~4 waves per SIMD, max 32)
-  int T = 1;
-  const int64_t target_threads = 256 * 4 * 4 * 64;
-  while (T < 32 && a.n_groups * T < target_threads) T <<= 1;
-  if (net->force_team > 0) T = net->force_team;
-  int ti = -1;
-  for (int k = 0; k < 5; ++k)
-    if (kTeamSizes[k] == T) ti = k;
-  if (T != 1 && (ti < 0 || net->lds_team[ti] > 160 * 1024)) T = 1, ti = -1;
-  if (T == 1 && net->lds_lane > 160 * 1024) ti = 4;
-  if (ti < 0) {
+  a.wave_words = net->wave_words;
+  a.gap_exact = net->gap_exact;
+  a.inv_log2q = net->inv_log2q;
+  a.fcompact = net->d_fcompact;
+  a.nrec = net->d_nrec;
+  // launch shape: one thread per 32-env group once that fills the chip
+  // (>= 4 waves per SIMD), else one wave per group (node loop across lanes)
+  a.n_steps = 1;
+  a.obs = nullptr;
+  bool use_lane = false;   // the wave kernel is faster at every measured size (profiles/)
+  if (net->force == 1) use_lane = true;
+  if (net->force == 2) use_lane = false;
+  if (use_lane && net->lds_lane > 160 * 1024) use_lane = false;
+  if (!use_lane && net->lds_wave > 160 * 1024) use_lane = true;
+  if (use_lane) {
     const int threads = 64 * net->waves_per_block;
     const unsigned blocks = (unsigned)((a.n_groups + threads - 1) / threads);
     hipLaunchKernelGGL(net->lane, dim3(blocks), dim3(threads), net->lds_lane, (hipStream_t)stream, a);
   } else {
-    const int gpb = 256 / kTeamSizes[ti];
-    const unsigned blocks = (unsigned)((a.n_groups + gpb - 1) / gpb);
-    hipLaunchKernelGGL(net->team[ti], dim3(blocks), dim3(256), net->lds_team[ti], (hipStream_t)stream, a);
+    const unsigned blocks = (unsigned)a.n_groups;  // one 64-lane wave per block and group
+    hipLaunchKernelGGL(net->wave1, dim3(blocks), dim3(64), net->lds_wave, (hipStream_t)stream, a);
   }
+  HIP_OK(hipGetLastError());
+  return PBN_OK;
+}
+
+int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs,
+                int32_t n_steps, uint32_t mode, uint32_t* d_state, uint32_t* d_flipmask, uint8_t* d_target,
+                uint8_t* d_t, uint32_t* d_obs, uint32_t* d_final_state, float* d_reward, uint8_t* d_flags,
+                void* stream) {
+  int rc = check_common(net, env_offset, n_envs);
+  if (rc) return rc;
+  if (n_steps < 0) return fail(PBN_EINVAL, "n_steps < 0");
+  if (n_envs == 0 || n_steps == 0) return PBN_OK;
+  if (mode & ~(PBN_MODE_AUTORESET | PBN_MODE_RANDOM_ACTIONS)) return fail(PBN_EINVAL, "unknown mode bits");
+  if (!d_state || !d_flipmask || !d_target || !d_t || !d_reward || !d_flags) return fail(PBN_EINVAL, "null buffer");
+  if (net->lds_wave > 160 * 1024) return fail(PBN_EINVAL, "network too large for the rollout kernel's LDS");
+  StepArgs a;
+  memset(&a, 0, sizeof a);
+  a.funcs = net->d_funcs;
+  a.node_fs = net->d_node_fs;
+  a.tab = net->d_tab;
+  a.att_start = net->d_att_start;
+  a.att_states = net->d_att_states;
+  a.state = d_state;
+  a.state_out = d_state;   // in place: every env is read and written by one lane only
+  a.flipmask = d_flipmask;
+  a.target = d_target;
+  a.t = d_t;
+  a.final_state = d_final_state;
+  a.obs = d_obs;
+  a.reward = d_reward;
+  a.flags = d_flags;
+  a.seed = seed;
+  a.step = step;
+  a.env_offset = env_offset;
+  a.n_envs = n_envs;
+  a.n_groups = n_envs / 32;
+  a.n_steps = n_steps;
+  a.n_nodes = net->n_nodes;
+  a.n_attr = net->n_attr;
+  a.horizon = net->horizon;
+  a.mode = (int)mode;
+  a.cdf_len = net->cdf_len;
+  a.hash_bits = net->n_attr ? net->hash_bits : 0;
+  a.hash_probes = net->hash_probes;
+  a.tab_words = net->tab_words;
+  memcpy(a.hash_mult, net->hash_mult, sizeof a.hash_mult);
+  a.prob_bits = net->B;
+  a.n_funcs = net->n_funcs;
+  a.wave_words = net->wave_words;
+  a.gap_exact = net->gap_exact;
+  a.inv_log2q = net->inv_log2q;
+  a.fcompact = net->d_fcompact;
+  a.nrec = net->d_nrec;
+#ifdef PBN_STAMPS
+  a.stamps = g_stamps;
+#endif
+  // few waves per SIMD: hoisting loop invariants shortens each step's critical path;
+  // many waves: occupancy wins (measured crossover in profiles/)
+  bool lean = a.n_groups > (int64_t)net->roll_lean_groups;
+  if (net->force_roll == 1) lean = false;
+  if (net->force_roll == 2) lean = true;
+  hipLaunchKernelGGL(lean ? net->wave_lean : net->wave, dim3((unsigned)a.n_groups), dim3(64), net->lds_wave,
+                     (hipStream_t)stream, a);
   HIP_OK(hipGetLastError());
   return PBN_OK;
 }

@@ -142,6 +142,42 @@ class VectorPBNEnv:
         k = self.num_envs
         return self.state[:, :k], self.reward[:k], self.flags[:k]
 
+    def rollout(self, n_steps: int, flipmasks: Optional[torch.Tensor] = None, random_actions: bool = True,
+                keep_obs: bool = False, keep_final: bool = True, out: Optional[dict] = None) -> dict:
+        """``n_steps`` transitions in one ``pbn_rollout`` launch (state kept on chip).
+
+        flipmasks: optional (n_steps, W, num_envs) interventions (else in-kernel random
+        actions when ``random_actions``, else none).  Returns views of
+        ``flipmask`` / ``reward`` / ``flags`` (+ ``obs`` / ``final_state``) shaped
+        (n_steps, ...); pass ``out`` (a previous result) to reuse its buffers."""
+        L = _lib.load()
+        W, n, k = self.words, self.n_alloc, self.num_envs
+        dev = self.device
+        if out is None or out["_n_steps"] != n_steps:
+            out = {"_n_steps": n_steps,
+                   "flipmask": torch.zeros(n_steps, W, n, dtype=torch.int32, device=dev),
+                   "reward": torch.zeros(n_steps, n, dtype=torch.float32, device=dev),
+                   "flags": torch.zeros(n_steps, n, dtype=torch.uint8, device=dev),
+                   "obs": torch.zeros(n_steps, W, n, dtype=torch.int32, device=dev) if keep_obs else None,
+                   "final_state": torch.zeros(n_steps, W, n, dtype=torch.int32, device=dev) if keep_final else None}
+        mode = _lib.MODE_AUTORESET if self.autoreset else 0
+        if flipmasks is not None:
+            out["flipmask"][:, :, :k].copy_(flipmasks)
+            out["flipmask"][:, :, k:].zero_()
+        elif random_actions:
+            mode |= _lib.MODE_RANDOM_ACTIONS
+        else:
+            out["flipmask"].zero_()
+        ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+        with torch.cuda.device(dev):
+            _lib.check(L.pbn_rollout(self.net.handle, self.seed, self.step_index, self.env_offset, n, n_steps, mode,
+                                     self.state.data_ptr(), out["flipmask"].data_ptr(), self.target.data_ptr(),
+                                     self.t.data_ptr(), ptr(out["obs"]), ptr(out["final_state"]),
+                                     out["reward"].data_ptr(), out["flags"].data_ptr(), self._stream()),
+                       "pbn_rollout")
+        self.step_index += n_steps
+        return out
+
     def step(self, actions: Optional[torch.Tensor] = None):
         """gymnasium-vector style: actions (n, k) in [0, N] (or None = no intervention).
         Returns (state_words, reward, terminated, truncated, info)."""

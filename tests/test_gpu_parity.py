@@ -81,15 +81,20 @@ def test_step_matches_oracle(name, mode):
     run_pair(spec, 2048, 12, mode=mode, env_offset=0 if mode < 2 else 4096)
 
 
+@pytest.mark.parametrize("kernel", ["lane", "wave"])
 @pytest.mark.parametrize("name", ["pbn28", "pbn70"])
-def test_high_perturbation_multi_flip_path(name):
+def test_high_perturbation_multi_flip_path(name, kernel, monkeypatch):
+    monkeypatch.setenv("PBN_KERNEL", kernel)
     ref = run_pair(make_spec(name, perturbation=0.3), 1024, 6, mode=3)
     assert (ref["flags"] & _lib.FLAG_PERTURBED).mean() > 0.9
 
 
+@pytest.mark.parametrize("kernel", ["lane", "wave"])
 @pytest.mark.parametrize("bits", [4, 8, 12, 16])
-def test_prob_bits(bits):
+def test_prob_bits(bits, kernel, monkeypatch):
+    monkeypatch.setenv("PBN_KERNEL", kernel)
     run_pair(make_spec("pbn28", prob_bits=bits, perturbation=0.0), 1024, 6, mode=1, start_random=True)
+    run_pair(make_spec("pbn70", prob_bits=bits, perturbation=0.02), 1024, 3, mode=3)
 
 
 @pytest.mark.parametrize("name", NETS)
@@ -144,11 +149,58 @@ def test_abi_rejects_bad_arguments():
     assert rc == -22
 
 
-@pytest.mark.parametrize("team", [1, 2, 4, 8, 16, 32])
-@pytest.mark.parametrize("name", ["pbn7", "pbn28", "pbn70"])
-def test_every_launch_shape(name, team, monkeypatch):
-    """Each kernel variant (one thread per group, or a team of T lanes per group)
-    gives the oracle's results; PBN_TEAM forces the variant at pbn_net_create."""
-    monkeypatch.setenv("PBN_TEAM", str(team))
+@pytest.mark.parametrize("kernel", ["lane", "wave"])
+@pytest.mark.parametrize("name", ["pbn7", "pbn10", "pbn28", "pbn70"])
+def test_every_kernel_variant(name, kernel, monkeypatch):
+    """Both kernel variants (one thread per 32-env group / one wave per group) give
+    the oracle's results; PBN_KERNEL forces the variant at pbn_net_create."""
+    monkeypatch.setenv("PBN_KERNEL", kernel)
     run_pair(make_spec(name, perturbation=0.05), 4096, 6, mode=3, env_offset=1024)
     run_pair(make_spec(name, perturbation=0.05), 2048, 4, mode=0)
+
+
+@pytest.mark.parametrize("variant", ["hoist", "lean"])
+@pytest.mark.parametrize("name", ["pbn7", "pbn28", "pbn70"])
+@pytest.mark.parametrize("mode", [1, 3])
+def test_rollout_matches_oracle(name, mode, variant, monkeypatch):
+    """pbn_rollout (R steps in one launch, state on chip) == R oracle steps."""
+    monkeypatch.setenv("PBN_ROLL", variant)
+    spec = make_spec(name, perturbation=0.05, horizon=7)
+    n, R, seed = 4096, 9, 4242
+    env = VectorPBNEnv(spec, n, seed=seed, env_offset=2048)
+    env.reset()
+    st, tg, t = oracle.reset(spec, seed, 0, 2048, n)
+    W = spec.words
+    rng = np.random.default_rng(3)
+    if mode & 2:
+        flips = None
+        fm = None
+    else:
+        flips = rng.integers(0, 2 ** 32, size=(R, W, n), dtype=np.uint64).astype(np.uint32) & np.uint32(0x04010020)
+        fm = torch.from_numpy(flips.view(np.int32)).to(env.device)
+    out = env.rollout(R, flipmasks=fm, random_actions=bool(mode & 2), keep_obs=True)
+    for k in range(R):
+        flip = np.zeros((W, n), np.uint32) if flips is None else flips[k]
+        ref = oracle.step(spec, seed, 1 + k, 2048, st, flip, tg, t, mode)
+        assert np.array_equal(u32(out["obs"][k]), st), k
+        assert np.array_equal(u32(out["final_state"][k]), ref["final_state"]), k
+        assert np.array_equal(out["flags"][k].cpu().numpy(), ref["flags"]), k
+        assert np.array_equal(out["reward"][k].cpu().numpy().view(np.uint32), ref["reward"].view(np.uint32)), k
+        assert np.array_equal(u32(out["flipmask"][k]), ref["flipmask"]), k
+        st, tg, t = ref["state_out"], ref["target"], ref["t"]
+    assert np.array_equal(u32(env.state), st)
+    assert np.array_equal(env.target.cpu().numpy(), tg)
+    assert np.array_equal(env.t.cpu().numpy(), t)
+
+
+def test_rollout_equals_steps_baseline_size():
+    spec = make_spec("pbn28")
+    a = VectorPBNEnv(spec, 65536, seed=9)
+    b = VectorPBNEnv(spec, 65536, seed=9)
+    a.reset(); b.reset()
+    out = a.rollout(20)
+    for k in range(20):
+        state, reward, flags = b.step_flipmask(random_actions=True)
+        assert torch.equal(out["flags"][k], flags) and torch.equal(out["reward"][k], reward)
+        assert torch.equal(out["final_state"][k], b.final_state)
+    assert torch.equal(a.state, b.state) and torch.equal(a.t, b.t) and torch.equal(a.target, b.target)

@@ -1,0 +1,70 @@
+"""In-kernel phase clocks of the wave kernel (diagnostic build, never the product).
+
+  python tools/stamps.py --build            # here: builds pbn_rl_amd/libpbn_env_stamps.so
+  python tools/stamps.py [--envs 65536]     # on the GPU box
+
+Per wave, lane 0 stamps s_memtime at the phase boundaries of pbn_step_wave; we
+report the median / p90 over waves of each phase's cycles and the spread of
+wave start times.  Read the shares, not the absolute length (stamps cost ~40
+cycles each and fence the schedule).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, ROOT)
+STAMP_LIB = os.path.join(ROOT, "pbn_rl_amd", "libpbn_env_stamps.so")
+PHASES = ["tables+barrier", "philox", "per-env", "transpose+S", "node eval", "back-transpose", "epilogue"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--envs", type=int, default=65536)
+    ap.add_argument("--network", default="pbn28")
+    args = ap.parse_args()
+    if args.build:
+        from pbn_rl_amd import _lib
+        _lib.build(out=STAMP_LIB, defines=["PBN_STAMPS"], verbose=True)
+        return
+    os.environ["PBN_LIB"] = STAMP_LIB
+    os.environ["PBN_KERNEL"] = "wave"
+    import numpy as np
+    import torch
+
+    from pbn_rl_amd import _lib
+    from pbn_rl_amd.attractors import load_attractors
+    from pbn_rl_amd.network import load_network
+    from pbn_rl_amd.spec import EnvSpec
+    from pbn_rl_amd.vector_env import VectorPBNEnv
+
+    L = _lib.load()
+    L.pbn_debug_set_stamps.argtypes = [ctypes.c_void_p]
+    spec = EnvSpec(load_network(args.network), load_attractors(args.network))
+    env = VectorPBNEnv(spec, args.envs, seed=1, keep_final_state=False)
+    env.reset()
+    waves = env.n_alloc // 32
+    buf = torch.zeros(waves * 16, dtype=torch.int64, device="cuda")
+    for _ in range(10):
+        env.step_flipmask(random_actions=True)
+    torch.cuda.synchronize()
+    L.pbn_debug_set_stamps(buf.data_ptr())
+    env.step_flipmask(random_actions=True)
+    torch.cuda.synchronize()
+    L.pbn_debug_set_stamps(None)
+    t = buf.view(waves, 16)[:, :8].cpu().numpy().astype(np.int64)
+    d = np.diff(t, axis=1)
+    rep = {"envs": args.envs, "waves": waves,
+           "start_spread_cycles": int(t[:, 0].max() - t[:, 0].min()),
+           "kernel_span_cycles": int(t[:, 7].max() - t[:, 0].min()),
+           "wave_total_median": int(np.median(t[:, 7] - t[:, 0])),
+           "phases": {PHASES[k]: {"median": int(np.median(d[:, k])), "p90": int(np.percentile(d[:, k], 90))}
+                      for k in range(7)}}
+    print(json.dumps(rep, indent=1))
+
+
+if __name__ == "__main__":
+    main()

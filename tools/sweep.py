@@ -25,7 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--network", default="pbn28")
     ap.add_argument("--envs", default="65536,1048576")
-    ap.add_argument("--teams", default="1,2,4,8,16,32")
+    ap.add_argument("--kernels", default="lane,wave,roll")
     ap.add_argument("--chunk", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--prob-bits", type=int, default=16)
@@ -36,11 +36,20 @@ def main():
     for n in [int(x) for x in args.envs.split(",")]:
         envs = {}
         graphs = {}
-        for T in [int(x) for x in args.teams.split(",")]:
-            os.environ["PBN_TEAM"] = str(T)
+        for T in args.kernels.split(","):
+            os.environ["PBN_KERNEL"] = "wave" if T.startswith("roll") else T
+            os.environ["PBN_ROLL"] = {"rollh": "hoist", "rolll": "lean"}.get(T, "auto")
             env = VectorPBNEnv(spec, n, seed=3, keep_final_state=False)
             env.reset()
             with torch.cuda.stream(stream):
+                if T.startswith("roll"):   # one pbn_rollout launch of `chunk` steps
+                    buf = env.rollout(args.chunk)
+                    torch.cuda.synchronize()
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=stream):
+                        env.rollout(args.chunk, out=buf)
+                    envs[T], graphs[T] = env, g
+                    continue
                 for _ in range(5):
                     env.step_flipmask(random_actions=True)
                 torch.cuda.synchronize()
@@ -49,7 +58,8 @@ def main():
                     for _ in range(args.chunk):
                         env.step_flipmask(random_actions=True)
             envs[T], graphs[T] = env, g
-        os.environ.pop("PBN_TEAM", None)
+        os.environ.pop("PBN_KERNEL", None)
+        os.environ.pop("PBN_ROLL", None)
         times = {T: [] for T in envs}
         for _ in range(args.rounds):
             for T, g in graphs.items():
@@ -62,7 +72,7 @@ def main():
                 times[T].append(s.elapsed_time(e) / args.chunk)
         for T, ts in times.items():
             med = statistics.median(ts)
-            rec = {"network": args.network, "envs": n, "team": T, "ms_per_step": med,
+            rec = {"network": args.network, "envs": n, "kernel": T, "ms_per_step": med,
                    "env_steps_per_s": n / (med * 1e-3), "min_ms": min(ts)}
             results.append(rec)
             print(json.dumps(rec), flush=True)
