@@ -3,10 +3,14 @@
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
-A "step" is one synchronous PBN transition of every env of the batch (one
-``pbn_step`` launch per GPU): in-kernel random interventions (3 uniform actions
-per env, the explore policy of bdq_model/__init__.py:76), perturbation,
-per-node rule selection + truth-table update, attractor reward, autoreset.
+A "step" is one synchronous PBN transition of every env of the batch:
+in-kernel random interventions (3 uniform actions per env, the explore policy
+of bdq_model/__init__.py:76), perturbation, per-node rule selection +
+truth-table update, attractor reward, autoreset.  By default steps run as
+``pbn_rollout`` launches of --chunk (20 = the horizon) steps, state kept on chip
+between steps, every step's observation, actions, reward and flags written to
+HBM (what a learner consumes); ``--mode step`` times one ``pbn_step`` launch per
+step instead.  The launches of the timed run are captured in one hipGraph.
 Default workload = BASELINE config 2: Bittner-28 (kaban/pbn28.ispl + the 14
 fixture attractors), 65,536 envs per GPU, horizon 20, p = 0.01.  Multi-GPU is
 weak scaling: every rank owns its own env range (env_offset = rank * envs), no
@@ -32,8 +36,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=200)
-    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--steps", type=int, default=2000)
+    p.add_argument("--warmup", type=int, default=200)
+    p.add_argument("--mode", choices=["rollout", "step"], default="rollout",
+                   help="rollout: pbn_rollout launches of --chunk steps (state kept on chip); "
+                        "step: one pbn_step launch per step")
+    p.add_argument("--chunk", type=int, default=20, help="steps per pbn_rollout launch")
     p.add_argument("--network", default="pbn28")
     p.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     p.add_argument("--perturbation", type=float, default=0.01)
@@ -50,6 +58,12 @@ def algorithmic_bytes_per_env(words: int) -> int:
     # read: state 4W, t 1, target 1 ; write: flipmask (in-kernel actions) 4W,
     # state_out 4W, reward 4, flags 1, t 1   (target is rewritten only on reset)
     return 4 * words + 1 + 1 + 4 * words + 4 * words + 4 + 1 + 1
+
+
+def rollout_bytes_per_env(words: int, steps: int) -> int:
+    # per launch: read + write state 4W, t 1, target 1 once; per step write
+    # obs 4W, flipmask (in-kernel actions) 4W, reward 4, flags 1
+    return 2 * (4 * words + 1 + 1) + steps * (4 * words + 4 * words + 4 + 1)
 
 
 def cpu_baseline(spec, envs: int, seconds: float):
@@ -91,6 +105,12 @@ def python_baseline(spec, seconds: float = 3.0):
             "sample": f"oracle/pyoracle.py single env, {k} steps"}
 
 
+def launch_plan(steps: int, chunk: int):
+    """Rollout launch lengths covering `steps` steps: full chunks, then the remainder."""
+    full, rem = divmod(steps, chunk)
+    return [chunk] * full + ([rem] if rem else [])
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -112,62 +132,58 @@ def main():
     env = VectorPBNEnv(spec, args.envs, seed=args.seed, device=dev, env_offset=rank * args.envs,
                        keep_final_state=False)
     env.reset()
-
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.synchronize(dev)
 
-    def one_step():
-        env.step_flipmask(random_actions=True)
+    rollout_mode = args.mode == "rollout"
+    chunk = args.chunk if rollout_mode else 1
+    bufs = {}   # rollout outputs per launch length; captured graphs write into them, so they live
+                # as long as the graphs (torch.cuda.graph empties the allocator cache on entry)
 
-    # step_index advances the RNG time coordinate on the host; a replayed graph
-    # would reuse one index, so the graph holds a whole chunk of distinct steps.
+    def launch(k: int):
+        """One kernel launch covering k steps of every env."""
+        if rollout_mode:
+            bufs[k] = env.rollout(k, random_actions=True, keep_obs=True, keep_final=False, out=bufs.get(k))
+        else:
+            env.step_flipmask(random_actions=True)
+
+    plan = launch_plan(args.steps, chunk)
     use_graph = not args.no_graph
-    chunk = 20
     with torch.cuda.stream(stream):
-        for _ in range(args.warmup):
-            one_step()
+        for k in launch_plan(args.warmup, chunk):
+            launch(k)
         torch.cuda.synchronize(dev)
-
-        # per-launch kernel duration with HIP events on the launch stream
-        n_ev = 50
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
-        for s, e in evs:
-            s.record(stream)
-            one_step()
-            e.record(stream)
-        torch.cuda.synchronize(dev)
-        kernel_ms = sum(s.elapsed_time(e) for s, e in evs) / n_ev
-
-        graphs = []
+        graph = None
         if use_graph:
-            n_graphs = (args.steps + chunk - 1) // chunk
-            for _ in range(n_graphs):
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=stream):
-                    for _ in range(chunk):
-                        one_step()
-                graphs.append(g)
+            # step_index (the RNG time coordinate) advances on the host, so the graph holds
+            # the whole timed run as distinct launches
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=stream):
+                for k in plan:
+                    launch(k)
             torch.cuda.synchronize(dev)
-            graphs[0].replay()  # warm the graph path
+            graph.replay()  # warm the graph path
             torch.cuda.synchronize(dev)
 
         if world > 1:
             torch.distributed.barrier()
         torch.cuda.synchronize(dev)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
+        ev0.record(stream)
         if use_graph:
-            full, rem = divmod(args.steps, chunk)
-            for i in range(full):
-                graphs[i].replay()
-            for _ in range(rem):
-                one_step()
+            graph.replay()
         else:
-            for _ in range(args.steps):
-                one_step()
+            for k in plan:
+                launch(k)
+        ev1.record(stream)
         torch.cuda.synchronize(dev)
         if world > 1:
             torch.distributed.barrier()
         elapsed = time.perf_counter() - t0
+    # average launch duration of the step kernel, from HIP events on its own stream over
+    # the timed region (launches are back to back inside the graph)
+    launch_ms = ev0.elapsed_time(ev1) / len(plan)
 
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -177,10 +193,18 @@ def main():
     value = total_env_steps / elapsed
 
     if rank == 0:
-        bytes_env = algorithmic_bytes_per_env(spec.words)
-        achieved = env.n_alloc * bytes_env / (kernel_ms * 1e-3) / 1e9
+        W = spec.words
+        if rollout_mode:
+            bytes_launch = env.n_alloc * rollout_bytes_per_env(W, chunk)
+            kernel = "pbn_step_wave (rollout, %d steps/launch)" % chunk
+        else:
+            bytes_launch = env.n_alloc * algorithmic_bytes_per_env(W)
+            kernel = "pbn_step_wave (single step)"
+        # the timed plan's launches are full chunks except possibly the last
+        full_launch_ms = launch_ms * len(plan) * chunk / args.steps if rollout_mode else launch_ms
+        achieved = bytes_launch / (full_launch_ms * 1e-3) / 1e9
         traffic = None
-        pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.network}_{args.envs}.json")
+        pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.network}_{args.envs}_{args.mode}.json")
         if os.path.exists(pmc_path):
             with open(pmc_path) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
@@ -198,15 +222,18 @@ def main():
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic",
-            "config": {"workload": f"{args.network} x {args.envs} envs per GPU, in-kernel random interventions, "
-                                   f"autoreset, horizon {args.horizon}, p={args.perturbation}, "
-                                   f"prob_bits={args.prob_bits}",
+            "config": {"workload": f"{args.network} x {args.envs} envs per GPU, in-kernel random interventions "
+                                   f"(3 uniform actions/env/step), autoreset, horizon {args.horizon}, "
+                                   f"p={args.perturbation}, prob_bits={args.prob_bits}; "
+                                   + (f"pbn_rollout, {chunk} steps/launch, per-step obs/actions/rewards/flags "
+                                      f"written to HBM" if rollout_mode else "pbn_step per step"),
                        "network": args.network, "envs_per_gpu": args.envs, "global_envs": world * args.envs,
                        "parallelism": f"env-shard x{world}", "launch": "hipGraph" if use_graph else "eager"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "pbn_step_kernel", "kernel_ms": kernel_ms,
-                         "bytes_per_env_step": bytes_env},
+                         "kernel": kernel, "launch_ms": full_launch_ms,
+                         "bytes_per_launch": bytes_launch,
+                         "note": "VALU-bound (Philox volume), see DESIGN.md 'What bounds it'"},
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(spec, args.envs, args.cpu_seconds)

@@ -84,6 +84,7 @@ struct StepArgs {
   unsigned long long* stamps;  // diagnostic builds (-DPBN_STAMPS) only: per-wave phase clocks
   int n_steps;       // steps per launch (wave kernel); outputs are [n_steps][...] arrays
   uint32_t* obs;     // [n_steps][W][n] observation before each step (nullable)
+  int n_states;      // attractor states (bounds of att_states; checked builds)
 };
 
 // In-kernel phase clocks (cdna_hip_programming.md section 7, "In-kernel stamps"):
@@ -100,6 +101,20 @@ struct StepArgs {
   } while (0)
 #else
 #define PBN_STAMP(k) do {} while (0)
+#endif
+
+// Bounds-checked global indexing for the diagnostic library (-DPBN_CHECKS): an
+// out-of-range index is printed and redirected to element 0 instead of faulting.
+#ifdef PBN_CHECKS
+__device__ __noinline__ size_t pbn_ck(size_t i, size_t len, int site) {
+  if (i < len) return i;
+  printf("pbn OOB site %d idx %llu len %llu block %u thread %u\n", site, (unsigned long long)i,
+         (unsigned long long)len, blockIdx.x, threadIdx.x);
+  return 0;
+}
+#define CK(i, len, site) pbn_ck((size_t)(i), (size_t)(len), (site))
+#else
+#define CK(i, len, site) (i)
 #endif
 
 // ---------------------------------------------------------------- helpers
@@ -615,9 +630,9 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
   for (int w = 0; w < W; ++w) st[w] = 0;
   if (lo) {
 #pragma unroll
-    for (int w = 0; w < W; ++w) st[w] = a.state[(size_t)w * n + le] & valid_word_mask(N, w);
-    tt0 = a.t[le];
-    tg0 = a.target[le];
+    for (int w = 0; w < W; ++w) st[w] = a.state[CK((size_t)w * n + le, plane, 1)] & valid_word_mask(N, w);
+    tt0 = a.t[CK(le, n, 2)];
+    tg0 = a.target[CK(le, n, 3)];
   }
   // node l32 + 32r: its first kNodeRecs compact records {inputs, table, threshold, meta}
   // (node-major, fixed stride: no dependent load); meta of record 0 = nf, of record 1 = f0
@@ -627,12 +642,12 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
     const int i = l32 + 32 * r;
     const int ic = i < N ? i : 0;
 #pragma unroll
-    for (int q = 0; q < kNodeRecs; ++q) rec_[r][q] = a.nrec[(size_t)ic * kNodeRecs + q];
+    for (int q = 0; q < kNodeRecs; ++q) rec_[r][q] = a.nrec[CK((size_t)ic * kNodeRecs + q, N * kNodeRecs, 4)];
   }
   {
     const uint4* src = reinterpret_cast<const uint4*>(a.tab);
     uint4* dst = reinterpret_cast<uint4*>(L);
-    for (int k = lane; k < (a.tab_words >> 2); k += 64) dst[k] = src[k];
+    for (int k = lane; k < (a.tab_words >> 2); k += 64) dst[k] = src[CK(k, a.tab_words >> 2, 5)];
   }
   __builtin_amdgcn_wave_barrier();
 
@@ -661,11 +676,11 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
   for (int w = 0; w < W; ++w) { m[w] = 0; s1[w] = st[w]; }
   if (lo && !random_actions) {
 #pragma unroll
-    for (int w = 0; w < W; ++w) m[w] = a.flipmask[ks * plane + (size_t)w * n + le];
+    for (int w = 0; w < W; ++w) m[w] = a.flipmask[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 6)];
   }
   if (lo && a.obs) {
 #pragma unroll
-    for (int w = 0; w < W; ++w) a.obs[ks * plane + (size_t)w * n + le] = st[w];
+    for (int w = 0; w < W; ++w) a.obs[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 7)] = st[w];
   }
 
   // ---- 1. all Philox calls of the group, two half-wave work lists
@@ -741,7 +756,7 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
         }
       }
 #pragma unroll
-      for (int w = 0; w < W; ++w) a.flipmask[ks * plane + (size_t)w * n + le] = m[w];
+      for (int w = 0; w < W; ++w) a.flipmask[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 8)] = m[w];
     }
 #pragma unroll
     for (int w = 0; w < W; ++w) {
@@ -798,7 +813,7 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
       // selection chain from the last function down: x = F_{nf-1}; x = lt_j ? F_j : x
       uint32_t x = 0;
       for (int j = nf - 1; j >= kNodeRecs; --j) {   // nodes with more than kNodeRecs functions (slow path)
-        const uint4 rc = a.fcompact[f0 + j];
+        const uint4 rc = a.fcompact[CK(f0 + j, a.n_funcs, 9)];
         const uint32_t fj = eval_compact(rc.x, rc.y, S);
         x = (j == nf - 1) ? fj : bfi(less_than(dig[r], rc.z, B), fj, x);
       }
@@ -823,7 +838,7 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
   if (lo) {
   if (a.final_state) {
 #pragma unroll
-    for (int w = 0; w < W; ++w) a.final_state[ks * plane + (size_t)w * n + le] = sp[w];
+    for (int w = 0; w < W; ++w) a.final_state[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 10)] = sp[w];
   }
   const int hmask = (1 << a.hash_bits) - 1;
   const uint32_t* hid = htab + (size_t)W * (hmask + 1);
@@ -848,7 +863,7 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
   int tt = (int)tt0 + 1;
   tt = tt > 255 ? 255 : tt;
   const bool trunc = a.horizon > 0 && tt >= a.horizon;
-  a.reward[ks * n + le] = rtab[(2 * (int)term + (int)wrong) * (N + 1) + (int)pc];
+  a.reward[CK(ks * n + le, n_steps * n, 11)] = rtab[(2 * (int)term + (int)wrong) * (N + 1) + (int)pc];
   uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) | ((uint32_t)pert << 3);
   if ((a.mode & PBN_MODE_AUTORESET) && (term || trunc)) {
     const uint32_t Rw = E.z;
@@ -856,11 +871,11 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
     if (a.n_attr >= 1) {
       const uint32_t A = (uint32_t)a.n_attr;
       const uint32_t as = ((Rw & 1023u) * A) >> 10;
-      const int st0 = a.att_start[as];
-      const uint32_t size = (uint32_t)(a.att_start[as + 1] - st0);
+      const int st0 = a.att_start[CK(as, a.n_attr + 1, 12)];
+      const uint32_t size = (uint32_t)(a.att_start[CK(as + 1, a.n_attr + 1, 13)] - st0);
       const uint32_t idx = (((Rw >> 20) & 4095u) * size) >> 12;
 #pragma unroll
-      for (int w = 0; w < W; ++w) sp[w] = a.att_states[(size_t)(st0 + idx) * W + w];
+      for (int w = 0; w < W; ++w) sp[w] = a.att_states[CK((size_t)(st0 + idx) * W + w, (size_t)a.n_states * W, 14)];
       nt = as;
       if (A >= 2) {
         nt = (((Rw >> 10) & 1023u) * (A - 1)) >> 10;
@@ -877,7 +892,7 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
     tt = 0;
     fl |= PBN_FLAG_RESET;
   }
-  a.flags[ks * n + le] = (uint8_t)fl;
+  a.flags[CK(ks * n + le, n_steps * n, 15)] = (uint8_t)fl;
   tt0 = (uint32_t)tt;
 #pragma unroll
   for (int w = 0; w < W; ++w) st[w] = sp[w];
@@ -887,9 +902,9 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
 
   if (lo) {
 #pragma unroll
-    for (int w = 0; w < W; ++w) a.state_out[(size_t)w * n + le] = st[w];
-    a.t[le] = (uint8_t)tt0;
-    a.target[le] = (uint8_t)tg0;
+    for (int w = 0; w < W; ++w) a.state_out[CK((size_t)w * n + le, plane, 16)] = st[w];
+    a.t[CK(le, n, 17)] = (uint8_t)tt0;
+    a.target[CK(le, n, 18)] = (uint8_t)tg0;
   }
 }
 
@@ -897,7 +912,7 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
 template <int W>
 __global__ void __launch_bounds__(256) pbn_reset_kernel(const int32_t* __restrict__ att_start,
                                                         const uint32_t* __restrict__ att_states,
-                                                        int n_attr, int N, uint64_t seed, uint64_t step,
+                                                        int n_attr, int n_states, int N, uint64_t seed, uint64_t step,
                                                         uint64_t env_offset, int64_t n, uint32_t* state,
                                                         uint8_t* target, uint8_t* t) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -909,11 +924,11 @@ __global__ void __launch_bounds__(256) pbn_reset_kernel(const int32_t* __restric
   if (n_attr >= 1) {
     const uint32_t Rw = r0.x, A = (uint32_t)n_attr;
     const uint32_t as = ((Rw & 1023u) * A) >> 10;
-    const int st0 = att_start[as];
-    const uint32_t size = (uint32_t)(att_start[as + 1] - st0);
+    const int st0 = att_start[CK(as, n_attr + 1, 20)];
+    const uint32_t size = (uint32_t)(att_start[CK(as + 1, n_attr + 1, 21)] - st0);
     const uint32_t idx = (((Rw >> 20) & 4095u) * size) >> 12;
 #pragma unroll
-    for (int w = 0; w < W; ++w) ns[w] = att_states[(size_t)(st0 + idx) * W + w];
+    for (int w = 0; w < W; ++w) ns[w] = att_states[CK((size_t)(st0 + idx) * W + w, (size_t)n_states * W, 22)];
     nt = as;
     if (A >= 2) {
       nt = (((Rw >> 10) & 1023u) * (A - 1)) >> 10;
@@ -981,7 +996,7 @@ StepFn pick_wave(int W, int B) {
   return nullptr;
 }
 
-using ResetFn = void (*)(const int32_t*, const uint32_t*, int, int, uint64_t, uint64_t, uint64_t, int64_t,
+using ResetFn = void (*)(const int32_t*, const uint32_t*, int, int, int, uint64_t, uint64_t, uint64_t, int64_t,
                          uint32_t*, uint8_t*, uint8_t*);
 ResetFn pick_reset(int W) {
   switch (W) {
@@ -1015,7 +1030,9 @@ struct pbn_net {
   StepFn wave_lean = nullptr;   // rollout with low VGPR count (large batches)
   int force = 0;             // PBN_KERNEL env override: 1 = lane, 2 = wave
   int force_roll = 0;        // PBN_ROLL env override: 1 = hoist, 2 = lean
-  int64_t roll_lean_groups = 1 << 16;  // rollouts above this many 32-env groups use the lean variant
+  int64_t roll_lean_groups = 0;  // rollouts above this many 32-env groups use the lean variant
+                                 // (lean won at every measured size, 65,536..8.4M envs:
+                                 // profiles/r01_sweep_pbn28_variants.jsonl)
   ResetFn reset = nullptr;
   FuncRec* d_funcs = nullptr;
   int32_t* d_node_fs = nullptr;
@@ -1323,7 +1340,7 @@ int pbn_reset(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, i
   const int threads = 256;
   const unsigned blocks = (unsigned)((n_envs + threads - 1) / threads);
   hipLaunchKernelGGL(net->reset, dim3(blocks), dim3(threads), 0, (hipStream_t)stream, net->d_att_start,
-                     net->d_att_states, net->n_attr, net->n_nodes, seed, step, env_offset, n_envs, d_state,
+                     net->d_att_states, net->n_attr, net->n_states, net->n_nodes, seed, step, env_offset, n_envs, d_state,
                      d_target, d_t);
   HIP_OK(hipGetLastError());
   return PBN_OK;
@@ -1372,6 +1389,7 @@ int pbn_step(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, in
   a.hash_bits = net->n_attr ? net->hash_bits : 0;
   a.hash_probes = net->hash_probes;
   a.tab_words = net->tab_words;
+  a.n_states = net->n_states;
   memcpy(a.hash_mult, net->hash_mult, sizeof a.hash_mult);
 #ifdef PBN_STAMPS
   a.stamps = g_stamps;
@@ -1445,6 +1463,7 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
   a.hash_bits = net->n_attr ? net->hash_bits : 0;
   a.hash_probes = net->hash_probes;
   a.tab_words = net->tab_words;
+  a.n_states = net->n_states;
   memcpy(a.hash_mult, net->hash_mult, sizeof a.hash_mult);
   a.prob_bits = net->B;
   a.n_funcs = net->n_funcs;
@@ -1456,8 +1475,8 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
 #ifdef PBN_STAMPS
   a.stamps = g_stamps;
 #endif
-  // few waves per SIMD: hoisting loop invariants shortens each step's critical path;
-  // many waves: occupancy wins (measured crossover in profiles/)
+  // hoisting loop invariants shortens each step's critical path, the lean variant keeps
+  // occupancy; lean measured faster at every size (profiles/r01_sweep_pbn28_variants.jsonl)
   bool lean = a.n_groups > (int64_t)net->roll_lean_groups;
   if (net->force_roll == 1) lean = false;
   if (net->force_roll == 2) lean = true;

@@ -1,0 +1,22 @@
+#!/bin/bash
+# On the GPU box: bench line + rocprofv3 kernel stats + two PMC passes (FETCH_SIZE, WRITE_SIZE)
+# for the same bench command.  Usage: tools/gpu_bench_profile.sh TAG [bench args...]
+# Outputs under gpurun_out/TAG/.  Every GPU step has its own time limit; the first failure ends the script.
+set -euo pipefail
+tag=$1; shift
+root=${GRAFT_REPO_ROOT:-/root/repo}
+out=$root/gpurun_out/$tag
+mkdir -p "$out"
+cd /tmp && export TMPDIR=/tmp
+cd "$root"
+timeout -k 10 300 python bench.py "$@" > "$out/bench.json" 2> "$out/bench.err"
+echo "bench done"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- \
+  python bench.py --no-cpu-baseline "$@" > "$out/trace_bench.json" 2> "$out/trace.err"
+echo "trace done"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --stats --output-format csv -d "$out/pmc_fetch" -o run -- \
+  python bench.py --no-cpu-baseline "$@" > /dev/null 2> "$out/pmc_fetch.err"
+echo "fetch done"
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats --output-format csv -d "$out/pmc_write" -o run -- \
+  python bench.py --no-cpu-baseline "$@" > /dev/null 2> "$out/pmc_write.err"
+echo "write done"

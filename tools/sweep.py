@@ -36,6 +36,8 @@ def main():
     for n in [int(x) for x in args.envs.split(",")]:
         envs = {}
         graphs = {}
+        bufs = {}   # a captured graph writes into these: they must outlive it (torch.cuda.graph
+                    # empties the allocator cache on entry, unmapping freed >= 20 MB segments)
         for T in args.kernels.split(","):
             os.environ["PBN_KERNEL"] = "wave" if T.startswith("roll") else T
             os.environ["PBN_ROLL"] = {"rollh": "hoist", "rolll": "lean"}.get(T, "auto")
@@ -43,11 +45,11 @@ def main():
             env.reset()
             with torch.cuda.stream(stream):
                 if T.startswith("roll"):   # one pbn_rollout launch of `chunk` steps
-                    buf = env.rollout(args.chunk)
+                    bufs[T] = env.rollout(args.chunk)
                     torch.cuda.synchronize()
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, stream=stream):
-                        env.rollout(args.chunk, out=buf)
+                        env.rollout(args.chunk, out=bufs[T])
                     envs[T], graphs[T] = env, g
                     continue
                 for _ in range(5):
