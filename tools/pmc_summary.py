@@ -1,0 +1,55 @@
+"""Turn the PMC passes of tools/gpu_bench_profile.sh into profiles/pmc_<net>_<envs>_<mode>.json.
+
+    python tools/pmc_summary.py gpurun_out/r01c --envs 65536 --steps-per-launch 20 [--words 1]
+
+HBM bytes per launch of the step kernel = 2 x FETCH_SIZE + WRITE_SIZE (kB units), the gfx950
+correction of MI355X_MICROARCH.md's HBM section.  bench.py reads `hbm_bytes_per_launch` as
+roofline.traffic.
+"""
+import argparse
+import csv
+import json
+import os
+
+
+def mean_counter(path, counter, kernel="pbn_step_wave"):
+    vals, name = [], None
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r["Counter_Name"] == counter and kernel in r["Kernel_Name"]:
+                vals.append(float(r["Counter_Value"]))
+                name = r["Kernel_Name"]
+    return sum(vals) / len(vals), len(vals), name
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("run_dir")
+    ap.add_argument("--network", default="pbn28")
+    ap.add_argument("--envs", type=int, default=65536)
+    ap.add_argument("--mode", default="rollout")
+    ap.add_argument("--steps-per-launch", type=int, default=20)
+    ap.add_argument("--words", type=int, default=1)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    f, n, name = mean_counter(os.path.join(args.run_dir, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    w, _, _ = mean_counter(os.path.join(args.run_dir, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    W, T = args.words, args.steps_per_launch
+    if args.mode == "rollout":
+        alg = args.envs * (2 * (4 * W + 2) + T * (8 * W + 5))
+    else:
+        alg = args.envs * (12 * W + 8)
+    out = {"kernel": name, "mode": args.mode, "envs": args.envs, "launches": n,
+           "FETCH_SIZE_kB_per_launch": f, "WRITE_SIZE_kB_per_launch": w,
+           "correction": "MI355X_MICROARCH.md HBM section: FETCH_SIZE x2 on gfx950; counter units kB (1024 B)",
+           "hbm_read_bytes_per_launch": f * 2 * 1024, "hbm_write_bytes_per_launch": w * 1024,
+           "hbm_bytes_per_launch": (2 * f + w) * 1024, "algorithmic_bytes_per_launch": alg,
+           "note": "the read side is 4-B and 1-B loads plus table reads, a width the guide leaves uncalibrated"}
+    path = args.out or os.path.join("profiles", f"pmc_{args.network}_{args.envs}_{args.mode}.json")
+    with open(path, "w") as fo:
+        json.dump(out, fo, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
