@@ -85,6 +85,7 @@ struct StepArgs {
   int n_steps;       // steps per launch (wave kernel); outputs are [n_steps][...] arrays
   uint32_t* obs;     // [n_steps][W][n] observation before each step (nullable)
   int n_states;      // attractor states (bounds of att_states; checked builds)
+  int att_off;       // LDS image offset of attractor start[A+1] | states[S][W] (wave kernel)
 };
 
 // In-kernel phase clocks (cdna_hip_programming.md section 7, "In-kernel stamps"):
@@ -588,6 +589,24 @@ __device__ __forceinline__ int gap_est(const uint32_t* __restrict__ cdf, int len
   return g;
 }
 
+// Lower lanes receive the upper lanes' four words (upper lanes end with junk): per pair of
+// words two v_permlane32_swap and no copies.  swap(X, Y) moves X's upper half into Y's
+// lower half; swap(Y', X') then moves Y's upper half into X''s lower half.
+__device__ __forceinline__ pbn::Word4 upper_to_lower(pbn::Word4 v) {
+  const auto a1 = __builtin_amdgcn_permlane32_swap(v.x, v.y, false, false);
+  const auto a2 = __builtin_amdgcn_permlane32_swap(a1[1], a1[0], false, false);
+  const auto b1 = __builtin_amdgcn_permlane32_swap(v.z, v.w, false, false);
+  const auto b2 = __builtin_amdgcn_permlane32_swap(b1[1], b1[0], false, false);
+  return pbn::Word4{a2[0], a2[1], b2[0], b2[1]};
+}
+
+template <int W>
+__device__ __forceinline__ void set_bit(uint32_t (&g)[W], int pos, int N) {
+#pragma unroll
+  for (int w = 0; w < W; ++w)
+    if (pos < N && (pos >> 5) == w) g[w] |= 1u << (pos & 31);
+}
+
 // VARIANT 0: rollout, loop invariants hoisted (small batches, few waves per SIMD);
 // 1: exactly one step (pbn_step; no loop, lowest VGPR count);
 // 2: rollout with invariants recomputed per step (large batches, occupancy first).
@@ -652,6 +671,9 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
   __builtin_amdgcn_wave_barrier();
 
   const int n_steps = VARIANT == 1 ? 1 : a.n_steps;
+  // Random-action mode issues no global load inside the step loop (attractor tables live in
+  // LDS), so stores never have to drain (vmcnt retires in issue order).  A given flip mask
+  // is loaded and consumed inside its own branch, so the wait for it stays on that path.
   for (int ks = 0; ks < n_steps; ++ks) {
   if constexpr (LEAN) {
     // LEAN (large batches): keep loop-invariant expansions (leaf masks, threshold digits,
@@ -674,10 +696,6 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
   uint32_t m[W], s1[W];
 #pragma unroll
   for (int w = 0; w < W; ++w) { m[w] = 0; s1[w] = st[w]; }
-  if (lo && !random_actions) {
-#pragma unroll
-    for (int w = 0; w < W; ++w) m[w] = a.flipmask[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 6)];
-  }
   if (lo && a.obs) {
 #pragma unroll
     for (int w = 0; w < W; ++w) a.obs[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 7)] = st[w];
@@ -712,29 +730,12 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
   for (int r = 0; r < W; ++r) {
 #pragma unroll
     for (int c = 0; c < CPN; ++c) {
-      Word4 d;
-      if (c < H) {
-        d = out[(1 + r * H + c) < IT ? (1 + r * H + c) : 0];
-      } else {
-        const Word4 src = out[r * (CPN - H) + (c - H)];
-        const auto sx = __builtin_amdgcn_permlane32_swap(src.x, src.x, false, false);
-        const auto sy = __builtin_amdgcn_permlane32_swap(src.y, src.y, false, false);
-        const auto sz = __builtin_amdgcn_permlane32_swap(src.z, src.z, false, false);
-        const auto sw = __builtin_amdgcn_permlane32_swap(src.w, src.w, false, false);
-        d.x = sx[1]; d.y = sy[1]; d.z = sz[1]; d.w = sw[1];   // lower lanes: value of lane + 32
-      }
+      const Word4 d = c < H ? out[(1 + r * H + c) < IT ? (1 + r * H + c) : 0]
+                            : upper_to_lower(out[r * (CPN - H) + (c - H)]);
       dig[r][4 * c + 0] = d.x; dig[r][4 * c + 1] = d.y; dig[r][4 * c + 2] = d.z; dig[r][4 * c + 3] = d.w;
     }
   }
-  uint32_t P4[4];
-  {
-    const Word4 src = out[W * (CPN - H)];
-    const auto sx = __builtin_amdgcn_permlane32_swap(src.x, src.x, false, false);
-    const auto sy = __builtin_amdgcn_permlane32_swap(src.y, src.y, false, false);
-    const auto sz = __builtin_amdgcn_permlane32_swap(src.z, src.z, false, false);
-    const auto sw = __builtin_amdgcn_permlane32_swap(src.w, src.w, false, false);
-    P4[0] = sx[1]; P4[1] = sy[1]; P4[2] = sz[1]; P4[3] = sw[1];
-  }
+  const Word4 P4 = upper_to_lower(out[W * (CPN - H)]);   // PERT call 0 of env l32
   const Word4 E = out[0];
 
   // ---- 2. per env (lower lanes): interventions, perturbation, reset word
@@ -757,55 +758,62 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
       }
 #pragma unroll
       for (int w = 0; w < W; ++w) a.flipmask[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 8)] = m[w];
+    } else {
+#pragma unroll
+      for (int w = 0; w < W; ++w)
+        m[w] = a.flipmask[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 6)] & valid_word_mask(N, w);
     }
 #pragma unroll
     for (int w = 0; w < W; ++w) {
-      m[w] &= valid_word_mask(N, w);
       pc += __builtin_popcount(m[w]);
       s1[w] ^= m[w];
     }
-    int pos = -1;
-    for (int kk = 0; pos < N - 1; ++kk) {
-      uint32_t u;
-      if (kk == 0) {
-        u = E.x;
-      } else if (kk == 1) {
-        u = E.y;
-      } else {
-        if (kk >= 6 && ((kk - 2) & 3) == 0) {
-          const Word4 pw = pbn::philox4x32_10(ge_lo, st_lo,
-                                              (pbn::kStreamPert << 28) | (uint32_t)((kk - 2) >> 2), ge_hi, kk0, kk1);
-          P4[0] = pw.x; P4[1] = pw.y; P4[2] = pw.z; P4[3] = pw.w;
-        }
+    // perturbation positions are prefix sums of geometric gaps; the first three gaps
+    // (u = E.x, E.y, PERT word 0) are independent, so they are computed side by side
+    int g0, g1, g2;
+    if (a.gap_exact) {
+      g0 = gap_of(cdf, a.cdf_len, E.x); g1 = gap_of(cdf, a.cdf_len, E.y); g2 = gap_of(cdf, a.cdf_len, P4.x);
+    } else {
+      g0 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.x);
+      g1 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.y);
+      g2 = gap_est(cdf, a.cdf_len, a.inv_log2q, P4.x);
+    }
+    const int p0 = g0 - 1, p1 = p0 + g1, p2 = p1 + g2;
+    set_bit<W>(gam, p0, N);
+    set_bit<W>(gam, p1, N);
+    set_bit<W>(gam, p2, N);
+    if (p2 < N - 1) {   // rare: a fourth flip is possible (gap k >= 3: PERT call (k-2)>>2, word (k-2)&3)
+      Word4 P = P4;
+      int pos = p2;
+      for (int kk = 3; pos < N - 1; ++kk) {
+        if ((kk & 3) == 2)
+          P = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamPert << 28) | (uint32_t)((kk - 2) >> 2), ge_hi, kk0, kk1);
         const int j4 = (kk - 2) & 3;
-        u = j4 == 0 ? P4[0] : (j4 == 1 ? P4[1] : (j4 == 2 ? P4[2] : P4[3]));
+        const uint32_t u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
+        pos += a.gap_exact ? gap_of(cdf, a.cdf_len, u) : gap_est(cdf, a.cdf_len, a.inv_log2q, u);
+        set_bit<W>(gam, pos, N);
       }
-      pos += a.gap_exact ? gap_of(cdf, a.cdf_len, u) : gap_est(cdf, a.cdf_len, a.inv_log2q, u);
-      if (pos >= N) break;
-#pragma unroll
-      for (int w = 0; w < W; ++w)
-        if ((pos >> 5) == w) gam[w] |= 1u << (pos & 31);
     }
 #pragma unroll
     for (int w = 0; w < W; ++w) pert = pert || gam[w] != 0;
   }
-  const uint32_t pmask = (uint32_t)__ballot(pert);
 
-  // ---- 3. bit-slice: lane p <- plane p of s1 (to LDS) and of s1 ^ gamma (register)
+  // ---- 3. bit-slice s1: lane p <- plane p (node p over the 32 envs), to LDS
   PBN_STAMP(3);
-  uint32_t R[W];
 #pragma unroll
   for (int w = 0; w < W; ++w) {
     const uint32_t sp = lane_transpose32(s1[w], lane);
-    R[w] = lane_transpose32(s1[w] ^ gam[w], lane);
     if (lo) S[32 * w + l32] = sp;
   }
   __builtin_amdgcn_wave_barrier();
 
-  // ---- 4. node l32 + 32r on lane l32
+  // ---- 4. node l32 + 32r on lane l32: X = rule update of every env (perturbed envs are
+  // replaced after the back-transpose)
   PBN_STAMP(4);
+  uint32_t X[W];
 #pragma unroll
   for (int r = 0; r < W; ++r) {
+    X[r] = 0;
     const int i = l32 + 32 * r;
     const int nf = (lo && i < N) ? (int)rec_[r][0].w : 0;
     if (nf > 0) {
@@ -825,7 +833,7 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
           x = (q == nf - 1) ? fj : bfi(less_than(dig[r], rc.z, B), fj, x);
         }
       }
-      R[r] = bfi(pmask, R[r], x);
+      X[r] = x;
     }
   }
 
@@ -833,22 +841,36 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
   PBN_STAMP(5);
   uint32_t sp[W];
 #pragma unroll
-  for (int w = 0; w < W; ++w) sp[w] = lane_transpose32(R[w], lane);
+  for (int w = 0; w < W; ++w) sp[w] = lane_transpose32(X[w], lane);
   PBN_STAMP(6);
   if (lo) {
+  if (pert) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) sp[w] = s1[w] ^ gam[w];
+  }
   if (a.final_state) {
 #pragma unroll
     for (int w = 0; w < W; ++w) a.final_state[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 10)] = sp[w];
   }
-  const int hmask = (1 << a.hash_bits) - 1;
-  const uint32_t* hid = htab + (size_t)W * (hmask + 1);
   int att = -1;
   if (a.hash_bits > 0) {
+    const int hmask = (1 << a.hash_bits) - 1;
+    const uint32_t* hid = htab + (size_t)W * (hmask + 1);
     uint32_t h = 0;
 #pragma unroll
     for (int w = 0; w < W; ++w) h += sp[w] * a.hash_mult[w];
     h >>= (32 - a.hash_bits);
-    for (int pr = 0; pr < a.hash_probes; ++pr) {
+    // keys are unique: probe order does not matter; the first four probes are read side by side
+#pragma unroll
+    for (int pr = 0; pr < 4; ++pr) {
+      const uint32_t slot = (h + pr) & hmask;
+      bool eq = pr < a.hash_probes;
+#pragma unroll
+      for (int w = 0; w < W; ++w) eq = eq && (htab[(size_t)w * (hmask + 1) + slot] == sp[w]);
+      const uint32_t id = hid[slot];
+      if (eq && id != 0xFFFFFFFFu) att = (int)id;
+    }
+    for (int pr = 4; pr < a.hash_probes; ++pr) {
       const uint32_t slot = (h + pr) & hmask;
       bool eq = true;
 #pragma unroll
@@ -869,13 +891,16 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
     const uint32_t Rw = E.z;
     uint32_t nt;
     if (a.n_attr >= 1) {
+      // attractor tables from the LDS image: start[A+1] then states[S][W]
+      const int32_t* att_first = reinterpret_cast<const int32_t*>(L + a.att_off);
+      const uint32_t* att_words = L + a.att_off + a.n_attr + 1;
       const uint32_t A = (uint32_t)a.n_attr;
       const uint32_t as = ((Rw & 1023u) * A) >> 10;
-      const int st0 = a.att_start[CK(as, a.n_attr + 1, 12)];
-      const uint32_t size = (uint32_t)(a.att_start[CK(as + 1, a.n_attr + 1, 13)] - st0);
+      const int st0 = att_first[as];
+      const uint32_t size = (uint32_t)(att_first[as + 1] - st0);
       const uint32_t idx = (((Rw >> 20) & 4095u) * size) >> 12;
 #pragma unroll
-      for (int w = 0; w < W; ++w) sp[w] = a.att_states[CK((size_t)(st0 + idx) * W + w, (size_t)a.n_states * W, 14)];
+      for (int w = 0; w < W; ++w) sp[w] = att_words[(size_t)(st0 + idx) * W + w];
       nt = as;
       if (A >= 2) {
         nt = (((Rw >> 10) & 1023u) * (A - 1)) >> 10;
@@ -1016,6 +1041,7 @@ struct pbn_net {
   int cdf_len = 0, hash_bits = 0, hash_probes = 0, tab_words = 0;
   uint32_t hash_mult[4] = {0, 0, 0, 0};
   int wave_words = 0;
+  int att_off = 0;
   int gap_exact = 1;
   float inv_log2q = 0.f;
   uint4* d_fcompact = nullptr;
@@ -1227,6 +1253,12 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     tab.push_back(u);
   }
   tab.insert(tab.end(), hash_img.begin(), hash_img.end());
+  // attractor start[A+1] | states[S][W], read by autoreset in the wave kernel
+  net->att_off = (int)tab.size();
+  if (A) {
+    for (int k = 0; k <= A; ++k) tab.push_back((uint32_t)d->attractor_start[k]);
+    tab.insert(tab.end(), d->attractor_states, d->attractor_states + (size_t)S * W);
+  }
   while (tab.size() & 3) tab.push_back(0u);  // keep the FuncRec image 16-byte aligned in LDS
   net->tab_words = (int)tab.size();
   net->n_funcs = d->n_funcs;
@@ -1390,6 +1422,7 @@ int pbn_step(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, in
   a.hash_probes = net->hash_probes;
   a.tab_words = net->tab_words;
   a.n_states = net->n_states;
+  a.att_off = net->att_off;
   memcpy(a.hash_mult, net->hash_mult, sizeof a.hash_mult);
 #ifdef PBN_STAMPS
   a.stamps = g_stamps;
@@ -1464,6 +1497,7 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
   a.hash_probes = net->hash_probes;
   a.tab_words = net->tab_words;
   a.n_states = net->n_states;
+  a.att_off = net->att_off;
   memcpy(a.hash_mult, net->hash_mult, sizeof a.hash_mult);
   a.prob_bits = net->B;
   a.n_funcs = net->n_funcs;

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--network", default="pbn28")
+    ap.add_argument("--rollout", type=int, default=0,
+                    help="stamp a pbn_rollout launch of this many steps (phases of its last step)")
     args = ap.parse_args()
     if args.build:
         from pbn_rl_amd import _lib
@@ -51,13 +53,18 @@ def main():
     for _ in range(10):
         env.step_flipmask(random_actions=True)
     torch.cuda.synchronize()
+    out = env.rollout(args.rollout) if args.rollout else None
+    torch.cuda.synchronize()
     L.pbn_debug_set_stamps(buf.data_ptr())
-    env.step_flipmask(random_actions=True)
+    if args.rollout:
+        env.rollout(args.rollout, out=out)
+    else:
+        env.step_flipmask(random_actions=True)
     torch.cuda.synchronize()
     L.pbn_debug_set_stamps(None)
     t = buf.view(waves, 16)[:, :8].cpu().numpy().astype(np.int64)
     d = np.diff(t, axis=1)
-    rep = {"envs": args.envs, "waves": waves,
+    rep = {"envs": args.envs, "waves": waves, "rollout_steps": args.rollout,
            "start_spread_cycles": int(t[:, 0].max() - t[:, 0].min()),
            "kernel_span_cycles": int(t[:, 7].max() - t[:, 0].min()),
            "wave_total_median": int(np.median(t[:, 7] - t[:, 0])),
