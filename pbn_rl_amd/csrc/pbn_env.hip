@@ -38,6 +38,7 @@ namespace {
 
 constexpr int kFuncRecWords = 24;  // in[4], leaf[16], thr, pad[3]
 constexpr int kNodeRecs = 4;       // compact records prefetched per node by the wave kernel
+constexpr int kWavesPerBlock = 4;  // wave kernel: waves (32-env groups) per block, sharing one LDS table image
 constexpr int kMaxHashBits = 12;
 
 struct FuncRec {
@@ -75,7 +76,7 @@ struct StepArgs {
   int tab_words;     // words of the LDS table image
   int prob_bits;
   int n_funcs;
-  int wave_words;    // wave kernel: per-wave LDS words (tables + S planes)
+  int wave_words;    // wave kernel: per-wave LDS words of S planes (after the shared table image)
   int gap_exact;     // 1: binary search for gaps (p == 0 or tiny); 0: log estimate + fix-up
   float inv_log2q;   // 1 / log2(1 - p)
   const uint4* fcompact;   // [n_funcs] {inputs (4 x u8), truth table, threshold, 0}
@@ -86,6 +87,9 @@ struct StepArgs {
   uint32_t* obs;     // [n_steps][W][n] observation before each step (nullable)
   int n_states;      // attractor states (bounds of att_states; checked builds)
   int att_off;       // LDS image offset of attractor start[A+1] | states[S][W] (wave kernel)
+  int sel_off;       // LDS image offset of the leaf selectors, uint4 [kNodeRecs][2][32W] (wave kernel)
+  int uni_nf;        // > 0: every node has uni_nf functions with thresholds uthr (wave-uniform)
+  uint32_t uthr[kNodeRecs];
 };
 
 // In-kernel phase clocks (cdna_hip_programming.md section 7, "In-kernel stamps"):
@@ -574,6 +578,20 @@ __device__ __forceinline__ uint32_t eval_compact(uint32_t ins, uint32_t T, const
   return bfi(x3, bfi(x2, w3, w2), bfi(x2, w1, w0));
 }
 
+// eval from per-lane leaf selectors: leaf m = (T bit 2m, T bit 2m+1) = (value at x0 = 0,
+// value at x0 = 1) is one of {0, x0, ~x0, ~0}, i.e. per byte one v_perm_b32 of {~x0 : x0}
+// with selector byte j, 4 + j, 12 (0x00) or 13 (0xFF); the selectors are built on the host.
+__device__ __forceinline__ uint32_t eval_sel(uint32_t ins, uint4 sa, uint4 sb, const uint32_t* __restrict__ S) {
+  const uint32_t x0 = S[ins & 0xFFu], x1 = S[(ins >> 8) & 0xFFu], x2 = S[(ins >> 16) & 0xFFu], x3 = S[ins >> 24];
+  const uint32_t nx0 = ~x0;
+  const uint32_t v0 = __builtin_amdgcn_perm(nx0, x0, sa.x), v1 = __builtin_amdgcn_perm(nx0, x0, sa.y);
+  const uint32_t v2 = __builtin_amdgcn_perm(nx0, x0, sa.z), v3 = __builtin_amdgcn_perm(nx0, x0, sa.w);
+  const uint32_t v4 = __builtin_amdgcn_perm(nx0, x0, sb.x), v5 = __builtin_amdgcn_perm(nx0, x0, sb.y);
+  const uint32_t v6 = __builtin_amdgcn_perm(nx0, x0, sb.z), v7 = __builtin_amdgcn_perm(nx0, x0, sb.w);
+  const uint32_t w0 = bfi(x1, v1, v0), w1 = bfi(x1, v3, v2), w2 = bfi(x1, v5, v4), w3 = bfi(x1, v7, v6);
+  return bfi(x3, bfi(x2, w3, w2), bfi(x2, w1, w0));
+}
+
 // gap(u) = min{m : u < C[m-1]} from a float estimate of log(1-x)/log(1-p) corrected
 // exactly (+-1) against the integer CDF in LDS; C padded with 0xFFFFFFFF.
 __device__ __forceinline__ int gap_est(const uint32_t* __restrict__ cdf, int len, float inv_log2q, uint32_t u) {
@@ -604,14 +622,14 @@ template <int W>
 __device__ __forceinline__ void set_bit(uint32_t (&g)[W], int pos, int N) {
 #pragma unroll
   for (int w = 0; w < W; ++w)
-    if (pos < N && (pos >> 5) == w) g[w] |= 1u << (pos & 31);
+    if ((unsigned)pos < (unsigned)N && (pos >> 5) == w) g[w] |= 1u << (pos & 31);
 }
 
 // VARIANT 0: rollout, loop invariants hoisted (small batches, few waves per SIMD);
 // 1: exactly one step (pbn_step; no loop, lowest VGPR count);
 // 2: rollout with invariants recomputed per step (large batches, occupancy first).
 template <int W, int B, int VARIANT>
-__global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
+__global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a) {
   constexpr bool LEAN = VARIANT == 2;
   constexpr int CPN = B / 4;               // selection calls per node
   constexpr int H = (CPN + 1) / 2;         // of which the lower half computes H
@@ -624,11 +642,11 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int64_t g = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
-  if (g >= a.n_groups) return;  // whole wave; the kernel has no block barrier
   const int N = a.n_nodes;
-  // per-wave LDS: [cdf | reward | hash] image, then S planes
-  uint32_t* L = smem + (size_t)wv * a.wave_words;
-  uint32_t* S = L + a.tab_words;
+  // LDS: the block's table image [cdf | reward | hash | attractors | leaf selectors], then
+  // each wave's S planes
+  uint32_t* L = smem;
+  uint32_t* S = smem + a.tab_words + (size_t)wv * a.wave_words;
   const uint32_t* cdf = L;
   const float* rtab = reinterpret_cast<const float*>(L + a.cdf_len);
   const uint32_t* htab = L + a.cdf_len + 4 * (N + 1);
@@ -647,7 +665,7 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
   uint32_t tt0 = 0, tg0 = 0;
 #pragma unroll
   for (int w = 0; w < W; ++w) st[w] = 0;
-  if (lo) {
+  if (lo && g < a.n_groups) {   // (waves past the end only help copy the tables)
 #pragma unroll
     for (int w = 0; w < W; ++w) st[w] = a.state[CK((size_t)w * n + le, plane, 1)] & valid_word_mask(N, w);
     tt0 = a.t[CK(le, n, 2)];
@@ -666,9 +684,11 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
   {
     const uint4* src = reinterpret_cast<const uint4*>(a.tab);
     uint4* dst = reinterpret_cast<uint4*>(L);
-    for (int k = lane; k < (a.tab_words >> 2); k += 64) dst[k] = src[CK(k, a.tab_words >> 2, 5)];
+    for (int k = threadIdx.x; k < (a.tab_words >> 2); k += blockDim.x) dst[k] = src[CK(k, a.tab_words >> 2, 5)];
   }
-  __builtin_amdgcn_wave_barrier();
+  __syncthreads();   // the kernel's only block barrier
+  if (g >= a.n_groups) return;  // whole wave
+  const uint4* selq = reinterpret_cast<const uint4*>(L + a.sel_off);
 
   const int n_steps = VARIANT == 1 ? 1 : a.n_steps;
   // Random-action mode issues no global load inside the step loop (attractor tables live in
@@ -748,13 +768,9 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
   if (lo) {
     if (random_actions) {
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const uint32_t act = (((E.w >> (10 * q)) & 1023u) * (uint32_t)(N + 1)) >> 10;
-        if (act > 0) {
-#pragma unroll
-          for (int w = 0; w < W; ++w)
-            if ((int)((act - 1) >> 5) == w) m[w] |= 1u << ((act - 1) & 31);
-        }
+      for (int q = 0; q < 3; ++q) {   // action a in [0, N]: 0 = no-op, else flip node a-1
+        const int act = (int)(__umul24((E.w >> (10 * q)) & 1023u, (uint32_t)(N + 1)) >> 10);
+        set_bit<W>(m, act - 1, N);
       }
 #pragma unroll
       for (int w = 0; w < W; ++w) a.flipmask[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 8)] = m[w];
@@ -815,11 +831,26 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
   for (int r = 0; r < W; ++r) {
     X[r] = 0;
     const int i = l32 + 32 * r;
-    const int nf = (lo && i < N) ? (int)rec_[r][0].w : 0;
-    if (nf > 0) {
+    const int ii = lo && i < N ? i : 0;   // other lanes evaluate node 0 and discard it
+    uint32_t x = 0;
+    if (a.uni_nf > 0) {
+      // every node has uni_nf <= kNodeRecs functions with the same thresholds: the
+      // threshold digits are wave-uniform (SGPR operands of the comparison)
+      const int K = a.uni_nf;
+#pragma unroll
+      for (int q = kNodeRecs - 1; q >= 0; --q) {
+        if (q < K) {
+          const uint32_t fj = eval_sel(rec_[r][q].x, selq[(2 * q) * 32 * W + ii], selq[(2 * q + 1) * 32 * W + ii], S);
+          uint32_t c = a.uthr[q];
+          asm volatile("" : "+s"(c));   // digits re-extracted per step on the SALU: hoisting them
+                                        // out of the step loop spills SGPRs to VGPR lanes
+          x = (q == K - 1) ? fj : bfi(less_than(dig[r], c, B), fj, x);
+        }
+      }
+    } else {
+      const int nf = (int)rec_[r][0].w;
       const int f0 = (int)rec_[r][1].w;
       // selection chain from the last function down: x = F_{nf-1}; x = lt_j ? F_j : x
-      uint32_t x = 0;
       for (int j = nf - 1; j >= kNodeRecs; --j) {   // nodes with more than kNodeRecs functions (slow path)
         const uint4 rc = a.fcompact[CK(f0 + j, a.n_funcs, 9)];
         const uint32_t fj = eval_compact(rc.x, rc.y, S);
@@ -829,12 +860,12 @@ __global__ void __launch_bounds__(64) pbn_step_wave(StepArgs a) {
       for (int q = kNodeRecs - 1; q >= 0; --q) {
         if (q < nf) {
           const uint4 rc = rec_[r][q];
-          const uint32_t fj = eval_compact(rc.x, rc.y, S);
+          const uint32_t fj = eval_sel(rc.x, selq[(2 * q) * 32 * W + ii], selq[(2 * q + 1) * 32 * W + ii], S);
           x = (q == nf - 1) ? fj : bfi(less_than(dig[r], rc.z, B), fj, x);
         }
       }
-      X[r] = x;
     }
+    if (lo && i < N) X[r] = x;
   }
 
   // ---- 5. back to per-env words, reward, termination, autoreset, stores
@@ -1042,6 +1073,9 @@ struct pbn_net {
   uint32_t hash_mult[4] = {0, 0, 0, 0};
   int wave_words = 0;
   int att_off = 0;
+  int sel_off = 0;
+  int uni_nf = 0;
+  uint32_t uthr[kNodeRecs] = {0, 0, 0, 0};
   int gap_exact = 1;
   float inv_log2q = 0.f;
   uint4* d_fcompact = nullptr;
@@ -1056,9 +1090,9 @@ struct pbn_net {
   StepFn wave_lean = nullptr;   // rollout with low VGPR count (large batches)
   int force = 0;             // PBN_KERNEL env override: 1 = lane, 2 = wave
   int force_roll = 0;        // PBN_ROLL env override: 1 = hoist, 2 = lean
-  int64_t roll_lean_groups = 0;  // rollouts above this many 32-env groups use the lean variant
-                                 // (lean won at every measured size, 65,536..8.4M envs:
-                                 // profiles/r01_sweep_pbn28_variants.jsonl)
+  int64_t roll_lean_groups = 4096;  // rollouts above this many 32-env groups use the lean variant
+                                    // (crossover between 65,536 and 262,144 envs:
+                                    // profiles/r01_sweep_pbn28_variants_v4.jsonl)
   ResetFn reset = nullptr;
   FuncRec* d_funcs = nullptr;
   int32_t* d_node_fs = nullptr;
@@ -1259,10 +1293,49 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     for (int k = 0; k <= A; ++k) tab.push_back((uint32_t)d->attractor_start[k]);
     tab.insert(tab.end(), d->attractor_states, d->attractor_states + (size_t)S * W);
   }
-  while (tab.size() & 3) tab.push_back(0u);  // keep the FuncRec image 16-byte aligned in LDS
+  while (tab.size() & 3) tab.push_back(0u);  // 16-byte aligned uint4 selectors
+  // leaf selectors of the first kNodeRecs functions of every node, uint4 [kNodeRecs][2][32W]
+  // (lane-consecutive 16-byte reads); see eval_sel
+  net->sel_off = (int)tab.size();
+  {
+    std::vector<uint32_t> sel((size_t)kNodeRecs * 2 * 32 * W * 4, 0x0C0C0C0Cu);
+    for (int i = 0; i < N; ++i) {
+      const int f0 = d->node_func_start[i], nf = d->node_func_start[i + 1] - f0;
+      for (int q = 0; q < kNodeRecs && q < nf; ++q) {
+        const uint32_t T = d->func_table[f0 + q];
+        const int k = d->func_arity[f0 + q];
+        for (int mm = 0; mm < 8; ++mm) {
+          // table bit of input index m (missing inputs read plane 0 but do not matter)
+          auto bit = [&](uint32_t m) { return (T >> (k >= 5 ? m : (m & ((1u << k) - 1u)))) & 1u; };
+          const uint32_t l0 = bit(2u * mm), l1 = bit(2u * mm + 1u);
+          uint32_t word = 0;
+          for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t b = (!l0 && !l1) ? 12u : (l0 && l1) ? 13u : (l1 ? j : 4u + j);
+            word |= b << (8 * j);
+          }
+          const int h = mm >> 2;
+          sel[(((size_t)q * 2 + h) * 32 * W + i) * 4 + (mm & 3)] = word;
+        }
+      }
+    }
+    tab.insert(tab.end(), sel.begin(), sel.end());
+  }
+  // wave-uniform thresholds when every node has the same function count and thresholds
+  {
+    const int nf0 = d->node_func_start[1] - d->node_func_start[0];
+    bool uni = nf0 >= 1 && nf0 <= kNodeRecs;
+    for (int i = 1; uni && i < N; ++i) {
+      const int f0 = d->node_func_start[i];
+      if (d->node_func_start[i + 1] - f0 != nf0) uni = false;
+      for (int q = 0; uni && q < nf0; ++q)
+        if (d->func_threshold[f0 + q] != d->func_threshold[q]) uni = false;
+    }
+    net->uni_nf = uni ? nf0 : 0;
+    for (int q = 0; q < kNodeRecs; ++q) net->uthr[q] = (uni && q < nf0) ? d->func_threshold[q] : 0u;
+  }
   net->tab_words = (int)tab.size();
   net->n_funcs = d->n_funcs;
-  net->wave_words = net->tab_words + ((32 * W + 3) & ~3);
+  net->wave_words = (32 * W + 3) & ~3;   // S planes per wave
   {
     const double p = (double)d->perturb_cdf[0] / 4294967296.0;
     net->gap_exact = (p < 1e-6 || p > 0.5) ? 1 : 0;
@@ -1270,7 +1343,7 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   }
   net->waves_per_block = (W == 1) ? 2 : 1;
   net->lds_lane = (size_t)net->tab_words * 4 + (size_t)net->waves_per_block * 2 * 32 * W * 64 * 4;
-  net->lds_wave = (size_t)net->wave_words * 4;
+  net->lds_wave = ((size_t)net->tab_words + (size_t)kWavesPerBlock * net->wave_words) * 4;
   // compact records for the wave kernel: {inputs as bytes, 4-input truth table, threshold, 0}
   std::vector<uint4> fcomp(d->n_funcs);
   for (int f = 0; f < d->n_funcs; ++f) {
@@ -1423,6 +1496,9 @@ int pbn_step(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, in
   a.tab_words = net->tab_words;
   a.n_states = net->n_states;
   a.att_off = net->att_off;
+  a.sel_off = net->sel_off;
+  a.uni_nf = net->uni_nf;
+  memcpy(a.uthr, net->uthr, sizeof a.uthr);
   memcpy(a.hash_mult, net->hash_mult, sizeof a.hash_mult);
 #ifdef PBN_STAMPS
   a.stamps = g_stamps;
@@ -1448,8 +1524,8 @@ int pbn_step(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, in
     const unsigned blocks = (unsigned)((a.n_groups + threads - 1) / threads);
     hipLaunchKernelGGL(net->lane, dim3(blocks), dim3(threads), net->lds_lane, (hipStream_t)stream, a);
   } else {
-    const unsigned blocks = (unsigned)a.n_groups;  // one 64-lane wave per block and group
-    hipLaunchKernelGGL(net->wave1, dim3(blocks), dim3(64), net->lds_wave, (hipStream_t)stream, a);
+    const unsigned blocks = (unsigned)((a.n_groups + kWavesPerBlock - 1) / kWavesPerBlock);  // one wave per group
+    hipLaunchKernelGGL(net->wave1, dim3(blocks), dim3(64 * kWavesPerBlock), net->lds_wave, (hipStream_t)stream, a);
   }
   HIP_OK(hipGetLastError());
   return PBN_OK;
@@ -1498,6 +1574,9 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
   a.tab_words = net->tab_words;
   a.n_states = net->n_states;
   a.att_off = net->att_off;
+  a.sel_off = net->sel_off;
+  a.uni_nf = net->uni_nf;
+  memcpy(a.uthr, net->uthr, sizeof a.uthr);
   memcpy(a.hash_mult, net->hash_mult, sizeof a.hash_mult);
   a.prob_bits = net->B;
   a.n_funcs = net->n_funcs;
@@ -1514,7 +1593,8 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
   bool lean = a.n_groups > (int64_t)net->roll_lean_groups;
   if (net->force_roll == 1) lean = false;
   if (net->force_roll == 2) lean = true;
-  hipLaunchKernelGGL(lean ? net->wave_lean : net->wave, dim3((unsigned)a.n_groups), dim3(64), net->lds_wave,
+  const unsigned blocks = (unsigned)((a.n_groups + kWavesPerBlock - 1) / kWavesPerBlock);  // one wave per group
+  hipLaunchKernelGGL(lean ? net->wave_lean : net->wave, dim3(blocks), dim3(64 * kWavesPerBlock), net->lds_wave,
                      (hipStream_t)stream, a);
   HIP_OK(hipGetLastError());
   return PBN_OK;
