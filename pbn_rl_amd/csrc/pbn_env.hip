@@ -90,6 +90,9 @@ struct StepArgs {
   int sel_off;       // LDS image offset of the leaf selectors, uint4 [kNodeRecs][2][32W] (wave kernel)
   int uni_nf;        // > 0: every node has uni_nf functions with thresholds uthr (wave-uniform)
   uint32_t uthr[kNodeRecs];
+  int max_nf;        // largest function count of a node
+  int lq;            // pipelined rollout: selection masks per node in a slot (max(max_nf - 1, 1))
+  int slot_words;    // pipelined rollout: words of one step slot
 };
 
 // In-kernel phase clocks (cdna_hip_programming.md section 7, "In-kernel stamps"):
@@ -104,8 +107,32 @@ struct StepArgs {
     if (a.stamps && (threadIdx.x & 63) == 0)                                                  \
       a.stamps[(size_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + (k)] = t_; \
   } while (0)
+// pipelined rollout: per role, clocks at the start of iteration 10, after its work, after the barrier
+#define PBN_PSTAMP(k, slot_)                                                                  \
+  do {                                                                                        \
+    if ((k) == 10) {                                                                          \
+      unsigned long long t_;                                                                  \
+      __builtin_amdgcn_sched_barrier(0);                                                      \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");             \
+      __builtin_amdgcn_sched_barrier(0);                                                      \
+      if (a.stamps && (threadIdx.x & 63) == 0)                                                \
+        a.stamps[(size_t)blockIdx.x * 16 + (threadIdx.x >> 6) * 4 + (slot_)] = t_;            \
+    }                                                                                         \
+  } while (0)
+#define PBN_PSTAMP_AT(k, idx_)                                                                \
+  do {                                                                                        \
+    if ((k) == 10) {                                                                          \
+      unsigned long long t_;                                                                  \
+      __builtin_amdgcn_sched_barrier(0);                                                      \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");             \
+      __builtin_amdgcn_sched_barrier(0);                                                      \
+      if (a.stamps && (threadIdx.x & 63) == 0) a.stamps[(size_t)blockIdx.x * 16 + (idx_)] = t_; \
+    }                                                                                         \
+  } while (0)
 #else
 #define PBN_STAMP(k) do {} while (0)
+#define PBN_PSTAMP(k, slot_) do {} while (0)
+#define PBN_PSTAMP_AT(k, idx_) do {} while (0)
 #endif
 
 // Bounds-checked global indexing for the diagnostic library (-DPBN_CHECKS): an
@@ -964,6 +991,370 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   }
 }
 
+
+// ------------------------------- rollout kernel, three waves per pair of 32-env groups
+// Block = two groups (64 envs; lanes 32h..32h+31 of every wave work on group 2*block + h).
+// The step splits into work that depends only on the counter-based RNG and work that
+// depends on the state, so different waves run different steps:
+//   wave 1 (env draws): ENV + PERT call 0 of env `lane` -> actions / given flip mask,
+//     perturbation mask, autoreset draw;
+//   wave 2 (selection): SEL calls of node `lane & 31` -> the (u < c_j) masks of its thresholds;
+//   wave 0 (state): s1 = s ^ m, bit-slice, node evaluation from the masks, back-transpose,
+//     attractor lookup, reward, flags, autoreset, stores.
+// Iteration k: waves 1 and 2 produce step k into slot k&1 while wave 0 consumes step k-1
+// from the other slot; the block barrier ends the iteration.  Same results as pbn_step_wave.
+// Each wave alone is latency-bound, so the split (three instruction streams per group pair)
+// is what fills the SIMDs at small batches.
+
+// node chain from precomputed selection masks: x = F_{nf-1}; x = lt_j ? F_j : x, with every
+// LDS read of the K records issued before any use (K = wave-uniform bound, nf per lane)
+template <int K>
+__device__ __forceinline__ uint32_t chain_from_masks(const uint4 (&rec)[kNodeRecs], const uint4* __restrict__ sel,
+                                                     int stride, const uint32_t* __restrict__ S,
+                                                     const uint32_t* __restrict__ lt, int lt_stride, int nf,
+                                                     uint32_t x) {
+  uint32_t xin[K][4], ltv[K];
+  uint4 sa[K], sb[K];
+#pragma unroll
+  for (int q = 0; q < K; ++q) {
+    const uint32_t ins = rec[q].x;
+    xin[q][0] = S[ins & 0xFFu]; xin[q][1] = S[(ins >> 8) & 0xFFu];
+    xin[q][2] = S[(ins >> 16) & 0xFFu]; xin[q][3] = S[ins >> 24];
+    sa[q] = sel[(2 * q) * stride];
+    sb[q] = sel[(2 * q + 1) * stride];
+    ltv[q] = q < K - 1 ? lt[q * lt_stride] : 0u;
+  }
+#pragma unroll
+  for (int q = K - 1; q >= 0; --q) {
+    const uint32_t x0 = xin[q][0], x1 = xin[q][1], x2 = xin[q][2], x3 = xin[q][3];
+    const uint32_t nx0 = ~x0;
+    const uint32_t v0 = __builtin_amdgcn_perm(nx0, x0, sa[q].x), v1 = __builtin_amdgcn_perm(nx0, x0, sa[q].y);
+    const uint32_t v2 = __builtin_amdgcn_perm(nx0, x0, sa[q].z), v3 = __builtin_amdgcn_perm(nx0, x0, sa[q].w);
+    const uint32_t v4 = __builtin_amdgcn_perm(nx0, x0, sb[q].x), v5 = __builtin_amdgcn_perm(nx0, x0, sb[q].y);
+    const uint32_t v6 = __builtin_amdgcn_perm(nx0, x0, sb[q].z), v7 = __builtin_amdgcn_perm(nx0, x0, sb[q].w);
+    const uint32_t w0 = bfi(x1, v1, v0), w1 = bfi(x1, v3, v2), w2 = bfi(x1, v5, v4), w3 = bfi(x1, v7, v6);
+    const uint32_t fj = bfi(x3, bfi(x2, w3, w2), bfi(x2, w1, w0));
+    const uint32_t y = (q == nf - 1) ? fj : bfi(ltv[q], fj, x);
+    x = (q < nf) ? y : x;
+  }
+  return x;
+}
+
+template <int W, int B>
+__global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
+  constexpr int CPN = B / 4;              // selection calls per node
+  extern __shared__ uint32_t smem[];
+  const int lane = threadIdx.x & 63;
+  const int role = threadIdx.x >> 6;
+  const int half = lane >> 5;
+  const int l32 = lane & 31;
+  const int64_t g = (int64_t)blockIdx.x * 2 + half;
+  const bool valid = g < a.n_groups;
+  const int N = a.n_nodes;
+  const int64_t n = a.n_envs;
+  const int64_t le = g * 32 + l32;
+  const uint64_t ge = a.env_offset + (uint64_t)le;
+  const uint64_t G = ge >> 5;
+  const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+  const bool random_actions = (a.mode & PBN_MODE_RANDOM_ACTIONS) != 0;
+  const size_t plane = (size_t)W * n;
+  const int n_steps = a.n_steps;
+  const int LQ = a.lq;
+  // LDS: table image | S planes [2][32W] | two slots
+  //   slot = m[W][64] | gam[W][64] | rs[W][64] | info[64] | lt[LQ][2][32W]
+  uint32_t* L = smem;
+  const uint32_t* cdf = L;
+  const float* rtab = reinterpret_cast<const float*>(L + a.cdf_len);
+  const uint32_t* htab = L + a.cdf_len + 4 * (N + 1);
+  const uint4* selq = reinterpret_cast<const uint4*>(L + a.sel_off);
+  uint32_t* Sg = smem + a.tab_words + half * 32 * W;   // this half's group
+  uint32_t* slots = smem + a.tab_words + 2 * 32 * W;
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(a.tab);
+    uint4* dst = reinterpret_cast<uint4*>(L);
+    for (int k = threadIdx.x; k < (a.tab_words >> 2); k += blockDim.x) dst[k] = src[CK(k, a.tab_words >> 2, 5)];
+  }
+  uint32_t st[W];
+  uint32_t tt0 = 0, tg0 = 0;
+#pragma unroll
+  for (int w = 0; w < W; ++w) st[w] = 0;
+  if (role == 0 && valid) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) st[w] = a.state[CK((size_t)w * n + le, plane, 1)] & valid_word_mask(N, w);
+    tt0 = a.t[CK(le, n, 2)];
+    tg0 = a.target[CK(le, n, 3)];
+  }
+  uint4 rec_[W][kNodeRecs];
+#pragma unroll
+  for (int r = 0; r < W; ++r) {
+    const int i = l32 + 32 * r;
+    const int ic = i < N ? i : 0;
+#pragma unroll
+    for (int q = 0; q < kNodeRecs; ++q)
+      rec_[r][q] = role != 1 ? a.nrec[CK((size_t)ic * kNodeRecs + q, N * kNodeRecs, 4)] : make_uint4(0, 0, 0, 0);
+  }
+  // wait for the record loads here, once: their first use inside the loop would make the
+  // wait (vmcnt(0), i.e. for every store in flight) part of each iteration
+#pragma unroll
+  for (int r = 0; r < W; ++r) {
+#pragma unroll
+    for (int q = 0; q < kNodeRecs; ++q) asm volatile("" : "+v"(rec_[r][q].x), "+v"(rec_[r][q].z));
+    asm volatile("" : "+v"(rec_[r][0].w), "+v"(rec_[r][1].w));
+  }
+  __syncthreads();
+
+  for (int k = 0; k <= n_steps; ++k) {
+    // keep per-step expansions of loop invariants (threshold digits, leaf selectors) inside
+    // the loop: hoisted they cost ~80 VGPRs, and occupancy is what hides latency here
+#pragma unroll
+    for (int r = 0; r < W; ++r) {
+#pragma unroll
+      for (int q = 0; q < kNodeRecs; ++q) asm volatile("" : "+v"(rec_[r][q].x), "+v"(rec_[r][q].z));
+      asm volatile("" : "+v"(rec_[r][0].w), "+v"(rec_[r][1].w));   // nf, f0
+    }
+    PBN_PSTAMP(k, 0);
+    if (role == 1 && k < n_steps) {
+      // ---- env draws of step k, env `lane`
+      uint32_t* slot = slots + (size_t)(k & 1) * a.slot_words;
+      const uint64_t step = a.step + (uint64_t)k;
+      const uint32_t st_lo = (uint32_t)step;
+      const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
+      const uint32_t ge_lo = (uint32_t)ge;
+      if (valid) {
+        const Word4 E = pbn::philox4x32_10(ge_lo, st_lo, pbn::kStreamEnv << 28, ge_hi, k0, k1);
+        const Word4 P4 = pbn::philox4x32_10(ge_lo, st_lo, pbn::kStreamPert << 28, ge_hi, k0, k1);
+        uint32_t m[W], gam[W], rs[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) { m[w] = 0; gam[w] = 0; rs[w] = 0; }
+        if (random_actions) {
+#pragma unroll
+          for (int q = 0; q < 3; ++q) {   // action a in [0, N]: 0 = no-op, else flip node a-1
+            const int act = (int)(__umul24((E.w >> (10 * q)) & 1023u, (uint32_t)(N + 1)) >> 10);
+            set_bit<W>(m, act - 1, N);
+          }
+#pragma unroll
+          for (int w = 0; w < W; ++w) a.flipmask[CK(k * plane + (size_t)w * n + le, (size_t)n_steps * plane, 8)] = m[w];
+        } else {
+#pragma unroll
+          for (int w = 0; w < W; ++w)
+            m[w] = a.flipmask[CK(k * plane + (size_t)w * n + le, (size_t)n_steps * plane, 6)] & valid_word_mask(N, w);
+        }
+        uint32_t pc = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) pc += __builtin_popcount(m[w]);
+        int g0, g1, g2;
+        if (a.gap_exact) {
+          g0 = gap_of(cdf, a.cdf_len, E.x); g1 = gap_of(cdf, a.cdf_len, E.y); g2 = gap_of(cdf, a.cdf_len, P4.x);
+        } else {
+          g0 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.x);
+          g1 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.y);
+          g2 = gap_est(cdf, a.cdf_len, a.inv_log2q, P4.x);
+        }
+        const int p0 = g0 - 1, p1 = p0 + g1, p2 = p1 + g2;
+        set_bit<W>(gam, p0, N);
+        set_bit<W>(gam, p1, N);
+        set_bit<W>(gam, p2, N);
+        if (p2 < N - 1) {   // rare: a fourth flip is possible (gap k >= 3: PERT call (k-2)>>2, word (k-2)&3)
+          Word4 P = P4;
+          int pos = p2;
+          for (int kk = 3; pos < N - 1; ++kk) {
+            if ((kk & 3) == 2)
+              P = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamPert << 28) | (uint32_t)((kk - 2) >> 2), ge_hi, k0, k1);
+            const int j4 = (kk - 2) & 3;
+            const uint32_t u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
+            pos += a.gap_exact ? gap_of(cdf, a.cdf_len, u) : gap_est(cdf, a.cdf_len, a.inv_log2q, u);
+            set_bit<W>(gam, pos, N);
+          }
+        }
+        bool pert = false;
+#pragma unroll
+        for (int w = 0; w < W; ++w) pert = pert || gam[w] != 0;
+        // autoreset draw (used by wave 0 only if the env's episode ends)
+        uint32_t rt;
+        const uint32_t Rw = E.z;
+        if (a.n_attr >= 1) {
+          const int32_t* att_first = reinterpret_cast<const int32_t*>(L + a.att_off);
+          const uint32_t* att_words = L + a.att_off + a.n_attr + 1;
+          const uint32_t A = (uint32_t)a.n_attr;
+          const uint32_t as = __umul24(Rw & 1023u, A) >> 10;
+          const int st0 = att_first[as];
+          const uint32_t size = (uint32_t)(att_first[as + 1] - st0);
+          const uint32_t idx = __umul24((Rw >> 20) & 4095u, size) >> 12;
+#pragma unroll
+          for (int w = 0; w < W; ++w) rs[w] = att_words[(size_t)(st0 + idx) * W + w];
+          rt = as;
+          if (A >= 2) {
+            rt = __umul24((Rw >> 10) & 1023u, A - 1) >> 10;
+            rt += (rt >= as) ? 1u : 0u;
+          }
+        } else {
+          const Word4 rr = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamReset << 28) | 1u, ge_hi, k0, k1);
+          const uint32_t rw4[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+          for (int w = 0; w < W; ++w) rs[w] = rw4[w] & valid_word_mask(N, w);
+          rt = PBN_NO_TARGET;
+        }
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          slot[w * 64 + lane] = m[w];
+          slot[(W + w) * 64 + lane] = gam[w];
+          slot[(2 * W + w) * 64 + lane] = rs[w];
+        }
+        slot[3 * W * 64 + lane] = rt | (pc << 8) | ((uint32_t)pert << 16);
+      }
+    } else if (role == 2 && k < n_steps) {
+      // ---- selection masks of step k: node l32 + 32r of group g
+      uint32_t* lt_out = slots + (size_t)(k & 1) * a.slot_words + (3 * W + 1) * 64 + half * 32 * W;
+      const uint64_t step = a.step + (uint64_t)k;
+      const uint32_t st_lo = (uint32_t)step;
+      const uint32_t G_hi = (uint32_t)((G >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
+      const uint32_t G_lo = (uint32_t)G;
+#pragma unroll
+      for (int r = 0; r < W; ++r) {
+        const int i = l32 + 32 * r;
+        if (valid && i < N && (a.uni_nf > 1 || (a.uni_nf == 0 && (int)rec_[r][0].w > 1))) {
+          uint32_t dig[16];
+#pragma unroll
+          for (int c = 0; c < CPN; ++c) {
+            const Word4 o = pbn::philox4x32_10(G_lo, st_lo, (pbn::kStreamSel << 28) | (uint32_t)(4 * i + c), G_hi, k0, k1);
+            dig[4 * c + 0] = o.x; dig[4 * c + 1] = o.y; dig[4 * c + 2] = o.z; dig[4 * c + 3] = o.w;
+          }
+          const int nf = (int)rec_[r][0].w;
+          if (a.uni_nf > 0) {
+#pragma unroll
+            for (int q = 0; q < kNodeRecs - 1; ++q) {
+              if (q < a.uni_nf - 1) {
+                uint32_t c = a.uthr[q];
+                asm volatile("" : "+s"(c));
+                lt_out[q * 64 * W + i] = less_than(dig, c, B);
+              }
+            }
+          } else {
+#pragma unroll
+            for (int q = 0; q < kNodeRecs - 1; ++q)
+              if (q < nf - 1) lt_out[q * 64 * W + i] = less_than(dig, rec_[r][q].z, B);
+            const int f0 = (int)rec_[r][1].w;
+            for (int j = kNodeRecs - 1; j < nf - 1; ++j)   // nodes with more than kNodeRecs functions
+              lt_out[j * 64 * W + i] = less_than(dig, a.fcompact[CK(f0 + j, a.n_funcs, 9)].z, B);
+          }
+        }
+      }
+    } else if (role == 0 && k >= 1) {
+      // ---- state part of step t = k - 1
+      const int t = k - 1;
+      const uint32_t* slot = slots + (size_t)(t & 1) * a.slot_words;
+      const uint32_t* lt_in = slot + (3 * W + 1) * 64 + half * 32 * W;
+      uint32_t s1[W], gam[W], rs[W];
+      uint32_t info = 0;
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        s1[w] = st[w] ^ slot[w * 64 + lane];
+        gam[w] = slot[(W + w) * 64 + lane];
+        rs[w] = slot[(2 * W + w) * 64 + lane];
+      }
+      info = slot[3 * W * 64 + lane];
+      if (valid && a.obs) {
+#pragma unroll
+        for (int w = 0; w < W; ++w) a.obs[CK(t * plane + (size_t)w * n + le, (size_t)n_steps * plane, 7)] = st[w];
+      }
+#pragma unroll
+      for (int w = 0; w < W; ++w) Sg[32 * w + l32] = lane_transpose32(s1[w], lane);
+      __builtin_amdgcn_wave_barrier();
+      PBN_PSTAMP_AT(k, 3);
+      uint32_t X[W];
+#pragma unroll
+      for (int r = 0; r < W; ++r) {
+        const int i = l32 + 32 * r;
+        int ii = i < N ? i : 0;
+        asm volatile("" : "+v"(ii));   // selector reads stay in the loop (see above)
+        const int nf = a.uni_nf > 0 ? a.uni_nf : (int)rec_[r][0].w;
+        uint32_t x = 0;
+        if (a.max_nf > kNodeRecs) {   // chain tail of nodes with more than kNodeRecs functions
+          const int f0 = (int)rec_[r][1].w;
+          for (int j = nf - 1; j >= kNodeRecs; --j) {
+            const uint4 rc = a.fcompact[CK(f0 + j, a.n_funcs, 9)];
+            const uint32_t fj = eval_compact(rc.x, rc.y, Sg);
+            x = (j == nf - 1) ? fj : bfi(lt_in[j * 64 * W + ii], fj, x);
+          }
+        }
+        const uint4* sel = selq + ii;
+        const uint32_t* lti = lt_in + ii;
+        switch (a.max_nf) {
+          case 1: x = chain_from_masks<1>(rec_[r], sel, 32 * W, Sg, lti, 64 * W, nf, x); break;
+          case 2: x = chain_from_masks<2>(rec_[r], sel, 32 * W, Sg, lti, 64 * W, nf, x); break;
+          case 3: x = chain_from_masks<3>(rec_[r], sel, 32 * W, Sg, lti, 64 * W, nf, x); break;
+          default: x = chain_from_masks<4>(rec_[r], sel, 32 * W, Sg, lti, 64 * W, nf, x); break;
+        }
+        X[r] = i < N ? x : 0u;
+      }
+      PBN_PSTAMP_AT(k, 12);
+      uint32_t sp[W];
+#pragma unroll
+      for (int w = 0; w < W; ++w) sp[w] = lane_transpose32(X[w], lane);
+      PBN_PSTAMP_AT(k, 13);
+      if (valid) {
+        const bool pert = (info >> 16) & 1u;
+        const uint32_t pc = (info >> 8) & 0xFFu;
+        if (pert) {
+#pragma unroll
+          for (int w = 0; w < W; ++w) sp[w] = s1[w] ^ gam[w];
+        }
+        if (a.final_state) {
+#pragma unroll
+          for (int w = 0; w < W; ++w) a.final_state[CK(t * plane + (size_t)w * n + le, (size_t)n_steps * plane, 10)] = sp[w];
+        }
+        // reward candidates depend only on popcount(flipmask): read them beside the hash
+        const float r_none = rtab[pc], r_wrong = rtab[(N + 1) + pc], r_term = rtab[2 * (N + 1) + pc];
+        int att = -1;
+        if (a.hash_bits > 0) {
+          const int hmask = (1 << a.hash_bits) - 1;
+          const uint32_t* hid = htab + (size_t)W * (hmask + 1);
+          uint32_t h = 0;
+#pragma unroll
+          for (int w = 0; w < W; ++w) h += sp[w] * a.hash_mult[w];
+          h >>= (32 - a.hash_bits);
+          for (int pr = 0; pr < a.hash_probes; ++pr) {
+            const uint32_t slot_i = (h + pr) & hmask;
+            bool eq = true;
+#pragma unroll
+            for (int w = 0; w < W; ++w) eq = eq && (htab[(size_t)w * (hmask + 1) + slot_i] == sp[w]);
+            const uint32_t id = hid[slot_i];
+            if (eq && id != 0xFFFFFFFFu) att = (int)id;
+          }
+        }
+        const bool in_attr = att >= 0;
+        const bool term = in_attr && (uint32_t)att == tg0;
+        const bool wrong = in_attr && !term;
+        int tt = (int)tt0 + 1;
+        tt = tt > 255 ? 255 : tt;
+        const bool trunc = a.horizon > 0 && tt >= a.horizon;
+        a.reward[CK(t * n + le, n_steps * n, 11)] = term ? r_term : (wrong ? r_wrong : r_none);
+        uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) | ((uint32_t)pert << 3);
+        if ((a.mode & PBN_MODE_AUTORESET) && (term || trunc)) {
+#pragma unroll
+          for (int w = 0; w < W; ++w) sp[w] = rs[w];
+          tg0 = info & 0xFFu;
+          tt = 0;
+          fl |= PBN_FLAG_RESET;
+        }
+        a.flags[CK(t * n + le, n_steps * n, 15)] = (uint8_t)fl;
+        tt0 = (uint32_t)tt;
+#pragma unroll
+        for (int w = 0; w < W; ++w) st[w] = sp[w];
+      }
+    }
+    PBN_PSTAMP(k, 1);
+    __syncthreads();
+    PBN_PSTAMP(k, 2);
+  }
+  if (role == 0 && valid) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) a.state_out[CK((size_t)w * n + le, plane, 16)] = st[w];
+    a.t[CK(le, n, 17)] = (uint8_t)tt0;
+    a.target[CK(le, n, 18)] = (uint8_t)tg0;
+  }
+}
+
 // ---------------------------------------------------------------- reset kernel
 template <int W>
 __global__ void __launch_bounds__(256) pbn_reset_kernel(const int32_t* __restrict__ att_start,
@@ -1052,6 +1443,27 @@ StepFn pick_wave(int W, int B) {
   return nullptr;
 }
 
+template <int W>
+StepFn pick_pipe_w(int B) {
+  switch (B) {
+    case 4: return pbn_rollout_pipe<W, 4>;
+    case 8: return pbn_rollout_pipe<W, 8>;
+    case 12: return pbn_rollout_pipe<W, 12>;
+    case 16: return pbn_rollout_pipe<W, 16>;
+  }
+  return nullptr;
+}
+
+StepFn pick_pipe(int W, int B) {
+  switch (W) {
+    case 1: return pick_pipe_w<1>(B);
+    case 2: return pick_pipe_w<2>(B);
+    case 3: return pick_pipe_w<3>(B);
+    case 4: return pick_pipe_w<4>(B);
+  }
+  return nullptr;
+}
+
 using ResetFn = void (*)(const int32_t*, const uint32_t*, int, int, int, uint64_t, uint64_t, uint64_t, int64_t,
                          uint32_t*, uint8_t*, uint8_t*);
 ResetFn pick_reset(int W) {
@@ -1088,6 +1500,10 @@ struct pbn_net {
   StepFn wave = nullptr;        // rollout, loop invariants hoisted (small batches)
   StepFn wave1 = nullptr;       // single step (pbn_step)
   StepFn wave_lean = nullptr;   // rollout with low VGPR count (large batches)
+  StepFn pipe = nullptr;        // rollout, three waves per group (small batches)
+  size_t lds_pipe = 0;
+  int max_nf = 0, lq = 1, slot_words = 0;
+  int64_t roll_pipe_groups = 1 << 30;  // rollouts with at most this many groups use the pipelined kernel
   int force = 0;             // PBN_KERNEL env override: 1 = lane, 2 = wave
   int force_roll = 0;        // PBN_ROLL env override: 1 = hoist, 2 = lean
   int64_t roll_lean_groups = 4096;  // rollouts above this many 32-env groups use the lean variant
@@ -1331,6 +1747,9 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
         if (d->func_threshold[f0 + q] != d->func_threshold[q]) uni = false;
     }
     net->uni_nf = uni ? nf0 : 0;
+    for (int i = 0; i < N; ++i)
+      net->max_nf = std::max(net->max_nf, d->node_func_start[i + 1] - d->node_func_start[i]);
+    net->lq = std::max(net->max_nf - 1, 1);
     for (int q = 0; q < kNodeRecs; ++q) net->uthr[q] = (uni && q < nf0) ? d->func_threshold[q] : 0u;
   }
   net->tab_words = (int)tab.size();
@@ -1344,6 +1763,8 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   net->waves_per_block = (W == 1) ? 2 : 1;
   net->lds_lane = (size_t)net->tab_words * 4 + (size_t)net->waves_per_block * 2 * 32 * W * 64 * 4;
   net->lds_wave = ((size_t)net->tab_words + (size_t)kWavesPerBlock * net->wave_words) * 4;
+  net->slot_words = (3 * W + 1) * 64 + net->lq * 64 * W;
+  net->lds_pipe = ((size_t)net->tab_words + 64 * (size_t)W + 2 * (size_t)net->slot_words) * 4;
   // compact records for the wave kernel: {inputs as bytes, 4-input truth table, threshold, 0}
   std::vector<uint4> fcomp(d->n_funcs);
   for (int f = 0; f < d->n_funcs; ++f) {
@@ -1366,11 +1787,13 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   net->wave = pick_wave<0>(W, d->prob_bits);
   net->wave1 = pick_wave<1>(W, d->prob_bits);
   net->wave_lean = pick_wave<2>(W, d->prob_bits);
+  net->pipe = pick_pipe(W, d->prob_bits);
   net->lane = pick_lane(W);
   net->reset = pick_reset(W);
   if (const char* env = getenv("PBN_ROLL")) {
     if (!strcmp(env, "hoist")) net->force_roll = 1;
     if (!strcmp(env, "lean")) net->force_roll = 2;
+    if (!strcmp(env, "pipe")) net->force_roll = 3;
   }
   if (const char* env = getenv("PBN_KERNEL")) {
     if (!strcmp(env, "lane")) net->force = 1;
@@ -1391,9 +1814,9 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     free_net(net);
     return rc;
   }
-  for (int ti = 0; ti < 4; ++ti) {
-    const StepFn fn = ti == 0 ? net->lane : (ti == 1 ? net->wave : (ti == 2 ? net->wave_lean : net->wave1));
-    const size_t bytes = ti == 0 ? net->lds_lane : net->lds_wave;
+  for (int ti = 0; ti < 5; ++ti) {
+    const StepFn fn = ti == 0 ? net->lane : (ti == 1 ? net->wave : (ti == 2 ? net->wave_lean : (ti == 3 ? net->wave1 : net->pipe)));
+    const size_t bytes = ti == 0 ? net->lds_lane : (ti == 4 ? net->lds_pipe : net->lds_wave);
     if (bytes > 160 * 1024) continue;  // variant unusable for this net; never picked
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)bytes) != hipSuccess) {
@@ -1498,6 +1921,9 @@ int pbn_step(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, in
   a.att_off = net->att_off;
   a.sel_off = net->sel_off;
   a.uni_nf = net->uni_nf;
+  a.max_nf = net->max_nf;
+  a.lq = net->lq;
+  a.slot_words = net->slot_words;
   memcpy(a.uthr, net->uthr, sizeof a.uthr);
   memcpy(a.hash_mult, net->hash_mult, sizeof a.hash_mult);
 #ifdef PBN_STAMPS
@@ -1576,6 +2002,9 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
   a.att_off = net->att_off;
   a.sel_off = net->sel_off;
   a.uni_nf = net->uni_nf;
+  a.max_nf = net->max_nf;
+  a.lq = net->lq;
+  a.slot_words = net->slot_words;
   memcpy(a.uthr, net->uthr, sizeof a.uthr);
   memcpy(a.hash_mult, net->hash_mult, sizeof a.hash_mult);
   a.prob_bits = net->B;
@@ -1590,9 +2019,17 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
 #endif
   // hoisting loop invariants shortens each step's critical path, the lean variant keeps
   // occupancy; lean measured faster at every size (profiles/r01_sweep_pbn28_variants.jsonl)
+  bool pipe = a.n_groups <= net->roll_pipe_groups && net->lds_pipe <= 64 * 1024;
   bool lean = a.n_groups > (int64_t)net->roll_lean_groups;
+  if (net->force_roll) pipe = net->force_roll == 3;
   if (net->force_roll == 1) lean = false;
   if (net->force_roll == 2) lean = true;
+  if (pipe) {   // one block of three waves per pair of groups
+    hipLaunchKernelGGL(net->pipe, dim3((unsigned)((a.n_groups + 1) / 2)), dim3(192), net->lds_pipe,
+                       (hipStream_t)stream, a);
+    HIP_OK(hipGetLastError());
+    return PBN_OK;
+  }
   const unsigned blocks = (unsigned)((a.n_groups + kWavesPerBlock - 1) / kWavesPerBlock);  // one wave per group
   hipLaunchKernelGGL(lean ? net->wave_lean : net->wave, dim3(blocks), dim3(64 * kWavesPerBlock), net->lds_wave,
                      (hipStream_t)stream, a);

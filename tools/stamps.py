@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--network", default="pbn28")
+    ap.add_argument("--pipe", action="store_true", help="pipelined rollout kernel: per-role clocks of iteration 10")
     ap.add_argument("--rollout", type=int, default=0,
                     help="stamp a pbn_rollout launch of this many steps (phases of its last step)")
     args = ap.parse_args()
@@ -62,6 +63,26 @@ def main():
         env.step_flipmask(random_actions=True)
     torch.cuda.synchronize()
     L.pbn_debug_set_stamps(None)
+    if args.pipe:
+        waves = (waves + 1) // 2   # one block per pair of groups
+        t = buf.view(-1, 16)[:waves, :12].cpu().numpy().astype(np.int64).reshape(waves, 3, 4)[:, :, :3]
+        rep = {"envs": args.envs, "blocks": waves, "rollout_steps": args.rollout}
+        for role, name in enumerate(["state", "env draws", "selection"]):
+            work = t[:, role, 1] - t[:, role, 0]
+            wait = t[:, role, 2] - t[:, role, 1]
+            rep[name] = {"work_median": int(np.median(work)), "work_p90": int(np.percentile(work, 90)),
+                         "barrier_wait_median": int(np.median(wait))}
+        full = buf.view(-1, 16)[:waves].cpu().numpy().astype(np.int64)
+        st0 = full[:, 0]
+        rep["state_phases"] = {
+            "slot+transpose": int(np.median(full[:, 3] - st0)),
+            "node eval": int(np.median(full[:, 12] - full[:, 3])),
+            "back-transpose": int(np.median(full[:, 13] - full[:, 12])),
+            "epilogue": int(np.median(full[:, 1] - full[:, 13]))}
+        it = t[:, :, 2].max(axis=1) - t[:, :, 0].min(axis=1)
+        rep["iteration_median"] = int(np.median(it))
+        print(json.dumps(rep, indent=1))
+        return
     t = buf.view(waves, 16)[:, :8].cpu().numpy().astype(np.int64)
     d = np.diff(t, axis=1)
     rep = {"envs": args.envs, "waves": waves, "rollout_steps": args.rollout,

@@ -40,7 +40,7 @@ def main():
                     # empties the allocator cache on entry, unmapping freed >= 20 MB segments)
         for T in args.kernels.split(","):
             os.environ["PBN_KERNEL"] = "wave" if T.startswith("roll") else T
-            os.environ["PBN_ROLL"] = {"rollh": "hoist", "rolll": "lean"}.get(T, "auto")
+            os.environ["PBN_ROLL"] = {"rollh": "hoist", "rolll": "lean", "rollp": "pipe"}.get(T, "auto")
             env = VectorPBNEnv(spec, n, seed=3, keep_final_state=False)
             env.reset()
             with torch.cuda.stream(stream):
