@@ -555,6 +555,13 @@ __device__ __forceinline__ uint32_t eval_func_lds(const uint32_t* __restrict__ f
 //   5. butterfly back to per-env words, reward/termination/autoreset, stores.
 
 // y = a of lane ^ J (J in 1, 2, 4, 8, 16), within 32-lane halves, without LDS
+// ~0 on lanes with bit J of the lane index set, else 0 (a VGPR value: selecting with it
+// needs no exec mask or SGPR pair, which the step loops cannot spare)
+template <int J>
+__device__ __forceinline__ uint32_t lane_bit_mask(int lane) {
+  return 0u - (uint32_t)((lane & J) != 0);
+}
+
 template <int J>
 __device__ __forceinline__ uint32_t xor_lane(uint32_t a, int lane) {
   if constexpr (J == 1) {
@@ -564,20 +571,26 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t a, int lane) {
   } else if constexpr (J == 4) {
     const uint32_t r4 = __builtin_amdgcn_update_dpp(0u, a, 0x124, 0xF, 0xF, false);   // row_ror:4
     const uint32_t r12 = __builtin_amdgcn_update_dpp(0u, a, 0x12C, 0xF, 0xF, false);  // row_ror:12
-    return (lane & 4) ? r4 : r12;
+    return bfi(lane_bit_mask<4>(lane), r4, r12);
   } else if constexpr (J == 8) {
     return __builtin_amdgcn_update_dpp(0u, a, 0x128, 0xF, 0xF, false);  // row_ror:8
   } else {
     const auto r = __builtin_amdgcn_permlane16_swap(a, a, false, false);
-    return (lane & 16) ? r[0] : r[1];
+    return bfi(lane_bit_mask<16>(lane), r[0], r[1]);
   }
 }
 
+// one butterfly stage: lanes without bit J keep their M bits and take the partner's M bits
+// shifted up by J; lanes with bit J take the partner's ~M bits shifted down.  Branch-free: the
+// shift is a per-lane rotate (v_alignbit_b32; wrapped bits land outside the kept field) and
+// the field a per-lane mask.
 template <int J>
 __device__ __forceinline__ uint32_t transpose_step(uint32_t a, int lane) {
   constexpr uint32_t M = J == 16 ? 0x0000FFFFu : (J == 8 ? 0x00FF00FFu : (J == 4 ? 0x0F0F0F0Fu : (J == 2 ? 0x33333333u : 0x55555555u)));
   const uint32_t y = xor_lane<J>(a, lane);
-  return (lane & J) ? bfi(M, y >> J, a) : bfi(M, a, y << J);
+  const uint32_t up = lane_bit_mask<J>(lane);
+  const uint32_t rot = __builtin_amdgcn_alignbit(y, y, (32u - J) ^ (up & ((32u - J) ^ (uint32_t)J)));
+  return bfi(M ^ ~up, rot, a);
 }
 
 // lane k holds row k of a 32x32 bit matrix (per 32-lane half); afterwards lane c holds column c
@@ -1045,7 +1058,7 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
   constexpr int CPN = B / 4;              // selection calls per node
   extern __shared__ uint32_t smem[];
   const int lane = threadIdx.x & 63;
-  const int role = threadIdx.x >> 6;
+  const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar branches
   const int half = lane >> 5;
   const int l32 = lane & 31;
   const int64_t g = (int64_t)blockIdx.x * 2 + half;
@@ -1101,6 +1114,13 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
     for (int q = 0; q < kNodeRecs; ++q) asm volatile("" : "+v"(rec_[r][q].x), "+v"(rec_[r][q].z));
     asm volatile("" : "+v"(rec_[r][0].w), "+v"(rec_[r][1].w));
   }
+  // wave-uniform parameters, re-defined (laundered) every iteration: hoisted out of the step
+  // loop, the conditions built from them occupy SGPR pairs and spill to VGPR lanes
+  uint32_t u_k0 = k0, u_k1 = k1;
+  int u_gx = a.gap_exact, u_na = a.n_attr, u_uni = a.uni_nf, u_mnf = a.max_nf, u_hb = a.hash_bits,
+      u_hp = a.hash_probes, u_hz = a.horizon;
+  uint32_t u_fl = __builtin_amdgcn_readfirstlane((a.obs ? 1u : 0u) | (a.final_state ? 2u : 0u) |
+                                                 (random_actions ? 4u : 0u) | ((a.mode & PBN_MODE_AUTORESET) ? 8u : 0u));
   __syncthreads();
 
   for (int k = 0; k <= n_steps; ++k) {
@@ -1112,6 +1132,8 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
       for (int q = 0; q < kNodeRecs; ++q) asm volatile("" : "+v"(rec_[r][q].x), "+v"(rec_[r][q].z));
       asm volatile("" : "+v"(rec_[r][0].w), "+v"(rec_[r][1].w));   // nf, f0
     }
+    asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_uni), "+s"(u_mnf));
+    asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
     PBN_PSTAMP(k, 0);
     if (role == 1 && k < n_steps) {
       // ---- env draws of step k, env `lane`
@@ -1121,12 +1143,12 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
       const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
       const uint32_t ge_lo = (uint32_t)ge;
       if (valid) {
-        const Word4 E = pbn::philox4x32_10(ge_lo, st_lo, pbn::kStreamEnv << 28, ge_hi, k0, k1);
-        const Word4 P4 = pbn::philox4x32_10(ge_lo, st_lo, pbn::kStreamPert << 28, ge_hi, k0, k1);
+        const Word4 E = pbn::philox4x32_10(ge_lo, st_lo, pbn::kStreamEnv << 28, ge_hi, u_k0, u_k1);
+        const Word4 P4 = pbn::philox4x32_10(ge_lo, st_lo, pbn::kStreamPert << 28, ge_hi, u_k0, u_k1);
         uint32_t m[W], gam[W], rs[W];
 #pragma unroll
         for (int w = 0; w < W; ++w) { m[w] = 0; gam[w] = 0; rs[w] = 0; }
-        if (random_actions) {
+        if (u_fl & 4u) {
 #pragma unroll
           for (int q = 0; q < 3; ++q) {   // action a in [0, N]: 0 = no-op, else flip node a-1
             const int act = (int)(__umul24((E.w >> (10 * q)) & 1023u, (uint32_t)(N + 1)) >> 10);
@@ -1143,7 +1165,7 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
 #pragma unroll
         for (int w = 0; w < W; ++w) pc += __builtin_popcount(m[w]);
         int g0, g1, g2;
-        if (a.gap_exact) {
+        if (u_gx) {
           g0 = gap_of(cdf, a.cdf_len, E.x); g1 = gap_of(cdf, a.cdf_len, E.y); g2 = gap_of(cdf, a.cdf_len, P4.x);
         } else {
           g0 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.x);
@@ -1159,10 +1181,10 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
           int pos = p2;
           for (int kk = 3; pos < N - 1; ++kk) {
             if ((kk & 3) == 2)
-              P = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamPert << 28) | (uint32_t)((kk - 2) >> 2), ge_hi, k0, k1);
+              P = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamPert << 28) | (uint32_t)((kk - 2) >> 2), ge_hi, u_k0, u_k1);
             const int j4 = (kk - 2) & 3;
             const uint32_t u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
-            pos += a.gap_exact ? gap_of(cdf, a.cdf_len, u) : gap_est(cdf, a.cdf_len, a.inv_log2q, u);
+            pos += u_gx ? gap_of(cdf, a.cdf_len, u) : gap_est(cdf, a.cdf_len, a.inv_log2q, u);
             set_bit<W>(gam, pos, N);
           }
         }
@@ -1172,10 +1194,10 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
         // autoreset draw (used by wave 0 only if the env's episode ends)
         uint32_t rt;
         const uint32_t Rw = E.z;
-        if (a.n_attr >= 1) {
+        if (u_na >= 1) {
           const int32_t* att_first = reinterpret_cast<const int32_t*>(L + a.att_off);
-          const uint32_t* att_words = L + a.att_off + a.n_attr + 1;
-          const uint32_t A = (uint32_t)a.n_attr;
+          const uint32_t* att_words = L + a.att_off + u_na + 1;
+          const uint32_t A = (uint32_t)u_na;
           const uint32_t as = __umul24(Rw & 1023u, A) >> 10;
           const int st0 = att_first[as];
           const uint32_t size = (uint32_t)(att_first[as + 1] - st0);
@@ -1188,7 +1210,7 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
             rt += (rt >= as) ? 1u : 0u;
           }
         } else {
-          const Word4 rr = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamReset << 28) | 1u, ge_hi, k0, k1);
+          const Word4 rr = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamReset << 28) | 1u, ge_hi, u_k0, u_k1);
           const uint32_t rw4[4] = {rr.x, rr.y, rr.z, rr.w};
 #pragma unroll
           for (int w = 0; w < W; ++w) rs[w] = rw4[w] & valid_word_mask(N, w);
@@ -1212,18 +1234,18 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
 #pragma unroll
       for (int r = 0; r < W; ++r) {
         const int i = l32 + 32 * r;
-        if (valid && i < N && (a.uni_nf > 1 || (a.uni_nf == 0 && (int)rec_[r][0].w > 1))) {
+        if (valid && i < N && (u_uni > 1 || (u_uni == 0 && (int)rec_[r][0].w > 1))) {
           uint32_t dig[16];
 #pragma unroll
           for (int c = 0; c < CPN; ++c) {
-            const Word4 o = pbn::philox4x32_10(G_lo, st_lo, (pbn::kStreamSel << 28) | (uint32_t)(4 * i + c), G_hi, k0, k1);
+            const Word4 o = pbn::philox4x32_10(G_lo, st_lo, (pbn::kStreamSel << 28) | (uint32_t)(4 * i + c), G_hi, u_k0, u_k1);
             dig[4 * c + 0] = o.x; dig[4 * c + 1] = o.y; dig[4 * c + 2] = o.z; dig[4 * c + 3] = o.w;
           }
           const int nf = (int)rec_[r][0].w;
-          if (a.uni_nf > 0) {
+          if (u_uni > 0) {
 #pragma unroll
             for (int q = 0; q < kNodeRecs - 1; ++q) {
-              if (q < a.uni_nf - 1) {
+              if (q < u_uni - 1) {
                 uint32_t c = a.uthr[q];
                 asm volatile("" : "+s"(c));
                 lt_out[q * 64 * W + i] = less_than(dig, c, B);
@@ -1253,7 +1275,7 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
         rs[w] = slot[(2 * W + w) * 64 + lane];
       }
       info = slot[3 * W * 64 + lane];
-      if (valid && a.obs) {
+      if (valid && (u_fl & 1u)) {
 #pragma unroll
         for (int w = 0; w < W; ++w) a.obs[CK(t * plane + (size_t)w * n + le, (size_t)n_steps * plane, 7)] = st[w];
       }
@@ -1267,9 +1289,9 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
         const int i = l32 + 32 * r;
         int ii = i < N ? i : 0;
         asm volatile("" : "+v"(ii));   // selector reads stay in the loop (see above)
-        const int nf = a.uni_nf > 0 ? a.uni_nf : (int)rec_[r][0].w;
+        const int nf = u_uni > 0 ? u_uni : (int)rec_[r][0].w;
         uint32_t x = 0;
-        if (a.max_nf > kNodeRecs) {   // chain tail of nodes with more than kNodeRecs functions
+        if (u_mnf > kNodeRecs) {   // chain tail of nodes with more than kNodeRecs functions
           const int f0 = (int)rec_[r][1].w;
           for (int j = nf - 1; j >= kNodeRecs; --j) {
             const uint4 rc = a.fcompact[CK(f0 + j, a.n_funcs, 9)];
@@ -1279,7 +1301,7 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
         }
         const uint4* sel = selq + ii;
         const uint32_t* lti = lt_in + ii;
-        switch (a.max_nf) {
+        switch (u_mnf) {
           case 1: x = chain_from_masks<1>(rec_[r], sel, 32 * W, Sg, lti, 64 * W, nf, x); break;
           case 2: x = chain_from_masks<2>(rec_[r], sel, 32 * W, Sg, lti, 64 * W, nf, x); break;
           case 3: x = chain_from_masks<3>(rec_[r], sel, 32 * W, Sg, lti, 64 * W, nf, x); break;
@@ -1292,28 +1314,38 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
 #pragma unroll
       for (int w = 0; w < W; ++w) sp[w] = lane_transpose32(X[w], lane);
       PBN_PSTAMP_AT(k, 13);
-      if (valid) {
+      {
+        // branch-free epilogue (this wave bounds the iteration): only the stores are guarded
         const bool pert = (info >> 16) & 1u;
         const uint32_t pc = (info >> 8) & 0xFFu;
-        if (pert) {
 #pragma unroll
-          for (int w = 0; w < W; ++w) sp[w] = s1[w] ^ gam[w];
-        }
-        if (a.final_state) {
+        for (int w = 0; w < W; ++w) sp[w] = pert ? (s1[w] ^ gam[w]) : sp[w];
+        if (valid && (u_fl & 2u)) {
 #pragma unroll
           for (int w = 0; w < W; ++w) a.final_state[CK(t * plane + (size_t)w * n + le, (size_t)n_steps * plane, 10)] = sp[w];
         }
         // reward candidates depend only on popcount(flipmask): read them beside the hash
         const float r_none = rtab[pc], r_wrong = rtab[(N + 1) + pc], r_term = rtab[2 * (N + 1) + pc];
         int att = -1;
-        if (a.hash_bits > 0) {
-          const int hmask = (1 << a.hash_bits) - 1;
+        if (u_hb > 0) {
+          const int hmask = (1 << u_hb) - 1;
           const uint32_t* hid = htab + (size_t)W * (hmask + 1);
           uint32_t h = 0;
 #pragma unroll
           for (int w = 0; w < W; ++w) h += sp[w] * a.hash_mult[w];
-          h >>= (32 - a.hash_bits);
-          for (int pr = 0; pr < a.hash_probes; ++pr) {
+          h >>= (32 - u_hb);
+          // keys are unique, so probe order does not matter: the first four probes are read
+          // side by side and combined without branches
+#pragma unroll
+          for (int pr = 0; pr < 4; ++pr) {
+            const uint32_t slot_i = (h + pr) & hmask;
+            uint32_t eq = pr < u_hp ? 1u : 0u;
+#pragma unroll
+            for (int w = 0; w < W; ++w) eq &= (htab[(size_t)w * (hmask + 1) + slot_i] == sp[w]) ? 1u : 0u;
+            const uint32_t id = hid[slot_i];
+            att = (eq != 0u && id != 0xFFFFFFFFu) ? (int)id : att;
+          }
+          for (int pr = 4; pr < u_hp; ++pr) {
             const uint32_t slot_i = (h + pr) & hmask;
             bool eq = true;
 #pragma unroll
@@ -1327,20 +1359,18 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
         const bool wrong = in_attr && !term;
         int tt = (int)tt0 + 1;
         tt = tt > 255 ? 255 : tt;
-        const bool trunc = a.horizon > 0 && tt >= a.horizon;
-        a.reward[CK(t * n + le, n_steps * n, 11)] = term ? r_term : (wrong ? r_wrong : r_none);
-        uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) | ((uint32_t)pert << 3);
-        if ((a.mode & PBN_MODE_AUTORESET) && (term || trunc)) {
-#pragma unroll
-          for (int w = 0; w < W; ++w) sp[w] = rs[w];
-          tg0 = info & 0xFFu;
-          tt = 0;
-          fl |= PBN_FLAG_RESET;
+        const bool trunc = u_hz > 0 && tt >= u_hz;
+        const bool reset = (u_fl & 8u) && (term || trunc);
+        const uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) |
+                            ((uint32_t)pert << 3) | ((uint32_t)reset << 4);
+        if (valid) {
+          a.reward[CK(t * n + le, n_steps * n, 11)] = term ? r_term : (wrong ? r_wrong : r_none);
+          a.flags[CK(t * n + le, n_steps * n, 15)] = (uint8_t)fl;
         }
-        a.flags[CK(t * n + le, n_steps * n, 15)] = (uint8_t)fl;
-        tt0 = (uint32_t)tt;
+        tg0 = reset ? (info & 0xFFu) : tg0;
+        tt0 = reset ? 0u : (uint32_t)tt;
 #pragma unroll
-        for (int w = 0; w < W; ++w) st[w] = sp[w];
+        for (int w = 0; w < W; ++w) st[w] = reset ? rs[w] : sp[w];
       }
     }
     PBN_PSTAMP(k, 1);
