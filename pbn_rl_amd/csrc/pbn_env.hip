@@ -640,8 +640,11 @@ __device__ __forceinline__ int gap_est(const uint32_t* __restrict__ cdf, int len
   float est = floorf(l2 * inv_log2q) + 1.0f;
   est = fminf(fmaxf(est, 1.0f), (float)len);
   int g = (int)est;
-  const uint32_t hi = cdf[g - 1];                       // C[g-1]
-  const uint32_t lo = g >= 2 ? cdf[g - 2] : 0u;         // C[g-2]
+  // C[g-2] and C[g-1] as one pair of adjacent reads (no branch: g == 1 reads C[0], C[1])
+  const int base = g >= 2 ? g - 2 : 0;
+  const uint32_t c0 = cdf[base], c1 = cdf[base + 1];
+  const uint32_t hi = g >= 2 ? c1 : c0;                 // C[g-1]
+  const uint32_t lo = g >= 2 ? c0 : 0u;                 // C[g-2]
   g += (u >= hi) ? 1 : 0;
   g -= (g >= 2 && u < lo) ? 1 : 0;
   return g;
@@ -1334,18 +1337,17 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
 #pragma unroll
           for (int w = 0; w < W; ++w) h += sp[w] * a.hash_mult[w];
           h >>= (32 - u_hb);
-          // keys are unique, so probe order does not matter: the first four probes are read
-          // side by side and combined without branches
-#pragma unroll
-          for (int pr = 0; pr < 4; ++pr) {
-            const uint32_t slot_i = (h + pr) & hmask;
-            uint32_t eq = pr < u_hp ? 1u : 0u;
+          // the table is usually collision-free (one probe); keys are unique, so probe order
+          // does not matter
+          {
+            const uint32_t slot_i = h & hmask;
+            uint32_t eq = 1u;
 #pragma unroll
             for (int w = 0; w < W; ++w) eq &= (htab[(size_t)w * (hmask + 1) + slot_i] == sp[w]) ? 1u : 0u;
             const uint32_t id = hid[slot_i];
             att = (eq != 0u && id != 0xFFFFFFFFu) ? (int)id : att;
           }
-          for (int pr = 4; pr < u_hp; ++pr) {
+          for (int pr = 1; pr < u_hp; ++pr) {
             const uint32_t slot_i = (h + pr) & hmask;
             bool eq = true;
 #pragma unroll
@@ -1580,6 +1582,8 @@ bool build_hash(const std::vector<std::vector<uint32_t>>& states, const std::vec
     rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
     return (uint32_t)(rng >> 11) | 1u;
   };
+  // prefer a collision-free table (one probe per lookup) up to 16x the minimal size
+  const int min_bits = bits;
   for (; bits <= kMaxHashBits; ++bits) {
     const uint32_t size = 1u << bits, mask = size - 1;
     int best_probes = 1 << 30;
@@ -1604,7 +1608,8 @@ bool build_hash(const std::vector<std::vector<uint32_t>>& states, const std::vec
       }
       if (best_probes == 1) break;
     }
-    if (best_probes <= 4 || bits == kMaxHashBits) {
+    const bool accept = best_probes == 1 || (best_probes <= 4 && bits >= std::min(min_bits + 4, kMaxHashBits));
+    if (accept || bits == kMaxHashBits) {
       image->assign((size_t)(W + 1) * size, 0u);
       std::vector<int> used(size, 0);
       for (uint32_t s = 0; s < size; ++s) (*image)[(size_t)W * size + s] = 0xFFFFFFFFu;
