@@ -196,7 +196,7 @@ def main():
         W = spec.words
         if rollout_mode:
             bytes_launch = env.n_alloc * rollout_bytes_per_env(W, chunk)
-            kernel = "pbn_step_wave (rollout, %d steps/launch)" % chunk
+            kernel = "pbn_rollout_pipe (rollout, %d steps/launch)" % chunk
         else:
             bytes_launch = env.n_alloc * algorithmic_bytes_per_env(W)
             kernel = "pbn_step_wave (single step)"

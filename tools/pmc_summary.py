@@ -12,11 +12,11 @@ import json
 import os
 
 
-def mean_counter(path, counter, kernel="pbn_step_wave"):
+def mean_counter(path, counter, kernel="pbn_"):
     vals, name = [], None
     with open(path) as f:
         for r in csv.DictReader(f):
-            if r["Counter_Name"] == counter and kernel in r["Kernel_Name"]:
+            if r["Counter_Name"] == counter and kernel in r["Kernel_Name"] and "reset" not in r["Kernel_Name"]:
                 vals.append(float(r["Counter_Value"]))
                 name = r["Kernel_Name"]
     return sum(vals) / len(vals), len(vals), name
