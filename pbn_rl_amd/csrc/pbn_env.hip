@@ -88,7 +88,8 @@ struct StepArgs {
   int n_states;      // attractor states (bounds of att_states; checked builds)
   int att_off;       // LDS image offset of attractor start[A+1] | states[S][W] (wave kernel)
   int sel_off;       // LDS image offset of the leaf selectors, uint4 [kNodeRecs][2][32W] (wave kernel)
-  int uni_nf;        // > 0: every node has uni_nf functions with thresholds uthr (wave-uniform)
+  int n_cls;         // 1..4: the first kNodeRecs thresholds of every node take one of n_cls values
+                     // uthr[0..n_cls) (record .y = class index); 0: per-node thresholds
   uint32_t uthr[kNodeRecs];
   int max_nf;        // largest function count of a node
   int lq;            // pipelined rollout: selection masks per node in a slot (max(max_nf - 1, 1))
@@ -650,6 +651,26 @@ __device__ __forceinline__ int gap_est(const uint32_t* __restrict__ cdf, int len
   return g;
 }
 
+// (u < c_q) for the wave-uniform threshold classes: one bit-sliced comparison per class with
+// SGPR digit masks, then a per-lane pick by class index (record .y)
+template <int B>
+__device__ __forceinline__ void class_masks(const uint32_t (&dig)[16], const uint32_t (&uthr)[kNodeRecs], int n_cls,
+                                            uint32_t (&ltc)[kNodeRecs]) {
+#pragma unroll
+  for (int v = 0; v < kNodeRecs; ++v) {
+    ltc[v] = 0;
+    if (v < n_cls) {
+      uint32_t c = uthr[v];
+      asm volatile("" : "+s"(c));   // digits re-extracted per step on the SALU (hoisted: SGPR spills)
+      ltc[v] = less_than(dig, c, B);
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t pick_class(const uint32_t (&ltc)[kNodeRecs], uint32_t cls) {
+  return cls == 0 ? ltc[0] : (cls == 1 ? ltc[1] : (cls == 2 ? ltc[2] : ltc[3]));
+}
+
 // Lower lanes receive the upper lanes' four words (upper lanes end with junk): per pair of
 // words two v_permlane32_swap and no copies.  swap(X, Y) moves X's upper half into Y's
 // lower half; swap(Y', X') then moves Y's upper half into X''s lower half.
@@ -746,7 +767,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
     for (int r = 0; r < W; ++r) {
 #pragma unroll
       for (int q = 0; q < kNodeRecs; ++q) {
-        asm volatile("" : "+v"(rec_[r][q].x), "+v"(rec_[r][q].y), "+v"(rec_[r][q].z));
+        asm volatile("" : "+v"(rec_[r][q].x), "+v"(rec_[r][q].z));
       }
     }
   }
@@ -876,18 +897,18 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
     const int i = l32 + 32 * r;
     const int ii = lo && i < N ? i : 0;   // other lanes evaluate node 0 and discard it
     uint32_t x = 0;
-    if (a.uni_nf > 0) {
-      // every node has uni_nf <= kNodeRecs functions with the same thresholds: the
-      // threshold digits are wave-uniform (SGPR operands of the comparison)
-      const int K = a.uni_nf;
+    if (a.n_cls > 0 && a.max_nf <= kNodeRecs) {
+      // thresholds from a few wave-uniform classes (all kaban networks: 1/3, 2/3)
+      const int nf = (int)rec_[r][0].w;
+      uint32_t ltc[kNodeRecs];
+      class_masks<B>(dig[r], a.uthr, a.n_cls, ltc);
 #pragma unroll
       for (int q = kNodeRecs - 1; q >= 0; --q) {
-        if (q < K) {
-          const uint32_t fj = eval_sel(rec_[r][q].x, selq[(2 * q) * 32 * W + ii], selq[(2 * q + 1) * 32 * W + ii], S);
-          uint32_t c = a.uthr[q];
-          asm volatile("" : "+s"(c));   // digits re-extracted per step on the SALU: hoisting them
-                                        // out of the step loop spills SGPRs to VGPR lanes
-          x = (q == K - 1) ? fj : bfi(less_than(dig[r], c, B), fj, x);
+        if (q < a.max_nf) {
+          const uint4 rc = rec_[r][q];
+          const uint32_t fj = eval_sel(rc.x, selq[(2 * q) * 32 * W + ii], selq[(2 * q + 1) * 32 * W + ii], S);
+          const uint32_t y = (q == nf - 1) ? fj : bfi(pick_class(ltc, rc.y), fj, x);
+          x = (q < nf) ? y : x;
         }
       }
     } else {
@@ -1120,7 +1141,7 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
   // wave-uniform parameters, re-defined (laundered) every iteration: hoisted out of the step
   // loop, the conditions built from them occupy SGPR pairs and spill to VGPR lanes
   uint32_t u_k0 = k0, u_k1 = k1;
-  int u_gx = a.gap_exact, u_na = a.n_attr, u_uni = a.uni_nf, u_mnf = a.max_nf, u_hb = a.hash_bits,
+  int u_gx = a.gap_exact, u_na = a.n_attr,  u_mnf = a.max_nf, u_hb = a.hash_bits,
       u_hp = a.hash_probes, u_hz = a.horizon;
   uint32_t u_fl = __builtin_amdgcn_readfirstlane((a.obs ? 1u : 0u) | (a.final_state ? 2u : 0u) |
                                                  (random_actions ? 4u : 0u) | ((a.mode & PBN_MODE_AUTORESET) ? 8u : 0u));
@@ -1135,7 +1156,7 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
       for (int q = 0; q < kNodeRecs; ++q) asm volatile("" : "+v"(rec_[r][q].x), "+v"(rec_[r][q].z));
       asm volatile("" : "+v"(rec_[r][0].w), "+v"(rec_[r][1].w));   // nf, f0
     }
-    asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_uni), "+s"(u_mnf));
+    asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
     asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
     PBN_PSTAMP(k, 0);
     if (role == 1 && k < n_steps) {
@@ -1237,7 +1258,7 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
 #pragma unroll
       for (int r = 0; r < W; ++r) {
         const int i = l32 + 32 * r;
-        if (valid && i < N && (u_uni > 1 || (u_uni == 0 && (int)rec_[r][0].w > 1))) {
+        if (valid && i < N && (int)rec_[r][0].w > 1) {
           uint32_t dig[16];
 #pragma unroll
           for (int c = 0; c < CPN; ++c) {
@@ -1245,16 +1266,7 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
             dig[4 * c + 0] = o.x; dig[4 * c + 1] = o.y; dig[4 * c + 2] = o.z; dig[4 * c + 3] = o.w;
           }
           const int nf = (int)rec_[r][0].w;
-          if (u_uni > 0) {
-#pragma unroll
-            for (int q = 0; q < kNodeRecs - 1; ++q) {
-              if (q < u_uni - 1) {
-                uint32_t c = a.uthr[q];
-                asm volatile("" : "+s"(c));
-                lt_out[q * 64 * W + i] = less_than(dig, c, B);
-              }
-            }
-          } else {
+          {   // per-lane thresholds: the selection wave has slack, the SGPRs are scarce
 #pragma unroll
             for (int q = 0; q < kNodeRecs - 1; ++q)
               if (q < nf - 1) lt_out[q * 64 * W + i] = less_than(dig, rec_[r][q].z, B);
@@ -1292,7 +1304,7 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
         const int i = l32 + 32 * r;
         int ii = i < N ? i : 0;
         asm volatile("" : "+v"(ii));   // selector reads stay in the loop (see above)
-        const int nf = u_uni > 0 ? u_uni : (int)rec_[r][0].w;
+        const int nf = (int)rec_[r][0].w;
         uint32_t x = 0;
         if (u_mnf > kNodeRecs) {   // chain tail of nodes with more than kNodeRecs functions
           const int f0 = (int)rec_[r][1].w;
@@ -1518,7 +1530,7 @@ struct pbn_net {
   int wave_words = 0;
   int att_off = 0;
   int sel_off = 0;
-  int uni_nf = 0;
+  int n_cls = 0;
   uint32_t uthr[kNodeRecs] = {0, 0, 0, 0};
   int gap_exact = 1;
   float inv_log2q = 0.f;
@@ -1771,21 +1783,30 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     }
     tab.insert(tab.end(), sel.begin(), sel.end());
   }
-  // wave-uniform thresholds when every node has the same function count and thresholds
+  // threshold classes: the distinct values among the first kNodeRecs thresholds of all nodes;
+  // with at most kNodeRecs of them the kernels compare against wave-uniform digits
+  std::vector<uint32_t> cls_of((size_t)d->n_funcs, 0u);
   {
-    const int nf0 = d->node_func_start[1] - d->node_func_start[0];
-    bool uni = nf0 >= 1 && nf0 <= kNodeRecs;
-    for (int i = 1; uni && i < N; ++i) {
-      const int f0 = d->node_func_start[i];
-      if (d->node_func_start[i + 1] - f0 != nf0) uni = false;
-      for (int q = 0; uni && q < nf0; ++q)
-        if (d->func_threshold[f0 + q] != d->func_threshold[q]) uni = false;
+    std::vector<uint32_t> vals;
+    bool ok = true;
+    for (int i = 0; i < N && ok; ++i) {
+      const int f0 = d->node_func_start[i], nf = d->node_func_start[i + 1] - f0;
+      for (int q = 0; q < kNodeRecs && q < nf - 1; ++q) {
+        const uint32_t c = d->func_threshold[f0 + q];
+        auto it = std::find(vals.begin(), vals.end(), c);
+        if (it == vals.end()) {
+          if ((int)vals.size() == kNodeRecs) { ok = false; break; }
+          vals.push_back(c);
+          it = vals.end() - 1;
+        }
+        cls_of[f0 + q] = (uint32_t)(it - vals.begin());
+      }
     }
-    net->uni_nf = uni ? nf0 : 0;
+    net->n_cls = ok ? (int)vals.size() : 0;
+    for (int q = 0; q < kNodeRecs; ++q) net->uthr[q] = (ok && q < (int)vals.size()) ? vals[q] : 0u;
     for (int i = 0; i < N; ++i)
       net->max_nf = std::max(net->max_nf, d->node_func_start[i + 1] - d->node_func_start[i]);
     net->lq = std::max(net->max_nf - 1, 1);
-    for (int q = 0; q < kNodeRecs; ++q) net->uthr[q] = (uni && q < nf0) ? d->func_threshold[q] : 0u;
   }
   net->tab_words = (int)tab.size();
   net->n_funcs = d->n_funcs;
@@ -1815,7 +1836,10 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   std::vector<uint4> nrec((size_t)N * kNodeRecs, make_uint4(0, 0, 0, 0));
   for (int i = 0; i < N; ++i) {
     const int f0 = d->node_func_start[i], nf = d->node_func_start[i + 1] - f0;
-    for (int q = 0; q < kNodeRecs && q < nf; ++q) nrec[(size_t)i * kNodeRecs + q] = fcomp[f0 + q];
+    for (int q = 0; q < kNodeRecs && q < nf; ++q) {
+      nrec[(size_t)i * kNodeRecs + q] = fcomp[f0 + q];
+      nrec[(size_t)i * kNodeRecs + q].y = cls_of[f0 + q];   // threshold class (the table lives in the selectors)
+    }
     nrec[(size_t)i * kNodeRecs + 0].w = (uint32_t)nf;
     nrec[(size_t)i * kNodeRecs + 1].w = (uint32_t)f0;
   }
@@ -1955,7 +1979,7 @@ int pbn_step(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, in
   a.n_states = net->n_states;
   a.att_off = net->att_off;
   a.sel_off = net->sel_off;
-  a.uni_nf = net->uni_nf;
+  a.n_cls = net->n_cls;
   a.max_nf = net->max_nf;
   a.lq = net->lq;
   a.slot_words = net->slot_words;
@@ -2036,7 +2060,7 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
   a.n_states = net->n_states;
   a.att_off = net->att_off;
   a.sel_off = net->sel_off;
-  a.uni_nf = net->uni_nf;
+  a.n_cls = net->n_cls;
   a.max_nf = net->max_nf;
   a.lq = net->lq;
   a.slot_words = net->slot_words;
