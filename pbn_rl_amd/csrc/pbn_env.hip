@@ -41,7 +41,7 @@ constexpr int kNodeRecs = 4;       // compact records prefetched per node by the
 constexpr int kWavesPerBlock = 4;  // wave kernel: waves (32-env groups) per block, sharing one LDS table image
 constexpr int kMaxHashBits = 12;
 
-struct FuncRec {
+struct FuncRec {   // host-side function record (validation, leaf tables for the selectors)
   uint32_t in[4];      // input node index per mux level (padded with 0)
   uint32_t leaf[16];   // leaf[m] = d_m (x0 mask), leaf[8+m] = beta_m
   uint32_t thr;        // cumulative selection threshold c_f (prob_bits units)
@@ -50,8 +50,6 @@ struct FuncRec {
 static_assert(sizeof(FuncRec) == kFuncRecWords * 4, "FuncRec layout");
 
 struct StepArgs {
-  const FuncRec* funcs;
-  const int32_t* node_fs;       // [N+1]
   const uint32_t* tab;          // packed LDS image (cdf | reward | hash)
   const int32_t* att_start;     // [A+1]
   const uint32_t* att_states;   // [S*W]
@@ -165,23 +163,6 @@ __device__ __forceinline__ int gap_of(const uint32_t* __restrict__ cdf, int len,
   return cnt + 1;
 }
 
-__device__ __forceinline__ uint32_t eval_func(const FuncRec* __restrict__ fr,
-                                              const uint32_t* __restrict__ S) {
-  const uint32_t x0 = S[fr->in[0] * 64];
-  const uint32_t x1 = S[fr->in[1] * 64];
-  const uint32_t x2 = S[fr->in[2] * 64];
-  const uint32_t x3 = S[fr->in[3] * 64];
-  uint32_t v[8];
-#pragma unroll
-  for (int m = 0; m < 8; ++m) v[m] = (x0 & fr->leaf[m]) ^ fr->leaf[8 + m];
-  uint32_t w[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) w[q] = bfi(x1, v[2 * q + 1], v[2 * q]);
-  const uint32_t y0 = bfi(x2, w[1], w[0]);
-  const uint32_t y1 = bfi(x2, w[3], w[2]);
-  return bfi(x3, y1, y0);
-}
-
 // lanes-of-32-envs bit mask of (u < c), u = digits dig[0..B) MSB first (B = prob_bits).
 // From the least significant digit up: lt' = c_d ? (u_d ? lt : 1) : (u_d ? 0 : lt),
 // one v_bitop3_b32 per digit over (u_d, lt, C_d) with LUT 0x8E.
@@ -197,353 +178,10 @@ __device__ __forceinline__ uint32_t less_than(const uint32_t (&dig)[16], uint32_
   return lt;
 }
 
-// ------------------------------------------------- step kernel, one thread per group
-template <int W>
-__global__ void __launch_bounds__(128) pbn_step_lane(StepArgs a) {
-  extern __shared__ uint32_t smem[];
-  for (int i = threadIdx.x; i < a.tab_words; i += blockDim.x) smem[i] = a.tab[i];
-  __syncthreads();
-
-  const int64_t grp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (grp >= a.n_groups) return;
-
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const uint32_t* cdf = smem;
-  const float* rtab = reinterpret_cast<const float*>(smem + a.cdf_len);
-  const uint32_t* htab = smem + a.cdf_len + 4 * (a.n_nodes + 1);
-  uint32_t* S = smem + a.tab_words + wave * (2 * 32 * W * 64) + lane;  // plane p at S[p*64]
-  uint32_t* R = S + 32 * W * 64;
-
-  const int N = a.n_nodes;
-  const int64_t n = a.n_envs;
-  const int64_t e0 = grp * 32;                       // first local env of the group
-  const uint64_t ge0 = a.env_offset + (uint64_t)e0;  // first global env id
-  const uint64_t G = ge0 >> 5;                       // global group id
-  const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
-  const uint32_t st_lo = (uint32_t)a.step;
-  const uint32_t st_hi = (uint32_t)((a.step >> 32) & 0xFFFFu) << 16;
-  const bool random_actions = (a.mode & PBN_MODE_RANDOM_ACTIONS) != 0;
-
-  // ---- A. load the group's state words, t, target
-  uint32_t s1[W][32];
-#pragma unroll
-  for (int w = 0; w < W; ++w) {
-    const uint4* p = reinterpret_cast<const uint4*>(a.state + (size_t)w * n + e0);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const uint4 v = p[q];
-      s1[w][4 * q + 0] = v.x;
-      s1[w][4 * q + 1] = v.y;
-      s1[w][4 * q + 2] = v.z;
-      s1[w][4 * q + 3] = v.w;
-    }
-  }
-  uint32_t tpk[8], tgpk[8];
-  {
-    const uint4* pt = reinterpret_cast<const uint4*>(a.t + e0);
-    const uint4* pg = reinterpret_cast<const uint4*>(a.target + e0);
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const uint4 v = pt[q], g = pg[q];
-      tpk[4 * q + 0] = v.x; tpk[4 * q + 1] = v.y; tpk[4 * q + 2] = v.z; tpk[4 * q + 3] = v.w;
-      tgpk[4 * q + 0] = g.x; tgpk[4 * q + 1] = g.y; tgpk[4 * q + 2] = g.z; tgpk[4 * q + 3] = g.w;
-    }
-  }
-
-  // ---- B. per env: interventions, perturbation gaps 0/1, reset word
-  uint32_t gam[W][32];
-  uint32_t rword[32];
-  uint32_t pcpk[8];      // popcount(flipmask) per env, packed bytes
-  uint32_t pmask = 0;    // bit b: env b perturbed
-  uint32_t pend = 0;     // bit b: env b needs gap draws beyond E1
-#pragma unroll
-  for (int q = 0; q < 8; ++q) pcpk[q] = 0;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    uint32_t mq[W][4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int b = 4 * q + r;
-      const uint64_t ge = ge0 + (uint64_t)b;
-      const Word4 E = pbn::philox4x32_10((uint32_t)ge, st_lo, pbn::kStreamEnv << 28,
-                                         (uint32_t)((ge >> 32) & 0xFFFFu) | st_hi, k0, k1);
-      uint32_t m[W];
-#pragma unroll
-      for (int w = 0; w < W; ++w) m[w] = 0;
-      if (random_actions) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const uint32_t act = (((E.w >> (10 * k)) & 1023u) * (uint32_t)(N + 1)) >> 10;
-          if (act > 0) {
-#pragma unroll
-            for (int w = 0; w < W; ++w)
-              if ((int)((act - 1) >> 5) == w) m[w] |= 1u << ((act - 1) & 31);
-          }
-        }
-      } else {
-#pragma unroll
-        for (int w = 0; w < W; ++w)
-          m[w] = a.flipmask[(size_t)w * n + e0 + b] & valid_word_mask(N, w);
-      }
-      uint32_t pc = 0;
-#pragma unroll
-      for (int w = 0; w < W; ++w) {
-        mq[w][r] = m[w];
-        pc += __builtin_popcount(m[w]);
-        s1[w][b] = (s1[w][b] & valid_word_mask(N, w)) ^ m[w];
-        gam[w][b] = 0;
-      }
-      pcpk[q] |= pc << (8 * r);
-      // perturbation: positions are partial sums of geometric gaps
-      int pos = gap_of(cdf, a.cdf_len, E.x) - 1;
-      if (pos < N) {
-#pragma unroll
-        for (int w = 0; w < W; ++w)
-          if ((pos >> 5) == w) gam[w][b] |= 1u << (pos & 31);
-        pmask |= 1u << b;
-        if (pos < N - 1) {
-          pos += gap_of(cdf, a.cdf_len, E.y);
-          if (pos < N) {
-#pragma unroll
-            for (int w = 0; w < W; ++w)
-              if ((pos >> 5) == w) gam[w][b] |= 1u << (pos & 31);
-            if (pos < N - 1) pend |= 1u << b;
-          }
-        }
-      }
-      rword[b] = E.z;
-    }
-    if (random_actions) {
-#pragma unroll
-      for (int w = 0; w < W; ++w)
-        reinterpret_cast<uint4*>(a.flipmask + (size_t)w * n + e0)[q] =
-            make_uint4(mq[w][0], mq[w][1], mq[w][2], mq[w][3]);
-    }
-  }
-  // rare: envs with >= 2 flips so far that may flip more nodes
-  while (__any(pend != 0)) {
-    if (pend) {
-      const int b = __builtin_ctz(pend);
-      pend &= pend - 1;
-      uint32_t g[W];
-      int pos = -1;
-#pragma unroll
-      for (int bb = 0; bb < 32; ++bb) {
-        if (bb == b) {
-#pragma unroll
-          for (int w = 0; w < W; ++w) g[w] = gam[w][bb];
-        }
-      }
-#pragma unroll
-      for (int w = 0; w < W; ++w)
-        if (g[w]) pos = 32 * w + 31 - __builtin_clz(g[w]);
-      const uint64_t ge = ge0 + (uint64_t)b;
-      uint32_t P[4] = {0, 0, 0, 0};
-      for (int k = 0; pos < N - 1; ++k) {
-        if ((k & 3) == 0) {
-          const Word4 pw = pbn::philox4x32_10(
-              (uint32_t)ge, st_lo, (pbn::kStreamPert << 28) | (uint32_t)(k >> 2),
-              (uint32_t)((ge >> 32) & 0xFFFFu) | st_hi, k0, k1);
-          P[0] = pw.x; P[1] = pw.y; P[2] = pw.z; P[3] = pw.w;
-        }
-        pos += gap_of(cdf, a.cdf_len, P[k & 3]);
-        if (pos >= N) break;
-#pragma unroll
-        for (int w = 0; w < W; ++w)
-          if ((pos >> 5) == w) g[w] |= 1u << (pos & 31);
-      }
-#pragma unroll
-      for (int bb = 0; bb < 32; ++bb) {
-        if (bb == b) {
-#pragma unroll
-          for (int w = 0; w < W; ++w) gam[w][bb] = g[w];
-        }
-      }
-    }
-  }
-
-  // ---- C. bit-slice: S = planes of s1, R = planes of s1 ^ gamma
-#pragma unroll
-  for (int w = 0; w < W; ++w) {
-    pbn::transpose32(s1[w]);
-    pbn::transpose32(gam[w]);
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-      S[(32 * w + k) * 64] = s1[w][k];
-      R[(32 * w + k) * 64] = s1[w][k] ^ gam[w][k];
-    }
-  }
-
-  // ---- D. node loop: selection digits, function evaluation, mux
-  for (int i = 0; i < N; ++i) {
-    const int f0 = a.node_fs[i];
-    const int nf = a.node_fs[i + 1] - f0;
-    uint32_t dig[16];
-    if (nf > 1) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        if (4 * c >= a.prob_bits) break;
-        const Word4 d = pbn::philox4x32_10((uint32_t)G, st_lo,
-                                           (pbn::kStreamSel << 28) | (uint32_t)(4 * i + c),
-                                           (uint32_t)((G >> 32) & 0xFFFFu) | st_hi, k0, k1);
-        dig[4 * c + 0] = d.x;
-        dig[4 * c + 1] = d.y;
-        dig[4 * c + 2] = d.z;
-        dig[4 * c + 3] = d.w;
-      }
-    }
-    uint32_t x = eval_func(a.funcs + f0 + nf - 1, S);
-    for (int j = nf - 2; j >= 0; --j) {
-      const FuncRec* fr = a.funcs + f0 + j;
-      const uint32_t fj = eval_func(fr, S);
-      const uint32_t lt = less_than(dig, fr->thr, a.prob_bits);
-      x = bfi(lt, fj, x);
-    }
-    R[i * 64] = bfi(pmask, R[i * 64], x);
-  }
-
-  // ---- E. back to per-env words
-  uint32_t sp[W][32];
-#pragma unroll
-  for (int w = 0; w < W; ++w) {
-#pragma unroll
-    for (int k = 0; k < 32; ++k) sp[w][k] = R[(32 * w + k) * 64];
-    pbn::transpose32(sp[w]);
-  }
-  if (a.final_state) {
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
-      uint4* p = reinterpret_cast<uint4*>(a.final_state + (size_t)w * n + e0);
-#pragma unroll
-      for (int q = 0; q < 8; ++q)
-        p[q] = make_uint4(sp[w][4 * q], sp[w][4 * q + 1], sp[w][4 * q + 2], sp[w][4 * q + 3]);
-    }
-  }
-
-  // ---- F. reward, termination, autoreset
-  const int hmask = (1 << a.hash_bits) - 1;
-  const uint32_t* hid = htab + (size_t)W * (hmask + 1);
-  uint32_t flpk[8], topk[8];
-  bool any_reset = false;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    float rq[4];
-    uint32_t fl4 = 0, t4 = 0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int b = 4 * q + r;
-      const uint32_t tgt = (tgpk[q] >> (8 * r)) & 0xFFu;
-      int att = -1;
-      if (a.hash_bits > 0) {
-        uint32_t h = 0;
-#pragma unroll
-        for (int w = 0; w < W; ++w) h += sp[w][b] * a.hash_mult[w];
-        h >>= (32 - a.hash_bits);
-        for (int pr = 0; pr < a.hash_probes; ++pr) {
-          const uint32_t slot = (h + pr) & hmask;
-          bool eq = true;
-#pragma unroll
-          for (int w = 0; w < W; ++w) eq = eq && (htab[(size_t)w * (hmask + 1) + slot] == sp[w][b]);
-          const uint32_t id = hid[slot];
-          if (eq && id != 0xFFFFFFFFu) att = (int)id;
-        }
-      }
-      const bool in_attr = att >= 0;
-      const bool term = in_attr && (uint32_t)att == tgt;
-      const bool wrong = in_attr && !term;
-      int tt = (int)((tpk[q] >> (8 * r)) & 0xFFu) + 1;
-      tt = tt > 255 ? 255 : tt;
-      const bool trunc = a.horizon > 0 && tt >= a.horizon;
-      const uint32_t pc = (pcpk[q] >> (8 * r)) & 0xFFu;
-      rq[r] = reinterpret_cast<const float*>(rtab)[(2 * (int)term + (int)wrong) * (N + 1) + (int)pc];
-      uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) |
-                    (((pmask >> b) & 1u) << 3);
-      uint32_t tnew = (uint32_t)tt;
-      if ((a.mode & PBN_MODE_AUTORESET) && (term || trunc)) {
-        const uint32_t Rw = rword[b];
-        uint32_t ns[W];
-        uint32_t nt;
-        const uint64_t ge = ge0 + (uint64_t)b;
-        if (a.n_attr >= 1) {
-          const uint32_t A = (uint32_t)a.n_attr;
-          const uint32_t as = ((Rw & 1023u) * A) >> 10;
-          const int st0 = a.att_start[as];
-          const uint32_t size = (uint32_t)(a.att_start[as + 1] - st0);
-          const uint32_t idx = (((Rw >> 20) & 4095u) * size) >> 12;
-#pragma unroll
-          for (int w = 0; w < W; ++w) ns[w] = a.att_states[(size_t)(st0 + idx) * W + w];
-          nt = as;
-          if (A >= 2) {
-            nt = (((Rw >> 10) & 1023u) * (A - 1)) >> 10;
-            nt += (nt >= as) ? 1u : 0u;
-          }
-        } else {
-          const Word4 rr = pbn::philox4x32_10((uint32_t)ge, st_lo, (pbn::kStreamReset << 28) | 1u,
-                                              (uint32_t)((ge >> 32) & 0xFFFFu) | st_hi, k0, k1);
-          const uint32_t rw[4] = {rr.x, rr.y, rr.z, rr.w};
-#pragma unroll
-          for (int w = 0; w < W; ++w) ns[w] = rw[w] & valid_word_mask(N, w);
-          nt = PBN_NO_TARGET;
-        }
-#pragma unroll
-        for (int w = 0; w < W; ++w) sp[w][b] = ns[w];
-        tgpk[q] = (tgpk[q] & ~(0xFFu << (8 * r))) | (nt << (8 * r));
-        tnew = 0;
-        fl |= PBN_FLAG_RESET;
-        any_reset = true;
-      }
-      fl4 |= fl << (8 * r);
-      t4 |= tnew << (8 * r);
-    }
-    reinterpret_cast<float4*>(a.reward + e0)[q] = make_float4(rq[0], rq[1], rq[2], rq[3]);
-    flpk[q] = fl4;
-    topk[q] = t4;
-  }
-#pragma unroll
-  for (int w = 0; w < W; ++w) {
-    uint4* p = reinterpret_cast<uint4*>(a.state_out + (size_t)w * n + e0);
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-      p[q] = make_uint4(sp[w][4 * q], sp[w][4 * q + 1], sp[w][4 * q + 2], sp[w][4 * q + 3]);
-  }
-  {
-    uint4* pf = reinterpret_cast<uint4*>(a.flags + e0);
-    uint4* pt = reinterpret_cast<uint4*>(a.t + e0);
-    pf[0] = make_uint4(flpk[0], flpk[1], flpk[2], flpk[3]);
-    pf[1] = make_uint4(flpk[4], flpk[5], flpk[6], flpk[7]);
-    pt[0] = make_uint4(topk[0], topk[1], topk[2], topk[3]);
-    pt[1] = make_uint4(topk[4], topk[5], topk[6], topk[7]);
-    if (any_reset) {
-      uint4* pg = reinterpret_cast<uint4*>(a.target + e0);
-      pg[0] = make_uint4(tgpk[0], tgpk[1], tgpk[2], tgpk[3]);
-      pg[1] = make_uint4(tgpk[4], tgpk[5], tgpk[6], tgpk[7]);
-    }
-  }
-}
-
-// eval of a lane-varying function: record in LDS, planes in LDS
-__device__ __forceinline__ uint32_t eval_func_lds(const uint32_t* __restrict__ fr,
-                                                  const uint32_t* __restrict__ S) {
-  const uint4 in = *reinterpret_cast<const uint4*>(fr);
-  const uint32_t x0 = S[in.x], x1 = S[in.y], x2 = S[in.z], x3 = S[in.w];
-  const uint4 d0 = *reinterpret_cast<const uint4*>(fr + 4);
-  const uint4 d1 = *reinterpret_cast<const uint4*>(fr + 8);
-  const uint4 b0 = *reinterpret_cast<const uint4*>(fr + 12);
-  const uint4 b1 = *reinterpret_cast<const uint4*>(fr + 16);
-  const uint32_t v0 = (x0 & d0.x) ^ b0.x, v1 = (x0 & d0.y) ^ b0.y, v2 = (x0 & d0.z) ^ b0.z,
-                 v3 = (x0 & d0.w) ^ b0.w, v4 = (x0 & d1.x) ^ b1.x, v5 = (x0 & d1.y) ^ b1.y,
-                 v6 = (x0 & d1.z) ^ b1.z, v7 = (x0 & d1.w) ^ b1.w;
-  const uint32_t w0 = bfi(x1, v1, v0), w1 = bfi(x1, v3, v2), w2 = bfi(x1, v5, v4), w3 = bfi(x1, v7, v6);
-  return bfi(x3, bfi(x2, w3, w2), bfi(x2, w1, w0));
-}
-
 // ------------------------------------------- step kernel, one wave per 32-env group
 //
-// For batches too small to fill the chip with one thread per group.  Lane j of
-// the wave is env j (lanes 0-31) for the per-env work and node j (+32r) for the
-// node work, so the node loop runs in parallel across lanes.  No block barrier:
-// every wave stages its own copy of the small tables + FuncRecs in LDS, and all
+// Lane j of the wave is env j (lanes 0-31) for the per-env work and node j (+32r) for
+// the node work.  Blocks of kWavesPerBlock waves share one LDS copy of the tables; all
 // global loads are issued before the Philox batch so their latency hides under it.
 //   1. Philox: the lower half computes each env's ENV call and the first half of
 //      its node's selection calls, the upper half the other selection calls plus
@@ -1049,7 +687,7 @@ template <int K>
 __device__ __forceinline__ uint32_t chain_from_masks(const uint4 (&rec)[kNodeRecs], const uint4* __restrict__ sel,
                                                      int stride, const uint32_t* __restrict__ S,
                                                      const uint32_t* __restrict__ lt, int lt_stride, int nf,
-                                                     uint32_t x) {
+                                                     bool tail, uint32_t x) {
   uint32_t xin[K][4], ltv[K];
   uint4 sa[K], sb[K];
 #pragma unroll
@@ -1059,7 +697,9 @@ __device__ __forceinline__ uint32_t chain_from_masks(const uint4 (&rec)[kNodeRec
     xin[q][2] = S[(ins >> 16) & 0xFFu]; xin[q][3] = S[ins >> 24];
     sa[q] = sel[(2 * q) * stride];
     sb[q] = sel[(2 * q + 1) * stride];
-    ltv[q] = q < K - 1 ? lt[q * lt_stride] : 0u;
+    // mask q exists for q < K - 1, and for q = K - 1 too when some node has more than K
+    // (= kNodeRecs) functions
+    ltv[q] = (q < K - 1 || tail) ? lt[q * lt_stride] : 0u;
   }
 #pragma unroll
   for (int q = K - 1; q >= 0; --q) {
@@ -1317,10 +957,10 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
         const uint4* sel = selq + ii;
         const uint32_t* lti = lt_in + ii;
         switch (u_mnf) {
-          case 1: x = chain_from_masks<1>(rec_[r], sel, 32 * W, Sg, lti, 64 * W, nf, x); break;
-          case 2: x = chain_from_masks<2>(rec_[r], sel, 32 * W, Sg, lti, 64 * W, nf, x); break;
-          case 3: x = chain_from_masks<3>(rec_[r], sel, 32 * W, Sg, lti, 64 * W, nf, x); break;
-          default: x = chain_from_masks<4>(rec_[r], sel, 32 * W, Sg, lti, 64 * W, nf, x); break;
+          case 1: x = chain_from_masks<1>(rec_[r], sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
+          case 2: x = chain_from_masks<2>(rec_[r], sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
+          case 3: x = chain_from_masks<3>(rec_[r], sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
+          default: x = chain_from_masks<4>(rec_[r], sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
         }
         X[r] = i < N ? x : 0u;
       }
@@ -1455,16 +1095,6 @@ int fail(int code, const std::string& msg) {
 using StepFn = void (*)(StepArgs);
 
 
-StepFn pick_lane(int W) {
-  switch (W) {
-    case 1: return pbn_step_lane<1>;
-    case 2: return pbn_step_lane<2>;
-    case 3: return pbn_step_lane<3>;
-    case 4: return pbn_step_lane<4>;
-  }
-  return nullptr;
-}
-
 template <int W, int V>
 StepFn pick_wave_w(int B) {
   switch (B) {
@@ -1537,10 +1167,7 @@ struct pbn_net {
   uint4* d_fcompact = nullptr;
   uint4* d_nrec = nullptr;
   int n_funcs = 0;
-  int waves_per_block = 1;   // lane kernel
-  size_t lds_lane = 0;
   size_t lds_wave = 0;
-  StepFn lane = nullptr;
   StepFn wave = nullptr;        // rollout, loop invariants hoisted (small batches)
   StepFn wave1 = nullptr;       // single step (pbn_step)
   StepFn wave_lean = nullptr;   // rollout with low VGPR count (large batches)
@@ -1548,14 +1175,11 @@ struct pbn_net {
   size_t lds_pipe = 0;
   int max_nf = 0, lq = 1, slot_words = 0;
   int64_t roll_pipe_groups = 1 << 30;  // rollouts with at most this many groups use the pipelined kernel
-  int force = 0;             // PBN_KERNEL env override: 1 = lane, 2 = wave
   int force_roll = 0;        // PBN_ROLL env override: 1 = hoist, 2 = lean
   int64_t roll_lean_groups = 4096;  // rollouts above this many 32-env groups use the lean variant
                                     // (crossover between 65,536 and 262,144 envs:
                                     // profiles/r01_sweep_pbn28_variants_v4.jsonl)
   ResetFn reset = nullptr;
-  FuncRec* d_funcs = nullptr;
-  int32_t* d_node_fs = nullptr;
   uint32_t* d_tab = nullptr;
   int32_t* d_att_start = nullptr;
   uint32_t* d_att_states = nullptr;
@@ -1565,8 +1189,6 @@ namespace {
 
 void free_net(pbn_net* net) {
   if (!net) return;
-  (void)hipFree(net->d_funcs);
-  (void)hipFree(net->d_node_fs);
   (void)hipFree(net->d_fcompact);
   (void)hipFree(net->d_nrec);
   (void)hipFree(net->d_tab);
@@ -1816,8 +1438,6 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     net->gap_exact = (p < 1e-6 || p > 0.5) ? 1 : 0;
     net->inv_log2q = net->gap_exact ? 0.f : (float)(1.0 / log2(1.0 - p));
   }
-  net->waves_per_block = (W == 1) ? 2 : 1;
-  net->lds_lane = (size_t)net->tab_words * 4 + (size_t)net->waves_per_block * 2 * 32 * W * 64 * 4;
   net->lds_wave = ((size_t)net->tab_words + (size_t)kWavesPerBlock * net->wave_words) * 4;
   net->slot_words = (3 * W + 1) * 64 + net->lq * 64 * W;
   net->lds_pipe = ((size_t)net->tab_words + 64 * (size_t)W + 2 * (size_t)net->slot_words) * 4;
@@ -1847,25 +1467,18 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   net->wave1 = pick_wave<1>(W, d->prob_bits);
   net->wave_lean = pick_wave<2>(W, d->prob_bits);
   net->pipe = pick_pipe(W, d->prob_bits);
-  net->lane = pick_lane(W);
   net->reset = pick_reset(W);
   if (const char* env = getenv("PBN_ROLL")) {
     if (!strcmp(env, "hoist")) net->force_roll = 1;
     if (!strcmp(env, "lean")) net->force_roll = 2;
     if (!strcmp(env, "pipe")) net->force_roll = 3;
   }
-  if (const char* env = getenv("PBN_KERNEL")) {
-    if (!strcmp(env, "lane")) net->force = 1;
-    if (!strcmp(env, "wave")) net->force = 2;
-  }
   int rc;
   if (hipGetDevice(&net->device) != hipSuccess) {
     free_net(net);
     return fail(PBN_EDEVICE, "no HIP device");
   }
-  if ((rc = upload(&net->d_funcs, recs.data(), recs.size())) ||
-      (rc = upload(&net->d_node_fs, d->node_func_start, (size_t)N + 1)) ||
-      (rc = upload(&net->d_fcompact, fcomp.data(), fcomp.size())) ||
+  if ((rc = upload(&net->d_fcompact, fcomp.data(), fcomp.size())) ||
       (rc = upload(&net->d_nrec, nrec.data(), nrec.size())) ||
       (rc = upload(&net->d_tab, tab.data(), tab.size())) ||
       (rc = upload(&net->d_att_start, A ? d->attractor_start : nullptr, (size_t)A + 1)) ||
@@ -1873,9 +1486,9 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     free_net(net);
     return rc;
   }
-  for (int ti = 0; ti < 5; ++ti) {
-    const StepFn fn = ti == 0 ? net->lane : (ti == 1 ? net->wave : (ti == 2 ? net->wave_lean : (ti == 3 ? net->wave1 : net->pipe)));
-    const size_t bytes = ti == 0 ? net->lds_lane : (ti == 4 ? net->lds_pipe : net->lds_wave);
+  for (int ti = 1; ti < 5; ++ti) {
+    const StepFn fn = ti == 1 ? net->wave : (ti == 2 ? net->wave_lean : (ti == 3 ? net->wave1 : net->pipe));
+    const size_t bytes = ti == 4 ? net->lds_pipe : net->lds_wave;
     if (bytes > 160 * 1024) continue;  // variant unusable for this net; never picked
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)bytes) != hipSuccess) {
@@ -1883,7 +1496,7 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
       return fail(PBN_EDEVICE, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
     }
   }
-  if (net->lds_lane > 160 * 1024 && net->lds_wave > 160 * 1024) {
+  if (net->lds_wave > 160 * 1024) {
     free_net(net);
     return fail(PBN_EINVAL, "LDS budget exceeded");
   }
@@ -1950,8 +1563,6 @@ int pbn_step(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, in
     return fail(PBN_EINVAL, "device buffers must be 16-byte aligned");
   StepArgs a;
   memset(&a, 0, sizeof a);
-  a.funcs = net->d_funcs;
-  a.node_fs = net->d_node_fs;
   a.tab = net->d_tab;
   a.att_start = net->d_att_start;
   a.att_states = net->d_att_states;
@@ -1999,19 +1610,9 @@ int pbn_step(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, in
   // (>= 4 waves per SIMD), else one wave per group (node loop across lanes)
   a.n_steps = 1;
   a.obs = nullptr;
-  bool use_lane = false;   // the wave kernel is faster at every measured size (profiles/)
-  if (net->force == 1) use_lane = true;
-  if (net->force == 2) use_lane = false;
-  if (use_lane && net->lds_lane > 160 * 1024) use_lane = false;
-  if (!use_lane && net->lds_wave > 160 * 1024) use_lane = true;
-  if (use_lane) {
-    const int threads = 64 * net->waves_per_block;
-    const unsigned blocks = (unsigned)((a.n_groups + threads - 1) / threads);
-    hipLaunchKernelGGL(net->lane, dim3(blocks), dim3(threads), net->lds_lane, (hipStream_t)stream, a);
-  } else {
-    const unsigned blocks = (unsigned)((a.n_groups + kWavesPerBlock - 1) / kWavesPerBlock);  // one wave per group
-    hipLaunchKernelGGL(net->wave1, dim3(blocks), dim3(64 * kWavesPerBlock), net->lds_wave, (hipStream_t)stream, a);
-  }
+  if (net->lds_wave > 160 * 1024) return fail(PBN_EINVAL, "network too large for the step kernel's LDS");
+  const unsigned blocks = (unsigned)((a.n_groups + kWavesPerBlock - 1) / kWavesPerBlock);  // one wave per group
+  hipLaunchKernelGGL(net->wave1, dim3(blocks), dim3(64 * kWavesPerBlock), net->lds_wave, (hipStream_t)stream, a);
   HIP_OK(hipGetLastError());
   return PBN_OK;
 }
@@ -2029,8 +1630,6 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
   if (net->lds_wave > 160 * 1024) return fail(PBN_EINVAL, "network too large for the rollout kernel's LDS");
   StepArgs a;
   memset(&a, 0, sizeof a);
-  a.funcs = net->d_funcs;
-  a.node_fs = net->d_node_fs;
   a.tab = net->d_tab;
   a.att_start = net->d_att_start;
   a.att_states = net->d_att_states;

@@ -19,6 +19,8 @@ from pbn_rl_amd.network import load_network
 from pbn_rl_amd.spec import EnvSpec
 from pbn_rl_amd.vector_env import VectorPBNEnv
 
+from .synthetic import random_spec
+
 pytestmark = pytest.mark.gpu
 
 NETS = ["pbn7", "pbn10", "pbn28", "pbn70"]
@@ -81,18 +83,14 @@ def test_step_matches_oracle(name, mode):
     run_pair(spec, 2048, 12, mode=mode, env_offset=0 if mode < 2 else 4096)
 
 
-@pytest.mark.parametrize("kernel", ["lane", "wave"])
 @pytest.mark.parametrize("name", ["pbn28", "pbn70"])
-def test_high_perturbation_multi_flip_path(name, kernel, monkeypatch):
-    monkeypatch.setenv("PBN_KERNEL", kernel)
+def test_high_perturbation_multi_flip_path(name):
     ref = run_pair(make_spec(name, perturbation=0.3), 1024, 6, mode=3)
     assert (ref["flags"] & _lib.FLAG_PERTURBED).mean() > 0.9
 
 
-@pytest.mark.parametrize("kernel", ["lane", "wave"])
 @pytest.mark.parametrize("bits", [4, 8, 12, 16])
-def test_prob_bits(bits, kernel, monkeypatch):
-    monkeypatch.setenv("PBN_KERNEL", kernel)
+def test_prob_bits(bits):
     run_pair(make_spec("pbn28", prob_bits=bits, perturbation=0.0), 1024, 6, mode=1, start_random=True)
     run_pair(make_spec("pbn70", prob_bits=bits, perturbation=0.02), 1024, 3, mode=3)
 
@@ -149,27 +147,18 @@ def test_abi_rejects_bad_arguments():
     assert rc == -22
 
 
-@pytest.mark.parametrize("kernel", ["lane", "wave"])
 @pytest.mark.parametrize("name", ["pbn7", "pbn10", "pbn28", "pbn70"])
-def test_every_kernel_variant(name, kernel, monkeypatch):
-    """Both kernel variants (one thread per 32-env group / one wave per group) give
-    the oracle's results; PBN_KERNEL forces the variant at pbn_net_create."""
-    monkeypatch.setenv("PBN_KERNEL", kernel)
+def test_step_offsets_and_modes(name):
+    """pbn_step (one wave per 32-env group) at an env offset, with and without autoreset."""
     run_pair(make_spec(name, perturbation=0.05), 4096, 6, mode=3, env_offset=1024)
     run_pair(make_spec(name, perturbation=0.05), 2048, 4, mode=0)
 
 
-@pytest.mark.parametrize("variant", ["hoist", "lean"])
-@pytest.mark.parametrize("name", ["pbn7", "pbn28", "pbn70"])
-@pytest.mark.parametrize("mode", [1, 3])
-def test_rollout_matches_oracle(name, mode, variant, monkeypatch):
-    """pbn_rollout (R steps in one launch, state on chip) == R oracle steps."""
-    monkeypatch.setenv("PBN_ROLL", variant)
-    spec = make_spec(name, perturbation=0.05, horizon=7)
-    n, R, seed = 4096, 9, 4242
-    env = VectorPBNEnv(spec, n, seed=seed, env_offset=2048)
+def run_rollout_pair(spec, n, R, mode, *, seed=4242, env_offset=2048):
+    """pbn_rollout (R steps in one launch, state on chip) == R oracle steps, every output."""
+    env = VectorPBNEnv(spec, n, seed=seed, env_offset=env_offset, autoreset=bool(mode & 1))
     env.reset()
-    st, tg, t = oracle.reset(spec, seed, 0, 2048, n)
+    st, tg, t = oracle.reset(spec, seed, 0, env_offset, n)
     W = spec.words
     rng = np.random.default_rng(3)
     if mode & 2:
@@ -177,20 +166,74 @@ def test_rollout_matches_oracle(name, mode, variant, monkeypatch):
         fm = None
     else:
         flips = rng.integers(0, 2 ** 32, size=(R, W, n), dtype=np.uint64).astype(np.uint32) & np.uint32(0x04010020)
+        if spec.n % 32:
+            flips[:, W - 1] &= np.uint32((1 << (spec.n % 32)) - 1)
         fm = torch.from_numpy(flips.view(np.int32)).to(env.device)
     out = env.rollout(R, flipmasks=fm, random_actions=bool(mode & 2), keep_obs=True)
     for k in range(R):
         flip = np.zeros((W, n), np.uint32) if flips is None else flips[k]
-        ref = oracle.step(spec, seed, 1 + k, 2048, st, flip, tg, t, mode)
-        assert np.array_equal(u32(out["obs"][k]), st), k
-        assert np.array_equal(u32(out["final_state"][k]), ref["final_state"]), k
-        assert np.array_equal(out["flags"][k].cpu().numpy(), ref["flags"]), k
-        assert np.array_equal(out["reward"][k].cpu().numpy().view(np.uint32), ref["reward"].view(np.uint32)), k
-        assert np.array_equal(u32(out["flipmask"][k]), ref["flipmask"]), k
+        ref = oracle.step(spec, seed, 1 + k, env_offset, st, flip, tg, t, mode)
+        assert np.array_equal(u32(out["obs"][k])[:, :n], st), k
+        assert np.array_equal(u32(out["final_state"][k])[:, :n], ref["final_state"]), k
+        assert np.array_equal(out["flags"][k].cpu().numpy()[:n], ref["flags"]), k
+        assert np.array_equal(out["reward"][k].cpu().numpy()[:n].view(np.uint32), ref["reward"].view(np.uint32)), k
+        assert np.array_equal(u32(out["flipmask"][k])[:, :n], ref["flipmask"]), k
         st, tg, t = ref["state_out"], ref["target"], ref["t"]
-    assert np.array_equal(u32(env.state), st)
-    assert np.array_equal(env.target.cpu().numpy(), tg)
-    assert np.array_equal(env.t.cpu().numpy(), t)
+    assert np.array_equal(u32(env.state)[:, :n], st)
+    assert np.array_equal(env.target.cpu().numpy()[:n], tg)
+    assert np.array_equal(env.t.cpu().numpy()[:n], t)
+    env.close()
+
+
+@pytest.mark.parametrize("variant", ["pipe", "hoist", "lean"])
+@pytest.mark.parametrize("name", ["pbn7", "pbn28", "pbn70"])
+@pytest.mark.parametrize("mode", [1, 3])
+def test_rollout_matches_oracle(name, mode, variant, monkeypatch):
+    monkeypatch.setenv("PBN_ROLL", variant)
+    run_rollout_pair(make_spec(name, perturbation=0.05, horizon=7), 4096, 9, mode)
+
+
+@pytest.mark.parametrize("variant", ["pipe", "lean"])
+@pytest.mark.parametrize("n_envs", [32, 96, 2080])
+def test_rollout_odd_group_counts(n_envs, variant, monkeypatch):
+    """The pipelined kernel pairs groups per block: an odd group count leaves a phantom half."""
+    monkeypatch.setenv("PBN_ROLL", variant)
+    run_rollout_pair(make_spec("pbn28", perturbation=0.05, horizon=5), n_envs, 7, 3, env_offset=96)
+
+
+@pytest.mark.parametrize("bits", [4, 8, 12])
+def test_rollout_prob_bits(bits, monkeypatch):
+    monkeypatch.setenv("PBN_ROLL", "pipe")
+    run_rollout_pair(make_spec("pbn28", prob_bits=bits, perturbation=0.02), 2048, 6, 3)
+    run_rollout_pair(make_spec("pbn70", prob_bits=bits, perturbation=0.02), 2048, 4, 3)
+
+
+@pytest.mark.parametrize("variant", ["pipe", "lean"])
+def test_rollout_high_perturbation_and_no_attractors(variant, monkeypatch):
+    monkeypatch.setenv("PBN_ROLL", variant)
+    run_rollout_pair(make_spec("pbn28", perturbation=0.3), 2048, 6, 3)
+    run_rollout_pair(EnvSpec(load_network("pbn28"), [], perturbation=0.01, horizon=3), 2048, 8, 3)
+
+
+# ---------------------------------------------------------------- synthetic networks
+SYNTH = [(5, 11), (33, 12), (80, 13), (128, 14)]   # 1, 2, 3, 4 state words
+
+
+@pytest.mark.parametrize("n_nodes,seed", SYNTH)
+def test_synthetic_networks_step(n_nodes, seed):
+    """Up to 6 functions per node, arbitrary weights, constant functions (kaban nets have none)."""
+    spec = random_spec(n_nodes, seed, perturbation=0.05, horizon=6)
+    run_pair(spec, 2048, 5, mode=3, env_offset=1024)
+    run_pair(spec, 1024, 3, mode=0)
+
+
+@pytest.mark.parametrize("variant", ["pipe", "hoist", "lean"])
+@pytest.mark.parametrize("n_nodes,seed", SYNTH)
+def test_synthetic_networks_rollout(n_nodes, seed, variant, monkeypatch):
+    monkeypatch.setenv("PBN_ROLL", variant)
+    spec = random_spec(n_nodes, seed, perturbation=0.05, horizon=6)
+    run_rollout_pair(spec, 2080, 6, 3)
+    run_rollout_pair(spec, 96, 5, 1)
 
 
 def test_rollout_equals_steps_baseline_size():

@@ -61,6 +61,32 @@ def test_c_oracle_equals_python_oracle(name, mode):
         st, tg, t = res["state_out"], res["target"], res["t"]
 
 
+@pytest.mark.parametrize("n_nodes,seed", [(5, 21), (40, 22)])
+@pytest.mark.parametrize("mode", [1, 3])
+def test_c_oracle_equals_python_oracle_synthetic(n_nodes, seed, mode):
+    """Random networks: up to 6 functions per node, arbitrary weights, 1-2 state words."""
+    from .synthetic import random_spec
+    spec = random_spec(n_nodes, seed, perturbation=0.1, horizon=3)
+    net = spec.network
+    n, sd, off = 32, 777, 32
+    W = spec.words
+    py = pyoracle.PyPBN(spec)
+    st, tg, t = oracle.reset(spec, sd, 0, off, n)
+    rng = np.random.default_rng(seed)
+    for step in range(1, 4):
+        flip = rng.integers(0, 2 ** 32, size=(W, n), dtype=np.uint64).astype(np.uint32) & np.uint32(0x00010201)
+        if spec.n % 32:
+            flip[W - 1] &= np.uint32((1 << (spec.n % 32)) - 1)
+        res = oracle.step(spec, sd, step, off, st, flip, tg, t, mode)
+        for i in range(n):
+            bits = net.unpack([int(st[w, i]) for w in range(W)])
+            fb = net.unpack([int(flip[w, i]) for w in range(W)])
+            r = py.step(sd, step, off + i, bits, fb, int(tg[i]), int(t[i]), mode)
+            assert net.pack(r["state_out"]) == [int(res["state_out"][w, i]) for w in range(W)]
+            assert r["flags"] == res["flags"][i] and np.float32(r["reward"]) == res["reward"][i]
+        st, tg, t = res["state_out"], res["target"], res["t"]
+
+
 def _one_step_from(spec, state_bits, n, seed=99, mode=0):
     net = spec.network
     W = spec.words

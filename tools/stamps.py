@@ -34,7 +34,6 @@ def main():
         _lib.build(out=STAMP_LIB, defines=["PBN_STAMPS"], verbose=True)
         return
     os.environ["PBN_LIB"] = STAMP_LIB
-    os.environ["PBN_KERNEL"] = "wave"
     import numpy as np
     import torch
 

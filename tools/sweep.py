@@ -1,6 +1,6 @@
-"""Launch-shape sweep: time pbn_step for each kernel variant (PBN_TEAM) and batch size.
+"""Kernel sweep: time pbn_step ("wave") and pbn_rollout variants (PBN_ROLL) per batch size.
 
-    python tools/sweep.py [--network pbn28] [--envs 65536,1048576] [--teams 1,2,4,8,16,32]
+    python tools/sweep.py [--network pbn28] [--envs 65536,1048576] [--kernels wave,rollp,rolll,rollh]
 
 Interleaves variants in one process (cdna_hip_programming.md rule 24) and
 reports median per-step kernel time from HIP events around graph replays.
@@ -25,7 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--network", default="pbn28")
     ap.add_argument("--envs", default="65536,1048576")
-    ap.add_argument("--kernels", default="lane,wave,roll")
+    ap.add_argument("--kernels", default="wave,rollp")
     ap.add_argument("--chunk", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--prob-bits", type=int, default=16)
@@ -39,7 +39,6 @@ def main():
         bufs = {}   # a captured graph writes into these: they must outlive it (torch.cuda.graph
                     # empties the allocator cache on entry, unmapping freed >= 20 MB segments)
         for T in args.kernels.split(","):
-            os.environ["PBN_KERNEL"] = "wave" if T.startswith("roll") else T
             os.environ["PBN_ROLL"] = {"rollh": "hoist", "rolll": "lean", "rollp": "pipe"}.get(T, "auto")
             env = VectorPBNEnv(spec, n, seed=3, keep_final_state=False)
             env.reset()
@@ -60,7 +59,6 @@ def main():
                     for _ in range(args.chunk):
                         env.step_flipmask(random_actions=True)
             envs[T], graphs[T] = env, g
-        os.environ.pop("PBN_KERNEL", None)
         os.environ.pop("PBN_ROLL", None)
         times = {T: [] for T in envs}
         for _ in range(args.rounds):
