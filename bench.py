@@ -50,6 +50,9 @@ def parse():
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a hipGraph")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--gather", action="store_true",
+                   help="also time rollouts followed by the per-rollout RCCL gather of (s, a, s', r, flags) "
+                        "records (SURVEY.md 8(e)); reported as value_with_gather, not the headline")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     return p.parse_args()
 
@@ -103,6 +106,44 @@ def python_baseline(spec, seconds: float = 3.0):
     el = time.perf_counter() - t0
     return {"value": k / el, "unit": "env-steps/s", "cores": 1, "kind": "port",
             "sample": f"oracle/pyoracle.py single env, {k} steps"}
+
+
+def gather_pass(env, args, world, dev, stream):
+    """Env-steps/s (all ranks) when every rollout of --chunk steps is followed by packing its
+    (obs, actions, s', reward, flags) records and one all_gather_into_tensor of them
+    (pbn_rl_amd.distributed record layout), eager launches."""
+    from pbn_rl_amd.distributed import record_rows
+
+    W, n, T = env.words, env.num_envs, args.chunk
+    rec = torch.empty((T, record_rows(W), n), dtype=torch.int32, device=dev)
+    flat = torch.empty((world * T, record_rows(W), n), dtype=torch.int32, device=dev)
+    buf = None
+    rounds = max(1, args.steps // T)
+    with torch.cuda.stream(stream):
+        def one():
+            nonlocal buf
+            buf = env.rollout(T, random_actions=True, keep_obs=True, keep_final=True, out=buf)
+            rec[:, 0:W] = buf["obs"][:, :, :n]
+            rec[:, W:2 * W] = buf["flipmask"][:, :, :n]
+            rec[:, 2 * W:3 * W] = buf["final_state"][:, :, :n]
+            rec[:, 3 * W] = buf["reward"][:, :n].view(torch.int32)
+            rec[:, 3 * W + 1] = buf["flags"][:, :n].to(torch.int32)
+            if world > 1:
+                torch.distributed.all_gather_into_tensor(flat, rec)
+        one()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            torch.distributed.barrier()
+        t0 = time.perf_counter()
+        for _ in range(rounds):
+            one()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            torch.distributed.barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+    return world * n * T * rounds / float(el.item())
 
 
 def launch_plan(steps: int, chunk: int):
@@ -192,6 +233,10 @@ def main():
     total_env_steps = world * args.envs * args.steps
     value = total_env_steps / elapsed
 
+    with_gather = None
+    if args.gather:
+        with_gather = gather_pass(env, args, world, dev, stream)
+
     if rank == 0:
         W = spec.words
         if rollout_mode:
@@ -235,6 +280,8 @@ def main():
                          "bytes_per_launch": bytes_launch,
                          "note": "VALU-bound (Philox volume), see DESIGN.md 'What bounds it'"},
         }
+        if with_gather is not None:
+            out["value_with_gather"] = with_gather
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(spec, args.envs, args.cpu_seconds)
             out["cpu_baseline_python"] = python_baseline(spec)

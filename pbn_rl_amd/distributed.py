@@ -64,6 +64,15 @@ class ShardedRollout:
         W, n = self.words, self.count
         env = self.env
         rec = torch.empty((steps, record_rows(W), n), dtype=torch.int32, device=env.state.device)
+        if policy is None and hasattr(env, "rollout"):
+            # one pbn_rollout launch for the whole rollout (state kept on chip between steps)
+            out = env.rollout(steps, random_actions=random_actions, keep_obs=True, keep_final=True)
+            rec[:, 0:W] = out["obs"][:, :, :n]
+            rec[:, W:2 * W] = out["flipmask"][:, :, :n]
+            rec[:, 2 * W:3 * W] = out["final_state"][:, :, :n]
+            rec[:, 3 * W] = out["reward"][:, :n].view(torch.int32)
+            rec[:, 3 * W + 1] = out["flags"][:, :n].to(torch.int32)
+            return rec
         for k in range(steps):
             rec[k, 0:W] = env.state[:, :n]
             if policy is not None:

@@ -28,3 +28,21 @@ class OracleVectorEnv:
         self.flipmask = torch.from_numpy(out["flipmask"].view(np.int32).copy())
         self.final_state = torch.from_numpy(out["final_state"].view(np.int32).copy())
         return self.state, torch.from_numpy(out["reward"]), torch.from_numpy(out["flags"])
+
+    def rollout(self, n_steps, flipmasks=None, random_actions=True, keep_obs=True, keep_final=True, out=None):
+        """Same contract as VectorPBNEnv.rollout (dict of [n_steps, ...] tensors)."""
+        W, n = self.words, self.count
+        rec = {"obs": torch.empty((n_steps, W, n), dtype=torch.int32),
+               "flipmask": torch.empty((n_steps, W, n), dtype=torch.int32),
+               "final_state": torch.empty((n_steps, W, n), dtype=torch.int32),
+               "reward": torch.empty((n_steps, n), dtype=torch.float32),
+               "flags": torch.empty((n_steps, n), dtype=torch.uint8)}
+        for k in range(n_steps):
+            rec["obs"][k] = self.state
+            fm = None if flipmasks is None else flipmasks[k]
+            _, reward, flags = self.step_flipmask(fm, random_actions=random_actions and fm is None)
+            rec["flipmask"][k] = self.flipmask
+            rec["final_state"][k] = self.final_state
+            rec["reward"][k] = reward
+            rec["flags"][k] = flags
+        return rec
