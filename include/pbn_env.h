@@ -15,6 +15,7 @@
  *        model_tester.py:561,624, ddqn_per/__init__.py:354     -> pbn_step
  *   env.close()  train_BDQ.py:116                              -> pbn_net_destroy
  *   T frames of the frame loop bdq_model/__init__.py:172-213     -> pbn_rollout
+ *   compute_ssd_hist(env, model, resets, iters) train_pbn_28.py:257 -> pbn_rollout + pbn_state_histogram
  *
  * The Python facade (pbn_rl_amd.env.PBNEnv / pbn_rl_amd.vector_env.VectorPBNEnv)
  * keeps that gym surface and calls these entry points through ctypes;
@@ -156,6 +157,17 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
                 int32_t n_steps, uint32_t mode, uint32_t* d_state, uint32_t* d_flipmask, uint8_t* d_target,
                 uint8_t* d_t, uint32_t* d_obs, uint32_t* d_final_state, float* d_reward, uint8_t* d_flags,
                 void* stream);
+
+/*
+ * State histogram, the accumulation step of the steady-state distribution
+ * (gym_PBN.utils.eval.compute_ssd_hist, train_pbn_28.py:257, train_pbn_10.py:257):
+ * d_hist[d_states[r * row_stride + c] & (2^n_bits - 1)] += 1 for r < n_rows, c < n_cols.
+ * Uses word 0 of each state (networks with n_nodes <= 32: pass the [steps][1][n] obs or
+ * final_state output of pbn_rollout with row_stride = n).  1 <= n_bits <= 32; 32-bit counters;
+ * the caller zeroes d_hist (2^n_bits entries).
+ */
+int pbn_state_histogram(const uint32_t* d_states, int64_t n_rows, int64_t n_cols, int64_t row_stride,
+                        int32_t n_bits, uint32_t* d_hist, void* stream);
 
 const char* pbn_last_error(void);
 int pbn_abi_version(void);

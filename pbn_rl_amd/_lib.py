@@ -24,7 +24,7 @@ FLAG_PERTURBED = 8
 FLAG_RESET = 16
 
 EXPORTS = ["pbn_net_create", "pbn_net_destroy", "pbn_net_words", "pbn_reset", "pbn_step", "pbn_rollout",
-           "pbn_last_error", "pbn_abi_version"]
+           "pbn_state_histogram", "pbn_last_error", "pbn_abi_version"]
 
 _lib: Optional[ctypes.CDLL] = None
 
@@ -67,6 +67,8 @@ def load() -> ctypes.CDLL:
     L.pbn_step.restype = ctypes.c_int
     L.pbn_rollout.argtypes = [vp, u64, u64, u64, i64, ctypes.c_int32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.pbn_rollout.restype = ctypes.c_int
+    L.pbn_state_histogram.argtypes = [vp, i64, i64, i64, ctypes.c_int32, vp, vp]
+    L.pbn_state_histogram.restype = ctypes.c_int
     L.pbn_last_error.argtypes = []
     L.pbn_last_error.restype = ctypes.c_char_p
     L.pbn_abi_version.argtypes = []

@@ -1039,6 +1039,38 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
   }
 }
 
+// ------------------------------------------------------------- state histogram
+// Visits per state for the steady-state distribution.  States of a steady-state chain
+// concentrate on a few attractor basins, so a wave first merges equal values (a few
+// ballot rounds: the leader adds the count of its value) before per-lane atomics.
+__global__ void __launch_bounds__(256) pbn_hist_kernel(const uint32_t* __restrict__ states, int64_t n_rows,
+                                                       int64_t n_cols, int64_t row_stride, uint32_t mask,
+                                                       uint32_t* __restrict__ hist) {
+  const int64_t total = n_rows * n_cols;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < total; base += stride) {
+    const int64_t i = base + threadIdx.x;
+    const bool have = i < total;
+    uint32_t v = 0;
+    if (have) {
+      const int64_t r = i / n_cols, c = i - r * n_cols;
+      v = states[r * row_stride + c] & mask;
+    }
+    bool pending = have;
+#pragma unroll
+    for (int round = 0; round < 4; ++round) {
+      const uint64_t act = __ballot(pending);
+      if (act == 0) break;
+      const int leader = __builtin_ctzll(act);
+      const uint32_t lv = __shfl(v, leader);
+      const uint64_t same = __ballot(pending && v == lv);
+      if ((threadIdx.x & 63) == leader) atomicAdd(&hist[lv], (uint32_t)__popcll(same));
+      if (pending && v == lv) pending = false;
+    }
+    if (pending) atomicAdd(&hist[v], 1u);
+  }
+}
+
 // ---------------------------------------------------------------- reset kernel
 template <int W>
 __global__ void __launch_bounds__(256) pbn_reset_kernel(const int32_t* __restrict__ att_start,
@@ -1272,6 +1304,21 @@ bool build_hash(const std::vector<std::vector<uint32_t>>& states, const std::vec
 extern "C" {
 
 const char* pbn_last_error(void) { return g_err.c_str(); }
+
+int pbn_state_histogram(const uint32_t* d_states, int64_t n_rows, int64_t n_cols, int64_t row_stride,
+                        int32_t n_bits, uint32_t* d_hist, void* stream) {
+  if (n_rows < 0 || n_cols < 0 || row_stride < n_cols) return fail(PBN_EINVAL, "bad histogram shape");
+  if (n_bits < 1 || n_bits > 32) return fail(PBN_EINVAL, "n_bits must be 1..32");
+  if (n_rows == 0 || n_cols == 0) return PBN_OK;
+  if (!d_states || !d_hist) return fail(PBN_EINVAL, "null buffer");
+  const uint32_t mask = n_bits == 32 ? 0xFFFFFFFFu : ((1u << n_bits) - 1u);
+  const int64_t total = n_rows * n_cols;
+  const unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(pbn_hist_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, d_states, n_rows, n_cols,
+                     row_stride, mask, d_hist);
+  HIP_OK(hipGetLastError());
+  return PBN_OK;
+}
 int pbn_abi_version(void) { return PBN_ABI_VERSION; }
 
 int pbn_net_words(const pbn_net* net) { return net ? net->W : PBN_EINVAL; }

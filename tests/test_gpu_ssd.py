@@ -1,0 +1,63 @@
+"""Steady-state distribution: pbn_state_histogram and compute_ssd_hist == the oracle's counts."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle
+from pbn_rl_amd.attractors import load_attractors
+from pbn_rl_amd.network import load_network
+from pbn_rl_amd.spec import EnvSpec
+from pbn_rl_amd.ssd import compute_ssd_hist, state_histogram
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n_bits", [7, 16, 28])
+def test_state_histogram_matches_bincount(n_bits):
+    rng = np.random.default_rng(n_bits)
+    rows, stride, cols = 37, 2080, 2050
+    hot = rng.integers(0, 1 << n_bits, size=5)            # heavy contention on a few bins
+    st = rng.integers(0, 2 ** 32, size=(rows, stride), dtype=np.uint64).astype(np.uint32)
+    pick = rng.random((rows, stride)) < 0.7
+    st[pick] = hot[rng.integers(0, 5, size=int(pick.sum()))].astype(np.uint32)
+    hist = torch.zeros(1 << n_bits, dtype=torch.int32, device="cuda")
+    state_histogram(torch.from_numpy(st.view(np.int32)).cuda(), cols, n_bits, hist)
+    want = np.bincount((st[:, :cols] & np.uint32((1 << n_bits) - 1)).ravel(), minlength=1 << n_bits)
+    assert np.array_equal(hist.cpu().numpy().view(np.uint32), want.astype(np.uint32))
+
+
+@pytest.mark.parametrize("name", ["pbn7", "pbn28"])
+def test_ssd_matches_oracle(name):
+    spec = EnvSpec(load_network(name), load_attractors(name), perturbation=0.02)
+    resets, iters, burn_in, seed = 70, 23, 4, 5
+    ssd, plot = compute_ssd_hist(spec, None, resets=resets, iters=iters, burn_in=burn_in, seed=seed, chunk=9)
+    n = 96   # resets rounded up to whole 32-env groups: the extra envs run but are not counted
+    st, tg, t = oracle.reset(spec, seed, 0, 0, n)
+    counts = np.zeros(1 << spec.n, dtype=np.int64)
+    for k in range(burn_in + iters):
+        out = oracle.step(spec, seed, 1 + k, 0, st, np.zeros_like(st), tg, t, 0)
+        if k >= burn_in:
+            counts += np.bincount(out["final_state"][0, :resets], minlength=1 << spec.n)
+        st, tg, t = out["state_out"], out["target"], out["t"]
+    assert np.array_equal(ssd, counts / counts.sum())
+    assert plot is None
+
+
+def test_ssd_with_policy_matches_oracle():
+    spec = EnvSpec(load_network("pbn7"), load_attractors("pbn7"), perturbation=0.02)
+    resets, iters, seed = 40, 12, 8
+
+    def policy(bits):   # flip node 0 whenever node 1 is on (a fixed, state-dependent control)
+        return (bits[:, 1].to(torch.int64) * 1)[:, None]
+
+    ssd, _ = compute_ssd_hist(spec, policy, resets=resets, iters=iters, seed=seed)
+    n = 64
+    st, tg, t = oracle.reset(spec, seed, 0, 0, n)
+    counts = np.zeros(1 << spec.n, dtype=np.int64)
+    for k in range(iters):
+        flip = np.zeros_like(st)
+        flip[0, :resets] = (st[0, :resets] >> 1) & 1          # action 1 = flip node 0
+        out = oracle.step(spec, seed, 1 + k, 0, st, flip, tg, t, 0)
+        counts += np.bincount(out["final_state"][0, :resets], minlength=1 << spec.n)
+        st, tg, t = out["state_out"], out["target"], out["t"]
+    assert np.array_equal(ssd, counts / counts.sum())
