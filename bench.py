@@ -157,9 +157,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one GPU per rank over RCCL; more ranks than GPUs (a rehearsal on a smaller box) share
+    # them round-robin and synchronise over gloo (RCCL refuses two ranks on one GPU)
+    n_dev = max(1, torch.cuda.device_count())
+    shared = world > n_dev
+    local = local % n_dev
     if world > 1:
         torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if shared:
+            torch.distributed.init_process_group("gloo")
+        else:
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
 
