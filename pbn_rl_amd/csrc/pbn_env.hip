@@ -38,6 +38,9 @@ namespace {
 
 constexpr int kFuncRecWords = 24;  // in[4], leaf[16], thr, pad[3]
 constexpr int kNodeRecs = 4;       // compact records prefetched per node by the wave kernel
+#ifndef PBN_STATE_PRIO
+#define PBN_STATE_PRIO 2
+#endif
 constexpr int kWavesPerBlock = 4;  // wave kernel: waves (32-env groups) per block, sharing one LDS table image
 constexpr int kMaxHashBits = 12;
 
@@ -723,6 +726,9 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
   extern __shared__ uint32_t smem[];
   const int lane = threadIdx.x & 63;
   const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar branches
+  // the state wave bounds every iteration: let it win VALU issue against the RNG waves of
+  // other blocks sharing its SIMD
+  if (role == 0) __builtin_amdgcn_s_setprio(PBN_STATE_PRIO);
   const int half = lane >> 5;
   const int l32 = lane & 31;
   const int64_t g = (int64_t)blockIdx.x * 2 + half;
