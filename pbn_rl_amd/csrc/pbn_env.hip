@@ -89,6 +89,7 @@ struct StepArgs {
   int n_states;      // attractor states (bounds of att_states; checked builds)
   int att_off;       // LDS image offset of attractor start[A+1] | states[S][W] (wave kernel)
   int sel_off;       // LDS image offset of the leaf selectors, uint4 [kNodeRecs][2][32W] (wave kernel)
+  int nrec_off;      // LDS image offset of the node-major records, uint4 [N][kNodeRecs]
   int n_cls;         // 1..4: the first kNodeRecs thresholds of every node take one of n_cls values
                      // uthr[0..n_cls) (record .y = class index); 0: per-node thresholds
   uint32_t uthr[kNodeRecs];
@@ -767,23 +768,9 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
     tt0 = a.t[CK(le, n, 2)];
     tg0 = a.target[CK(le, n, 3)];
   }
-  uint4 rec_[W][kNodeRecs];
-#pragma unroll
-  for (int r = 0; r < W; ++r) {
-    const int i = l32 + 32 * r;
-    const int ic = i < N ? i : 0;
-#pragma unroll
-    for (int q = 0; q < kNodeRecs; ++q)
-      rec_[r][q] = role != 1 ? a.nrec[CK((size_t)ic * kNodeRecs + q, N * kNodeRecs, 4)] : make_uint4(0, 0, 0, 0);
-  }
-  // wait for the record loads here, once: their first use inside the loop would make the
-  // wait (vmcnt(0), i.e. for every store in flight) part of each iteration
-#pragma unroll
-  for (int r = 0; r < W; ++r) {
-#pragma unroll
-    for (int q = 0; q < kNodeRecs; ++q) asm volatile("" : "+v"(rec_[r][q].x), "+v"(rec_[r][q].z));
-    asm volatile("" : "+v"(rec_[r][0].w), "+v"(rec_[r][1].w));
-  }
+  // node records live in LDS (L + nrec_off): each role reads what it needs per step, so no
+  // record is carried in VGPRs across the step loop
+  const uint4* recL = reinterpret_cast<const uint4*>(L + a.nrec_off);
   // wave-uniform parameters, re-defined (laundered) every iteration: hoisted out of the step
   // loop, the conditions built from them occupy SGPR pairs and spill to VGPR lanes
   uint32_t u_k0 = k0, u_k1 = k1;
@@ -794,14 +781,6 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
   __syncthreads();
 
   for (int k = 0; k <= n_steps; ++k) {
-    // keep per-step expansions of loop invariants (threshold digits, leaf selectors) inside
-    // the loop: hoisted they cost ~80 VGPRs, and occupancy is what hides latency here
-#pragma unroll
-    for (int r = 0; r < W; ++r) {
-#pragma unroll
-      for (int q = 0; q < kNodeRecs; ++q) asm volatile("" : "+v"(rec_[r][q].x), "+v"(rec_[r][q].z));
-      asm volatile("" : "+v"(rec_[r][0].w), "+v"(rec_[r][1].w));   // nf, f0
-    }
     asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
     asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
     PBN_PSTAMP(k, 0);
@@ -904,19 +883,21 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
 #pragma unroll
       for (int r = 0; r < W; ++r) {
         const int i = l32 + 32 * r;
-        if (valid && i < N && (int)rec_[r][0].w > 1) {
+        const int ic = i < N ? i : 0;
+        const uint4 r0 = recL[ic * kNodeRecs];
+        if (valid && i < N && (int)r0.w > 1) {
           uint32_t dig[16];
 #pragma unroll
           for (int c = 0; c < CPN; ++c) {
             const Word4 o = pbn::philox4x32_10(G_lo, st_lo, (pbn::kStreamSel << 28) | (uint32_t)(4 * i + c), G_hi, u_k0, u_k1);
             dig[4 * c + 0] = o.x; dig[4 * c + 1] = o.y; dig[4 * c + 2] = o.z; dig[4 * c + 3] = o.w;
           }
-          const int nf = (int)rec_[r][0].w;
+          const int nf = (int)r0.w;
           {   // per-lane thresholds: the selection wave has slack, the SGPRs are scarce
 #pragma unroll
             for (int q = 0; q < kNodeRecs - 1; ++q)
-              if (q < nf - 1) lt_out[q * 64 * W + i] = less_than(dig, rec_[r][q].z, B);
-            const int f0 = (int)rec_[r][1].w;
+              if (q < nf - 1) lt_out[q * 64 * W + i] = less_than(dig, recL[ic * kNodeRecs + q].z, B);
+            const int f0 = (int)recL[ic * kNodeRecs + 1].w;
             for (int j = kNodeRecs - 1; j < nf - 1; ++j)   // nodes with more than kNodeRecs functions
               lt_out[j * 64 * W + i] = less_than(dig, a.fcompact[CK(f0 + j, a.n_funcs, 9)].z, B);
           }
@@ -949,11 +930,14 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
       for (int r = 0; r < W; ++r) {
         const int i = l32 + 32 * r;
         int ii = i < N ? i : 0;
-        asm volatile("" : "+v"(ii));   // selector reads stay in the loop (see above)
-        const int nf = (int)rec_[r][0].w;
+        asm volatile("" : "+v"(ii));   // selector and record reads stay in the step loop
+        uint4 rec_r[kNodeRecs];
+#pragma unroll
+        for (int q = 0; q < kNodeRecs; ++q) rec_r[q] = recL[ii * kNodeRecs + q];
+        const int nf = (int)rec_r[0].w;
         uint32_t x = 0;
         if (u_mnf > kNodeRecs) {   // chain tail of nodes with more than kNodeRecs functions
-          const int f0 = (int)rec_[r][1].w;
+          const int f0 = (int)rec_r[1].w;
           for (int j = nf - 1; j >= kNodeRecs; --j) {
             const uint4 rc = a.fcompact[CK(f0 + j, a.n_funcs, 9)];
             const uint32_t fj = eval_compact(rc.x, rc.y, Sg);
@@ -963,10 +947,10 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
         const uint4* sel = selq + ii;
         const uint32_t* lti = lt_in + ii;
         switch (u_mnf) {
-          case 1: x = chain_from_masks<1>(rec_[r], sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
-          case 2: x = chain_from_masks<2>(rec_[r], sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
-          case 3: x = chain_from_masks<3>(rec_[r], sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
-          default: x = chain_from_masks<4>(rec_[r], sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
+          case 1: x = chain_from_masks<1>(rec_r, sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
+          case 2: x = chain_from_masks<2>(rec_r, sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
+          case 3: x = chain_from_masks<3>(rec_r, sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
+          default: x = chain_from_masks<4>(rec_r, sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
         }
         X[r] = i < N ? x : 0u;
       }
@@ -1198,6 +1182,7 @@ struct pbn_net {
   int wave_words = 0;
   int att_off = 0;
   int sel_off = 0;
+  int nrec_off = 0;
   int n_cls = 0;
   uint32_t uthr[kNodeRecs] = {0, 0, 0, 0};
   int gap_exact = 1;
@@ -1483,18 +1468,6 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
       net->max_nf = std::max(net->max_nf, d->node_func_start[i + 1] - d->node_func_start[i]);
     net->lq = std::max(net->max_nf - 1, 1);
   }
-  net->tab_words = (int)tab.size();
-  net->n_funcs = d->n_funcs;
-  net->wave_words = (32 * W + 3) & ~3;   // S planes per wave
-  {
-    const double p = (double)d->perturb_cdf[0] / 4294967296.0;
-    net->gap_exact = (p < 1e-6 || p > 0.5) ? 1 : 0;
-    net->inv_log2q = net->gap_exact ? 0.f : (float)(1.0 / log2(1.0 - p));
-  }
-  net->lds_wave = ((size_t)net->tab_words + (size_t)kWavesPerBlock * net->wave_words) * 4;
-  net->slot_words = (3 * W + 1) * 64 + net->lq * 64 * W;
-  net->lds_pipe = ((size_t)net->tab_words + 64 * (size_t)W + 2 * (size_t)net->slot_words) * 4;
-  // compact records for the wave kernel: {inputs as bytes, 4-input truth table, threshold, 0}
   std::vector<uint4> fcomp(d->n_funcs);
   for (int f = 0; f < d->n_funcs; ++f) {
     const FuncRec& r = recs[f];
@@ -1516,6 +1489,24 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     nrec[(size_t)i * kNodeRecs + 0].w = (uint32_t)nf;
     nrec[(size_t)i * kNodeRecs + 1].w = (uint32_t)f0;
   }
+  // node-major records in the LDS image too (the pipelined kernel reads them per step
+  // instead of keeping them in VGPRs across its loop)
+  net->nrec_off = (int)tab.size();
+  for (const uint4& r4 : nrec) {
+    tab.push_back(r4.x); tab.push_back(r4.y); tab.push_back(r4.z); tab.push_back(r4.w);
+  }
+  net->tab_words = (int)tab.size();
+  net->n_funcs = d->n_funcs;
+  net->wave_words = (32 * W + 3) & ~3;   // S planes per wave
+  {
+    const double p = (double)d->perturb_cdf[0] / 4294967296.0;
+    net->gap_exact = (p < 1e-6 || p > 0.5) ? 1 : 0;
+    net->inv_log2q = net->gap_exact ? 0.f : (float)(1.0 / log2(1.0 - p));
+  }
+  net->lds_wave = ((size_t)net->tab_words + (size_t)kWavesPerBlock * net->wave_words) * 4;
+  net->slot_words = (3 * W + 1) * 64 + net->lq * 64 * W;
+  net->lds_pipe = ((size_t)net->tab_words + 64 * (size_t)W + 2 * (size_t)net->slot_words) * 4;
+  // compact records for the wave kernel: {inputs as bytes, 4-input truth table, threshold, 0}
   net->wave = pick_wave<0>(W, d->prob_bits);
   net->wave1 = pick_wave<1>(W, d->prob_bits);
   net->wave_lean = pick_wave<2>(W, d->prob_bits);
@@ -1643,6 +1634,7 @@ int pbn_step(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, in
   a.n_states = net->n_states;
   a.att_off = net->att_off;
   a.sel_off = net->sel_off;
+  a.nrec_off = net->nrec_off;
   a.n_cls = net->n_cls;
   a.max_nf = net->max_nf;
   a.lq = net->lq;
@@ -1712,6 +1704,7 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
   a.n_states = net->n_states;
   a.att_off = net->att_off;
   a.sel_off = net->sel_off;
+  a.nrec_off = net->nrec_off;
   a.n_cls = net->n_cls;
   a.max_nf = net->max_nf;
   a.lq = net->lq;
