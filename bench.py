@@ -31,19 +31,26 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+FP32_MATRIX_TFLOPS = 157.3  # MI355X FP32 MFMA/vector peak (MI355X_MICROARCH.md)
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=2000)
-    p.add_argument("--warmup", type=int, default=200)
+    p.add_argument("--steps", type=int, default=None, help="timed steps (default 2000; bdq workload 200)")
+    p.add_argument("--warmup", type=int, default=None, help="untimed steps (default 200; bdq workload 20)")
+    p.add_argument("--workload", choices=["env", "bdq"], default="env",
+                   help="env: BASELINE config 2, the env step alone (in-kernel random interventions); "
+                        "bdq: config 5, the full BDQ frame per step (pbn_obs_unpack -> BranchingQNetwork "
+                        "forward in PyTorch -> pbn_q_to_flipmask -> pbn_step)")
+    p.add_argument("--epsilon", type=float, default=0.0, help="bdq workload: exploration rate")
     p.add_argument("--mode", choices=["rollout", "step"], default="rollout",
                    help="rollout: pbn_rollout launches of --chunk steps (state kept on chip); "
                         "step: one pbn_step launch per step")
     p.add_argument("--chunk", type=int, default=20, help="steps per pbn_rollout launch")
     p.add_argument("--network", default="pbn28")
-    p.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    p.add_argument("--envs", type=int, default=None,
+                   help="envs per GPU (default 65,536; bdq workload 32,768 = 262,144 over 8 GPUs)")
     p.add_argument("--perturbation", type=float, default=0.01)
     p.add_argument("--prob-bits", type=int, default=16)
     p.add_argument("--horizon", type=int, default=20)
@@ -54,7 +61,21 @@ def parse():
                    help="also time rollouts followed by the per-rollout RCCL gather of (s, a, s', r, flags) "
                         "records (SURVEY.md 8(e)); reported as value_with_gather, not the headline")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
-    return p.parse_args()
+    a = p.parse_args()
+    bdq = a.workload == "bdq"
+    a.steps = a.steps if a.steps is not None else (200 if bdq else 2000)
+    a.warmup = a.warmup if a.warmup is not None else (20 if bdq else 200)
+    a.envs = a.envs if a.envs is not None else (32768 if bdq else 65536)
+    if bdq:
+        a.mode = "step"
+    return a
+
+
+def qnet_flops_per_env(n: int, branches: int = 3) -> int:
+    """Multiply-add FLOPs of one BranchingQNetwork forward per env (bdq_model/network.py:24-63):
+    bilinear N*N*256, trunk 256-128-64-32, value 32-64-1, branches x (32-64-(N+1))."""
+    macs = n * n * 256 + 256 * 128 + 128 * 64 + 64 * 32 + 32 * 64 + 64 + branches * (32 * 64 + 64 * (n + 1))
+    return 2 * macs
 
 
 def algorithmic_bytes_per_env(words: int) -> int:
@@ -106,6 +127,49 @@ def python_baseline(spec, seconds: float = 3.0):
     el = time.perf_counter() - t0
     return {"value": k / el, "unit": "env-steps/s", "cores": 1, "kind": "port",
             "sample": f"oracle/pyoracle.py single env, {k} steps"}
+
+
+def cpu_baseline_bdq(spec, qnet, seconds: float):
+    """The BDQ frame on the host cores for ~`seconds`: numpy observation, the same Q-network
+    on CPU torch, greedy flip masks and the C oracle step, 4096 envs per frame."""
+    import copy
+
+    import numpy as np
+
+    from oracle import agent_oracle, oracle
+
+    threads = max(1, min(16, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    q_cpu = copy.deepcopy(qnet).to("cpu").eval()
+    n = 4096
+    st, tg, t = oracle.reset(spec, 1, 0, 0, n)
+    frames, t0 = 0, time.perf_counter()
+    with torch.no_grad():
+        while True:
+            obs = agent_oracle.obs_unpack(spec, st, tg)
+            q = q_cpu(torch.from_numpy(obs)).numpy()
+            flip, _ = agent_oracle.q_to_flipmask(spec, q, 1, frames + 1, 0, 0.0)
+            out = oracle.step(spec, 1, frames + 1, 0, st, flip, tg, t, 1, want_final=False, n_threads=threads)
+            st, tg, t = out["state_out"], out["target"], out["t"]
+            frames += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+    return {"value": n * frames / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"BDQ frame on CPU: numpy obs + torch CPU BranchingQNetwork ({threads} threads) + greedy "
+                      f"flip masks + oracle/pbn_oracle.c step, {n} envs x {frames} frames ({el:.1f} s)"}
+
+
+def workload_text(args, chunk: int, rollout_mode: bool) -> str:
+    common = (f"horizon {args.horizon}, p={args.perturbation}, prob_bits={args.prob_bits}")
+    if args.workload == "bdq":
+        return (f"full BDQ rollout (config 5): {args.network} x {args.envs} envs per GPU, per step pbn_obs_unpack -> "
+                f"BranchingQNetwork fp32 forward (random init, seed 0) -> epsilon-greedy (eps={args.epsilon}) "
+                f"pbn_q_to_flipmask -> pbn_step, autoreset, {common}")
+    return (f"{args.network} x {args.envs} envs per GPU, in-kernel random interventions (3 uniform actions/env/step), "
+            f"autoreset, {common}; "
+            + (f"pbn_rollout, {chunk} steps/launch, per-step obs/actions/rewards/flags written to HBM"
+               if rollout_mode else "pbn_step per step"))
 
 
 def gather_pass(env, args, world, dev, stream):
@@ -181,6 +245,12 @@ def main():
     env = VectorPBNEnv(spec, args.envs, seed=args.seed, device=dev, env_offset=rank * args.envs,
                        keep_final_state=False)
     env.reset()
+    agent = None
+    if args.workload == "bdq":
+        from pbn_rl_amd.agent import BatchedBDQ, BranchingQNetwork
+
+        torch.manual_seed(0)   # random-init weights of the reference architecture
+        agent = BatchedBDQ(env, BranchingQNetwork((spec.n, spec.n), spec.n + 1, 3), epsilon=args.epsilon)
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.synchronize(dev)
 
@@ -193,6 +263,8 @@ def main():
         """One kernel launch covering k steps of every env."""
         if rollout_mode:
             bufs[k] = env.rollout(k, random_actions=True, keep_obs=True, keep_final=False, out=bufs.get(k))
+        elif agent is not None:
+            agent.step()
         else:
             env.step_flipmask(random_actions=True)
 
@@ -247,7 +319,10 @@ def main():
 
     if rank == 0:
         W = spec.words
-        if rollout_mode:
+        if agent is not None:
+            bytes_launch = None
+            kernel = "BDQ frame (pbn_obs_unpack, BranchingQNetwork fp32 forward, pbn_q_to_flipmask, pbn_step)"
+        elif rollout_mode:
             bytes_launch = env.n_alloc * rollout_bytes_per_env(W, chunk)
             kernel = "pbn_rollout_pipe (rollout, %d steps/launch)" % chunk
         else:
@@ -255,12 +330,28 @@ def main():
             kernel = "pbn_step_wave (single step)"
         # the timed plan's launches are full chunks except possibly the last
         full_launch_ms = launch_ms * len(plan) * chunk / args.steps if rollout_mode else launch_ms
-        achieved = bytes_launch / (full_launch_ms * 1e-3) / 1e9
         traffic = None
-        pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.network}_{args.envs}_{args.mode}.json")
-        if os.path.exists(pmc_path):
-            with open(pmc_path) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+        if agent is not None:
+            # the frame is dominated by the Q-network's fp32 GEMMs: price it against the
+            # FP32 matrix peak (MI355X_MICROARCH.md: 157.3 TFLOP/s)
+            flops = env.n_alloc * qnet_flops_per_env(spec.n)
+            achieved = flops / (full_launch_ms * 1e-3) / 1e12
+            roofline = {"bound": "mfma", "achieved": achieved, "peak": FP32_MATRIX_TFLOPS, "unit": "TFLOP/s",
+                        "frac": achieved / FP32_MATRIX_TFLOPS, "traffic": None, "kernel": kernel,
+                        "launch_ms": full_launch_ms, "flops_per_launch": flops,
+                        "note": "one launch = one whole BDQ frame (4+ kernels); achieved = Q-network FLOPs / "
+                                "frame time"}
+        else:
+            achieved = bytes_launch / (full_launch_ms * 1e-3) / 1e9
+            pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.network}_{args.envs}_{args.mode}.json")
+            if os.path.exists(pmc_path):
+                with open(pmc_path) as f:
+                    traffic = json.load(f).get("hbm_bytes_per_launch")
+            roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                        "kernel": kernel, "launch_ms": full_launch_ms,
+                        "bytes_per_launch": bytes_launch,
+                        "note": "VALU-bound (Philox volume), see DESIGN.md 'What bounds it'"}
         out = {
             "metric": "env steps/sec (batched PBN transitions), Bittner-28 at 1/2/4/8 GPUs"
             if args.network == "pbn28" else f"env steps/sec (batched PBN transitions), {args.network}",
@@ -273,26 +364,21 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u32",
+            "dtype": "f32+u32" if agent is not None else "u32",
             "data": "synthetic",
-            "config": {"workload": f"{args.network} x {args.envs} envs per GPU, in-kernel random interventions "
-                                   f"(3 uniform actions/env/step), autoreset, horizon {args.horizon}, "
-                                   f"p={args.perturbation}, prob_bits={args.prob_bits}; "
-                                   + (f"pbn_rollout, {chunk} steps/launch, per-step obs/actions/rewards/flags "
-                                      f"written to HBM" if rollout_mode else "pbn_step per step"),
+            "config": {"workload": workload_text(args, chunk, rollout_mode),
                        "network": args.network, "envs_per_gpu": args.envs, "global_envs": world * args.envs,
                        "parallelism": f"env-shard x{world}", "launch": "hipGraph" if use_graph else "eager"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": kernel, "launch_ms": full_launch_ms,
-                         "bytes_per_launch": bytes_launch,
-                         "note": "VALU-bound (Philox volume), see DESIGN.md 'What bounds it'"},
+            "roofline": roofline,
         }
         if with_gather is not None:
             out["value_with_gather"] = with_gather
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(spec, args.envs, args.cpu_seconds)
-            out["cpu_baseline_python"] = python_baseline(spec)
+            if agent is not None:
+                out["cpu_baseline"] = cpu_baseline_bdq(spec, agent.q, args.cpu_seconds)
+            else:
+                out["cpu_baseline"] = cpu_baseline(spec, args.envs, args.cpu_seconds)
+                out["cpu_baseline_python"] = python_baseline(spec)
         print(json.dumps(out), flush=True)
     env.close()
     if world > 1:

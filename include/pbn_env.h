@@ -169,6 +169,38 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
 int pbn_state_histogram(const uint32_t* d_states, int64_t n_rows, int64_t n_cols, int64_t row_stride,
                         int32_t n_bits, uint32_t* d_hist, void* stream);
 
+/*
+ * Agent edges of the batched BDQ frame loop (bdq_model/__init__.py:69-98,172-177;
+ * SURVEY.md 8(d) config 5).  The Q-network forward itself runs in PyTorch between them.
+ *
+ * pbn_obs_unpack replaces the host np.stack((state, target)) -> float tensor of
+ * BranchingDQN.predict (bdq_model/__init__.py:92-93) for a whole batch:
+ *   d_obs  out  float [2][n][N]: [0][e][i] = bit i of env e's state, [1][e][i] = bit i of
+ *               the first state of env e's target attractor (0 without a target)
+ *               -- the (2, B, N) input of BranchingQNetwork (bdq_model/network.py:55-57).
+ * n_envs multiple of 32, n_envs * n_nodes < 2^31, d_obs 16-byte aligned.
+ */
+int pbn_obs_unpack(const pbn_net* net, int64_t n_envs, const uint32_t* d_state, const uint8_t* d_target,
+                   float* d_obs, void* stream);
+
+/*
+ * pbn_q_to_flipmask replaces epsilon-greedy predict + list(action.unique()) + the env's
+ * action decoding (bdq_model/__init__.py:69-98,176; action a > 0 flips node a-1, :81-84):
+ *   d_q         in   float [n][n_branches][n_actions], n_actions == n_nodes + 1, 16-byte aligned
+ *   epsilon     explore with probability epsilon: env e explores iff EXPLORE word 0 <
+ *               floor(epsilon * 2^32); its branch k action is then
+ *               ((word (1 + k/3) >> 10(k%3)) & 1023) * (N+1) >> 10  (uniform over [0, N],
+ *               as np.random.randint at :76); otherwise argmax over the branch (first
+ *               maximum, NaN counts as the maximum: torch.argmax at :96).  EXPLORE = Philox
+ *               stream 4 keyed by (seed, global env id, step), as in DESIGN.md.
+ *   d_flipmask  out  uint32 [W][n]: bit a-1 set for every distinct action a > 0
+ *   d_actions   out  int32 [n][n_branches] (nullable): the chosen actions
+ * n_branches 1..9.  n_envs and env_offset multiples of 32.
+ */
+int pbn_q_to_flipmask(const pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs,
+                      int32_t n_branches, int32_t n_actions, const float* d_q, float epsilon,
+                      uint32_t* d_flipmask, int32_t* d_actions, void* stream);
+
 const char* pbn_last_error(void);
 int pbn_abi_version(void);
 

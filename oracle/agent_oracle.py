@@ -1,0 +1,91 @@
+"""numpy restatement of the agent-edge kernels (pbn_obs_unpack, pbn_q_to_flipmask).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/ as the checker of
+pbn_rl_amd/csrc/pbn_agent.hip.  Follows the frame loop of the reference:
+  - observation = np.stack((state, target)) as float (bdq_model/__init__.py:92-93), batched
+    to (2, n, N); target = the first state of the env's target attractor;
+  - epsilon-greedy: explore -> uniform ints in [0, N] per branch (:74-76), else
+    argmax of each branch's Q row (:95-96, torch.argmax: first maximum, NaN is the maximum);
+  - env actions: list(action.unique()) (:176), a > 0 flips node a-1 (:81-84).
+The explore draws follow DESIGN.md (Philox4x32-10, stream EXPLORE = 4); Philox is vectorised
+here over envs and checked against oracle/pyoracle.philox4x32_10 by the tests.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+M0, M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+W0, W1 = 0x9E3779B9, 0xBB67AE85
+EXPLORE = 4
+
+
+def philox_vec(c0, c1, c2, c3, k0: int, k1: int):
+    """Philox4x32-10 over arrays of counters (uint32), scalar key."""
+    c0, c1, c2, c3 = (np.asarray(c, dtype=np.uint64) & np.uint64(0xFFFFFFFF) for c in (c0, c1, c2, c3))
+    mask = np.uint64(0xFFFFFFFF)
+    for _ in range(10):
+        p0 = M0 * c0
+        p1 = M1 * c2
+        n0 = (p1 >> np.uint64(32)) ^ c1 ^ np.uint64(k0)
+        n2 = (p0 >> np.uint64(32)) ^ c3 ^ np.uint64(k1)
+        c0, c1, c2, c3 = n0 & mask, p1 & mask, n2 & mask, p0 & mask
+        k0 = (k0 + W0) & 0xFFFFFFFF
+        k1 = (k1 + W1) & 0xFFFFFFFF
+    return [c.astype(np.uint32) for c in (c0, c1, c2, c3)]
+
+
+def explore_words(seed: int, step: int, env_offset: int, n: int):
+    ge = np.arange(n, dtype=np.uint64) + np.uint64(env_offset)
+    c0 = ge & np.uint64(0xFFFFFFFF)
+    c1 = np.full(n, step & 0xFFFFFFFF, dtype=np.uint64)
+    c2 = np.full(n, EXPLORE << 28, dtype=np.uint64)
+    c3 = ((ge >> np.uint64(32)) & np.uint64(0xFFFF)) | np.uint64(((step >> 32) & 0xFFFF) << 16)
+    return philox_vec(c0, c1, c2, c3, seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+
+
+def obs_unpack(spec, state: np.ndarray, target: np.ndarray) -> np.ndarray:
+    """state (W, n) uint32, target (n,) uint8 -> (2, n, N) float32."""
+    N = spec.n
+    W, n = state.shape
+    bits = (state.T[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1          # (n, W, 32)
+    s = bits.reshape(n, 32 * W)[:, :N].astype(np.float32)
+    first = np.zeros((len(spec.attractors) + 1, N), dtype=np.float32)            # last row: no target
+    for a, att in enumerate(spec.attractors):
+        first[a] = np.asarray(att[0], dtype=np.float32)
+    tg = np.asarray(target).astype(np.int64)
+    tg = np.where(tg < len(spec.attractors), tg, len(spec.attractors))
+    return np.stack([s, first[tg]])
+
+
+def argmax_torch(q: np.ndarray) -> np.ndarray:
+    """argmax over the last axis with torch.argmax's tie and NaN rules."""
+    nan = np.isnan(q)
+    has_nan = nan.any(axis=-1)
+    first_nan = np.argmax(nan, axis=-1)
+    plain = np.argmax(np.where(nan, -np.inf, q), axis=-1)   # np.argmax: first maximum
+    return np.where(has_nan, first_nan, plain)
+
+
+def q_to_flipmask(spec, q: np.ndarray, seed: int, step: int, env_offset: int, epsilon: float):
+    """q (n, K, N+1) float32 -> (flipmask (W, n) uint32, actions (n, K) int32)."""
+    n, K, A = q.shape
+    N, W = spec.n, spec.words
+    assert A == N + 1
+    w = explore_words(seed, step, env_offset, n)
+    eps_u = int(np.floor(np.float64(np.float32(epsilon)) * 4294967296.0))
+    explore = w[0].astype(np.uint64) < np.uint64(eps_u) if eps_u < (1 << 32) else np.ones(n, dtype=bool)
+    greedy = argmax_torch(q)                                                     # (n, K)
+    rnd = np.zeros((n, K), dtype=np.int64)
+    for k in range(K):
+        word = w[1 + k // 3].astype(np.uint64)
+        rnd[:, k] = (((word >> np.uint64(10 * (k % 3))) & np.uint64(1023)) * np.uint64(N + 1)) >> np.uint64(10)
+    actions = np.where(explore[:, None], rnd, greedy).astype(np.int32)
+    flip = np.zeros((W, n), dtype=np.uint32)
+    for k in range(K):
+        a = actions[:, k].astype(np.int64)
+        hit = a > 0
+        node = np.where(hit, a - 1, 0)
+        for ww in range(W):
+            sel = hit & ((node >> 5) == ww)
+            flip[ww] |= np.where(sel, np.left_shift(np.uint32(1), (node & 31).astype(np.uint32)), np.uint32(0))
+    return flip, actions

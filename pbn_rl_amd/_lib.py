@@ -24,7 +24,8 @@ FLAG_PERTURBED = 8
 FLAG_RESET = 16
 
 EXPORTS = ["pbn_net_create", "pbn_net_destroy", "pbn_net_words", "pbn_reset", "pbn_step", "pbn_rollout",
-           "pbn_state_histogram", "pbn_last_error", "pbn_abi_version"]
+           "pbn_state_histogram", "pbn_obs_unpack", "pbn_q_to_flipmask", "pbn_last_error", "pbn_abi_version"]
+SOURCES = ["pbn_env.hip", "pbn_agent.hip"]
 
 _lib: Optional[ctypes.CDLL] = None
 
@@ -36,9 +37,9 @@ class PbnError(RuntimeError):
 def build(verbose: bool = False, out: str = LIB_PATH, defines=()) -> str:
     """Compile csrc/pbn_env.hip for gfx950 into pbn_rl_amd/libpbn_env.so (in-tree).
     ``defines`` builds a diagnostic variant (e.g. PBN_STAMPS) into another path."""
-    src = os.path.join(SRC_DIR, "pbn_env.hip")
+    srcs = [os.path.join(SRC_DIR, f) for f in SOURCES]
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-unused-result", *[f"-D{d}" for d in defines], "-o", out + ".tmp", src]
+           "-Wno-unused-result", *[f"-D{d}" for d in defines], "-o", out + ".tmp", *srcs]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
@@ -69,6 +70,11 @@ def load() -> ctypes.CDLL:
     L.pbn_rollout.restype = ctypes.c_int
     L.pbn_state_histogram.argtypes = [vp, i64, i64, i64, ctypes.c_int32, vp, vp]
     L.pbn_state_histogram.restype = ctypes.c_int
+    L.pbn_obs_unpack.argtypes = [vp, i64, vp, vp, vp, vp]
+    L.pbn_obs_unpack.restype = ctypes.c_int
+    L.pbn_q_to_flipmask.argtypes = [vp, u64, u64, u64, i64, ctypes.c_int32, ctypes.c_int32, vp, ctypes.c_float,
+                                    vp, vp, vp]
+    L.pbn_q_to_flipmask.restype = ctypes.c_int
     L.pbn_last_error.argtypes = []
     L.pbn_last_error.restype = ctypes.c_char_p
     L.pbn_abi_version.argtypes = []

@@ -1,0 +1,151 @@
+"""Batched BDQ frame loop on the GPU.
+
+The reference steps one env per frame: ``BranchingDQN.predict`` stacks (state, target) on the
+host into a float (2, 1, N) tensor, runs ``BranchingQNetwork``, takes argmax over each of the
+3 action branches (bdq_model/__init__.py:69-98), and ``env.step(list(action.unique()))``
+flips node a-1 for every action a > 0 (:81-84,176-177).  Here one frame covers a whole
+``VectorPBNEnv`` batch, and nothing leaves HBM:
+
+    pbn_obs_unpack      packed state words + target id -> fp32 (2, n, N)       (HIP)
+    BranchingQNetwork   (2, n, N) -> Q (n, 3, N+1)                             (PyTorch-ROCm)
+    pbn_q_to_flipmask   epsilon-greedy over Q -> flip-mask words (W, n)         (HIP)
+    pbn_step            the PBN transition                                      (HIP)
+
+``BranchingQNetwork`` keeps the reference module tree (bdq_model/network.py:24-63), so the
+reference's checkpoints load into it with ``load_state_dict``; its forward computes the
+bilinear layer as one GEMM over the outer product of the two inputs.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from .vector_env import VectorPBNEnv
+
+__all__ = ["MyBilinear", "BranchingQNetwork", "BatchedBDQ", "load_bdq_checkpoint", "formula_weights"]
+
+
+class MyBilinear(nn.Module):
+    """nn.Bilinear over input[0], input[1] (bdq_model/network.py:8-21).  The forward is the
+    same sum, arranged as (B, N1*N2) @ (N1*N2, out) so one GEMM does all of it."""
+
+    def __init__(self, input1_dim: int, input2_dim: int, output_dim: int):
+        super().__init__()
+        self.input1_dim, self.input2_dim, self.output_dim = input1_dim, input2_dim, output_dim
+        self.bilinear = nn.Bilinear(input1_dim, input2_dim, output_dim)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        a, b = x[0], x[1]
+        lead = a.shape[:-1]
+        a2 = a.reshape(-1, self.input1_dim)
+        b2 = b.reshape(-1, self.input2_dim)
+        outer = (a2[:, :, None] * b2[:, None, :]).reshape(a2.shape[0], -1)
+        w = self.bilinear.weight.reshape(self.output_dim, -1)
+        y = torch.addmm(self.bilinear.bias, outer, w.t())
+        return y.reshape(*lead, self.output_dim)
+
+
+def _mlp(i: int, h: int, o: int) -> nn.Sequential:
+    return nn.Sequential(nn.Linear(i, h), nn.LeakyReLU(), nn.Linear(h, o))
+
+
+class BranchingQNetwork(nn.Module):
+    """Dueling branching Q-network of bdq_model/network.py:24-63, same parameter names.
+
+    observation = (N, N) (state and target lengths), action_space_dimension = N + 1,
+    number_of_actions = branches (3 in train_BDQ.py:83).  forward: (2, B, N) -> (B, K, N+1),
+    q = value + advantage - mean(advantage) per branch (:59-61)."""
+
+    def __init__(self, observation: Tuple[int, int], action_space_dimension: int, number_of_actions: int):
+        super().__init__()
+        self.ac_dim = action_space_dimension
+        self.n = number_of_actions
+        s, t = observation
+        self.model = nn.Sequential(MyBilinear(s, t, 256), nn.LeakyReLU(),
+                                   nn.Linear(256, 128), nn.LeakyReLU(),
+                                   nn.Linear(128, 64), nn.LeakyReLU(),
+                                   nn.Linear(64, 32), nn.LeakyReLU())
+        self.value_head = _mlp(32, 64, 1)
+        self.adv_heads = nn.ModuleList([_mlp(32, 64, action_space_dimension) for _ in range(number_of_actions)])
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        h = self.model(x)
+        v = self.value_head(h)                                        # (B, 1)
+        adv = torch.stack([head(h) for head in self.adv_heads], dim=1)   # (B, K, A)
+        return v.unsqueeze(2) + adv - adv.mean(2, keepdim=True)
+
+
+class BatchedBDQ:
+    """The BDQ acting loop over a VectorPBNEnv: obs unpack -> Q -> epsilon-greedy flip masks ->
+    pbn_step, all on the env's device and the current stream (graph-capturable)."""
+
+    def __init__(self, env: VectorPBNEnv, qnet: Optional[BranchingQNetwork] = None, *, branches: int = 3,
+                 epsilon: float = 0.0):
+        self.env = env
+        N = env.n_nodes
+        self.branches = int(branches)
+        self.q = qnet if qnet is not None else BranchingQNetwork((N, N), N + 1, self.branches)
+        self.q = self.q.to(env.device).eval()
+        self.epsilon = float(epsilon)
+        n = env.n_alloc
+        self.obs = torch.empty(2, n, N, dtype=torch.float32, device=env.device)
+        self.actions = torch.empty(n, self.branches, dtype=torch.int32, device=env.device)
+
+    def observe(self) -> torch.Tensor:
+        """(2, n, N) fp32: env states and their target attractors' first states."""
+        env = self.env
+        L = _lib.load()
+        with torch.cuda.device(env.device):
+            _lib.check(L.pbn_obs_unpack(env.net.handle, env.n_alloc, env.state.data_ptr(), env.target.data_ptr(),
+                                        self.obs.data_ptr(), env._stream()), "pbn_obs_unpack")
+        return self.obs
+
+    def act(self, q: torch.Tensor, epsilon: Optional[float] = None) -> torch.Tensor:
+        """Q (n, K, N+1) -> env.flipmask (W, n) and self.actions (n, K), keyed by the env's
+        next step index."""
+        env = self.env
+        q = q.contiguous()
+        if q.shape != (env.n_alloc, self.branches, env.n_nodes + 1):
+            raise ValueError(f"Q must have shape {(env.n_alloc, self.branches, env.n_nodes + 1)}")
+        eps = self.epsilon if epsilon is None else float(epsilon)
+        L = _lib.load()
+        with torch.cuda.device(env.device):
+            _lib.check(L.pbn_q_to_flipmask(env.net.handle, env.seed, env.step_index, env.env_offset, env.n_alloc,
+                                           self.branches, env.n_nodes + 1, q.data_ptr(), eps,
+                                           env.flipmask.data_ptr(), self.actions.data_ptr(), env._stream()),
+                       "pbn_q_to_flipmask")
+        return env.flipmask
+
+    @torch.no_grad()
+    def step(self, epsilon: Optional[float] = None):
+        """One frame for every env; returns (state', reward, flags) views as VectorPBNEnv.step_flipmask."""
+        q = self.q(self.observe())
+        self.act(q, epsilon)
+        return self.env.step_flipmask(use_current=True)
+
+
+def load_bdq_checkpoint(qnet: BranchingQNetwork, path: str, prefix: str = "q.") -> BranchingQNetwork:
+    """Load the ``q`` (or ``target``) network of a reference BranchingDQN checkpoint
+    (``torch.save(self.state_dict())`` at bdq_model/__init__.py:237,240-244) into ``qnet``.
+    Tensors only (``weights_only=True``); nothing in the file is executed."""
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    sub = {k[len(prefix):]: v for k, v in sd.items() if k.startswith(prefix)}
+    if not sub:
+        sub = dict(sd)
+    qnet.load_state_dict(sub)
+    return qnet
+
+
+@torch.no_grad()
+def formula_weights(qnet: nn.Module) -> nn.Module:
+    """Deterministic, RNG-free parameters (sin ramps scaled by 1/sqrt(fan-in)) for golden
+    vectors that must not depend on torch's generator across versions."""
+    for idx, (name, p) in enumerate(sorted(qnet.named_parameters())):
+        k = torch.arange(p.numel(), dtype=torch.float64)
+        fan_in = p.shape[-1] if p.dim() >= 2 else max(1, p.numel())
+        vals = torch.sin(0.731 * k + 0.5 * idx) / (fan_in ** 0.5)
+        p.copy_(vals.reshape(p.shape).to(p.dtype))
+    return qnet

@@ -1,0 +1,176 @@
+// pbn_agent.hip -- the env<->agent edges of the batched BDQ frame loop.
+//
+// The reference's frame loop (bdq_model/__init__.py:172-177) builds the Q-network input on
+// the host (np.stack((state, target)) -> float (2,1,N), :92-93), takes argmax over each of the
+// 3 action branches (:95-96), and hands list(action.unique()) to env.step (:176-177), whose
+// action a > 0 flips node a-1 (:81-84).  Batched on the GPU these become two HBM-bound kernels
+// around the PyTorch Q-network forward:
+//
+//   pbn_obs_unpack     packed state words + target attractor id -> fp32 (2, n, N)
+//   pbn_q_to_flipmask  Q (n, K, N+1) -> epsilon-greedy actions -> flip mask words (W, n)
+//
+// Neither kernel does arithmetic worth an MFMA; both are one pass over their bytes with
+// coalesced 16-byte accesses.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "../../include/pbn_env.h"
+#include "net_view.h"
+#include "philox.h"
+
+namespace {
+
+constexpr int kObsThreads = 256;
+constexpr int kQEnvs = 64;          // envs per q_to_flipmask block (one wave, one env per lane)
+constexpr int kMaxBranches = 9;     // random actions: 3 x 10 bits in each of EXPLORE words 1..3
+
+// out[p][e][i], p = 0: bit i of env e's state, p = 1: bit i of the first state of env e's
+// target attractor (all zeros without a target).  Four consecutive (e, i) elements per
+// thread, written as one float4 per plane; n * N is a multiple of 4 because n is a
+// multiple of 32.
+__global__ void __launch_bounds__(kObsThreads) obs_unpack_kernel(const uint32_t* __restrict__ state,
+                                                                 const uint8_t* __restrict__ target,
+                                                                 const int32_t* __restrict__ att_start,
+                                                                 const uint32_t* __restrict__ att_states,
+                                                                 int n_attr, int N, int W, uint32_t n,
+                                                                 float* __restrict__ out) {
+  const uint32_t total4 = n * (uint32_t)N / 4u;
+  float4* out_s = reinterpret_cast<float4*>(out);
+  float4* out_t = reinterpret_cast<float4*>(out + (size_t)n * N);
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < total4; q += gridDim.x * blockDim.x) {
+    const uint32_t f = 4u * q;
+    uint32_t e = f / (uint32_t)N;
+    int i = (int)(f - e * (uint32_t)N);
+    float vs[4], vt[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t sw = state[(size_t)(i >> 5) * n + e];
+      const uint32_t tg = target[e];
+      const uint32_t tw = tg < (uint32_t)n_attr ? att_states[(size_t)att_start[tg] * W + (i >> 5)] : 0u;
+      vs[r] = (float)((sw >> (i & 31)) & 1u);
+      vt[r] = (float)((tw >> (i & 31)) & 1u);
+      if (++i == N) {
+        i = 0;
+        ++e;
+      }
+    }
+    out_s[q] = make_float4(vs[0], vs[1], vs[2], vs[3]);
+    out_t[q] = make_float4(vt[0], vt[1], vt[2], vt[3]);
+  }
+}
+
+// torch.argmax semantics: the first maximal index; NaN counts as the maximum
+__device__ __forceinline__ int argmax_row(const float* __restrict__ r, int A) {
+  float best = r[0];
+  int bi = 0;
+  for (int j = 1; j < A; ++j) {
+    const float v = r[j];
+    const bool take = !isnan(best) && (isnan(v) || v > best);
+    best = take ? v : best;
+    bi = take ? j : bi;
+  }
+  return bi;
+}
+
+// One wave per 64 envs: the block's Q rows (contiguous, 64 * K * A floats) are staged through
+// LDS with coalesced float4 loads, then lane e reduces its K rows.  Row stride K * A words:
+// odd for the kaban networks' K = 3, so the per-lane row reads spread over the banks.
+__global__ void __launch_bounds__(kQEnvs) q_to_flipmask_kernel(const float* __restrict__ q, int K, int A, int N,
+                                                               int W, int64_t n, uint64_t seed, uint64_t step,
+                                                               uint64_t env_offset, uint64_t eps_u,
+                                                               uint32_t* __restrict__ flipmask,
+                                                               int32_t* __restrict__ actions) {
+  extern __shared__ float sq[];
+  const int64_t e0 = (int64_t)blockIdx.x * kQEnvs;
+  const int row = K * A;
+  const int n_blk = (int)((n - e0) < kQEnvs ? (n - e0) : kQEnvs);   // 32 or 64
+  const float4* src = reinterpret_cast<const float4*>(q + (size_t)e0 * row);
+  const int words4 = n_blk * row / 4;
+  for (int k = threadIdx.x; k < words4; k += kQEnvs) reinterpret_cast<float4*>(sq)[k] = src[k];
+  __syncthreads();
+  if ((int)threadIdx.x >= n_blk) return;
+  const int64_t e = e0 + threadIdx.x;
+  const uint64_t ge = env_offset + (uint64_t)e;
+  const pbn::Word4 r = pbn::draw(seed, ge, step, pbn::kStreamExplore, 0);
+  const bool explore = (uint64_t)r.x < eps_u;
+  const uint32_t rw[3] = {r.y, r.z, r.w};
+  uint32_t m[4] = {0u, 0u, 0u, 0u};
+  const float* my = sq + (size_t)threadIdx.x * row;
+  for (int k = 0; k < K; ++k) {
+    int a;
+    if (explore) {
+      a = (int)((((rw[k / 3] >> (10 * (k % 3))) & 1023u) * (uint32_t)(N + 1)) >> 10);
+    } else {
+      a = argmax_row(my + k * A, A);
+    }
+    if (actions) actions[e * K + k] = a;
+    if (a > 0 && a <= N) {   // a > 0 flips node a-1, once however often it repeats
+      const int node = a - 1;
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+        if (w == (node >> 5)) m[w] |= 1u << (node & 31);
+    }
+  }
+#pragma unroll
+  for (int w = 0; w < 4; ++w)
+    if (w < W) flipmask[(size_t)w * n + e] = m[w];
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int pbn_obs_unpack(const pbn_net* net, int64_t n_envs, const uint32_t* d_state, const uint8_t* d_target,
+                   float* d_obs, void* stream) {
+  pbn::NetView v;
+  int rc = pbn::net_view(net, &v);
+  if (rc) return rc;
+  if ((rc = pbn::check_device(net))) return rc;
+  if (n_envs < 0 || (n_envs & 31)) return pbn::set_error(PBN_EINVAL, "n_envs must be a non-negative multiple of 32");
+  if ((int64_t)n_envs * v.n_nodes >= ((int64_t)1 << 31)) return pbn::set_error(PBN_EINVAL, "n_envs * n_nodes >= 2^31");
+  if (n_envs == 0) return PBN_OK;
+  if (!d_state || !d_target || !d_obs) return pbn::set_error(PBN_EINVAL, "null buffer");
+  if (!aligned16(d_obs)) return pbn::set_error(PBN_EINVAL, "d_obs must be 16-byte aligned");
+  const int64_t total4 = n_envs * v.n_nodes / 4;
+  const unsigned blocks = (unsigned)std::min<int64_t>((total4 + kObsThreads - 1) / kObsThreads, 8192);
+  hipLaunchKernelGGL(obs_unpack_kernel, dim3(blocks), dim3(kObsThreads), 0, (hipStream_t)stream, d_state, d_target,
+                     v.att_start, v.att_states, v.n_attr, v.n_nodes, v.W, (uint32_t)n_envs, d_obs);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return pbn::set_error(PBN_EDEVICE, hipGetErrorString(e));
+  return PBN_OK;
+}
+
+int pbn_q_to_flipmask(const pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs,
+                      int32_t n_branches, int32_t n_actions, const float* d_q, float epsilon, uint32_t* d_flipmask,
+                      int32_t* d_actions, void* stream) {
+  pbn::NetView v;
+  int rc = pbn::net_view(net, &v);
+  if (rc) return rc;
+  if ((rc = pbn::check_device(net))) return rc;
+  if (n_envs < 0 || (n_envs & 31) || (env_offset & 31))
+    return pbn::set_error(PBN_EINVAL, "n_envs and env_offset must be multiples of 32");
+  if (n_branches < 1 || n_branches > kMaxBranches) return pbn::set_error(PBN_EINVAL, "n_branches must be 1..9");
+  if (n_actions != v.n_nodes + 1) return pbn::set_error(PBN_EINVAL, "n_actions must be n_nodes + 1");
+  if (!(epsilon >= 0.f && epsilon <= 1.f)) return pbn::set_error(PBN_EINVAL, "epsilon must be in [0, 1]");
+  if (n_envs == 0) return PBN_OK;
+  if (!d_q || !d_flipmask) return pbn::set_error(PBN_EINVAL, "null buffer");
+  if (!aligned16(d_q)) return pbn::set_error(PBN_EINVAL, "d_q must be 16-byte aligned");
+  // explore iff word 0 < floor(epsilon * 2^32): epsilon = 1 always explores, 0 never
+  const uint64_t eps_u = (uint64_t)floor((double)epsilon * 4294967296.0);
+  const size_t lds = (size_t)kQEnvs * n_branches * n_actions * sizeof(float);
+  if (lds > 64 * 1024) return pbn::set_error(PBN_EINVAL, "n_branches * n_actions too large");
+  const unsigned blocks = (unsigned)((n_envs + kQEnvs - 1) / kQEnvs);
+  hipLaunchKernelGGL(q_to_flipmask_kernel, dim3(blocks), dim3(kQEnvs), lds, (hipStream_t)stream, d_q, n_branches,
+                     n_actions, v.n_nodes, v.W, n_envs, seed, step, env_offset, eps_u, d_flipmask, d_actions);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return pbn::set_error(PBN_EDEVICE, hipGetErrorString(e));
+  return PBN_OK;
+}
+
+}  // extern "C"

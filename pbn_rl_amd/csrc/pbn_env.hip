@@ -29,6 +29,7 @@
 
 #include "../../include/pbn_env.h"
 #include "bitslice.h"
+#include "net_view.h"
 #include "philox.h"
 
 using pbn::bfi;
@@ -1207,6 +1208,32 @@ struct pbn_net {
   int32_t* d_att_start = nullptr;
   uint32_t* d_att_states = nullptr;
 };
+
+namespace pbn {
+
+int set_error(int code, const char* msg) { return fail(code, msg); }
+
+int net_view(const pbn_net* net, NetView* v) {
+  if (!net || !v) return fail(PBN_EINVAL, "null net");
+  v->device = net->device;
+  v->n_nodes = net->n_nodes;
+  v->W = net->W;
+  v->n_attr = net->n_attr;
+  v->n_states = net->n_states;
+  v->att_start = net->d_att_start;
+  v->att_states = net->d_att_states;
+  return PBN_OK;
+}
+
+int check_device(const pbn_net* net) {
+  if (!net) return fail(PBN_EINVAL, "null net");
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || dev != net->device)
+    return fail(PBN_EDEVICE, "current device differs from the net's device");
+  return PBN_OK;
+}
+
+}  // namespace pbn
 
 namespace {
 

@@ -11,7 +11,9 @@
 
 namespace pbn {
 
-enum : uint32_t { kStreamSel = 0, kStreamEnv = 1, kStreamPert = 2, kStreamReset = 3 };
+// EXPLORE = 4: epsilon-greedy draws of pbn_q_to_flipmask (per env; word 0 = explore test,
+// words 1-3 = the random actions, 10 bits each)
+enum : uint32_t { kStreamSel = 0, kStreamEnv = 1, kStreamPert = 2, kStreamReset = 3, kStreamExplore = 4 };
 
 struct Word4 {
   uint32_t x, y, z, w;

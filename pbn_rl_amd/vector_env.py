@@ -117,12 +117,17 @@ class VectorPBNEnv:
         self.step_index += 1
         return self.state[:, : self.num_envs], self.target[: self.num_envs]
 
-    def step_flipmask(self, flipmask: Optional[torch.Tensor] = None, random_actions: bool = False):
-        """One transition for every env; returns views (state', reward, flags)."""
+    def step_flipmask(self, flipmask: Optional[torch.Tensor] = None, random_actions: bool = False,
+                      use_current: bool = False):
+        """One transition for every env; returns views (state', reward, flags).
+        ``use_current``: step with what ``self.flipmask`` already holds (e.g. written by
+        pbn_q_to_flipmask), for all ``n_alloc`` envs."""
         L = _lib.load()
         mode = _lib.MODE_AUTORESET if self.autoreset else 0
         if random_actions:
             mode |= _lib.MODE_RANDOM_ACTIONS
+        elif use_current:
+            pass
         elif flipmask is not None:
             if flipmask.shape != (self.words, self.num_envs):
                 raise ValueError(f"flipmask must have shape {(self.words, self.num_envs)}")

@@ -1,0 +1,133 @@
+"""Config 5 agent edges on the GPU, through the C-ABI: pbn_obs_unpack and pbn_q_to_flipmask
+are bit-exact against oracle/agent_oracle.py, and the batched BDQ frame loop
+(BatchedBDQ: unpack -> Q-network -> epsilon-greedy flip masks -> pbn_step) is bit-exact
+against the oracle chain fed with the same Q values."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import agent_oracle, oracle
+from pbn_rl_amd import _lib
+from pbn_rl_amd.agent import BatchedBDQ, BranchingQNetwork
+from pbn_rl_amd.attractors import load_attractors
+from pbn_rl_amd.network import load_network
+from pbn_rl_amd.spec import EnvSpec
+from pbn_rl_amd.vector_env import VectorPBNEnv
+
+pytestmark = pytest.mark.gpu
+
+
+def make_spec(name, **kw):
+    return EnvSpec(load_network(name), load_attractors(name), **kw)
+
+
+def u32(x):
+    return x.cpu().numpy().view(np.uint32)
+
+
+@pytest.mark.parametrize("name,n", [("pbn7", 96), ("pbn28", 4096), ("pbn70", 2080)])
+def test_obs_unpack_exact(name, n):
+    spec = make_spec(name)
+    env = VectorPBNEnv(spec, n, seed=5)
+    rng = np.random.default_rng(1)
+    W = spec.words
+    st = rng.integers(0, 2 ** 32, size=(W, n), dtype=np.uint64).astype(np.uint32)
+    if spec.n % 32:
+        st[W - 1] &= np.uint32((1 << (spec.n % 32)) - 1)
+    tg = rng.integers(0, len(spec.attractors), size=n).astype(np.uint8)
+    tg[::7] = 0xFF
+    env.set_state(torch.from_numpy(st.view(np.int32)).cuda(), torch.from_numpy(tg).cuda())
+    agent = BatchedBDQ(env, BranchingQNetwork((spec.n, spec.n), spec.n + 1, 3))
+    obs = agent.observe()
+    torch.cuda.synchronize()
+    assert np.array_equal(obs.cpu().numpy(), agent_oracle.obs_unpack(spec, st, tg))
+
+
+@pytest.mark.parametrize("name,K,eps", [("pbn28", 3, 0.0), ("pbn28", 3, 0.3), ("pbn28", 3, 1.0),
+                                        ("pbn70", 3, 0.25), ("pbn7", 1, 0.5), ("pbn7", 5, 0.1)])
+def test_q_to_flipmask_exact(name, K, eps):
+    spec = make_spec(name)
+    n = 4160
+    env = VectorPBNEnv(spec, n, seed=77, env_offset=320)
+    env.step_index = 9
+    rng = np.random.default_rng(K)
+    q = rng.integers(-3, 4, size=(n, K, spec.n + 1)).astype(np.float32)   # many ties
+    q[::13, 0, 2] = np.nan
+    q[::17, -1, :] = np.nan
+    agent = BatchedBDQ(env, BranchingQNetwork((spec.n, spec.n), spec.n + 1, K), branches=K)
+    fm = agent.act(torch.from_numpy(q).cuda(), eps)
+    torch.cuda.synchronize()
+    flip, act = agent_oracle.q_to_flipmask(spec, q, 77, 9, 320, eps)
+    assert np.array_equal(agent.actions.cpu().numpy(), act)
+    assert np.array_equal(u32(fm), flip)
+    if eps == 0.0:
+        assert np.array_equal(act, torch.argmax(torch.from_numpy(q), dim=2).numpy())
+
+
+def test_q_to_flipmask_rejects_bad_arguments():
+    spec = make_spec("pbn28")
+    env = VectorPBNEnv(spec, 64)
+    L = _lib.load()
+    q = torch.zeros(64, 3, 29, device="cuda")
+    fm = torch.zeros(1, 64, dtype=torch.int32, device="cuda")
+    h = env.net.handle
+    assert L.pbn_q_to_flipmask(h, 0, 0, 0, 64, 3, 28, q.data_ptr(), 0.0, fm.data_ptr(), None, None) == -22
+    assert L.pbn_q_to_flipmask(h, 0, 0, 0, 64, 10, 29, q.data_ptr(), 0.0, fm.data_ptr(), None, None) == -22
+    assert L.pbn_q_to_flipmask(h, 0, 0, 0, 64, 3, 29, q.data_ptr(), ctypes.c_float(1.5), fm.data_ptr(), None,
+                               None) == -22
+    assert L.pbn_q_to_flipmask(h, 0, 0, 0, 40, 3, 29, q.data_ptr(), 0.0, fm.data_ptr(), None, None) == -22
+    assert L.pbn_q_to_flipmask(h, 0, 0, 0, 64, 3, 29, q.data_ptr() + 4, 0.0, fm.data_ptr(), None, None) == -22
+    assert L.pbn_obs_unpack(h, 64, None, None, None, None) == -22
+
+
+@pytest.mark.parametrize("eps", [0.0, 0.2])
+def test_bdq_frame_loop_matches_oracle_chain(eps):
+    spec = make_spec("pbn28")
+    n, seed, frames = 2048, 31, 12
+    torch.manual_seed(0)
+    env = VectorPBNEnv(spec, n, seed=seed)
+    agent = BatchedBDQ(env, BranchingQNetwork((28, 28), 29, 3), epsilon=eps)
+    env.reset()
+    st, tg, t = oracle.reset(spec, seed, 0, 0, n)
+    for k in range(frames):
+        step = env.step_index
+        obs = agent.observe()
+        with torch.no_grad():
+            q = agent.q(obs)
+        agent.act(q)
+        state, reward, flags = env.step_flipmask(use_current=True)
+        torch.cuda.synchronize()
+        assert np.array_equal(obs.cpu().numpy(), agent_oracle.obs_unpack(spec, st, tg)), f"obs frame {k}"
+        flip, _ = agent_oracle.q_to_flipmask(spec, q.cpu().numpy(), seed, step, 0, eps)
+        ref = oracle.step(spec, seed, step, 0, st, flip, tg, t, 1)
+        assert np.array_equal(u32(env.flipmask), flip), f"flipmask frame {k}"
+        assert np.array_equal(u32(state), ref["state_out"]), f"state frame {k}"
+        assert np.array_equal(reward.cpu().numpy(), ref["reward"])
+        assert np.array_equal(flags.cpu().numpy(), ref["flags"])
+        st, tg, t = ref["state_out"], ref["target"], ref["t"]
+
+
+def test_bdq_step_graph_capture():
+    """The whole frame (unpack, Q-network, flip masks, step) replays from one hipGraph."""
+    spec = make_spec("pbn28")
+    env = VectorPBNEnv(spec, 1024, seed=3, keep_final_state=False)
+    torch.manual_seed(0)
+    agent = BatchedBDQ(env, BranchingQNetwork((28, 28), 29, 3))
+    env.reset()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        agent.step()
+        torch.cuda.synchronize()
+        ref_env = VectorPBNEnv(spec, 1024, seed=3, keep_final_state=False)
+        ref_env.set_state(env.state.clone(), env.target.clone(), env.t.clone())
+        ref_env.step_index = env.step_index
+        ref_agent = BatchedBDQ(ref_env, agent.q)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            agent.step()
+        g.replay()
+        ref_agent.step()
+        torch.cuda.synchronize()
+    assert torch.equal(env.state, ref_env.state)
