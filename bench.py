@@ -32,6 +32,9 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FP32_MATRIX_TFLOPS = 157.3  # MI355X FP32 MFMA/vector peak (MI355X_MICROARCH.md)
+# VALU issue: 256 CUs x 4 SIMD-32 x 2.4 GHz, one wave64 instruction per 2 cycles per SIMD
+# (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles")
+VALU_WAVE_INSTS_PER_S = 256 * 4 * 2.4e9 / 2
 
 
 def parse():
@@ -344,14 +347,27 @@ def main():
         else:
             achieved = bytes_launch / (full_launch_ms * 1e-3) / 1e9
             pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.network}_{args.envs}_{args.mode}.json")
+            valu_launch = None
             if os.path.exists(pmc_path):
                 with open(pmc_path) as f:
-                    traffic = json.load(f).get("hbm_bytes_per_launch")
+                    pmc = json.load(f)
+                traffic = pmc.get("hbm_bytes_per_launch")
+                valu_launch = pmc.get("valu_insts_per_launch")
             roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                         "kernel": kernel, "launch_ms": full_launch_ms,
                         "bytes_per_launch": bytes_launch,
                         "note": "VALU-bound (Philox volume), see DESIGN.md 'What bounds it'"}
+            if valu_launch:
+                # the compute side of the same kernel: wave-level VALU instructions per launch
+                # (rocprofv3 SQ_INSTS_VALU, profiles/) over this run's launch time, against the
+                # issue rate of one wave64 instruction per 2 cycles per SIMD
+                achieved_valu = valu_launch / (full_launch_ms * 1e-3)
+                roofline["valu"] = {"achieved": achieved_valu, "peak": VALU_WAVE_INSTS_PER_S,
+                                    "unit": "wave-instructions/s", "frac": achieved_valu / VALU_WAVE_INSTS_PER_S,
+                                    "insts_per_launch": valu_launch,
+                                    "note": "issue slots only: a v_mad_u64_u32 (20 per Philox call) holds its "
+                                            "SIMD longer than one slot"}
         out = {
             "metric": "env steps/sec (batched PBN transitions), Bittner-28 at 1/2/4/8 GPUs"
             if args.network == "pbn28" else f"env steps/sec (batched PBN transitions), {args.network}",

@@ -4,7 +4,8 @@
 
 HBM bytes per launch of the step kernel = 2 x FETCH_SIZE + WRITE_SIZE (kB units), the gfx950
 correction of MI355X_MICROARCH.md's HBM section.  bench.py reads `hbm_bytes_per_launch` as
-roofline.traffic.
+roofline.traffic.  With the SQ pass (pmc_sq/), also the wave-level VALU / SALU instruction
+counts per launch, which bench.py turns into the VALU issue fraction.
 """
 import argparse
 import csv
@@ -45,6 +46,11 @@ def main():
            "hbm_read_bytes_per_launch": f * 2 * 1024, "hbm_write_bytes_per_launch": w * 1024,
            "hbm_bytes_per_launch": (2 * f + w) * 1024, "algorithmic_bytes_per_launch": alg,
            "note": "the read side is 4-B and 1-B loads plus table reads, a width the guide leaves uncalibrated"}
+    sq = os.path.join(args.run_dir, "pmc_sq", "run_counter_collection.csv")
+    if os.path.exists(sq):
+        for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES", "SQ_BUSY_CYCLES"):
+            out[c + "_per_launch"] = mean_counter(sq, c)[0]
+        out["valu_insts_per_launch"] = out["SQ_INSTS_VALU_per_launch"]
     path = args.out or os.path.join("profiles", f"pmc_{args.network}_{args.envs}_{args.mode}.json")
     with open(path, "w") as fo:
         json.dump(out, fo, indent=1)

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--network", default="pbn28")
     ap.add_argument("--pipe", action="store_true", help="pipelined rollout kernel: per-role clocks of iteration 10")
+    ap.add_argument("--plane", action="store_true", help="plane-resident rollout kernel (4 roles; implies --pipe)")
     ap.add_argument("--rollout", type=int, default=0,
                     help="stamp a pbn_rollout launch of this many steps (phases of its last step)")
     args = ap.parse_args()
@@ -34,6 +35,8 @@ def main():
         _lib.build(out=STAMP_LIB, defines=["PBN_STAMPS"], verbose=True)
         return
     os.environ["PBN_LIB"] = STAMP_LIB
+    if args.plane or args.pipe:
+        os.environ["PBN_ROLL"] = "plane" if args.plane else "pipe"
     import numpy as np
     import torch
 
@@ -62,17 +65,24 @@ def main():
         env.step_flipmask(random_actions=True)
     torch.cuda.synchronize()
     L.pbn_debug_set_stamps(None)
-    if args.pipe:
+    if args.pipe or args.plane:
         waves = (waves + 1) // 2   # one block per pair of groups
-        t = buf.view(-1, 16)[:waves, :12].cpu().numpy().astype(np.int64).reshape(waves, 3, 4)[:, :, :3]
+        nr = 4 if args.plane else 3
+        t = buf.view(-1, 16)[:waves, :4 * nr].cpu().numpy().astype(np.int64).reshape(waves, nr, 4)[:, :, :3]
         rep = {"envs": args.envs, "blocks": waves, "rollout_steps": args.rollout}
-        for role, name in enumerate(["state", "env draws", "selection"]):
+        names = ["state", "env draws", "selection", "planes+outputs"][:nr]
+        for role, name in enumerate(names):
             work = t[:, role, 1] - t[:, role, 0]
             wait = t[:, role, 2] - t[:, role, 1]
             rep[name] = {"work_median": int(np.median(work)), "work_p90": int(np.percentile(work, 90)),
                          "barrier_wait_median": int(np.median(wait))}
         full = buf.view(-1, 16)[:waves].cpu().numpy().astype(np.int64)
         st0 = full[:, 0]
+        if args.plane:
+            it = t[:, :, 2].max(axis=1) - t[:, :, 0].min(axis=1)
+            rep["iteration_median"] = int(np.median(it))
+            print(json.dumps(rep, indent=1))
+            return
         rep["state_phases"] = {
             "slot+transpose": int(np.median(full[:, 3] - st0)),
             "node eval": int(np.median(full[:, 12] - full[:, 3])),

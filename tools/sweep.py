@@ -39,7 +39,8 @@ def main():
         bufs = {}   # a captured graph writes into these: they must outlive it (torch.cuda.graph
                     # empties the allocator cache on entry, unmapping freed >= 20 MB segments)
         for T in args.kernels.split(","):
-            os.environ["PBN_ROLL"] = {"rollh": "hoist", "rolll": "lean", "rollp": "pipe"}.get(T, "auto")
+            os.environ["PBN_ROLL"] = {"rollh": "hoist", "rolll": "lean", "rollp": "pipe",
+                                      "rollq": "plane"}.get(T, "auto")
             env = VectorPBNEnv(spec, n, seed=3, keep_final_state=False)
             env.reset()
             with torch.cuda.stream(stream):
