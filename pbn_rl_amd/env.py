@@ -132,7 +132,13 @@ class PBNEnv:
         if N is not None and N != network.n:
             raise ValueError(f"N={N} but the network has {network.n} nodes")
         if attractors is None:
-            attractors = find_attractors(network) if network.n <= 20 else []
+            # exhaustive STG search while it is cheap; beyond that, GPU simulation + exact
+            # verification (discovery.py); both return bottom SCCs (print_graph.py:15-34)
+            if network.n <= 16:
+                attractors = find_attractors(network)
+            else:
+                from .discovery import discover_attractors
+                attractors = discover_attractors(network, prob_bits=prob_bits, device=device)
         if min_attractors is not None and len(attractors) < min_attractors:
             warnings.warn(f"network has {len(attractors)} attractors < min_attractors={min_attractors}")
         self.spec = EnvSpec(network, attractors, perturbation=perturbation, prob_bits=prob_bits, horizon=horizon,

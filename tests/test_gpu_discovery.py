@@ -1,0 +1,57 @@
+"""Attractor discovery by GPU simulation (pbn_rl_amd.discovery) against the exhaustive STG
+search (attractors.find_attractors, the print_graph.py:15-34 definition)."""
+import time
+
+import pytest
+
+from pbn_rl_amd.attractors import find_attractors, load_attractors
+from pbn_rl_amd.discovery import bottom_sccs, discover_attractors
+from pbn_rl_amd.network import load_network
+
+from .synthetic import random_network
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", ["pbn7", "pbn10"])
+def test_discovery_equals_exhaustive(name):
+    net = load_network(name)
+    got = discover_attractors(net, chains=4096, burn_in=200, window=64)
+    assert got == find_attractors(net)
+
+
+def test_discovery_pbn7_fixture():
+    got = discover_attractors(load_network("pbn7"), chains=2048, burn_in=100)
+    assert {frozenset(a) for a in got} == {frozenset(a) for a in load_attractors("pbn7")}
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_discovery_random_networks(seed):
+    net = random_network(12, seed, max_funcs=3)
+    assert discover_attractors(net, chains=8192, burn_in=300, window=64, seed=seed) == find_attractors(net)
+
+
+def test_discovery_pbn28_sets_are_bottom_sccs():
+    """28 nodes: beyond the exhaustive search.  Every reported set must re-verify as a bottom
+    SCC when the verification is seeded with that set alone."""
+    net = load_network("pbn28")
+    t0 = time.perf_counter()
+    got = discover_attractors(net, chains=65536, burn_in=1000, window=32, max_states=1 << 17)
+    print(f"pbn28: {len(got)} attractors, sizes {[len(a) for a in got]}, {time.perf_counter() - t0:.1f} s")
+    assert got
+    for att in got:
+        import numpy as np
+        assert bottom_sccs(net, np.array(att, dtype=np.uint8)) == [att]
+
+
+def test_pbnenv_uses_discovery_beyond_exhaustive_size():
+    """gym-style construction from logic functions (train_assa_BQN.py:121-124) of a 28-node
+    network: no fixture given, so PBNEnv discovers the attractors on the GPU."""
+    from pbn_rl_amd.env import PBNEnv
+
+    net = load_network("pbn28")
+    env = PBNEnv(N=28, genes=net.genes, logic_functions=net.logic_functions, min_attractors=7)
+    assert len(env.all_attractors) >= 7
+    (state, target), info = env.reset()
+    assert tuple(target) in {s for a in env.all_attractors for s in a}
+    env.close()
