@@ -42,10 +42,12 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=None, help="timed steps (default 2000; bdq workload 200)")
     p.add_argument("--warmup", type=int, default=None, help="untimed steps (default 200; bdq workload 20)")
-    p.add_argument("--workload", choices=["env", "bdq"], default="env",
+    p.add_argument("--workload", choices=["env", "bdq", "bdq-learn"], default="env",
                    help="env: BASELINE config 2, the env step alone (in-kernel random interventions); "
                         "bdq: config 5, the full BDQ frame per step (pbn_obs_unpack -> BranchingQNetwork "
-                        "forward in PyTorch -> pbn_q_to_flipmask -> pbn_step)")
+                        "forward in PyTorch -> pbn_q_to_flipmask -> pbn_step); bdq-learn: that frame plus "
+                        "storing the transitions in the device replay and one update_policy step of "
+                        "batch 256 (eager launches: the replay's ring position lives on the host)")
     p.add_argument("--epsilon", type=float, default=0.0, help="bdq workload: exploration rate")
     p.add_argument("--mode", choices=["rollout", "step"], default="rollout",
                    help="rollout: pbn_rollout launches of --chunk steps (state kept on chip); "
@@ -65,7 +67,10 @@ def parse():
                         "records (SURVEY.md 8(e)); reported as value_with_gather, not the headline")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     a = p.parse_args()
-    bdq = a.workload == "bdq"
+    bdq = a.workload in ("bdq", "bdq-learn")
+    if a.workload == "bdq-learn":
+        a.no_graph = True
+        a.no_cpu_baseline = True   # the CPU baseline restates acting only
     a.steps = a.steps if a.steps is not None else (200 if bdq else 2000)
     a.warmup = a.warmup if a.warmup is not None else (20 if bdq else 200)
     a.envs = a.envs if a.envs is not None else (32768 if bdq else 65536)
@@ -169,6 +174,10 @@ def workload_text(args, chunk: int, rollout_mode: bool) -> str:
         return (f"full BDQ rollout (config 5): {args.network} x {args.envs} envs per GPU, per step pbn_obs_unpack -> "
                 f"BranchingQNetwork fp32 forward (random init, seed 0) -> epsilon-greedy (eps={args.epsilon}) "
                 f"pbn_q_to_flipmask -> pbn_step, autoreset, {common}")
+    if args.workload == "bdq-learn":
+        return (f"BDQ training frames: {args.network} x {args.envs} envs per GPU, per step the config-5 frame "
+                f"(eps={args.epsilon}), the envs' transitions into the device replay, one update_policy step "
+                f"(batch 256, Adam, double-DQN target), {common}")
     return (f"{args.network} x {args.envs} envs per GPU, in-kernel random interventions (3 uniform actions/env/step), "
             f"autoreset, {common}; "
             + (f"pbn_rollout, {chunk} steps/launch, per-step obs/actions/rewards/flags written to HBM"
@@ -246,7 +255,7 @@ def main():
     spec = EnvSpec(load_network(args.network), load_attractors(args.network), perturbation=args.perturbation,
                    prob_bits=args.prob_bits, horizon=args.horizon)
     env = VectorPBNEnv(spec, args.envs, seed=args.seed, device=dev, env_offset=rank * args.envs,
-                       keep_final_state=False)
+                       keep_final_state=args.workload == "bdq-learn")
     env.reset()
     agent = None
     if args.workload == "bdq":
@@ -254,6 +263,14 @@ def main():
 
         torch.manual_seed(0)   # random-init weights of the reference architecture
         agent = BatchedBDQ(env, BranchingQNetwork((spec.n, spec.n), spec.n + 1, 3), epsilon=args.epsilon)
+    elif args.workload == "bdq-learn":
+        from pbn_rl_amd.agent import BranchingQNetwork
+        from pbn_rl_amd.replay import BDQLearner
+
+        torch.manual_seed(0)
+        learner = BDQLearner(env, BranchingQNetwork((spec.n, spec.n), spec.n + 1, 3), capacity=4 * args.envs,
+                             learning_starts=256, epsilon_start=args.epsilon, epsilon_final=args.epsilon)
+        agent = learner.agent
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.synchronize(dev)
 
@@ -266,6 +283,8 @@ def main():
         """One kernel launch covering k steps of every env."""
         if rollout_mode:
             bufs[k] = env.rollout(k, random_actions=True, keep_obs=True, keep_final=False, out=bufs.get(k))
+        elif args.workload == "bdq-learn":
+            learner.frame()
         elif agent is not None:
             agent.step()
         else:
@@ -325,6 +344,8 @@ def main():
         if agent is not None:
             bytes_launch = None
             kernel = "BDQ frame (pbn_obs_unpack, BranchingQNetwork fp32 forward, pbn_q_to_flipmask, pbn_step)"
+            if args.workload == "bdq-learn":
+                kernel += " + replay store + update_policy (batch 256)"
         elif rollout_mode:
             bytes_launch = env.n_alloc * rollout_bytes_per_env(W, chunk)
             kernel = "pbn_rollout_pipe (rollout, %d steps/launch)" % chunk

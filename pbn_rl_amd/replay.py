@@ -1,0 +1,186 @@
+"""On-device replay and the BDQ learner update (rows A9, A10).
+
+The reference keeps transitions as host ``Transition`` namedtuples in a Python list
+(``ExperienceReplay``, bdq_model/memory.py:17-62), and every update ``np.stack``s 256 of them
+and copies them to the GPU (``update_policy``, bdq_model/__init__.py:100-109).  Here the
+replay is a ring of packed transitions in HBM, filled straight from the batched env:
+
+    state, next_state   int32 [W][capacity]   packed words (bit i of word w = node 32w + i)
+    target              uint8 [capacity]      target attractor id
+    action              int32 [capacity][K]   the branch actions
+    reward              float32 [capacity]
+    done                uint8 [capacity]      terminated or truncated
+
+Sampling gathers rows by index and unpacks them to the fp32 (2, B, N) network input with
+``pbn_obs_unpack`` (the HIP kernel the acting frame uses), so nothing goes through the host.
+Indices are drawn with replacement (torch's device generator); ``random.sample`` at
+bdq_model/memory.py:62 draws without replacement, which only matters for batches comparable
+to the ring size.
+
+``bdq_update`` restates ``update_policy`` (bdq_model/__init__.py:100-139) on such a batch:
+double-DQN targets ``r + gamma * mask * Q_target(s', argmax_a Q(s', a))`` with the
+reference's ``mask = done`` (:109,122 -- it bootstraps only on done transitions; kept as is),
+MSE loss, gradients clamped to [-1, 1] (:129-130), one Adam step, and every
+``target_update`` updates the target network moves halfway to the online one (:133-139).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+from .agent import BatchedBDQ, BranchingQNetwork
+from .vector_env import VectorPBNEnv
+
+__all__ = ["DeviceReplay", "bdq_update", "soft_update", "BDQLearner"]
+
+
+class DeviceReplay:
+    def __init__(self, capacity: int, words: int, branches: int, device):
+        self.capacity = int(capacity)
+        self.words = int(words)
+        self.device = torch.device(device)
+        dev = self.device
+        self.state = torch.zeros(words, capacity, dtype=torch.int32, device=dev)
+        self.next_state = torch.zeros(words, capacity, dtype=torch.int32, device=dev)
+        self.target = torch.zeros(capacity, dtype=torch.uint8, device=dev)
+        self.action = torch.zeros(capacity, branches, dtype=torch.int32, device=dev)
+        self.reward = torch.zeros(capacity, dtype=torch.float32, device=dev)
+        self.done = torch.zeros(capacity, dtype=torch.uint8, device=dev)
+        self.pos = 0
+        self.size = 0
+
+    def _slots(self, n: int) -> torch.Tensor:
+        return (torch.arange(n, device=self.device, dtype=torch.int64) + self.pos) % self.capacity
+
+    def store(self, state: torch.Tensor, target: torch.Tensor, action: torch.Tensor, reward: torch.Tensor,
+              next_state: torch.Tensor, done: torch.Tensor) -> None:
+        """Append n transitions: state / next_state (W, n) words, target (n,), action (n, K),
+        reward (n,), done (n,) (any dtype castable to the ring's)."""
+        n = target.shape[0]
+        if n > self.capacity:
+            raise ValueError("more transitions than the ring holds")
+        idx = self._slots(n)
+        self.state.index_copy_(1, idx, state)
+        self.next_state.index_copy_(1, idx, next_state)
+        self.target.index_copy_(0, idx, target.to(torch.uint8))
+        self.action.index_copy_(0, idx, action.to(torch.int32))
+        self.reward.index_copy_(0, idx, reward.to(torch.float32))
+        self.done.index_copy_(0, idx, done.to(torch.uint8))
+        self.pos = (self.pos + n) % self.capacity
+        self.size = min(self.size + n, self.capacity)
+
+    def sample_indices(self, batch: int, generator: Optional[torch.Generator] = None) -> torch.Tensor:
+        if self.size == 0:
+            raise ValueError("empty replay")
+        return torch.randint(0, self.size, (batch,), device=self.device, generator=generator)
+
+    def gather(self, idx: torch.Tensor, net_handle, stream=None) -> Dict[str, torch.Tensor]:
+        """Rows ``idx`` (B a multiple of 32) as network inputs: obs / next_obs fp32 (2, B, N)
+        (state or next state, and the target attractor's first state), actions (B, K, 1) int64,
+        rewards (B, 1), masks (B, 1)."""
+        B = idx.shape[0]
+        if B % 32:
+            raise ValueError("batch size must be a multiple of 32")
+        st = self.state.index_select(1, idx).contiguous()
+        nst = self.next_state.index_select(1, idx).contiguous()
+        tg = self.target.index_select(0, idx).contiguous()
+        N = net_handle.spec.n
+        obs = torch.empty(2, B, N, dtype=torch.float32, device=self.device)
+        next_obs = torch.empty_like(obs)
+        L = _lib.load()
+        s = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
+        with torch.cuda.device(self.device):
+            _lib.check(L.pbn_obs_unpack(net_handle.handle, B, st.data_ptr(), tg.data_ptr(), obs.data_ptr(), s),
+                       "pbn_obs_unpack")
+            _lib.check(L.pbn_obs_unpack(net_handle.handle, B, nst.data_ptr(), tg.data_ptr(), next_obs.data_ptr(), s),
+                       "pbn_obs_unpack")
+        return {"obs": obs, "next_obs": next_obs,
+                "actions": self.action.index_select(0, idx).long().unsqueeze(-1),
+                "rewards": self.reward.index_select(0, idx).reshape(-1, 1),
+                "masks": self.done.index_select(0, idx).float().reshape(-1, 1)}
+
+
+@torch.no_grad()
+def soft_update(target: torch.nn.Module, online: torch.nn.Module) -> None:
+    """target <- target / 2 + online / 2, parameter by parameter (bdq_model/__init__.py:137-139)."""
+    for (kt, t), (ko, o) in zip(target.state_dict().items(), online.state_dict().items()):
+        t.div_(2).add_(o / 2)
+
+
+def bdq_update(q: torch.nn.Module, target: torch.nn.Module, opt: torch.optim.Optimizer, batch: Dict[str, torch.Tensor],
+               gamma: float = 0.999, grad_clamp: float = 1.0) -> torch.Tensor:
+    """One update_policy step (bdq_model/__init__.py:111-131) on a gathered batch; returns the loss."""
+    qvals = q(batch["obs"])                                             # (B, K, A)
+    current = qvals.gather(2, batch["actions"]).squeeze(-1)              # (B, K)
+    with torch.no_grad():
+        argmax = torch.argmax(q(batch["next_obs"]), dim=2)
+        max_next = target(batch["next_obs"]).gather(2, argmax.unsqueeze(2)).squeeze(-1)
+    expected = batch["rewards"] + max_next * gamma * batch["masks"]
+    loss = F.mse_loss(expected, current)
+    opt.zero_grad()
+    loss.backward()
+    for p in q.parameters():
+        p.grad.data.clamp_(-grad_clamp, grad_clamp)
+    opt.step()
+    return loss.detach()
+
+
+class BDQLearner:
+    """BranchingDQN.learn (bdq_model/__init__.py:150-238) over a VectorPBNEnv: every frame acts
+    for all envs (BatchedBDQ), appends their transitions to the device replay, and, once
+    ``learning_starts`` transitions are stored, takes ``updates_per_frame`` update_policy steps.
+    Exploration decays linearly from ``epsilon_start`` to ``epsilon_final`` over
+    ``epsilon_decay`` frames after ``learning_starts`` (decrement_epsilon, :141-148)."""
+
+    def __init__(self, env: VectorPBNEnv, qnet: Optional[BranchingQNetwork] = None, *, capacity: int = 10 ** 4,
+                 batch_size: int = 256, learning_rate: float = 1e-4, gamma: float = 0.999,
+                 target_update: int = 10_000, learning_starts: int = 288, updates_per_frame: int = 1,
+                 epsilon_start: float = 1.0, epsilon_final: float = 0.0, epsilon_decay: int = 10_000, seed: int = 0):
+        if not env.keep_final_state:
+            raise ValueError("BDQLearner needs the env's final_state (keep_final_state=True)")
+        self.env = env
+        self.agent = BatchedBDQ(env, qnet)
+        self.q = self.agent.q.train()
+        self.target = BranchingQNetwork((env.n_nodes, env.n_nodes), env.n_nodes + 1, self.agent.branches).to(env.device)
+        self.target.load_state_dict(self.q.state_dict())
+        # one fused multi-tensor kernel per step instead of a handful per parameter tensor
+        self.opt = torch.optim.Adam(self.q.parameters(), lr=learning_rate, fused=True)
+        self.replay = DeviceReplay(max(capacity, env.n_alloc), env.words, self.agent.branches, env.device)
+        self.batch_size, self.gamma, self.target_update = batch_size, gamma, target_update
+        self.learning_starts = max(learning_starts, batch_size)
+        self.updates_per_frame = updates_per_frame
+        self.epsilon = epsilon_start
+        self.epsilon_final = epsilon_final
+        self.epsilon_step = (epsilon_start - epsilon_final) / max(1, epsilon_decay)
+        self.frames = 0
+        self.updates = 0
+        self.gen = torch.Generator(device=env.device)
+        self.gen.manual_seed(seed)
+        self.last_loss: Optional[torch.Tensor] = None
+
+    def frame(self):
+        env = self.env
+        state = env.state.clone()
+        target = env.target.clone()
+        with torch.no_grad():
+            q = self.q(self.agent.observe())
+        self.agent.act(q, self.epsilon)
+        _, reward, flags = env.step_flipmask(use_current=True)
+        done_all = (env.flags & (_lib.FLAG_TERMINATED | _lib.FLAG_TRUNCATED)) != 0
+        # all n_alloc envs are stored (the padding envs of a ragged batch are real envs too)
+        self.replay.store(state, target, self.agent.actions, env.reward, env.final_state, done_all)
+        done = done_all[: env.num_envs]
+        self.frames += 1
+        if self.replay.size >= self.learning_starts:
+            self.epsilon = max(self.epsilon_final, self.epsilon - self.epsilon_step)
+            for _ in range(self.updates_per_frame):
+                idx = self.replay.sample_indices(self.batch_size, self.gen)
+                batch = self.replay.gather(idx, env.net)
+                self.last_loss = bdq_update(self.q, self.target, self.opt, batch, self.gamma)
+                self.updates += 1
+                if self.updates % self.target_update == 0:
+                    soft_update(self.target, self.q)
+        return reward, done

@@ -1,0 +1,87 @@
+"""On-device replay and the batched BDQ learner (pbn_rl_amd.replay) on the GPU: the ring holds
+exactly the transitions the oracle produces for the same actions, sampled rows unpack to the
+oracle's network inputs, and learning steps run end to end."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import agent_oracle, oracle
+from pbn_rl_amd.agent import BranchingQNetwork
+from pbn_rl_amd.attractors import load_attractors
+from pbn_rl_amd.network import load_network
+from pbn_rl_amd.replay import BDQLearner, DeviceReplay
+from pbn_rl_amd.spec import EnvSpec
+from pbn_rl_amd.vector_env import VectorPBNEnv
+
+pytestmark = pytest.mark.gpu
+
+
+def u32(x):
+    return x.cpu().numpy().view(np.uint32)
+
+
+def test_learner_transitions_match_oracle():
+    spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.02)
+    n, seed = 1024, 17
+    env = VectorPBNEnv(spec, n, seed=seed)
+    torch.manual_seed(0)
+    learner = BDQLearner(env, BranchingQNetwork((28, 28), 29, 3), capacity=4 * n, learning_starts=2 * n,
+                         epsilon_start=0.5, seed=3)
+    env.reset()
+    st, tg, t = oracle.reset(spec, seed, 0, 0, n)
+    for k in range(3):
+        step = env.step_index
+        learner.frame()
+        torch.cuda.synchronize()
+        acts = learner.agent.actions.cpu().numpy()
+        flip = np.zeros((1, n), dtype=np.uint32)
+        for b in range(3):
+            a = acts[:, b].astype(np.int64)
+            flip[0] |= np.where(a > 0, np.left_shift(np.uint32(1), np.maximum(a - 1, 0).astype(np.uint32)), 0).astype(np.uint32)
+        ref = oracle.step(spec, seed, step, 0, st, flip, tg, t, 1)
+        sl = slice(k * n, (k + 1) * n)
+        R = learner.replay
+        assert np.array_equal(u32(R.state[:, sl]), st)
+        assert np.array_equal(R.target[sl].cpu().numpy(), tg)
+        assert np.array_equal(u32(R.next_state[:, sl]), ref["final_state"])
+        assert np.array_equal(R.reward[sl].cpu().numpy(), ref["reward"])
+        assert np.array_equal(R.done[sl].cpu().numpy(), ((ref["flags"] & 3) != 0).astype(np.uint8))
+        st, tg, t = ref["state_out"], ref["target"], ref["t"]
+    # the ring is now 3n of 4n: learning started at 2n
+    assert learner.updates == 2 and torch.isfinite(learner.last_loss)
+    assert learner.epsilon < 0.5
+
+
+def test_gather_unpacks_like_the_oracle():
+    spec = EnvSpec(load_network("pbn70"), load_attractors("pbn70"))
+    env = VectorPBNEnv(spec, 64)
+    R = DeviceReplay(512, spec.words, 3, env.device)
+    rng = np.random.default_rng(0)
+    st = rng.integers(0, 2 ** 32, size=(3, 512), dtype=np.uint64).astype(np.uint32)
+    st[2] &= np.uint32((1 << 6) - 1)
+    nst = st[:, ::-1].copy()
+    tg = rng.integers(0, 16, size=512).astype(np.uint8)
+    to = lambda a: torch.from_numpy(a.view(np.int32).copy()).cuda()  # noqa: E731
+    R.store(to(st), torch.from_numpy(tg).cuda(), torch.zeros(512, 3, dtype=torch.int32, device="cuda"),
+            torch.zeros(512, device="cuda"), to(nst), torch.zeros(512, dtype=torch.uint8, device="cuda"))
+    idx = R.sample_indices(96, torch.Generator(device="cuda").manual_seed(1))
+    b = R.gather(idx, env.net)
+    torch.cuda.synchronize()
+    i = idx.cpu().numpy()
+    assert np.array_equal(b["obs"].cpu().numpy(), agent_oracle.obs_unpack(spec, st[:, i], tg[i]))
+    assert np.array_equal(b["next_obs"].cpu().numpy(), agent_oracle.obs_unpack(spec, nst[:, i], tg[i]))
+
+
+def test_learner_many_frames():
+    spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"))
+    env = VectorPBNEnv(spec, 4096, seed=1)
+    torch.manual_seed(1)
+    learner = BDQLearner(env, capacity=1 << 16, learning_starts=4096, updates_per_frame=2, target_update=5)
+    env.reset()
+    w0 = learner.q.model[0].bilinear.weight.detach().clone()
+    for _ in range(12):
+        learner.frame()
+    torch.cuda.synchronize()
+    assert learner.updates == 24 and torch.isfinite(learner.last_loss)   # learning starts after frame 1
+    assert not torch.equal(w0, learner.q.model[0].bilinear.weight)
+    assert learner.replay.size == 12 * 4096

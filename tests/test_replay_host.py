@@ -1,0 +1,56 @@
+"""bdq_update / soft_update (pbn_rl_amd.replay), CPU: the restated update_policy step
+(bdq_model/__init__.py:111-139) against the same arithmetic written out longhand."""
+import copy
+
+import torch
+import torch.nn.functional as F
+
+from pbn_rl_amd.agent import BranchingQNetwork
+from pbn_rl_amd.replay import bdq_update, soft_update
+
+
+def batch_for(N, B, K=3, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return {"obs": torch.randint(0, 2, (2, B, N), generator=g).float(),
+            "next_obs": torch.randint(0, 2, (2, B, N), generator=g).float(),
+            "actions": torch.randint(0, N + 1, (B, K, 1), generator=g),
+            "rewards": torch.randn(B, 1, generator=g),
+            "masks": torch.randint(0, 2, (B, 1), generator=g).float()}
+
+
+def test_update_matches_longhand():
+    torch.manual_seed(0)
+    N, B = 7, 64
+    q = BranchingQNetwork((N, N), N + 1, 3)
+    tgt = copy.deepcopy(q)
+    for p in tgt.parameters():
+        p.data.add_(0.01)
+    q2, tgt2 = copy.deepcopy(q), copy.deepcopy(tgt)
+    opt = torch.optim.Adam(q.parameters(), lr=1e-3)
+    opt2 = torch.optim.Adam(q2.parameters(), lr=1e-3)
+    b = batch_for(N, B)
+    loss = bdq_update(q, tgt, opt, b, gamma=0.9)
+    # longhand: update_policy lines 111-131
+    cur = q2(b["obs"]).gather(2, b["actions"]).squeeze(-1)
+    with torch.no_grad():
+        am = q2(b["next_obs"]).argmax(dim=2)
+        nxt = tgt2(b["next_obs"]).gather(2, am.unsqueeze(2)).squeeze(-1)
+    want = F.mse_loss(b["rewards"] + nxt * 0.9 * b["masks"], cur)
+    opt2.zero_grad()
+    want.backward()
+    for p in q2.parameters():
+        p.grad.data.clamp_(-1.0, 1.0)
+    opt2.step()
+    assert torch.allclose(loss, want.detach())
+    for a, c in zip(q.parameters(), q2.parameters()):
+        assert torch.equal(a, c)
+
+
+def test_soft_update_halves():
+    torch.manual_seed(1)
+    q = BranchingQNetwork((5, 5), 6, 3)
+    t = BranchingQNetwork((5, 5), 6, 3)
+    before = {k: v.clone() for k, v in t.state_dict().items()}
+    soft_update(t, q)
+    for k, v in t.state_dict().items():
+        assert torch.allclose(v, before[k] / 2 + q.state_dict()[k] / 2)
