@@ -7,7 +7,7 @@ A "step" is one synchronous PBN transition of every env of the batch:
 in-kernel random interventions (3 uniform actions per env, the explore policy
 of bdq_model/__init__.py:76), perturbation, per-node rule selection +
 truth-table update, attractor reward, autoreset.  By default steps run as
-``pbn_rollout`` launches of --chunk (20 = the horizon) steps, state kept on chip
+``pbn_rollout`` launches of --chunk (100 = five horizons) steps, state kept on chip
 between steps, every step's observation, actions, reward and flags written to
 HBM (what a learner consumes); ``--mode step`` times one ``pbn_step`` launch per
 step instead.  The launches of the timed run are captured in one hipGraph.
@@ -52,7 +52,10 @@ def parse():
     p.add_argument("--mode", choices=["rollout", "step"], default="rollout",
                    help="rollout: pbn_rollout launches of --chunk steps (state kept on chip); "
                         "step: one pbn_step launch per step")
-    p.add_argument("--chunk", type=int, default=20, help="steps per pbn_rollout launch")
+    p.add_argument("--chunk", type=int, default=100,
+                   help="steps per pbn_rollout launch (5 horizons; each launch re-reads the tables and "
+                        "refills the wave pipeline: 20 steps/launch runs at ~0.85x the rate of 100, "
+                        "profiles/r01_sweep_chunk_pbn28_65536.jsonl)")
     p.add_argument("--network", default="pbn28")
     p.add_argument("--envs", type=int, default=None,
                    help="envs per GPU (default 65,536; bdq workload 32,768 = 262,144 over 8 GPUs)")

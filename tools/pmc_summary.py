@@ -1,6 +1,6 @@
 """Turn the PMC passes of tools/gpu_bench_profile.sh into profiles/pmc_<net>_<envs>_<mode>.json.
 
-    python tools/pmc_summary.py gpurun_out/r01c --envs 65536 --steps-per-launch 20 [--words 1]
+    python tools/pmc_summary.py gpurun_out/r01c --envs 65536 --steps-per-launch 100 [--words 1]
 
 HBM bytes per launch of the step kernel = 2 x FETCH_SIZE + WRITE_SIZE (kB units), the gfx950
 correction of MI355X_MICROARCH.md's HBM section.  bench.py reads `hbm_bytes_per_launch` as
@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--network", default="pbn28")
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--mode", default="rollout")
-    ap.add_argument("--steps-per-launch", type=int, default=20)
+    ap.add_argument("--steps-per-launch", type=int, default=100)
     ap.add_argument("--words", type=int, default=1)
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
