@@ -21,6 +21,7 @@ from typing import Optional, Tuple
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from . import _lib
 from .vector_env import VectorPBNEnv
@@ -72,9 +73,25 @@ class BranchingQNetwork(nn.Module):
         self.adv_heads = nn.ModuleList([_mlp(32, 64, action_space_dimension) for _ in range(number_of_actions)])
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        h = self.model(x)
-        v = self.value_head(h)                                        # (B, 1)
-        adv = torch.stack([head(h) for head in self.adv_heads], dim=1)   # (B, K, A)
+        h = self.model(x)                                             # (B, 32)
+        # the value head and the K advantage heads read the same h: their first layers run as
+        # one (32 -> 64(K+1)) GEMM, their second layers as one batched GEMM over K+1 heads
+        heads = [self.value_head] + list(self.adv_heads)
+        w1 = torch.cat([hd[0].weight for hd in heads], 0)             # (64(K+1), 32)
+        b1 = torch.cat([hd[0].bias for hd in heads], 0)
+        z = F.leaky_relu(torch.addmm(b1, h, w1.t()))                  # (B, 64(K+1))
+        z = z.view(z.shape[0], len(heads), -1).transpose(0, 1)        # (K+1, B, 64)
+        A = self.ac_dim
+        w2 = torch.zeros(len(heads), A, z.shape[2], dtype=h.dtype, device=h.device)
+        b2 = torch.zeros(len(heads), 1, A, dtype=h.dtype, device=h.device)
+        w2[0, :1] = self.value_head[2].weight                         # value: output 0 of head 0
+        b2[0, 0, :1] = self.value_head[2].bias
+        for k, hd in enumerate(self.adv_heads):
+            w2[k + 1] = hd[2].weight
+            b2[k + 1, 0] = hd[2].bias
+        out = torch.baddbmm(b2, z, w2.transpose(1, 2))                # (K+1, B, A)
+        v = out[0, :, :1]                                             # (B, 1)
+        adv = out[1:].transpose(0, 1)                                 # (B, K, A)
         return v.unsqueeze(2) + adv - adv.mean(2, keepdim=True)
 
 
