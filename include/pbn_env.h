@@ -54,12 +54,13 @@
 extern "C" {
 #endif
 
-#define PBN_ABI_VERSION 1
+#define PBN_ABI_VERSION 2
 
 #define PBN_MAX_NODES 128
 #define PBN_MAX_ARITY 4
 #define PBN_MAX_FUNCS_PER_NODE 16
 #define PBN_MAX_ATTRACTORS 254
+#define PBN_MAX_GATES 224          /* and 32 * ceil(n_nodes / 32) + n_gates <= 256 */
 #define PBN_NO_TARGET 0xFF
 
 /* error codes */
@@ -83,7 +84,7 @@ extern "C" {
 /*
  * Network description (semantic form; the library derives its kernel encodings).
  * Function f of node i (node_func_start[i] <= f < node_func_start[i+1]) has
- * func_arity[f] <= 4 inputs func_inputs[4f..4f+arity) (node indices) and truth
+ * func_arity[f] <= 4 inputs func_inputs[4f..4f+arity) (plane references, below) and truth
  * table func_table[f]: bit m = value when input j = bit j of m.
  * func_threshold[f] is the cumulative selection threshold c_f in units of
  * 2^-prob_bits (strictly: c_{f-1} <= c_f, last of a node == 2^prob_bits).
@@ -108,6 +109,15 @@ typedef struct pbn_net_desc {
   const int32_t* attractor_start;   /* [n_attractors + 1] */
   const uint32_t* attractor_states; /* [n_attractor_states * W] */
   const float* reward_table;        /* [4 * (n_nodes + 1)] */
+  /* Combinational gates: functions of more than 4 inputs, lowered by the compiler
+   * (pbn_rl_amd/lowering.py) into functions of at most 4 "planes".  A plane reference
+   * r < n_nodes is node r of the pre-step state s1; r >= n_nodes is gate r - n_nodes.  Gate g
+   * may read nodes and gates < g; func_inputs may hold any reference.  All gates are evaluated
+   * on s1, like the node functions, so the update stays synchronous.  0 gates = none. */
+  int32_t n_gates;
+  const int32_t* gate_arity;        /* [n_gates] 0..4 */
+  const int32_t* gate_inputs;       /* [n_gates * 4], unused slots -1 */
+  const uint32_t* gate_table;       /* [n_gates] */
 } pbn_net_desc;
 
 typedef struct pbn_net pbn_net;

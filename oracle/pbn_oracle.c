@@ -75,13 +75,24 @@ static int gap_of(const pbn_net_desc* d, uint32_t u) {
   return d->n_nodes + 1;
 }
 
-static int eval_func(const pbn_net_desc* d, int f, const uint32_t* s) {
+/* plane reference r: node r of s (r < N), else the value of gate r - N (gv) */
+static int plane_of(const pbn_net_desc* d, int r, const uint32_t* s, const uint8_t* gv) {
+  return r < d->n_nodes ? (int)((s[r >> 5] >> (r & 31)) & 1u) : gv[r - d->n_nodes];
+}
+
+/* the combinational gates of the lowered wide functions, in order (gate g reads gates < g) */
+static void eval_gates(const pbn_net_desc* d, const uint32_t* s, uint8_t* gv) {
+  for (int g = 0; g < d->n_gates; ++g) {
+    uint32_t m = 0;
+    for (int j = 0; j < d->gate_arity[g]; ++j) m |= (uint32_t)plane_of(d, d->gate_inputs[4 * g + j], s, gv) << j;
+    gv[g] = (uint8_t)((d->gate_table[g] >> m) & 1u);
+  }
+}
+
+static int eval_func(const pbn_net_desc* d, int f, const uint32_t* s, const uint8_t* gv) {
   int k = d->func_arity[f];
   uint32_t m = 0;
-  for (int j = 0; j < k; ++j) {
-    int g = d->func_inputs[4 * f + j];
-    m |= ((s[g >> 5] >> (g & 31)) & 1u) << j;
-  }
+  for (int j = 0; j < k; ++j) m |= (uint32_t)plane_of(d, d->func_inputs[4 * f + j], s, gv) << j;
   return (int)((d->func_table[f] >> m) & 1u);
 }
 
@@ -210,16 +221,18 @@ int oracle_step(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t en
       if (perturbed) {
         for (int w = 0; w < W; ++w) sp[w] = s1[w] ^ gam[w];
       } else {
+        uint8_t gv[PBN_MAX_GATES];
+        eval_gates(d, s1, gv);
         for (int i = 0; i < N; ++i) {
           int f0 = d->node_func_start[i], nf = d->node_func_start[i + 1] - f0, x;
           if (nf == 1) {
-            x = eval_func(d, f0, s1);
+            x = eval_func(d, f0, s1, gv);
           } else {
             uint32_t u = 0;
             for (int dd = 0; dd < B; ++dd) u |= ((D[i][dd] >> b) & 1u) << (B - 1 - dd);
             int j = 0;
             while (j < nf - 1 && !(u < d->func_threshold[f0 + j])) ++j;
-            x = eval_func(d, f0 + j, s1);
+            x = eval_func(d, f0 + j, s1, gv);
           }
           if (x) sp[i >> 5] |= 1u << (i & 31);
         }

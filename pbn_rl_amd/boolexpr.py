@@ -14,6 +14,8 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Sequence, Tuple, Union
 
+import numpy as np
+
 __all__ = ["Expr", "parse", "variables", "evaluate", "ExprError"]
 
 
@@ -150,14 +152,33 @@ def evaluate(tree: Expr, env: Dict[str, bool] | Callable[[str], bool]) -> bool:
     raise TypeError(tree)
 
 
+def _evaluate_all(tree: Expr, planes: Dict[str, "np.ndarray"], size: int) -> "np.ndarray":
+    if isinstance(tree, Var):
+        return planes[tree.name]
+    if isinstance(tree, Const):
+        return np.full(size, tree.value, dtype=bool)
+    if isinstance(tree, Not):
+        return ~_evaluate_all(tree.arg, planes, size)
+    if isinstance(tree, And):
+        out = _evaluate_all(tree.args[0], planes, size).copy()
+        for a in tree.args[1:]:
+            out &= _evaluate_all(a, planes, size)
+        return out
+    if isinstance(tree, Or):
+        out = _evaluate_all(tree.args[0], planes, size).copy()
+        for a in tree.args[1:]:
+            out |= _evaluate_all(a, planes, size)
+        return out
+    raise TypeError(tree)
+
+
 def compile_truth_table(tree: Expr, inputs: Sequence[str]) -> int:
-    """Truth table as an int: bit m is f(x) with inputs[j] = (m >> j) & 1."""
+    """Truth table as an int: bit m is f(x) with inputs[j] = (m >> j) & 1.  All 2^k
+    assignments are evaluated at once over numpy bit vectors."""
     k = len(inputs)
     if k > 20:
         raise ExprError(f"arity {k} > 20 is not supported")
-    table = 0
-    for m in range(1 << k):
-        assign = {name: bool((m >> j) & 1) for j, name in enumerate(inputs)}
-        if evaluate(tree, assign):
-            table |= 1 << m
-    return table
+    m = np.arange(1 << k, dtype=np.int64)
+    planes = {name: ((m >> j) & 1).astype(bool) for j, name in enumerate(inputs)}
+    vals = _evaluate_all(tree, planes, 1 << k)
+    return int.from_bytes(np.packbits(vals.astype(np.uint8), bitorder="little").tobytes(), "little")

@@ -97,6 +97,9 @@ struct StepArgs {
   int max_nf;        // largest function count of a node
   int lq;            // pipelined rollout: selection masks per node in a slot (max(max_nf - 1, 1))
   int slot_words;    // pipelined rollout: words of one step slot
+  int gate_off;      // wave kernel: LDS image offset of the gate records, uint4 [n_gates] by level
+  int glayer_off;    // LDS image offset of the level starts, int32 [n_glayers + 1]
+  int n_glayers;     // 0: no gates
 };
 
 // In-kernel phase clocks (cdna_hip_programming.md section 7, "In-kernel stamps"):
@@ -529,6 +532,21 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
     if (lo) S[32 * w + l32] = sp;
   }
   __builtin_amdgcn_wave_barrier();
+  if (a.n_glayers > 0) {
+    // combinational gates of the lowered wide functions (lowering.py), level by level, all
+    // 64 lanes: gate record {input S indices, 16-bit table, output S index}; one wave's LDS
+    // operations execute in order, so level l + 1 reads what level l wrote
+    const uint4* grec = reinterpret_cast<const uint4*>(L + a.gate_off);
+    const int32_t* glev = reinterpret_cast<const int32_t*>(L + a.glayer_off);
+    for (int lv = 0; lv < a.n_glayers; ++lv) {
+      const int end = glev[lv + 1];
+      for (int gi = glev[lv] + lane; gi < end; gi += 64) {
+        const uint4 r = grec[gi];
+        S[r.z] = eval_compact(r.x, r.y, S);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
 
   // ---- 4. node l32 + 32r on lane l32: X = rule update of every env (perturbed envs are
   // replaced after the back-transpose)
@@ -1603,6 +1621,7 @@ struct pbn_net {
   size_t lds_pipe = 0;
   StepFn plane = nullptr;       // rollout, plane-resident state (W == 1, single-state attractors)
   size_t lds_plane = 0;
+  int n_gates = 0, n_glayers = 0, gate_off = 0, glayer_off = 0;   // lowered wide functions
   int max_nf = 0, lq = 1, slot_words = 0;
   int64_t roll_pipe_groups = 1 << 30;  // rollouts with at most this many groups use the pipelined kernel
   int force_roll = 0;        // PBN_ROLL env override: 1 = hoist, 2 = lean, 3 = pipe, 4 = plane
@@ -1762,6 +1781,23 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     return fail(PBN_EINVAL, "null table in descriptor");
   const int W = (N + 31) / 32;
   const uint32_t one = 1u << d->prob_bits;
+  const int n_gates = d->n_gates;
+  if (n_gates < 0 || n_gates > PBN_MAX_GATES || 32 * W + n_gates > 256)
+    return fail(PBN_EINVAL, "n_gates out of range (32 * W + n_gates must be <= 256)");
+  if (n_gates && (!d->gate_arity || !d->gate_inputs || !d->gate_table)) return fail(PBN_EINVAL, "null gate table");
+  // gate levels: 1 + the deepest gate input (nodes are level 0)
+  std::vector<int> glevel(n_gates, 1);
+  for (int g = 0; g < n_gates; ++g) {
+    const int k = d->gate_arity[g];
+    if (k < 0 || k > PBN_MAX_ARITY) return fail(PBN_EINVAL, "gate arity must be 0..4");
+    if (k < 5 && (1u << k) < 32 && (d->gate_table[g] >> (1u << k)) != 0u)
+      return fail(PBN_EINVAL, "gate truth table has bits beyond 2^arity");
+    for (int j = 0; j < k; ++j) {
+      const int r = d->gate_inputs[4 * g + j];
+      if (r < 0 || r >= N + g) return fail(PBN_EINVAL, "gate input must be a node or an earlier gate");
+      if (r >= N) glevel[g] = std::max(glevel[g], glevel[r - N] + 1);
+    }
+  }
   if (d->node_func_start[0] != 0 || d->node_func_start[N] != d->n_funcs)
     return fail(PBN_EINVAL, "node_func_start must span 0..n_funcs");
   std::vector<FuncRec> recs(d->n_funcs);
@@ -1781,8 +1817,8 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
       memset(&r, 0, sizeof r);
       for (int j = 0; j < 4; ++j) {
         int g = j < k ? d->func_inputs[4 * f + j] : 0;
-        if (g < 0 || g >= N) return fail(PBN_EINVAL, "function input index out of range");
-        r.in[j] = (uint32_t)g;
+        if (g < 0 || g >= N + n_gates) return fail(PBN_EINVAL, "function input reference out of range");
+        r.in[j] = (uint32_t)(g < N ? g : 32 * W + (g - N));   // LDS plane index
       }
       const uint32_t T = d->func_table[f];
       const uint32_t kmask = (k >= 5) ? 0xFFFFFFFFu : ((1u << k) - 1u);
@@ -1928,9 +1964,43 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   for (const uint4& r4 : nrec) {
     tab.push_back(r4.x); tab.push_back(r4.y); tab.push_back(r4.z); tab.push_back(r4.w);
   }
+  // gate records by level: {input plane indices as bytes, 16-bit table (unused inputs
+  // replicated), output plane index 32W + g, 0}, then the level starts
+  net->n_gates = n_gates;
+  if (n_gates) {
+    int n_lv = 0;
+    for (int g = 0; g < n_gates; ++g) n_lv = std::max(n_lv, glevel[g]);
+    std::vector<int> order(n_gates);
+    for (int g = 0; g < n_gates; ++g) order[g] = g;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return glevel[x] < glevel[y]; });
+    net->gate_off = (int)tab.size();
+    std::vector<int> starts(n_lv + 1, 0);
+    for (int idx = 0; idx < n_gates; ++idx) {
+      const int g = order[idx], k = d->gate_arity[g];
+      uint32_t ins = 0;
+      for (int j = 0; j < k; ++j) {
+        const int r = d->gate_inputs[4 * g + j];
+        ins |= (uint32_t)(r < N ? r : 32 * W + (r - N)) << (8 * j);
+      }
+      const uint32_t T = d->gate_table[g];
+      const uint32_t kmask = (1u << k) - 1u;
+      uint32_t T16 = 0;
+      for (uint32_t m = 0; m < 16; ++m) T16 |= ((T >> (m & kmask)) & 1u) << m;
+      tab.push_back(ins); tab.push_back(T16); tab.push_back((uint32_t)(32 * W + g)); tab.push_back(0u);
+      starts[glevel[g]] = idx + 1;   // running end of each level (levels are contiguous)
+    }
+    net->glayer_off = (int)tab.size();
+    tab.push_back(0u);
+    for (int lv = 1; lv <= n_lv; ++lv) {
+      if (starts[lv] == 0) starts[lv] = starts[lv - 1];
+      tab.push_back((uint32_t)starts[lv]);
+    }
+    net->n_glayers = n_lv;
+  }
+  while (tab.size() & 3) tab.push_back(0u);   // the kernels copy the image as uint4
   net->tab_words = (int)tab.size();
   net->n_funcs = d->n_funcs;
-  net->wave_words = (32 * W + 3) & ~3;   // S planes per wave
+  net->wave_words = (32 * W + n_gates + 3) & ~3;   // S planes (+ gate planes) per wave
   {
     const double p = (double)d->perturb_cdf[0] / 4294967296.0;
     net->gap_exact = (p < 1e-6 || p > 0.5) ? 1 : 0;
@@ -2082,6 +2152,9 @@ int pbn_step(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, in
   a.max_nf = net->max_nf;
   a.lq = net->lq;
   a.slot_words = net->slot_words;
+  a.gate_off = net->gate_off;
+  a.glayer_off = net->glayer_off;
+  a.n_glayers = net->n_glayers;
   memcpy(a.uthr, net->uthr, sizeof a.uthr);
   memcpy(a.hash_mult, net->hash_mult, sizeof a.hash_mult);
 #ifdef PBN_STAMPS
@@ -2152,6 +2225,9 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
   a.max_nf = net->max_nf;
   a.lq = net->lq;
   a.slot_words = net->slot_words;
+  a.gate_off = net->gate_off;
+  a.glayer_off = net->glayer_off;
+  a.n_glayers = net->n_glayers;
   memcpy(a.uthr, net->uthr, sizeof a.uthr);
   memcpy(a.hash_mult, net->hash_mult, sizeof a.hash_mult);
   a.prob_bits = net->B;
@@ -2172,6 +2248,7 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
   bool pipe = a.n_groups <= net->roll_pipe_groups && net->lds_pipe <= 64 * 1024;
   bool lean = a.n_groups > (int64_t)net->roll_lean_groups;
   if (net->force_roll) pipe = net->force_roll == 3;
+  if (net->n_gates) pipe = plane = false;   // gates (wide functions) run in the wave kernels only
   if (net->force_roll == 1) lean = false;
   if (net->force_roll == 2) lean = true;
   if (plane) {   // one block of four waves per pair of groups

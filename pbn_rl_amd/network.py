@@ -32,6 +32,7 @@ import numpy as np
 
 from . import boolexpr
 from .ispl import parse_ispl_file
+from .lowering import MAX_GATES, _reduce_refs, lower_network_functions
 
 __all__ = [
     "NodeFunction",
@@ -46,7 +47,7 @@ __all__ = [
 ]
 
 MAX_NODES = 128            # 4 x u32 state words
-MAX_ARITY = 4              # kernel mux tree depth; kaban/*.ispl functions have <= 4 inputs
+MAX_ARITY = 4              # kernel mux tree depth; wider functions are lowered to gates (lowering.py)
 MAX_FUNCS_PER_NODE = 16
 NETWORK_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "networks")
 
@@ -71,29 +72,7 @@ class NodeFunction:
 
 def _reduce(inputs: List[int], table: int) -> Tuple[Tuple[int, ...], int]:
     """Drop inputs the function does not depend on; sort the rest ascending."""
-    k = len(inputs)
-    keep = []
-    for j in range(k):
-        depends = False
-        for m in range(1 << k):
-            if not (m >> j) & 1:
-                if ((table >> m) & 1) != ((table >> (m | (1 << j))) & 1):
-                    depends = True
-                    break
-        if depends:
-            keep.append(j)
-    # re-tabulate over kept inputs, ordered by gene index
-    order = sorted(keep, key=lambda j: inputs[j])
-    new_inputs = tuple(inputs[j] for j in order)
-    new_table = 0
-    for m2 in range(1 << len(order)):
-        m = 0
-        for jj, j in enumerate(order):
-            if (m2 >> jj) & 1:
-                m |= 1 << j
-        if (table >> m) & 1:
-            new_table |= 1 << m2
-    return new_inputs, new_table
+    return _reduce_refs(inputs, table)
 
 
 def quantize_weights(weights: Sequence[Union[float, Fraction]], bits: int) -> List[int]:
@@ -243,27 +222,42 @@ class Network:
         return p
 
     # --------------------------------------------------------------- tables
+    def lowered(self):
+        """(Lowering, records): functions of more than 4 inputs as <= 4-input records over node
+        planes and combinational gates (lowering.py); cached."""
+        if getattr(self, "_lowered", None) is None:
+            self._lowered = lower_network_functions(self.nodes, self.genes)
+        return self._lowered
+
     def descriptor_arrays(self, prob_bits: int = 16) -> Dict[str, np.ndarray]:
         if prob_bits not in (4, 8, 12, 16):
             raise ValueError("prob_bits must be 4, 8, 12 or 16")
-        if self.max_arity > MAX_ARITY:
-            raise ValueError(f"function arity {self.max_arity} > {MAX_ARITY} is not supported by the kernel")
+        low, recs = self.lowered()
+        if 32 * self.words + len(low.gates) > 256 or len(low.gates) > MAX_GATES:
+            raise ValueError(f"{len(low.gates)} gates after lowering the wide functions: more than the kernels "
+                             f"address ({256 - 32 * self.words} for {self.n} nodes)")
         starts = [0]
         arity, inputs, tables, thr = [], [], [], []
-        for fl, c in zip(self.nodes, self.thresholds(prob_bits)):
-            for f, cj in zip(fl, c):
-                arity.append(f.arity)
-                ins = list(f.inputs) + [-1] * (MAX_ARITY - f.arity)
-                inputs.extend(ins)
-                tables.append(f.table)
+        for rl, c in zip(recs, self.thresholds(prob_bits)):
+            for (refs, tab), cj in zip(rl, c):
+                arity.append(len(refs))
+                inputs.extend(list(refs) + [-1] * (MAX_ARITY - len(refs)))
+                tables.append(tab)
                 thr.append(cj)
             starts.append(len(arity))
+        g_ar = [len(ins) for ins, _ in low.gates]
+        g_in = [r for ins, _ in low.gates for r in list(ins) + [-1] * (MAX_ARITY - len(ins))]
+        g_tab = [tab for _, tab in low.gates]
         return {
             "node_func_start": np.asarray(starts, dtype=np.int32),
             "func_arity": np.asarray(arity, dtype=np.int32),
             "func_inputs": np.asarray(inputs, dtype=np.int32),
             "func_table": np.asarray(tables, dtype=np.uint32),
             "func_threshold": np.asarray(thr, dtype=np.uint32),
+            "n_gates": np.asarray([len(g_ar)], dtype=np.int32),
+            "gate_arity": np.asarray(g_ar or [0], dtype=np.int32),
+            "gate_inputs": np.asarray(g_in or [-1] * MAX_ARITY, dtype=np.int32),
+            "gate_table": np.asarray(g_tab or [0], dtype=np.uint32),
         }
 
     # ------------------------------------------------------------ state utils

@@ -48,6 +48,10 @@ class PbnNetDesc(ctypes.Structure):
         ("attractor_start", ctypes.c_void_p),
         ("attractor_states", ctypes.c_void_p),
         ("reward_table", ctypes.c_void_p),
+        ("n_gates", ctypes.c_int32),
+        ("gate_arity", ctypes.c_void_p),
+        ("gate_inputs", ctypes.c_void_p),
+        ("gate_table", ctypes.c_void_p),
     ]
 
 
@@ -146,6 +150,10 @@ class EnvSpec:
         d.attractor_start = _ptr(a["attractor_start"])
         d.attractor_states = _ptr(a["attractor_states"])
         d.reward_table = _ptr(a["reward_table"])
+        d.n_gates = int(a["n_gates"][0])
+        d.gate_arity = _ptr(a["gate_arity"])
+        d.gate_inputs = _ptr(a["gate_inputs"])
+        d.gate_table = _ptr(a["gate_table"])
         return d
 
     @property

@@ -2,8 +2,8 @@
 
 Every kaban network has 2-3 functions per node with weights 1 (a few merged duplicates).
 These networks add nodes with up to 6 distinct functions (the > kNodeRecs chain tail),
-arbitrary relative weights (per-node thresholds), constant (arity 0) functions, and
-node counts that give 1..4 state words.
+arbitrary relative weights (per-node thresholds), constant (arity 0) functions, node counts
+that give 1..4 state words, and (max_arity > 4) wide functions that need gates.
 """
 from fractions import Fraction
 
@@ -23,7 +23,10 @@ def random_network(n_nodes: int, seed: int, max_funcs: int = 6, max_arity: int =
         while len(funcs) < nf:
             k = int(rng.integers(0, min(max_arity, n_nodes) + 1))
             ins = [int(x) for x in rng.choice(n_nodes, size=k, replace=False)]
-            table = int(rng.integers(0, 1 << (1 << k)))
+            if (1 << k) <= 32:
+                table = int(rng.integers(0, 1 << (1 << k)))
+            else:   # wide functions (k >= 6): a random 2^k-bit table
+                table = int.from_bytes(rng.bytes((1 << k) // 8), "little")
             key = _reduce(ins, table)
             if key in seen:
                 continue

@@ -41,13 +41,14 @@ def test_library_exports_every_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.pbn_abi_version() == 1
+    assert lib.pbn_abi_version() == 2
 
 
 def test_descriptor_layout_matches_header():
     # pointer-sized fields follow four int32; same order as pbn_net_desc
     assert PbnNetDesc.node_func_start.offset == 16
-    assert ctypes.sizeof(PbnNetDesc) == 16 + 6 * 8 + 8 + 3 * 8
+    assert ctypes.sizeof(PbnNetDesc) == 16 + 6 * 8 + 8 + 3 * 8 + 8 + 3 * 8
+    assert PbnNetDesc.n_gates.offset == 96 and PbnNetDesc.gate_arity.offset == 104
 
 
 def _create(lib, spec):

@@ -259,3 +259,28 @@ def test_rollout_equals_steps_baseline_size():
         assert torch.equal(out["flags"][k], flags) and torch.equal(out["reward"][k], reward)
         assert torch.equal(out["final_state"][k], b.final_state)
     assert torch.equal(a.state, b.state) and torch.equal(a.t, b.t) and torch.equal(a.target, b.target)
+
+
+# ---------------------------------------------------------------- wide functions (gates)
+@pytest.mark.parametrize("name", ["bb33", "m47"])
+def test_wide_networks(name, monkeypatch):
+    """Functions of up to 6 (bb33) and 20 (model_tester's 47-node network) inputs, lowered to
+    gates that the wave kernels evaluate level by level before the node functions."""
+    spec = make_spec(name, perturbation=0.01, horizon=6)
+    assert spec.arrays["n_gates"][0] > 0
+    run_pair(spec, 2048, 5, mode=3, start_random=True)
+    run_pair(spec, 1024, 3, mode=0, start_random=True)
+    for variant in ("auto", "hoist", "lean"):
+        monkeypatch.setenv("PBN_ROLL", variant)
+        run_rollout_pair(spec, 2080, 6, 3)
+
+
+def test_wide_random_network(monkeypatch):
+    """Table-only wide functions (Shannon-lowered, 86 gates) with several functions per node."""
+    from pbn_rl_amd.attractors import random_state_targets
+    from .synthetic import random_network
+    net = random_network(12, 7, max_funcs=3, max_arity=7)
+    spec = EnvSpec(net, random_state_targets(12, 4, 8), perturbation=0.02, horizon=5)
+    run_pair(spec, 1024, 5, mode=3, start_random=True)
+    monkeypatch.setenv("PBN_ROLL", "lean")
+    run_rollout_pair(spec, 1024, 6, 3)

@@ -56,7 +56,9 @@ def test_descriptor_pinned_by_golden():
     for name in ["pbn7", "pbn10", "pbn28", "pbn70"]:
         net = load_network(name)
         arr = net.descriptor_arrays(16)
-        h = hashlib.sha256(b"".join(arr[k].tobytes() for k in sorted(arr))).hexdigest()
+        assert arr["n_gates"][0] == 0, name            # every kaban function has <= 4 inputs
+        keys = ["func_arity", "func_inputs", "func_table", "func_threshold", "node_func_start"]
+        h = hashlib.sha256(b"".join(arr[k].tobytes() for k in keys)).hexdigest()
         assert h == g[name]["descriptor_sha256"], name
         assert net.n == g[name]["n_nodes"]
 
@@ -74,9 +76,22 @@ def test_bittner28_fixture_attractors():
     assert hexes[0] == 0xEDDF7D7 and hexes[-1] == 0xF7DFEEF
 
 
-def test_arity_limit():
+def test_wide_function_is_lowered_to_gates():
+    """Arity 5 > the kernels' 4: the record reads gate planes (refs >= n) instead."""
     genes = [f"g{i}" for i in range(6)]
     lf = [[("g0 and g1 and g2 and g3 and g4", 1.0)]] + [[("g0", 1.0)]] * 5
     net = Network.from_logic_functions(genes, lf)
-    with pytest.raises(ValueError, match="arity"):
+    arr = net.descriptor_arrays(16)
+    assert arr["n_gates"][0] >= 1 and (arr["func_arity"] <= 4).all()
+    assert (arr["func_inputs"][:4] >= 6).any()
+
+
+def test_gate_budget_is_enforced():
+    """More gates than one-byte plane addressing allows is a clear error, not a silent fallback."""
+    genes = [f"g{i}" for i in range(20)]
+    rng = np.random.default_rng(0)
+    lf = [[(" or ".join(f"({' and '.join(f'g{j}' for j in rng.choice(20, 5, replace=False))})"
+                        for _ in range(12)), 1.0)] for _ in range(20)]
+    net = Network.from_logic_functions(genes, lf)
+    with pytest.raises(ValueError, match="gates"):
         net.descriptor_arrays(16)

@@ -159,3 +159,43 @@ def test_shard_invariance_oracle():
     b = oracle.step(spec, 5, 1, 128, st[:, 128:], np.zeros_like(st[:, 128:]), tg[128:], t[128:], 3)
     for key in ("state_out", "reward", "flags", "target", "t", "flipmask"):
         assert np.array_equal(full[key], np.concatenate([a[key], b[key]], axis=-1)), key
+
+
+def _wide_pair(spec, n, steps, mode, seed=4711, start_random=True):
+    net = spec.network
+    W = spec.words
+    py = pyoracle.PyPBN(spec)
+    rng = np.random.default_rng(seed)
+    st, tg, t = oracle.reset(spec, seed, 0, 0, n)
+    if start_random:
+        st = rng.integers(0, 2 ** 32, size=(W, n), dtype=np.uint64).astype(np.uint32)
+        if net.n % 32:
+            st[W - 1] &= np.uint32((1 << (net.n % 32)) - 1)
+    for step in range(1, steps + 1):
+        flip = np.zeros((W, n), dtype=np.uint32)
+        res = oracle.step(spec, seed, step, 0, st, flip, tg, t, mode)
+        for i in range(n):
+            bits = net.unpack([int(st[w, i]) for w in range(W)])
+            r = py.step(seed, step, i, bits, [0] * net.n, int(tg[i]), int(t[i]), mode)
+            assert net.pack(r["final_state"]) == [int(res["final_state"][w, i]) for w in range(W)], (step, i)
+            assert r["flags"] == res["flags"][i]
+        st, tg, t = res["state_out"], res["target"], res["t"]
+
+
+@pytest.mark.parametrize("name", ["bb33", "m47"])
+def test_wide_networks_c_oracle_equals_python_oracle(name):
+    """Functions of more than 4 inputs: the C oracle evaluates the lowered records and gates
+    (lowering.py), the Python oracle the original wide truth tables."""
+    spec = spec_for(name, perturbation=0.005, horizon=5)
+    assert spec.arrays["n_gates"][0] > 0
+    _wide_pair(spec, 64, 4, 3)
+
+
+def test_wide_random_network_c_oracle_equals_python_oracle():
+    """Table-only wide functions (Shannon lowering) with several functions per node."""
+    from .synthetic import random_network
+    from pbn_rl_amd.attractors import random_state_targets
+    net = random_network(12, 7, max_funcs=3, max_arity=7)
+    assert net.max_arity > 4
+    spec = EnvSpec(net, random_state_targets(12, 4, 8), perturbation=0.01, horizon=4)
+    _wide_pair(spec, 96, 4, 3)

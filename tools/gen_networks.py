@@ -5,6 +5,10 @@ The JSON keeps the parser output (genes + (expression, weight) lists, exactly
 what the reference passes to gym.make("gym-PBN/PBNEnv"), train_assa_BQN.py:121-124)
 plus the compiled canonical functions, so the GPU box never reads /root/reference.
 
+Also bb33 (models/bb33/bb33.ispl, 33 nodes, functions of up to 6 inputs) and the 47-node
+inline network of model_tester.py:97-137 (functions of up to 20 inputs, read from the script's
+literal lists): the wide-function networks that exercise the gate lowering (lowering.py).
+
 Attractor sets written alongside (see pbn_rl_amd/attractors.py for provenance):
   pbn28_attractors.json  14 singleton states, SURVEY.md Appendix B (derived from
                          data/attractors_Bittner-28.pkl, which this round's safe
@@ -48,6 +52,34 @@ def main():
             json.dump({"network": name, "source": src,
                        "attractors": [["".join(str(b) for b in s) for s in a] for a in atts]}, f, indent=1)
         print(name, net.n, "nodes,", len(atts), "attractors")
+    wide = {"bb33": Network.from_ispl("/root/reference/models/bb33/bb33.ispl", name="bb33"),
+            "m47": model_tester_network(47)}
+    for name, net in wide.items():
+        obj = net.to_json()
+        obj["source"] = {"bb33": "models/bb33/bb33.ispl of jakub-zarzycki2022/pbn-rl, parsed by pbn_rl_amd.ispl",
+                         "m47": "inline 47-node network of model_tester.py:97-137 (its literal gene and "
+                                "logic-function lists)"}[name]
+        with open(os.path.join(NETWORK_DIR, f"{name}.json"), "w") as f:
+            json.dump(obj, f, indent=1)
+        atts = random_state_targets(net.n, 8, seed=net.n)
+        with open(os.path.join(NETWORK_DIR, f"{name}_attractors.json"), "w") as f:
+            json.dump({"network": name, "source": f"no fixture: 8 seeded random states (numpy default_rng({net.n}))",
+                       "attractors": [["".join(str(b) for b in s) for s in a] for a in atts]}, f, indent=1)
+        print(name, net.n, "nodes, max arity", net.max_arity, ",", len(net.lowered()[0].gates), "gates")
+
+
+def model_tester_network(n: int) -> Network:
+    """The inline gym.make("gym-PBN/PBNEnv", N=n, genes=[...], logic_functions=[...]) of
+    model_tester.py, read as literals (ast.literal_eval: nothing is executed)."""
+    import ast
+    src = open("/root/reference/model_tester.py").read()
+    i = src.index(f"N={n}")
+    j = src.index("genes=[", i)
+    k = src.index("])", src.index("logic_functions=[", j))
+    block = src[j:k + 1]
+    genes = ast.literal_eval(block[block.index("["):block.index("]") + 1])
+    funcs = ast.literal_eval(block[block.index("logic_functions=") + len("logic_functions="):])
+    return Network.from_logic_functions(genes, funcs, name=f"m{n}")
 
 
 if __name__ == "__main__":
