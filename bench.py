@@ -47,7 +47,8 @@ def parse():
                         "bdq: config 5, the full BDQ frame per step (pbn_obs_unpack -> BranchingQNetwork "
                         "forward in PyTorch -> pbn_q_to_flipmask -> pbn_step); bdq-learn: that frame plus "
                         "storing the transitions in the device replay and one update_policy step of "
-                        "batch 256 (eager launches: the replay's ring position lives on the host)")
+                        "batch 256 (one hipGraph per frame: step index, epsilon and ring position live on "
+                        "the device; --no-graph launches it eagerly)")
     p.add_argument("--epsilon", type=float, default=0.0, help="bdq workload: exploration rate")
     p.add_argument("--mode", choices=["rollout", "step"], default="rollout",
                    help="rollout: pbn_rollout launches of --chunk steps (state kept on chip); "
@@ -71,7 +72,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     a = p.parse_args()
     bdq = a.workload in ("bdq", "bdq-learn")
+    a.learn_graph = False
     if a.workload == "bdq-learn":
+        a.learn_graph = not a.no_graph   # the learner captures its own one-frame graph
         a.no_graph = True
         a.no_cpu_baseline = True   # the CPU baseline restates acting only
     a.steps = a.steps if a.steps is not None else (200 if bdq else 2000)
@@ -180,7 +183,8 @@ def workload_text(args, chunk: int, rollout_mode: bool) -> str:
     if args.workload == "bdq-learn":
         return (f"BDQ training frames: {args.network} x {args.envs} envs per GPU, per step the config-5 frame "
                 f"(eps={args.epsilon}), the envs' transitions into the device replay, one update_policy step "
-                f"(batch 256, Adam, double-DQN target), {common}")
+                f"(batch 256, Adam, double-DQN target), "
+                f"{'one captured hipGraph per frame' if args.learn_graph else 'eager launches'}, {common}")
     return (f"{args.network} x {args.envs} envs per GPU, in-kernel random interventions (3 uniform actions/env/step), "
             f"autoreset, {common}; "
             + (f"pbn_rollout, {chunk} steps/launch, per-step obs/actions/rewards/flags written to HBM"
@@ -272,7 +276,8 @@ def main():
 
         torch.manual_seed(0)
         learner = BDQLearner(env, BranchingQNetwork((spec.n, spec.n), spec.n + 1, 3), capacity=4 * args.envs,
-                             learning_starts=256, epsilon_start=args.epsilon, epsilon_final=args.epsilon)
+                             learning_starts=256, epsilon_start=args.epsilon, epsilon_final=args.epsilon,
+                             graphable=args.learn_graph)
         agent = learner.agent
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.synchronize(dev)
@@ -298,6 +303,8 @@ def main():
     with torch.cuda.stream(stream):
         for k in launch_plan(args.warmup, chunk):
             launch(k)
+        if args.learn_graph:
+            learner.capture()   # frame() replays the captured frame from here on
         torch.cuda.synchronize(dev)
         graph = None
         if use_graph:
@@ -349,6 +356,7 @@ def main():
             kernel = "BDQ frame (pbn_obs_unpack, BranchingQNetwork fp32 forward, pbn_q_to_flipmask, pbn_step)"
             if args.workload == "bdq-learn":
                 kernel += " + replay store + update_policy (batch 256)"
+                kernel += ", one hipGraph replay per frame" if args.learn_graph else ", eager"
         elif rollout_mode:
             bytes_launch = env.n_alloc * rollout_bytes_per_env(W, chunk)
             kernel = "pbn_rollout_pipe (rollout, %d steps/launch)" % chunk
@@ -408,7 +416,7 @@ def main():
             "data": "synthetic",
             "config": {"workload": workload_text(args, chunk, rollout_mode),
                        "network": args.network, "envs_per_gpu": args.envs, "global_envs": world * args.envs,
-                       "parallelism": f"env-shard x{world}", "launch": "hipGraph" if use_graph else "eager"},
+                       "parallelism": f"env-shard x{world}", "launch": "hipGraph" if (use_graph or args.learn_graph) else "eager"},
             "roofline": roofline,
         }
         if with_gather is not None:

@@ -155,6 +155,17 @@ int pbn_step(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, in
              uint8_t* d_flags, void* stream);
 
 /*
+ * pbn_step with the step index read from device memory (*d_step, 8-byte aligned) when the
+ * kernel runs instead of passed by value, so one captured hipGraph of a frame (act + step +
+ * replay + update) can be replayed for successive steps: the caller advances *d_step on the
+ * stream (e.g. a captured add).  Results are bit-identical to pbn_step(step = *d_step).
+ */
+int pbn_step_dev(pbn_net* net, uint64_t seed, const uint64_t* d_step, uint64_t env_offset, int64_t n_envs,
+                 uint32_t mode, const uint32_t* d_state, uint32_t* d_flipmask, uint8_t* d_target,
+                 uint8_t* d_t, uint32_t* d_state_out, uint32_t* d_final_state, float* d_reward,
+                 uint8_t* d_flags, void* stream);
+
+/*
  * n_steps synchronous transitions in one launch (steps step .. step+n_steps-1), with the
  * envs' state kept on chip between steps.  Bit-identical to n_steps successive pbn_step
  * calls that ping-pong d_state.  State, target and t are updated in place.
@@ -210,6 +221,16 @@ int pbn_obs_unpack(const pbn_net* net, int64_t n_envs, const uint32_t* d_state, 
 int pbn_q_to_flipmask(const pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs,
                       int32_t n_branches, int32_t n_actions, const float* d_q, float epsilon,
                       uint32_t* d_flipmask, int32_t* d_actions, void* stream);
+
+/*
+ * pbn_q_to_flipmask with the step index read from device memory, as pbn_step_dev, and
+ * epsilon read from *d_epsilon when that is not NULL (clamped to [0, 1], NaN -> 0), so an
+ * epsilon schedule can advance on the device between graph replays.
+ */
+int pbn_q_to_flipmask_dev(const pbn_net* net, uint64_t seed, const uint64_t* d_step, uint64_t env_offset,
+                          int64_t n_envs, int32_t n_branches, int32_t n_actions, const float* d_q,
+                          float epsilon, const float* d_epsilon, uint32_t* d_flipmask, int32_t* d_actions,
+                          void* stream);
 
 const char* pbn_last_error(void);
 int pbn_abi_version(void);

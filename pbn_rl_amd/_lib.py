@@ -23,8 +23,9 @@ FLAG_IN_ATTRACTOR = 4
 FLAG_PERTURBED = 8
 FLAG_RESET = 16
 
-EXPORTS = ["pbn_net_create", "pbn_net_destroy", "pbn_net_words", "pbn_reset", "pbn_step", "pbn_rollout",
-           "pbn_state_histogram", "pbn_obs_unpack", "pbn_q_to_flipmask", "pbn_last_error", "pbn_abi_version"]
+EXPORTS = ["pbn_net_create", "pbn_net_destroy", "pbn_net_words", "pbn_reset", "pbn_step", "pbn_step_dev",
+           "pbn_rollout", "pbn_state_histogram", "pbn_obs_unpack", "pbn_q_to_flipmask", "pbn_q_to_flipmask_dev",
+           "pbn_last_error", "pbn_abi_version"]
 SOURCES = ["pbn_env.hip", "pbn_agent.hip"]
 
 _lib: Optional[ctypes.CDLL] = None
@@ -66,6 +67,8 @@ def load() -> ctypes.CDLL:
     L.pbn_reset.restype = ctypes.c_int
     L.pbn_step.argtypes = [vp, u64, u64, u64, i64, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.pbn_step.restype = ctypes.c_int
+    L.pbn_step_dev.argtypes = [vp, u64, vp, u64, i64, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.pbn_step_dev.restype = ctypes.c_int
     L.pbn_rollout.argtypes = [vp, u64, u64, u64, i64, ctypes.c_int32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.pbn_rollout.restype = ctypes.c_int
     L.pbn_state_histogram.argtypes = [vp, i64, i64, i64, ctypes.c_int32, vp, vp]
@@ -75,6 +78,9 @@ def load() -> ctypes.CDLL:
     L.pbn_q_to_flipmask.argtypes = [vp, u64, u64, u64, i64, ctypes.c_int32, ctypes.c_int32, vp, ctypes.c_float,
                                     vp, vp, vp]
     L.pbn_q_to_flipmask.restype = ctypes.c_int
+    L.pbn_q_to_flipmask_dev.argtypes = [vp, u64, vp, u64, i64, ctypes.c_int32, ctypes.c_int32, vp, ctypes.c_float,
+                                        vp, vp, vp, vp]
+    L.pbn_q_to_flipmask_dev.restype = ctypes.c_int
     L.pbn_last_error.argtypes = []
     L.pbn_last_error.restype = ctypes.c_char_p
     L.pbn_abi_version.argtypes = []

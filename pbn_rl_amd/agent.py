@@ -30,22 +30,39 @@ __all__ = ["MyBilinear", "BranchingQNetwork", "BatchedBDQ", "load_bdq_checkpoint
 
 
 class MyBilinear(nn.Module):
-    """nn.Bilinear over input[0], input[1] (bdq_model/network.py:8-21).  The forward is the
-    same sum, arranged as (B, N1*N2) @ (N1*N2, out) so one GEMM does all of it."""
+    """nn.Bilinear over input[0], input[1] (bdq_model/network.py:8-21), as GEMMs.
+
+    y[b, o] = bias[o] + sum_ij a[b, i] W[o, i, j] b[b, j] is evaluated in one of two orders:
+      outer     (B, N1*N2) @ (N1*N2, out): one GEMM over the outer product (large batches:
+                the acting forward over all envs)
+      contract  T = b @ W.view(out*N1, N2)^T, then y = T.view(B, out, N1) @ a (batched): for
+                small batches (replay updates), where the outer form's (B x out) output is one
+                or two GEMM tiles and leaves the chip idle
+    ``form`` = "auto" picks contract below ``contract_rows`` rows."""
+
+    contract_rows = 4096
 
     def __init__(self, input1_dim: int, input2_dim: int, output_dim: int):
         super().__init__()
         self.input1_dim, self.input2_dim, self.output_dim = input1_dim, input2_dim, output_dim
         self.bilinear = nn.Bilinear(input1_dim, input2_dim, output_dim)
+        self.form = "auto"
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         a, b = x[0], x[1]
         lead = a.shape[:-1]
         a2 = a.reshape(-1, self.input1_dim)
         b2 = b.reshape(-1, self.input2_dim)
-        outer = (a2[:, :, None] * b2[:, None, :]).reshape(a2.shape[0], -1)
-        w = self.bilinear.weight.reshape(self.output_dim, -1)
-        y = torch.addmm(self.bilinear.bias, outer, w.t())
+        rows = a2.shape[0]
+        form = self.form if self.form != "auto" else ("contract" if rows < self.contract_rows else "outer")
+        if form == "contract":
+            t = b2 @ self.bilinear.weight.reshape(-1, self.input2_dim).t()          # (B, out*N1)
+            y = torch.baddbmm(self.bilinear.bias.view(1, -1, 1), t.view(rows, self.output_dim, self.input1_dim),
+                              a2.unsqueeze(2)).squeeze(2)
+        else:
+            outer = (a2[:, :, None] * b2[:, None, :]).reshape(rows, -1)
+            w = self.bilinear.weight.reshape(self.output_dim, -1)
+            y = torch.addmm(self.bilinear.bias, outer, w.t())
         return y.reshape(*lead, self.output_dim)
 
 
@@ -82,13 +99,11 @@ class BranchingQNetwork(nn.Module):
         z = F.leaky_relu(torch.addmm(b1, h, w1.t()))                  # (B, 64(K+1))
         z = z.view(z.shape[0], len(heads), -1).transpose(0, 1)        # (K+1, B, 64)
         A = self.ac_dim
-        w2 = torch.zeros(len(heads), A, z.shape[2], dtype=h.dtype, device=h.device)
-        b2 = torch.zeros(len(heads), 1, A, dtype=h.dtype, device=h.device)
-        w2[0, :1] = self.value_head[2].weight                         # value: output 0 of head 0
-        b2[0, 0, :1] = self.value_head[2].bias
-        for k, hd in enumerate(self.adv_heads):
-            w2[k + 1] = hd[2].weight
-            b2[k + 1, 0] = hd[2].bias
+        # value head zero-padded to A outputs (only output 0 is used); one stack per operand
+        w2 = torch.stack([F.pad(self.value_head[2].weight, (0, 0, 0, A - 1))]
+                         + [hd[2].weight for hd in self.adv_heads])   # (K+1, A, 64)
+        b2 = torch.stack([F.pad(self.value_head[2].bias, (0, A - 1))]
+                         + [hd[2].bias for hd in self.adv_heads]).unsqueeze(1)   # (K+1, 1, A)
         out = torch.baddbmm(b2, z, w2.transpose(1, 2))                # (K+1, B, A)
         v = out[0, :, :1]                                             # (B, 1)
         adv = out[1:].transpose(0, 1)                                 # (B, K, A)
@@ -134,6 +149,28 @@ class BatchedBDQ:
                                            self.branches, env.n_nodes + 1, q.data_ptr(), eps,
                                            env.flipmask.data_ptr(), self.actions.data_ptr(), env._stream()),
                        "pbn_q_to_flipmask")
+        return env.flipmask
+
+    def act_dev(self, q: torch.Tensor, step_t: torch.Tensor, epsilon_t: Optional[torch.Tensor] = None,
+                epsilon: Optional[float] = None) -> torch.Tensor:
+        """``act`` through ``pbn_q_to_flipmask_dev``: the step index (int64) and, when given,
+        epsilon (float32) are read from one-element device tensors (graph replays)."""
+        env = self.env
+        q = q.contiguous()
+        if q.shape != (env.n_alloc, self.branches, env.n_nodes + 1):
+            raise ValueError(f"Q must have shape {(env.n_alloc, self.branches, env.n_nodes + 1)}")
+        if step_t.dtype != torch.int64 or step_t.numel() != 1:
+            raise ValueError("step_t must be a one-element int64 tensor")
+        if epsilon_t is not None and (epsilon_t.dtype != torch.float32 or epsilon_t.numel() != 1):
+            raise ValueError("epsilon_t must be a one-element float32 tensor")
+        eps = self.epsilon if epsilon is None else float(epsilon)
+        L = _lib.load()
+        with torch.cuda.device(env.device):
+            _lib.check(L.pbn_q_to_flipmask_dev(env.net.handle, env.seed, step_t.data_ptr(), env.env_offset,
+                                               env.n_alloc, self.branches, env.n_nodes + 1, q.data_ptr(), eps,
+                                               epsilon_t.data_ptr() if epsilon_t is not None else None,
+                                               env.flipmask.data_ptr(), self.actions.data_ptr(), env._stream()),
+                       "pbn_q_to_flipmask_dev")
         return env.flipmask
 
     @torch.no_grad()

@@ -81,7 +81,9 @@ __device__ __forceinline__ int argmax_row(const float* __restrict__ r, int A) {
 // odd for the kaban networks' K = 3, so the per-lane row reads spread over the banks.
 __global__ void __launch_bounds__(kQEnvs) q_to_flipmask_kernel(const float* __restrict__ q, int K, int A, int N,
                                                                int W, int64_t n, uint64_t seed, uint64_t step,
+                                                               const uint64_t* __restrict__ d_step,
                                                                uint64_t env_offset, uint64_t eps_u,
+                                                               const float* __restrict__ d_eps,
                                                                uint32_t* __restrict__ flipmask,
                                                                int32_t* __restrict__ actions) {
   extern __shared__ float sq[];
@@ -95,7 +97,11 @@ __global__ void __launch_bounds__(kQEnvs) q_to_flipmask_kernel(const float* __re
   if ((int)threadIdx.x >= n_blk) return;
   const int64_t e = e0 + threadIdx.x;
   const uint64_t ge = env_offset + (uint64_t)e;
-  const pbn::Word4 r = pbn::draw(seed, ge, step, pbn::kStreamExplore, 0);
+  const pbn::Word4 r = pbn::draw(seed, ge, d_step ? *d_step : step, pbn::kStreamExplore, 0);
+  if (d_eps) {   // device epsilon (graph replays): clamped to [0, 1], NaN -> 0
+    const float ef = fminf(fmaxf(*d_eps, 0.f), 1.f);
+    eps_u = (uint64_t)floor((double)ef * 4294967296.0);
+  }
   const bool explore = (uint64_t)r.x < eps_u;
   const uint32_t rw[3] = {r.y, r.z, r.w};
   uint32_t m[4] = {0u, 0u, 0u, 0u};
@@ -146,9 +152,10 @@ int pbn_obs_unpack(const pbn_net* net, int64_t n_envs, const uint32_t* d_state, 
   return PBN_OK;
 }
 
-int pbn_q_to_flipmask(const pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs,
-                      int32_t n_branches, int32_t n_actions, const float* d_q, float epsilon, uint32_t* d_flipmask,
-                      int32_t* d_actions, void* stream) {
+static int q_to_flipmask_impl(const pbn_net* net, uint64_t seed, uint64_t step, const uint64_t* d_step,
+                              uint64_t env_offset, int64_t n_envs, int32_t n_branches, int32_t n_actions,
+                              const float* d_q, float epsilon, const float* d_epsilon, uint32_t* d_flipmask,
+                              int32_t* d_actions, void* stream) {
   pbn::NetView v;
   int rc = pbn::net_view(net, &v);
   if (rc) return rc;
@@ -167,10 +174,27 @@ int pbn_q_to_flipmask(const pbn_net* net, uint64_t seed, uint64_t step, uint64_t
   if (lds > 64 * 1024) return pbn::set_error(PBN_EINVAL, "n_branches * n_actions too large");
   const unsigned blocks = (unsigned)((n_envs + kQEnvs - 1) / kQEnvs);
   hipLaunchKernelGGL(q_to_flipmask_kernel, dim3(blocks), dim3(kQEnvs), lds, (hipStream_t)stream, d_q, n_branches,
-                     n_actions, v.n_nodes, v.W, n_envs, seed, step, env_offset, eps_u, d_flipmask, d_actions);
+                     n_actions, v.n_nodes, v.W, n_envs, seed, step, d_step, env_offset, eps_u, d_epsilon, d_flipmask, d_actions);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return pbn::set_error(PBN_EDEVICE, hipGetErrorString(e));
   return PBN_OK;
+}
+
+int pbn_q_to_flipmask(const pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs,
+                      int32_t n_branches, int32_t n_actions, const float* d_q, float epsilon, uint32_t* d_flipmask,
+                      int32_t* d_actions, void* stream) {
+  return q_to_flipmask_impl(net, seed, step, nullptr, env_offset, n_envs, n_branches, n_actions, d_q, epsilon,
+                            nullptr, d_flipmask, d_actions, stream);
+}
+
+int pbn_q_to_flipmask_dev(const pbn_net* net, uint64_t seed, const uint64_t* d_step, uint64_t env_offset,
+                          int64_t n_envs, int32_t n_branches, int32_t n_actions, const float* d_q, float epsilon,
+                          const float* d_epsilon, uint32_t* d_flipmask, int32_t* d_actions, void* stream) {
+  if (!d_step) return pbn::set_error(PBN_EINVAL, "null d_step");
+  if (((uintptr_t)d_step & 7u) != 0) return pbn::set_error(PBN_EINVAL, "d_step must be 8-byte aligned");
+  if (d_epsilon && ((uintptr_t)d_epsilon & 3u) != 0) return pbn::set_error(PBN_EINVAL, "d_epsilon misaligned");
+  return q_to_flipmask_impl(net, seed, 0, d_step, env_offset, n_envs, n_branches, n_actions, d_q, epsilon,
+                            d_epsilon, d_flipmask, d_actions, stream);
 }
 
 }  // extern "C"

@@ -66,6 +66,7 @@ struct StepArgs {
   float* reward;
   uint8_t* flags;
   uint64_t seed, step, env_offset;
+  const uint64_t* step_ptr;     // single-step kernel: step index read from device memory (nullable)
   int64_t n_envs;
   int64_t n_groups;
   int n_nodes;
@@ -418,7 +419,10 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
     }
   }
   const uint32_t kk0 = k0, kk1 = k1, ge_lo = (uint32_t)ge, G_lo = (uint32_t)G;
-  const uint64_t step = a.step + (uint64_t)ks;
+  uint64_t step = a.step + (uint64_t)ks;
+  if constexpr (VARIANT == 1) {
+    if (a.step_ptr) step = *a.step_ptr;   // graph-replayable single step (pbn_step_dev)
+  }
   const uint32_t st_lo = (uint32_t)step;
   const uint32_t st_hi = (uint32_t)((step >> 32) & 0xFFFFu) << 16;
   const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | st_hi;
@@ -2103,10 +2107,10 @@ int pbn_reset(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, i
   return PBN_OK;
 }
 
-int pbn_step(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs, uint32_t mode,
-             const uint32_t* d_state, uint32_t* d_flipmask, uint8_t* d_target, uint8_t* d_t,
-             uint32_t* d_state_out, uint32_t* d_final_state, float* d_reward, uint8_t* d_flags,
-             void* stream) {
+static int step_impl(pbn_net* net, uint64_t seed, uint64_t step, const uint64_t* d_step, uint64_t env_offset,
+                     int64_t n_envs, uint32_t mode, const uint32_t* d_state, uint32_t* d_flipmask,
+                     uint8_t* d_target, uint8_t* d_t, uint32_t* d_state_out, uint32_t* d_final_state,
+                     float* d_reward, uint8_t* d_flags, void* stream) {
   int rc = check_common(net, env_offset, n_envs);
   if (rc) return rc;
   if (n_envs == 0) return PBN_OK;
@@ -2133,6 +2137,7 @@ int pbn_step(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, in
   a.flags = d_flags;
   a.seed = seed;
   a.step = step;
+  a.step_ptr = d_step;
   a.env_offset = env_offset;
   a.n_envs = n_envs;
   a.n_groups = n_envs / 32;
@@ -2176,6 +2181,24 @@ int pbn_step(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, in
   hipLaunchKernelGGL(net->wave1, dim3(blocks), dim3(64 * kWavesPerBlock), net->lds_wave, (hipStream_t)stream, a);
   HIP_OK(hipGetLastError());
   return PBN_OK;
+}
+
+int pbn_step(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs, uint32_t mode,
+             const uint32_t* d_state, uint32_t* d_flipmask, uint8_t* d_target, uint8_t* d_t,
+             uint32_t* d_state_out, uint32_t* d_final_state, float* d_reward, uint8_t* d_flags,
+             void* stream) {
+  return step_impl(net, seed, step, nullptr, env_offset, n_envs, mode, d_state, d_flipmask, d_target, d_t,
+                   d_state_out, d_final_state, d_reward, d_flags, stream);
+}
+
+int pbn_step_dev(pbn_net* net, uint64_t seed, const uint64_t* d_step, uint64_t env_offset, int64_t n_envs,
+                 uint32_t mode, const uint32_t* d_state, uint32_t* d_flipmask, uint8_t* d_target, uint8_t* d_t,
+                 uint32_t* d_state_out, uint32_t* d_final_state, float* d_reward, uint8_t* d_flags,
+                 void* stream) {
+  if (!d_step) return fail(PBN_EINVAL, "null d_step");
+  if (((uintptr_t)d_step & 7u) != 0) return fail(PBN_EINVAL, "d_step must be 8-byte aligned");
+  return step_impl(net, seed, 0, d_step, env_offset, n_envs, mode, d_state, d_flipmask, d_target, d_t,
+                   d_state_out, d_final_state, d_reward, d_flags, stream);
 }
 
 int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs,

@@ -72,10 +72,36 @@ class DeviceReplay:
         self.pos = (self.pos + n) % self.capacity
         self.size = min(self.size + n, self.capacity)
 
-    def sample_indices(self, batch: int, generator: Optional[torch.Generator] = None) -> torch.Tensor:
-        if self.size == 0:
-            raise ValueError("empty replay")
-        return torch.randint(0, self.size, (batch,), device=self.device, generator=generator)
+    def store_at(self, pos_t: torch.Tensor, size_t: torch.Tensor, state, target, action, reward, next_state,
+                 done) -> None:
+        """``store`` with the ring position and fill level held in one-element int64 device
+        tensors (advanced here, on the stream) instead of host ints: graph-capturable.  The
+        caller mirrors them in ``pos`` / ``size``."""
+        n = target.shape[0]
+        if n > self.capacity:
+            raise ValueError("more transitions than the ring holds")
+        idx = (torch.arange(n, device=self.device, dtype=torch.int64) + pos_t) % self.capacity
+        self.state.index_copy_(1, idx, state)
+        self.next_state.index_copy_(1, idx, next_state)
+        self.target.index_copy_(0, idx, target.to(torch.uint8))
+        self.action.index_copy_(0, idx, action.to(torch.int32))
+        self.reward.index_copy_(0, idx, reward.to(torch.float32))
+        self.done.index_copy_(0, idx, done.to(torch.uint8))
+        pos_t.add_(n).remainder_(self.capacity)
+        size_t.add_(n).clamp_(max=self.capacity)
+
+    def sample_indices(self, batch: int, generator: Optional[torch.Generator] = None,
+                       size_t: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``batch`` indices uniform over the filled part, with replacement: floor(u * size)
+        for fp64 uniforms u.  ``size_t`` (a one-element int64 device tensor) replaces the host
+        fill level in graph-captured frames; both forms draw the same indices."""
+        if size_t is None:
+            if self.size == 0:
+                raise ValueError("empty replay")
+            size_t = torch.full((1,), self.size, dtype=torch.int64, device=self.device)
+        u = torch.rand(batch, dtype=torch.float64, device=self.device, generator=generator)
+        idx = (u * size_t).long()
+        return torch.minimum(idx, size_t - 1)
 
     def gather(self, idx: torch.Tensor, net_handle, stream=None) -> Dict[str, torch.Tensor]:
         """Rows ``idx`` (B a multiple of 32) as network inputs: obs / next_obs fp32 (2, B, N)
@@ -113,17 +139,21 @@ def soft_update(target: torch.nn.Module, online: torch.nn.Module) -> None:
 def bdq_update(q: torch.nn.Module, target: torch.nn.Module, opt: torch.optim.Optimizer, batch: Dict[str, torch.Tensor],
                gamma: float = 0.999, grad_clamp: float = 1.0) -> torch.Tensor:
     """One update_policy step (bdq_model/__init__.py:111-131) on a gathered batch; returns the loss."""
-    qvals = q(batch["obs"])                                             # (B, K, A)
-    current = qvals.gather(2, batch["actions"]).squeeze(-1)              # (B, K)
+    # q(obs) and q(next_obs) as one forward over 2B rows (half the launches; only the first
+    # half carries gradient)
+    B = batch["obs"].shape[1]
+    q_all = q(torch.cat([batch["obs"], batch["next_obs"]], 1))          # (2B, K, A)
+    current = q_all[:B].gather(2, batch["actions"]).squeeze(-1)         # (B, K)
     with torch.no_grad():
-        argmax = torch.argmax(q(batch["next_obs"]), dim=2)
+        argmax = torch.argmax(q_all[B:].detach(), dim=2)
         max_next = target(batch["next_obs"]).gather(2, argmax.unsqueeze(2)).squeeze(-1)
     expected = batch["rewards"] + max_next * gamma * batch["masks"]
     loss = F.mse_loss(expected, current)
     opt.zero_grad()
     loss.backward()
-    for p in q.parameters():
-        p.grad.data.clamp_(-grad_clamp, grad_clamp)
+    grads = [p.grad for p in q.parameters() if p.grad is not None]
+    torch._foreach_clamp_min_(grads, -grad_clamp)      # two multi-tensor launches, not one per tensor
+    torch._foreach_clamp_max_(grads, grad_clamp)
     opt.step()
     return loss.detach()
 
@@ -138,7 +168,8 @@ class BDQLearner:
     def __init__(self, env: VectorPBNEnv, qnet: Optional[BranchingQNetwork] = None, *, capacity: int = 10 ** 4,
                  batch_size: int = 256, learning_rate: float = 1e-4, gamma: float = 0.999,
                  target_update: int = 10_000, learning_starts: int = 288, updates_per_frame: int = 1,
-                 epsilon_start: float = 1.0, epsilon_final: float = 0.0, epsilon_decay: int = 10_000, seed: int = 0):
+                 epsilon_start: float = 1.0, epsilon_final: float = 0.0, epsilon_decay: int = 10_000, seed: int = 0,
+                 graphable: bool = False):
         if not env.keep_final_state:
             raise ValueError("BDQLearner needs the env's final_state (keep_final_state=True)")
         self.env = env
@@ -147,7 +178,8 @@ class BDQLearner:
         self.target = BranchingQNetwork((env.n_nodes, env.n_nodes), env.n_nodes + 1, self.agent.branches).to(env.device)
         self.target.load_state_dict(self.q.state_dict())
         # one fused multi-tensor kernel per step instead of a handful per parameter tensor
-        self.opt = torch.optim.Adam(self.q.parameters(), lr=learning_rate, fused=True)
+        # capturable keeps Adam's step counts on the device (needed to replay it in a hipGraph)
+        self.opt = torch.optim.Adam(self.q.parameters(), lr=learning_rate, fused=True, capturable=graphable)
         self.replay = DeviceReplay(max(capacity, env.n_alloc), env.words, self.agent.branches, env.device)
         self.batch_size, self.gamma, self.target_update = batch_size, gamma, target_update
         self.learning_starts = max(learning_starts, batch_size)
@@ -160,8 +192,12 @@ class BDQLearner:
         self.gen = torch.Generator(device=env.device)
         self.gen.manual_seed(seed)
         self.last_loss: Optional[torch.Tensor] = None
+        self.graphable = graphable
+        self._graph: Optional[torch.cuda.CUDAGraph] = None
 
     def frame(self):
+        if self._graph is not None:
+            return self._replay_frame()
         env = self.env
         state = env.state.clone()
         target = env.target.clone()
@@ -184,3 +220,78 @@ class BDQLearner:
                 if self.updates % self.target_update == 0:
                     soft_update(self.target, self.q)
         return reward, done
+
+    # ---- graph-captured frames -------------------------------------------------------------
+    def capture(self, min_updates: int = 3) -> None:
+        """Capture one whole learning frame (obs unpack, Q forward, epsilon-greedy flip masks,
+        pbn_step_dev, replay store, epsilon decay, ``updates_per_frame`` update_policy steps)
+        in a hipGraph; ``frame()`` replays it from then on.  The step index, epsilon, ring
+        position and fill level live in device tensors the graph advances, mirrored on the
+        host after every replay; target-network soft updates stay on the host (between
+        replays), so ``target_update`` must be a multiple of ``updates_per_frame``.
+
+        Frames run eagerly (on a side stream, as graph capture requires) until learning has
+        started and ``min_updates`` updates have initialised Adam's state and library
+        workspaces.  After capture, the env must only be stepped through ``frame()``."""
+        if not self.graphable:
+            raise ValueError("construct the learner with graphable=True to capture it")
+        if self.target_update % self.updates_per_frame:
+            raise ValueError("target_update must be a multiple of updates_per_frame")
+        env = self.env
+        dev = env.device
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            while self.replay.size < self.learning_starts or self.updates < min_updates:
+                self.frame()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self._step_t = torch.full((1,), env.step_index, dtype=torch.int64, device=dev)
+        self._eps64 = torch.full((1,), self.epsilon, dtype=torch.float64, device=dev)
+        self._eps32 = self._eps64.float()
+        self._pos_t = torch.full((1,), self.replay.pos, dtype=torch.int64, device=dev)
+        self._size_t = torch.full((1,), self.replay.size, dtype=torch.int64, device=dev)
+        g = torch.cuda.CUDAGraph()
+        g.register_generator_state(self.gen)
+        self.opt.zero_grad(set_to_none=True)
+        with torch.cuda.graph(g):
+            self._g_out = self._graph_body()
+        self._graph = g
+        # the capture recorded the frame without running it: nothing above advanced
+        torch.cuda.current_stream(dev).synchronize()
+
+    def _graph_body(self):
+        env = self.env
+        state = env.state.clone()
+        target = env.target.clone()
+        with torch.no_grad():
+            q = self.q(self.agent.observe())
+        self.agent.act_dev(q, self._step_t, self._eps32)
+        env.step_flipmask_dev(self._step_t)
+        self._step_t.add_(1)
+        done_all = (env.flags & (_lib.FLAG_TERMINATED | _lib.FLAG_TRUNCATED)) != 0
+        self.replay.store_at(self._pos_t, self._size_t, state, target, self.agent.actions, env.reward,
+                             env.final_state, done_all)
+        final = torch.full_like(self._eps64, self.epsilon_final)
+        self._eps64.copy_(torch.maximum(final, self._eps64 - self.epsilon_step))
+        self._eps32.copy_(self._eps64)
+        loss = None
+        for _ in range(self.updates_per_frame):
+            idx = self.replay.sample_indices(self.batch_size, self.gen, size_t=self._size_t)
+            batch = self.replay.gather(idx, env.net)
+            loss = bdq_update(self.q, self.target, self.opt, batch, self.gamma)
+        return env.reward[: env.num_envs], done_all[: env.num_envs], loss
+
+    def _replay_frame(self):
+        env, rp = self.env, self.replay
+        self._graph.replay()
+        env.step_index += 1
+        rp.pos = (rp.pos + env.n_alloc) % rp.capacity
+        rp.size = min(rp.size + env.n_alloc, rp.capacity)
+        self.epsilon = max(self.epsilon_final, self.epsilon - self.epsilon_step)
+        self.frames += 1
+        self.updates += self.updates_per_frame
+        if self.updates % self.target_update == 0:
+            soft_update(self.target, self.q)
+        reward, done, self.last_loss = self._g_out
+        return reward, done
+

@@ -147,6 +147,26 @@ class VectorPBNEnv:
         k = self.num_envs
         return self.state[:, :k], self.reward[:k], self.flags[:k]
 
+    def step_flipmask_dev(self, step_t: torch.Tensor):
+        """``step_flipmask(use_current=True)`` through ``pbn_step_dev``: the step index is read
+        from the int64 device tensor ``step_t`` when the kernel runs, and the new state is
+        copied back into ``self.state`` (no buffer swap), so the call can be captured in a
+        hipGraph and replayed.  Neither ``step_t`` nor ``step_index`` is advanced here: the
+        caller advances ``step_t`` on the stream and mirrors it in ``step_index``."""
+        if step_t.dtype != torch.int64 or step_t.device != self.device or step_t.numel() != 1:
+            raise ValueError("step_t must be a one-element int64 tensor on the env's device")
+        L = _lib.load()
+        mode = _lib.MODE_AUTORESET if self.autoreset else 0
+        fs = self.final_state.data_ptr() if self.final_state is not None else None
+        with torch.cuda.device(self.device):
+            _lib.check(L.pbn_step_dev(self.net.handle, self.seed, step_t.data_ptr(), self.env_offset, self.n_alloc,
+                                      mode, self.state.data_ptr(), self.flipmask.data_ptr(), self.target.data_ptr(),
+                                      self.t.data_ptr(), self._state_next.data_ptr(), fs, self.reward.data_ptr(),
+                                      self.flags.data_ptr(), self._stream()), "pbn_step_dev")
+        self.state.copy_(self._state_next)
+        k = self.num_envs
+        return self.state[:, :k], self.reward[:k], self.flags[:k]
+
     def rollout(self, n_steps: int, flipmasks: Optional[torch.Tensor] = None, random_actions: bool = True,
                 keep_obs: bool = False, keep_final: bool = True, out: Optional[dict] = None) -> dict:
         """``n_steps`` transitions in one ``pbn_rollout`` launch (state kept on chip).

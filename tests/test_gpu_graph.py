@@ -1,0 +1,134 @@
+"""Device-step entry points (pbn_step_dev / pbn_q_to_flipmask_dev) and the graph-captured BDQ
+learner: the device-index forms are bit-identical to the by-value forms, and replaying the
+captured frame reproduces the eager learner (same env trajectory and replay ring bit for
+bit; network parameters to fp32 rounding)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle
+from pbn_rl_amd.agent import BatchedBDQ, BranchingQNetwork
+from pbn_rl_amd.attractors import load_attractors
+from pbn_rl_amd.network import load_network
+from pbn_rl_amd.replay import BDQLearner
+from pbn_rl_amd.spec import EnvSpec
+from pbn_rl_amd.vector_env import VectorPBNEnv
+
+pytestmark = pytest.mark.gpu
+
+
+def u32(x):
+    return x.cpu().numpy().view(np.uint32)
+
+
+@pytest.mark.parametrize("name,p", [("pbn28", 0.02), ("pbn70", 0.01)])
+def test_step_dev_matches_step(name, p):
+    spec = EnvSpec(load_network(name), load_attractors(name), perturbation=p, horizon=6)
+    n, seed = 2048, 5
+    a, b = VectorPBNEnv(spec, n, seed=seed), VectorPBNEnv(spec, n, seed=seed)
+    a.reset()
+    b.reset()
+    rng = np.random.default_rng(1)
+    step_t = torch.zeros(1, dtype=torch.int64, device=b.device)
+    for k in range(8):
+        fm = torch.from_numpy(rng.integers(0, 2 ** 31, size=(spec.words, n), dtype=np.int64).astype(np.int32)
+                              & rng.integers(0, 2, size=(1, n)).astype(np.int32)).cuda()
+        if spec.n % 32:
+            fm[-1] &= (1 << (spec.n % 32)) - 1
+        sa, ra, fa = a.step_flipmask(fm)
+        step_t.fill_(b.step_index)
+        b.flipmask.copy_(fm)
+        sb, rb, fb = b.step_flipmask_dev(step_t)
+        b.step_index += 1
+        torch.cuda.synchronize()
+        assert torch.equal(sa, sb) and torch.equal(ra, rb) and torch.equal(fa, fb), k
+        assert torch.equal(a.final_state, b.final_state) and torch.equal(a.target, b.target)
+        assert torch.equal(a.t, b.t)
+
+
+def test_step_dev_matches_oracle():
+    spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.05)
+    n, seed = 256, 9
+    env = VectorPBNEnv(spec, n, seed=seed)
+    env.reset()
+    st, tg, t = oracle.reset(spec, seed, 0, 0, n)
+    step_t = torch.full((1,), 41, dtype=torch.int64, device=env.device)
+    env.flipmask.zero_()
+    env.step_flipmask_dev(step_t)
+    torch.cuda.synchronize()
+    ref = oracle.step(spec, seed, 41, 0, st, np.zeros((1, n), np.uint32), tg, t, 1)
+    assert np.array_equal(u32(env.state), ref["state_out"])
+    assert np.array_equal(env.reward.cpu().numpy(), ref["reward"])
+
+
+def test_act_dev_matches_act():
+    spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"))
+    n = 4096
+    env = VectorPBNEnv(spec, n, seed=3)
+    env.reset()
+    agent = BatchedBDQ(env, BranchingQNetwork((28, 28), 29, 3))
+    q = torch.randn(n, 3, 29, device=env.device)
+    step_t = torch.full((1,), 123, dtype=torch.int64, device=env.device)
+    env.step_index = 123
+    for eps in (0.0, 0.3, 1.0):
+        agent.act(q, eps)
+        fm, acts = env.flipmask.clone(), agent.actions.clone()
+        agent.act_dev(q, step_t, torch.full((1,), eps, dtype=torch.float32, device=env.device))
+        assert torch.equal(env.flipmask, fm) and torch.equal(agent.actions, acts), eps
+        agent.act_dev(q, step_t, None, epsilon=eps)
+        assert torch.equal(env.flipmask, fm) and torch.equal(agent.actions, acts), eps
+
+
+def _learner(n, seed):
+    spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.01)
+    env = VectorPBNEnv(spec, n, seed=seed)
+    torch.manual_seed(4)
+    lr = BDQLearner(env, BranchingQNetwork((28, 28), 29, 3), capacity=8 * n, learning_starts=2 * n,
+                    batch_size=256, target_update=4, epsilon_start=1.0, epsilon_final=1.0, seed=11,
+                    graphable=True)
+    env.reset()
+    return env, lr
+
+
+def test_captured_learner_matches_eager():
+    """epsilon = 1: actions do not depend on Q, so env and ring must agree exactly."""
+    n = 1024
+    env_e, eager = _learner(n, 21)
+    env_g, graph = _learner(n, 21)
+    graph.capture()
+    assert graph.updates == 3 and graph.frames == 4
+    for _ in range(graph.frames):
+        eager.frame()
+    for k in range(9):
+        re, de = eager.frame()
+        rg, dg = graph.frame()
+        torch.cuda.synchronize()
+        assert torch.equal(re, rg) and torch.equal(de, dg), k
+        assert torch.equal(env_e.state, env_g.state), k
+    assert graph.frames == eager.frames and graph.updates == eager.updates
+    assert env_e.step_index == env_g.step_index == int(graph._step_t.item())
+    R, S = eager.replay, graph.replay
+    assert R.pos == S.pos == int(graph._pos_t.item()) and R.size == S.size == int(graph._size_t.item())
+    for f in ("state", "next_state", "target", "action", "reward", "done"):
+        assert torch.equal(getattr(R, f), getattr(S, f)), f
+    for (k, pe), (_, pg) in zip(eager.q.named_parameters(), graph.q.named_parameters()):
+        assert torch.allclose(pe, pg, rtol=1e-4, atol=1e-5), k
+    for (k, pe), (_, pg) in zip(eager.target.named_parameters(), graph.target.named_parameters()):
+        assert torch.allclose(pe, pg, rtol=1e-4, atol=1e-5), k
+    assert torch.isfinite(graph.last_loss)
+    assert abs(float(eager.last_loss) - float(graph.last_loss)) <= 1e-3 * max(1.0, abs(float(eager.last_loss)))
+
+
+def test_captured_learner_epsilon_schedule():
+    spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"))
+    env = VectorPBNEnv(spec, 512, seed=2)
+    lr = BDQLearner(env, capacity=4096, learning_starts=1024, batch_size=128, epsilon_start=1.0,
+                    epsilon_final=0.5, epsilon_decay=6, target_update=2, updates_per_frame=2, graphable=True)
+    env.reset()
+    lr.capture(min_updates=2)
+    for _ in range(8):
+        lr.frame()
+    torch.cuda.synchronize()
+    assert lr.epsilon == 0.5
+    assert float(lr._eps64.item()) == lr.epsilon and lr.replay.size == 4096
+    assert torch.isfinite(lr.last_loss)

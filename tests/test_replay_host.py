@@ -54,3 +54,27 @@ def test_soft_update_halves():
     soft_update(t, q)
     for k, v in t.state_dict().items():
         assert torch.allclose(v, before[k] / 2 + q.state_dict()[k] / 2)
+
+
+def test_ring_device_position_matches_host_position():
+    """store_at / sample_indices(size_t=...) (the graph-captured forms) against store /
+    sample_indices with host ints, on CPU tensors."""
+    from pbn_rl_amd.replay import DeviceReplay
+    a, b = DeviceReplay(100, 2, 3, "cpu"), DeviceReplay(100, 2, 3, "cpu")
+    pos_t, size_t = torch.zeros(1, dtype=torch.int64), torch.zeros(1, dtype=torch.int64)
+    g = torch.Generator().manual_seed(0)
+    for k in range(5):          # 5 x 32 = 160 > 100: wraps
+        n = 32
+        st = torch.randint(-2 ** 31, 2 ** 31 - 1, (2, n), generator=g, dtype=torch.int32)
+        nst = torch.randint(-2 ** 31, 2 ** 31 - 1, (2, n), generator=g, dtype=torch.int32)
+        tg = torch.randint(0, 14, (n,), generator=g)
+        act = torch.randint(0, 29, (n, 3), generator=g)
+        rw, dn = torch.randn(n, generator=g), torch.randint(0, 2, (n,), generator=g)
+        a.store(st, tg, act, rw, nst, dn)
+        b.store_at(pos_t, size_t, st, tg, act, rw, nst, dn)
+        assert int(pos_t) == a.pos and int(size_t) == a.size
+    for f in ("state", "next_state", "target", "action", "reward", "done"):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+    i1 = a.sample_indices(4096, torch.Generator().manual_seed(3))
+    i2 = b.sample_indices(4096, torch.Generator().manual_seed(3), size_t=size_t)
+    assert torch.equal(i1, i2) and int(i1.min()) >= 0 and int(i1.max()) == 99

@@ -4,6 +4,8 @@
 
   ref     nn.Bilinear (torch's bilinear kernel path, as bdq_model/network.py runs it)
   gemm    pbn_rl_amd.agent.MyBilinear: one addmm over the outer product (the default)
+  --train B[,B..]: also forward + backward of the whole network at these batch sizes for both
+          MyBilinear forms (outer / contract), to place MyBilinear.contract_rows
 Prints one JSON line per variant: ms per forward and TFLOP/s.
 """
 import argparse
@@ -35,6 +37,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=32768)
     ap.add_argument("--n", type=int, default=28)
+    ap.add_argument("--train", default="")
     args = ap.parse_args()
     torch.manual_seed(0)
     net = BranchingQNetwork((args.n, args.n), args.n + 1, 3).cuda().eval()
@@ -50,6 +53,24 @@ def main():
             print(json.dumps({"variant": name, "envs": args.envs, "ms": ms, "tflops": f / ms / 1e9}), flush=True)
         err = (ref_first() - gemm_first()).abs().max().item()
         print(json.dumps({"bilinear_max_abs_diff": err}))
+    net.train()
+    for B in [int(v) for v in args.train.split(",") if v]:
+        xb = torch.randint(0, 2, (2, B, args.n), device="cuda").float()
+        outs = {}
+        for form in ("outer", "contract"):
+            net.model[0].form = form
+
+            def fb():
+                net.zero_grad(set_to_none=True)
+                q = net(xb)
+                q.square().mean().backward()
+                return q
+            ms = time_fn(fb)
+            with torch.no_grad():
+                outs[form] = net(xb)
+            print(json.dumps({"variant": f"fwd_bwd_{form}", "batch": B, "ms": ms}), flush=True)
+        print(json.dumps({"batch": B, "forms_max_abs_diff": (outs["outer"] - outs["contract"]).abs().max().item()}))
+        net.model[0].form = "auto"
 
 
 if __name__ == "__main__":
