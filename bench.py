@@ -143,6 +143,42 @@ def python_baseline(spec, seconds: float = 3.0):
             "sample": f"oracle/pyoracle.py single env, {k} steps"}
 
 
+def numpy_baseline(spec, envs: int, seconds: float = 5.0):
+    """The batched numpy restatement (oracle/np_oracle.py, vectorised over envs), 1 process."""
+    import numpy as np
+
+    from oracle import np_oracle
+
+    npo = np_oracle.NpPBN(spec)
+    n = min(envs, 65536)
+    st, tg, t = npo.reset(1, 0, 0, n)
+    flip = np.zeros_like(st)
+    k, t0 = 0, time.perf_counter()
+    while True:
+        out = npo.step(1, k + 1, 0, st, flip, tg, t, 3)
+        st, tg, t = out["state_out"], out["target"], out["t"]
+        k += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": n * k / el, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/np_oracle.py (numpy, vectorised over envs), {n} {spec.network.name} envs x {k} steps "
+                      f"({el:.1f} s)"}
+
+
+def host_info() -> dict:
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_count": os.cpu_count(), "cpu_model": model}
+
+
 def cpu_baseline_bdq(spec, qnet, seconds: float):
     """The BDQ frame on the host cores for ~`seconds`: numpy observation, the same Q-network
     on CPU torch, greedy flip masks and the C oracle step, 4096 envs per frame."""
@@ -427,6 +463,8 @@ def main():
             else:
                 out["cpu_baseline"] = cpu_baseline(spec, args.envs, args.cpu_seconds)
                 out["cpu_baseline_python"] = python_baseline(spec)
+                out["cpu_baseline_numpy"] = numpy_baseline(spec, args.envs)
+            out["host"] = host_info()
         print(json.dumps(out), flush=True)
     env.close()
     if world > 1:
