@@ -40,7 +40,7 @@ from .network import Network, load_network
 from .spec import NO_TARGET, EnvSpec
 from .vector_env import VectorPBNEnv
 
-__all__ = ["PBNEnv", "make", "Box", "MultiDiscrete"]
+__all__ = ["PBNEnv", "ControlPBNEnv", "make", "Box", "MultiDiscrete"]
 
 
 class Box:
@@ -263,11 +263,45 @@ class PBNEnv:
         self._venv.close()
 
 
+class ControlPBNEnv(PBNEnv):
+    """gym-PBN/ControlPBNEnv (train_control_gbdq.py:45-72): PBNEnv whose action is one binary
+    value per control node (control_gbdq_model/__init__.py:35,169: action_count =
+    len(env.control_nodes), 2 choices per branch).  Control node c_k is set to action[k] in s1
+    before the synchronous update: the flip mask is (s XOR v) on the control nodes, so the step
+    kernel runs unchanged and the action cost counts the control nodes that changed.  This is
+    an assumed semantics (PBNControlMultiEnv is absent; unpinned).
+
+    Control node indices outside [0, N) are kept in ``control_nodes`` (the agent sizes its
+    action from its length) but their action entries are ignored, with a warning: the reference
+    script lists node 14 of a 14-gene network."""
+
+    def __init__(self, N: Optional[int] = None, genes: Optional[Sequence[str]] = None, logic_functions=None,
+                 min_attractors: Optional[int] = None, *, control_nodes: Sequence[int] = (), **kwargs):
+        super().__init__(N, genes, logic_functions, min_attractors, **kwargs)
+        self.control_nodes = [int(c) for c in control_nodes]
+        bad = [c for c in self.control_nodes if not 0 <= c < self.N]
+        if bad:
+            warnings.warn(f"control nodes {bad} are outside [0, {self.N}) and will be ignored")
+        self._ctrl = [(k, c) for k, c in enumerate(self.control_nodes) if 0 <= c < self.N]
+        self.action_space = MultiDiscrete([2] * len(self.control_nodes))
+        self.discrete_action_space = self.action_space
+
+    def step(self, action):
+        vals = self._actions(action)
+        if len(vals) != len(self.control_nodes):
+            raise ValueError(f"expected {len(self.control_nodes)} control values, got {len(vals)}")
+        state = self._read_state()
+        flips = [c + 1 for k, c in self._ctrl if (int(vals[k]) & 1) != int(state[c])]
+        return super().step(flips)
+
+
 def make(env_id: str, **kwargs):
     """Minimal stand-in for gymnasium.make over the env ids the reference uses."""
     key = env_id.split("/")[-1]
     if key == "PBNEnv":
         return PBNEnv(**kwargs)
+    if key == "ControlPBNEnv":
+        return ControlPBNEnv(**kwargs)
     if key.startswith("BittnerMultiGeneral") or key.startswith("BittnerMulti-") or key.startswith("Bittner-"):
         n = kwargs.pop("N", None)
         if n is None:

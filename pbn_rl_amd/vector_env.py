@@ -16,7 +16,7 @@ import torch
 from . import _lib
 from .spec import EnvSpec
 
-__all__ = ["VectorPBNEnv", "actions_to_flipmask", "unpack_states", "pack_states"]
+__all__ = ["VectorPBNEnv", "actions_to_flipmask", "control_to_flipmask", "unpack_states", "pack_states"]
 
 
 def _round32(n: int) -> int:
@@ -41,6 +41,34 @@ def actions_to_flipmask(actions: torch.Tensor, n_nodes: int) -> torch.Tensor:
     words = (pad.view(n, W, 32) * weights).sum(dim=2)                  # (n, W) in [0, 2^32)
     words = torch.where(words >= 2 ** 31, words - 2 ** 32, words)
     return words.to(torch.int32).t().contiguous()
+
+
+def control_to_flipmask(state: torch.Tensor, values: torch.Tensor, control_nodes: Sequence[int],
+                        n_nodes: int) -> torch.Tensor:
+    """The ControlPBNEnv action form (train_control_gbdq.py:45-72, control_gbdq_model/__init__.py:
+    35,169): one binary action per control node.  Assumed semantics (gym_PBN's
+    PBNControlMultiEnv is absent, so this is unpinned): control node c_k takes the value
+    values[:, k] in s1, i.e. the flip mask is (s XOR v) restricted to the control nodes, and the
+    step then runs unchanged.  state (W, n) int32 words, values (n, C) 0/1 -> (W, n) int32."""
+    W, n = state.shape
+    if W != (n_nodes + 31) // 32:
+        raise ValueError(f"state has {W} words, {n_nodes} nodes need {(n_nodes + 31) // 32}")
+    if values.dim() == 1:
+        values = values[None, :]
+    if values.shape != (n, len(control_nodes)):
+        raise ValueError(f"values must have shape {(n, len(control_nodes))}")
+    v = values.to(device=state.device, dtype=torch.int64) & 1
+    vw = torch.zeros(W, n, dtype=torch.int64, device=state.device)
+    cw = [0] * W
+    for k, c in enumerate(control_nodes):
+        if not 0 <= c < n_nodes:
+            raise ValueError(f"control node {c} outside [0, {n_nodes})")
+        vw[c >> 5] |= v[:, k] << (c & 31)
+        cw[c >> 5] |= 1 << (c & 31)
+    vw = torch.where(vw >= 2 ** 31, vw - 2 ** 32, vw).to(torch.int32)
+    cm = torch.tensor([m - (1 << 32) if m >= 1 << 31 else m for m in cw], dtype=torch.int32,
+                      device=state.device)[:, None]
+    return (state ^ vw) & cm
 
 
 def unpack_states(words: torch.Tensor, n_nodes: int) -> torch.Tensor:
@@ -146,6 +174,12 @@ class VectorPBNEnv:
         self.state, self._state_next = self._state_next, self.state
         k = self.num_envs
         return self.state[:, :k], self.reward[:k], self.flags[:k]
+
+    def step_control(self, values: torch.Tensor, control_nodes: Sequence[int]):
+        """One transition with the ControlPBNEnv action form: control node c_k set to
+        values[:, k] (0/1, shape (num_envs, C)) before the update (see control_to_flipmask)."""
+        fm = control_to_flipmask(self.state[:, : self.num_envs], values, control_nodes, self.n_nodes)
+        return self.step_flipmask(fm)
 
     def step_flipmask_dev(self, step_t: torch.Tensor):
         """``step_flipmask(use_current=True)`` through ``pbn_step_dev``: the step index is read

@@ -120,3 +120,65 @@ def test_sharded_rollout_single_rank():
 def _reset(env):
     env.reset()
     return env
+
+
+MUSCLE_GENES = ["Pax7", "Myf5", "MyoD1", "MyoG", "miR1", "miR206", "FGF8", "SHH", "Pax3", "Mrf4",
+                "Mef2c", "Mef2a", "ID3", "WNT"]
+MUSCLE_FUNCS = [[("not miR1 and not MyoG and not miR206", 1.0)], [("Pax7 or Pax3 or WNT or SHH", 1.0)],
+                [("not ID3 and (FGF8 or Mef2c or Mef2a or Pax7 or SHH or WNT or Pax3)", 1.0)],
+                [("MyoG or MyoD1", 1.0)], [("Myf5", 1.0)], [("MyoG or Myf5 or MyoD1 or Mef2c", 1.0)],
+                [("FGF8", 1.0)], [("SHH", 1.0)], [("Pax3", 1.0)], [("MyoG or Mef2c or Mef2a", 1.0)],
+                [("Mef2c", 1.0)], [("Mef2a", 1.0)], [("ID3", 1.0)], [("WNT", 1.0)]]
+
+
+def test_control_env_like_train_control_gbdq():
+    """train_control_gbdq.py:45-72: the 14-gene network, control nodes [6..14] (14 is out of
+    range and ignored); each action sets the control nodes, checked against the Python oracle
+    fed the equivalent flip mask."""
+    with pytest.warns(UserWarning, match="control nodes"):
+        env = make("gym-PBN/ControlPBNEnv", N=14, genes=MUSCLE_GENES, logic_functions=MUSCLE_FUNCS,
+                   control_nodes=[6, 7, 8, 10, 11, 12, 13, 14], seed=3, perturbation=0.02)
+    assert len(env.control_nodes) == 8 and list(env.action_space.nvec) == [2] * 8
+    py = pyoracle.PyPBN(env.spec)
+    (state, target), _ = env.reset()
+    tgt, t = env.target_attractor_id, 0
+    rng = np.random.default_rng(1)
+    for k in range(30):
+        vals = rng.integers(0, 2, size=8)
+        step_idx = env._venv.step_index
+        obs, r, term, trunc, info = env.step(torch.tensor(vals, device="cuda"))
+        flip = [0] * 14
+        for j, c in enumerate(env.control_nodes):
+            if c < 14 and int(vals[j]) != int(state[c]):
+                flip[c] = 1
+        ref = py.step(env._seed, step_idx, 0, list(state), flip, tgt, t, 0)
+        assert list(obs) == ref["final_state"]
+        assert np.float32(r) == np.float32(ref["reward"])
+        # the identity-function inputs hold the set value unless perturbed
+        if not info["perturbed"]:
+            for j, c in enumerate(env.control_nodes[:7]):
+                if env.spec.network.nodes[c][0].inputs == (c,):
+                    assert obs[c] == vals[j]
+        state, t = obs, ref["t"]
+        if term or trunc:
+            (state, target), _ = env.reset()
+            tgt, t = env.target_attractor_id, 0
+    env.close()
+
+
+def test_vector_step_control_matches_flipmask_step():
+    from pbn_rl_amd.attractors import load_attractors
+    from pbn_rl_amd.network import load_network
+    from pbn_rl_amd.spec import EnvSpec
+    spec = EnvSpec(load_network("pbn70"), load_attractors("pbn70"), perturbation=0.01)
+    a, b = VectorPBNEnv(spec, 4096, seed=8), VectorPBNEnv(spec, 4096, seed=8)
+    a.reset()
+    b.reset()
+    ctrl = [1, 5, 33, 64, 69]
+    vals = torch.randint(0, 2, (4096, len(ctrl)), device="cuda")
+    from pbn_rl_amd.vector_env import control_to_flipmask
+    fm = control_to_flipmask(b.state[:, :4096], vals, ctrl, 70)
+    sa, ra, fa = a.step_control(vals, ctrl)
+    sb, rb, fb = b.step_flipmask(fm)
+    torch.cuda.synchronize()
+    assert torch.equal(sa, sb) and torch.equal(ra, rb) and torch.equal(fa, fb)

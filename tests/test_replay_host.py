@@ -78,3 +78,23 @@ def test_ring_device_position_matches_host_position():
     i1 = a.sample_indices(4096, torch.Generator().manual_seed(3))
     i2 = b.sample_indices(4096, torch.Generator().manual_seed(3), size_t=size_t)
     assert torch.equal(i1, i2) and int(i1.min()) >= 0 and int(i1.max()) == 99
+
+
+def test_control_to_flipmask():
+    """ControlPBNEnv action form: flip exactly the control nodes whose value differs."""
+    import pytest
+    from pbn_rl_amd.vector_env import control_to_flipmask, pack_states, unpack_states
+    g = torch.Generator().manual_seed(5)
+    N, n = 40, 64
+    bits = torch.randint(0, 2, (n, N), generator=g)
+    st = pack_states(bits, N)
+    ctrl = [0, 3, 31, 32, 39]
+    vals = torch.randint(0, 2, (n, len(ctrl)), generator=g)
+    fm = control_to_flipmask(st, vals, ctrl, N)
+    s1 = unpack_states(st ^ fm, N).long()
+    for k, c in enumerate(ctrl):
+        assert torch.equal(s1[:, c], vals[:, k])
+    others = [i for i in range(N) if i not in ctrl]
+    assert torch.equal(s1[:, others], bits[:, others].long())
+    with pytest.raises(ValueError):
+        control_to_flipmask(st, vals, [0, 3, 31, 32, 40], N)
