@@ -694,6 +694,16 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
 }
 
 
+// Block barrier ordering LDS only.  __syncthreads() is a workgroup fence on every address
+// space, so each wave would first wait (s_waitcnt vmcnt(0)) for its global stores -- the
+// per-step obs / reward / flags / flip-mask stores -- to complete.  The step loops
+// communicate through LDS alone and never read back what they store to HBM in the loop.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // ------------------------------- rollout kernel, three waves per pair of 32-env groups
 // Block = two groups (64 envs; lanes 32h..32h+31 of every wave work on group 2*block + h).
 // The step splits into work that depends only on the counter-based RNG and work that
@@ -802,6 +812,9 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
   uint32_t u_fl = __builtin_amdgcn_readfirstlane((a.obs ? 1u : 0u) | (a.final_state ? 2u : 0u) |
                                                  (random_actions ? 4u : 0u) | ((a.mode & PBN_MODE_AUTORESET) ? 8u : 0u));
   __syncthreads();
+  // drain the initial state loads here: otherwise the loop-carried st / t / target copies at
+  // the bottom of the loop wait on vmcnt(0), which also waits for every store of the step
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
 
   for (int k = 0; k <= n_steps; ++k) {
     asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
@@ -1041,7 +1054,7 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
       }
     }
     PBN_PSTAMP(k, 1);
-    __syncthreads();
+    lds_barrier();
     PBN_PSTAMP(k, 2);
   }
   if (role == 0 && valid) {
@@ -1432,7 +1445,7 @@ __global__ void __launch_bounds__(256, 4) pbn_rollout_plane(StepArgs a) {
       }
     }
     PBN_PSTAMP(k, 1);
-    __syncthreads();
+    lds_barrier();
     PBN_PSTAMP(k, 2);
   }
   if (role == 0) {
