@@ -53,13 +53,17 @@ def _spec_of(env) -> EnvSpec:
 
 def compute_ssd_hist(env, model: Optional[Callable] = None, resets: int = 300, iters: int = 100_000,
                      multiprocess: bool = False, *, burn_in: int = 0, seed: int = 0, chunk: int = 200,
-                     device=None) -> Tuple[np.ndarray, None]:
+                     device=None, graph: bool = True) -> Tuple[np.ndarray, None]:
     """Returns (ssd, plot): ssd[s] = fraction of counted steps spent in state s (float64,
     2^N entries, state s = bit i for node i); plot is None (no plotting backend here).
 
     ``model``: None (no interventions) or a policy mapping the (resets, N) uint8 state bits on
     the GPU to (resets, k) actions in [0, N] (0 = no-op), called every step.
     ``multiprocess`` is accepted for signature compatibility; chains already run in parallel.
+    ``graph``: with a model, capture one policy step (state unpack, model, flip masks,
+    pbn_step_dev, histogram) in a hipGraph after a first eager step has validated the
+    actions, and replay it; a model that cannot be captured (host syncs) raises, and
+    ``graph=False`` runs every step eagerly.  Both give the same histogram.
     """
     spec = _spec_of(env)
     N = spec.n
@@ -86,13 +90,34 @@ def compute_ssd_hist(env, model: Optional[Callable] = None, resets: int = 300, i
                 state_histogram(buf["final_state"].view(k, n), resets, N, hist)
                 left -= k
         else:
-            for it in range(burn_in + iters):
+            step_t = torch.full((1,), venv.step_index, dtype=torch.int64, device=dev)
+
+            def policy_step(count: bool, check: bool) -> None:
                 bits = unpack_states(venv.state[:, :resets], N)
-                actions = model(bits)
-                fm = actions_to_flipmask(actions.to(dev), N)
-                venv.step_flipmask(fm)
-                if it >= burn_in:
+                fm = actions_to_flipmask(model(bits).to(dev), N, check=check)
+                venv.flipmask[:, :resets].copy_(fm)
+                venv.step_flipmask_dev(step_t)
+                step_t.add_(1)
+                if count:
                     state_histogram(venv.final_state.view(1, n), resets, N, hist)
+
+            venv.flipmask.zero_()      # padding envs (n_alloc > resets) are never intervened on
+            total = burn_in + iters
+            it = 0
+            graphs = {}
+            while it < total:
+                count = it >= burn_in
+                if not graph or it == 0:
+                    policy_step(count, check=True)      # eager: the first step validates the actions
+                else:
+                    g = graphs.get(count)
+                    if g is None:
+                        g = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(g):
+                            policy_step(count, check=False)
+                        graphs[count] = g
+                    g.replay()
+                it += 1
         counts = hist.cpu().numpy().view(np.uint32).astype(np.float64)
     venv.close()
     total = counts.sum()

@@ -23,15 +23,17 @@ def _round32(n: int) -> int:
     return (n + 31) // 32 * 32
 
 
-def actions_to_flipmask(actions: torch.Tensor, n_nodes: int) -> torch.Tensor:
+def actions_to_flipmask(actions: torch.Tensor, n_nodes: int, check: bool = True) -> torch.Tensor:
     """(n, k) ints in [0, N] -> (W, n) int32 flip masks; 0 = no-op, a > 0 flips node a-1
-    once however often it is repeated (bdq_model/__init__.py:81-84,176)."""
+    once however often it is repeated (bdq_model/__init__.py:81-84,176).  ``check=False``
+    skips the range check (a host sync; out-of-range actions then flip nothing), for
+    graph-captured loops."""
     if actions.dim() == 1:
         actions = actions[:, None]
     n = actions.shape[0]
     W = (n_nodes + 31) // 32
     a = actions.to(torch.int64)
-    if bool(((a < 0) | (a > n_nodes)).any()):
+    if check and bool(((a < 0) | (a > n_nodes)).any()):
         raise ValueError(f"actions must be in [0, {n_nodes}]")
     node = torch.arange(1, n_nodes + 1, device=a.device)
     hit = (a[:, :, None] == node[None, None, :]).any(dim=1)          # (n, N)
