@@ -1,0 +1,49 @@
+"""bench.py's host-side arithmetic (no GPU): the algorithmic byte and FLOP counts the
+roofline is computed from (DESIGN.md "Kernels"), the launch plan, and the parameter count
+of the Q-network the FLOP formula describes."""
+import sys
+
+import pytest
+import torch
+
+import bench
+from pbn_rl_amd.agent import BranchingQNetwork
+
+
+def test_rollout_bytes_match_design():
+    # 12 + 13 T bytes per env per launch for one state word; 1,312 B at T = 100
+    assert bench.rollout_bytes_per_env(1, 100) == 1312
+    assert bench.rollout_bytes_per_env(1, 100) * 65536 == 85983232        # profiles/pmc_*: algorithmic
+    assert bench.rollout_bytes_per_env(3, 1) == 2 * (12 + 2) + 12 + 12 + 5
+
+
+def test_step_bytes():
+    assert bench.algorithmic_bytes_per_env(1) == 20                        # 20 B/env-step
+    assert bench.algorithmic_bytes_per_env(2) == 32
+
+
+@pytest.mark.parametrize("steps,chunk", [(2000, 100), (250, 100), (7, 3), (5, 10), (0, 4)])
+def test_launch_plan(steps, chunk):
+    plan = bench.launch_plan(steps, chunk)
+    assert sum(plan) == steps and all(0 < k <= chunk for k in plan)
+    assert all(k == chunk for k in plan[:-1])
+
+
+@pytest.mark.parametrize("n", [7, 28, 70])
+def test_qnet_flops_count_every_weight(n):
+    """2 x (multiply-adds) = 2 x (weights), since every weight is used once per env."""
+    net = BranchingQNetwork((n, n), n + 1, 3)
+    weights = sum(p.numel() for name, p in net.named_parameters() if name.endswith("weight"))
+    assert bench.qnet_flops_per_env(n) == 2 * weights
+
+
+def test_parse_defaults(monkeypatch):
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    a = bench.parse()
+    assert (a.gpus, a.steps, a.warmup, a.envs, a.network, a.chunk) == (1, 2000, 200, 65536, "pbn28", 100)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--workload", "bdq"])
+    a = bench.parse()
+    assert (a.steps, a.warmup, a.envs) == (200, 20, 32768)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--workload", "bdq-learn"])
+    a = bench.parse()
+    assert a.learn_graph and a.no_graph and a.no_cpu_baseline
