@@ -23,7 +23,7 @@ is probabilistic: an attractor that no chain reached within ``burn_in`` steps is
 from __future__ import annotations
 
 from collections import deque
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 

@@ -18,7 +18,7 @@ Defaults: success 5, wrong attractor 2, action 1, step 0 (constructor kwargs).
 from __future__ import annotations
 
 import ctypes
-from typing import List, Optional, Sequence, Tuple
+from typing import Optional, Sequence
 
 import numpy as np
 

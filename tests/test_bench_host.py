@@ -4,7 +4,6 @@ of the Q-network the FLOP formula describes."""
 import sys
 
 import pytest
-import torch
 
 import bench
 from pbn_rl_amd.agent import BranchingQNetwork

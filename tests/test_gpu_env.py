@@ -7,7 +7,6 @@ import torch
 from oracle import pyoracle
 from pbn_rl_amd.distributed import ShardedRollout
 from pbn_rl_amd.env import PBNEnv, make
-from pbn_rl_amd.ispl import parse_ispl
 from pbn_rl_amd.vector_env import VectorPBNEnv, actions_to_flipmask, pack_states, unpack_states
 
 pytestmark = pytest.mark.gpu

@@ -2,7 +2,6 @@
 import json
 import os
 
-import numpy as np
 
 from oracle import oracle, pyoracle
 
