@@ -118,7 +118,13 @@ def compute_ssd_hist(env, model: Optional[Callable] = None, resets: int = 300, i
                         graphs[count] = g
                     g.replay()
                 it += 1
-        counts = hist.cpu().numpy().view(np.uint32).astype(np.float64)
+        total = int(hist.sum(dtype=torch.int64).item())
+        counts = hist.cpu().numpy().view(np.uint32)
     venv.close()
-    total = counts.sum()
-    return (counts / total if total > 0 else counts), None
+    # one host pass over the 2^N bins (float64 out), not astype + divide
+    ssd = np.empty(counts.shape, dtype=np.float64)
+    if total > 0:
+        np.divide(counts, total, out=ssd)
+    else:
+        ssd[:] = 0.0
+    return ssd, None
