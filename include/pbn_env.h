@@ -205,6 +205,20 @@ int pbn_obs_unpack(const pbn_net* net, int64_t n_envs, const uint32_t* d_state, 
                    float* d_obs, void* stream);
 
 /*
+ * The bilinear first layer of BranchingQNetwork (bdq_model/network.py:8-21) for the
+ * observation pbn_obs_unpack would build, straight from the packed state:
+ *   d_y[e][o] = d_bias[o] + sum over the set bits i of env e's state of d_T[target_e][i][o]
+ *   d_T     in   float [n_attr][n_nodes][out_dim]: T[a][i][o] = sum_j t_a[j] W[o][i][j], t_a the
+ *                first state of attractor a (the caller's GEMM; W = the layer's weight)
+ *   d_bias  in   float [out_dim];  d_y out float [n][out_dim]
+ * Envs without a target (id >= n_attr) get the bias.  n_envs multiple of 32, out_dim a
+ * multiple of 4 in 4..1024, d_T / d_bias / d_y 16-byte aligned.
+ * Rows are added in ascending i (fp32; not bit-identical to a GEMM's order).
+ */
+int pbn_bilinear_targets(const pbn_net* net, int64_t n_envs, const uint32_t* d_state, const uint8_t* d_target,
+                         const float* d_T, const float* d_bias, int32_t out_dim, float* d_y, void* stream);
+
+/*
  * pbn_q_to_flipmask replaces epsilon-greedy predict + list(action.unique()) + the env's
  * action decoding (bdq_model/__init__.py:69-98,176; action a > 0 flips node a-1, :81-84):
  *   d_q         in   float [n][n_branches][n_actions], n_actions == n_nodes + 1, 16-byte aligned

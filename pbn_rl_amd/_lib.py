@@ -24,7 +24,8 @@ FLAG_PERTURBED = 8
 FLAG_RESET = 16
 
 EXPORTS = ["pbn_net_create", "pbn_net_destroy", "pbn_net_words", "pbn_reset", "pbn_step", "pbn_step_dev",
-           "pbn_rollout", "pbn_state_histogram", "pbn_obs_unpack", "pbn_q_to_flipmask", "pbn_q_to_flipmask_dev",
+           "pbn_rollout", "pbn_state_histogram", "pbn_obs_unpack", "pbn_bilinear_targets", "pbn_q_to_flipmask",
+           "pbn_q_to_flipmask_dev",
            "pbn_last_error", "pbn_abi_version"]
 SOURCES = ["pbn_env.hip", "pbn_agent.hip"]
 
@@ -75,6 +76,8 @@ def load() -> ctypes.CDLL:
     L.pbn_state_histogram.restype = ctypes.c_int
     L.pbn_obs_unpack.argtypes = [vp, i64, vp, vp, vp, vp]
     L.pbn_obs_unpack.restype = ctypes.c_int
+    L.pbn_bilinear_targets.argtypes = [vp, i64, vp, vp, vp, vp, ctypes.c_int32, vp, vp]
+    L.pbn_bilinear_targets.restype = ctypes.c_int
     L.pbn_q_to_flipmask.argtypes = [vp, u64, u64, u64, i64, ctypes.c_int32, ctypes.c_int32, vp, ctypes.c_float,
                                     vp, vp, vp]
     L.pbn_q_to_flipmask.restype = ctypes.c_int

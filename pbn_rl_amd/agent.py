@@ -65,6 +65,13 @@ class MyBilinear(nn.Module):
             y = torch.addmm(self.bilinear.bias, outer, w.t())
         return y.reshape(*lead, self.output_dim)
 
+    def target_table(self, targets: torch.Tensor) -> torch.Tensor:
+        """T[a, i, o] = sum_j targets[a, j] W[o, i, j] for (A, N2) 0/1 target rows: the layer
+        contracted with each target, the table pbn_bilinear_targets reads."""
+        w = self.bilinear.weight                                     # (out, N1, N2)
+        t = targets.to(w.dtype) @ w.permute(2, 1, 0).reshape(self.input2_dim, -1)
+        return t.view(targets.shape[0], self.input1_dim, self.output_dim)
+
 
 def _mlp(i: int, h: int, o: int) -> nn.Sequential:
     return nn.Sequential(nn.Linear(i, h), nn.LeakyReLU(), nn.Linear(h, o))
@@ -90,7 +97,11 @@ class BranchingQNetwork(nn.Module):
         self.adv_heads = nn.ModuleList([_mlp(32, 64, action_space_dimension) for _ in range(number_of_actions)])
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        h = self.model(x)                                             # (B, 32)
+        return self.forward_tail(self.model[0](x))
+
+    def forward_tail(self, y: torch.Tensor) -> torch.Tensor:
+        """The network after the bilinear layer: y (B, 256) -> Q (B, K, A)."""
+        h = self.model[1:](y)                                         # (B, 32)
         # the value head and the K advantage heads read the same h: their first layers run as
         # one (32 -> 64(K+1)) GEMM, their second layers as one batched GEMM over K+1 heads
         heads = [self.value_head] + list(self.adv_heads)
@@ -125,6 +136,13 @@ class BatchedBDQ:
         n = env.n_alloc
         self.obs = torch.empty(2, n, N, dtype=torch.float32, device=env.device)
         self.actions = torch.empty(n, self.branches, dtype=torch.int32, device=env.device)
+        # first state of every attractor: the target half of the observation (pbn_obs_unpack)
+        atts = env.spec.attractors
+        self.targets = torch.tensor([list(a[0]) for a in atts], dtype=torch.float32,
+                                    device=env.device).reshape(len(atts), N)
+        self.fast = isinstance(self.q.model[0], MyBilinear)
+        self._y = torch.empty(n, self.q.model[0].output_dim if self.fast else 1, dtype=torch.float32,
+                              device=env.device)
 
     def observe(self) -> torch.Tensor:
         """(2, n, N) fp32: env states and their target attractors' first states."""
@@ -173,10 +191,30 @@ class BatchedBDQ:
                        "pbn_q_to_flipmask_dev")
         return env.flipmask
 
+    def q_values(self) -> torch.Tensor:
+        """Q (n, K, N+1) of every env's (state, target) observation.  With the reference's
+        MyBilinear first layer this skips the fp32 observation: pbn_bilinear_targets computes
+        the bilinear layer from the packed state and a per-target table (one small GEMM), and
+        the rest of the network runs in PyTorch.  Equal to ``q(observe())`` up to fp32
+        summation order."""
+        if not self.fast:
+            return self.q(self.observe())
+        env = self.env
+        bil = self.q.model[0]
+        T = bil.target_table(self.targets).contiguous() if self.targets.shape[0] else None
+        bias = bil.bilinear.bias.contiguous()
+        L = _lib.load()
+        with torch.cuda.device(env.device):
+            _lib.check(L.pbn_bilinear_targets(env.net.handle, env.n_alloc, env.state.data_ptr(),
+                                              env.target.data_ptr(), T.data_ptr() if T is not None else None,
+                                              bias.data_ptr(), bil.output_dim, self._y.data_ptr(), env._stream()),
+                       "pbn_bilinear_targets")
+        return self.q.forward_tail(self._y)
+
     @torch.no_grad()
     def step(self, epsilon: Optional[float] = None):
         """One frame for every env; returns (state', reward, flags) views as VectorPBNEnv.step_flipmask."""
-        q = self.q(self.observe())
+        q = self.q_values()
         self.act(q, epsilon)
         return self.env.step_flipmask(use_current=True)
 

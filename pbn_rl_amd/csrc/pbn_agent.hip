@@ -6,11 +6,12 @@
 // action a > 0 flips node a-1 (:81-84).  Batched on the GPU these become two HBM-bound kernels
 // around the PyTorch Q-network forward:
 //
-//   pbn_obs_unpack     packed state words + target attractor id -> fp32 (2, n, N)
-//   pbn_q_to_flipmask  Q (n, K, N+1) -> epsilon-greedy actions -> flip mask words (W, n)
+//   pbn_obs_unpack        packed state words + target attractor id -> fp32 (2, n, N)
+//   pbn_bilinear_targets  the Q-network's bilinear layer straight from the packed state (below)
+//   pbn_q_to_flipmask     Q (n, K, N+1) -> epsilon-greedy actions -> flip mask words (W, n)
 //
-// Neither kernel does arithmetic worth an MFMA; both are one pass over their bytes with
-// coalesced 16-byte accesses.
+// None of them does arithmetic worth an MFMA; they are one pass over their bytes with
+// coalesced accesses.
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -60,6 +61,73 @@ __global__ void __launch_bounds__(kObsThreads) obs_unpack_kernel(const uint32_t*
     }
     out_s[q] = make_float4(vs[0], vs[1], vs[2], vs[3]);
     out_t[q] = make_float4(vt[0], vt[1], vt[2], vt[3]);
+  }
+}
+
+// The first layer of BranchingQNetwork is bilinear in (state, target):
+//   y[e][o] = bias[o] + sum_ij s_e[i] t_e[j] W[o][i][j]   (bdq_model/network.py:8-21).
+// Both inputs are 0/1 and t_e is the first state of env e's target attractor, one of A.  With
+// T[a][i][o] = sum_j t_a[j] W[o][i][j] precomputed (a (A, N) @ (N, N*O) GEMM), the layer is
+//   y[e][o] = bias[o] + sum over the set bits i of s_e of T[target_e][i][o],
+// i.e. |s_e| row reads of T (L2-resident: A * N * O floats) per env instead of the
+// (n, N*N) outer product and its (n, N*N) @ (N*N, O) GEMM.  Rows are added in ascending i.
+// One wave per env (four per block, kBilEnvs envs per block); lane l owns outputs 4l..4l+3
+// (+ 256 k), read and written as float4.  The env's state words and target id are
+// wave-uniform, so the bit loop is scalar; its row loads go out eight at a time and are then
+// added in ascending i (the L2 round trip, not the adds, is the cost of a row).
+constexpr int kBilThreads = 256;
+constexpr int kBilEnvs = 16;
+constexpr int kBilBatch = 8;
+
+template <int W>
+__global__ void __launch_bounds__(kBilThreads) bilinear_targets_kernel(const uint32_t* __restrict__ state,
+                                                                       const uint8_t* __restrict__ target,
+                                                                       const float* __restrict__ T,
+                                                                       const float* __restrict__ bias, int N,
+                                                                       int A, int O, uint32_t n,
+                                                                       float* __restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int O4 = O >> 2;
+  const uint32_t e0 = blockIdx.x * kBilEnvs;
+  const float4* bias4 = reinterpret_cast<const float4*>(bias);
+  for (int r = wv; r < kBilEnvs; r += kBilThreads / 64) {
+    const uint32_t e = e0 + (uint32_t)r;
+    if (e >= n) break;
+    const uint32_t tg = __builtin_amdgcn_readfirstlane((uint32_t)target[e]);
+    uint32_t words[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) words[w] = __builtin_amdgcn_readfirstlane(state[(size_t)w * n + e]);
+    float4* y4 = reinterpret_cast<float4*>(y + (size_t)e * O);
+    for (int o4 = lane; o4 < O4; o4 += 64) {
+      float4 acc = bias4[o4];
+      if (tg < (uint32_t)A) {
+        const float4* Ta = reinterpret_cast<const float4*>(T + (size_t)tg * N * O) + o4;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          uint32_t b = words[w];
+          while (b) {
+            int idx[kBilBatch];
+#pragma unroll
+            for (int k = 0; k < kBilBatch; ++k) {
+              idx[k] = b ? 32 * w + __builtin_ctz(b) : -1;
+              b = b ? (b & (b - 1u)) : 0u;
+            }
+            float4 v[kBilBatch];
+#pragma unroll
+            for (int k = 0; k < kBilBatch; ++k)
+              v[k] = idx[k] >= 0 ? Ta[(size_t)idx[k] * O4] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int k = 0; k < kBilBatch; ++k) {
+              if (idx[k] >= 0) {
+                acc.x += v[k].x; acc.y += v[k].y; acc.z += v[k].z; acc.w += v[k].w;
+              }
+            }
+          }
+        }
+      }
+      y4[o4] = acc;
+    }
   }
 }
 
@@ -147,6 +215,36 @@ int pbn_obs_unpack(const pbn_net* net, int64_t n_envs, const uint32_t* d_state, 
   const unsigned blocks = (unsigned)std::min<int64_t>((total4 + kObsThreads - 1) / kObsThreads, 8192);
   hipLaunchKernelGGL(obs_unpack_kernel, dim3(blocks), dim3(kObsThreads), 0, (hipStream_t)stream, d_state, d_target,
                      v.att_start, v.att_states, v.n_attr, v.n_nodes, v.W, (uint32_t)n_envs, d_obs);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return pbn::set_error(PBN_EDEVICE, hipGetErrorString(e));
+  return PBN_OK;
+}
+
+int pbn_bilinear_targets(const pbn_net* net, int64_t n_envs, const uint32_t* d_state, const uint8_t* d_target,
+                         const float* d_T, const float* d_bias, int32_t out_dim, float* d_y, void* stream) {
+  pbn::NetView v;
+  int rc = pbn::net_view(net, &v);
+  if (rc) return rc;
+  if ((rc = pbn::check_device(net))) return rc;
+  if (n_envs < 0 || (n_envs & 31)) return pbn::set_error(PBN_EINVAL, "n_envs must be a non-negative multiple of 32");
+  if (n_envs >= ((int64_t)1 << 31) / 1024) return pbn::set_error(PBN_EINVAL, "n_envs too large");
+  if (out_dim < 4 || out_dim > 1024 || (out_dim & 3)) return pbn::set_error(PBN_EINVAL, "out_dim must be a multiple of 4 in 4..1024");
+  if (n_envs == 0) return PBN_OK;
+  if (!d_state || !d_target || !d_bias || !d_y || (v.n_attr > 0 && !d_T)) return pbn::set_error(PBN_EINVAL, "null buffer");
+  if (!aligned16(d_bias) || !aligned16(d_y) || (d_T && !aligned16(d_T)))
+    return pbn::set_error(PBN_EINVAL, "d_T, d_bias and d_y must be 16-byte aligned");
+  const unsigned blocks = (unsigned)((n_envs + kBilEnvs - 1) / kBilEnvs);
+  const uint32_t n = (uint32_t)n_envs;
+  switch (v.W) {
+    case 1: hipLaunchKernelGGL(bilinear_targets_kernel<1>, dim3(blocks), dim3(kBilThreads), 0, (hipStream_t)stream,
+                               d_state, d_target, d_T, d_bias, v.n_nodes, v.n_attr, out_dim, n, d_y); break;
+    case 2: hipLaunchKernelGGL(bilinear_targets_kernel<2>, dim3(blocks), dim3(kBilThreads), 0, (hipStream_t)stream,
+                               d_state, d_target, d_T, d_bias, v.n_nodes, v.n_attr, out_dim, n, d_y); break;
+    case 3: hipLaunchKernelGGL(bilinear_targets_kernel<3>, dim3(blocks), dim3(kBilThreads), 0, (hipStream_t)stream,
+                               d_state, d_target, d_T, d_bias, v.n_nodes, v.n_attr, out_dim, n, d_y); break;
+    default: hipLaunchKernelGGL(bilinear_targets_kernel<4>, dim3(blocks), dim3(kBilThreads), 0, (hipStream_t)stream,
+                                d_state, d_target, d_T, d_bias, v.n_nodes, v.n_attr, out_dim, n, d_y); break;
+  }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return pbn::set_error(PBN_EDEVICE, hipGetErrorString(e));
   return PBN_OK;

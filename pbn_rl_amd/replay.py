@@ -202,7 +202,7 @@ class BDQLearner:
         state = env.state.clone()
         target = env.target.clone()
         with torch.no_grad():
-            q = self.q(self.agent.observe())
+            q = self.agent.q_values()
         self.agent.act(q, self.epsilon)
         _, reward, flags = env.step_flipmask(use_current=True)
         done_all = (env.flags & (_lib.FLAG_TERMINATED | _lib.FLAG_TRUNCATED)) != 0
@@ -264,7 +264,7 @@ class BDQLearner:
         state = env.state.clone()
         target = env.target.clone()
         with torch.no_grad():
-            q = self.q(self.agent.observe())
+            q = self.agent.q_values()
         self.agent.act_dev(q, self._step_t, self._eps32)
         env.step_flipmask_dev(self._step_t)
         self._step_t.add_(1)

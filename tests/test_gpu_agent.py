@@ -131,3 +131,40 @@ def test_bdq_step_graph_capture():
         ref_agent.step()
         torch.cuda.synchronize()
     assert torch.equal(env.state, ref_env.state)
+
+
+@pytest.mark.parametrize("name", ["pbn28", "pbn70", "pbn7"])
+def test_bilinear_targets_matches_module(name):
+    """pbn_bilinear_targets (from the packed state and a per-target table) against the
+    PyTorch fp32 MyBilinear on the unpacked observation; Q of the fast path against the module.
+    Tolerance: fp32, different summation order (<= 28 or 70 added rows of |w| < 1)."""
+    spec = make_spec(name, perturbation=0.05)
+    torch.manual_seed(5)
+    env = VectorPBNEnv(spec, 4096, seed=2)
+    agent = BatchedBDQ(env, BranchingQNetwork((spec.n, spec.n), spec.n + 1, 3))
+    env.reset()
+    for _ in range(3):
+        env.step_flipmask(random_actions=True)
+    with torch.no_grad():
+        q_fast = agent.q_values().clone()
+        y_fast = agent._y.clone()
+        obs = agent.observe()
+        y_ref = agent.q.model[0](obs)
+        q_ref = agent.q(obs)
+    torch.cuda.synchronize()
+    assert torch.allclose(y_fast, y_ref, rtol=1e-5, atol=1e-5), (y_fast - y_ref).abs().max()
+    assert torch.allclose(q_fast, q_ref, rtol=1e-4, atol=1e-5), (q_fast - q_ref).abs().max()
+
+
+def test_bilinear_targets_without_attractors_is_bias():
+    spec = EnvSpec(load_network("pbn28"), [], perturbation=0.01)
+    env = VectorPBNEnv(spec, 256, seed=1)
+    agent = BatchedBDQ(env, BranchingQNetwork((28, 28), 29, 3))
+    env.reset()
+    with torch.no_grad():
+        agent.q_values()
+        obs = agent.observe()
+        y_ref = agent.q.model[0](obs)
+    torch.cuda.synchronize()
+    bias = agent.q.model[0].bilinear.bias
+    assert torch.equal(agent._y, bias.expand_as(agent._y)) and torch.allclose(y_ref, agent._y, atol=1e-6)
