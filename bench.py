@@ -44,8 +44,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=None, help="untimed steps (default 200; bdq workload 20)")
     p.add_argument("--workload", choices=["env", "bdq", "bdq-learn"], default="env",
                    help="env: BASELINE config 2, the env step alone (in-kernel random interventions); "
-                        "bdq: config 5, the full BDQ frame per step (pbn_obs_unpack -> BranchingQNetwork "
-                        "forward in PyTorch -> pbn_q_to_flipmask -> pbn_step); bdq-learn: that frame plus "
+                        "bdq: config 5, the full BDQ frame per step (BranchingQNetwork forward: bilinear layer "
+                        "by pbn_bilinear_targets, the rest in PyTorch -> pbn_q_to_flipmask -> pbn_step); "
+                        "bdq-learn: that frame plus "
                         "storing the transitions in the device replay and one update_policy step of "
                         "batch 256 (one hipGraph per frame: step index, epsilon and ring position live on "
                         "the device; --no-graph launches it eagerly)")
@@ -213,9 +214,10 @@ def cpu_baseline_bdq(spec, qnet, seconds: float):
 def workload_text(args, chunk: int, rollout_mode: bool) -> str:
     common = (f"horizon {args.horizon}, p={args.perturbation}, prob_bits={args.prob_bits}")
     if args.workload == "bdq":
-        return (f"full BDQ rollout (config 5): {args.network} x {args.envs} envs per GPU, per step pbn_obs_unpack -> "
-                f"BranchingQNetwork fp32 forward (random init, seed 0) -> epsilon-greedy (eps={args.epsilon}) "
-                f"pbn_q_to_flipmask -> pbn_step, autoreset, {common}")
+        return (f"full BDQ rollout (config 5): {args.network} x {args.envs} envs per GPU, per step the "
+                f"BranchingQNetwork fp32 forward (random init, seed 0; bilinear layer by pbn_bilinear_targets from "
+                f"the packed state) -> epsilon-greedy (eps={args.epsilon}) pbn_q_to_flipmask -> pbn_step, "
+                f"autoreset, {common}")
     if args.workload == "bdq-learn":
         return (f"BDQ training frames: {args.network} x {args.envs} envs per GPU, per step the config-5 frame "
                 f"(eps={args.epsilon}), the envs' transitions into the device replay, one update_policy step "
@@ -389,7 +391,8 @@ def main():
         W = spec.words
         if agent is not None:
             bytes_launch = None
-            kernel = "BDQ frame (pbn_obs_unpack, BranchingQNetwork fp32 forward, pbn_q_to_flipmask, pbn_step)"
+            kernel = ("BDQ frame (pbn_bilinear_targets, BranchingQNetwork fp32 layers after the bilinear, "
+                      "pbn_q_to_flipmask, pbn_step)")
             if args.workload == "bdq-learn":
                 kernel += " + replay store + update_policy (batch 256)"
                 kernel += ", one hipGraph replay per frame" if args.learn_graph else ", eager"
@@ -403,15 +406,17 @@ def main():
         full_launch_ms = launch_ms * len(plan) * chunk / args.steps if rollout_mode else launch_ms
         traffic = None
         if agent is not None:
-            # the frame is dominated by the Q-network's fp32 GEMMs: price it against the
-            # FP32 matrix peak (MI355X_MICROARCH.md: 157.3 TFLOP/s)
+            # the frame is the Q-network: price the reference forward's FLOPs against the
+            # FP32 matrix peak (MI355X_MICROARCH.md: 157.3 TFLOP/s), as model-FLOPs utilisation
             flops = env.n_alloc * qnet_flops_per_env(spec.n)
             achieved = flops / (full_launch_ms * 1e-3) / 1e12
             roofline = {"bound": "mfma", "achieved": achieved, "peak": FP32_MATRIX_TFLOPS, "unit": "TFLOP/s",
                         "frac": achieved / FP32_MATRIX_TFLOPS, "traffic": None, "kernel": kernel,
                         "launch_ms": full_launch_ms, "flops_per_launch": flops,
-                        "note": "one launch = one whole BDQ frame (4+ kernels); achieved = Q-network FLOPs / "
-                                "frame time"}
+                        "note": "one launch = one whole BDQ frame (~20 kernels); achieved = the reference "
+                                "forward's FLOPs (bilinear counted as N*N*256 MACs per env) / frame time, i.e. "
+                                "model-FLOPs utilisation. The bilinear layer itself runs as per-target table "
+                                "reads (pbn_bilinear_targets), so the executed FLOPs are ~4x lower"}
         else:
             achieved = bytes_launch / (full_launch_ms * 1e-3) / 1e9
             pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.network}_{args.envs}_{args.mode}.json")
