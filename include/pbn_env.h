@@ -213,10 +213,12 @@ int pbn_obs_unpack(const pbn_net* net, int64_t n_envs, const uint32_t* d_state, 
  *   d_bias  in   float [out_dim];  d_y out float [n][out_dim]
  * Envs without a target (id >= n_attr) get the bias.  n_envs multiple of 32, out_dim a
  * multiple of 4 in 4..1024, d_T / d_bias / d_y 16-byte aligned.
- * Rows are added in ascending i (fp32; not bit-identical to a GEMM's order).
+ * Rows are added in ascending i (fp32; not bit-identical to a GEMM's order).  leaky != 0 applies
+ * the network's LeakyReLU (x > 0 ? x : x * slope) before the store.
  */
 int pbn_bilinear_targets(const pbn_net* net, int64_t n_envs, const uint32_t* d_state, const uint8_t* d_target,
-                         const float* d_T, const float* d_bias, int32_t out_dim, float* d_y, void* stream);
+                         const float* d_T, const float* d_bias, int32_t out_dim, int32_t leaky, float slope,
+                         float* d_y, void* stream);
 
 /*
  * pbn_q_to_flipmask replaces epsilon-greedy predict + list(action.unique()) + the env's

@@ -76,7 +76,8 @@ def load() -> ctypes.CDLL:
     L.pbn_state_histogram.restype = ctypes.c_int
     L.pbn_obs_unpack.argtypes = [vp, i64, vp, vp, vp, vp]
     L.pbn_obs_unpack.restype = ctypes.c_int
-    L.pbn_bilinear_targets.argtypes = [vp, i64, vp, vp, vp, vp, ctypes.c_int32, vp, vp]
+    L.pbn_bilinear_targets.argtypes = [vp, i64, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_float,
+                                       vp, vp]
     L.pbn_bilinear_targets.restype = ctypes.c_int
     L.pbn_q_to_flipmask.argtypes = [vp, u64, u64, u64, i64, ctypes.c_int32, ctypes.c_int32, vp, ctypes.c_float,
                                     vp, vp, vp]

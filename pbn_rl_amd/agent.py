@@ -99,9 +99,10 @@ class BranchingQNetwork(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return self.forward_tail(self.model[0](x))
 
-    def forward_tail(self, y: torch.Tensor) -> torch.Tensor:
-        """The network after the bilinear layer: y (B, 256) -> Q (B, K, A)."""
-        h = self.model[1:](y)                                         # (B, 32)
+    def forward_tail(self, y: torch.Tensor, skip_act: bool = False) -> torch.Tensor:
+        """The network after the bilinear layer: y (B, 256) -> Q (B, K, A); ``skip_act``: y
+        already went through model[1] (the LeakyReLU)."""
+        h = self.model[2:](y) if skip_act else self.model[1:](y)      # (B, 32)
         # the value head and the K advantage heads read the same h: their first layers run as
         # one (32 -> 64(K+1)) GEMM, their second layers as one batched GEMM over K+1 heads
         heads = [self.value_head] + list(self.adv_heads)
@@ -141,6 +142,9 @@ class BatchedBDQ:
         self.targets = torch.tensor([list(a[0]) for a in atts], dtype=torch.float32,
                                     device=env.device).reshape(len(atts), N)
         self.fast = isinstance(self.q.model[0], MyBilinear)
+        act = self.q.model[1] if len(self.q.model) > 1 else None
+        self._act = isinstance(act, nn.LeakyReLU)
+        self._slope = float(act.negative_slope) if self._act else 0.0
         self._y = torch.empty(n, self.q.model[0].output_dim if self.fast else 1, dtype=torch.float32,
                               device=env.device)
 
@@ -207,9 +211,11 @@ class BatchedBDQ:
         with torch.cuda.device(env.device):
             _lib.check(L.pbn_bilinear_targets(env.net.handle, env.n_alloc, env.state.data_ptr(),
                                               env.target.data_ptr(), T.data_ptr() if T is not None else None,
-                                              bias.data_ptr(), bil.output_dim, self._y.data_ptr(), env._stream()),
+                                              bias.data_ptr(), bil.output_dim, 1 if self._act else 0,
+                                              self._slope, self._y.data_ptr(), env._stream()),
                        "pbn_bilinear_targets")
-        return self.q.forward_tail(self._y)
+        # the kernel applied model[1] (LeakyReLU) when _act
+        return self.q.forward_tail(self._y, skip_act=self._act)
 
     @torch.no_grad()
     def step(self, epsilon: Optional[float] = None):

@@ -84,8 +84,8 @@ __global__ void __launch_bounds__(kBilThreads) bilinear_targets_kernel(const uin
                                                                        const uint8_t* __restrict__ target,
                                                                        const float* __restrict__ T,
                                                                        const float* __restrict__ bias, int N,
-                                                                       int A, int O, uint32_t n,
-                                                                       float* __restrict__ y) {
+                                                                       int A, int O, uint32_t n, int leaky,
+                                                                       float slope, float* __restrict__ y) {
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int O4 = O >> 2;
@@ -125,6 +125,12 @@ __global__ void __launch_bounds__(kBilThreads) bilinear_targets_kernel(const uin
             }
           }
         }
+      }
+      if (leaky) {   // the LeakyReLU after the layer, as torch computes it: x > 0 ? x : x * slope
+        acc.x = acc.x > 0.f ? acc.x : acc.x * slope;
+        acc.y = acc.y > 0.f ? acc.y : acc.y * slope;
+        acc.z = acc.z > 0.f ? acc.z : acc.z * slope;
+        acc.w = acc.w > 0.f ? acc.w : acc.w * slope;
       }
       y4[o4] = acc;
     }
@@ -221,7 +227,8 @@ int pbn_obs_unpack(const pbn_net* net, int64_t n_envs, const uint32_t* d_state, 
 }
 
 int pbn_bilinear_targets(const pbn_net* net, int64_t n_envs, const uint32_t* d_state, const uint8_t* d_target,
-                         const float* d_T, const float* d_bias, int32_t out_dim, float* d_y, void* stream) {
+                         const float* d_T, const float* d_bias, int32_t out_dim, int32_t leaky, float slope,
+                         float* d_y, void* stream) {
   pbn::NetView v;
   int rc = pbn::net_view(net, &v);
   if (rc) return rc;
@@ -237,13 +244,13 @@ int pbn_bilinear_targets(const pbn_net* net, int64_t n_envs, const uint32_t* d_s
   const uint32_t n = (uint32_t)n_envs;
   switch (v.W) {
     case 1: hipLaunchKernelGGL(bilinear_targets_kernel<1>, dim3(blocks), dim3(kBilThreads), 0, (hipStream_t)stream,
-                               d_state, d_target, d_T, d_bias, v.n_nodes, v.n_attr, out_dim, n, d_y); break;
+                               d_state, d_target, d_T, d_bias, v.n_nodes, v.n_attr, out_dim, n, leaky, slope, d_y); break;
     case 2: hipLaunchKernelGGL(bilinear_targets_kernel<2>, dim3(blocks), dim3(kBilThreads), 0, (hipStream_t)stream,
-                               d_state, d_target, d_T, d_bias, v.n_nodes, v.n_attr, out_dim, n, d_y); break;
+                               d_state, d_target, d_T, d_bias, v.n_nodes, v.n_attr, out_dim, n, leaky, slope, d_y); break;
     case 3: hipLaunchKernelGGL(bilinear_targets_kernel<3>, dim3(blocks), dim3(kBilThreads), 0, (hipStream_t)stream,
-                               d_state, d_target, d_T, d_bias, v.n_nodes, v.n_attr, out_dim, n, d_y); break;
+                               d_state, d_target, d_T, d_bias, v.n_nodes, v.n_attr, out_dim, n, leaky, slope, d_y); break;
     default: hipLaunchKernelGGL(bilinear_targets_kernel<4>, dim3(blocks), dim3(kBilThreads), 0, (hipStream_t)stream,
-                                d_state, d_target, d_T, d_bias, v.n_nodes, v.n_attr, out_dim, n, d_y); break;
+                                d_state, d_target, d_T, d_bias, v.n_nodes, v.n_attr, out_dim, n, leaky, slope, d_y); break;
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return pbn::set_error(PBN_EDEVICE, hipGetErrorString(e));

@@ -148,8 +148,9 @@ def test_bilinear_targets_matches_module(name):
     with torch.no_grad():
         q_fast = agent.q_values().clone()
         y_fast = agent._y.clone()
+        assert agent._act                   # the kernel applied the LeakyReLU
         obs = agent.observe()
-        y_ref = agent.q.model[0](obs)
+        y_ref = agent.q.model[1](agent.q.model[0](obs))       # bilinear + LeakyReLU
         q_ref = agent.q(obs)
     torch.cuda.synchronize()
     assert torch.allclose(y_fast, y_ref, rtol=1e-5, atol=1e-5), (y_fast - y_ref).abs().max()
@@ -164,7 +165,7 @@ def test_bilinear_targets_without_attractors_is_bias():
     with torch.no_grad():
         agent.q_values()
         obs = agent.observe()
-        y_ref = agent.q.model[0](obs)
+        y_ref = agent.q.model[1](agent.q.model[0](obs))
+        act_bias = agent.q.model[1](agent.q.model[0].bilinear.bias)
     torch.cuda.synchronize()
-    bias = agent.q.model[0].bilinear.bias
-    assert torch.equal(agent._y, bias.expand_as(agent._y)) and torch.allclose(y_ref, agent._y, atol=1e-6)
+    assert torch.equal(agent._y, act_bias.expand_as(agent._y)) and torch.allclose(y_ref, agent._y, atol=1e-6)
