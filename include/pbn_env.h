@@ -248,6 +248,19 @@ int pbn_q_to_flipmask_dev(const pbn_net* net, uint64_t seed, const uint64_t* d_s
                           float epsilon, const float* d_epsilon, uint32_t* d_flipmask, int32_t* d_actions,
                           void* stream);
 
+/*
+ * pbn_q_to_flipmask on the raw head outputs of BranchingQNetwork instead of Q:
+ *   d_heads  in  float [n_branches + 1][n][n_actions], head 0 = the value head (output 0 used),
+ *                heads 1.. = the advantage heads (bdq_model/network.py:55-61)
+ * The dueling combination is done in the kernel: q_a = (v + adv_a) - mean with mean the
+ * sequential sum of adv over a divided by n_actions, then as pbn_q_to_flipmask.  d_step and
+ * d_epsilon are optional device pointers (NULL: use step / epsilon), as in the _dev forms.
+ */
+int pbn_heads_to_flipmask(const pbn_net* net, uint64_t seed, uint64_t step, const uint64_t* d_step,
+                          uint64_t env_offset, int64_t n_envs, int32_t n_branches, int32_t n_actions,
+                          const float* d_heads, float epsilon, const float* d_epsilon, uint32_t* d_flipmask,
+                          int32_t* d_actions, void* stream);
+
 const char* pbn_last_error(void);
 int pbn_abi_version(void);
 

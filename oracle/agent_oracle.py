@@ -89,3 +89,19 @@ def q_to_flipmask(spec, q: np.ndarray, seed: int, step: int, env_offset: int, ep
             sel = hit & ((node >> 5) == ww)
             flip[ww] |= np.where(sel, np.left_shift(np.uint32(1), (node & 31).astype(np.uint32)), np.uint32(0))
     return flip, actions
+
+
+def heads_q(heads: np.ndarray) -> np.ndarray:
+    """Q (n, K, A) from raw head outputs (K+1, n, A) with pbn_heads_to_flipmask's arithmetic:
+    q_a = (v + adv_a) - mean, mean = sequential float32 sum of adv over a / A
+    (bdq_model/network.py:59-61; torch's mean reduces in a different order)."""
+    h = np.asarray(heads, dtype=np.float32)
+    K1, n, A = h.shape
+    v = h[0, :, 0]
+    adv = h[1:]                                            # (K, n, A)
+    s = np.zeros((K1 - 1, n), dtype=np.float32)
+    for j in range(A):                                     # left to right, in float32
+        s = (s + adv[:, :, j]).astype(np.float32)
+    mean = (s / np.float32(A)).astype(np.float32)
+    q = ((v[None, :, None] + adv).astype(np.float32) - mean[:, :, None]).astype(np.float32)
+    return np.ascontiguousarray(q.transpose(1, 0, 2))

@@ -26,7 +26,7 @@ FLAG_RESET = 16
 EXPORTS = ["pbn_net_create", "pbn_net_destroy", "pbn_net_words", "pbn_reset", "pbn_step", "pbn_step_dev",
            "pbn_rollout", "pbn_state_histogram", "pbn_obs_unpack", "pbn_bilinear_targets", "pbn_q_to_flipmask",
            "pbn_q_to_flipmask_dev",
-           "pbn_last_error", "pbn_abi_version"]
+           "pbn_heads_to_flipmask", "pbn_last_error", "pbn_abi_version"]
 SOURCES = ["pbn_env.hip", "pbn_agent.hip"]
 
 _lib: Optional[ctypes.CDLL] = None
@@ -85,6 +85,9 @@ def load() -> ctypes.CDLL:
     L.pbn_q_to_flipmask_dev.argtypes = [vp, u64, vp, u64, i64, ctypes.c_int32, ctypes.c_int32, vp, ctypes.c_float,
                                         vp, vp, vp, vp]
     L.pbn_q_to_flipmask_dev.restype = ctypes.c_int
+    L.pbn_heads_to_flipmask.argtypes = [vp, u64, u64, vp, u64, i64, ctypes.c_int32, ctypes.c_int32, vp, ctypes.c_float,
+                                        vp, vp, vp, vp]
+    L.pbn_heads_to_flipmask.restype = ctypes.c_int
     L.pbn_last_error.argtypes = []
     L.pbn_last_error.restype = ctypes.c_char_p
     L.pbn_abi_version.argtypes = []

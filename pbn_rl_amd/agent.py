@@ -102,6 +102,18 @@ class BranchingQNetwork(nn.Module):
     def forward_tail(self, y: torch.Tensor, skip_act: bool = False) -> torch.Tensor:
         """The network after the bilinear layer: y (B, 256) -> Q (B, K, A); ``skip_act``: y
         already went through model[1] (the LeakyReLU)."""
+        return self.dueling(self.forward_heads(y, skip_act))
+
+    @staticmethod
+    def dueling(out: torch.Tensor) -> torch.Tensor:
+        """Raw head outputs (K+1, B, A) -> Q (B, K, A) = v + adv - mean(adv) (:59-61)."""
+        v = out[0, :, :1]                                             # (B, 1)
+        adv = out[1:].transpose(0, 1)                                 # (B, K, A)
+        return v.unsqueeze(2) + adv - adv.mean(2, keepdim=True)
+
+    def forward_heads(self, y: torch.Tensor, skip_act: bool = False) -> torch.Tensor:
+        """y (B, 256) -> the raw outputs (K+1, B, A) of the value head (output 0) and the
+        advantage heads, before the dueling combination."""
         h = self.model[2:](y) if skip_act else self.model[1:](y)      # (B, 32)
         # the value head and the K advantage heads read the same h: their first layers run as
         # one (32 -> 64(K+1)) GEMM, their second layers as one batched GEMM over K+1 heads
@@ -116,10 +128,7 @@ class BranchingQNetwork(nn.Module):
                          + [hd[2].weight for hd in self.adv_heads])   # (K+1, A, 64)
         b2 = torch.stack([F.pad(self.value_head[2].bias, (0, A - 1))]
                          + [hd[2].bias for hd in self.adv_heads]).unsqueeze(1)   # (K+1, 1, A)
-        out = torch.baddbmm(b2, z, w2.transpose(1, 2))                # (K+1, B, A)
-        v = out[0, :, :1]                                             # (B, 1)
-        adv = out[1:].transpose(0, 1)                                 # (B, K, A)
-        return v.unsqueeze(2) + adv - adv.mean(2, keepdim=True)
+        return torch.baddbmm(b2, z, w2.transpose(1, 2))               # (K+1, B, A)
 
 
 class BatchedBDQ:
@@ -195,14 +204,23 @@ class BatchedBDQ:
                        "pbn_q_to_flipmask_dev")
         return env.flipmask
 
+    def q_heads(self) -> torch.Tensor:
+        """The raw head outputs (K+1, n, A) of every env's observation (q_values before the
+        dueling combination, which pbn_heads_to_flipmask does)."""
+        return self._forward(heads=True)
+
     def q_values(self) -> torch.Tensor:
         """Q (n, K, N+1) of every env's (state, target) observation.  With the reference's
         MyBilinear first layer this skips the fp32 observation: pbn_bilinear_targets computes
         the bilinear layer from the packed state and a per-target table (one small GEMM), and
         the rest of the network runs in PyTorch.  Equal to ``q(observe())`` up to fp32
         summation order."""
+        return self._forward(heads=False)
+
+    def _forward(self, heads: bool) -> torch.Tensor:
         if not self.fast:
-            return self.q(self.observe())
+            y = self.q.model[0](self.observe())
+            return self.q.forward_heads(y) if heads else self.q.forward_tail(y)
         env = self.env
         bil = self.q.model[0]
         T = bil.target_table(self.targets).contiguous() if self.targets.shape[0] else None
@@ -215,13 +233,35 @@ class BatchedBDQ:
                                               self._slope, self._y.data_ptr(), env._stream()),
                        "pbn_bilinear_targets")
         # the kernel applied model[1] (LeakyReLU) when _act
+        if heads:
+            return self.q.forward_heads(self._y, skip_act=self._act)
         return self.q.forward_tail(self._y, skip_act=self._act)
+
+    def act_heads(self, heads: torch.Tensor, epsilon: Optional[float] = None,
+                  step_t: Optional[torch.Tensor] = None, epsilon_t: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``act`` on raw head outputs (K+1, n, N+1): pbn_heads_to_flipmask does the dueling
+        combination, epsilon-greedy and flip masks in one launch.  ``step_t`` / ``epsilon_t``:
+        optional one-element device tensors (int64 / float32) read when the kernel runs."""
+        env = self.env
+        heads = heads.contiguous()
+        if heads.shape != (self.branches + 1, env.n_alloc, env.n_nodes + 1):
+            raise ValueError(f"heads must have shape {(self.branches + 1, env.n_alloc, env.n_nodes + 1)}")
+        eps = self.epsilon if epsilon is None else float(epsilon)
+        L = _lib.load()
+        with torch.cuda.device(env.device):
+            _lib.check(L.pbn_heads_to_flipmask(env.net.handle, env.seed, env.step_index,
+                                               step_t.data_ptr() if step_t is not None else None,
+                                               env.env_offset, env.n_alloc, self.branches, env.n_nodes + 1,
+                                               heads.data_ptr(), eps,
+                                               epsilon_t.data_ptr() if epsilon_t is not None else None,
+                                               env.flipmask.data_ptr(), self.actions.data_ptr(), env._stream()),
+                       "pbn_heads_to_flipmask")
+        return env.flipmask
 
     @torch.no_grad()
     def step(self, epsilon: Optional[float] = None):
         """One frame for every env; returns (state', reward, flags) views as VectorPBNEnv.step_flipmask."""
-        q = self.q_values()
-        self.act(q, epsilon)
+        self.act_heads(self.q_heads(), epsilon)
         return self.env.step_flipmask(use_current=True)
 
 

@@ -153,8 +153,12 @@ __device__ __forceinline__ int argmax_row(const float* __restrict__ r, int A) {
 // One wave per 64 envs: the block's Q rows (contiguous, 64 * K * A floats) are staged through
 // LDS with coalesced float4 loads, then lane e reduces its K rows.  Row stride K * A words:
 // odd for the kaban networks' K = 3, so the per-lane row reads spread over the banks.
-__global__ void __launch_bounds__(kQEnvs) q_to_flipmask_kernel(const float* __restrict__ q, int K, int A, int N,
-                                                               int W, int64_t n, uint64_t seed, uint64_t step,
+// heads = 1: q holds the raw head outputs (K+1, n, A) of BranchingQNetwork (head 0 = value,
+// output 0) instead of Q; the dueling combination is done here, per env and branch, as
+//   q_a = (v + adv_a) - mean,  mean = (adv_0 + adv_1 + ... + adv_{A-1}) / A   (left to right),
+// the order of bdq_model/network.py:59-61 with the mean summed sequentially.
+__global__ void __launch_bounds__(kQEnvs) q_to_flipmask_kernel(const float* __restrict__ q, int heads, int K, int A,
+                                                               int N, int W, int64_t n, uint64_t seed, uint64_t step,
                                                                const uint64_t* __restrict__ d_step,
                                                                uint64_t env_offset, uint64_t eps_u,
                                                                const float* __restrict__ d_eps,
@@ -164,9 +168,18 @@ __global__ void __launch_bounds__(kQEnvs) q_to_flipmask_kernel(const float* __re
   const int64_t e0 = (int64_t)blockIdx.x * kQEnvs;
   const int row = K * A;
   const int n_blk = (int)((n - e0) < kQEnvs ? (n - e0) : kQEnvs);   // 32 or 64
-  const float4* src = reinterpret_cast<const float4*>(q + (size_t)e0 * row);
-  const int words4 = n_blk * row / 4;
-  for (int k = threadIdx.x; k < words4; k += kQEnvs) reinterpret_cast<float4*>(sq)[k] = src[k];
+  if (!heads) {
+    const float4* src = reinterpret_cast<const float4*>(q + (size_t)e0 * row);
+    const int words4 = n_blk * row / 4;
+    for (int k = threadIdx.x; k < words4; k += kQEnvs) reinterpret_cast<float4*>(sq)[k] = src[k];
+  } else {   // K + 1 chunks of n_blk rows, one per head
+    const int chunk4 = n_blk * A / 4;
+    for (int h = 0; h <= K; ++h) {
+      const float4* src = reinterpret_cast<const float4*>(q + ((size_t)h * n + e0) * A);
+      float4* dst = reinterpret_cast<float4*>(sq + (size_t)h * n_blk * A);
+      for (int k = threadIdx.x; k < chunk4; k += kQEnvs) dst[k] = src[k];
+    }
+  }
   __syncthreads();
   if ((int)threadIdx.x >= n_blk) return;
   const int64_t e = e0 + threadIdx.x;
@@ -180,12 +193,27 @@ __global__ void __launch_bounds__(kQEnvs) q_to_flipmask_kernel(const float* __re
   const uint32_t rw[3] = {r.y, r.z, r.w};
   uint32_t m[4] = {0u, 0u, 0u, 0u};
   const float* my = sq + (size_t)threadIdx.x * row;
+  const float v = heads ? sq[(size_t)threadIdx.x * A] : 0.f;
   for (int k = 0; k < K; ++k) {
     int a;
     if (explore) {
       a = (int)((((rw[k / 3] >> (10 * (k % 3))) & 1023u) * (uint32_t)(N + 1)) >> 10);
-    } else {
+    } else if (!heads) {
       a = argmax_row(my + k * A, A);
+    } else {
+      const float* adv = sq + ((size_t)(k + 1) * n_blk + threadIdx.x) * A;
+      float sum = 0.f;
+      for (int j = 0; j < A; ++j) sum += adv[j];
+      const float mean = sum / (float)A;
+      float best = (v + adv[0]) - mean;
+      int bi = 0;
+      for (int j = 1; j < A; ++j) {   // torch.argmax: first maximum, NaN is the maximum
+        const float qj = (v + adv[j]) - mean;
+        const bool take = !isnan(best) && (isnan(qj) || qj > best);
+        best = take ? qj : best;
+        bi = take ? j : bi;
+      }
+      a = bi;
     }
     if (actions) actions[e * K + k] = a;
     if (a > 0 && a <= N) {   // a > 0 flips node a-1, once however often it repeats
@@ -260,7 +288,7 @@ int pbn_bilinear_targets(const pbn_net* net, int64_t n_envs, const uint32_t* d_s
 static int q_to_flipmask_impl(const pbn_net* net, uint64_t seed, uint64_t step, const uint64_t* d_step,
                               uint64_t env_offset, int64_t n_envs, int32_t n_branches, int32_t n_actions,
                               const float* d_q, float epsilon, const float* d_epsilon, uint32_t* d_flipmask,
-                              int32_t* d_actions, void* stream) {
+                              int32_t* d_actions, void* stream, int heads = 0) {
   pbn::NetView v;
   int rc = pbn::net_view(net, &v);
   if (rc) return rc;
@@ -275,10 +303,20 @@ static int q_to_flipmask_impl(const pbn_net* net, uint64_t seed, uint64_t step, 
   if (!aligned16(d_q)) return pbn::set_error(PBN_EINVAL, "d_q must be 16-byte aligned");
   // explore iff word 0 < floor(epsilon * 2^32): epsilon = 1 always explores, 0 never
   const uint64_t eps_u = (uint64_t)floor((double)epsilon * 4294967296.0);
-  const size_t lds = (size_t)kQEnvs * n_branches * n_actions * sizeof(float);
-  if (lds > 64 * 1024) return pbn::set_error(PBN_EINVAL, "n_branches * n_actions too large");
+  const size_t lds = (size_t)kQEnvs * (n_branches + heads) * n_actions * sizeof(float);
+  if (lds > 160 * 1024) return pbn::set_error(PBN_EINVAL, "n_branches * n_actions too large");
+  if (lds > 64 * 1024) {   // beyond the default dynamic-LDS limit (e.g. heads of a 70-node network)
+    static bool raised[64] = {};   // per device (a pbn_net is bound to one)
+    const int dv = v.device >= 0 && v.device < 64 ? v.device : 0;
+    if (!raised[dv]) {
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(q_to_flipmask_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+        return pbn::set_error(PBN_EDEVICE, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+      raised[dv] = true;
+    }
+  }
   const unsigned blocks = (unsigned)((n_envs + kQEnvs - 1) / kQEnvs);
-  hipLaunchKernelGGL(q_to_flipmask_kernel, dim3(blocks), dim3(kQEnvs), lds, (hipStream_t)stream, d_q, n_branches,
+  hipLaunchKernelGGL(q_to_flipmask_kernel, dim3(blocks), dim3(kQEnvs), lds, (hipStream_t)stream, d_q, heads, n_branches,
                      n_actions, v.n_nodes, v.W, n_envs, seed, step, d_step, env_offset, eps_u, d_epsilon, d_flipmask, d_actions);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return pbn::set_error(PBN_EDEVICE, hipGetErrorString(e));
@@ -300,6 +338,16 @@ int pbn_q_to_flipmask_dev(const pbn_net* net, uint64_t seed, const uint64_t* d_s
   if (d_epsilon && ((uintptr_t)d_epsilon & 3u) != 0) return pbn::set_error(PBN_EINVAL, "d_epsilon misaligned");
   return q_to_flipmask_impl(net, seed, 0, d_step, env_offset, n_envs, n_branches, n_actions, d_q, epsilon,
                             d_epsilon, d_flipmask, d_actions, stream);
+}
+
+int pbn_heads_to_flipmask(const pbn_net* net, uint64_t seed, uint64_t step, const uint64_t* d_step,
+                          uint64_t env_offset, int64_t n_envs, int32_t n_branches, int32_t n_actions,
+                          const float* d_heads, float epsilon, const float* d_epsilon, uint32_t* d_flipmask,
+                          int32_t* d_actions, void* stream) {
+  if (d_step && ((uintptr_t)d_step & 7u) != 0) return pbn::set_error(PBN_EINVAL, "d_step must be 8-byte aligned");
+  if (d_epsilon && ((uintptr_t)d_epsilon & 3u) != 0) return pbn::set_error(PBN_EINVAL, "d_epsilon misaligned");
+  return q_to_flipmask_impl(net, seed, step, d_step, env_offset, n_envs, n_branches, n_actions, d_heads, epsilon,
+                            d_epsilon, d_flipmask, d_actions, stream, 1);
 }
 
 }  // extern "C"

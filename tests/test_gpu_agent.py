@@ -169,3 +169,52 @@ def test_bilinear_targets_without_attractors_is_bias():
         act_bias = agent.q.model[1](agent.q.model[0].bilinear.bias)
     torch.cuda.synchronize()
     assert torch.equal(agent._y, act_bias.expand_as(agent._y)) and torch.allclose(y_ref, agent._y, atol=1e-6)
+
+
+@pytest.mark.parametrize("name,K,eps", [("pbn28", 3, 0.0), ("pbn28", 3, 0.3), ("pbn70", 3, 0.25),
+                                        ("pbn7", 1, 0.5), ("pbn7", 5, 0.0), ("pbn28", 3, 1.0)])
+def test_heads_to_flipmask_exact(name, K, eps):
+    """pbn_heads_to_flipmask (dueling combination in the kernel) against the oracle's
+    restatement of its arithmetic, bit for bit; and its Q against torch's dueling to fp32."""
+    spec = make_spec(name)
+    n, A, seed, step = 2080 if name == "pbn70" else 4096, spec.n + 1, 9, 17
+    env = VectorPBNEnv(spec, n, seed=seed)
+    env.step_index = step
+    agent = BatchedBDQ(env, BranchingQNetwork((spec.n, spec.n), A, K), branches=K)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    heads = torch.randn(K + 1, env.n_alloc, A, device="cuda", generator=g)
+    heads[1:, :64, 5] = heads[1:, :64, 2]                    # ties: the first maximum wins
+    agent.act_heads(heads, eps)
+    torch.cuda.synchronize()
+    h = heads.cpu().numpy()
+    q = agent_oracle.heads_q(h)
+    flip, acts = agent_oracle.q_to_flipmask(spec, q, seed, step, 0, eps)
+    assert np.array_equal(u32(env.flipmask), flip)
+    assert np.array_equal(agent.actions.cpu().numpy(), acts)
+    q_torch = BranchingQNetwork.dueling(heads).cpu().numpy()
+    assert np.allclose(q, q_torch, rtol=1e-5, atol=1e-5)
+    # device step / epsilon forms
+    fm = env.flipmask.clone()
+    step_t = torch.full((1,), step, dtype=torch.int64, device="cuda")
+    eps_t = torch.full((1,), eps, dtype=torch.float32, device="cuda")
+    env.flipmask.zero_()
+    agent.act_heads(heads, 0.77, step_t=step_t, epsilon_t=eps_t)
+    assert torch.equal(env.flipmask, fm)
+
+
+def test_bdq_step_uses_fused_heads():
+    """BatchedBDQ.step (bilinear kernel + heads kernel) picks the flip masks the module's Q
+    gives through pbn_q_to_flipmask, except where fp32 summation order splits a near-tie."""
+    spec = make_spec("pbn28")
+    torch.manual_seed(7)
+    env = VectorPBNEnv(spec, 8192, seed=4)
+    agent = BatchedBDQ(env, BranchingQNetwork((28, 28), 29, 3))
+    env.reset()
+    with torch.no_grad():
+        q = agent.q(agent.observe())
+        agent.act(q, 0.0)
+        ref = env.flipmask.clone()
+        agent.act_heads(agent.q_heads(), 0.0)
+    torch.cuda.synchronize()
+    same = (env.flipmask == ref).float().mean().item()
+    assert same > 0.999, same
