@@ -111,23 +111,30 @@ class BranchingQNetwork(nn.Module):
         adv = out[1:].transpose(0, 1)                                 # (B, K, A)
         return v.unsqueeze(2) + adv - adv.mean(2, keepdim=True)
 
-    def forward_heads(self, y: torch.Tensor, skip_act: bool = False) -> torch.Tensor:
-        """y (B, 256) -> the raw outputs (K+1, B, A) of the value head (output 0) and the
-        advantage heads, before the dueling combination."""
-        h = self.model[2:](y) if skip_act else self.model[1:](y)      # (B, 32)
-        # the value head and the K advantage heads read the same h: their first layers run as
-        # one (32 -> 64(K+1)) GEMM, their second layers as one batched GEMM over K+1 heads
+    def head_weights(self):
+        """(w1, b1, w2, b2): the value head and the K advantage heads as one (32 -> 64(K+1))
+        layer and one batched (K+1) x (64 -> A) layer; the value head is zero-padded to A
+        outputs (only output 0 is used)."""
         heads = [self.value_head] + list(self.adv_heads)
+        A = self.ac_dim
         w1 = torch.cat([hd[0].weight for hd in heads], 0)             # (64(K+1), 32)
         b1 = torch.cat([hd[0].bias for hd in heads], 0)
-        z = F.leaky_relu(torch.addmm(b1, h, w1.t()))                  # (B, 64(K+1))
-        z = z.view(z.shape[0], len(heads), -1).transpose(0, 1)        # (K+1, B, 64)
-        A = self.ac_dim
-        # value head zero-padded to A outputs (only output 0 is used); one stack per operand
         w2 = torch.stack([F.pad(self.value_head[2].weight, (0, 0, 0, A - 1))]
                          + [hd[2].weight for hd in self.adv_heads])   # (K+1, A, 64)
         b2 = torch.stack([F.pad(self.value_head[2].bias, (0, A - 1))]
                          + [hd[2].bias for hd in self.adv_heads]).unsqueeze(1)   # (K+1, 1, A)
+        return w1, b1, w2, b2
+
+    def forward_heads(self, y: torch.Tensor, skip_act: bool = False, weights=None) -> torch.Tensor:
+        """y (B, 256) -> the raw outputs (K+1, B, A) of the value head (output 0) and the
+        advantage heads, before the dueling combination.  ``weights``: head_weights() computed
+        beforehand (prepacked for a frozen network)."""
+        h = self.model[2:](y) if skip_act else self.model[1:](y)      # (B, 32)
+        # the value head and the K advantage heads read the same h: their first layers run as
+        # one (32 -> 64(K+1)) GEMM, their second layers as one batched GEMM over K+1 heads
+        w1, b1, w2, b2 = weights if weights is not None else self.head_weights()
+        z = F.leaky_relu(torch.addmm(b1, h, w1.t()))                  # (B, 64(K+1))
+        z = z.view(z.shape[0], w2.shape[0], -1).transpose(0, 1)       # (K+1, B, 64)
         return torch.baddbmm(b2, z, w2.transpose(1, 2))               # (K+1, B, A)
 
 
@@ -154,6 +161,7 @@ class BatchedBDQ:
         act = self.q.model[1] if len(self.q.model) > 1 else None
         self._act = isinstance(act, nn.LeakyReLU)
         self._slope = float(act.negative_slope) if self._act else 0.0
+        self._pack, self._pack_key = None, None
         self._y = torch.empty(n, self.q.model[0].output_dim if self.fast else 1, dtype=torch.float32,
                               device=env.device)
 
@@ -217,14 +225,32 @@ class BatchedBDQ:
         summation order."""
         return self._forward(heads=False)
 
+    def _packed(self):
+        """Weight-derived operands of the fast forward: the target table of the bilinear layer,
+        its bias and the head weights.  For a network in eval mode they are computed once per
+        version of its parameters (prepacked, as inference packs weights at load time) and
+        reused, so a frame runs no assembly kernels; a captured frame keeps the pack of its
+        capture (re-capture after changing the weights).  In train mode (the learner) they are
+        recomputed every call."""
+        key = None
+        if not self.q.training:
+            key = tuple((p.data_ptr(), p._version) for p in self.q.parameters())
+            if key == self._pack_key:
+                return self._pack
+        bil = self.q.model[0]
+        T = bil.target_table(self.targets).contiguous() if self.targets.shape[0] else None
+        pack = (T, bil.bilinear.bias.contiguous(), self.q.head_weights())
+        if key is not None:
+            self._pack, self._pack_key = pack, key
+        return pack
+
     def _forward(self, heads: bool) -> torch.Tensor:
         if not self.fast:
             y = self.q.model[0](self.observe())
             return self.q.forward_heads(y) if heads else self.q.forward_tail(y)
         env = self.env
         bil = self.q.model[0]
-        T = bil.target_table(self.targets).contiguous() if self.targets.shape[0] else None
-        bias = bil.bilinear.bias.contiguous()
+        T, bias, hw = self._packed()
         L = _lib.load()
         with torch.cuda.device(env.device):
             _lib.check(L.pbn_bilinear_targets(env.net.handle, env.n_alloc, env.state.data_ptr(),
@@ -233,9 +259,8 @@ class BatchedBDQ:
                                               self._slope, self._y.data_ptr(), env._stream()),
                        "pbn_bilinear_targets")
         # the kernel applied model[1] (LeakyReLU) when _act
-        if heads:
-            return self.q.forward_heads(self._y, skip_act=self._act)
-        return self.q.forward_tail(self._y, skip_act=self._act)
+        out = self.q.forward_heads(self._y, skip_act=self._act, weights=hw)
+        return out if heads else self.q.dueling(out)
 
     def act_heads(self, heads: torch.Tensor, epsilon: Optional[float] = None,
                   step_t: Optional[torch.Tensor] = None, epsilon_t: Optional[torch.Tensor] = None) -> torch.Tensor:

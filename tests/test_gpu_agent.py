@@ -218,3 +218,22 @@ def test_bdq_step_uses_fused_heads():
     torch.cuda.synchronize()
     same = (env.flipmask == ref).float().mean().item()
     assert same > 0.999, same
+
+
+def test_prepacked_weights_follow_in_place_updates():
+    """The eval-mode pack (target table, head weights) is rebuilt when a parameter changes."""
+    spec = make_spec("pbn28")
+    torch.manual_seed(8)
+    env = VectorPBNEnv(spec, 1024, seed=6)
+    agent = BatchedBDQ(env, BranchingQNetwork((28, 28), 29, 3))
+    env.reset()
+    with torch.no_grad():
+        agent.q_values()
+        key = agent._pack_key
+        agent.q.model[0].bilinear.weight.mul_(1.5)
+        agent.q.adv_heads[1][2].bias.add_(0.25)
+        q_fast = agent.q_values()
+        q_ref = agent.q(agent.observe())
+    torch.cuda.synchronize()
+    assert agent._pack_key != key
+    assert torch.allclose(q_fast, q_ref, rtol=1e-4, atol=1e-5)
