@@ -16,6 +16,13 @@
  *   env.close()  train_BDQ.py:116                              -> pbn_net_destroy
  *   T frames of the frame loop bdq_model/__init__.py:172-213     -> pbn_rollout
  *   compute_ssd_hist(env, model, resets, iters) train_pbn_28.py:257 -> pbn_rollout + pbn_state_histogram
+ *   BranchingDQN.predict + list(action.unique())
+ *        bdq_model/__init__.py:69-98,176                       -> pbn_bilinear_targets (first layer),
+ *                                                                 pbn_heads_to_flipmask / pbn_q_to_flipmask
+ *   update_policy's np.stack of sampled Transitions
+ *        bdq_model/__init__.py:100-109                         -> pbn_obs_unpack
+ *   a frame loop captured once and replayed (no reference counterpart)
+ *                                                              -> pbn_step_dev, pbn_q_to_flipmask_dev
  *
  * The Python facade (pbn_rl_amd.env.PBNEnv / pbn_rl_amd.vector_env.VectorPBNEnv)
  * keeps that gym surface and calls these entry points through ctypes;
