@@ -157,51 +157,50 @@ __device__ __forceinline__ int argmax_row(const float* __restrict__ r, int A) {
 // output 0) instead of Q; the dueling combination is done here, per env and branch, as
 //   q_a = (v + adv_a) - mean,  mean = (adv_0 + adv_1 + ... + adv_{A-1}) / A   (left to right),
 // the order of bdq_model/network.py:59-61 with the mean summed sequentially.
-__global__ void __launch_bounds__(kQEnvs) q_to_flipmask_kernel(const float* __restrict__ q, int heads, int K, int A,
-                                                               int N, int W, int64_t n, uint64_t seed, uint64_t step,
-                                                               const uint64_t* __restrict__ d_step,
-                                                               uint64_t env_offset, uint64_t eps_u,
-                                                               const float* __restrict__ d_eps,
-                                                               uint32_t* __restrict__ flipmask,
-                                                               int32_t* __restrict__ actions) {
+__global__ void __launch_bounds__(kQEnvs * kMaxBranches) q_to_flipmask_kernel(
+    const float* __restrict__ q, int heads, int K, int A, int N, int W, int64_t n, uint64_t seed, uint64_t step,
+    const uint64_t* __restrict__ d_step, uint64_t env_offset, uint64_t eps_u, const float* __restrict__ d_eps,
+    uint32_t* __restrict__ flipmask, int32_t* __restrict__ actions) {
+  // one wave per branch (K waves), lane = env of the block; the chosen actions meet in LDS
   extern __shared__ float sq[];
   const int64_t e0 = (int64_t)blockIdx.x * kQEnvs;
   const int row = K * A;
   const int n_blk = (int)((n - e0) < kQEnvs ? (n - e0) : kQEnvs);   // 32 or 64
+  const int nthr = (int)blockDim.x;
   if (!heads) {
     const float4* src = reinterpret_cast<const float4*>(q + (size_t)e0 * row);
     const int words4 = n_blk * row / 4;
-    for (int k = threadIdx.x; k < words4; k += kQEnvs) reinterpret_cast<float4*>(sq)[k] = src[k];
+    for (int k = threadIdx.x; k < words4; k += nthr) reinterpret_cast<float4*>(sq)[k] = src[k];
   } else {   // K + 1 chunks of n_blk rows, one per head
     const int chunk4 = n_blk * A / 4;
     for (int h = 0; h <= K; ++h) {
       const float4* src = reinterpret_cast<const float4*>(q + ((size_t)h * n + e0) * A);
       float4* dst = reinterpret_cast<float4*>(sq + (size_t)h * n_blk * A);
-      for (int k = threadIdx.x; k < chunk4; k += kQEnvs) dst[k] = src[k];
+      for (int k = threadIdx.x; k < chunk4; k += nthr) dst[k] = src[k];
     }
   }
+  int* act_lds = reinterpret_cast<int*>(sq + (size_t)(heads ? K + 1 : K) * kQEnvs * A);   // [K][64]
   __syncthreads();
-  if ((int)threadIdx.x >= n_blk) return;
-  const int64_t e = e0 + threadIdx.x;
-  const uint64_t ge = env_offset + (uint64_t)e;
-  const pbn::Word4 r = pbn::draw(seed, ge, d_step ? *d_step : step, pbn::kStreamExplore, 0);
-  if (d_eps) {   // device epsilon (graph replays): clamped to [0, 1], NaN -> 0
-    const float ef = fminf(fmaxf(*d_eps, 0.f), 1.f);
-    eps_u = (uint64_t)floor((double)ef * 4294967296.0);
-  }
-  const bool explore = (uint64_t)r.x < eps_u;
-  const uint32_t rw[3] = {r.y, r.z, r.w};
-  uint32_t m[4] = {0u, 0u, 0u, 0u};
-  const float* my = sq + (size_t)threadIdx.x * row;
-  const float v = heads ? sq[(size_t)threadIdx.x * A] : 0.f;
-  for (int k = 0; k < K; ++k) {
+  const int k = (int)threadIdx.x >> 6;            // this wave's branch
+  const int t = (int)threadIdx.x & 63;            // env of the block
+  if (t < n_blk) {
+    const int64_t e = e0 + t;
+    const uint64_t ge = env_offset + (uint64_t)e;
+    const pbn::Word4 r = pbn::draw(seed, ge, d_step ? *d_step : step, pbn::kStreamExplore, 0);
+    if (d_eps) {   // device epsilon (graph replays): clamped to [0, 1], NaN -> 0
+      const float ef = fminf(fmaxf(*d_eps, 0.f), 1.f);
+      eps_u = (uint64_t)floor((double)ef * 4294967296.0);
+    }
+    const bool explore = (uint64_t)r.x < eps_u;
+    const uint32_t rw = k < 3 ? r.y : (k < 6 ? r.z : r.w);
     int a;
     if (explore) {
-      a = (int)((((rw[k / 3] >> (10 * (k % 3))) & 1023u) * (uint32_t)(N + 1)) >> 10);
+      a = (int)((((rw >> (10 * (k % 3))) & 1023u) * (uint32_t)(N + 1)) >> 10);
     } else if (!heads) {
-      a = argmax_row(my + k * A, A);
+      a = argmax_row(sq + (size_t)t * row + k * A, A);
     } else {
-      const float* adv = sq + ((size_t)(k + 1) * n_blk + threadIdx.x) * A;
+      const float v = sq[(size_t)t * A];
+      const float* adv = sq + ((size_t)(k + 1) * n_blk + t) * A;
       float sum = 0.f;
       for (int j = 0; j < A; ++j) sum += adv[j];
       const float mean = sum / (float)A;
@@ -216,16 +215,25 @@ __global__ void __launch_bounds__(kQEnvs) q_to_flipmask_kernel(const float* __re
       a = bi;
     }
     if (actions) actions[e * K + k] = a;
-    if (a > 0 && a <= N) {   // a > 0 flips node a-1, once however often it repeats
-      const int node = a - 1;
-#pragma unroll
-      for (int w = 0; w < 4; ++w)
-        if (w == (node >> 5)) m[w] |= 1u << (node & 31);
-    }
+    act_lds[k * kQEnvs + t] = a;
   }
+  __syncthreads();
+  if (k == 0 && t < n_blk) {
+    uint32_t m[4] = {0u, 0u, 0u, 0u};
+    for (int kk = 0; kk < K; ++kk) {
+      const int a = act_lds[kk * kQEnvs + t];
+      if (a > 0 && a <= N) {   // a > 0 flips node a-1, once however often it repeats
+        const int node = a - 1;
 #pragma unroll
-  for (int w = 0; w < 4; ++w)
-    if (w < W) flipmask[(size_t)w * n + e] = m[w];
+        for (int w = 0; w < 4; ++w)
+          if (w == (node >> 5)) m[w] |= 1u << (node & 31);
+      }
+    }
+    const int64_t e = e0 + t;
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+      if (w < W) flipmask[(size_t)w * n + e] = m[w];
+  }
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
@@ -303,7 +311,8 @@ static int q_to_flipmask_impl(const pbn_net* net, uint64_t seed, uint64_t step, 
   if (!aligned16(d_q)) return pbn::set_error(PBN_EINVAL, "d_q must be 16-byte aligned");
   // explore iff word 0 < floor(epsilon * 2^32): epsilon = 1 always explores, 0 never
   const uint64_t eps_u = (uint64_t)floor((double)epsilon * 4294967296.0);
-  const size_t lds = (size_t)kQEnvs * (n_branches + heads) * n_actions * sizeof(float);
+  const size_t lds = (size_t)kQEnvs * (n_branches + heads) * n_actions * sizeof(float) +
+                    (size_t)kQEnvs * n_branches * sizeof(int);
   if (lds > 160 * 1024) return pbn::set_error(PBN_EINVAL, "n_branches * n_actions too large");
   if (lds > 64 * 1024) {   // beyond the default dynamic-LDS limit (e.g. heads of a 70-node network)
     static bool raised[64] = {};   // per device (a pbn_net is bound to one)
@@ -316,7 +325,7 @@ static int q_to_flipmask_impl(const pbn_net* net, uint64_t seed, uint64_t step, 
     }
   }
   const unsigned blocks = (unsigned)((n_envs + kQEnvs - 1) / kQEnvs);
-  hipLaunchKernelGGL(q_to_flipmask_kernel, dim3(blocks), dim3(kQEnvs), lds, (hipStream_t)stream, d_q, heads, n_branches,
+  hipLaunchKernelGGL(q_to_flipmask_kernel, dim3(blocks), dim3(kQEnvs * n_branches), lds, (hipStream_t)stream, d_q, heads, n_branches,
                      n_actions, v.n_nodes, v.W, n_envs, seed, step, d_step, env_offset, eps_u, d_epsilon, d_flipmask, d_actions);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return pbn::set_error(PBN_EDEVICE, hipGetErrorString(e));
