@@ -187,6 +187,19 @@ __device__ __forceinline__ uint32_t less_than(const uint32_t (&dig)[16], uint32_
   return lt;
 }
 
+// less_than with the threshold's digit masks read from LDS: cmq[d * stride] = ~0 if bit
+// (B-1-d) of the threshold is set, else 0 (built once per block; saves a v_bfe per digit)
+template <int B>
+__device__ __forceinline__ uint32_t less_than_cm(const uint32_t (&dig)[16], const uint32_t* __restrict__ cmq,
+                                                 int stride) {
+  uint32_t lt = 0;
+#pragma unroll
+  for (int d = 15; d >= 0; --d) {
+    if (d < B) lt = __builtin_amdgcn_bitop3_b32(dig[d], lt, cmq[d * stride], 0x8E);
+  }
+  return lt;
+}
+
 // ------------------------------------------- step kernel, one wave per 32-env group
 //
 // Lane j of the wave is env j (lanes 0-31) for the per-env work and node j (+32r) for
@@ -811,6 +824,19 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
       u_hp = a.hash_probes, u_hz = a.horizon;
   uint32_t u_fl = __builtin_amdgcn_readfirstlane((a.obs ? 1u : 0u) | (a.final_state ? 2u : 0u) |
                                                  (random_actions ? 4u : 0u) | ((a.mode & PBN_MODE_AUTORESET) ? 8u : 0u));
+  // digit masks of the first kNodeRecs - 1 thresholds of every node, [q][d][32W], for the
+  // selection wave's compares (from the global node records: the LDS copy is in flight)
+  // (single-word states only: for W > 1 the extra LDS costs more occupancy than it saves,
+  // measured -15 % on pbn70 x 1M)
+  uint32_t* cm = slots + 2 * (size_t)a.slot_words;
+  if constexpr (W == 1) {
+    for (int idx = threadIdx.x; idx < (kNodeRecs - 1) * B * 32; idx += blockDim.x) {
+      const int i = idx % 32, d = (idx / 32) % B, q = idx / (32 * B);
+      uint32_t c = 0;
+      if (i < N && q < (int)a.nrec[i * kNodeRecs].w - 1) c = a.nrec[i * kNodeRecs + q].z;
+      cm[idx] = ((c >> (B - 1 - d)) & 1u) ? ~0u : 0u;
+    }
+  }
   __syncthreads();
   // drain the initial state loads here: otherwise the loop-carried st / t / target copies at
   // the bottom of the loop wait on vmcnt(0), which also waits for every store of the step
@@ -932,7 +958,12 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
           {   // per-lane thresholds: the selection wave has slack, the SGPRs are scarce
 #pragma unroll
             for (int q = 0; q < kNodeRecs - 1; ++q)
-              if (q < nf - 1) lt_out[q * 64 * W + i] = less_than(dig, recL[ic * kNodeRecs + q].z, B);
+              if (q < nf - 1) {
+                if constexpr (W == 1)
+                  lt_out[q * 64 * W + i] = less_than_cm<B>(dig, cm + (size_t)q * B * 32 + i, 32);
+                else
+                  lt_out[q * 64 * W + i] = less_than(dig, recL[ic * kNodeRecs + q].z, B);
+              }
             const int f0 = (int)recL[ic * kNodeRecs + 1].w;
             for (int j = kNodeRecs - 1; j < nf - 1; ++j)   // nodes with more than kNodeRecs functions
               lt_out[j * 64 * W + i] = less_than(dig, a.fcompact[CK(f0 + j, a.n_funcs, 9)].z, B);
@@ -2025,7 +2056,9 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   }
   net->lds_wave = ((size_t)net->tab_words + (size_t)kWavesPerBlock * net->wave_words) * 4;
   net->slot_words = (3 * W + 1) * 64 + net->lq * 64 * W;
-  net->lds_pipe = ((size_t)net->tab_words + 64 * (size_t)W + 2 * (size_t)net->slot_words) * 4;
+  // + the selection wave's threshold digit masks [kNodeRecs - 1][B][32] (W == 1)
+  net->lds_pipe = ((size_t)net->tab_words + 64 * (size_t)W + 2 * (size_t)net->slot_words +
+                   (W == 1 ? (size_t)(kNodeRecs - 1) * d->prob_bits * 32 : 0)) * 4;
   {
     bool single = true;
     for (int at = 0; at < A; ++at) single = single && (d->attractor_start[at + 1] - d->attractor_start[at] == 1);
