@@ -4,16 +4,17 @@ The reference steps one env per frame: ``BranchingDQN.predict`` stacks (state, t
 host into a float (2, 1, N) tensor, runs ``BranchingQNetwork``, takes argmax over each of the
 3 action branches (bdq_model/__init__.py:69-98), and ``env.step(list(action.unique()))``
 flips node a-1 for every action a > 0 (:81-84,176-177).  Here one frame covers a whole
-``VectorPBNEnv`` batch, and nothing leaves HBM:
+``VectorPBNEnv`` batch, and nothing leaves HBM (BatchedBDQ.step):
 
-    pbn_obs_unpack      packed state words + target id -> fp32 (2, n, N)       (HIP)
-    BranchingQNetwork   (2, n, N) -> Q (n, 3, N+1)                             (PyTorch-ROCm)
-    pbn_q_to_flipmask   epsilon-greedy over Q -> flip-mask words (W, n)         (HIP)
-    pbn_step            the PBN transition                                      (HIP)
+    pbn_bilinear_targets   packed state + target id -> the bilinear layer (+ LeakyReLU)   (HIP)
+    BranchingQNetwork      the rest of the network -> raw head outputs (4, n, N+1)         (PyTorch-ROCm)
+    pbn_heads_to_flipmask  dueling combination + epsilon-greedy -> flip-mask words (W, n)  (HIP)
+    pbn_step               the PBN transition                                             (HIP)
 
 ``BranchingQNetwork`` keeps the reference module tree (bdq_model/network.py:24-63), so the
-reference's checkpoints load into it with ``load_state_dict``; its forward computes the
-bilinear layer as one GEMM over the outer product of the two inputs.
+reference's checkpoints load into it with ``load_state_dict``; its own forward (used for
+training) computes the bilinear layer as GEMMs (MyBilinear), and ``pbn_obs_unpack`` +
+``pbn_q_to_flipmask`` give the unfused path on an explicit observation and Q.
 """
 from __future__ import annotations
 
