@@ -80,6 +80,28 @@ def test_q_to_flipmask_rejects_bad_arguments():
     assert L.pbn_q_to_flipmask(h, 0, 0, 0, 40, 3, 29, q.data_ptr(), 0.0, fm.data_ptr(), None, None) == -22
     assert L.pbn_q_to_flipmask(h, 0, 0, 0, 64, 3, 29, q.data_ptr() + 4, 0.0, fm.data_ptr(), None, None) == -22
     assert L.pbn_obs_unpack(h, 64, None, None, None, None) == -22
+    # pbn_heads_to_flipmask: (K+1, n, A) heads, same checks plus device-pointer alignment
+    heads = torch.zeros(4, 64, 29, device="cuda")
+    st = torch.zeros(8, dtype=torch.int64, device="cuda")
+    assert L.pbn_heads_to_flipmask(h, 0, 0, None, 0, 64, 3, 28, heads.data_ptr(), 0.0, None, fm.data_ptr(), None,
+                                   None) == -22
+    assert L.pbn_heads_to_flipmask(h, 0, 0, st.data_ptr() + 4, 0, 64, 3, 29, heads.data_ptr(), 0.0, None,
+                                   fm.data_ptr(), None, None) == -22
+    assert L.pbn_heads_to_flipmask(h, 0, 0, None, 0, 64, 3, 29, heads.data_ptr(), 0.0, None, fm.data_ptr(), None,
+                                   None) == 0
+    # pbn_bilinear_targets: out_dim a multiple of 4 in 4..1024, aligned buffers, non-null
+    y = torch.zeros(64, 256, device="cuda")
+    b = torch.zeros(256, device="cuda")
+    T = torch.zeros(14, 28, 256, device="cuda")
+    args = (h, 64, env.state.data_ptr(), env.target.data_ptr(), T.data_ptr(), b.data_ptr())
+    assert L.pbn_bilinear_targets(*args, 254, 0, 0.0, y.data_ptr(), None) == -22
+    assert L.pbn_bilinear_targets(*args, 2048, 0, 0.0, y.data_ptr(), None) == -22
+    assert L.pbn_bilinear_targets(*args, 256, 0, 0.0, y.data_ptr() + 4, None) == -22
+    assert L.pbn_bilinear_targets(h, 64, None, env.target.data_ptr(), T.data_ptr(), b.data_ptr(), 256, 0, 0.0,
+                                  y.data_ptr(), None) == -22
+    assert L.pbn_bilinear_targets(h, 40, *args[2:], 256, 0, 0.0, y.data_ptr(), None) == -22
+    assert L.pbn_bilinear_targets(*args, 256, 1, 0.01, y.data_ptr(), None) == 0
+    torch.cuda.synchronize()
 
 
 @pytest.mark.parametrize("eps", [0.0, 0.2])
