@@ -160,7 +160,7 @@ def bottom_sccs(net: Network, candidates: np.ndarray, *, prob_bits: int = 16, ma
 
 
 def discover_attractors(net: Network, *, chains: int = 65536, burn_in: int = 1000, window: int = 64, seed: int = 0,
-                        prob_bits: int = 16, device=None, chunk: int = 250, max_box: int = 1 << 12,
+                        prob_bits: int = 16, device=None, chunk: int = 250, max_box: int = 1 << 14,
                         max_states: int = 1 << 20) -> Attractors:
     """Bottom SCCs of ``net``'s STG that ``chains`` GPU chains reach within ``burn_in`` steps."""
     import torch
