@@ -1,26 +1,35 @@
 """Benchmark: batched PBN env-steps/s (BASELINE.json metric) on 1..8 MI355X.
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]          # N > 1: spawns N ranks itself
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 A "step" is one synchronous PBN transition of every env of the batch:
 in-kernel random interventions (3 uniform actions per env, the explore policy
 of bdq_model/__init__.py:76), perturbation, per-node rule selection +
-truth-table update, attractor reward, autoreset.  By default steps run as
-``pbn_rollout`` launches of --chunk (100 = five horizons) steps, state kept on chip
+truth-table update, attractor reward, autoreset.  Steps run as ``pbn_rollout``
+launches of at most --chunk (100 = five horizons) steps, state kept on chip
 between steps, every step's observation, actions, reward and flags written to
 HBM (what a learner consumes); ``--mode step`` times one ``pbn_step`` launch per
 step instead.  The launches of the timed run are captured in one hipGraph.
 Default workload = BASELINE config 2: Bittner-28 (kaban/pbn28.ispl + the 14
-fixture attractors), 65,536 envs per GPU, horizon 20, p = 0.01.  Multi-GPU is
-weak scaling: every rank owns its own env range (env_offset = rank * envs), no
-data-path collective; the timed region is bracketed by barrier + synchronize
-and the max over ranks is reported.  Inputs are resident in HBM before timing.
+fixture attractors), 65,536 envs per GPU, horizon 20, p = 0.01.
+
+One process per GPU, RCCL ("nccl") process group over all ranks (world 1 too).
+Multi-GPU is weak scaling: every rank owns its own env range (env_offset =
+rank * envs).  ``value`` times the steps alone; ``value_with_gather`` times the
+same steps with one ``all_gather_into_tensor`` of the rollout's (s, a, s', r,
+flags) records (17 B per env-step for Bittner-28) after every rollout launch
+(SURVEY.md 8(e), config 4).  Each timed region is bracketed by barrier +
+synchronize, timed with HIP events on the launch stream, and the max over ranks
+is reported.  Inputs are resident in HBM before timing.  Before the timed region
+the captured run is replayed untimed for at least --clock-warm seconds so the
+GPU clocks have ramped (the W warmup steps alone are microseconds of GPU work).
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -67,9 +76,11 @@ def parse():
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a hipGraph")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--gather", action="store_true",
-                   help="also time rollouts followed by the per-rollout RCCL gather of (s, a, s', r, flags) "
-                        "records (SURVEY.md 8(e)); reported as value_with_gather, not the headline")
+    p.add_argument("--no-gather", action="store_true",
+                   help="skip the second timed pass (rollouts + one RCCL all_gather of their (s, a, s', r, "
+                        "flags) records per launch, SURVEY.md 8(e)) reported as value_with_gather")
+    p.add_argument("--clock-warm", type=float, default=0.3,
+                   help="seconds of untimed replays of the captured run before timing (GPU clock ramp)")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     a = p.parse_args()
     bdq = a.workload in ("bdq", "bdq-learn")
@@ -105,13 +116,32 @@ def rollout_bytes_per_env(words: int, steps: int) -> int:
     return 2 * (4 * words + 1 + 1) + steps * (4 * words + 4 * words + 4 + 1)
 
 
-def cpu_baseline(spec, envs: int, seconds: float):
-    """Time the C oracle (port of the step) on the host cores for ~`seconds`."""
+def usable_cpus() -> dict:
+    """Host CPUs this process may run on: the affinity mask, capped by a cgroup v2 CPU quota
+    (on the GPU box the job gets a share of a larger host)."""
+    total = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = total
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(math.ceil(quota))))
+    return {"cpu_count": total, "affinity": aff, "cgroup_quota": quota, "usable": usable}
+
+
+def cpu_baseline(spec, envs: int, seconds: float, threads: int):
+    """Time the C oracle (port of the step) on `threads` host threads for ~`seconds`."""
     import numpy as np
 
     from oracle import oracle
 
-    threads = max(1, min(16, os.cpu_count() or 1))
     n = min(envs, 65536)
     st, tg, t = oracle.reset(spec, 1, 0, 0, n)
     flip = np.zeros_like(st)
@@ -124,8 +154,9 @@ def cpu_baseline(spec, envs: int, seconds: float):
         if el >= seconds:
             break
     return {"value": n * done_steps / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/pbn_oracle.c (OpenMP, {threads} threads), {n} {spec.network.name} envs x "
-                      f"{done_steps} steps ({el:.1f} s), in-kernel-equivalent random actions, autoreset"}
+            "sample": f"oracle/pbn_oracle.c (OpenMP, {threads} threads = every CPU this job may use), {n} "
+                      f"{spec.network.name} envs x {done_steps} steps ({el:.1f} s), in-kernel-equivalent random "
+                      f"actions, autoreset"}
 
 
 def python_baseline(spec, seconds: float = 3.0):
@@ -141,7 +172,7 @@ def python_baseline(spec, seconds: float = 3.0):
         k += 1
     el = time.perf_counter() - t0
     return {"value": k / el, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/pyoracle.py single env, {k} steps"}
+            "sample": f"oracle/pyoracle.py single {spec.network.name} env, {k} steps"}
 
 
 def numpy_baseline(spec, envs: int, seconds: float = 5.0):
@@ -167,6 +198,35 @@ def numpy_baseline(spec, envs: int, seconds: float = 5.0):
                       f"({el:.1f} s)"}
 
 
+def config1_line(dev, seconds: float = 2.0) -> dict:
+    """BASELINE config 1: pbn7, ONE env, the gym facade stepped with random interventions
+    (3 uniform ints in [0, 7], duplicates once: bdq_model/__init__.py:76,176), reset on done.
+    Timed through the GPU facade (PBNEnv -> pbn_step, one launch + one packed copy back per
+    step) and through the per-env Python restatement on one host core."""
+    import numpy as np
+
+    from pbn_rl_amd.env import PBNEnv
+
+    env = PBNEnv(network="pbn7", seed=7, device=dev)
+    rng = np.random.default_rng(7)
+    env.reset()
+    for _ in range(20):
+        env.step(list(np.unique(rng.integers(0, 8, size=3))))
+    k, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        _, _, term, trunc, _ = env.step(list(np.unique(rng.integers(0, 8, size=3))))
+        if term or trunc:
+            env.reset()
+        k += 1
+    el = time.perf_counter() - t0
+    spec7 = env.spec
+    env.close()
+    return {"workload": "pbn7 single env through the gym facade, random interventions, reset on done",
+            "facade_gpu": {"value": k / el, "unit": "env-steps/s", "us_per_step": el / k * 1e6,
+                           "sample": f"PBNEnv(network='pbn7').step x {k}"},
+            "cpu_python": python_baseline(spec7, seconds)}
+
+
 def host_info() -> dict:
     model = None
     try:
@@ -177,10 +237,12 @@ def host_info() -> dict:
                     break
     except OSError:
         pass
-    return {"cpu_count": os.cpu_count(), "cpu_model": model}
+    info = usable_cpus()
+    info["cpu_model"] = model
+    return info
 
 
-def cpu_baseline_bdq(spec, qnet, seconds: float):
+def cpu_baseline_bdq(spec, qnet, seconds: float, threads: int):
     """The BDQ frame on the host cores for ~`seconds`: numpy observation, the same Q-network
     on CPU torch, greedy flip masks and the C oracle step, 4096 envs per frame."""
     import copy
@@ -189,7 +251,6 @@ def cpu_baseline_bdq(spec, qnet, seconds: float):
 
     from oracle import agent_oracle, oracle
 
-    threads = max(1, min(16, os.cpu_count() or 1))
     torch.set_num_threads(threads)
     q_cpu = copy.deepcopy(qnet).to("cpu").eval()
     n = 4096
@@ -216,7 +277,7 @@ def workload_text(args, chunk: int, rollout_mode: bool) -> str:
     if args.workload == "bdq":
         return (f"full BDQ rollout (config 5): {args.network} x {args.envs} envs per GPU, per step the "
                 f"BranchingQNetwork fp32 forward (random init, seed 0; bilinear layer by pbn_bilinear_targets from "
-                f"the packed state) -> epsilon-greedy (eps={args.epsilon}) pbn_q_to_flipmask -> pbn_step, "
+                f"the packed state) -> epsilon-greedy (eps={args.epsilon}) pbn_heads_to_flipmask -> pbn_step, "
                 f"autoreset, {common}")
     if args.workload == "bdq-learn":
         return (f"BDQ training frames: {args.network} x {args.envs} envs per GPU, per step the config-5 frame "
@@ -225,46 +286,8 @@ def workload_text(args, chunk: int, rollout_mode: bool) -> str:
                 f"{'one captured hipGraph per frame' if args.learn_graph else 'eager launches'}, {common}")
     return (f"{args.network} x {args.envs} envs per GPU, in-kernel random interventions (3 uniform actions/env/step), "
             f"autoreset, {common}; "
-            + (f"pbn_rollout, {chunk} steps/launch, per-step obs/actions/rewards/flags written to HBM"
+            + (f"pbn_rollout, launches of up to {chunk} steps, per-step obs/actions/rewards/flags written to HBM"
                if rollout_mode else "pbn_step per step"))
-
-
-def gather_pass(env, args, world, dev, stream):
-    """Env-steps/s (all ranks) when every rollout of --chunk steps is followed by packing its
-    (obs, actions, s', reward, flags) records and one all_gather_into_tensor of them
-    (pbn_rl_amd.distributed record layout), eager launches."""
-    from pbn_rl_amd.distributed import record_rows
-
-    W, n, T = env.words, env.num_envs, args.chunk
-    rec = torch.empty((T, record_rows(W), n), dtype=torch.int32, device=dev)
-    flat = torch.empty((world * T, record_rows(W), n), dtype=torch.int32, device=dev)
-    buf = None
-    rounds = max(1, args.steps // T)
-    with torch.cuda.stream(stream):
-        def one():
-            nonlocal buf
-            buf = env.rollout(T, random_actions=True, keep_obs=True, keep_final=True, out=buf)
-            rec[:, 0:W] = buf["obs"][:, :, :n]
-            rec[:, W:2 * W] = buf["flipmask"][:, :, :n]
-            rec[:, 2 * W:3 * W] = buf["final_state"][:, :, :n]
-            rec[:, 3 * W] = buf["reward"][:, :n].view(torch.int32)
-            rec[:, 3 * W + 1] = buf["flags"][:, :n].to(torch.int32)
-            if world > 1:
-                torch.distributed.all_gather_into_tensor(flat, rec)
-        one()
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            torch.distributed.barrier()
-        t0 = time.perf_counter()
-        for _ in range(rounds):
-            one()
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            torch.distributed.barrier()
-        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
-    return world * n * T * rounds / float(el.item())
 
 
 def launch_plan(steps: int, chunk: int):
@@ -273,24 +296,115 @@ def launch_plan(steps: int, chunk: int):
     return [chunk] * full + ([rem] if rem else [])
 
 
+def max_over_ranks(x: float, world: int, dev) -> float:
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier(world: int, local: int) -> None:
+    if world > 1:
+        torch.distributed.barrier(device_ids=[local])
+
+
+def timed(fn, stream, dev, world, local):
+    """Device milliseconds of fn() (launches on `stream`), bracketed by barrier + synchronize,
+    max over ranks."""
+    barrier(world, local)
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    fn()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    barrier(world, local)
+    host_s = time.perf_counter() - t0
+    return max_over_ranks(ev0.elapsed_time(ev1), world, dev), max_over_ranks(host_s, world, dev)
+
+
+def gather_pass(env, plan, world, local, dev, stream):
+    """The timed steps again, each rollout launch followed by one all_gather_into_tensor (RCCL)
+    of its (s, a, s', r, flags) records, written in place by the kernel (TransitionRecords):
+    device ms, max over ranks."""
+    from pbn_rl_amd.distributed import TransitionRecords
+
+    recs = {k: TransitionRecords(k, env.words, env.n_alloc, device=dev) for k in set(plan)}
+    outs = {k: torch.empty(world * r.flat.numel(), dtype=torch.uint8, device=dev) for k, r in recs.items()}
+
+    def run():
+        for k in plan:
+            env.rollout(k, random_actions=True, keep_obs=True, keep_final=True, out=recs[k].rollout_out())
+            torch.distributed.all_gather_into_tensor(outs[k], recs[k].flat)
+
+    with torch.cuda.stream(stream):
+        run()
+        torch.cuda.synchronize(dev)
+        ms, _ = timed(run, stream, dev, world, local)
+    wire = sum(recs[k].flat.numel() for k in plan)
+    return ms, wire
+
+
+def pmc_profile(args, plan):
+    """The rocprofv3 PMC summary of the same launch shape, if one is committed under profiles/
+    (network, envs, steps per launch): HBM bytes and VALU instructions per launch."""
+    if len(set(plan)) != 1:
+        return None, None
+    path = os.path.join(ROOT, "profiles", f"pmc_{args.network}_{args.envs}_{args.mode}_T{plan[0]}.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        return json.load(f), os.path.relpath(path, ROOT)
+
+
+def spawn_ranks(args) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes (one per GPU) before
+    this process touches the GPU, wait for them, return the worst exit code."""
+    import socket
+    import subprocess
+
+    n_dev = torch.cuda.device_count()   # does not initialise the GPU on this image
+    if args.gpus > n_dev:
+        print(f"bench.py: --gpus {args.gpus} but only {n_dev} GPU(s) visible; refusing to run "
+              f"several ranks on one GPU", file=sys.stderr, flush=True)
+        return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=abs)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one GPU per rank over RCCL; more ranks than GPUs (a rehearsal on a smaller box) share
-    # them round-robin and synchronise over gloo (RCCL refuses two ranks on one GPU)
-    n_dev = max(1, torch.cuda.device_count())
-    shared = world > n_dev
-    local = local % n_dev
-    if world > 1:
-        torch.cuda.set_device(local)
-        if shared:
-            torch.distributed.init_process_group("gloo")
-        else:
-            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    n_dev = torch.cuda.device_count()
+    if world > n_dev or local >= n_dev:
+        print(f"bench.py: {world} rank(s) need {world} GPUs, {n_dev} visible", file=sys.stderr, flush=True)
+        sys.exit(2)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if "MASTER_PORT" not in os.environ:
+        import socket
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+    dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    # one process per GPU, RCCL ("nccl" on ROCm) over xGMI; world 1 too (the per-rollout gather)
+    torch.distributed.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
     from pbn_rl_amd.attractors import load_attractors
     from pbn_rl_amd.network import load_network
@@ -320,7 +434,7 @@ def main():
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.synchronize(dev)
 
-    rollout_mode = args.mode == "rollout"
+    rollout_mode = args.mode == "rollout" and agent is None
     chunk = args.chunk if rollout_mode else 1
     bufs = {}   # rollout outputs per launch length; captured graphs write into them, so they live
                 # as long as the graphs (torch.cuda.graph empties the allocator cache on entry)
@@ -353,94 +467,107 @@ def main():
                 for k in plan:
                     launch(k)
             torch.cuda.synchronize(dev)
-            graph.replay()  # warm the graph path
+
+        def run():
+            if use_graph:
+                graph.replay()
+            else:
+                for k in plan:
+                    launch(k)
+
+        # untimed clock ramp: replays of the captured run (no timing, no results kept)
+        warm_reps, t_end = 0, time.perf_counter() + args.clock_warm
+        while True:
+            run()
             torch.cuda.synchronize(dev)
-
-        if world > 1:
-            torch.distributed.barrier()
-        torch.cuda.synchronize(dev)
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        t0 = time.perf_counter()
-        ev0.record(stream)
-        if use_graph:
-            graph.replay()
-        else:
-            for k in plan:
-                launch(k)
-        ev1.record(stream)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            torch.distributed.barrier()
-        elapsed = time.perf_counter() - t0
-    # average launch duration of the step kernel, from HIP events on its own stream over
-    # the timed region (launches are back to back inside the graph)
-    launch_ms = ev0.elapsed_time(ev1) / len(plan)
-
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
-    elapsed = float(el.item())
+            warm_reps += 1
+            if time.perf_counter() >= t_end:
+                break
+        dev_ms, host_s = timed(run, stream, dev, world, local)
+    elapsed = dev_ms * 1e-3
     total_env_steps = world * args.envs * args.steps
     value = total_env_steps / elapsed
 
     with_gather = None
-    if args.gather:
-        with_gather = gather_pass(env, args, world, dev, stream)
+    if rollout_mode and not args.no_gather:
+        gms, wire = gather_pass(env, plan, world, local, dev, stream)
+        with_gather = {"value": total_env_steps / (gms * 1e-3), "ms_per_step": gms / args.steps,
+                       "collective": "torch.distributed.all_gather_into_tensor (RCCL) once per rollout launch",
+                       "launches": len(plan), "wire_bytes_per_rank": wire,
+                       "wire_bytes_per_env_step": wire // (env.n_alloc * args.steps)}
+
+    bil_ms = None
+    if args.workload == "bdq":
+        def bil():
+            for _ in range(50):
+                agent.bilinear()
+        with torch.cuda.stream(stream):
+            agent.bilinear()
+            bil_ms, _ = timed(bil, stream, dev, world, local)
+            bil_ms /= 50
 
     if rank == 0:
         W = spec.words
+        pmc, pmc_path = (None, None) if agent is not None else pmc_profile(args, plan)
         if agent is not None:
-            bytes_launch = None
             kernel = ("BDQ frame (pbn_bilinear_targets, BranchingQNetwork fp32 layers after the bilinear, "
-                      "pbn_q_to_flipmask, pbn_step)")
+                      "pbn_heads_to_flipmask, pbn_step)")
             if args.workload == "bdq-learn":
                 kernel += " + replay store + update_policy (batch 256)"
                 kernel += ", one hipGraph replay per frame" if args.learn_graph else ", eager"
+        frame_ms = dev_ms / args.steps
+        if args.workload == "bdq":
+            # dominant launch: pbn_bilinear_targets.  HBM bytes it must move per frame: the packed
+            # state and target id in, the (n, 256) fp32 layer out, the per-target table and bias
+            # once; the table rows it sums come from L2 (a few hundred KB, re-read by every env)
+            out_dim = agent.q.model[0].output_dim
+            n = env.n_alloc
+            A = max(1, len(spec.attractors))
+            bil_bytes = n * (4 * W + 1) + n * out_dim * 4 + A * spec.n * out_dim * 4 + out_dim * 4
+            achieved = bil_bytes / (bil_ms * 1e-3) / 1e9
+            flops = env.n_alloc * qnet_flops_per_env(spec.n)
+            roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                        "kernel": "pbn_bilinear_targets (the frame's longest launch)", "launch_ms": bil_ms,
+                        "bytes_per_launch": bil_bytes,
+                        "note": "bytes = state+target in, the (n,256) fp32 layer out, the per-target table once; "
+                                "the per-set-bit row sums are L2 reads (the kernel is L2-bound), so the HBM "
+                                "fraction understates how busy it is",
+                        "model_flops_utilisation": {"achieved_tflops": flops / (frame_ms * 1e-3) / 1e12,
+                                                    "peak_tflops": FP32_MATRIX_TFLOPS,
+                                                    "note": "the reference forward's FLOPs (bilinear as N*N*256 "
+                                                            "MACs/env) over the whole frame time; the frame "
+                                                            "executes ~4x fewer"}}
+        elif agent is not None:
+            roofline = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                        "traffic": None, "kernel": kernel, "launch_ms": frame_ms,
+                        "note": "training frame (~150 launches): no single dominant kernel is priced"}
         elif rollout_mode:
-            bytes_launch = env.n_alloc * rollout_bytes_per_env(W, chunk)
-            kernel = "pbn_rollout_pipe (rollout, %d steps/launch)" % chunk
+            bytes_run = sum(env.n_alloc * rollout_bytes_per_env(W, k) for k in plan)
+            achieved = bytes_run / elapsed / 1e9
+            roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS,
+                        "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+                        "kernel": "pbn_rollout (%s)" % ", ".join(f"{k} steps" for k in plan),
+                        "launch_ms": dev_ms / len(plan), "bytes_per_launch": bytes_run / len(plan),
+                        "bytes_per_env_step": bytes_run / (env.n_alloc * args.steps),
+                        "note": "algorithmic bytes (DESIGN.md 'Algorithmic bytes') over HIP-event time; the "
+                                "kernel is compute/latency bound, see DESIGN.md 'What bounds it'"}
+            if pmc:
+                roofline["traffic_source"] = {"file": pmc_path, "command": pmc.get("command")}
+                if pmc.get("valu_insts_per_launch"):
+                    v = pmc["valu_insts_per_launch"] * len(plan) / elapsed
+                    roofline["valu"] = {"achieved": v, "peak": VALU_WAVE_INSTS_PER_S, "unit": "wave-instructions/s",
+                                        "frac": v / VALU_WAVE_INSTS_PER_S,
+                                        "insts_per_launch": pmc["valu_insts_per_launch"],
+                                        "note": "SQ_INSTS_VALU of the same launch shape (traffic_source) over this "
+                                                "run's time; issue slots only"}
         else:
             bytes_launch = env.n_alloc * algorithmic_bytes_per_env(W)
-            kernel = "pbn_step_wave (single step)"
-        # the timed plan's launches are full chunks except possibly the last
-        full_launch_ms = launch_ms * len(plan) * chunk / args.steps if rollout_mode else launch_ms
-        traffic = None
-        if agent is not None:
-            # the frame is the Q-network: price the reference forward's FLOPs against the
-            # FP32 matrix peak (MI355X_MICROARCH.md: 157.3 TFLOP/s), as model-FLOPs utilisation
-            flops = env.n_alloc * qnet_flops_per_env(spec.n)
-            achieved = flops / (full_launch_ms * 1e-3) / 1e12
-            roofline = {"bound": "mfma", "achieved": achieved, "peak": FP32_MATRIX_TFLOPS, "unit": "TFLOP/s",
-                        "frac": achieved / FP32_MATRIX_TFLOPS, "traffic": None, "kernel": kernel,
-                        "launch_ms": full_launch_ms, "flops_per_launch": flops,
-                        "note": "one launch = one whole BDQ frame (~20 kernels); achieved = the reference "
-                                "forward's FLOPs (bilinear counted as N*N*256 MACs per env) / frame time, i.e. "
-                                "model-FLOPs utilisation. The bilinear layer itself runs as per-target table "
-                                "reads (pbn_bilinear_targets), so the executed FLOPs are ~4x lower"}
-        else:
-            achieved = bytes_launch / (full_launch_ms * 1e-3) / 1e9
-            pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.network}_{args.envs}_{args.mode}.json")
-            valu_launch = None
-            if os.path.exists(pmc_path):
-                with open(pmc_path) as f:
-                    pmc = json.load(f)
-                traffic = pmc.get("hbm_bytes_per_launch")
-                valu_launch = pmc.get("valu_insts_per_launch")
+            achieved = bytes_launch / (frame_ms * 1e-3) / 1e9
             roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                        "kernel": kernel, "launch_ms": full_launch_ms,
-                        "bytes_per_launch": bytes_launch,
-                        "note": "VALU-bound (Philox volume), see DESIGN.md 'What bounds it'"}
-            if valu_launch:
-                # the compute side of the same kernel: wave-level VALU instructions per launch
-                # (rocprofv3 SQ_INSTS_VALU, profiles/) over this run's launch time, against the
-                # issue rate of one wave64 instruction per 2 cycles per SIMD
-                achieved_valu = valu_launch / (full_launch_ms * 1e-3)
-                roofline["valu"] = {"achieved": achieved_valu, "peak": VALU_WAVE_INSTS_PER_S,
-                                    "unit": "wave-instructions/s", "frac": achieved_valu / VALU_WAVE_INSTS_PER_S,
-                                    "insts_per_launch": valu_launch,
-                                    "note": "issue slots only: a v_mad_u64_u32 (20 per Philox call) holds its "
-                                            "SIMD longer than one slot"}
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "pbn_step",
+                        "launch_ms": frame_ms, "bytes_per_launch": bytes_launch}
         out = {
             "metric": "env steps/sec (batched PBN transitions), Bittner-28 at 1/2/4/8 GPUs"
             if args.network == "pbn28" else f"env steps/sec (batched PBN transitions), {args.network}",
@@ -449,7 +576,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed * 1e3 / args.steps,
+            "ms_per_step": dev_ms / args.steps,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -457,23 +584,29 @@ def main():
             "data": "synthetic",
             "config": {"workload": workload_text(args, chunk, rollout_mode),
                        "network": args.network, "envs_per_gpu": args.envs, "global_envs": world * args.envs,
-                       "parallelism": f"env-shard x{world}", "launch": "hipGraph" if (use_graph or args.learn_graph) else "eager"},
+                       "parallelism": f"env-shard x{world} (RCCL process group)",
+                       "launch": "hipGraph" if (use_graph or args.learn_graph) else "eager"},
             "roofline": roofline,
+            "timing": {"clock": "HIP events on the launch stream, max over ranks",
+                       "host_ms_per_step": host_s * 1e3 / args.steps, "clock_warm_replays": warm_reps},
         }
         if with_gather is not None:
-            out["value_with_gather"] = with_gather
+            out["value_with_gather"] = with_gather["value"]
+            out["gather"] = with_gather
         if world == 1 and not args.no_cpu_baseline:
+            host = host_info()
+            threads = host["usable"]
             if agent is not None:
-                out["cpu_baseline"] = cpu_baseline_bdq(spec, agent.q, args.cpu_seconds)
+                out["cpu_baseline"] = cpu_baseline_bdq(spec, agent.q, args.cpu_seconds, threads)
             else:
-                out["cpu_baseline"] = cpu_baseline(spec, args.envs, args.cpu_seconds)
+                out["cpu_baseline"] = cpu_baseline(spec, args.envs, args.cpu_seconds, threads)
                 out["cpu_baseline_python"] = python_baseline(spec)
                 out["cpu_baseline_numpy"] = numpy_baseline(spec, args.envs)
-            out["host"] = host_info()
+                out["config1"] = config1_line(dev)
+            out["host"] = host
         print(json.dumps(out), flush=True)
     env.close()
-    if world > 1:
-        torch.distributed.destroy_process_group()
+    torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -13,7 +13,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpbn_oracle.so")
+# PBN_ORACLE_LIB selects another build of the same source (the ASan one, tests/test_oracle_asan.py)
+LIB_PATH = os.environ.get("PBN_ORACLE_LIB") or os.path.join(HERE, "libpbn_oracle.so")
 _lib = None
 
 

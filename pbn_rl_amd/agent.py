@@ -245,10 +245,9 @@ class BatchedBDQ:
             self._pack, self._pack_key = pack, key
         return pack
 
-    def _forward(self, heads: bool) -> torch.Tensor:
-        if not self.fast:
-            y = self.q.model[0](self.observe())
-            return self.q.forward_heads(y) if heads else self.q.forward_tail(y)
+    def bilinear(self):
+        """One ``pbn_bilinear_targets`` launch into ``self._y`` (the first layer + LeakyReLU of the
+        fast forward); returns the head weights of the same pack."""
         env = self.env
         bil = self.q.model[0]
         T, bias, hw = self._packed()
@@ -259,6 +258,13 @@ class BatchedBDQ:
                                               bias.data_ptr(), bil.output_dim, 1 if self._act else 0,
                                               self._slope, self._y.data_ptr(), env._stream()),
                        "pbn_bilinear_targets")
+        return hw
+
+    def _forward(self, heads: bool) -> torch.Tensor:
+        if not self.fast:
+            y = self.q.model[0](self.observe())
+            return self.q.forward_heads(y) if heads else self.q.forward_tail(y)
+        hw = self.bilinear()
         # the kernel applied model[1] (LeakyReLU) when _act
         out = self.q.forward_heads(self._y, skip_act=self._act, weights=hw)
         return out if heads else self.q.dueling(out)

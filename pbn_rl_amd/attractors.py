@@ -37,10 +37,12 @@ def clean_state(state: Sequence) -> Tuple[int, ...]:
     return tuple(0 if v == "*" else int(v) for v in state)
 
 
-def _successor_options(net: Network, s: int) -> List[Tuple[int, ...]]:
+def _successor_options(net: Network, s: int, prob_bits: int = 16) -> List[Tuple[int, ...]]:
+    """Values each node can take next from state s, over the functions whose quantised weight
+    at ``prob_bits`` is non-zero (the functions the kernel can select)."""
     bits = [(s >> i) & 1 for i in range(net.n)]
     opts = []
-    thr = net.thresholds(16)
+    thr = net.thresholds(prob_bits)
     for i, fl in enumerate(net.nodes):
         vals = set()
         prev = 0
@@ -52,7 +54,7 @@ def _successor_options(net: Network, s: int) -> List[Tuple[int, ...]]:
     return opts
 
 
-def find_attractors(net: Network, max_nodes: int = 20) -> Attractors:
+def find_attractors(net: Network, max_nodes: int = 20, prob_bits: int = 16) -> Attractors:
     """Bottom SCCs of the asynchronous-free synchronous PBN STG (exhaustive)."""
     n = net.n
     if n > max_nodes:
@@ -60,7 +62,7 @@ def find_attractors(net: Network, max_nodes: int = 20) -> Attractors:
     total = 1 << n
     succ: List[List[int]] = []
     for s in range(total):
-        opts = _successor_options(net, s)
+        opts = _successor_options(net, s, prob_bits)
         nexts = [0]
         for i, vals in enumerate(opts):
             if len(vals) == 1:

@@ -30,7 +30,7 @@ import numpy as np
 from .attractors import Attractors
 from .network import Network
 
-__all__ = ["successor_boxes", "bottom_sccs", "discover_attractors"]
+__all__ = ["successor_boxes", "bottom_sccs", "discover_attractors", "discover_attractors_escalating"]
 
 
 def successor_boxes(net: Network, bits: np.ndarray, prob_bits: int = 16) -> Tuple[np.ndarray, np.ndarray]:
@@ -43,10 +43,13 @@ def successor_boxes(net: Network, bits: np.ndarray, prob_bits: int = 16) -> Tupl
         prev = 0
         for f, c in zip(fl, thr):
             if c > prev:
+                # the truth table as a byte per row: a Python-int table of arity >= 6 does not
+                # fit an int64 shift (bb33, model_tester.py's 47-node network: arity up to 20)
+                lut = np.array([(f.table >> m) & 1 for m in range(1 << f.arity)], dtype=np.uint8)
                 idx = np.zeros(S, dtype=np.int64)
                 for j, g in enumerate(f.inputs):
                     idx |= bits[:, g].astype(np.int64) << j
-                v = (f.table >> idx) & 1
+                v = lut[idx]
                 can1[:, i] |= v == 1
                 can0[:, i] |= v == 0
             prev = c
@@ -188,3 +191,16 @@ def discover_attractors(net: Network, *, chains: int = 65536, burn_in: int = 100
     shifts = np.arange(32, dtype=np.uint32)
     bits = ((words[:, :, None] >> shifts) & 1).reshape(len(words), -1)[:, :net.n].astype(np.uint8)
     return bottom_sccs(net, bits, prob_bits=prob_bits, max_box=max_box, max_states=max_states)
+
+
+def discover_attractors_escalating(net: Network, *, burn_ins=(1000, 5000, 20000), **kwargs) -> Attractors:
+    """``discover_attractors`` with a growing burn-in until a bottom SCC is certified: 1,000
+    steps suffice for pbn28 but not pbn70 (20,000 certify its bottom SCC).  Returns
+    the first non-empty result (empty if every burn-in fails)."""
+    kwargs.pop("burn_in", None)
+    found: Attractors = []
+    for b in burn_ins:
+        found = discover_attractors(net, burn_in=b, **kwargs)
+        if found:
+            break
+    return found

@@ -104,7 +104,7 @@ class _Graph:
             raise ValueError("genSTG is exhaustive; limited to 20 nodes")
         stg = {}
         for s in range(1 << net.n):
-            opts = _successor_options(net, s)
+            opts = _successor_options(net, s, self._env.spec.prob_bits)
             nexts = [0]
             for i, vals in enumerate(opts):
                 nexts = [x | (v << i) for x in nexts for v in vals]
@@ -120,7 +120,8 @@ class PBNEnv:
                  attractors: Optional[Attractors] = None, horizon: int = 20, perturbation: float = 0.01,
                  prob_bits: int = 16, seed: Optional[int] = None, device=None, render_mode=None,
                  success_reward: float = 5.0, wrong_attractor_cost: float = 2.0, action_cost: float = 1.0,
-                 step_cost: float = 0.0, name: Optional[str] = None):
+                 step_cost: float = 0.0, name: Optional[str] = None, grow_attractors: bool = True,
+                 discovery: Optional[dict] = None):
         if isinstance(network, str):
             if attractors is None:
                 attractors = load_attractors(network)
@@ -135,15 +136,20 @@ class PBNEnv:
             # exhaustive STG search while it is cheap; beyond that, GPU simulation + exact
             # verification (discovery.py); both return bottom SCCs (print_graph.py:15-34)
             if network.n <= 16:
-                attractors = find_attractors(network)
+                attractors = find_attractors(network, prob_bits=prob_bits)
             else:
-                from .discovery import discover_attractors
-                attractors = discover_attractors(network, prob_bits=prob_bits, device=device)
+                from .discovery import discover_attractors_escalating
+                attractors = discover_attractors_escalating(network, prob_bits=prob_bits, device=device,
+                                                            **(discovery or {}))
+        if not attractors:
+            raise ValueError(f"{network.name}: no attractor found (no targets or terminal states); pass "
+                             f"attractors= or discovery= (chains/burn_in) explicitly")
         if min_attractors is not None and len(attractors) < min_attractors:
             warnings.warn(f"network has {len(attractors)} attractors < min_attractors={min_attractors}")
-        self.spec = EnvSpec(network, attractors, perturbation=perturbation, prob_bits=prob_bits, horizon=horizon,
-                            success_reward=success_reward, wrong_attractor_cost=wrong_attractor_cost,
-                            action_cost=action_cost, step_cost=step_cost)
+        self._spec_kwargs = dict(perturbation=perturbation, prob_bits=prob_bits, horizon=horizon,
+                                 success_reward=success_reward, wrong_attractor_cost=wrong_attractor_cost,
+                                 action_cost=action_cost, step_cost=step_cost)
+        self.spec = EnvSpec(network, attractors, **self._spec_kwargs)
         self.N = network.n
         self.render_mode = render_mode
         self._seed = int(seed if seed is not None else np.random.SeedSequence().entropy % (1 << 63))
@@ -153,7 +159,8 @@ class PBNEnv:
         self.discrete_action_space = self.action_space
         self.graph = _Graph(self)
         self.all_attractors: List[List[Tuple[int, ...]]] = [list(a) for a in self.spec.attractors]
-        self.real_attractors = self.all_attractors
+        # the attractor set the env was built with; all_attractors may grow (grow())
+        self.real_attractors = [list(a) for a in self.spec.attractors]
         self.attracting_states = [s for a in self.all_attractors for s in a]
         self.state_attractor_id = -1
         self.target_attractor_id = -1
@@ -162,6 +169,19 @@ class PBNEnv:
         self.target_nodes: List[int] = []
         self.control_nodes = list(range(self.N))
         self._ep_lens: List[int] = []
+        W = self.spec.words
+        self._pin_flip = torch.zeros(W, 1, dtype=torch.int32).pin_memory()
+        self._pin_state = torch.zeros(W, 1, dtype=torch.int32).pin_memory()
+        self._pin_reward = torch.zeros(1, dtype=torch.float32).pin_memory()
+        self._pin_flags = torch.zeros(1, dtype=torch.uint8).pin_memory()
+        # attractor growth (bdq_model/__init__.py:182-184): states revisited outside the known
+        # attractors are verified as bottom SCCs (discovery.bottom_sccs) at episode ends
+        self.grow_attractors = grow_attractors
+        self._visits: dict = {}
+        self._checked: set = set()
+        # rework_probas (bdq_model/__init__.py:203): per (start, target) pair weights
+        self._pair_len: Optional[np.ndarray] = None
+        self._rng = np.random.default_rng(self._seed)
 
     # gymnasium wrapper chain compatibility (env.env.env, env.unwrapped)
     @property
@@ -186,6 +206,8 @@ class PBNEnv:
         if seed is not None:
             self._seed = int(seed)
         self._venv.reset(seed=self._seed)
+        if self._pair_len is not None and len(self.all_attractors) >= 2:
+            self._reset_reweighted()
         state = self._read_state()
         tgt = int(self._venv.target[0].item())
         self.target_attractor_id = tgt if tgt != NO_TARGET else -1
@@ -216,13 +238,23 @@ class PBNEnv:
                 raise ValueError(f"action {a} outside [0, {self.N}]")
             if a > 0:
                 bits[a - 1] = 1
-        fm = torch.tensor(np.array(self.spec.network.pack(bits), dtype=np.uint32).view(np.int32)[:, None],
-                          device=self._venv.device)
-        state_w, reward, flags = self._venv.step_flipmask(fm)
-        fl = int(flags[0].item())
-        r = float(reward[0].item())
-        obs = self._read_state()
+        venv = self._venv
+        self._pin_flip.numpy()[:, 0] = np.array(self.spec.network.pack(bits), dtype=np.uint32).view(np.int32)
+        venv.flipmask[:, :1].copy_(self._pin_flip, non_blocking=True)
+        venv.step_flipmask(use_current=True)
+        # one host synchronisation per step: the three results come back by async copies
+        self._pin_state.copy_(venv.state[:, :1], non_blocking=True)
+        self._pin_reward.copy_(venv.reward[:1], non_blocking=True)
+        self._pin_flags.copy_(venv.flags[:1], non_blocking=True)
+        torch.cuda.current_stream(venv.device).synchronize()
+        fl = int(self._pin_flags[0])
+        r = float(self._pin_reward[0])
+        obs = np.array(self.spec.network.unpack(list(self._pin_state.numpy()[:, 0].view(np.uint32))),
+                       dtype=np.int64)
         self.n_steps += 1
+        if self.grow_attractors and not fl & _lib.FLAG_IN_ATTRACTOR:
+            key = tuple(int(v) for v in obs)
+            self._visits[key] = self._visits.get(key, 0) + 1
         info = {"perturbed": bool(fl & _lib.FLAG_PERTURBED), "in_attractor": bool(fl & _lib.FLAG_IN_ATTRACTOR),
                 "flags": fl}
         return obs, r, bool(fl & _lib.FLAG_TERMINATED), bool(fl & _lib.FLAG_TRUNCATED), info
@@ -253,11 +285,81 @@ class PBNEnv:
         self._venv.target[:1].fill_(idx)
 
     def rework_probas(self, ep_len: Optional[int] = None) -> None:
-        """The fork of gym-PBN reweights future (start, target) draws after each episode
-        (bdq_model/__init__.py:203); that rule is unavailable.  Reset draws
-        here are uniform and keyed by (seed, env, step); episode lengths are only recorded."""
+        """Called by the learner after every episode (bdq_model/__init__.py:203;
+        graph_classifier/__init__.py:155 without an argument).  The fork's rule is unavailable
+        (SURVEY.md 0.2); this build's documented rule, a curriculum over (start, target) pairs:
+
+        * ``ep_len`` updates the finished episode's pair: its weight is the running mean of its
+          episode lengths (every pair starts at the horizon), so pairs that take long or time
+          out are drawn more often;
+        * from the first call on, ``reset()`` draws the pair with probability proportional to
+          its weight (target != start), from a host generator seeded with the env seed, and
+          places the start attractor's first state; before it, reset draws are the device's
+          uniform ones (keyed by seed, env and step).
+
+        It also runs the attractor-growth check (``grow()``) at the episode end."""
+        A = len(self.all_attractors)
         if ep_len is not None:
             self._ep_lens.append(int(ep_len))
+            if A >= 2:
+                if self._pair_len is None or self._pair_len.shape[0] != A:
+                    old = self._pair_len
+                    self._pair_len = np.full((A, A, 2), [float(self.spec.horizon or 20), 1.0])
+                    if old is not None:
+                        k = old.shape[0]
+                        self._pair_len[:k, :k] = old
+                s, t = self.state_attractor_id, self.target_attractor_id
+                if 0 <= s < A and 0 <= t < A:
+                    tot, cnt = self._pair_len[s, t]
+                    self._pair_len[s, t] = (tot + float(ep_len), cnt + 1)
+        if self.grow_attractors:
+            self.grow()
+
+    def pair_weights(self) -> Optional[np.ndarray]:
+        """(A, A) reset probabilities of the rework_probas curriculum (None before its first call)."""
+        if self._pair_len is None:
+            return None
+        w = self._pair_len[:, :, 0] / self._pair_len[:, :, 1]
+        np.fill_diagonal(w, 0.0)
+        return w / w.sum()
+
+    def _reset_reweighted(self) -> None:
+        w = self.pair_weights().reshape(-1)
+        k = int(self._rng.choice(w.size, p=w))
+        A = len(self.all_attractors)
+        s, t = divmod(k, A)
+        self._set_state(self.all_attractors[s][0])
+        self._venv.target[:1].fill_(t)
+
+    def grow(self, min_visits: int = 2, max_states: int = 1 << 14) -> int:
+        """Attractor growth (bdq_model/__init__.py:182-184 re-raises epsilon when
+        ``len(env.all_attractors)`` grows): states the env revisited outside every known attractor
+        are closed under the successor relation and verified as bottom SCCs of the STG
+        (``discovery.bottom_sccs``, the print_graph.py:15-34 definition); new ones are appended
+        to ``all_attractors``/``attracting_states`` and become reward/target states on the
+        device.  Returns the number added."""
+        from .discovery import bottom_sccs
+        from .spec import MAX_ATTRACTORS
+
+        cand = [s for s, c in self._visits.items() if c >= min_visits and s not in self._checked]
+        if not cand or len(self.all_attractors) >= MAX_ATTRACTORS:
+            return 0
+        self._checked.update(cand)
+        found = bottom_sccs(self.spec.network, np.array(cand, dtype=np.uint8), prob_bits=self.spec.prob_bits,
+                            max_states=max_states)
+        known = {s for a in self.all_attractors for s in a}
+        new = [a for a in found if not any(s in known for s in a)]
+        new = new[:MAX_ATTRACTORS - len(self.all_attractors)]
+        if not new:
+            return 0
+        self.all_attractors.extend([list(a) for a in new])
+        self.attracting_states = [s for a in self.all_attractors for s in a]
+        self.spec = EnvSpec(self.spec.network, self.all_attractors, **self._spec_kwargs)
+        self._venv.set_spec(self.spec)
+        for a in new:
+            for s in a:
+                self._visits.pop(s, None)
+        return len(new)
 
     def close(self) -> None:
         self._venv.close()

@@ -69,6 +69,9 @@ def compute_ssd_hist(env, model: Optional[Callable] = None, resets: int = 300, i
     N = spec.n
     if N > 32:
         raise ValueError("the SSD histogram has 2^N bins: networks with at most 32 nodes")
+    if resets * iters >= 1 << 32:
+        # the histogram's bins are 32-bit counters: a fixed-point attractor could take every count
+        raise ValueError(f"resets * iters = {resets * iters} counted steps overflow the 32-bit bins (< 2^32)")
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     venv = VectorPBNEnv(spec, resets, seed=seed, device=dev, autoreset=False, keep_final_state=True)
     venv.reset()
@@ -118,8 +121,8 @@ def compute_ssd_hist(env, model: Optional[Callable] = None, resets: int = 300, i
                         graphs[count] = g
                     g.replay()
                 it += 1
-        total = int(hist.sum(dtype=torch.int64).item())
         counts = hist.cpu().numpy().view(np.uint32)
+    total = int(counts.sum(dtype=np.uint64))     # the bins are unsigned 32-bit counts
     venv.close()
     # one host pass over the 2^N bins (float64 out), not astype + divide
     ssd = np.empty(counts.shape, dtype=np.float64)

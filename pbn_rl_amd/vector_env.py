@@ -259,5 +259,15 @@ class VectorPBNEnv:
         if t is not None:
             self.t[: self.num_envs].copy_(t)
 
+    def set_spec(self, spec: EnvSpec) -> None:
+        """Swap in a spec of the same network shape (e.g. a grown attractor set): the device
+        tables are rebuilt; state, targets and step counter are kept."""
+        if spec.n != self.n_nodes or spec.words != self.words:
+            raise ValueError("set_spec needs a spec with the same node count")
+        with torch.cuda.device(self.device):
+            net = _lib.NetHandle(spec)
+        self.net.close()
+        self.net, self.spec = net, spec
+
     def close(self) -> None:
         self.net.close()

@@ -16,6 +16,7 @@ class OracleVectorEnv:
         self.state = torch.from_numpy(st.view(np.int32).copy())
         self.flipmask = torch.zeros_like(self.state)
         self.final_state = torch.zeros_like(self.state)
+        self.device = torch.device("cpu")
 
     def step_flipmask(self, flipmask=None, random_actions=False):
         flip = np.zeros_like(self._st) if flipmask is None else flipmask.numpy().view(np.uint32)
@@ -32,11 +33,12 @@ class OracleVectorEnv:
     def rollout(self, n_steps, flipmasks=None, random_actions=True, keep_obs=True, keep_final=True, out=None):
         """Same contract as VectorPBNEnv.rollout (dict of [n_steps, ...] tensors)."""
         W, n = self.words, self.count
-        rec = {"obs": torch.empty((n_steps, W, n), dtype=torch.int32),
-               "flipmask": torch.empty((n_steps, W, n), dtype=torch.int32),
-               "final_state": torch.empty((n_steps, W, n), dtype=torch.int32),
-               "reward": torch.empty((n_steps, n), dtype=torch.float32),
-               "flags": torch.empty((n_steps, n), dtype=torch.uint8)}
+        rec = out if out is not None else {
+            "obs": torch.empty((n_steps, W, n), dtype=torch.int32),
+            "flipmask": torch.empty((n_steps, W, n), dtype=torch.int32),
+            "final_state": torch.empty((n_steps, W, n), dtype=torch.int32),
+            "reward": torch.empty((n_steps, n), dtype=torch.float32),
+            "flags": torch.empty((n_steps, n), dtype=torch.uint8)}
         for k in range(n_steps):
             rec["obs"][k] = self.state
             fm = None if flipmasks is None else flipmasks[k]

@@ -46,3 +46,24 @@ def test_parse_defaults(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py", "--workload", "bdq-learn"])
     a = bench.parse()
     assert a.learn_graph and a.no_graph and a.no_cpu_baseline
+
+
+def test_multi_gpu_request_without_gpus_fails_loudly():
+    """`bench.py --gpus 2` launches its own ranks; with fewer GPUs than ranks it must refuse
+    (exit 2) instead of rehearsing several ranks on one device."""
+    import os
+    import subprocess
+
+    r = subprocess.run([sys.executable, bench.__file__, "--gpus", "2", "--steps", "1"], capture_output=True,
+                       text=True, timeout=300, env=dict(os.environ, HIP_VISIBLE_DEVICES=""))
+    assert r.returncode == 2 and "--gpus 2" in r.stderr
+    r = subprocess.run([sys.executable, bench.__file__, "--gpus", "1"], capture_output=True, text=True,
+                       timeout=300, env=dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"))
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_usable_cpus():
+    info = bench.usable_cpus()
+    assert 1 <= info["usable"] <= info["affinity"] <= info["cpu_count"]
+    if info["cgroup_quota"] is not None:
+        assert info["usable"] <= max(1, -(-info["cgroup_quota"] // 1))

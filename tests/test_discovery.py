@@ -60,3 +60,32 @@ def test_capped_expansion_never_reports_unverified_sets():
     got = bottom_sccs(net, all_states(10), max_box=1)
     exact = find_attractors(net)
     assert all(a in exact for a in got)
+
+
+@pytest.mark.parametrize("name", ["bb33", "m47"])
+def test_successor_boxes_wide_functions(name):
+    """Functions of arity >= 6 (bb33: 6, model_tester.py's 47-node network: 20) have truth
+    tables wider than an int64 shift; the boxes must still equal the per-state function values."""
+    net = load_network(name)
+    rng = np.random.default_rng(1)
+    bits = rng.integers(0, 2, size=(32, net.n)).astype(np.uint8)
+    can0, can1 = successor_boxes(net, bits)
+    for r in range(32):
+        vals = net.function_values(list(bits[r]))
+        for i, fv in enumerate(vals):
+            assert can1[r, i] == (1 in fv) and can0[r, i] == (0 in fv)
+
+
+def test_find_attractors_threads_prob_bits():
+    """At prob_bits = 4 a function whose weight quantises to 0 adds no STG edge (the kernel can
+    never select it), so the exhaustive search must use the same quantisation."""
+    from fractions import Fraction
+
+    from pbn_rl_amd.network import Network, NodeFunction
+
+    f_keep = NodeFunction((0,), 0b10, Fraction(1000))   # x0' = x0
+    f_flip = NodeFunction((0,), 0b01, Fraction(1))      # x0' = not x0: weight 0 at 4 bits
+    net = Network(["a"], [[f_keep, f_flip]], name="q")
+    assert net.thresholds(4)[0][0] == 16        # all mass on f_keep
+    assert find_attractors(net, prob_bits=4) == [[(0,)], [(1,)]]
+    assert find_attractors(net, prob_bits=16) == [[(0,), (1,)]]

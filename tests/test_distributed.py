@@ -8,7 +8,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from pbn_rl_amd.distributed import ShardedRollout, record_rows, shard_range
+from pbn_rl_amd.distributed import ShardedRollout, TransitionRecords, record_bytes_per_env_step, shard_range
 
 
 def test_shard_range_partitions():
@@ -41,7 +41,7 @@ def _worker(rank, world, port, n_total, steps, result_path):
     rec = ro.rollout(steps)
     glob = ShardedRollout.to_global(ro.gather(rec))
     if rank == 0:
-        torch.save(glob, result_path)
+        torch.save({k: v.clone() for k, v in glob.items()}, result_path)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -59,5 +59,19 @@ def test_two_rank_gather_equals_single_run(tmp_path):
     spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.05)
     single = ShardedRollout(n_total, lambda off, cnt: OracleVectorEnv(spec, off, cnt, seed=11))
     want = single.rollout(steps)
-    assert got.shape == (steps, record_rows(1), n_total)
-    assert torch.equal(got, want)
+    assert set(got) == {"obs", "flipmask", "final_state", "reward", "flags"}
+    for name, t in got.items():
+        assert t.shape[-1] == n_total
+        assert torch.equal(t, want[name]), name
+
+
+def test_record_wire_format():
+    rec = TransitionRecords(3, 1, 64)
+    assert rec.flat.numel() == 3 * 64 * 17 == 3 * 64 * record_bytes_per_env_step(1)
+    assert rec["obs"].shape == (3, 1, 64) and rec["reward"].dtype == torch.float32
+    rec["flags"].fill_(7)
+    assert int(rec.flat[-1]) == 7                       # flags are the last field
+    rec2 = TransitionRecords(2, 3, 32)
+    assert rec2.flat.numel() == 2 * 32 * (12 * 3 + 5)
+    with pytest.raises(ValueError):
+        TransitionRecords(1, 1, 48)

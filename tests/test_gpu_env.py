@@ -108,11 +108,12 @@ def test_sharded_rollout_single_rank():
     spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"))
     ro = ShardedRollout(4096, lambda off, cnt: _reset(VectorPBNEnv(spec, cnt, seed=5, env_offset=off)))
     rec = ro.rollout(8)
+    assert rec.flat.numel() == 8 * 4096 * 17          # the 17 B/env-step wire format
     g = ShardedRollout.to_global(ro.gather(rec))
-    assert g.shape == (8, 5, 4096)
+    assert g["obs"].shape == (8, 1, 4096) and g["flags"].shape == (8, 4096)
     # the record's s' of step k is the next step's obs unless the env reset
-    flags = g[:, 4]
-    nxt_ok = (g[1:, 0] == g[:-1, 2]) | ((flags[:-1] & 16) != 0)
+    flags = g["flags"]
+    nxt_ok = (g["obs"][1:, 0] == g["final_state"][:-1, 0]) | ((flags[:-1] & 16) != 0)
     assert bool(nxt_ok.all())
 
 
@@ -181,3 +182,65 @@ def test_vector_step_control_matches_flipmask_step():
     sb, rb, fb = b.step_flipmask(fm)
     torch.cuda.synchronize()
     assert torch.equal(sa, sb) and torch.equal(ra, rb) and torch.equal(fa, fb)
+
+
+def test_all_attractors_grow_during_training_loop():
+    """bdq_model/__init__.py:182-184 re-raises epsilon when len(env.all_attractors) grows.  The
+    bundled Bittner-28 set (14 fixture states) misses most bottom SCCs of
+    the network (DESIGN.md 'Parity status'), so an env left to run without interventions must
+    discover new ones; every added set is a verified bottom SCC and becomes a device target."""
+    from pbn_rl_amd.discovery import bottom_sccs
+
+    env = PBNEnv(network="pbn28", seed=3, perturbation=0.0, horizon=0)
+    n0 = len(env.all_attractors)
+    real = [list(a) for a in env.real_attractors]
+    (state, _), _ = env.reset()
+    grew = 0
+    for ep in range(6):
+        for _ in range(60):
+            state, *_ = env.step([])
+        env.rework_probas(60)                      # episode end: growth check
+        grew = len(env.all_attractors) - n0
+        if grew:
+            break
+        env.reset()
+    assert grew > 0
+    assert env.real_attractors == real            # the construction-time set is kept apart
+    new = env.all_attractors[n0:]
+    for att in new:
+        assert bottom_sccs(env.spec.network, np.array([att[0]], dtype=np.uint8)) == [sorted(att, key=lambda s: sum(b << i for i, b in enumerate(s)))]
+    assert len(env.attracting_states) == sum(len(a) for a in env.all_attractors)
+    # the device now reports the new attractor: stepping inside it flags IN_ATTRACTOR
+    env.graph.setState(new[0][0])
+    _, _, _, _, info = env.step([])
+    assert info["in_attractor"] or env.spec.attractor_id(env.render()) >= 0
+    env.close()
+
+
+def test_rework_probas_reweights_reset_pairs():
+    env = PBNEnv(network="pbn7", seed=9, perturbation=0.0, grow_attractors=False)
+    A = len(env.all_attractors)
+    assert env.pair_weights() is None
+    env.reset()
+    hard = (env.state_attractor_id, env.target_attractor_id)
+    env.rework_probas(200)                         # one very long episode on this pair
+    w = env.pair_weights()
+    assert w.shape == (A, A) and abs(w.sum() - 1) < 1e-12 and np.all(np.diag(w) == 0)
+    assert w[hard] == w.max() and w[hard] > 2 * np.median(w[w > 0])
+    hits = 0
+    for _ in range(400):
+        env.reset()
+        assert env.state_attractor_id != env.target_attractor_id
+        hits += (env.state_attractor_id, env.target_attractor_id) == hard
+    assert abs(hits / 400 - w[hard]) < 4 * np.sqrt(w[hard] * (1 - w[hard]) / 400) + 0.01
+    env.close()
+
+
+def test_facade_step_single_sync_matches_render():
+    env = PBNEnv(network="pbn70", seed=2, perturbation=0.02, attractors=[[tuple([0] * 70)], [tuple([1] * 70)]])
+    env.reset()
+    rng = np.random.default_rng(2)
+    for _ in range(20):
+        obs, r, term, trunc, info = env.step(list(rng.integers(0, 71, size=3)))
+        assert list(obs) == env.render() and isinstance(r, float)
+    env.close()
