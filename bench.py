@@ -308,12 +308,21 @@ def barrier(world: int, local: int) -> None:
         torch.distributed.barrier(device_ids=[local])
 
 
+# cycles of the spin kernel queued ahead of the start event (~0.1 ms at the shader clock)
+GATE_CYCLES = 250_000
+
+
 def timed(fn, stream, dev, world, local):
     """Device milliseconds of fn() (launches on `stream`), bracketed by barrier + synchronize,
-    max over ranks."""
+    max over ranks.  A spin kernel is queued on the stream ahead of the start event (the
+    "blocking kernel" of nvbench): while it runs the host enqueues the start event, fn's
+    launches and the end event, so the events time the GPU work of fn and not the host's
+    graph-launch latency in front of it.  The spin itself lies outside the two events."""
     barrier(world, local)
     torch.cuda.synchronize(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(stream):
+        torch.cuda._sleep(GATE_CYCLES)
     t0 = time.perf_counter()
     ev0.record(stream)
     fn()
@@ -452,6 +461,11 @@ def main():
 
     plan = launch_plan(args.steps, chunk)
     use_graph = not args.no_graph
+    if rollout_mode:
+        # output buffers of every launch length exist before the capture, so the graph holds
+        # the rollout launches alone (no allocation or fill kernels in the timed region)
+        for k in set(plan) | set(launch_plan(args.warmup, chunk)):
+            bufs[k] = env.rollout_buffers(k, keep_obs=True, keep_final=False)
     with torch.cuda.stream(stream):
         for k in launch_plan(args.warmup, chunk):
             launch(k)

@@ -349,9 +349,9 @@ __device__ __forceinline__ void set_bit(uint32_t (&g)[W], int pos, int N) {
     if ((unsigned)pos < (unsigned)N && (pos >> 5) == w) g[w] |= 1u << (pos & 31);
 }
 
-// VARIANT 0: rollout, loop invariants hoisted (small batches, few waves per SIMD);
-// 1: exactly one step (pbn_step; no loop, lowest VGPR count);
-// 2: rollout with invariants recomputed per step (large batches, occupancy first).
+// VARIANT 1: exactly one step (pbn_step; no loop, lowest VGPR count);
+// 2: rollout with invariants recomputed per step (occupancy first; the rollout of networks
+//    with gates, which the pipelined kernel does not run).
 template <int W, int B, int VARIANT>
 __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a) {
   constexpr bool LEAN = VARIANT == 2;
@@ -420,9 +420,8 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   // is loaded and consumed inside its own branch, so the wait for it stays on that path.
   for (int ks = 0; ks < n_steps; ++ks) {
   if constexpr (LEAN) {
-    // LEAN (large batches): keep loop-invariant expansions (leaf masks, threshold digits,
-    // key schedule, first-round products) inside the loop so VGPRs stay low and
-    // occupancy high; the default variant lets the compiler hoist them (small batches).
+    // keep loop-invariant expansions (leaf masks, threshold digits, key schedule, first-round
+    // products) inside the loop so VGPRs stay low and occupancy high
 #pragma unroll
     for (int r = 0; r < W; ++r) {
 #pragma unroll
@@ -825,19 +824,22 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
   uint32_t u_fl = __builtin_amdgcn_readfirstlane((a.obs ? 1u : 0u) | (a.final_state ? 2u : 0u) |
                                                  (random_actions ? 4u : 0u) | ((a.mode & PBN_MODE_AUTORESET) ? 8u : 0u));
   // digit masks of the first kNodeRecs - 1 thresholds of every node, [q][d][32W], for the
-  // selection wave's compares (from the global node records: the LDS copy is in flight)
+  // selection wave's compares, built from the LDS copy of the node records once it has
+  // landed (from the global records this was two dependent L2 round trips per entry, eight
+  // entries per thread: most of the launch's fixed cost)
   // (single-word states only: for W > 1 the extra LDS costs more occupancy than it saves,
   // measured -15 % on pbn70 x 1M)
   uint32_t* cm = slots + 2 * (size_t)a.slot_words;
+  __syncthreads();
   if constexpr (W == 1) {
     for (int idx = threadIdx.x; idx < (kNodeRecs - 1) * B * 32; idx += blockDim.x) {
       const int i = idx % 32, d = (idx / 32) % B, q = idx / (32 * B);
       uint32_t c = 0;
-      if (i < N && q < (int)a.nrec[i * kNodeRecs].w - 1) c = a.nrec[i * kNodeRecs + q].z;
+      if (i < N && q < (int)recL[i * kNodeRecs].w - 1) c = recL[i * kNodeRecs + q].z;
       cm[idx] = ((c >> (B - 1 - d)) & 1u) ? ~0u : 0u;
     }
+    __syncthreads();
   }
-  __syncthreads();
   // drain the initial state loads here: otherwise the loop-carried st / t / target copies at
   // the bottom of the loop wait on vmcnt(0), which also waits for every store of the step
   __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
@@ -1096,399 +1098,6 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
   }
 }
 
-// ------------------------ rollout kernel with plane-resident state, four waves per group pair
-// For single-word states (N <= 32) whose attractors are all single states (every kaban
-// network with a fixture: pbn28's 14, the synthetic targets).  The state never leaves
-// bit-sliced form: wave 0 holds node plane `lane & 31` of group 2*block + (lane >> 5) in a
-// VGPR across the whole rollout, so its per-step chain has no transposes, no attractor
-// hash, no reward and no global store:
-//   wave 0 (state, step s = k-2): s1 = X ^ M; inputs by ds_bpermute from s1; node chain
-//     from the selection masks; perturbed envs <- s1 ^ G; termination = no node plane
-//     differs from the target planes T (OR-reduced across the half-wave); truncation from
-//     the per-env step counters (lane = env); X, T <- reset planes where an env restarts;
-//   wave 1 (env draws, step k): ENV + PERT calls, actions / flip mask, perturbation gaps,
-//     autoreset state and target -> per-env words;
-//   wave 2 (selection, step k): SEL calls -> (u < c_j) masks, as in pbn_rollout_pipe;
-//   wave 3 (planes + outputs): per-env words of step k-1 -> M, G, reset and new-target planes
-//     (four transposes); step k-3's final planes -> per-env s' (one transpose), attractor
-//     hash, reward, flags, obs / final_state stores.
-// Rings in LDS: draws [4] (written k, read k+1..k+3), planes [3], selection [3], finals [2];
-// the block barrier ends each of the n_steps + 3 iterations.  Results are those of
-// pbn_rollout_pipe bit for bit (term: with single-state attractors, s' is in the target
-// attractor iff s' equals its state).
-namespace plane {
-// per-env draw slot (words): m[64] | gam[64] | rs[64] | tn[64] | info[64]
-constexpr int kM = 0, kG = 64, kRS = 128, kTN = 192, kInfo = 256, kDrawWords = 320;
-// plane slot: Mp[64] | Gp[64] | RSp[64] | TNp[64] | pmask[2] (+pad)
-constexpr int kPM = 256, kPlaneWords = 260;
-// final slot: sp planes[64] | term[2] | trunc[2] | reset[2] (+pad)
-constexpr int kTerm = 64, kTrunc = 66, kReset = 68, kFinalWords = 72;
-}  // namespace plane
-
-// y = OR of a over the 32 lanes of this half-wave, in every lane of the half
-__device__ __forceinline__ uint32_t half_or(uint32_t a, int lane) {
-  a |= xor_lane<1>(a, lane);
-  a |= xor_lane<2>(a, lane);
-  a |= xor_lane<4>(a, lane);
-  a |= xor_lane<8>(a, lane);
-  a |= xor_lane<16>(a, lane);
-  return a;
-}
-
-// 32-bit ballot of this half-wave (bit e = predicate of lane 32h + e), in every lane of the half
-__device__ __forceinline__ uint32_t half_ballot(bool p, int half) {
-  const uint64_t b = __ballot(p);
-  return half ? (uint32_t)(b >> 32) : (uint32_t)b;
-}
-
-template <int K>
-__device__ __forceinline__ uint32_t chain_bp(const uint32_t (&paddr)[kNodeRecs], const uint4* __restrict__ sel,
-                                             int stride, uint32_t s1, const uint32_t* __restrict__ lt, int lt_stride,
-                                             int nf, bool tail, uint32_t x) {
-  uint32_t xin[K][4], ltv[K];
-  uint4 sa[K], sb[K];
-#pragma unroll
-  for (int q = 0; q < K; ++q) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      xin[q][j] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)__builtin_amdgcn_ubfe(paddr[q], 8 * j, 8), (int)s1);
-    sa[q] = sel[(2 * q) * stride];
-    sb[q] = sel[(2 * q + 1) * stride];
-    ltv[q] = (q < K - 1 || tail) ? lt[q * lt_stride] : 0u;
-  }
-#pragma unroll
-  for (int q = K - 1; q >= 0; --q) {
-    const uint32_t x0 = xin[q][0], x1 = xin[q][1], x2 = xin[q][2], x3 = xin[q][3];
-    const uint32_t nx0 = ~x0;
-    const uint32_t v0 = __builtin_amdgcn_perm(nx0, x0, sa[q].x), v1 = __builtin_amdgcn_perm(nx0, x0, sa[q].y);
-    const uint32_t v2 = __builtin_amdgcn_perm(nx0, x0, sa[q].z), v3 = __builtin_amdgcn_perm(nx0, x0, sa[q].w);
-    const uint32_t v4 = __builtin_amdgcn_perm(nx0, x0, sb[q].x), v5 = __builtin_amdgcn_perm(nx0, x0, sb[q].y);
-    const uint32_t v6 = __builtin_amdgcn_perm(nx0, x0, sb[q].z), v7 = __builtin_amdgcn_perm(nx0, x0, sb[q].w);
-    const uint32_t w0 = bfi(x1, v1, v0), w1 = bfi(x1, v3, v2), w2 = bfi(x1, v5, v4), w3 = bfi(x1, v7, v6);
-    const uint32_t fj = bfi(x3, bfi(x2, w3, w2), bfi(x2, w1, w0));
-    const uint32_t y = (q == nf - 1) ? fj : bfi(ltv[q], fj, x);
-    x = (q < nf) ? y : x;
-  }
-  return x;
-}
-
-template <int B>
-__global__ void __launch_bounds__(256, 4) pbn_rollout_plane(StepArgs a) {
-  using namespace plane;
-  constexpr int CPN = B / 4;
-  extern __shared__ uint32_t smem[];
-  const int lane = threadIdx.x & 63;
-  const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (role == 0) __builtin_amdgcn_s_setprio(PBN_STATE_PRIO);
-  const int half = lane >> 5;
-  const int l32 = lane & 31;
-  const int64_t g = (int64_t)blockIdx.x * 2 + half;
-  const bool valid = g < a.n_groups;
-  const int N = a.n_nodes;
-  const int64_t n = a.n_envs;
-  const int64_t le = g * 32 + l32;
-  const uint64_t ge = a.env_offset + (uint64_t)le;
-  const uint64_t G = ge >> 5;
-  const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
-  const bool random_actions = (a.mode & PBN_MODE_RANDOM_ACTIONS) != 0;
-  const int n_steps = a.n_steps;
-  const int LQ = a.lq;
-  uint32_t* L = smem;
-  const uint32_t* cdf = L;
-  const float* rtab = reinterpret_cast<const float*>(L + a.cdf_len);
-  const uint32_t* htab = L + a.cdf_len + 4 * (N + 1);
-  const uint4* selq = reinterpret_cast<const uint4*>(L + a.sel_off);
-  const uint4* recL = reinterpret_cast<const uint4*>(L + a.nrec_off);
-  const int32_t* att_first = reinterpret_cast<const int32_t*>(L + a.att_off);
-  uint32_t* draws = smem + a.tab_words;                    // [4][kDrawWords]
-  uint32_t* planes = draws + 4 * kDrawWords;               // [3][kPlaneWords]
-  uint32_t* sels = planes + 3 * kPlaneWords;               // [3][LQ * 64]
-  uint32_t* finals = sels + 3 * LQ * 64;                   // [2][kFinalWords]
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(a.tab);
-    uint4* dst = reinterpret_cast<uint4*>(L);
-    for (int k = threadIdx.x; k < (a.tab_words >> 2); k += blockDim.x) dst[k] = src[CK(k, a.tab_words >> 2, 5)];
-  }
-  __syncthreads();
-  const uint32_t vmask = valid_word_mask(N, 0);
-  const uint32_t* att_words = L + a.att_off + a.n_attr + 1;
-  // wave 0's loop-carried state: node plane X and target plane T of node l32; per-env step
-  // counter and target id of env l32; bpermute byte addresses 4 * (32h + input) of the
-  // node's function inputs, four to a register (each <= 252)
-  uint32_t X = 0, T = 0, tt0 = 0, tg0 = 0;
-  uint32_t paddr[kNodeRecs];
-  {
-    const int ic = l32 < N ? l32 : 0;
-#pragma unroll
-    for (int q = 0; q < kNodeRecs; ++q) {
-      const uint32_t ins = recL[ic * kNodeRecs + q].x;
-      paddr[q] = (ins << 2) + (half ? 0x80808080u : 0u);   // bytes: 4 * input + 128h, no carries
-    }
-  }
-  if (role == 0 || role == 3) {
-    uint32_t st = 0;
-    if (valid) {
-      st = a.state[CK(le, n, 1)] & vmask;
-      tt0 = a.t[CK(le, n, 2)];
-      tg0 = a.target[CK(le, n, 3)];
-    }
-    if (role == 3 && valid && a.obs) a.obs[CK(le, (size_t)n_steps * n, 7)] = st;   // obs[0]
-    const uint32_t tw = (tg0 < (uint32_t)a.n_attr) ? att_words[att_first[tg0]] : 0u;
-    X = lane_transpose32(st, lane);
-    T = lane_transpose32(tw, lane);
-  }
-  uint32_t u_k0 = k0, u_k1 = k1;
-  int u_gx = a.gap_exact, u_na = a.n_attr, u_mnf = a.max_nf, u_hb = a.hash_bits, u_hp = a.hash_probes,
-      u_hz = a.horizon;
-  uint32_t u_fl = __builtin_amdgcn_readfirstlane((a.obs ? 1u : 0u) | (a.final_state ? 2u : 0u) |
-                                                 (random_actions ? 4u : 0u) | ((a.mode & PBN_MODE_AUTORESET) ? 8u : 0u));
-
-  for (int k = 0; k <= n_steps + 2; ++k) {
-    // per-lane output offsets recomputed every iteration: hoisted, the five 64-bit output
-    // addresses stay live across the loop and push the kernel past 128 VGPRs
-    int64_t lel = le;
-    asm volatile("" : "+v"(lel));
-    asm volatile("" : "+v"(paddr[0]), "+v"(paddr[1]), "+v"(paddr[2]), "+v"(paddr[3]));
-    asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
-    asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
-    PBN_PSTAMP(k, 0);
-    if (role == 1 && k < n_steps) {
-      // ---- env draws of step k, env l32 of group g -> draws[k % 4]
-      uint32_t* dslot = draws + (k & 3) * kDrawWords;
-      uint32_t* pslot = planes + (k % 3) * kPlaneWords;
-      const uint64_t step = a.step + (uint64_t)k;
-      const uint32_t st_lo = (uint32_t)step;
-      const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
-      const uint32_t ge_lo = (uint32_t)ge;
-      bool gam_any_lane = false;
-      if (valid) {
-        const Word4 E = pbn::philox4x32_10(ge_lo, st_lo, pbn::kStreamEnv << 28, ge_hi, u_k0, u_k1);
-        const Word4 P4 = pbn::philox4x32_10(ge_lo, st_lo, pbn::kStreamPert << 28, ge_hi, u_k0, u_k1);
-        uint32_t m[1] = {0u}, gam[1] = {0u};
-        if (u_fl & 4u) {
-#pragma unroll
-          for (int q = 0; q < 3; ++q) {
-            const int act = (int)(__umul24((E.w >> (10 * q)) & 1023u, (uint32_t)(N + 1)) >> 10);
-            set_bit<1>(m, act - 1, N);
-          }
-          a.flipmask[CK((size_t)k * n + lel, (size_t)n_steps * n, 8)] = m[0];
-        } else {
-          m[0] = a.flipmask[CK((size_t)k * n + lel, (size_t)n_steps * n, 6)] & vmask;
-        }
-        const uint32_t pc = __builtin_popcount(m[0]);
-        int g0, g1, g2;
-        if (u_gx) {
-          g0 = gap_of(cdf, a.cdf_len, E.x); g1 = gap_of(cdf, a.cdf_len, E.y); g2 = gap_of(cdf, a.cdf_len, P4.x);
-        } else {
-          g0 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.x);
-          g1 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.y);
-          g2 = gap_est(cdf, a.cdf_len, a.inv_log2q, P4.x);
-        }
-        const int p0 = g0 - 1, p1 = p0 + g1, p2 = p1 + g2;
-        set_bit<1>(gam, p0, N);
-        set_bit<1>(gam, p1, N);
-        set_bit<1>(gam, p2, N);
-        if (p2 < N - 1) {   // rare: a fourth flip is possible
-          Word4 P = P4;
-          int pos = p2;
-          for (int kk = 3; pos < N - 1; ++kk) {
-            if ((kk & 3) == 2)
-              P = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamPert << 28) | (uint32_t)((kk - 2) >> 2), ge_hi, u_k0, u_k1);
-            const int j4 = (kk - 2) & 3;
-            const uint32_t u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
-            pos += u_gx ? gap_of(cdf, a.cdf_len, u) : gap_est(cdf, a.cdf_len, a.inv_log2q, u);
-            set_bit<1>(gam, pos, N);
-          }
-        }
-        const bool pert = gam[0] != 0u;
-        gam_any_lane = pert;
-        uint32_t rs, rt, tn;
-        const uint32_t Rw = E.z;
-        if (u_na >= 1) {   // single-state attractors: attractor a is state a
-          const uint32_t A = (uint32_t)u_na;
-          const uint32_t as = __umul24(Rw & 1023u, A) >> 10;
-          rs = att_words[as];
-          rt = as;
-          if (A >= 2) {
-            rt = __umul24((Rw >> 10) & 1023u, A - 1) >> 10;
-            rt += (rt >= as) ? 1u : 0u;
-          }
-          tn = att_words[rt];
-        } else {
-          const Word4 rr = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamReset << 28) | 1u, ge_hi, u_k0, u_k1);
-          rs = rr.x & vmask;
-          rt = PBN_NO_TARGET;
-          tn = 0u;
-        }
-        dslot[kM + lane] = m[0];
-        dslot[kG + lane] = gam[0];
-        dslot[kRS + lane] = rs;
-        dslot[kTN + lane] = tn;
-        dslot[kInfo + lane] = rt | (pc << 8) | ((uint32_t)pert << 16);
-      }
-      const uint32_t pm = half_ballot(valid && gam_any_lane, half);
-      if (l32 == 0) pslot[kPM + half] = pm;
-    } else if (role == 2 && k < n_steps) {
-      // ---- selection masks of step k -> sels[k % 3], [q][32h + node]
-      uint32_t* lt_out = sels + (k % 3) * LQ * 64 + half * 32;
-      const uint64_t step = a.step + (uint64_t)k;
-      const uint32_t st_lo = (uint32_t)step;
-      const uint32_t G_hi = (uint32_t)((G >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
-      const uint32_t G_lo = (uint32_t)G;
-      const int i = l32;
-      const int ic = i < N ? i : 0;
-      const uint4 r0 = recL[ic * kNodeRecs];
-      if (valid && i < N && (int)r0.w > 1) {
-        uint32_t dig[16];
-#pragma unroll
-        for (int c = 0; c < CPN; ++c) {
-          const Word4 o = pbn::philox4x32_10(G_lo, st_lo, (pbn::kStreamSel << 28) | (uint32_t)(4 * i + c), G_hi, u_k0, u_k1);
-          dig[4 * c + 0] = o.x; dig[4 * c + 1] = o.y; dig[4 * c + 2] = o.z; dig[4 * c + 3] = o.w;
-        }
-        const int nf = (int)r0.w;
-#pragma unroll
-        for (int q = 0; q < kNodeRecs - 1; ++q)
-          if (q < nf - 1) lt_out[q * 64 + i] = less_than(dig, recL[ic * kNodeRecs + q].z, B);
-        const int f0 = (int)recL[ic * kNodeRecs + 1].w;
-        for (int j = kNodeRecs - 1; j < nf - 1; ++j)
-          lt_out[j * 64 + i] = less_than(dig, a.fcompact[CK(f0 + j, a.n_funcs, 9)].z, B);
-      }
-    } else if (role == 0 && k >= 2 && k <= n_steps + 1) {
-      // ---- state part of step s = k - 2
-      const int s = k - 2;
-      const uint32_t* pslot = planes + (s % 3) * kPlaneWords;
-      const uint32_t* dslot = draws + (s & 3) * kDrawWords;
-      const uint32_t* lt_in = sels + (s % 3) * LQ * 64 + half * 32;
-      uint32_t* fslot = finals + (s & 1) * kFinalWords;
-      const uint32_t Mp = pslot[kM + lane], Gp = pslot[kG + lane], RSp = pslot[kRS + lane], TNp = pslot[kTN + lane];
-      const uint32_t pm = pslot[kPM + half];
-      const uint32_t info = dslot[kInfo + lane];
-      const uint32_t s1 = X ^ Mp;
-      const int i = l32;
-      int ii = i < N ? i : 0;
-      asm volatile("" : "+v"(ii));
-      const int nf = (int)recL[ii * kNodeRecs].w;
-      uint32_t x = 0;
-      if (u_mnf > kNodeRecs) {   // chain tail of nodes with more than kNodeRecs functions
-        const int f0 = (int)recL[ii * kNodeRecs + 1].w;
-        for (int j = nf - 1; j >= kNodeRecs; --j) {
-          const uint4 rc = a.fcompact[CK(f0 + j, a.n_funcs, 9)];
-          uint32_t xi[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            xi[q] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * (32u * half + ((rc.x >> (8 * q)) & 0xFFu))), (int)s1);
-          uint32_t v[8];
-#pragma unroll
-          for (int mm = 0; mm < 8; ++mm) {
-            const uint32_t l0 = (uint32_t)__builtin_amdgcn_sbfe((int)rc.y, 2 * mm, 1);
-            const uint32_t l1 = (uint32_t)__builtin_amdgcn_sbfe((int)rc.y, 2 * mm + 1, 1);
-            v[mm] = bfi(xi[0], l1, l0);
-          }
-          const uint32_t w0 = bfi(xi[1], v[1], v[0]), w1 = bfi(xi[1], v[3], v[2]);
-          const uint32_t w2 = bfi(xi[1], v[5], v[4]), w3 = bfi(xi[1], v[7], v[6]);
-          const uint32_t fj = bfi(xi[3], bfi(xi[2], w3, w2), bfi(xi[2], w1, w0));
-          x = (j == nf - 1) ? fj : bfi(lt_in[j * 64 + ii], fj, x);
-        }
-      }
-      const uint4* sel = selq + ii;
-      const uint32_t* lti = lt_in + ii;
-      switch (u_mnf) {
-        case 1: x = chain_bp<1>(paddr, sel, 32, s1, lti, 64, nf, u_mnf > kNodeRecs, x); break;
-        case 2: x = chain_bp<2>(paddr, sel, 32, s1, lti, 64, nf, u_mnf > kNodeRecs, x); break;
-        case 3: x = chain_bp<3>(paddr, sel, 32, s1, lti, 64, nf, u_mnf > kNodeRecs, x); break;
-        default: x = chain_bp<4>(paddr, sel, 32, s1, lti, 64, nf, u_mnf > kNodeRecs, x); break;
-      }
-      x = i < N ? x : 0u;
-      x = bfi(pm, s1 ^ Gp, x);                       // perturbed envs: s' = s1 ^ gamma
-      // termination: env e's s' equals its target state in every node plane
-      const uint32_t differs = half_or(x ^ T, lane);
-      const uint32_t has_target = half_ballot(tg0 < (uint32_t)u_na, half);
-      const uint32_t term = ~differs & has_target;
-      int tt = (int)tt0 + 1;
-      tt = tt > 255 ? 255 : tt;
-      const uint32_t trunc = half_ballot(u_hz > 0 && tt >= u_hz, half);
-      const uint32_t reset = (u_fl & 8u) ? (term | trunc) : 0u;
-      fslot[lane] = x;
-      if (l32 == 0) {
-        fslot[kTerm + half] = term;
-        fslot[kTrunc + half] = trunc;
-        fslot[kReset + half] = reset;
-      }
-      X = bfi(reset, RSp, x);
-      T = bfi(reset, TNp, T);
-      const bool rs_e = (reset >> l32) & 1u;
-      tt0 = rs_e ? 0u : (uint32_t)tt;
-      tg0 = rs_e ? (info & 0xFFu) : tg0;
-    } else if (role == 3) {
-      // ---- planes of step k - 1 (draws -> node planes)
-      if (k >= 1 && k <= n_steps) {
-        const int s = k - 1;
-        const uint32_t* dslot = draws + (s & 3) * kDrawWords;
-        uint32_t* pslot = planes + (s % 3) * kPlaneWords;
-        const uint32_t rs = dslot[kRS + lane], tn = dslot[kTN + lane];
-        pslot[kM + lane] = lane_transpose32(dslot[kM + lane], lane);
-        pslot[kG + lane] = lane_transpose32(dslot[kG + lane], lane);
-        pslot[kRS + lane] = lane_transpose32(rs, lane);
-        pslot[kTN + lane] = lane_transpose32(tn, lane);
-      }
-      // ---- outputs of step k - 3
-      if (k >= 3) {
-        const int s = k - 3;
-        const uint32_t* fslot = finals + (s & 1) * kFinalWords;
-        const uint32_t* dslot = draws + (s & 3) * kDrawWords;
-        const uint32_t sp = lane_transpose32(fslot[lane], lane);
-        const uint32_t term_h = fslot[kTerm + half], trunc_h = fslot[kTrunc + half], reset_h = fslot[kReset + half];
-        const uint32_t info = dslot[kInfo + lane];
-        const uint32_t rs = dslot[kRS + lane];
-        const bool pert = (info >> 16) & 1u;
-        const uint32_t pc = (info >> 8) & 0xFFu;
-        const float r_none = rtab[pc], r_wrong = rtab[(N + 1) + pc], r_term = rtab[2 * (N + 1) + pc];
-        int att = -1;
-        if (u_hb > 0) {
-          const int hmask = (1 << u_hb) - 1;
-          const uint32_t* hid = htab + (hmask + 1);
-          const uint32_t h = (sp * a.hash_mult[0]) >> (32 - u_hb);
-          {
-            const uint32_t slot_i = h & hmask;
-            const uint32_t id = hid[slot_i];
-            att = (htab[slot_i] == sp && id != 0xFFFFFFFFu) ? (int)id : att;
-          }
-          for (int pr = 1; pr < u_hp; ++pr) {
-            const uint32_t slot_i = (h + pr) & hmask;
-            const uint32_t id = hid[slot_i];
-            if (htab[slot_i] == sp && id != 0xFFFFFFFFu) att = (int)id;
-          }
-        }
-        const bool term = (term_h >> l32) & 1u;
-        const bool trunc = (trunc_h >> l32) & 1u;
-        const bool reset = (reset_h >> l32) & 1u;
-        const bool in_attr = att >= 0;
-        const bool wrong = in_attr && !term;
-        const uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) |
-                            ((uint32_t)pert << 3) | ((uint32_t)reset << 4);
-        if (valid) {
-          a.reward[CK((size_t)s * n + lel, (size_t)n_steps * n, 11)] = term ? r_term : (wrong ? r_wrong : r_none);
-          a.flags[CK((size_t)s * n + lel, (size_t)n_steps * n, 15)] = (uint8_t)fl;
-          if (u_fl & 2u) a.final_state[CK((size_t)s * n + lel, (size_t)n_steps * n, 10)] = sp;
-          if ((u_fl & 1u) && s + 1 < n_steps)
-            a.obs[CK((size_t)(s + 1) * n + lel, (size_t)n_steps * n, 7)] = reset ? rs : sp;
-        }
-      }
-    }
-    PBN_PSTAMP(k, 1);
-    lds_barrier();
-    PBN_PSTAMP(k, 2);
-  }
-  if (role == 0) {
-    const uint32_t st = lane_transpose32(X, lane);
-    if (valid) {
-      a.state_out[CK(le, n, 16)] = st;
-      a.t[CK(le, n, 17)] = (uint8_t)tt0;
-      a.target[CK(le, n, 18)] = (uint8_t)tg0;
-    }
-  }
-}
-
 // ------------------------------------------------------------- state histogram
 // Visits per state for the steady-state distribution.  States of a steady-state chain
 // concentrate on a few attractor basins, so a wave first merges equal values (a few
@@ -1610,17 +1219,6 @@ StepFn pick_pipe_w(int B) {
   return nullptr;
 }
 
-StepFn pick_plane(int W, int B) {
-  if (W != 1) return nullptr;
-  switch (B) {
-    case 4: return pbn_rollout_plane<4>;
-    case 8: return pbn_rollout_plane<8>;
-    case 12: return pbn_rollout_plane<12>;
-    case 16: return pbn_rollout_plane<16>;
-  }
-  return nullptr;
-}
-
 StepFn pick_pipe(int W, int B) {
   switch (W) {
     case 1: return pick_pipe_w<1>(B);
@@ -1662,20 +1260,13 @@ struct pbn_net {
   uint4* d_nrec = nullptr;
   int n_funcs = 0;
   size_t lds_wave = 0;
-  StepFn wave = nullptr;        // rollout, loop invariants hoisted (small batches)
   StepFn wave1 = nullptr;       // single step (pbn_step)
-  StepFn wave_lean = nullptr;   // rollout with low VGPR count (large batches)
-  StepFn pipe = nullptr;        // rollout, three waves per group (small batches)
+  StepFn wave_lean = nullptr;   // rollout, one wave per group (networks with gates)
+  StepFn pipe = nullptr;        // rollout, three waves per group pair (every other network)
   size_t lds_pipe = 0;
-  StepFn plane = nullptr;       // rollout, plane-resident state (W == 1, single-state attractors)
-  size_t lds_plane = 0;
   int n_gates = 0, n_glayers = 0, gate_off = 0, glayer_off = 0;   // lowered wide functions
   int max_nf = 0, lq = 1, slot_words = 0;
-  int64_t roll_pipe_groups = 1 << 30;  // rollouts with at most this many groups use the pipelined kernel
-  int force_roll = 0;        // PBN_ROLL env override: 1 = hoist, 2 = lean, 3 = pipe, 4 = plane
-  int64_t roll_lean_groups = 4096;  // rollouts above this many 32-env groups use the lean variant
-                                    // (crossover between 65,536 and 262,144 envs:
-                                    // profiles/r01_sweep_pbn28_variants_v4.jsonl)
+  int force_roll = 0;        // PBN_ROLL env override: 2 = lean (wave kernel), 3 = pipe
   ResetFn reset = nullptr;
   uint32_t* d_tab = nullptr;
   int32_t* d_att_start = nullptr;
@@ -2059,26 +1650,14 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   // + the selection wave's threshold digit masks [kNodeRecs - 1][B][32] (W == 1)
   net->lds_pipe = ((size_t)net->tab_words + 64 * (size_t)W + 2 * (size_t)net->slot_words +
                    (W == 1 ? (size_t)(kNodeRecs - 1) * d->prob_bits * 32 : 0)) * 4;
-  {
-    bool single = true;
-    for (int at = 0; at < A; ++at) single = single && (d->attractor_start[at + 1] - d->attractor_start[at] == 1);
-    if (W == 1 && single) {
-      net->plane = pick_plane(W, d->prob_bits);
-      net->lds_plane = ((size_t)net->tab_words + 4 * plane::kDrawWords + 3 * plane::kPlaneWords +
-                        3 * (size_t)net->lq * 64 + 2 * plane::kFinalWords) * 4;
-    }
-  }
   // compact records for the wave kernel: {inputs as bytes, 4-input truth table, threshold, 0}
-  net->wave = pick_wave<0>(W, d->prob_bits);
   net->wave1 = pick_wave<1>(W, d->prob_bits);
   net->wave_lean = pick_wave<2>(W, d->prob_bits);
   net->pipe = pick_pipe(W, d->prob_bits);
   net->reset = pick_reset(W);
   if (const char* env = getenv("PBN_ROLL")) {
-    if (!strcmp(env, "hoist")) net->force_roll = 1;
     if (!strcmp(env, "lean")) net->force_roll = 2;
     if (!strcmp(env, "pipe")) net->force_roll = 3;
-    if (!strcmp(env, "plane")) net->force_roll = 4;
   }
   int rc;
   if (hipGetDevice(&net->device) != hipSuccess) {
@@ -2093,9 +1672,9 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     free_net(net);
     return rc;
   }
-  for (int ti = 1; ti < 6; ++ti) {
-    const StepFn fn = ti == 1 ? net->wave : (ti == 2 ? net->wave_lean : (ti == 3 ? net->wave1 : (ti == 4 ? net->pipe : net->plane)));
-    const size_t bytes = ti == 4 ? net->lds_pipe : (ti == 5 ? net->lds_plane : net->lds_wave);
+  for (int ti = 2; ti < 5; ++ti) {
+    const StepFn fn = ti == 2 ? net->wave_lean : (ti == 3 ? net->wave1 : net->pipe);
+    const size_t bytes = ti == 4 ? net->lds_pipe : net->lds_wave;
     if (!fn || bytes > 160 * 1024) continue;  // variant unusable for this net; never picked
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)bytes) != hipSuccess) {
@@ -2309,23 +1888,11 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
 #ifdef PBN_STAMPS
   a.stamps = g_stamps;
 #endif
-  // hoisting loop invariants shortens each step's critical path, the lean variant keeps
-  // occupancy; lean measured faster at every size (profiles/r01_sweep_pbn28_variants.jsonl)
-  // the plane-resident kernel is opt-in (PBN_ROLL=plane): its shorter state-wave chain buys
-  // nothing once the SIMDs are VALU-bound (profiles/r01_sweep_plane_vs_pipe.jsonl)
-  bool plane = net->force_roll == 4 && net->plane != nullptr && net->lds_plane <= 64 * 1024;
-  bool pipe = a.n_groups <= net->roll_pipe_groups && net->lds_pipe <= 64 * 1024;
-  bool lean = a.n_groups > (int64_t)net->roll_lean_groups;
-  if (net->force_roll) pipe = net->force_roll == 3;
-  if (net->n_gates) pipe = plane = false;   // gates (wide functions) run in the wave kernels only
-  if (net->force_roll == 1) lean = false;
-  if (net->force_roll == 2) lean = true;
-  if (plane) {   // one block of four waves per pair of groups
-    hipLaunchKernelGGL(net->plane, dim3((unsigned)((a.n_groups + 1) / 2)), dim3(256), net->lds_plane,
-                       (hipStream_t)stream, a);
-    HIP_OK(hipGetLastError());
-    return PBN_OK;
-  }
+  // the pipelined kernel for every network it supports (it beats the one-wave-per-group
+  // rollout at every measured size: profiles/r01_sweep_pbn28_variants_v4.jsonl); networks
+  // with gates (lowered wide functions) run the wave kernel.  PBN_ROLL=lean|pipe forces one.
+  bool pipe = net->lds_pipe <= 64 * 1024 && !net->n_gates;
+  if (net->force_roll) pipe = net->force_roll == 3 && !net->n_gates;
   if (pipe) {   // one block of three waves per pair of groups
     hipLaunchKernelGGL(net->pipe, dim3((unsigned)((a.n_groups + 1) / 2)), dim3(192), net->lds_pipe,
                        (hipStream_t)stream, a);
@@ -2333,7 +1900,7 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
     return PBN_OK;
   }
   const unsigned blocks = (unsigned)((a.n_groups + kWavesPerBlock - 1) / kWavesPerBlock);  // one wave per group
-  hipLaunchKernelGGL(lean ? net->wave_lean : net->wave, dim3(blocks), dim3(64 * kWavesPerBlock), net->lds_wave,
+  hipLaunchKernelGGL(net->wave_lean, dim3(blocks), dim3(64 * kWavesPerBlock), net->lds_wave,
                      (hipStream_t)stream, a);
   HIP_OK(hipGetLastError());
   return PBN_OK;

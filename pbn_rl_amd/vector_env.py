@@ -203,6 +203,19 @@ class VectorPBNEnv:
         k = self.num_envs
         return self.state[:, :k], self.reward[:k], self.flags[:k]
 
+    def rollout_buffers(self, n_steps: int, keep_obs: bool = False, keep_final: bool = True) -> dict:
+        """Output buffers of an ``n_steps`` rollout.  Uninitialised: the kernel writes every
+        element of every buffer it is given (all ``n_alloc`` envs, all steps), and ``rollout``
+        writes the flip masks itself when it does not draw them.  Allocate them before a
+        hipGraph capture so that the graph holds the rollout launch alone."""
+        W, n, dev = self.words, self.n_alloc, self.device
+        return {"_n_steps": n_steps,
+                "flipmask": torch.empty(n_steps, W, n, dtype=torch.int32, device=dev),
+                "reward": torch.empty(n_steps, n, dtype=torch.float32, device=dev),
+                "flags": torch.empty(n_steps, n, dtype=torch.uint8, device=dev),
+                "obs": torch.empty(n_steps, W, n, dtype=torch.int32, device=dev) if keep_obs else None,
+                "final_state": torch.empty(n_steps, W, n, dtype=torch.int32, device=dev) if keep_final else None}
+
     def rollout(self, n_steps: int, flipmasks: Optional[torch.Tensor] = None, random_actions: bool = True,
                 keep_obs: bool = False, keep_final: bool = True, out: Optional[dict] = None) -> dict:
         """``n_steps`` transitions in one ``pbn_rollout`` launch (state kept on chip).
@@ -212,15 +225,9 @@ class VectorPBNEnv:
         ``flipmask`` / ``reward`` / ``flags`` (+ ``obs`` / ``final_state``) shaped
         (n_steps, ...); pass ``out`` (a previous result) to reuse its buffers."""
         L = _lib.load()
-        W, n, k = self.words, self.n_alloc, self.num_envs
-        dev = self.device
+        n, k = self.n_alloc, self.num_envs
         if out is None or out["_n_steps"] != n_steps:
-            out = {"_n_steps": n_steps,
-                   "flipmask": torch.zeros(n_steps, W, n, dtype=torch.int32, device=dev),
-                   "reward": torch.zeros(n_steps, n, dtype=torch.float32, device=dev),
-                   "flags": torch.zeros(n_steps, n, dtype=torch.uint8, device=dev),
-                   "obs": torch.zeros(n_steps, W, n, dtype=torch.int32, device=dev) if keep_obs else None,
-                   "final_state": torch.zeros(n_steps, W, n, dtype=torch.int32, device=dev) if keep_final else None}
+            out = self.rollout_buffers(n_steps, keep_obs, keep_final)
         mode = _lib.MODE_AUTORESET if self.autoreset else 0
         if flipmasks is not None:
             out["flipmask"][:, :, :k].copy_(flipmasks)
@@ -230,7 +237,7 @@ class VectorPBNEnv:
         else:
             out["flipmask"].zero_()
         ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
-        with torch.cuda.device(dev):
+        with torch.cuda.device(self.device):
             _lib.check(L.pbn_rollout(self.net.handle, self.seed, self.step_index, self.env_offset, n, n_steps, mode,
                                      self.state.data_ptr(), out["flipmask"].data_ptr(), self.target.data_ptr(),
                                      self.t.data_ptr(), ptr(out["obs"]), ptr(out["final_state"]),
