@@ -75,6 +75,10 @@ def parse():
     p.add_argument("--horizon", type=int, default=20)
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a hipGraph")
+    p.add_argument("--graph", action="store_true",
+                   help="rollout workload: replay the timed launches as one hipGraph (default: eager launches "
+                        "queued behind the spin gate; a graph replay adds ~8 us of device-side overhead per "
+                        "replay on this stack, profiles/r02_chunk_fit_pbn28_65536.jsonl)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-gather", action="store_true",
                    help="skip the second timed pass (rollouts + one RCCL all_gather of their (s, a, s', r, "
@@ -460,7 +464,10 @@ def main():
             env.step_flipmask(random_actions=True)
 
     plan = launch_plan(args.steps, chunk)
-    use_graph = not args.no_graph
+    # rollouts: eager launches (the gate hides the host's enqueue cost; each launch is 35-160 us
+    # of GPU work, so the host stays ahead); the BDQ frames are launch-bound chains of small
+    # kernels and replay as graphs
+    use_graph = (not args.no_graph) and (args.graph or not rollout_mode)
     if rollout_mode:
         # output buffers of every launch length exist before the capture, so the graph holds
         # the rollout launches alone (no allocation or fill kernels in the timed region)
@@ -498,6 +505,9 @@ def main():
             if time.perf_counter() >= t_end:
                 break
         dev_ms, host_s = timed(run, stream, dev, world, local)
+        # the floor of this timing method: the same gate + event pair around a one-element kernel
+        tiny = torch.zeros(1, device=dev)
+        floor_ms = min(timed(lambda: tiny.add_(1.0), stream, dev, world, local)[0] for _ in range(5))
     elapsed = dev_ms * 1e-3
     total_env_steps = world * args.envs * args.steps
     value = total_env_steps / elapsed
@@ -601,8 +611,11 @@ def main():
                        "parallelism": f"env-shard x{world} (RCCL process group)",
                        "launch": "hipGraph" if (use_graph or args.learn_graph) else "eager"},
             "roofline": roofline,
-            "timing": {"clock": "HIP events on the launch stream, max over ranks",
-                       "host_ms_per_step": host_s * 1e3 / args.steps, "clock_warm_replays": warm_reps},
+            "timing": {"clock": "HIP events on the launch stream behind a spin gate, max over ranks",
+                       "event_floor_us": floor_ms * 1e3,
+                       "note": "event_floor_us: the same gate + event pair around a one-element kernel (dispatch "
+                               "and event overhead, part of every timed region)",
+                       "host_ms_per_step": host_s * 1e3 / args.steps, "clock_warm_runs": warm_reps},
         }
         if with_gather is not None:
             out["value_with_gather"] = with_gather["value"]

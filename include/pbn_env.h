@@ -233,13 +233,14 @@ int pbn_bilinear_targets(const pbn_net* net, int64_t n_envs, const uint32_t* d_s
  *   d_q         in   float [n][n_branches][n_actions], n_actions == n_nodes + 1, 16-byte aligned
  *   epsilon     explore with probability epsilon: env e explores iff EXPLORE word 0 <
  *               floor(epsilon * 2^32); its branch k action is then
- *               ((word (1 + k/3) >> 10(k%3)) & 1023) * (N+1) >> 10  (uniform over [0, N],
- *               as np.random.randint at :76); otherwise argmax over the branch (first
+ *               (word (k + 1) * (N+1)) >> 32, words numbered across EXPLORE calls 0, 1
+ *               (uniform over [0, N] to (N+1)/2^32, as np.random.randint at :76);
+ *               otherwise argmax over the branch (first
  *               maximum, NaN counts as the maximum: torch.argmax at :96).  EXPLORE = Philox
  *               stream 4 keyed by (seed, global env id, step), as in DESIGN.md.
  *   d_flipmask  out  uint32 [W][n]: bit a-1 set for every distinct action a > 0
  *   d_actions   out  int32 [n][n_branches] (nullable): the chosen actions
- * n_branches 1..9.  n_envs and env_offset multiples of 32.
+ * n_branches 1..7.  n_envs and env_offset multiples of 32.
  */
 int pbn_q_to_flipmask(const pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs,
                       int32_t n_branches, int32_t n_actions, const float* d_q, float epsilon,

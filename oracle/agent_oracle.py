@@ -4,7 +4,8 @@ TEST INFRASTRUCTURE ONLY: imported by tests/ as the checker of
 pbn_rl_amd/csrc/pbn_agent.hip.  Follows the frame loop of the reference:
   - observation = np.stack((state, target)) as float (bdq_model/__init__.py:92-93), batched
     to (2, n, N); target = the first state of the env's target attractor;
-  - epsilon-greedy: explore -> uniform ints in [0, N] per branch (:74-76), else
+  - epsilon-greedy: explore (EXPLORE word 0 < floor(eps * 2^32)) -> uniform ints in [0, N] per
+    branch, branch k from EXPLORE word k + 1 by a 32-bit multiply-high (:74-76), else
     argmax of each branch's Q row (:95-96, torch.argmax: first maximum, NaN is the maximum);
   - env actions: list(action.unique()) (:176), a > 0 flips node a-1 (:81-84).
 The explore draws follow DESIGN.md (Philox4x32-10, stream EXPLORE = 4); Philox is vectorised
@@ -34,13 +35,17 @@ def philox_vec(c0, c1, c2, c3, k0: int, k1: int):
     return [c.astype(np.uint32) for c in (c0, c1, c2, c3)]
 
 
-def explore_words(seed: int, step: int, env_offset: int, n: int):
+def explore_words(seed: int, step: int, env_offset: int, n: int, calls: int = 1):
+    """EXPLORE-stream words of every env: word j = call j >> 2, word j & 3 (4 * calls words)."""
     ge = np.arange(n, dtype=np.uint64) + np.uint64(env_offset)
     c0 = ge & np.uint64(0xFFFFFFFF)
     c1 = np.full(n, step & 0xFFFFFFFF, dtype=np.uint64)
-    c2 = np.full(n, EXPLORE << 28, dtype=np.uint64)
     c3 = ((ge >> np.uint64(32)) & np.uint64(0xFFFF)) | np.uint64(((step >> 32) & 0xFFFF) << 16)
-    return philox_vec(c0, c1, c2, c3, seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+    out = []
+    for c in range(calls):
+        c2 = np.full(n, (EXPLORE << 28) | c, dtype=np.uint64)
+        out += philox_vec(c0, c1, c2, c3, seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+    return out
 
 
 def obs_unpack(spec, state: np.ndarray, target: np.ndarray) -> np.ndarray:
@@ -71,14 +76,13 @@ def q_to_flipmask(spec, q: np.ndarray, seed: int, step: int, env_offset: int, ep
     n, K, A = q.shape
     N, W = spec.n, spec.words
     assert A == N + 1
-    w = explore_words(seed, step, env_offset, n)
+    w = explore_words(seed, step, env_offset, n, calls=(K + 1 + 3) // 4)
     eps_u = int(np.floor(np.float64(np.float32(epsilon)) * 4294967296.0))
     explore = w[0].astype(np.uint64) < np.uint64(eps_u) if eps_u < (1 << 32) else np.ones(n, dtype=bool)
     greedy = argmax_torch(q)                                                     # (n, K)
     rnd = np.zeros((n, K), dtype=np.int64)
-    for k in range(K):
-        word = w[1 + k // 3].astype(np.uint64)
-        rnd[:, k] = (((word >> np.uint64(10 * (k % 3))) & np.uint64(1023)) * np.uint64(N + 1)) >> np.uint64(10)
+    for k in range(K):   # branch k: explore word k + 1, multiply-high onto [0, N] (bias <= (N+1) / 2^32)
+        rnd[:, k] = (w[1 + k].astype(np.uint64) * np.uint64(N + 1)) >> np.uint64(32)
     actions = np.where(explore[:, None], rnd, greedy).astype(np.int32)
     flip = np.zeros((W, n), dtype=np.uint32)
     for k in range(K):

@@ -29,6 +29,15 @@ def _draw(seed: int, ident: np.ndarray, step: int, stream: int, idx) -> list:
     return philox_vec(c0, c1, c2, c3, seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
 
 
+def ext64(hi: np.ndarray, lo: np.ndarray, k):
+    """Bounded draws from 64-bit uniforms (hi:lo) (pyoracle.ext64, batched): returns
+    (floor(x * k / 2^64), hi', lo') with x' = x * k mod 2^64; k < 2^32 scalar or per env."""
+    k = np.asarray(k, dtype=np.uint64)
+    a = lo.astype(np.uint64) * k                          # < 2^64
+    b = hi.astype(np.uint64) * k + (a >> np.uint64(32))   # < 2^64
+    return (b >> np.uint64(32)).astype(np.int64), (b & _U32).astype(np.uint32), (a & _U32).astype(np.uint32)
+
+
 class NpPBN:
     """Batched env semantics over an EnvSpec (network + attractors + constants)."""
 
@@ -112,21 +121,22 @@ class NpPBN:
     def _bit(self, words: np.ndarray, i: int) -> np.ndarray:
         return (words[i >> 5] >> np.uint32(i & 31)) & np.uint32(1)
 
-    def reset_from_word(self, seed: int, e: np.ndarray, step: int, R: np.ndarray):
-        """(state words (W, n), target ids (n,)) for reset word R per env (pyoracle.reset_from_word)."""
-        R = R.astype(np.int64)
+    def reset_from_words(self, seed: int, e: np.ndarray, step: int, hi: np.ndarray, lo: np.ndarray):
+        """(state words (W, n), target ids (n,)) from the 64-bit uniform (hi:lo) per env
+        (pyoracle.reset_from_words)."""
         n = len(e)
         A = self.A
         if A >= 1:
-            a_s = ((R & 1023) * A) >> 10
+            a_s = np.zeros(n, dtype=np.int64)
+            a_t = np.zeros(n, dtype=np.int64)
+            if A >= 2:
+                c, hi, lo = ext64(hi, lo, A * (A - 1))
+                a_s, a_t = c // (A - 1), c % (A - 1)
+                a_t += (a_t >= a_s)
             size = np.asarray(self.att_len, dtype=np.int64)[a_s]
-            idx = (((R >> 20) & 4095) * size) >> 12
+            idx, hi, lo = ext64(hi, lo, size)
             rows = np.asarray(self.att_first, dtype=np.int64)[a_s] + idx
             state = self.att_words[rows].T.copy()
-            a_t = a_s.copy()
-            if A >= 2:
-                a_t = (((R >> 10) & 1023) * (A - 1)) >> 10
-                a_t += (a_t >= a_s)
             return state, a_t.astype(np.uint8)
         r = _draw(seed, e, step, RESET, 1)
         state = np.zeros((self.W, n), dtype=np.uint32)
@@ -137,8 +147,8 @@ class NpPBN:
 
     def reset(self, seed: int, step: int, env_offset: int, n: int):
         e = np.arange(n, dtype=np.uint64) + np.uint64(env_offset)
-        R = _draw(seed, e, step, RESET, 0)[0]
-        state, tgt = self.reset_from_word(seed, e, step, R)
+        R = _draw(seed, e, step, RESET, 0)
+        state, tgt = self.reset_from_words(seed, e, step, R[1], R[0])
         return state, tgt, np.zeros(n, dtype=np.uint8)
 
     def step(self, seed: int, step: int, env_offset: int, state, flipmask, target, t, mode: int) -> dict:
@@ -147,30 +157,30 @@ class NpPBN:
         n = state.shape[1]
         e = np.arange(n, dtype=np.uint64) + np.uint64(env_offset)
         E = _draw(seed, e, step, ENV, 0)
+        F = _draw(seed, e, step, ENV, 1)
         if mode & MODE_RANDOM_ACTIONS:
             flip = np.zeros((W, n), dtype=np.uint32)
+            c, _, _ = ext64(E[3], E[2], (n_nodes + 1) ** 3)
             for k in range(3):
-                a = (((E[3] >> np.uint32(10 * k)) & np.uint32(1023)).astype(np.int64) * (n_nodes + 1)) >> 10
+                c, a = c // (n_nodes + 1), c % (n_nodes + 1)
                 for w in range(W):
                     sel = (a > 0) & (((a - 1) >> 5) == w)
                     flip[w, sel] |= (np.uint32(1) << ((a[sel] - 1) & 31).astype(np.uint32))
         else:
             flip = np.asarray(flipmask, dtype=np.uint32).copy()
         s1 = state ^ flip
-        # perturbation: geometric gaps from ENV words 0, 1 then PERT calls
+        # perturbation: geometric gaps from ENV words 0, 1 of calls 0, 1, then PERT calls
         gamma = np.zeros((W, n), dtype=np.uint32)
         pos = np.full(n, -1, dtype=np.int64)
         live = np.ones(n, dtype=bool)
         k, P = 0, None
         while live.any():
-            if k == 0:
-                u = E[0]
-            elif k == 1:
-                u = E[1]
+            if k < 4:
+                u = (F if k >= 2 else E)[k & 1]
             else:
-                if (k - 2) % 4 == 0:
-                    P = _draw(seed, e, step, PERT, (k - 2) // 4)
-                u = P[(k - 2) % 4]
+                if (k - 4) % 4 == 0:
+                    P = _draw(seed, e, step, PERT, (k - 4) // 4)
+                u = P[(k - 4) % 4]
             k += 1
             gap = np.searchsorted(self.cdf, u.astype(np.uint64), side="right") + 1
             pos = np.where(live, pos + gap, pos)
@@ -233,7 +243,7 @@ class NpPBN:
         if mode & MODE_AUTORESET:
             done = term | trunc
             if done.any():
-                ns, ntg = self.reset_from_word(seed, e[done], step, E[2][done])
+                ns, ntg = self.reset_from_words(seed, e[done], step, F[3][done], F[2][done])
                 state_out[:, done] = ns
                 tgt[done] = ntg
                 t_out[done] = 0

@@ -116,23 +116,37 @@ static void valid_mask(int n, int W, uint32_t* m) {
   }
 }
 
-/* reset formula shared by pbn_reset (word from STREAM_RESET call 0) and autoreset (E2) */
-static void reset_one(const pbn_net_desc* d, uint64_t seed, uint64_t e, uint64_t step, uint32_t R,
+/* one bounded draw from a 64-bit uniform X = (hi:lo), keeping the rest of X for the next:
+ * v = floor(X * K / 2^64) in [0, K), X <- X * K mod 2^64 (multiply-shift "batched dice rolls",
+ * Brackett-Rozinsky & Lemire 2024, without rejection): bias <= K / 2^64 per draw */
+static uint32_t ext64(uint32_t* hi, uint32_t* lo, uint32_t K) {
+  uint64_t a = (uint64_t)(*lo) * K;
+  uint64_t b = (uint64_t)(*hi) * K + (a >> 32);
+  *lo = (uint32_t)a;
+  *hi = (uint32_t)b;
+  return (uint32_t)(b >> 32);
+}
+
+/* reset formula shared by pbn_reset (RESET call 0, words 1:0) and autoreset (ENV call 1,
+ * words 3:2): start attractor a_s and target a_t != a_s in one draw over A(A-1) pairs, then
+ * the start state uniformly within a_s */
+static void reset_one(const pbn_net_desc* d, uint64_t seed, uint64_t e, uint64_t step, uint32_t hi, uint32_t lo,
                       uint32_t* state, uint8_t* target) {
   int N = d->n_nodes, W = words_of(N), A = d->n_attractors;
   uint32_t vm[4];
   valid_mask(N, W, vm);
   if (A >= 1) {
-    uint32_t as = (uint32_t)(((uint64_t)(R & 1023u) * (uint32_t)A) >> 10);
-    int start = d->attractor_start[as];
-    uint32_t size = (uint32_t)(d->attractor_start[as + 1] - start);
-    uint32_t idx = (uint32_t)(((uint64_t)((R >> 20) & 4095u) * size) >> 12);
-    for (int w = 0; w < W; ++w) state[w] = d->attractor_states[(size_t)(start + idx) * W + w];
-    uint32_t at = as;
+    uint32_t as = 0, at = 0;
     if (A >= 2) {
-      at = (uint32_t)(((uint64_t)((R >> 10) & 1023u) * (uint32_t)(A - 1)) >> 10);
+      uint32_t c = ext64(&hi, &lo, (uint32_t)A * (uint32_t)(A - 1));
+      as = c / (uint32_t)(A - 1);
+      at = c % (uint32_t)(A - 1);
       at += (at >= as);
     }
+    int start = d->attractor_start[as];
+    uint32_t size = (uint32_t)(d->attractor_start[as + 1] - start);
+    uint32_t idx = ext64(&hi, &lo, size);
+    for (int w = 0; w < W; ++w) state[w] = d->attractor_states[(size_t)(start + idx) * W + w];
     *target = (uint8_t)at;
   } else {
     uint32_t r[4];
@@ -149,7 +163,7 @@ int oracle_reset(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t e
     uint64_t e = env_offset + (uint64_t)i;
     uint32_t r[4], s[4];
     draw(seed, e, step, STREAM_RESET, 0, r);
-    reset_one(d, seed, e, step, r[0], s, &target[i]);
+    reset_one(d, seed, e, step, r[1], r[0], s, &target[i]);
     for (int w = 0; w < W; ++w) state[(size_t)w * n + i] = s[w];
     t[i] = 0;
   }
@@ -182,14 +196,20 @@ int oracle_step(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t en
       uint32_t vm[4], s[4] = {0, 0, 0, 0}, m[4] = {0, 0, 0, 0}, s1[4], gam[4] = {0, 0, 0, 0},
                sp[4] = {0, 0, 0, 0};
       valid_mask(N, W, vm);
-      uint32_t E[4];
+      uint32_t E[4], F[4];
       draw(seed, e, step, STREAM_ENV, 0, E);
+      draw(seed, e, step, STREAM_ENV, 1, F);
       for (int w = 0; w < W; ++w) s[w] = state[(size_t)w * n + li] & vm[w];
       /* 1-2. interventions: 0 = no-op, a > 0 flips node a-1, each distinct node once
        *      (bdq_model/__init__.py:76-84 explore branch, :176 action.unique()) */
       if (mode & PBN_MODE_RANDOM_ACTIONS) {
+        /* three actions uniform on [0, N] (np.random.randint(0, N+1, 3), bdq_model/__init__.py:76):
+         * the base-(N+1) digits of one draw over (N+1)^3 from ENV words 3:2 */
+        uint32_t hi = E[3], lo = E[2], n1 = (uint32_t)(N + 1);
+        uint32_t c = ext64(&hi, &lo, n1 * n1 * n1);
         for (int k = 0; k < 3; ++k) {
-          uint32_t a = (uint32_t)(((uint64_t)((E[3] >> (10 * k)) & 1023u) * (uint32_t)(N + 1)) >> 10);
+          uint32_t a = c % n1;
+          c /= n1;
           if (a > 0) m[(a - 1) >> 5] |= 1u << ((a - 1) & 31);
         }
         for (int w = 0; w < W; ++w) flipmask[(size_t)w * n + li] = m[w];
@@ -197,17 +217,17 @@ int oracle_step(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t en
         for (int w = 0; w < W; ++w) m[w] = flipmask[(size_t)w * n + li] & vm[w];
       }
       for (int w = 0; w < W; ++w) s1[w] = s[w] ^ m[w];
-      /* 3. perturbation: gaps between flipped nodes are geometric(p) draws */
+      /* 3. perturbation: gaps between flipped nodes are geometric(p) draws; gaps 0-3 are
+       *    ENV words 0, 1 of calls 0, 1; gap k >= 4 is PERT call (k-4)>>2, word (k-4)&3 */
       {
         int pos = -1, k = 0;
         uint32_t P[4];
         while (pos < N - 1) {
           uint32_t u;
-          if (k == 0) u = E[0];
-          else if (k == 1) u = E[1];
+          if (k < 4) u = (k & 2) ? F[k & 1] : E[k & 1];
           else {
-            if (((k - 2) & 3) == 0) draw(seed, e, step, STREAM_PERT, (uint32_t)((k - 2) >> 2), P);
-            u = P[(k - 2) & 3];
+            if (((k - 4) & 3) == 0) draw(seed, e, step, STREAM_PERT, (uint32_t)((k - 4) >> 2), P);
+            u = P[(k - 4) & 3];
           }
           ++k;
           pos += gap_of(d, u);
@@ -254,7 +274,7 @@ int oracle_step(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t en
       if ((mode & PBN_MODE_AUTORESET) && (term || trunc)) {
         uint32_t ns[4];
         uint8_t tg;
-        reset_one(d, seed, e, step, E[2], ns, &tg);
+        reset_one(d, seed, e, step, F[3], F[2], ns, &tg);
         for (int w = 0; w < W; ++w) state_out[(size_t)w * n + li] = ns[w];
         target[li] = tg;
         t[li] = 0;

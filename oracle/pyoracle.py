@@ -37,6 +37,12 @@ def draw(seed: int, ident: int, step: int, stream: int, idx: int):
     return philox4x32_10(ctr, (seed & MASK32, (seed >> 32) & MASK32))
 
 
+def ext64(x: int, k: int) -> Tuple[int, int]:
+    """One bounded draw from the 64-bit uniform x: (floor(x * k / 2^64), x * k mod 2^64)."""
+    prod = x * k
+    return prod >> 64, prod & ((1 << 64) - 1)
+
+
 class PyPBN:
     """Scalar env semantics over an EnvSpec (network + attractors + constants)."""
 
@@ -57,25 +63,27 @@ class PyPBN:
                 return m
         return self.n + 1
 
-    def reset_from_word(self, seed: int, e: int, step: int, R: int):
+    def reset_from_words(self, seed: int, e: int, step: int, hi: int, lo: int):
+        """(start state, target id) from the 64-bit uniform (hi:lo): one draw over the A(A-1)
+        ordered (start, target) pairs, then the state uniformly within the start attractor."""
         A = len(self.spec.attractors)
         if A >= 1:
-            a_s = ((R & 1023) * A) >> 10
-            att = self.spec.attractors[a_s]
-            idx = (((R >> 20) & 4095) * len(att)) >> 12
-            state = list(att[idx])
-            a_t = a_s
+            x = (hi << 32) | lo
+            a_s = a_t = 0
             if A >= 2:
-                a_t = (((R >> 10) & 1023) * (A - 1)) >> 10
+                c, x = ext64(x, A * (A - 1))
+                a_s, a_t = divmod(c, A - 1)
                 a_t += a_t >= a_s
-            return state, a_t
+            att = self.spec.attractors[a_s]
+            idx, x = ext64(x, len(att))
+            return list(att[idx]), a_t
         r = draw(seed, e, step, RESET, 1)
         bits = [(r[i >> 5] >> (i & 31)) & 1 for i in range(self.n)]
         return bits, 0xFF
 
     def reset(self, seed: int, step: int, e: int):
-        R = draw(seed, e, step, RESET, 0)[0]
-        state, tgt = self.reset_from_word(seed, e, step, R)
+        R = draw(seed, e, step, RESET, 0)
+        state, tgt = self.reset_from_words(seed, e, step, R[1], R[0])
         return state, tgt, 0
 
     def step(self, seed: int, step: int, e: int, state: List[int], flip: List[int], target: int, t: int,
@@ -83,24 +91,24 @@ class PyPBN:
         n, B = self.n, self.spec.prob_bits
         G, b = e >> 5, e & 31
         E = draw(seed, e, step, ENV, 0)
+        F = draw(seed, e, step, ENV, 1)
         if mode & MODE_RANDOM_ACTIONS:
             flip = [0] * n
+            c, _ = ext64((E[3] << 32) | E[2], (n + 1) ** 3)   # 3 uniform ints in [0, N] (:76)
             for k in range(3):
-                a = (((E[3] >> (10 * k)) & 1023) * (n + 1)) >> 10
+                c, a = divmod(c, n + 1)
                 if a > 0:
                     flip[a - 1] = 1  # each distinct node once (bdq_model/__init__.py:81-84,176)
         s1 = [state[i] ^ flip[i] for i in range(n)]
         gamma = [0] * n
         pos, k, P = -1, 0, None
         while pos < n - 1:
-            if k == 0:
-                u = E[0]
-            elif k == 1:
-                u = E[1]
+            if k < 4:
+                u = (F if k >= 2 else E)[k & 1]
             else:
-                if (k - 2) % 4 == 0:
-                    P = draw(seed, e, step, PERT, (k - 2) // 4)
-                u = P[(k - 2) % 4]
+                if (k - 4) % 4 == 0:
+                    P = draw(seed, e, step, PERT, (k - 4) // 4)
+                u = P[(k - 4) % 4]
             k += 1
             pos += self.gap(u)
             if pos >= n:
@@ -133,7 +141,7 @@ class PyPBN:
         flags = int(term) | (int(trunc) << 1) | (int(in_attr) << 2) | (int(perturbed) << 3)
         out = {"final_state": sp, "reward": reward, "flipmask": flip, "target": target}
         if (mode & MODE_AUTORESET) and (term or trunc):
-            ns, tg = self.reset_from_word(seed, e, step, E[2])
+            ns, tg = self.reset_from_words(seed, e, step, F[3], F[2])
             out.update(state_out=ns, target=tg, t=0, flags=flags | 16)
         else:
             out.update(state_out=sp, t=tt, flags=flags)

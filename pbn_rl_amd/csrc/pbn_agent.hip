@@ -27,7 +27,7 @@ namespace {
 
 constexpr int kObsThreads = 256;
 constexpr int kQEnvs = 64;          // envs per q_to_flipmask block (one wave, one env per lane)
-constexpr int kMaxBranches = 9;     // random actions: 3 x 10 bits in each of EXPLORE words 1..3
+constexpr int kMaxBranches = 7;     // random actions: branch k from EXPLORE word k + 1 (two calls)
 
 // out[p][e][i], p = 0: bit i of env e's state, p = 1: bit i of the first state of env e's
 // target attractor (all zeros without a target).  Four consecutive (e, i) elements per
@@ -186,16 +186,23 @@ __global__ void __launch_bounds__(kQEnvs * kMaxBranches) q_to_flipmask_kernel(
   if (t < n_blk) {
     const int64_t e = e0 + t;
     const uint64_t ge = env_offset + (uint64_t)e;
-    const pbn::Word4 r = pbn::draw(seed, ge, d_step ? *d_step : step, pbn::kStreamExplore, 0);
+    const uint64_t st = d_step ? *d_step : step;
+    const pbn::Word4 r = pbn::draw(seed, ge, st, pbn::kStreamExplore, 0);
     if (d_eps) {   // device epsilon (graph replays): clamped to [0, 1], NaN -> 0
       const float ef = fminf(fmaxf(*d_eps, 0.f), 1.f);
       eps_u = (uint64_t)floor((double)ef * 4294967296.0);
     }
     const bool explore = (uint64_t)r.x < eps_u;
-    const uint32_t rw = k < 3 ? r.y : (k < 6 ? r.z : r.w);
     int a;
     if (explore) {
-      a = (int)((((rw >> (10 * (k % 3))) & 1023u) * (uint32_t)(N + 1)) >> 10);
+      // branch k: EXPLORE word k + 1 (call (k + 1) >> 2), multiply-high onto [0, N]:
+      // bias <= (N + 1) / 2^32 against np.random.randint (bdq_model/__init__.py:76)
+      uint32_t rw = k == 0 ? r.y : (k == 1 ? r.z : r.w);
+      if (k >= 3) {
+        const pbn::Word4 r1 = pbn::draw(seed, ge, st, pbn::kStreamExplore, 1);
+        rw = k == 3 ? r1.x : (k == 4 ? r1.y : (k == 5 ? r1.z : r1.w));
+      }
+      a = (int)__umulhi(rw, (uint32_t)(N + 1));
     } else if (!heads) {
       a = argmax_row(sq + (size_t)t * row + k * A, A);
     } else {
@@ -303,7 +310,7 @@ static int q_to_flipmask_impl(const pbn_net* net, uint64_t seed, uint64_t step, 
   if ((rc = pbn::check_device(net))) return rc;
   if (n_envs < 0 || (n_envs & 31) || (env_offset & 31))
     return pbn::set_error(PBN_EINVAL, "n_envs and env_offset must be multiples of 32");
-  if (n_branches < 1 || n_branches > kMaxBranches) return pbn::set_error(PBN_EINVAL, "n_branches must be 1..9");
+  if (n_branches < 1 || n_branches > kMaxBranches) return pbn::set_error(PBN_EINVAL, "n_branches must be 1..7");
   if (n_actions != v.n_nodes + 1) return pbn::set_error(PBN_EINVAL, "n_actions must be n_nodes + 1");
   if (!(epsilon >= 0.f && epsilon <= 1.f)) return pbn::set_error(PBN_EINVAL, "epsilon must be in [0, 1]");
   if (n_envs == 0) return PBN_OK;

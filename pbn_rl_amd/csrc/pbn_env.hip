@@ -101,6 +101,8 @@ struct StepArgs {
   int gate_off;      // wave kernel: LDS image offset of the gate records, uint4 [n_gates] by level
   int glayer_off;    // LDS image offset of the level starts, int32 [n_glayers + 1]
   int n_glayers;     // 0: no gates
+  uint32_t n1_magic; // ceil(2^32 / (N + 1)): random-action digits
+  uint32_t am1_magic;  // ceil(2^32 / (A - 1)) for A >= 2: autoreset (start, target) split
 };
 
 // In-kernel phase clocks (cdna_hip_programming.md section 7, "In-kernel stamps"):
@@ -161,6 +163,35 @@ __device__ __noinline__ size_t pbn_ck(size_t i, size_t len, int site) {
 __device__ __forceinline__ uint32_t valid_word_mask(int n, int w) {
   const int bits = n - 32 * w;
   return bits >= 32 ? 0xFFFFFFFFu : (bits <= 0 ? 0u : ((1u << bits) - 1u));
+}
+
+// One bounded draw from the 64-bit uniform X = (hi:lo), keeping the rest of X: v =
+// floor(X * K / 2^64) in [0, K), X <- X * K mod 2^64 (two v_mad_u64_u32; bias <= K / 2^64;
+// oracle/pbn_oracle.c ext64).
+__device__ __forceinline__ uint32_t ext64(uint32_t& hi, uint32_t& lo, uint32_t K) {
+  const uint64_t x = (uint64_t)lo * K;
+  const uint64_t y = (uint64_t)hi * K + (x >> 32);
+  lo = (uint32_t)x;
+  hi = (uint32_t)y;
+  return (uint32_t)(y >> 32);
+}
+
+// Three actions uniform on [0, N]: the base-(N+1) digits of one draw over (N+1)^3 from the
+// 64-bit value (hi:lo).  Division by N+1 is a multiply-high by magic = ceil(2^32 / (N+1)),
+// exact for c * (N+1) < 2^32 (c < (N+1)^3 <= 129^3).
+template <int W>
+__device__ __forceinline__ void random_actions3(uint32_t hi, uint32_t lo, int N, uint32_t magic, uint32_t (&m)[W]) {
+  const uint32_t n1 = (uint32_t)(N + 1);
+  uint32_t c = ext64(hi, lo, n1 * n1 * n1);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {   // action a in [0, N]: 0 = no-op, else flip node a-1
+    const uint32_t qt = __umulhi(c, magic);
+    const int act = (int)(c - qt * n1);
+    c = qt;
+#pragma unroll
+    for (int w = 0; w < W; ++w)
+      if (act > 0 && ((act - 1) >> 5) == w) m[w] |= 1u << ((act - 1) & 31);
+  }
 }
 
 // gap(u) = min{m in 1..N : u < C[m-1]} (N+1 or more if none); C padded with 0xFFFFFFFF.
@@ -358,7 +389,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   constexpr int CPN = B / 4;               // selection calls per node
   constexpr int H = (CPN + 1) / 2;         // of which the lower half computes H
   constexpr int NLO = 1 + W * H;           // lower list: ENV, SEL(c < H)
-  constexpr int NUP = W * (CPN - H) + 1;   // upper list: SEL(c >= H), PERT call 0
+  constexpr int NUP = W * (CPN - H) + 1;   // upper list: SEL(c >= H), ENV call 1
   constexpr int IT = NLO > NUP ? NLO : NUP;
   constexpr int UPC = (CPN - H) > 0 ? (CPN - H) : 1;  // divisor guard (B = 4: no upper calls)
   extern __shared__ uint32_t smem[];
@@ -466,7 +497,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
       const int c = H + it % UPC;
       uc0 = G_lo; uc2 = (pbn::kStreamSel << 28) | (uint32_t)(4 * (l32 + 32 * r) + c); uc3 = G_hi;
     } else {
-      uc0 = ge_lo; uc2 = pbn::kStreamPert << 28; uc3 = ge_hi;
+      uc0 = ge_lo; uc2 = (pbn::kStreamEnv << 28) | 1u; uc3 = ge_hi;
     }
     out[it] = pbn::philox4x32_10(lo ? lc0 : uc0, st_lo, lo ? lc2 : uc2, lo ? lc3 : uc3, kk0, kk1);
   }
@@ -481,7 +512,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
       dig[r][4 * c + 0] = d.x; dig[r][4 * c + 1] = d.y; dig[r][4 * c + 2] = d.z; dig[r][4 * c + 3] = d.w;
     }
   }
-  const Word4 P4 = upper_to_lower(out[W * (CPN - H)]);   // PERT call 0 of env l32
+  const Word4 F = upper_to_lower(out[W * (CPN - H)]);   // ENV call 1 of env l32
   const Word4 E = out[0];
 
   // ---- 2. per env (lower lanes): interventions, perturbation, reset word
@@ -493,11 +524,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   for (int w = 0; w < W; ++w) gam[w] = 0;
   if (lo) {
     if (random_actions) {
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {   // action a in [0, N]: 0 = no-op, else flip node a-1
-        const int act = (int)(__umul24((E.w >> (10 * q)) & 1023u, (uint32_t)(N + 1)) >> 10);
-        set_bit<W>(m, act - 1, N);
-      }
+      random_actions3<W>(E.w, E.z, N, a.n1_magic, m);
 #pragma unroll
       for (int w = 0; w < W; ++w) a.flipmask[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 8)] = m[w];
     } else {
@@ -511,27 +538,30 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
       s1[w] ^= m[w];
     }
     // perturbation positions are prefix sums of geometric gaps; the first three gaps
-    // (u = E.x, E.y, PERT word 0) are independent, so they are computed side by side
+    // (u = E.x, E.y, F.x) are independent, so they are computed side by side
     int g0, g1, g2;
     if (a.gap_exact) {
-      g0 = gap_of(cdf, a.cdf_len, E.x); g1 = gap_of(cdf, a.cdf_len, E.y); g2 = gap_of(cdf, a.cdf_len, P4.x);
+      g0 = gap_of(cdf, a.cdf_len, E.x); g1 = gap_of(cdf, a.cdf_len, E.y); g2 = gap_of(cdf, a.cdf_len, F.x);
     } else {
       g0 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.x);
       g1 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.y);
-      g2 = gap_est(cdf, a.cdf_len, a.inv_log2q, P4.x);
+      g2 = gap_est(cdf, a.cdf_len, a.inv_log2q, F.x);
     }
     const int p0 = g0 - 1, p1 = p0 + g1, p2 = p1 + g2;
     set_bit<W>(gam, p0, N);
     set_bit<W>(gam, p1, N);
     set_bit<W>(gam, p2, N);
-    if (p2 < N - 1) {   // rare: a fourth flip is possible (gap k >= 3: PERT call (k-2)>>2, word (k-2)&3)
-      Word4 P = P4;
+    if (p2 < N - 1) {   // rare: a fourth flip is possible (gap 3 = F.y, gap k >= 4: PERT call (k-4)>>2, word (k-4)&3)
+      Word4 P = F;
       int pos = p2;
       for (int kk = 3; pos < N - 1; ++kk) {
-        if ((kk & 3) == 2)
-          P = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamPert << 28) | (uint32_t)((kk - 2) >> 2), ge_hi, kk0, kk1);
-        const int j4 = (kk - 2) & 3;
-        const uint32_t u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
+        uint32_t u = F.y;
+        if (kk >= 4) {
+          if (((kk - 4) & 3) == 0)
+            P = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamPert << 28) | (uint32_t)((kk - 4) >> 2), ge_hi, kk0, kk1);
+          const int j4 = (kk - 4) & 3;
+          u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
+        }
         pos += a.gap_exact ? gap_of(cdf, a.cdf_len, u) : gap_est(cdf, a.cdf_len, a.inv_log2q, u);
         set_bit<W>(gam, pos, N);
       }
@@ -660,24 +690,26 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   a.reward[CK(ks * n + le, n_steps * n, 11)] = rtab[(2 * (int)term + (int)wrong) * (N + 1) + (int)pc];
   uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) | ((uint32_t)pert << 3);
   if ((a.mode & PBN_MODE_AUTORESET) && (term || trunc)) {
-    const uint32_t Rw = E.z;
     uint32_t nt;
     if (a.n_attr >= 1) {
-      // attractor tables from the LDS image: start[A+1] then states[S][W]
+      // attractor tables from the LDS image: start[A+1] then states[S][W]; (start, target)
+      // in one draw over the A(A-1) pairs, then the state within the start attractor
       const int32_t* att_first = reinterpret_cast<const int32_t*>(L + a.att_off);
       const uint32_t* att_words = L + a.att_off + a.n_attr + 1;
       const uint32_t A = (uint32_t)a.n_attr;
-      const uint32_t as = ((Rw & 1023u) * A) >> 10;
-      const int st0 = att_first[as];
-      const uint32_t size = (uint32_t)(att_first[as + 1] - st0);
-      const uint32_t idx = (((Rw >> 20) & 4095u) * size) >> 12;
-#pragma unroll
-      for (int w = 0; w < W; ++w) sp[w] = att_words[(size_t)(st0 + idx) * W + w];
-      nt = as;
+      uint32_t hi = F.w, lo = F.z, as = 0;
+      nt = 0;
       if (A >= 2) {
-        nt = (((Rw >> 10) & 1023u) * (A - 1)) >> 10;
+        const uint32_t c = ext64(hi, lo, A * (A - 1));
+        as = a.am1_magic ? __umulhi(c, a.am1_magic) : c;   // c / (A - 1)
+        nt = c - as * (A - 1);
         nt += (nt >= as) ? 1u : 0u;
       }
+      const int st0 = att_first[as];
+      const uint32_t size = (uint32_t)(att_first[as + 1] - st0);
+      const uint32_t idx = ext64(hi, lo, size);
+#pragma unroll
+      for (int w = 0; w < W; ++w) sp[w] = att_words[(size_t)(st0 + idx) * W + w];
     } else {
       const Word4 rr = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamReset << 28) | 1u, ge_hi, kk0, kk1);
       const uint32_t rw4[4] = {rr.x, rr.y, rr.z, rr.w};
@@ -857,16 +889,12 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
       const uint32_t ge_lo = (uint32_t)ge;
       if (valid) {
         const Word4 E = pbn::philox4x32_10(ge_lo, st_lo, pbn::kStreamEnv << 28, ge_hi, u_k0, u_k1);
-        const Word4 P4 = pbn::philox4x32_10(ge_lo, st_lo, pbn::kStreamPert << 28, ge_hi, u_k0, u_k1);
+        const Word4 F = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamEnv << 28) | 1u, ge_hi, u_k0, u_k1);
         uint32_t m[W], gam[W], rs[W];
 #pragma unroll
         for (int w = 0; w < W; ++w) { m[w] = 0; gam[w] = 0; rs[w] = 0; }
         if (u_fl & 4u) {
-#pragma unroll
-          for (int q = 0; q < 3; ++q) {   // action a in [0, N]: 0 = no-op, else flip node a-1
-            const int act = (int)(__umul24((E.w >> (10 * q)) & 1023u, (uint32_t)(N + 1)) >> 10);
-            set_bit<W>(m, act - 1, N);
-          }
+          random_actions3<W>(E.w, E.z, N, a.n1_magic, m);
 #pragma unroll
           for (int w = 0; w < W; ++w) a.flipmask[CK(k * plane + (size_t)w * n + le, (size_t)n_steps * plane, 8)] = m[w];
         } else {
@@ -879,24 +907,27 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
         for (int w = 0; w < W; ++w) pc += __builtin_popcount(m[w]);
         int g0, g1, g2;
         if (u_gx) {
-          g0 = gap_of(cdf, a.cdf_len, E.x); g1 = gap_of(cdf, a.cdf_len, E.y); g2 = gap_of(cdf, a.cdf_len, P4.x);
+          g0 = gap_of(cdf, a.cdf_len, E.x); g1 = gap_of(cdf, a.cdf_len, E.y); g2 = gap_of(cdf, a.cdf_len, F.x);
         } else {
           g0 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.x);
           g1 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.y);
-          g2 = gap_est(cdf, a.cdf_len, a.inv_log2q, P4.x);
+          g2 = gap_est(cdf, a.cdf_len, a.inv_log2q, F.x);
         }
         const int p0 = g0 - 1, p1 = p0 + g1, p2 = p1 + g2;
         set_bit<W>(gam, p0, N);
         set_bit<W>(gam, p1, N);
         set_bit<W>(gam, p2, N);
-        if (p2 < N - 1) {   // rare: a fourth flip is possible (gap k >= 3: PERT call (k-2)>>2, word (k-2)&3)
-          Word4 P = P4;
+        if (p2 < N - 1) {   // rare: a fourth flip is possible (gap 3 = F.y, gap k >= 4: PERT call (k-4)>>2, word (k-4)&3)
+          Word4 P = F;
           int pos = p2;
           for (int kk = 3; pos < N - 1; ++kk) {
-            if ((kk & 3) == 2)
-              P = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamPert << 28) | (uint32_t)((kk - 2) >> 2), ge_hi, u_k0, u_k1);
-            const int j4 = (kk - 2) & 3;
-            const uint32_t u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
+            uint32_t u = F.y;
+            if (kk >= 4) {
+              if (((kk - 4) & 3) == 0)
+                P = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamPert << 28) | (uint32_t)((kk - 4) >> 2), ge_hi, u_k0, u_k1);
+              const int j4 = (kk - 4) & 3;
+              u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
+            }
             pos += u_gx ? gap_of(cdf, a.cdf_len, u) : gap_est(cdf, a.cdf_len, a.inv_log2q, u);
             set_bit<W>(gam, pos, N);
           }
@@ -904,24 +935,26 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
         bool pert = false;
 #pragma unroll
         for (int w = 0; w < W; ++w) pert = pert || gam[w] != 0;
-        // autoreset draw (used by wave 0 only if the env's episode ends)
+        // autoreset draw (used by wave 0 only if the env's episode ends): (start, target) in
+        // one draw over the A(A-1) pairs, then the state within the start attractor
         uint32_t rt;
-        const uint32_t Rw = E.z;
         if (u_na >= 1) {
           const int32_t* att_first = reinterpret_cast<const int32_t*>(L + a.att_off);
           const uint32_t* att_words = L + a.att_off + u_na + 1;
           const uint32_t A = (uint32_t)u_na;
-          const uint32_t as = __umul24(Rw & 1023u, A) >> 10;
-          const int st0 = att_first[as];
-          const uint32_t size = (uint32_t)(att_first[as + 1] - st0);
-          const uint32_t idx = __umul24((Rw >> 20) & 4095u, size) >> 12;
-#pragma unroll
-          for (int w = 0; w < W; ++w) rs[w] = att_words[(size_t)(st0 + idx) * W + w];
-          rt = as;
+          uint32_t hi = F.w, lo = F.z, as = 0;
+          rt = 0;
           if (A >= 2) {
-            rt = __umul24((Rw >> 10) & 1023u, A - 1) >> 10;
+            const uint32_t c = ext64(hi, lo, A * (A - 1));
+            as = a.am1_magic ? __umulhi(c, a.am1_magic) : c;   // c / (A - 1)
+            rt = c - as * (A - 1);
             rt += (rt >= as) ? 1u : 0u;
           }
+          const int st0 = att_first[as];
+          const uint32_t size = (uint32_t)(att_first[as + 1] - st0);
+          const uint32_t idx = ext64(hi, lo, size);
+#pragma unroll
+          for (int w = 0; w < W; ++w) rs[w] = att_words[(size_t)(st0 + idx) * W + w];
         } else {
           const Word4 rr = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamReset << 28) | 1u, ge_hi, u_k0, u_k1);
           const uint32_t rw4[4] = {rr.x, rr.y, rr.z, rr.w};
@@ -1144,18 +1177,23 @@ __global__ void __launch_bounds__(256) pbn_reset_kernel(const int32_t* __restric
   uint32_t ns[W];
   uint32_t nt;
   if (n_attr >= 1) {
-    const uint32_t Rw = r0.x, A = (uint32_t)n_attr;
-    const uint32_t as = ((Rw & 1023u) * A) >> 10;
-    const int st0 = att_start[CK(as, n_attr + 1, 20)];
-    const uint32_t size = (uint32_t)(att_start[CK(as + 1, n_attr + 1, 21)] - st0);
-    const uint32_t idx = (((Rw >> 20) & 4095u) * size) >> 12;
-#pragma unroll
-    for (int w = 0; w < W; ++w) ns[w] = att_states[CK((size_t)(st0 + idx) * W + w, (size_t)n_states * W, 22)];
-    nt = as;
+    // (start, target != start) in one draw over the A(A-1) pairs, then the start state
+    // uniformly within the start attractor, from the 64-bit value (word 1 : word 0)
+    uint32_t hi = r0.y, lo = r0.x;
+    const uint32_t A = (uint32_t)n_attr;
+    uint32_t as = 0;
+    nt = 0;
     if (A >= 2) {
-      nt = (((Rw >> 10) & 1023u) * (A - 1)) >> 10;
+      const uint32_t c = ext64(hi, lo, A * (A - 1));
+      as = c / (A - 1);
+      nt = c - as * (A - 1);
       nt += (nt >= as) ? 1u : 0u;
     }
+    const int st0 = att_start[CK(as, n_attr + 1, 20)];
+    const uint32_t size = (uint32_t)(att_start[CK(as + 1, n_attr + 1, 21)] - st0);
+    const uint32_t idx = ext64(hi, lo, size);
+#pragma unroll
+    for (int w = 0; w < W; ++w) ns[w] = att_states[CK((size_t)(st0 + idx) * W + w, (size_t)n_states * W, 22)];
   } else {
     const Word4 r1 = pbn::draw(seed, ge, step, pbn::kStreamReset, 1);
     const uint32_t rw[4] = {r1.x, r1.y, r1.z, r1.w};
@@ -1266,6 +1304,7 @@ struct pbn_net {
   size_t lds_pipe = 0;
   int n_gates = 0, n_glayers = 0, gate_off = 0, glayer_off = 0;   // lowered wide functions
   int max_nf = 0, lq = 1, slot_words = 0;
+  uint32_t n1_magic = 0, am1_magic = 0;   // ceil(2^32 / (N + 1)), ceil(2^32 / (A - 1))
   int force_roll = 0;        // PBN_ROLL env override: 2 = lean (wave kernel), 3 = pipe
   ResetFn reset = nullptr;
   uint32_t* d_tab = nullptr;
@@ -1655,6 +1694,9 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   net->wave_lean = pick_wave<2>(W, d->prob_bits);
   net->pipe = pick_pipe(W, d->prob_bits);
   net->reset = pick_reset(W);
+  // multiply-high divisors (exact for the operand ranges used: see random_actions3, autoreset)
+  net->n1_magic = (uint32_t)(((1ull << 32) + (uint64_t)N) / (uint64_t)(N + 1));
+  net->am1_magic = A >= 3 ? (uint32_t)(((1ull << 32) + (uint64_t)(A - 2)) / (uint64_t)(A - 1)) : 0u;   // 0: A - 1 == 1
   if (const char* env = getenv("PBN_ROLL")) {
     if (!strcmp(env, "lean")) net->force_roll = 2;
     if (!strcmp(env, "pipe")) net->force_roll = 3;
@@ -1797,6 +1839,8 @@ static int step_impl(pbn_net* net, uint64_t seed, uint64_t step, const uint64_t*
   a.inv_log2q = net->inv_log2q;
   a.fcompact = net->d_fcompact;
   a.nrec = net->d_nrec;
+  a.n1_magic = net->n1_magic;
+  a.am1_magic = net->am1_magic;
   // launch shape: one thread per 32-env group once that fills the chip
   // (>= 4 waves per SIMD), else one wave per group (node loop across lanes)
   a.n_steps = 1;
@@ -1885,6 +1929,8 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
   a.inv_log2q = net->inv_log2q;
   a.fcompact = net->d_fcompact;
   a.nrec = net->d_nrec;
+  a.n1_magic = net->n1_magic;
+  a.am1_magic = net->am1_magic;
 #ifdef PBN_STAMPS
   a.stamps = g_stamps;
 #endif

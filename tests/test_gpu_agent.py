@@ -46,7 +46,7 @@ def test_obs_unpack_exact(name, n):
 
 
 @pytest.mark.parametrize("name,K,eps", [("pbn28", 3, 0.0), ("pbn28", 3, 0.3), ("pbn28", 3, 1.0),
-                                        ("pbn70", 3, 0.25), ("pbn7", 1, 0.5), ("pbn7", 5, 0.1)])
+                                        ("pbn70", 3, 0.25), ("pbn7", 1, 0.5), ("pbn7", 5, 0.1), ("pbn7", 7, 1.0)])
 def test_q_to_flipmask_exact(name, K, eps):
     spec = make_spec(name)
     n = 4160

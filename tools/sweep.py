@@ -1,6 +1,6 @@
 """Kernel sweep: time pbn_step ("wave") and pbn_rollout variants (PBN_ROLL) per batch size.
 
-    python tools/sweep.py [--network pbn28] [--envs 65536,1048576] [--kernels wave,rollp,rolll,rollh]
+    python tools/sweep.py [--network pbn28] [--envs 65536,1048576] [--kernels wave,rollp,rolll]
 
 Interleaves variants in one process (cdna_hip_programming.md rule 24) and
 reports median per-step kernel time from HIP events around graph replays.
@@ -39,8 +39,7 @@ def main():
         bufs = {}   # a captured graph writes into these: they must outlive it (torch.cuda.graph
                     # empties the allocator cache on entry, unmapping freed >= 20 MB segments)
         for T in args.kernels.split(","):
-            os.environ["PBN_ROLL"] = {"rollh": "hoist", "rolll": "lean", "rollp": "pipe",
-                                      "rollq": "plane"}.get(T, "auto")
+            os.environ["PBN_ROLL"] = {"rolll": "lean", "rollp": "pipe"}.get(T, "auto")
             env = VectorPBNEnv(spec, n, seed=3, keep_final_state=False)
             env.reset()
             with torch.cuda.stream(stream):
