@@ -13,6 +13,16 @@ __host__ __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_
   return (m & a) | (~m & b);
 }
 
+// bfi as one v_bitop3_b32 (LUT 0xCA) on the device: for per-lane masks, where the compiler
+// splits the and/or form into v_and + v_and_or (the transpose stages)
+__host__ __device__ __forceinline__ uint32_t bfi3(uint32_t m, uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(m, a, b, 0xCA);
+#else
+  return (m & a) | (~m & b);
+#endif
+}
+
 // byte permute: result byte i = byte sel_i of {hi:lo} (lo = bytes 0-3, hi = bytes 4-7)
 __host__ __device__ __forceinline__ uint32_t perm_bytes(uint32_t hi, uint32_t lo, uint32_t sel) {
 #if defined(__HIP_DEVICE_COMPILE__)

@@ -80,7 +80,11 @@ struct StepArgs {
   int prob_bits;
   int n_funcs;
   int wave_words;    // wave kernel: per-wave LDS words of S planes (after the shared table image)
-  int gap_exact;     // 1: binary search for gaps (p == 0 or tiny); 0: log estimate + fix-up
+  int gap_exact;     // 1: binary search for gaps (p == 0 or tiny); 0: log estimate + fix-up;
+                     // 2: bucket table (gap_lut_off)
+  int gap_lut_off;   // LDS image offset of the gap bucket table, uint2 [gap_nb + 1] {threshold, gap}
+  int gap_shift;     // bucket of u = u >> gap_shift
+  int gap_nb;        // buckets below C[N-1]; entry gap_nb is the sentinel {0xFFFFFFFF, N+1}
   float inv_log2q;   // 1 / log2(1 - p)
   const uint4* fcompact;   // [n_funcs] {inputs (4 x u8), truth table, threshold, 0}
   const uint4* nrec;       // [N * kNodeRecs] node-major copy of the first records (+ nf, f0 in .w)
@@ -91,7 +95,7 @@ struct StepArgs {
   int n_states;      // attractor states (bounds of att_states; checked builds)
   int att_off;       // LDS image offset of attractor start[A+1] | states[S][W] (wave kernel)
   int sel_off;       // LDS image offset of the leaf selectors, uint4 [kNodeRecs][2][32W] (wave kernel)
-  int nrec_off;      // LDS image offset of the node-major records, uint4 [N][kNodeRecs]
+  int nrec_off;      // LDS image offset of the node records, record-major uint4 [kNodeRecs][32W]
   int n_cls;         // 1..4: the first kNodeRecs thresholds of every node take one of n_cls values
                      // uthr[0..n_cls) (record .y = class index); 0: per-node thresholds
   uint32_t uthr[kNodeRecs];
@@ -101,6 +105,7 @@ struct StepArgs {
   int gate_off;      // wave kernel: LDS image offset of the gate records, uint4 [n_gates] by level
   int glayer_off;    // LDS image offset of the level starts, int32 [n_glayers + 1]
   int n_glayers;     // 0: no gates
+  int att_single;    // every attractor is one state: the reset state is attractor a's state a
   uint32_t n1_magic; // ceil(2^32 / (N + 1)): random-action digits
   uint32_t am1_magic;  // ceil(2^32 / (A - 1)) for A >= 2: autoreset (start, target) split
 };
@@ -254,21 +259,24 @@ __device__ __forceinline__ uint32_t lane_bit_mask(int lane) {
   return 0u - (uint32_t)((lane & J) != 0);
 }
 
+// (every lane's DPP source is inside its row for these controls, so each lane is written and
+// the "old" operand is never used: mov_dpp leaves it undefined, which saves the v_mov that
+// update_dpp(0, ...) spends initialising the destination)
 template <int J>
 __device__ __forceinline__ uint32_t xor_lane(uint32_t a, int lane) {
   if constexpr (J == 1) {
-    return __builtin_amdgcn_update_dpp(0u, a, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    return __builtin_amdgcn_mov_dpp(a, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
   } else if constexpr (J == 2) {
-    return __builtin_amdgcn_update_dpp(0u, a, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    return __builtin_amdgcn_mov_dpp(a, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
   } else if constexpr (J == 4) {
-    const uint32_t r4 = __builtin_amdgcn_update_dpp(0u, a, 0x124, 0xF, 0xF, false);   // row_ror:4
-    const uint32_t r12 = __builtin_amdgcn_update_dpp(0u, a, 0x12C, 0xF, 0xF, false);  // row_ror:12
-    return bfi(lane_bit_mask<4>(lane), r4, r12);
+    const uint32_t r4 = __builtin_amdgcn_mov_dpp(a, 0x124, 0xF, 0xF, true);   // row_ror:4
+    const uint32_t r12 = __builtin_amdgcn_mov_dpp(a, 0x12C, 0xF, 0xF, true);  // row_ror:12
+    return pbn::bfi3(lane_bit_mask<4>(lane), r4, r12);
   } else if constexpr (J == 8) {
-    return __builtin_amdgcn_update_dpp(0u, a, 0x128, 0xF, 0xF, false);  // row_ror:8
+    return __builtin_amdgcn_mov_dpp(a, 0x128, 0xF, 0xF, true);  // row_ror:8
   } else {
     const auto r = __builtin_amdgcn_permlane16_swap(a, a, false, false);
-    return bfi(lane_bit_mask<16>(lane), r[0], r[1]);
+    return pbn::bfi3(lane_bit_mask<16>(lane), r[0], r[1]);
   }
 }
 
@@ -282,7 +290,7 @@ __device__ __forceinline__ uint32_t transpose_step(uint32_t a, int lane) {
   const uint32_t y = xor_lane<J>(a, lane);
   const uint32_t up = lane_bit_mask<J>(lane);
   const uint32_t rot = __builtin_amdgcn_alignbit(y, y, (32u - J) ^ (up & ((32u - J) ^ (uint32_t)J)));
-  return bfi(M ^ ~up, rot, a);
+  return pbn::bfi3(M ^ ~up, rot, a);
 }
 
 // lane k holds row k of a 32x32 bit matrix (per 32-lane half); afterwards lane c holds column c
@@ -340,6 +348,21 @@ __device__ __forceinline__ int gap_est(const uint32_t* __restrict__ cdf, int len
   g += (u >= hi) ? 1 : 0;
   g -= (g >= 2 && u < lo) ? 1 : 0;
   return g;
+}
+
+// gap(u) from the bucket table: within a bucket of u (its top bits) the gap takes at most two
+// values, lo and lo + 1, split at threshold C[lo-1]; buckets from C[N-1] on share one sentinel
+// entry (gap N+1, no flip).  One LDS read and two VALU ops, where gap_est spends ~22.
+__device__ __forceinline__ int gap_lut(const uint2* __restrict__ lut, int shift, int nb, uint32_t u) {
+  const uint32_t b = min(u >> shift, (uint32_t)nb);
+  const uint2 e = lut[b];
+  return (int)e.y + (u >= e.x ? 1 : 0);
+}
+
+// one gap by the net's method (mode: 0 estimate, 1 binary search, 2 bucket table)
+__device__ __forceinline__ int gap_any(int mode, const uint32_t* __restrict__ L, const StepArgs& a, uint32_t u) {
+  if (mode == 2) return gap_lut(reinterpret_cast<const uint2*>(L + a.gap_lut_off), a.gap_shift, a.gap_nb, u);
+  return mode ? gap_of(L, a.cdf_len, u) : gap_est(L, a.cdf_len, a.inv_log2q, u);
 }
 
 // (u < c_q) for the wave-uniform threshold classes: one bit-sliced comparison per class with
@@ -540,7 +563,9 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
     // perturbation positions are prefix sums of geometric gaps; the first three gaps
     // (u = E.x, E.y, F.x) are independent, so they are computed side by side
     int g0, g1, g2;
-    if (a.gap_exact) {
+    if (a.gap_exact == 2) {
+      g0 = gap_any(2, L, a, E.x); g1 = gap_any(2, L, a, E.y); g2 = gap_any(2, L, a, F.x);
+    } else if (a.gap_exact) {
       g0 = gap_of(cdf, a.cdf_len, E.x); g1 = gap_of(cdf, a.cdf_len, E.y); g2 = gap_of(cdf, a.cdf_len, F.x);
     } else {
       g0 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.x);
@@ -562,7 +587,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
           const int j4 = (kk - 4) & 3;
           u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
         }
-        pos += a.gap_exact ? gap_of(cdf, a.cdf_len, u) : gap_est(cdf, a.cdf_len, a.inv_log2q, u);
+        pos += gap_any(a.gap_exact, L, a, u);
         set_bit<W>(gam, pos, N);
       }
     }
@@ -705,9 +730,9 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
         nt = c - as * (A - 1);
         nt += (nt >= as) ? 1u : 0u;
       }
-      const int st0 = att_first[as];
-      const uint32_t size = (uint32_t)(att_first[as + 1] - st0);
-      const uint32_t idx = ext64(hi, lo, size);
+      // (single-state attractors: the draw over one state is 0 and state a is attractor a's)
+      const int st0 = a.att_single ? (int)as : att_first[as];
+      const uint32_t idx = a.att_single ? 0u : ext64(hi, lo, (uint32_t)(att_first[as + 1] - st0));
 #pragma unroll
       for (int w = 0; w < W; ++w) sp[w] = att_words[(size_t)(st0 + idx) * W + w];
     } else {
@@ -798,6 +823,34 @@ __device__ __forceinline__ uint32_t chain_from_masks(const uint4 (&rec)[kNodeRec
   return x;
 }
 
+// chain_from_masks with the records' input bytes, the selectors and the selection masks
+// already in registers (read before the step's transposes; only the S-plane gathers remain)
+template <int K>
+__device__ __forceinline__ uint32_t chain_pre(const uint32_t (&ins)[kNodeRecs], const uint4 (&sa)[kNodeRecs],
+                                              const uint4 (&sb)[kNodeRecs], const uint32_t (&ltv)[kNodeRecs],
+                                              const uint32_t* __restrict__ S, int nf, uint32_t x) {
+  uint32_t xin[K][4];
+#pragma unroll
+  for (int q = 0; q < K; ++q) {
+    xin[q][0] = S[ins[q] & 0xFFu]; xin[q][1] = S[(ins[q] >> 8) & 0xFFu];
+    xin[q][2] = S[(ins[q] >> 16) & 0xFFu]; xin[q][3] = S[ins[q] >> 24];
+  }
+#pragma unroll
+  for (int q = K - 1; q >= 0; --q) {
+    const uint32_t x0 = xin[q][0], x1 = xin[q][1], x2 = xin[q][2], x3 = xin[q][3];
+    const uint32_t nx0 = ~x0;
+    const uint32_t v0 = __builtin_amdgcn_perm(nx0, x0, sa[q].x), v1 = __builtin_amdgcn_perm(nx0, x0, sa[q].y);
+    const uint32_t v2 = __builtin_amdgcn_perm(nx0, x0, sa[q].z), v3 = __builtin_amdgcn_perm(nx0, x0, sa[q].w);
+    const uint32_t v4 = __builtin_amdgcn_perm(nx0, x0, sb[q].x), v5 = __builtin_amdgcn_perm(nx0, x0, sb[q].y);
+    const uint32_t v6 = __builtin_amdgcn_perm(nx0, x0, sb[q].z), v7 = __builtin_amdgcn_perm(nx0, x0, sb[q].w);
+    const uint32_t w0 = bfi(x1, v1, v0), w1 = bfi(x1, v3, v2), w2 = bfi(x1, v5, v4), w3 = bfi(x1, v7, v6);
+    const uint32_t fj = bfi(x3, bfi(x2, w3, w2), bfi(x2, w1, w0));
+    const uint32_t y = (q == nf - 1) ? fj : bfi(ltv[q], fj, x);
+    x = (q < nf) ? y : x;
+  }
+  return x;
+}
+
 template <int W, int B>
 __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
   constexpr int CPN = B / 4;              // selection calls per node
@@ -845,8 +898,9 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
     tt0 = a.t[CK(le, n, 2)];
     tg0 = a.target[CK(le, n, 3)];
   }
-  // node records live in LDS (L + nrec_off): each role reads what it needs per step, so no
-  // record is carried in VGPRs across the step loop
+  // node records live in LDS (L + nrec_off), record-major [kNodeRecs][32W] so that a wave's
+  // lanes (nodes) read consecutive 16-byte records without bank conflicts: each role reads
+  // what it needs per step, so no record is carried in VGPRs across the step loop
   const uint4* recL = reinterpret_cast<const uint4*>(L + a.nrec_off);
   // wave-uniform parameters, re-defined (laundered) every iteration: hoisted out of the step
   // loop, the conditions built from them occupy SGPR pairs and spill to VGPR lanes
@@ -854,7 +908,8 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
   int u_gx = a.gap_exact, u_na = a.n_attr,  u_mnf = a.max_nf, u_hb = a.hash_bits,
       u_hp = a.hash_probes, u_hz = a.horizon;
   uint32_t u_fl = __builtin_amdgcn_readfirstlane((a.obs ? 1u : 0u) | (a.final_state ? 2u : 0u) |
-                                                 (random_actions ? 4u : 0u) | ((a.mode & PBN_MODE_AUTORESET) ? 8u : 0u));
+                                                 (random_actions ? 4u : 0u) | ((a.mode & PBN_MODE_AUTORESET) ? 8u : 0u) |
+                                                 (a.att_single ? 16u : 0u));
   // digit masks of the first kNodeRecs - 1 thresholds of every node, [q][d][32W], for the
   // selection wave's compares, built from the LDS copy of the node records once it has
   // landed (from the global records this was two dependent L2 round trips per entry, eight
@@ -867,7 +922,7 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
     for (int idx = threadIdx.x; idx < (kNodeRecs - 1) * B * 32; idx += blockDim.x) {
       const int i = idx % 32, d = (idx / 32) % B, q = idx / (32 * B);
       uint32_t c = 0;
-      if (i < N && q < (int)recL[i * kNodeRecs].w - 1) c = recL[i * kNodeRecs + q].z;
+      if (i < N && q < (int)recL[i].w - 1) c = recL[q * 32 * W + i].z;
       cm[idx] = ((c >> (B - 1 - d)) & 1u) ? ~0u : 0u;
     }
     __syncthreads();
@@ -906,7 +961,9 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
 #pragma unroll
         for (int w = 0; w < W; ++w) pc += __builtin_popcount(m[w]);
         int g0, g1, g2;
-        if (u_gx) {
+        if (u_gx == 2) {
+          g0 = gap_any(2, L, a, E.x); g1 = gap_any(2, L, a, E.y); g2 = gap_any(2, L, a, F.x);
+        } else if (u_gx) {
           g0 = gap_of(cdf, a.cdf_len, E.x); g1 = gap_of(cdf, a.cdf_len, E.y); g2 = gap_of(cdf, a.cdf_len, F.x);
         } else {
           g0 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.x);
@@ -928,7 +985,7 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
               const int j4 = (kk - 4) & 3;
               u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
             }
-            pos += u_gx ? gap_of(cdf, a.cdf_len, u) : gap_est(cdf, a.cdf_len, a.inv_log2q, u);
+            pos += gap_any(u_gx, L, a, u);
             set_bit<W>(gam, pos, N);
           }
         }
@@ -950,9 +1007,9 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
             rt = c - as * (A - 1);
             rt += (rt >= as) ? 1u : 0u;
           }
-          const int st0 = att_first[as];
-          const uint32_t size = (uint32_t)(att_first[as + 1] - st0);
-          const uint32_t idx = ext64(hi, lo, size);
+          // (single-state attractors: the draw over one state is 0 and state a is attractor a's)
+          const int st0 = (u_fl & 16u) ? (int)as : att_first[as];
+          const uint32_t idx = (u_fl & 16u) ? 0u : ext64(hi, lo, (uint32_t)(att_first[as + 1] - st0));
 #pragma unroll
           for (int w = 0; w < W; ++w) rs[w] = att_words[(size_t)(st0 + idx) * W + w];
         } else {
@@ -981,7 +1038,7 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
       for (int r = 0; r < W; ++r) {
         const int i = l32 + 32 * r;
         const int ic = i < N ? i : 0;
-        const uint4 r0 = recL[ic * kNodeRecs];
+        const uint4 r0 = recL[ic];
         if (valid && i < N && (int)r0.w > 1) {
           uint32_t dig[16];
 #pragma unroll
@@ -997,9 +1054,9 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
                 if constexpr (W == 1)
                   lt_out[q * 64 * W + i] = less_than_cm<B>(dig, cm + (size_t)q * B * 32 + i, 32);
                 else
-                  lt_out[q * 64 * W + i] = less_than(dig, recL[ic * kNodeRecs + q].z, B);
+                  lt_out[q * 64 * W + i] = less_than(dig, recL[q * 32 * W + ic].z, B);
               }
-            const int f0 = (int)recL[ic * kNodeRecs + 1].w;
+            const int f0 = (int)recL[32 * W + ic].w;
             for (int j = kNodeRecs - 1; j < nf - 1; ++j)   // nodes with more than kNodeRecs functions
               lt_out[j * 64 * W + i] = less_than(dig, a.fcompact[CK(f0 + j, a.n_funcs, 9)].z, B);
           }
@@ -1010,6 +1067,30 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
       const int t = k - 1;
       const uint32_t* slot = slots + (size_t)(t & 1) * a.slot_words;
       const uint32_t* lt_in = slot + (3 * W + 1) * 64 + half * 32 * W;
+#ifdef PBN_PREFETCH_RECS
+      // single-word states: the loop-invariant node operands (input bytes, leaf selectors) and
+      // this step's selection masks are read first, so their LDS latency overlaps the slot
+      // reads and the transpose instead of following them
+      uint32_t p_ins[kNodeRecs], p_lt[kNodeRecs];
+      uint4 p_sa[kNodeRecs], p_sb[kNodeRecs];
+      int p_nf = 1;
+      if constexpr (W == 1) {
+        int ii = l32 < N ? l32 : 0;
+        asm volatile("" : "+v"(ii));
+#pragma unroll
+        for (int q = 0; q < kNodeRecs; ++q) {
+          p_ins[q] = 0; p_lt[q] = 0; p_sa[q] = make_uint4(0, 0, 0, 0); p_sb[q] = p_sa[q];
+          if (q < u_mnf) {
+            const uint4 r = recL[q * 32 + ii];
+            p_ins[q] = r.x;
+            if (q == 0) p_nf = (int)r.w;
+            p_sa[q] = selq[(2 * q) * 32 + ii];
+            p_sb[q] = selq[(2 * q + 1) * 32 + ii];
+            if (q < u_mnf - 1) p_lt[q] = lt_in[q * 64 + ii];
+          }
+        }
+      }
+#endif
       uint32_t s1[W], gam[W], rs[W];
       uint32_t info = 0;
 #pragma unroll
@@ -1028,6 +1109,21 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
       __builtin_amdgcn_wave_barrier();
       PBN_PSTAMP_AT(k, 3);
       uint32_t X[W];
+#ifdef PBN_PREFETCH_RECS
+      if constexpr (W == 1) {
+        if (u_mnf <= kNodeRecs) {
+          uint32_t x = 0;
+          switch (u_mnf) {
+            case 1: x = chain_pre<1>(p_ins, p_sa, p_sb, p_lt, Sg, p_nf, x); break;
+            case 2: x = chain_pre<2>(p_ins, p_sa, p_sb, p_lt, Sg, p_nf, x); break;
+            case 3: x = chain_pre<3>(p_ins, p_sa, p_sb, p_lt, Sg, p_nf, x); break;
+            default: x = chain_pre<4>(p_ins, p_sa, p_sb, p_lt, Sg, p_nf, x); break;
+          }
+          X[0] = l32 < N ? x : 0u;
+        }
+      }
+      if (W > 1 || u_mnf > kNodeRecs)
+#endif
 #pragma unroll
       for (int r = 0; r < W; ++r) {
         const int i = l32 + 32 * r;
@@ -1035,7 +1131,7 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
         asm volatile("" : "+v"(ii));   // selector and record reads stay in the step loop
         uint4 rec_r[kNodeRecs];
 #pragma unroll
-        for (int q = 0; q < kNodeRecs; ++q) rec_r[q] = recL[ii * kNodeRecs + q];
+        for (int q = 0; q < kNodeRecs; ++q) rec_r[q] = recL[q * 32 * W + ii];
         const int nf = (int)rec_r[0].w;
         uint32_t x = 0;
         if (u_mnf > kNodeRecs) {   // chain tail of nodes with more than kNodeRecs functions
@@ -1293,6 +1389,7 @@ struct pbn_net {
   int n_cls = 0;
   uint32_t uthr[kNodeRecs] = {0, 0, 0, 0};
   int gap_exact = 1;
+  int gap_lut_off = 0, gap_shift = 0, gap_nb = 0;
   float inv_log2q = 0.f;
   uint4* d_fcompact = nullptr;
   uint4* d_nrec = nullptr;
@@ -1305,6 +1402,7 @@ struct pbn_net {
   int n_gates = 0, n_glayers = 0, gate_off = 0, glayer_off = 0;   // lowered wide functions
   int max_nf = 0, lq = 1, slot_words = 0;
   uint32_t n1_magic = 0, am1_magic = 0;   // ceil(2^32 / (N + 1)), ceil(2^32 / (A - 1))
+  int att_single = 0;                     // every attractor is a single state
   int force_roll = 0;        // PBN_ROLL env override: 2 = lean (wave kernel), 3 = pipe
   ResetFn reset = nullptr;
   uint32_t* d_tab = nullptr;
@@ -1636,12 +1734,16 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     nrec[(size_t)i * kNodeRecs + 0].w = (uint32_t)nf;
     nrec[(size_t)i * kNodeRecs + 1].w = (uint32_t)f0;
   }
-  // node-major records in the LDS image too (the pipelined kernel reads them per step
-  // instead of keeping them in VGPRs across its loop)
+  // the records in the LDS image too, record-major uint4 [kNodeRecs][32W] (the pipelined
+  // kernel reads them per step instead of keeping them in VGPRs across its loop; lane = node,
+  // so consecutive lanes read consecutive 16-byte records: no LDS bank conflicts, where the
+  // node-major layout's 64-byte lane stride conflicted 4 ways)
   net->nrec_off = (int)tab.size();
-  for (const uint4& r4 : nrec) {
-    tab.push_back(r4.x); tab.push_back(r4.y); tab.push_back(r4.z); tab.push_back(r4.w);
-  }
+  for (int q = 0; q < kNodeRecs; ++q)
+    for (int i = 0; i < 32 * W; ++i) {
+      const uint4 r4 = i < N ? nrec[(size_t)i * kNodeRecs + q] : make_uint4(0, 0, 0, 0);
+      tab.push_back(r4.x); tab.push_back(r4.y); tab.push_back(r4.z); tab.push_back(r4.w);
+    }
   // gate records by level: {input plane indices as bytes, 16-bit table (unused inputs
   // replicated), output plane index 32W + g, 0}, then the level starts
   net->n_gates = n_gates;
@@ -1675,13 +1777,48 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     }
     net->n_glayers = n_lv;
   }
+  // gap bucket table (gap_lut): the smallest bucket width 2^shift, shift = 32 - k with
+  // k = 6..10, under which every bucket below C[N-1] holds at most one CDF threshold;
+  // none found (p tiny) -> the estimate / binary search paths
+  {
+    const double p = (double)d->perturb_cdf[0] / 4294967296.0;
+    const bool exact = p < 1e-6 || p > 0.5;
+    auto gap_at = [&](uint64_t u) {   // min{m : u < C[m-1]}, N+1 if none
+      int m = 1;
+      while (m <= N && (uint64_t)d->perturb_cdf[m - 1] <= u) ++m;
+      return m;
+    };
+    if (!exact) {
+      for (int k = 6; k <= 10 && !net->gap_nb; ++k) {
+        const int shift = 32 - k;
+        const uint64_t w = 1ull << shift;
+        const uint32_t nb = (uint32_t)(((uint64_t)d->perturb_cdf[N - 1]) >> shift) + 1u;   // buckets that can see a flip
+        bool ok = true;
+        std::vector<uint32_t> lut;
+        for (uint32_t b = 0; b < nb && ok; ++b) {
+          const int lo = gap_at((uint64_t)b * w), hi = gap_at((uint64_t)b * w + w - 1);
+          ok = hi - lo <= 1;
+          lut.push_back(lo <= N ? d->perturb_cdf[lo - 1] : 0xFFFFFFFFu);
+          lut.push_back((uint32_t)lo);
+        }
+        if (!ok) continue;
+        lut.push_back(0xFFFFFFFFu);   // sentinel: u >= C[N-1] -> gap N+1 (u = 2^32-1 gives N+2, also no flip)
+        lut.push_back((uint32_t)(N + 1));
+        while (tab.size() & 1) tab.push_back(0u);
+        net->gap_lut_off = (int)tab.size();
+        tab.insert(tab.end(), lut.begin(), lut.end());
+        net->gap_shift = shift;
+        net->gap_nb = (int)nb;
+      }
+    }
+  }
   while (tab.size() & 3) tab.push_back(0u);   // the kernels copy the image as uint4
   net->tab_words = (int)tab.size();
   net->n_funcs = d->n_funcs;
   net->wave_words = (32 * W + n_gates + 3) & ~3;   // S planes (+ gate planes) per wave
   {
     const double p = (double)d->perturb_cdf[0] / 4294967296.0;
-    net->gap_exact = (p < 1e-6 || p > 0.5) ? 1 : 0;
+    net->gap_exact = (p < 1e-6 || p > 0.5) ? 1 : (net->gap_nb ? 2 : 0);
     net->inv_log2q = net->gap_exact ? 0.f : (float)(1.0 / log2(1.0 - p));
   }
   net->lds_wave = ((size_t)net->tab_words + (size_t)kWavesPerBlock * net->wave_words) * 4;
@@ -1696,6 +1833,7 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   net->reset = pick_reset(W);
   // multiply-high divisors (exact for the operand ranges used: see random_actions3, autoreset)
   net->n1_magic = (uint32_t)(((1ull << 32) + (uint64_t)N) / (uint64_t)(N + 1));
+  net->att_single = A >= 1 && S == A ? 1 : 0;
   net->am1_magic = A >= 3 ? (uint32_t)(((1ull << 32) + (uint64_t)(A - 2)) / (uint64_t)(A - 1)) : 0u;   // 0: A - 1 == 1
   if (const char* env = getenv("PBN_ROLL")) {
     if (!strcmp(env, "lean")) net->force_roll = 2;
@@ -1836,10 +1974,14 @@ static int step_impl(pbn_net* net, uint64_t seed, uint64_t step, const uint64_t*
   a.n_funcs = net->n_funcs;
   a.wave_words = net->wave_words;
   a.gap_exact = net->gap_exact;
+  a.gap_lut_off = net->gap_lut_off;
+  a.gap_shift = net->gap_shift;
+  a.gap_nb = net->gap_nb;
   a.inv_log2q = net->inv_log2q;
   a.fcompact = net->d_fcompact;
   a.nrec = net->d_nrec;
   a.n1_magic = net->n1_magic;
+  a.att_single = net->att_single;
   a.am1_magic = net->am1_magic;
   // launch shape: one thread per 32-env group once that fills the chip
   // (>= 4 waves per SIMD), else one wave per group (node loop across lanes)
@@ -1926,10 +2068,14 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
   a.n_funcs = net->n_funcs;
   a.wave_words = net->wave_words;
   a.gap_exact = net->gap_exact;
+  a.gap_lut_off = net->gap_lut_off;
+  a.gap_shift = net->gap_shift;
+  a.gap_nb = net->gap_nb;
   a.inv_log2q = net->inv_log2q;
   a.fcompact = net->d_fcompact;
   a.nrec = net->d_nrec;
   a.n1_magic = net->n1_magic;
+  a.att_single = net->att_single;
   a.am1_magic = net->am1_magic;
 #ifdef PBN_STAMPS
   a.stamps = g_stamps;

@@ -12,7 +12,7 @@
 namespace pbn {
 
 // EXPLORE = 4: epsilon-greedy draws of pbn_q_to_flipmask (per env; word 0 = explore test,
-// words 1-3 = the random actions, 10 bits each)
+// word k + 1 = branch k's random action, by multiply-high)
 enum : uint32_t { kStreamSel = 0, kStreamEnv = 1, kStreamPert = 2, kStreamReset = 3, kStreamExplore = 4 };
 
 struct Word4 {
@@ -28,10 +28,16 @@ __host__ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32
 #endif
 }
 
+// PBN_DIAG_PHILOX_ROUNDS: diagnostic builds only (timing the RNG's share of a kernel; the
+// results are then wrong); the product is always Philox4x32-10
+#ifndef PBN_DIAG_PHILOX_ROUNDS
+#define PBN_DIAG_PHILOX_ROUNDS 10
+#endif
+
 __host__ __device__ __forceinline__ Word4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2,
                                                          uint32_t c3, uint32_t k0, uint32_t k1) {
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
+  for (int r = 0; r < PBN_DIAG_PHILOX_ROUNDS; ++r) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
     const uint32_t n0 = xor3((uint32_t)(p1 >> 32), c1, k0);
