@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--steps-per-launch", type=int, default=100)
     ap.add_argument("--words", type=int, default=1)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--command", default=None, help="the profiled command, recorded in the summary")
     args = ap.parse_args()
     f, n, name = mean_counter(os.path.join(args.run_dir, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     w, _, _ = mean_counter(os.path.join(args.run_dir, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
@@ -45,13 +46,14 @@ def main():
            "correction": "MI355X_MICROARCH.md HBM section: FETCH_SIZE x2 on gfx950; counter units kB (1024 B)",
            "hbm_read_bytes_per_launch": f * 2 * 1024, "hbm_write_bytes_per_launch": w * 1024,
            "hbm_bytes_per_launch": (2 * f + w) * 1024, "algorithmic_bytes_per_launch": alg,
-           "note": "the read side is 4-B and 1-B loads plus table reads, a width the guide leaves uncalibrated"}
+           "note": "the read side is 4-B and 1-B loads plus table reads, a width the guide leaves uncalibrated",
+           "command": args.command, "steps_per_launch": args.steps_per_launch}
     sq = os.path.join(args.run_dir, "pmc_sq", "run_counter_collection.csv")
     if os.path.exists(sq):
         for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES", "SQ_BUSY_CYCLES"):
             out[c + "_per_launch"] = mean_counter(sq, c)[0]
         out["valu_insts_per_launch"] = out["SQ_INSTS_VALU_per_launch"]
-    path = args.out or os.path.join("profiles", f"pmc_{args.network}_{args.envs}_{args.mode}.json")
+    path = args.out or os.path.join("profiles", f"pmc_{args.network}_{args.envs}_{args.mode}_T{args.steps_per_launch}.json")
     with open(path, "w") as fo:
         json.dump(out, fo, indent=1)
     print(json.dumps(out))
