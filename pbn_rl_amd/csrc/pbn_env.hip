@@ -935,7 +935,11 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
     asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
     asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
     PBN_PSTAMP(k, 0);
-    if (role == 1 && k < n_steps) {
+#ifndef PBN_DIAG_SKIP_ROLE
+#define PBN_DIAG_SKIP_ROLE -1   // diagnostic builds only: one role does no work (timing shares)
+#endif
+    if (role == PBN_DIAG_SKIP_ROLE) {
+    } else if (role == 1 && k < n_steps) {
       // ---- env draws of step k, env `lane`
       uint32_t* slot = slots + (size_t)(k & 1) * a.slot_words;
       const uint64_t step = a.step + (uint64_t)k;

@@ -111,10 +111,14 @@ def test_captured_learner_matches_eager():
     assert R.pos == S.pos == int(graph._pos_t.item()) and R.size == S.size == int(graph._size_t.item())
     for f in ("state", "next_state", "target", "action", "reward", "done"):
         assert torch.equal(getattr(R, f), getattr(S, f)), f
+    # weights to optimiser rounding: GEMM reductions are not bit-reproducible between a captured
+    # and an eager run, and Adam normalises each update, so a weight whose gradient is ~0 can move
+    # by up to ~lr per update in one run and not the other (9 updates of lr 1e-4 here); a 1e-5
+    # tolerance failed intermittently on that, with the env, ring and loss equal
     for (k, pe), (_, pg) in zip(eager.q.named_parameters(), graph.q.named_parameters()):
-        assert torch.allclose(pe, pg, rtol=1e-4, atol=1e-5), k
+        assert torch.allclose(pe, pg, rtol=1e-3, atol=2e-3), k
     for (k, pe), (_, pg) in zip(eager.target.named_parameters(), graph.target.named_parameters()):
-        assert torch.allclose(pe, pg, rtol=1e-4, atol=1e-5), k
+        assert torch.allclose(pe, pg, rtol=1e-3, atol=2e-3), k
     assert torch.isfinite(graph.last_loss)
     assert abs(float(eager.last_loss) - float(graph.last_loss)) <= 1e-3 * max(1.0, abs(float(eager.last_loss)))
 
