@@ -293,11 +293,36 @@ __device__ __forceinline__ uint32_t transpose_step(uint32_t a, int lane) {
   return pbn::bfi3(M ^ ~up, rot, a);
 }
 
-// lane k holds row k of a 32x32 bit matrix (per 32-lane half); afterwards lane c holds column c
+// the partner value of lane ^ J within 32-lane halves through the LDS crossbar (ds_swizzle,
+// bit mode: and 0x1F, xor J): no VALU issue slot, where DPP cannot cross rows of 16 lanes
+template <int J>
+__device__ __forceinline__ uint32_t swizzle_xor(uint32_t a) {
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)a, (J << 10) | 0x1F);
+}
+
+// byte-granular stages (J = 16, 8) as one v_perm_b32 with a per-lane selector: the shift and
+// the field select of transpose_step in one instruction.  perm(y, a, sel): bytes 0-3 are a's,
+// 4-7 the partner's.
+//   J = 16: low lanes [a0 a1 y0 y1], high lanes [y2 y3 a2 a3]
+//   J = 8:  low lanes [a0 y0 a2 y2], high lanes [y1 a1 y3 a3]
+template <int J>
+__device__ __forceinline__ uint32_t perm_sel(int lane) {
+  if constexpr (J == 16) return (lane & 16) ? 0x03020706u : 0x05040100u;
+  else return (lane & 8) ? 0x03070105u : 0x06020400u;
+}
+
+// lane k holds row k of a 32x32 bit matrix (per 32-lane half); afterwards lane c holds column c.
+// 11 VALU (J = 16: swizzle + perm; 8: DPP + perm; 4: swizzle + alignbit + bitop3; 2, 1: DPP +
+// alignbit + bitop3) where five transpose_step spend 20.
 __device__ __forceinline__ uint32_t lane_transpose32(uint32_t a, int lane) {
-  a = transpose_step<16>(a, lane);
-  a = transpose_step<8>(a, lane);
-  a = transpose_step<4>(a, lane);
+  a = __builtin_amdgcn_perm(swizzle_xor<16>(a), a, perm_sel<16>(lane));
+  a = __builtin_amdgcn_perm(xor_lane<8>(a, lane), a, perm_sel<8>(lane));
+  {
+    const uint32_t y = swizzle_xor<4>(a);
+    const uint32_t up = lane_bit_mask<4>(lane);
+    const uint32_t rot = __builtin_amdgcn_alignbit(y, y, 28u ^ (up & (28u ^ 4u)));
+    a = pbn::bfi3(0x0F0F0F0Fu ^ ~up, rot, a);
+  }
   a = transpose_step<2>(a, lane);
   a = transpose_step<1>(a, lane);
   return a;
@@ -330,6 +355,17 @@ __device__ __forceinline__ uint32_t eval_sel(uint32_t ins, uint4 sa, uint4 sb, c
   const uint32_t v6 = __builtin_amdgcn_perm(nx0, x0, sb.z), v7 = __builtin_amdgcn_perm(nx0, x0, sb.w);
   const uint32_t w0 = bfi(x1, v1, v0), w1 = bfi(x1, v3, v2), w2 = bfi(x1, v5, v4), w3 = bfi(x1, v7, v6);
   return bfi(x3, bfi(x2, w3, w2), bfi(x2, w1, w0));
+}
+
+// eval_sel with the four input planes already read
+__device__ __forceinline__ uint32_t eval_sel_in(const uint32_t (&x)[4], uint4 sa, uint4 sb) {
+  const uint32_t x0 = x[0], nx0 = ~x0;
+  const uint32_t v0 = __builtin_amdgcn_perm(nx0, x0, sa.x), v1 = __builtin_amdgcn_perm(nx0, x0, sa.y);
+  const uint32_t v2 = __builtin_amdgcn_perm(nx0, x0, sa.z), v3 = __builtin_amdgcn_perm(nx0, x0, sa.w);
+  const uint32_t v4 = __builtin_amdgcn_perm(nx0, x0, sb.x), v5 = __builtin_amdgcn_perm(nx0, x0, sb.y);
+  const uint32_t v6 = __builtin_amdgcn_perm(nx0, x0, sb.z), v7 = __builtin_amdgcn_perm(nx0, x0, sb.w);
+  const uint32_t w0 = bfi(x[1], v1, v0), w1 = bfi(x[1], v3, v2), w2 = bfi(x[1], v5, v4), w3 = bfi(x[1], v7, v6);
+  return bfi(x[3], bfi(x[2], w3, w2), bfi(x[2], w1, w0));
 }
 
 // gap(u) = min{m : u < C[m-1]} from a float estimate of log(1-x)/log(1-p) corrected
@@ -787,9 +823,19 @@ __device__ __forceinline__ void lds_barrier() {
 // Each wave alone is latency-bound, so the split (three instruction streams per group pair)
 // is what fills the SIMDs at small batches.
 
+// input plane k of a record's input word: byte k is a plane index, or with BY (the pipelined
+// kernel's LDS records for W <= 2) the plane's byte offset, so that the address is one add of
+// a byte field (v_add_u32 with an SDWA byte select) instead of extract + shift-add
+template <bool BY>
+__device__ __forceinline__ uint32_t plane_in(const uint32_t* __restrict__ S, uint32_t ins, int k) {
+  const uint32_t f = k == 3 ? ins >> 24 : (ins >> (8 * k)) & 0xFFu;
+  if constexpr (BY) return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(S) + f);
+  else return S[f];
+}
+
 // node chain from precomputed selection masks: x = F_{nf-1}; x = lt_j ? F_j : x, with every
 // LDS read of the K records issued before any use (K = wave-uniform bound, nf per lane)
-template <int K>
+template <int K, bool BY>
 __device__ __forceinline__ uint32_t chain_from_masks(const uint4 (&rec)[kNodeRecs], const uint4* __restrict__ sel,
                                                      int stride, const uint32_t* __restrict__ S,
                                                      const uint32_t* __restrict__ lt, int lt_stride, int nf,
@@ -799,8 +845,8 @@ __device__ __forceinline__ uint32_t chain_from_masks(const uint4 (&rec)[kNodeRec
 #pragma unroll
   for (int q = 0; q < K; ++q) {
     const uint32_t ins = rec[q].x;
-    xin[q][0] = S[ins & 0xFFu]; xin[q][1] = S[(ins >> 8) & 0xFFu];
-    xin[q][2] = S[(ins >> 16) & 0xFFu]; xin[q][3] = S[ins >> 24];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) xin[q][k] = plane_in<BY>(S, ins, k);
     sa[q] = sel[(2 * q) * stride];
     sb[q] = sel[(2 * q + 1) * stride];
     // mask q exists for q < K - 1, and for q = K - 1 too when some node has more than K
@@ -823,30 +869,29 @@ __device__ __forceinline__ uint32_t chain_from_masks(const uint4 (&rec)[kNodeRec
   return x;
 }
 
-// chain_from_masks with the records' input bytes, the selectors and the selection masks
-// already in registers (read before the step's transposes; only the S-plane gathers remain)
-template <int K>
-__device__ __forceinline__ uint32_t chain_pre(const uint32_t (&ins)[kNodeRecs], const uint4 (&sa)[kNodeRecs],
-                                              const uint4 (&sb)[kNodeRecs], const uint32_t (&ltv)[kNodeRecs],
-                                              const uint32_t* __restrict__ S, int nf, uint32_t x) {
-  uint32_t xin[K][4];
+// chain over padded records (every node has max_nf <= kNodeRecs records, the last function
+// repeated; lanes past N have all-zero selectors and evaluate to 0): x = F_{K-1}; x = lt_q ? F_q
+// : x, with no per-lane function count
+template <int K, bool BY>
+__device__ __forceinline__ uint32_t chain_padded(const uint4* __restrict__ rec, const uint4* __restrict__ sel,
+                                                 int stride, const uint32_t* __restrict__ S,
+                                                 const uint32_t* __restrict__ lt, int lt_stride) {
+  uint32_t xin[K][4], ltv[K];
+  uint4 sa[K], sb[K];
 #pragma unroll
   for (int q = 0; q < K; ++q) {
-    xin[q][0] = S[ins[q] & 0xFFu]; xin[q][1] = S[(ins[q] >> 8) & 0xFFu];
-    xin[q][2] = S[(ins[q] >> 16) & 0xFFu]; xin[q][3] = S[ins[q] >> 24];
+    const uint32_t ins = rec[q * stride].x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) xin[q][k] = plane_in<BY>(S, ins, k);
+    sa[q] = sel[(2 * q) * stride];
+    sb[q] = sel[(2 * q + 1) * stride];
+    ltv[q] = q < K - 1 ? lt[q * lt_stride] : 0u;
   }
+  uint32_t x = 0;
 #pragma unroll
   for (int q = K - 1; q >= 0; --q) {
-    const uint32_t x0 = xin[q][0], x1 = xin[q][1], x2 = xin[q][2], x3 = xin[q][3];
-    const uint32_t nx0 = ~x0;
-    const uint32_t v0 = __builtin_amdgcn_perm(nx0, x0, sa[q].x), v1 = __builtin_amdgcn_perm(nx0, x0, sa[q].y);
-    const uint32_t v2 = __builtin_amdgcn_perm(nx0, x0, sa[q].z), v3 = __builtin_amdgcn_perm(nx0, x0, sa[q].w);
-    const uint32_t v4 = __builtin_amdgcn_perm(nx0, x0, sb[q].x), v5 = __builtin_amdgcn_perm(nx0, x0, sb[q].y);
-    const uint32_t v6 = __builtin_amdgcn_perm(nx0, x0, sb[q].z), v7 = __builtin_amdgcn_perm(nx0, x0, sb[q].w);
-    const uint32_t w0 = bfi(x1, v1, v0), w1 = bfi(x1, v3, v2), w2 = bfi(x1, v5, v4), w3 = bfi(x1, v7, v6);
-    const uint32_t fj = bfi(x3, bfi(x2, w3, w2), bfi(x2, w1, w0));
-    const uint32_t y = (q == nf - 1) ? fj : bfi(ltv[q], fj, x);
-    x = (q < nf) ? y : x;
+    const uint32_t fj = eval_sel_in(xin[q], sa[q], sb[q]);
+    x = (q == K - 1) ? fj : bfi(ltv[q], fj, x);
   }
   return x;
 }
@@ -931,303 +976,303 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
   // the bottom of the loop wait on vmcnt(0), which also waits for every store of the step
   __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
 
-  for (int k = 0; k <= n_steps; ++k) {
-    asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
-    asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
-    PBN_PSTAMP(k, 0);
 #ifndef PBN_DIAG_SKIP_ROLE
 #define PBN_DIAG_SKIP_ROLE -1   // diagnostic builds only: one role does no work (timing shares)
 #endif
-    if (role == PBN_DIAG_SKIP_ROLE) {
-    } else if (role == 1 && k < n_steps) {
-      // ---- env draws of step k, env `lane`
-      uint32_t* slot = slots + (size_t)(k & 1) * a.slot_words;
-      const uint64_t step = a.step + (uint64_t)k;
-      const uint32_t st_lo = (uint32_t)step;
-      const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
-      const uint32_t ge_lo = (uint32_t)ge;
-      if (valid) {
-        const Word4 E = pbn::philox4x32_10(ge_lo, st_lo, pbn::kStreamEnv << 28, ge_hi, u_k0, u_k1);
-        const Word4 F = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamEnv << 28) | 1u, ge_hi, u_k0, u_k1);
-        uint32_t m[W], gam[W], rs[W];
+  // one loop per role: every wave passes the same n_steps + 1 block barriers, and each role's
+  // loop-carried values (hoisted invariants) occupy registers only in that role's loop
+  if (role == PBN_DIAG_SKIP_ROLE) {
+    for (int k = 0; k <= n_steps; ++k) lds_barrier();
+  } else if (role == 1) {
+    for (int k = 0; k <= n_steps; ++k) {
+      asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
+      asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
+      PBN_PSTAMP(k, 0);
+      if (k < n_steps) {
+        // ---- env draws of step k, env `lane`
+        uint32_t* slot = slots + (size_t)(k & 1) * a.slot_words;
+        const uint64_t step = a.step + (uint64_t)k;
+        const uint32_t st_lo = (uint32_t)step;
+        const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
+        const uint32_t ge_lo = (uint32_t)ge;
+        if (valid) {
+          const Word4 E = pbn::philox4x32_10(ge_lo, st_lo, pbn::kStreamEnv << 28, ge_hi, u_k0, u_k1);
+          const Word4 F = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamEnv << 28) | 1u, ge_hi, u_k0, u_k1);
+          uint32_t m[W], gam[W], rs[W];
 #pragma unroll
-        for (int w = 0; w < W; ++w) { m[w] = 0; gam[w] = 0; rs[w] = 0; }
-        if (u_fl & 4u) {
-          random_actions3<W>(E.w, E.z, N, a.n1_magic, m);
+          for (int w = 0; w < W; ++w) { m[w] = 0; gam[w] = 0; rs[w] = 0; }
+          if (u_fl & 4u) {
+            random_actions3<W>(E.w, E.z, N, a.n1_magic, m);
 #pragma unroll
-          for (int w = 0; w < W; ++w) a.flipmask[CK(k * plane + (size_t)w * n + le, (size_t)n_steps * plane, 8)] = m[w];
-        } else {
+            for (int w = 0; w < W; ++w) a.flipmask[CK(k * plane + (size_t)w * n + le, (size_t)n_steps * plane, 8)] = m[w];
+          } else {
 #pragma unroll
-          for (int w = 0; w < W; ++w)
-            m[w] = a.flipmask[CK(k * plane + (size_t)w * n + le, (size_t)n_steps * plane, 6)] & valid_word_mask(N, w);
-        }
-        uint32_t pc = 0;
+            for (int w = 0; w < W; ++w)
+              m[w] = a.flipmask[CK(k * plane + (size_t)w * n + le, (size_t)n_steps * plane, 6)] & valid_word_mask(N, w);
+          }
+          uint32_t pc = 0;
 #pragma unroll
-        for (int w = 0; w < W; ++w) pc += __builtin_popcount(m[w]);
-        int g0, g1, g2;
-        if (u_gx == 2) {
-          g0 = gap_any(2, L, a, E.x); g1 = gap_any(2, L, a, E.y); g2 = gap_any(2, L, a, F.x);
-        } else if (u_gx) {
-          g0 = gap_of(cdf, a.cdf_len, E.x); g1 = gap_of(cdf, a.cdf_len, E.y); g2 = gap_of(cdf, a.cdf_len, F.x);
-        } else {
-          g0 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.x);
-          g1 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.y);
-          g2 = gap_est(cdf, a.cdf_len, a.inv_log2q, F.x);
-        }
-        const int p0 = g0 - 1, p1 = p0 + g1, p2 = p1 + g2;
-        set_bit<W>(gam, p0, N);
-        set_bit<W>(gam, p1, N);
-        set_bit<W>(gam, p2, N);
-        if (p2 < N - 1) {   // rare: a fourth flip is possible (gap 3 = F.y, gap k >= 4: PERT call (k-4)>>2, word (k-4)&3)
-          Word4 P = F;
-          int pos = p2;
-          for (int kk = 3; pos < N - 1; ++kk) {
-            uint32_t u = F.y;
-            if (kk >= 4) {
-              if (((kk - 4) & 3) == 0)
-                P = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamPert << 28) | (uint32_t)((kk - 4) >> 2), ge_hi, u_k0, u_k1);
-              const int j4 = (kk - 4) & 3;
-              u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
+          for (int w = 0; w < W; ++w) pc += __builtin_popcount(m[w]);
+          int g0, g1, g2;
+          if (u_gx == 2) {
+            g0 = gap_any(2, L, a, E.x); g1 = gap_any(2, L, a, E.y); g2 = gap_any(2, L, a, F.x);
+          } else if (u_gx) {
+            g0 = gap_of(cdf, a.cdf_len, E.x); g1 = gap_of(cdf, a.cdf_len, E.y); g2 = gap_of(cdf, a.cdf_len, F.x);
+          } else {
+            g0 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.x);
+            g1 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.y);
+            g2 = gap_est(cdf, a.cdf_len, a.inv_log2q, F.x);
+          }
+          const int p0 = g0 - 1, p1 = p0 + g1, p2 = p1 + g2;
+          set_bit<W>(gam, p0, N);
+          set_bit<W>(gam, p1, N);
+          set_bit<W>(gam, p2, N);
+          if (p2 < N - 1) {   // rare: a fourth flip is possible (gap 3 = F.y, gap k >= 4: PERT call (k-4)>>2, word (k-4)&3)
+            Word4 P = F;
+            int pos = p2;
+            for (int kk = 3; pos < N - 1; ++kk) {
+              uint32_t u = F.y;
+              if (kk >= 4) {
+                if (((kk - 4) & 3) == 0)
+                  P = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamPert << 28) | (uint32_t)((kk - 4) >> 2), ge_hi, u_k0, u_k1);
+                const int j4 = (kk - 4) & 3;
+                u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
+              }
+              pos += gap_any(u_gx, L, a, u);
+              set_bit<W>(gam, pos, N);
             }
-            pos += gap_any(u_gx, L, a, u);
-            set_bit<W>(gam, pos, N);
+          }
+          bool pert = false;
+#pragma unroll
+          for (int w = 0; w < W; ++w) pert = pert || gam[w] != 0;
+          // autoreset draw (used by wave 0 only if the env's episode ends): (start, target) in
+          // one draw over the A(A-1) pairs, then the state within the start attractor
+          uint32_t rt;
+          if (u_na >= 1) {
+            const int32_t* att_first = reinterpret_cast<const int32_t*>(L + a.att_off);
+            const uint32_t* att_words = L + a.att_off + u_na + 1;
+            const uint32_t A = (uint32_t)u_na;
+            uint32_t hi = F.w, lo = F.z, as = 0;
+            rt = 0;
+            if (A >= 2) {
+              const uint32_t c = ext64(hi, lo, A * (A - 1));
+              as = a.am1_magic ? __umulhi(c, a.am1_magic) : c;   // c / (A - 1)
+              rt = c - as * (A - 1);
+              rt += (rt >= as) ? 1u : 0u;
+            }
+            // (single-state attractors: the draw over one state is 0 and state a is attractor a's)
+            const int st0 = (u_fl & 16u) ? (int)as : att_first[as];
+            const uint32_t idx = (u_fl & 16u) ? 0u : ext64(hi, lo, (uint32_t)(att_first[as + 1] - st0));
+#pragma unroll
+            for (int w = 0; w < W; ++w) rs[w] = att_words[(size_t)(st0 + idx) * W + w];
+          } else {
+            const Word4 rr = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamReset << 28) | 1u, ge_hi, u_k0, u_k1);
+            const uint32_t rw4[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+            for (int w = 0; w < W; ++w) rs[w] = rw4[w] & valid_word_mask(N, w);
+            rt = PBN_NO_TARGET;
+          }
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            slot[w * 64 + lane] = m[w];
+            slot[(W + w) * 64 + lane] = gam[w];
+            slot[(2 * W + w) * 64 + lane] = rs[w];
+          }
+          slot[3 * W * 64 + lane] = rt | (pc << 8) | ((uint32_t)pert << 16);
+        }
+      }
+      PBN_PSTAMP(k, 1);
+      lds_barrier();
+    }
+  } else if (role == 2) {
+    for (int k = 0; k <= n_steps; ++k) {
+      asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
+      asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
+      PBN_PSTAMP(k, 0);
+      if (k < n_steps) {
+        // ---- selection masks of step k: node l32 + 32r of group g
+        uint32_t* lt_out = slots + (size_t)(k & 1) * a.slot_words + (3 * W + 1) * 64 + half * 32 * W;
+        const uint64_t step = a.step + (uint64_t)k;
+        const uint32_t st_lo = (uint32_t)step;
+        const uint32_t G_hi = (uint32_t)((G >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
+        const uint32_t G_lo = (uint32_t)G;
+#pragma unroll
+        for (int r = 0; r < W; ++r) {
+          const int i = l32 + 32 * r;
+          const int ic = i < N ? i : 0;
+          const uint4 r0 = recL[ic];
+          if (valid && i < N && (int)r0.w > 1) {
+            uint32_t dig[16];
+#pragma unroll
+            for (int c = 0; c < CPN; ++c) {
+              const Word4 o = pbn::philox4x32_10(G_lo, st_lo, (pbn::kStreamSel << 28) | (uint32_t)(4 * i + c), G_hi, u_k0, u_k1);
+              dig[4 * c + 0] = o.x; dig[4 * c + 1] = o.y; dig[4 * c + 2] = o.z; dig[4 * c + 3] = o.w;
+            }
+            const int nf = (int)r0.w;
+            {   // per-lane thresholds: the selection wave has slack, the SGPRs are scarce
+#pragma unroll
+              for (int q = 0; q < kNodeRecs - 1; ++q)
+                if (q < nf - 1) {
+                  if constexpr (W == 1)
+                    lt_out[q * 64 * W + i] = less_than_cm<B>(dig, cm + (size_t)q * B * 32 + i, 32);
+                  else
+                    lt_out[q * 64 * W + i] = less_than(dig, recL[q * 32 * W + ic].z, B);
+                }
+              const int f0 = (int)recL[32 * W + ic].w;
+              for (int j = kNodeRecs - 1; j < nf - 1; ++j)   // nodes with more than kNodeRecs functions
+                lt_out[j * 64 * W + i] = less_than(dig, a.fcompact[CK(f0 + j, a.n_funcs, 9)].z, B);
+            }
           }
         }
-        bool pert = false;
-#pragma unroll
-        for (int w = 0; w < W; ++w) pert = pert || gam[w] != 0;
-        // autoreset draw (used by wave 0 only if the env's episode ends): (start, target) in
-        // one draw over the A(A-1) pairs, then the state within the start attractor
-        uint32_t rt;
-        if (u_na >= 1) {
-          const int32_t* att_first = reinterpret_cast<const int32_t*>(L + a.att_off);
-          const uint32_t* att_words = L + a.att_off + u_na + 1;
-          const uint32_t A = (uint32_t)u_na;
-          uint32_t hi = F.w, lo = F.z, as = 0;
-          rt = 0;
-          if (A >= 2) {
-            const uint32_t c = ext64(hi, lo, A * (A - 1));
-            as = a.am1_magic ? __umulhi(c, a.am1_magic) : c;   // c / (A - 1)
-            rt = c - as * (A - 1);
-            rt += (rt >= as) ? 1u : 0u;
-          }
-          // (single-state attractors: the draw over one state is 0 and state a is attractor a's)
-          const int st0 = (u_fl & 16u) ? (int)as : att_first[as];
-          const uint32_t idx = (u_fl & 16u) ? 0u : ext64(hi, lo, (uint32_t)(att_first[as + 1] - st0));
-#pragma unroll
-          for (int w = 0; w < W; ++w) rs[w] = att_words[(size_t)(st0 + idx) * W + w];
-        } else {
-          const Word4 rr = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamReset << 28) | 1u, ge_hi, u_k0, u_k1);
-          const uint32_t rw4[4] = {rr.x, rr.y, rr.z, rr.w};
-#pragma unroll
-          for (int w = 0; w < W; ++w) rs[w] = rw4[w] & valid_word_mask(N, w);
-          rt = PBN_NO_TARGET;
-        }
+      }
+      PBN_PSTAMP(k, 1);
+      lds_barrier();
+    }
+  } else {
+    for (int k = 0; k <= n_steps; ++k) {
+      asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
+      asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
+      PBN_PSTAMP(k, 0);
+      if (k >= 1) {
+        // ---- state part of step t = k - 1
+        const int t = k - 1;
+        const uint32_t* slot = slots + (size_t)(t & 1) * a.slot_words;
+        const uint32_t* lt_in = slot + (3 * W + 1) * 64 + half * 32 * W;
+        uint32_t s1[W], gam[W], rs[W];
+        uint32_t info = 0;
 #pragma unroll
         for (int w = 0; w < W; ++w) {
-          slot[w * 64 + lane] = m[w];
-          slot[(W + w) * 64 + lane] = gam[w];
-          slot[(2 * W + w) * 64 + lane] = rs[w];
+          s1[w] = st[w] ^ slot[w * 64 + lane];
+          gam[w] = slot[(W + w) * 64 + lane];
+          rs[w] = slot[(2 * W + w) * 64 + lane];
         }
-        slot[3 * W * 64 + lane] = rt | (pc << 8) | ((uint32_t)pert << 16);
-      }
-    } else if (role == 2 && k < n_steps) {
-      // ---- selection masks of step k: node l32 + 32r of group g
-      uint32_t* lt_out = slots + (size_t)(k & 1) * a.slot_words + (3 * W + 1) * 64 + half * 32 * W;
-      const uint64_t step = a.step + (uint64_t)k;
-      const uint32_t st_lo = (uint32_t)step;
-      const uint32_t G_hi = (uint32_t)((G >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
-      const uint32_t G_lo = (uint32_t)G;
+        info = slot[3 * W * 64 + lane];
+        if (valid && (u_fl & 1u)) {
 #pragma unroll
-      for (int r = 0; r < W; ++r) {
-        const int i = l32 + 32 * r;
-        const int ic = i < N ? i : 0;
-        const uint4 r0 = recL[ic];
-        if (valid && i < N && (int)r0.w > 1) {
-          uint32_t dig[16];
-#pragma unroll
-          for (int c = 0; c < CPN; ++c) {
-            const Word4 o = pbn::philox4x32_10(G_lo, st_lo, (pbn::kStreamSel << 28) | (uint32_t)(4 * i + c), G_hi, u_k0, u_k1);
-            dig[4 * c + 0] = o.x; dig[4 * c + 1] = o.y; dig[4 * c + 2] = o.z; dig[4 * c + 3] = o.w;
-          }
-          const int nf = (int)r0.w;
-          {   // per-lane thresholds: the selection wave has slack, the SGPRs are scarce
-#pragma unroll
-            for (int q = 0; q < kNodeRecs - 1; ++q)
-              if (q < nf - 1) {
-                if constexpr (W == 1)
-                  lt_out[q * 64 * W + i] = less_than_cm<B>(dig, cm + (size_t)q * B * 32 + i, 32);
-                else
-                  lt_out[q * 64 * W + i] = less_than(dig, recL[q * 32 * W + ic].z, B);
-              }
-            const int f0 = (int)recL[32 * W + ic].w;
-            for (int j = kNodeRecs - 1; j < nf - 1; ++j)   // nodes with more than kNodeRecs functions
-              lt_out[j * 64 * W + i] = less_than(dig, a.fcompact[CK(f0 + j, a.n_funcs, 9)].z, B);
-          }
+          for (int w = 0; w < W; ++w) a.obs[CK(t * plane + (size_t)w * n + le, (size_t)n_steps * plane, 7)] = st[w];
         }
-      }
-    } else if (role == 0 && k >= 1) {
-      // ---- state part of step t = k - 1
-      const int t = k - 1;
-      const uint32_t* slot = slots + (size_t)(t & 1) * a.slot_words;
-      const uint32_t* lt_in = slot + (3 * W + 1) * 64 + half * 32 * W;
-#ifdef PBN_PREFETCH_RECS
-      // single-word states: the loop-invariant node operands (input bytes, leaf selectors) and
-      // this step's selection masks are read first, so their LDS latency overlaps the slot
-      // reads and the transpose instead of following them
-      uint32_t p_ins[kNodeRecs], p_lt[kNodeRecs];
-      uint4 p_sa[kNodeRecs], p_sb[kNodeRecs];
-      int p_nf = 1;
-      if constexpr (W == 1) {
-        int ii = l32 < N ? l32 : 0;
-        asm volatile("" : "+v"(ii));
 #pragma unroll
-        for (int q = 0; q < kNodeRecs; ++q) {
-          p_ins[q] = 0; p_lt[q] = 0; p_sa[q] = make_uint4(0, 0, 0, 0); p_sb[q] = p_sa[q];
-          if (q < u_mnf) {
-            const uint4 r = recL[q * 32 + ii];
-            p_ins[q] = r.x;
-            if (q == 0) p_nf = (int)r.w;
-            p_sa[q] = selq[(2 * q) * 32 + ii];
-            p_sb[q] = selq[(2 * q + 1) * 32 + ii];
-            if (q < u_mnf - 1) p_lt[q] = lt_in[q * 64 + ii];
-          }
-        }
-      }
-#endif
-      uint32_t s1[W], gam[W], rs[W];
-      uint32_t info = 0;
-#pragma unroll
-      for (int w = 0; w < W; ++w) {
-        s1[w] = st[w] ^ slot[w * 64 + lane];
-        gam[w] = slot[(W + w) * 64 + lane];
-        rs[w] = slot[(2 * W + w) * 64 + lane];
-      }
-      info = slot[3 * W * 64 + lane];
-      if (valid && (u_fl & 1u)) {
-#pragma unroll
-        for (int w = 0; w < W; ++w) a.obs[CK(t * plane + (size_t)w * n + le, (size_t)n_steps * plane, 7)] = st[w];
-      }
-#pragma unroll
-      for (int w = 0; w < W; ++w) Sg[32 * w + l32] = lane_transpose32(s1[w], lane);
-      __builtin_amdgcn_wave_barrier();
-      PBN_PSTAMP_AT(k, 3);
-      uint32_t X[W];
-#ifdef PBN_PREFETCH_RECS
-      if constexpr (W == 1) {
+        for (int w = 0; w < W; ++w) Sg[32 * w + l32] = lane_transpose32(s1[w], lane);
+        __builtin_amdgcn_wave_barrier();
+        PBN_PSTAMP_AT(k, 3);
+        uint32_t X[W];
         if (u_mnf <= kNodeRecs) {
+#pragma unroll
+          for (int r = 0; r < W; ++r) {
+            int i = l32 + 32 * r;
+            asm volatile("" : "+v"(i));   // selector and record reads stay in the step loop
+            const uint4* rc = recL + i;
+            const uint4* sel = selq + i;
+            const uint32_t* lti = lt_in + i;
+            switch (u_mnf) {
+              case 1: X[r] = chain_padded<1, (W <= 2)>(rc, sel, 32 * W, Sg, lti, 64 * W); break;
+              case 2: X[r] = chain_padded<2, (W <= 2)>(rc, sel, 32 * W, Sg, lti, 64 * W); break;
+              case 3: X[r] = chain_padded<3, (W <= 2)>(rc, sel, 32 * W, Sg, lti, 64 * W); break;
+              default: X[r] = chain_padded<4, (W <= 2)>(rc, sel, 32 * W, Sg, lti, 64 * W); break;
+            }
+          }
+        } else
+#pragma unroll
+        for (int r = 0; r < W; ++r) {
+          const int i = l32 + 32 * r;
+          int ii = i < N ? i : 0;
+          asm volatile("" : "+v"(ii));   // selector and record reads stay in the step loop
+          uint4 rec_r[kNodeRecs];
+#pragma unroll
+          for (int q = 0; q < kNodeRecs; ++q) rec_r[q] = recL[q * 32 * W + ii];
+          const int nf = (int)rec_r[0].w;
           uint32_t x = 0;
+          if (u_mnf > kNodeRecs) {   // chain tail of nodes with more than kNodeRecs functions
+            const int f0 = (int)rec_r[1].w;
+            for (int j = nf - 1; j >= kNodeRecs; --j) {
+              const uint4 rc = a.fcompact[CK(f0 + j, a.n_funcs, 9)];
+              const uint32_t fj = eval_compact(rc.x, rc.y, Sg);
+              x = (j == nf - 1) ? fj : bfi(lt_in[j * 64 * W + ii], fj, x);
+            }
+          }
+          const uint4* sel = selq + ii;
+          const uint32_t* lti = lt_in + ii;
           switch (u_mnf) {
-            case 1: x = chain_pre<1>(p_ins, p_sa, p_sb, p_lt, Sg, p_nf, x); break;
-            case 2: x = chain_pre<2>(p_ins, p_sa, p_sb, p_lt, Sg, p_nf, x); break;
-            case 3: x = chain_pre<3>(p_ins, p_sa, p_sb, p_lt, Sg, p_nf, x); break;
-            default: x = chain_pre<4>(p_ins, p_sa, p_sb, p_lt, Sg, p_nf, x); break;
+            case 1: x = chain_from_masks<1, (W <= 2)>(rec_r, sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
+            case 2: x = chain_from_masks<2, (W <= 2)>(rec_r, sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
+            case 3: x = chain_from_masks<3, (W <= 2)>(rec_r, sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
+            default: x = chain_from_masks<4, (W <= 2)>(rec_r, sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
           }
-          X[0] = l32 < N ? x : 0u;
+          X[r] = i < N ? x : 0u;
+        }
+        PBN_PSTAMP_AT(k, 12);
+        uint32_t sp[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) sp[w] = lane_transpose32(X[w], lane);
+        PBN_PSTAMP_AT(k, 13);
+        {
+          // branch-free epilogue (this wave bounds the iteration): only the stores are guarded
+          const bool pert = (info >> 16) & 1u;
+          const uint32_t pc = (info >> 8) & 0xFFu;
+#pragma unroll
+          for (int w = 0; w < W; ++w) sp[w] = pert ? (s1[w] ^ gam[w]) : sp[w];
+          if (valid && (u_fl & 2u)) {
+#pragma unroll
+            for (int w = 0; w < W; ++w) a.final_state[CK(t * plane + (size_t)w * n + le, (size_t)n_steps * plane, 10)] = sp[w];
+          }
+          // reward candidates depend only on popcount(flipmask): read them beside the hash
+          const float r_none = rtab[pc], r_wrong = rtab[(N + 1) + pc], r_term = rtab[2 * (N + 1) + pc];
+          int att = -1;
+          if (u_hb > 0) {
+            const int hmask = (1 << u_hb) - 1;
+            const uint32_t* hid = htab + (size_t)W * (hmask + 1);
+            uint32_t h = 0;
+#pragma unroll
+            for (int w = 0; w < W; ++w) h += sp[w] * a.hash_mult[w];
+            h >>= (32 - u_hb);
+            // the table is usually collision-free (one probe); keys are unique, so probe order
+            // does not matter
+            {
+              const uint32_t slot_i = h & hmask;
+              uint32_t eq = 1u;
+#pragma unroll
+              for (int w = 0; w < W; ++w) eq &= (htab[(size_t)w * (hmask + 1) + slot_i] == sp[w]) ? 1u : 0u;
+              const uint32_t id = hid[slot_i];
+              att = (eq != 0u && id != 0xFFFFFFFFu) ? (int)id : att;
+            }
+            for (int pr = 1; pr < u_hp; ++pr) {
+              const uint32_t slot_i = (h + pr) & hmask;
+              bool eq = true;
+#pragma unroll
+              for (int w = 0; w < W; ++w) eq = eq && (htab[(size_t)w * (hmask + 1) + slot_i] == sp[w]);
+              const uint32_t id = hid[slot_i];
+              if (eq && id != 0xFFFFFFFFu) att = (int)id;
+            }
+          }
+          const bool in_attr = att >= 0;
+          const bool term = in_attr && (uint32_t)att == tg0;
+          const bool wrong = in_attr && !term;
+          int tt = (int)tt0 + 1;
+          tt = tt > 255 ? 255 : tt;
+          const bool trunc = u_hz > 0 && tt >= u_hz;
+          const bool reset = (u_fl & 8u) && (term || trunc);
+          const uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) |
+                              ((uint32_t)pert << 3) | ((uint32_t)reset << 4);
+          if (valid) {
+            a.reward[CK(t * n + le, n_steps * n, 11)] = term ? r_term : (wrong ? r_wrong : r_none);
+            a.flags[CK(t * n + le, n_steps * n, 15)] = (uint8_t)fl;
+          }
+          tg0 = reset ? (info & 0xFFu) : tg0;
+          tt0 = reset ? 0u : (uint32_t)tt;
+#pragma unroll
+          for (int w = 0; w < W; ++w) st[w] = reset ? rs[w] : sp[w];
         }
       }
-      if (W > 1 || u_mnf > kNodeRecs)
-#endif
-#pragma unroll
-      for (int r = 0; r < W; ++r) {
-        const int i = l32 + 32 * r;
-        int ii = i < N ? i : 0;
-        asm volatile("" : "+v"(ii));   // selector and record reads stay in the step loop
-        uint4 rec_r[kNodeRecs];
-#pragma unroll
-        for (int q = 0; q < kNodeRecs; ++q) rec_r[q] = recL[q * 32 * W + ii];
-        const int nf = (int)rec_r[0].w;
-        uint32_t x = 0;
-        if (u_mnf > kNodeRecs) {   // chain tail of nodes with more than kNodeRecs functions
-          const int f0 = (int)rec_r[1].w;
-          for (int j = nf - 1; j >= kNodeRecs; --j) {
-            const uint4 rc = a.fcompact[CK(f0 + j, a.n_funcs, 9)];
-            const uint32_t fj = eval_compact(rc.x, rc.y, Sg);
-            x = (j == nf - 1) ? fj : bfi(lt_in[j * 64 * W + ii], fj, x);
-          }
-        }
-        const uint4* sel = selq + ii;
-        const uint32_t* lti = lt_in + ii;
-        switch (u_mnf) {
-          case 1: x = chain_from_masks<1>(rec_r, sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
-          case 2: x = chain_from_masks<2>(rec_r, sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
-          case 3: x = chain_from_masks<3>(rec_r, sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
-          default: x = chain_from_masks<4>(rec_r, sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
-        }
-        X[r] = i < N ? x : 0u;
-      }
-      PBN_PSTAMP_AT(k, 12);
-      uint32_t sp[W];
-#pragma unroll
-      for (int w = 0; w < W; ++w) sp[w] = lane_transpose32(X[w], lane);
-      PBN_PSTAMP_AT(k, 13);
-      {
-        // branch-free epilogue (this wave bounds the iteration): only the stores are guarded
-        const bool pert = (info >> 16) & 1u;
-        const uint32_t pc = (info >> 8) & 0xFFu;
-#pragma unroll
-        for (int w = 0; w < W; ++w) sp[w] = pert ? (s1[w] ^ gam[w]) : sp[w];
-        if (valid && (u_fl & 2u)) {
-#pragma unroll
-          for (int w = 0; w < W; ++w) a.final_state[CK(t * plane + (size_t)w * n + le, (size_t)n_steps * plane, 10)] = sp[w];
-        }
-        // reward candidates depend only on popcount(flipmask): read them beside the hash
-        const float r_none = rtab[pc], r_wrong = rtab[(N + 1) + pc], r_term = rtab[2 * (N + 1) + pc];
-        int att = -1;
-        if (u_hb > 0) {
-          const int hmask = (1 << u_hb) - 1;
-          const uint32_t* hid = htab + (size_t)W * (hmask + 1);
-          uint32_t h = 0;
-#pragma unroll
-          for (int w = 0; w < W; ++w) h += sp[w] * a.hash_mult[w];
-          h >>= (32 - u_hb);
-          // the table is usually collision-free (one probe); keys are unique, so probe order
-          // does not matter
-          {
-            const uint32_t slot_i = h & hmask;
-            uint32_t eq = 1u;
-#pragma unroll
-            for (int w = 0; w < W; ++w) eq &= (htab[(size_t)w * (hmask + 1) + slot_i] == sp[w]) ? 1u : 0u;
-            const uint32_t id = hid[slot_i];
-            att = (eq != 0u && id != 0xFFFFFFFFu) ? (int)id : att;
-          }
-          for (int pr = 1; pr < u_hp; ++pr) {
-            const uint32_t slot_i = (h + pr) & hmask;
-            bool eq = true;
-#pragma unroll
-            for (int w = 0; w < W; ++w) eq = eq && (htab[(size_t)w * (hmask + 1) + slot_i] == sp[w]);
-            const uint32_t id = hid[slot_i];
-            if (eq && id != 0xFFFFFFFFu) att = (int)id;
-          }
-        }
-        const bool in_attr = att >= 0;
-        const bool term = in_attr && (uint32_t)att == tg0;
-        const bool wrong = in_attr && !term;
-        int tt = (int)tt0 + 1;
-        tt = tt > 255 ? 255 : tt;
-        const bool trunc = u_hz > 0 && tt >= u_hz;
-        const bool reset = (u_fl & 8u) && (term || trunc);
-        const uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) |
-                            ((uint32_t)pert << 3) | ((uint32_t)reset << 4);
-        if (valid) {
-          a.reward[CK(t * n + le, n_steps * n, 11)] = term ? r_term : (wrong ? r_wrong : r_none);
-          a.flags[CK(t * n + le, n_steps * n, 15)] = (uint8_t)fl;
-        }
-        tg0 = reset ? (info & 0xFFu) : tg0;
-        tt0 = reset ? 0u : (uint32_t)tt;
-#pragma unroll
-        for (int w = 0; w < W; ++w) st[w] = reset ? rs[w] : sp[w];
-      }
+      PBN_PSTAMP(k, 1);
+      lds_barrier();
+      PBN_PSTAMP(k, 2);
     }
-    PBN_PSTAMP(k, 1);
-    lds_barrier();
-    PBN_PSTAMP(k, 2);
-  }
-  if (role == 0 && valid) {
+    if (valid) {
 #pragma unroll
-    for (int w = 0; w < W; ++w) a.state_out[CK((size_t)w * n + le, plane, 16)] = st[w];
-    a.t[CK(le, n, 17)] = (uint8_t)tt0;
-    a.target[CK(le, n, 18)] = (uint8_t)tg0;
+      for (int w = 0; w < W; ++w) a.state_out[CK((size_t)w * n + le, plane, 16)] = st[w];
+      a.t[CK(le, n, 17)] = (uint8_t)tt0;
+      a.target[CK(le, n, 18)] = (uint8_t)tg0;
+    }
   }
 }
 
@@ -1673,9 +1718,13 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     std::vector<uint32_t> sel((size_t)kNodeRecs * 2 * 32 * W * 4, 0x0C0C0C0Cu);
     for (int i = 0; i < N; ++i) {
       const int f0 = d->node_func_start[i], nf = d->node_func_start[i + 1] - f0;
-      for (int q = 0; q < kNodeRecs && q < nf; ++q) {
-        const uint32_t T = d->func_table[f0 + q];
-        const int k = d->func_arity[f0 + q];
+      // records beyond a node's last function (up to kNodeRecs) repeat the last one: the
+      // pipelined kernel's chain then needs no per-lane function count (x = lt ? f : x with
+      // f == x is x)
+      for (int q = 0; q < kNodeRecs; ++q) {
+        const int qf = std::min(q, nf - 1);
+        const uint32_t T = d->func_table[f0 + qf];
+        const int k = d->func_arity[f0 + qf];
         for (int mm = 0; mm < 8; ++mm) {
           // table bit of input index m (missing inputs read plane 0 but do not matter)
           auto bit = [&](uint32_t m) { return (T >> (k >= 5 ? m : (m & ((1u << k) - 1u)))) & 1u; };
@@ -1745,7 +1794,12 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   net->nrec_off = (int)tab.size();
   for (int q = 0; q < kNodeRecs; ++q)
     for (int i = 0; i < 32 * W; ++i) {
-      const uint4 r4 = i < N ? nrec[(size_t)i * kNodeRecs + q] : make_uint4(0, 0, 0, 0);
+      uint4 r4 = i < N ? nrec[(size_t)i * kNodeRecs + q] : make_uint4(0, 0, 0, 0);
+      if (i < N) {   // padded inputs as the selectors above (the .w metadata stays)
+        const int nf = d->node_func_start[i + 1] - d->node_func_start[i];
+        if (q >= nf) r4.x = nrec[(size_t)i * kNodeRecs + nf - 1].x;
+      }
+      if (W <= 2) r4.x *= 4u;   // plane byte offsets (every index < 64: no carry between bytes)
       tab.push_back(r4.x); tab.push_back(r4.y); tab.push_back(r4.z); tab.push_back(r4.w);
     }
   // gate records by level: {input plane indices as bytes, 16-bit table (unused inputs
