@@ -121,29 +121,39 @@ class NpPBN:
     def _bit(self, words: np.ndarray, i: int) -> np.ndarray:
         return (words[i >> 5] >> np.uint32(i & 31)) & np.uint32(1)
 
-    def reset_from_words(self, seed: int, e: np.ndarray, step: int, hi: np.ndarray, lo: np.ndarray):
-        """(state words (W, n), target ids (n,)) from the 64-bit uniform (hi:lo) per env
-        (pyoracle.reset_from_words)."""
-        n = len(e)
+    def reset_draw(self, hi: np.ndarray, lo: np.ndarray):
+        """Attractor draws from the 64-bit uniforms (hi:lo) per env (pyoracle.reset_draw; A >= 1):
+        (state words (W, n), target ids (n,), hi', lo')."""
+        n = len(hi)
         A = self.A
-        if A >= 1:
-            a_s = np.zeros(n, dtype=np.int64)
-            a_t = np.zeros(n, dtype=np.int64)
-            if A >= 2:
-                c, hi, lo = ext64(hi, lo, A * (A - 1))
-                a_s, a_t = c // (A - 1), c % (A - 1)
-                a_t += (a_t >= a_s)
-            size = np.asarray(self.att_len, dtype=np.int64)[a_s]
-            idx, hi, lo = ext64(hi, lo, size)
-            rows = np.asarray(self.att_first, dtype=np.int64)[a_s] + idx
-            state = self.att_words[rows].T.copy()
-            return state, a_t.astype(np.uint8)
+        a_s = np.zeros(n, dtype=np.int64)
+        a_t = np.zeros(n, dtype=np.int64)
+        if A >= 2:
+            c, hi, lo = ext64(hi, lo, A * (A - 1))
+            a_s, a_t = c // (A - 1), c % (A - 1)
+            a_t += (a_t >= a_s)
+        size = np.asarray(self.att_len, dtype=np.int64)[a_s]
+        idx, hi, lo = ext64(hi, lo, size)
+        rows = np.asarray(self.att_first, dtype=np.int64)[a_s] + idx
+        state = self.att_words[rows].T.copy()
+        return state, a_t.astype(np.uint8), hi, lo
+
+    def random_state(self, seed: int, e: np.ndarray, step: int):
+        n = len(e)
         r = _draw(seed, e, step, RESET, 1)
         state = np.zeros((self.W, n), dtype=np.uint32)
         for w in range(self.W):
             nb = min(32, self.n - 32 * w)
             state[w] = r[w] & np.uint32(0xFFFFFFFF if nb == 32 else (1 << nb) - 1)
         return state, np.full(n, 0xFF, dtype=np.uint8)
+
+    def reset_from_words(self, seed: int, e: np.ndarray, step: int, hi: np.ndarray, lo: np.ndarray):
+        """pbn_reset's draw: (state words (W, n), target ids (n,)) from the 64-bit uniform (hi:lo)
+        per env (pyoracle.reset_from_words)."""
+        if self.A >= 1:
+            state, tgt, _, _ = self.reset_draw(hi, lo)
+            return state, tgt
+        return self.random_state(seed, e, step)
 
     def reset(self, seed: int, step: int, env_offset: int, n: int):
         e = np.arange(n, dtype=np.uint64) + np.uint64(env_offset)
@@ -156,11 +166,17 @@ class NpPBN:
         state = np.asarray(state, dtype=np.uint32)
         n = state.shape[1]
         e = np.arange(n, dtype=np.uint64) + np.uint64(env_offset)
+        # one ENV call: words 0, 1 = gaps 0, 1; X = words 3:2 gives, in order, the action draw
+        # (every mode), the autoreset draws and gap 2's uniform (pyoracle.step)
         E = _draw(seed, e, step, ENV, 0)
-        F = _draw(seed, e, step, ENV, 1)
+        c, hi, lo = ext64(E[3], E[2], (n_nodes + 1) ** 3)
+        reset_to = None
+        if self.A >= 1:
+            rs, rt, hi, lo = self.reset_draw(hi, lo)
+            reset_to = (rs, rt)
+        u2 = hi
         if mode & MODE_RANDOM_ACTIONS:
             flip = np.zeros((W, n), dtype=np.uint32)
-            c, _, _ = ext64(E[3], E[2], (n_nodes + 1) ** 3)
             for k in range(3):
                 c, a = c // (n_nodes + 1), c % (n_nodes + 1)
                 for w in range(W):
@@ -169,18 +185,20 @@ class NpPBN:
         else:
             flip = np.asarray(flipmask, dtype=np.uint32).copy()
         s1 = state ^ flip
-        # perturbation: geometric gaps from ENV words 0, 1 of calls 0, 1, then PERT calls
+        # perturbation: geometric gaps from ENV words 0, 1, u2, then PERT calls
         gamma = np.zeros((W, n), dtype=np.uint32)
         pos = np.full(n, -1, dtype=np.int64)
         live = np.ones(n, dtype=bool)
         k, P = 0, None
         while live.any():
-            if k < 4:
-                u = (F if k >= 2 else E)[k & 1]
+            if k < 2:
+                u = E[k]
+            elif k == 2:
+                u = u2
             else:
-                if (k - 4) % 4 == 0:
-                    P = _draw(seed, e, step, PERT, (k - 4) // 4)
-                u = P[(k - 4) % 4]
+                if (k - 3) % 4 == 0:
+                    P = _draw(seed, e, step, PERT, (k - 3) // 4)
+                u = P[(k - 3) % 4]
             k += 1
             gap = np.searchsorted(self.cdf, u.astype(np.uint64), side="right") + 1
             pos = np.where(live, pos + gap, pos)
@@ -243,7 +261,10 @@ class NpPBN:
         if mode & MODE_AUTORESET:
             done = term | trunc
             if done.any():
-                ns, ntg = self.reset_from_words(seed, e[done], step, F[3][done], F[2][done])
+                if reset_to is not None:
+                    ns, ntg = reset_to[0][:, done], reset_to[1][done]
+                else:
+                    ns, ntg = self.random_state(seed, e[done], step)
                 state_out[:, done] = ns
                 tgt[done] = ntg
                 t_out[done] = 0

@@ -127,27 +127,36 @@ static uint32_t ext64(uint32_t* hi, uint32_t* lo, uint32_t K) {
   return (uint32_t)(b >> 32);
 }
 
-/* reset formula shared by pbn_reset (RESET call 0, words 1:0) and autoreset (ENV call 1,
- * words 3:2): start attractor a_s and target a_t != a_s in one draw over A(A-1) pairs, then
- * the start state uniformly within a_s */
+/* the attractor draws of a reset from the 64-bit uniform X = (hi:lo), advancing X: start
+ * attractor a_s and target a_t != a_s in one draw over the A(A-1) pairs (A >= 2), then the start
+ * state uniformly within a_s; *sidx = its row in attractor_states (A >= 1) */
+static void reset_draw(const pbn_net_desc* d, uint32_t* hi, uint32_t* lo, int* sidx, uint8_t* target) {
+  int A = d->n_attractors;
+  uint32_t as = 0, at = 0;
+  if (A >= 2) {
+    uint32_t c = ext64(hi, lo, (uint32_t)A * (uint32_t)(A - 1));
+    as = c / (uint32_t)(A - 1);
+    at = c % (uint32_t)(A - 1);
+    at += (at >= as);
+  }
+  int start = d->attractor_start[as];
+  uint32_t size = (uint32_t)(d->attractor_start[as + 1] - start);
+  uint32_t idx = ext64(hi, lo, size);
+  *sidx = start + (int)idx;
+  *target = (uint8_t)at;
+}
+
+/* pbn_reset: the attractor draws from RESET call 0 words 1:0, or (no attractors) a uniform
+ * random state from RESET call 1 */
 static void reset_one(const pbn_net_desc* d, uint64_t seed, uint64_t e, uint64_t step, uint32_t hi, uint32_t lo,
                       uint32_t* state, uint8_t* target) {
   int N = d->n_nodes, W = words_of(N), A = d->n_attractors;
   uint32_t vm[4];
   valid_mask(N, W, vm);
   if (A >= 1) {
-    uint32_t as = 0, at = 0;
-    if (A >= 2) {
-      uint32_t c = ext64(&hi, &lo, (uint32_t)A * (uint32_t)(A - 1));
-      as = c / (uint32_t)(A - 1);
-      at = c % (uint32_t)(A - 1);
-      at += (at >= as);
-    }
-    int start = d->attractor_start[as];
-    uint32_t size = (uint32_t)(d->attractor_start[as + 1] - start);
-    uint32_t idx = ext64(&hi, &lo, size);
-    for (int w = 0; w < W; ++w) state[w] = d->attractor_states[(size_t)(start + idx) * W + w];
-    *target = (uint8_t)at;
+    int sidx;
+    reset_draw(d, &hi, &lo, &sidx, target);
+    for (int w = 0; w < W; ++w) state[w] = d->attractor_states[(size_t)sidx * W + w];
   } else {
     uint32_t r[4];
     draw(seed, e, step, STREAM_RESET, 1, r);
@@ -196,17 +205,23 @@ int oracle_step(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t en
       uint32_t vm[4], s[4] = {0, 0, 0, 0}, m[4] = {0, 0, 0, 0}, s1[4], gam[4] = {0, 0, 0, 0},
                sp[4] = {0, 0, 0, 0};
       valid_mask(N, W, vm);
-      uint32_t E[4], F[4];
+      /* one ENV call per env-step: words 0, 1 are the first two perturbation gaps; words 3:2
+       * are a 64-bit uniform X from which, in this order, the action draw, the autoreset draws
+       * and the third gap's uniform (the top word of what remains of X) are taken */
+      uint32_t E[4];
       draw(seed, e, step, STREAM_ENV, 0, E);
-      draw(seed, e, step, STREAM_ENV, 1, F);
       for (int w = 0; w < W; ++w) s[w] = state[(size_t)w * n + li] & vm[w];
+      uint32_t hi = E[3], lo = E[2], n1 = (uint32_t)(N + 1);
+      uint32_t c = ext64(&hi, &lo, n1 * n1 * n1);   /* drawn in every mode */
+      int rs_idx = 0;
+      uint8_t rs_tg = PBN_NO_TARGET;
+      if (d->n_attractors >= 1) reset_draw(d, &hi, &lo, &rs_idx, &rs_tg);
+      const uint32_t u2 = hi;
       /* 1-2. interventions: 0 = no-op, a > 0 flips node a-1, each distinct node once
        *      (bdq_model/__init__.py:76-84 explore branch, :176 action.unique()) */
       if (mode & PBN_MODE_RANDOM_ACTIONS) {
         /* three actions uniform on [0, N] (np.random.randint(0, N+1, 3), bdq_model/__init__.py:76):
-         * the base-(N+1) digits of one draw over (N+1)^3 from ENV words 3:2 */
-        uint32_t hi = E[3], lo = E[2], n1 = (uint32_t)(N + 1);
-        uint32_t c = ext64(&hi, &lo, n1 * n1 * n1);
+         * the base-(N+1) digits of one draw over (N+1)^3 */
         for (int k = 0; k < 3; ++k) {
           uint32_t a = c % n1;
           c /= n1;
@@ -217,17 +232,18 @@ int oracle_step(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t en
         for (int w = 0; w < W; ++w) m[w] = flipmask[(size_t)w * n + li] & vm[w];
       }
       for (int w = 0; w < W; ++w) s1[w] = s[w] ^ m[w];
-      /* 3. perturbation: gaps between flipped nodes are geometric(p) draws; gaps 0-3 are
-       *    ENV words 0, 1 of calls 0, 1; gap k >= 4 is PERT call (k-4)>>2, word (k-4)&3 */
+      /* 3. perturbation: gaps between flipped nodes are geometric(p) draws; gaps 0, 1 are ENV
+       *    words 0, 1, gap 2 is u2, gap k >= 3 is PERT call (k-3)>>2, word (k-3)&3 */
       {
         int pos = -1, k = 0;
         uint32_t P[4];
         while (pos < N - 1) {
           uint32_t u;
-          if (k < 4) u = (k & 2) ? F[k & 1] : E[k & 1];
+          if (k < 2) u = E[k];
+          else if (k == 2) u = u2;
           else {
-            if (((k - 4) & 3) == 0) draw(seed, e, step, STREAM_PERT, (uint32_t)((k - 4) >> 2), P);
-            u = P[(k - 4) & 3];
+            if (((k - 3) & 3) == 0) draw(seed, e, step, STREAM_PERT, (uint32_t)((k - 3) >> 2), P);
+            u = P[(k - 3) & 3];
           }
           ++k;
           pos += gap_of(d, u);
@@ -272,11 +288,15 @@ int oracle_step(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t en
       if (final_state)
         for (int w = 0; w < W; ++w) final_state[(size_t)w * n + li] = sp[w];
       if ((mode & PBN_MODE_AUTORESET) && (term || trunc)) {
-        uint32_t ns[4];
-        uint8_t tg;
-        reset_one(d, seed, e, step, F[3], F[2], ns, &tg);
-        for (int w = 0; w < W; ++w) state_out[(size_t)w * n + li] = ns[w];
-        target[li] = tg;
+        if (d->n_attractors >= 1) {
+          for (int w = 0; w < W; ++w) state_out[(size_t)w * n + li] = d->attractor_states[(size_t)rs_idx * W + w];
+          target[li] = rs_tg;
+        } else {
+          uint32_t r[4];
+          draw(seed, e, step, STREAM_RESET, 1, r);
+          for (int w = 0; w < W; ++w) state_out[(size_t)w * n + li] = r[w] & vm[w];
+          target[li] = PBN_NO_TARGET;
+        }
         t[li] = 0;
         fl |= PBN_FLAG_RESET;
       } else {

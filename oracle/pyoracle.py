@@ -63,23 +63,30 @@ class PyPBN:
                 return m
         return self.n + 1
 
-    def reset_from_words(self, seed: int, e: int, step: int, hi: int, lo: int):
-        """(start state, target id) from the 64-bit uniform (hi:lo): one draw over the A(A-1)
-        ordered (start, target) pairs, then the state uniformly within the start attractor."""
+    def reset_draw(self, x: int):
+        """Attractor draws from the 64-bit uniform x: one draw over the A(A-1) ordered (start,
+        target) pairs (A >= 2), then the state uniformly within the start attractor.  Returns
+        (start state, target id, what remains of x); A >= 1."""
         A = len(self.spec.attractors)
-        if A >= 1:
-            x = (hi << 32) | lo
-            a_s = a_t = 0
-            if A >= 2:
-                c, x = ext64(x, A * (A - 1))
-                a_s, a_t = divmod(c, A - 1)
-                a_t += a_t >= a_s
-            att = self.spec.attractors[a_s]
-            idx, x = ext64(x, len(att))
-            return list(att[idx]), a_t
+        a_s = a_t = 0
+        if A >= 2:
+            c, x = ext64(x, A * (A - 1))
+            a_s, a_t = divmod(c, A - 1)
+            a_t += a_t >= a_s
+        att = self.spec.attractors[a_s]
+        idx, x = ext64(x, len(att))
+        return list(att[idx]), a_t, x
+
+    def random_state(self, seed: int, e: int, step: int):
         r = draw(seed, e, step, RESET, 1)
-        bits = [(r[i >> 5] >> (i & 31)) & 1 for i in range(self.n)]
-        return bits, 0xFF
+        return [(r[i >> 5] >> (i & 31)) & 1 for i in range(self.n)], 0xFF
+
+    def reset_from_words(self, seed: int, e: int, step: int, hi: int, lo: int):
+        """pbn_reset's draw: (start state, target id) from the 64-bit uniform (hi:lo)."""
+        if self.spec.attractors:
+            state, tgt, _ = self.reset_draw((hi << 32) | lo)
+            return state, tgt
+        return self.random_state(seed, e, step)
 
     def reset(self, seed: int, step: int, e: int):
         R = draw(seed, e, step, RESET, 0)
@@ -90,11 +97,17 @@ class PyPBN:
              mode: int):
         n, B = self.n, self.spec.prob_bits
         G, b = e >> 5, e & 31
+        # one ENV call: words 0, 1 = gaps 0, 1; X = words 3:2 gives, in order, the action draw
+        # (every mode), the autoreset draws and gap 2's uniform (the top word of what remains)
         E = draw(seed, e, step, ENV, 0)
-        F = draw(seed, e, step, ENV, 1)
+        c, x = ext64((E[3] << 32) | E[2], (n + 1) ** 3)   # 3 uniform ints in [0, N] (:76)
+        reset_to = None
+        if self.spec.attractors:
+            rs, rt, x = self.reset_draw(x)
+            reset_to = (rs, rt)
+        u2 = x >> 32
         if mode & MODE_RANDOM_ACTIONS:
             flip = [0] * n
-            c, _ = ext64((E[3] << 32) | E[2], (n + 1) ** 3)   # 3 uniform ints in [0, N] (:76)
             for k in range(3):
                 c, a = divmod(c, n + 1)
                 if a > 0:
@@ -103,12 +116,14 @@ class PyPBN:
         gamma = [0] * n
         pos, k, P = -1, 0, None
         while pos < n - 1:
-            if k < 4:
-                u = (F if k >= 2 else E)[k & 1]
+            if k < 2:
+                u = E[k]
+            elif k == 2:
+                u = u2
             else:
-                if (k - 4) % 4 == 0:
-                    P = draw(seed, e, step, PERT, (k - 4) // 4)
-                u = P[(k - 4) % 4]
+                if (k - 3) % 4 == 0:
+                    P = draw(seed, e, step, PERT, (k - 3) // 4)
+                u = P[(k - 3) % 4]
             k += 1
             pos += self.gap(u)
             if pos >= n:
@@ -141,7 +156,7 @@ class PyPBN:
         flags = int(term) | (int(trunc) << 1) | (int(in_attr) << 2) | (int(perturbed) << 3)
         out = {"final_state": sp, "reward": reward, "flipmask": flip, "target": target}
         if (mode & MODE_AUTORESET) and (term or trunc):
-            ns, tg = self.reset_from_words(seed, e, step, F[3], F[2])
+            ns, tg = reset_to if reset_to is not None else self.random_state(seed, e, step)
             out.update(state_out=ns, target=tg, t=0, flags=flags | 16)
         else:
             out.update(state_out=sp, t=tt, flags=flags)

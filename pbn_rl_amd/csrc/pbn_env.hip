@@ -108,6 +108,8 @@ struct StepArgs {
   int att_single;    // every attractor is one state: the reset state is attractor a's state a
   uint32_t n1_magic; // ceil(2^32 / (N + 1)): random-action digits
   uint32_t am1_magic;  // ceil(2^32 / (A - 1)) for A >= 2: autoreset (start, target) split
+  uint64_t x_mult;     // (N+1)^3 * A(A-1) (A >= 2) mod 2^64: what the ENV draws before gap 2 leave
+                       // of X is X * x_mult (times the start attractor's size, multi-state nets)
 };
 
 // In-kernel phase clocks (cdna_hip_programming.md section 7, "In-kernel stamps"):
@@ -181,13 +183,12 @@ __device__ __forceinline__ uint32_t ext64(uint32_t& hi, uint32_t& lo, uint32_t K
   return (uint32_t)(y >> 32);
 }
 
-// Three actions uniform on [0, N]: the base-(N+1) digits of one draw over (N+1)^3 from the
-// 64-bit value (hi:lo).  Division by N+1 is a multiply-high by magic = ceil(2^32 / (N+1)),
-// exact for c * (N+1) < 2^32 (c < (N+1)^3 <= 129^3).
+// Three actions uniform on [0, N]: the base-(N+1) digits of c, one draw over (N+1)^3.
+// Division by N+1 is a multiply-high by magic = ceil(2^32 / (N+1)), exact for c * (N+1) < 2^32
+// (c < (N+1)^3 <= 129^3).
 template <int W>
-__device__ __forceinline__ void random_actions3(uint32_t hi, uint32_t lo, int N, uint32_t magic, uint32_t (&m)[W]) {
+__device__ __forceinline__ void actions_from_draw(uint32_t c, int N, uint32_t magic, uint32_t (&m)[W]) {
   const uint32_t n1 = (uint32_t)(N + 1);
-  uint32_t c = ext64(hi, lo, n1 * n1 * n1);
 #pragma unroll
   for (int q = 0; q < 3; ++q) {   // action a in [0, N]: 0 = no-op, else flip node a-1
     const uint32_t qt = __umulhi(c, magic);
@@ -448,7 +449,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   constexpr int CPN = B / 4;               // selection calls per node
   constexpr int H = (CPN + 1) / 2;         // of which the lower half computes H
   constexpr int NLO = 1 + W * H;           // lower list: ENV, SEL(c < H)
-  constexpr int NUP = W * (CPN - H) + 1;   // upper list: SEL(c >= H), ENV call 1
+  constexpr int NUP = W * (CPN - H);       // upper list: SEL(c >= H)
   constexpr int IT = NLO > NUP ? NLO : NUP;
   constexpr int UPC = (CPN - H) > 0 ? (CPN - H) : 1;  // divisor guard (B = 4: no upper calls)
   extern __shared__ uint32_t smem[];
@@ -555,8 +556,8 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
       const int r = it / UPC;
       const int c = H + it % UPC;
       uc0 = G_lo; uc2 = (pbn::kStreamSel << 28) | (uint32_t)(4 * (l32 + 32 * r) + c); uc3 = G_hi;
-    } else {
-      uc0 = ge_lo; uc2 = (pbn::kStreamEnv << 28) | 1u; uc3 = ge_hi;
+    } else {   // (upper list done: a discarded call)
+      uc0 = ge_lo; uc2 = pbn::kStreamEnv << 28; uc3 = ge_hi;
     }
     out[it] = pbn::philox4x32_10(lo ? lc0 : uc0, st_lo, lo ? lc2 : uc2, lo ? lc3 : uc3, kk0, kk1);
   }
@@ -571,7 +572,6 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
       dig[r][4 * c + 0] = d.x; dig[r][4 * c + 1] = d.y; dig[r][4 * c + 2] = d.z; dig[r][4 * c + 3] = d.w;
     }
   }
-  const Word4 F = upper_to_lower(out[W * (CPN - H)]);   // ENV call 1 of env l32
   const Word4 E = out[0];
 
   // ---- 2. per env (lower lanes): interventions, perturbation, reset word
@@ -581,9 +581,30 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   bool pert = false;
 #pragma unroll
   for (int w = 0; w < W; ++w) gam[w] = 0;
+  // ENV words 3:2 = a 64-bit uniform X: the action draw (every mode), the autoreset draws,
+  // then gap 2's uniform u2 = what remains of X's top word (DESIGN.md "Step semantics")
+  uint32_t r_row = 0, r_nt = 0, u2 = 0;
   if (lo) {
+    uint32_t xhi = E.w, xlo = E.z;
+    const uint32_t n1 = (uint32_t)(N + 1);
+    const uint32_t c_act = ext64(xhi, xlo, n1 * n1 * n1);
+    if (a.n_attr >= 1) {
+      const int32_t* att_first = reinterpret_cast<const int32_t*>(L + a.att_off);
+      const uint32_t A = (uint32_t)a.n_attr;
+      uint32_t as = 0;
+      if (A >= 2) {
+        const uint32_t c = ext64(xhi, xlo, A * (A - 1));
+        as = a.am1_magic ? __umulhi(c, a.am1_magic) : c;   // c / (A - 1)
+        r_nt = c - as * (A - 1);
+        r_nt += (r_nt >= as) ? 1u : 0u;
+      }
+      // (single-state attractors: the draw over one state is 0 and state a is attractor a's)
+      const int st0 = a.att_single ? (int)as : att_first[as];
+      r_row = (uint32_t)st0 + (a.att_single ? 0u : ext64(xhi, xlo, (uint32_t)(att_first[as + 1] - st0)));
+    }
+    u2 = xhi;
     if (random_actions) {
-      random_actions3<W>(E.w, E.z, N, a.n1_magic, m);
+      actions_from_draw<W>(c_act, N, a.n1_magic, m);
 #pragma unroll
       for (int w = 0; w < W; ++w) a.flipmask[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 8)] = m[w];
     } else {
@@ -597,32 +618,29 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
       s1[w] ^= m[w];
     }
     // perturbation positions are prefix sums of geometric gaps; the first three gaps
-    // (u = E.x, E.y, F.x) are independent, so they are computed side by side
+    // (u = E.x, E.y, u2) are independent, so they are computed side by side
     int g0, g1, g2;
     if (a.gap_exact == 2) {
-      g0 = gap_any(2, L, a, E.x); g1 = gap_any(2, L, a, E.y); g2 = gap_any(2, L, a, F.x);
+      g0 = gap_any(2, L, a, E.x); g1 = gap_any(2, L, a, E.y); g2 = gap_any(2, L, a, u2);
     } else if (a.gap_exact) {
-      g0 = gap_of(cdf, a.cdf_len, E.x); g1 = gap_of(cdf, a.cdf_len, E.y); g2 = gap_of(cdf, a.cdf_len, F.x);
+      g0 = gap_of(cdf, a.cdf_len, E.x); g1 = gap_of(cdf, a.cdf_len, E.y); g2 = gap_of(cdf, a.cdf_len, u2);
     } else {
       g0 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.x);
       g1 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.y);
-      g2 = gap_est(cdf, a.cdf_len, a.inv_log2q, F.x);
+      g2 = gap_est(cdf, a.cdf_len, a.inv_log2q, u2);
     }
     const int p0 = g0 - 1, p1 = p0 + g1, p2 = p1 + g2;
     set_bit<W>(gam, p0, N);
     set_bit<W>(gam, p1, N);
     set_bit<W>(gam, p2, N);
-    if (p2 < N - 1) {   // rare: a fourth flip is possible (gap 3 = F.y, gap k >= 4: PERT call (k-4)>>2, word (k-4)&3)
-      Word4 P = F;
+    if (p2 < N - 1) {   // rare: a fourth flip is possible (gap k >= 3: PERT call (k-3)>>2, word (k-3)&3)
+      Word4 P = E;
       int pos = p2;
       for (int kk = 3; pos < N - 1; ++kk) {
-        uint32_t u = F.y;
-        if (kk >= 4) {
-          if (((kk - 4) & 3) == 0)
-            P = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamPert << 28) | (uint32_t)((kk - 4) >> 2), ge_hi, kk0, kk1);
-          const int j4 = (kk - 4) & 3;
-          u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
-        }
+        if (((kk - 3) & 3) == 0)
+          P = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamPert << 28) | (uint32_t)((kk - 3) >> 2), ge_hi, kk0, kk1);
+        const int j4 = (kk - 3) & 3;
+        const uint32_t u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
         pos += gap_any(a.gap_exact, L, a, u);
         set_bit<W>(gam, pos, N);
       }
@@ -752,25 +770,11 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) | ((uint32_t)pert << 3);
   if ((a.mode & PBN_MODE_AUTORESET) && (term || trunc)) {
     uint32_t nt;
-    if (a.n_attr >= 1) {
-      // attractor tables from the LDS image: start[A+1] then states[S][W]; (start, target)
-      // in one draw over the A(A-1) pairs, then the state within the start attractor
-      const int32_t* att_first = reinterpret_cast<const int32_t*>(L + a.att_off);
+    if (a.n_attr >= 1) {   // the attractor draws of step 2 (attractor states from the LDS image)
       const uint32_t* att_words = L + a.att_off + a.n_attr + 1;
-      const uint32_t A = (uint32_t)a.n_attr;
-      uint32_t hi = F.w, lo = F.z, as = 0;
-      nt = 0;
-      if (A >= 2) {
-        const uint32_t c = ext64(hi, lo, A * (A - 1));
-        as = a.am1_magic ? __umulhi(c, a.am1_magic) : c;   // c / (A - 1)
-        nt = c - as * (A - 1);
-        nt += (nt >= as) ? 1u : 0u;
-      }
-      // (single-state attractors: the draw over one state is 0 and state a is attractor a's)
-      const int st0 = a.att_single ? (int)as : att_first[as];
-      const uint32_t idx = a.att_single ? 0u : ext64(hi, lo, (uint32_t)(att_first[as + 1] - st0));
 #pragma unroll
-      for (int w = 0; w < W; ++w) sp[w] = att_words[(size_t)(st0 + idx) * W + w];
+      for (int w = 0; w < W; ++w) sp[w] = att_words[(size_t)r_row * W + w];
+      nt = r_nt;
     } else {
       const Word4 rr = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamReset << 28) | 1u, ge_hi, kk0, kk1);
       const uint32_t rw4[4] = {rr.x, rr.y, rr.z, rr.w};
@@ -996,13 +1000,53 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
         const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
         const uint32_t ge_lo = (uint32_t)ge;
         if (valid) {
+          // one ENV call: words 0, 1 = gaps 0, 1; X = words 3:2 gives, in order, the action draw
+          // (every mode), the autoreset draws and gap 2's uniform u2 (DESIGN.md "Step semantics")
           const Word4 E = pbn::philox4x32_10(ge_lo, st_lo, pbn::kStreamEnv << 28, ge_hi, u_k0, u_k1);
-          const Word4 F = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamEnv << 28) | 1u, ge_hi, u_k0, u_k1);
           uint32_t m[W], gam[W], rs[W];
 #pragma unroll
           for (int w = 0; w < W; ++w) { m[w] = 0; gam[w] = 0; rs[w] = 0; }
+          uint32_t xhi = E.w, xlo = E.z;
+          const uint32_t n1 = (uint32_t)(N + 1);
+          const uint32_t c_act = ext64(xhi, xlo, n1 * n1 * n1);
+          // X after the action and pair draws, X * x_mult mod 2^64, as one product off the
+          // draws' dependency chain
+          uint64_t xr = ((((uint64_t)E.w) << 32) | E.z) * a.x_mult;
+          // autoreset draw (used by wave 0 only if the env's episode ends): (start, target) in
+          // one draw over the A(A-1) pairs, then the state within the start attractor
+          uint32_t rt;
+          if (u_na >= 1) {
+            const int32_t* att_first = reinterpret_cast<const int32_t*>(L + a.att_off);
+            const uint32_t* att_words = L + a.att_off + u_na + 1;
+            const uint32_t A = (uint32_t)u_na;
+            uint32_t as = 0;
+            rt = 0;
+            if (A >= 2) {
+              const uint32_t c = ext64(xhi, xlo, A * (A - 1));
+              as = a.am1_magic ? __umulhi(c, a.am1_magic) : c;   // c / (A - 1)
+              rt = c - as * (A - 1);
+              rt += (rt >= as) ? 1u : 0u;
+            }
+            // (single-state attractors: the draw over one state is 0 and state a is attractor a's)
+            const int st0 = (u_fl & 16u) ? (int)as : att_first[as];
+            uint32_t idx = 0;
+            if (!(u_fl & 16u)) {
+              const uint32_t size = (uint32_t)(att_first[as + 1] - st0);
+              idx = ext64(xhi, xlo, size);
+              xr *= size;
+            }
+#pragma unroll
+            for (int w = 0; w < W; ++w) rs[w] = att_words[(size_t)(st0 + idx) * W + w];
+          } else {
+            const Word4 rr = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamReset << 28) | 1u, ge_hi, u_k0, u_k1);
+            const uint32_t rw4[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+            for (int w = 0; w < W; ++w) rs[w] = rw4[w] & valid_word_mask(N, w);
+            rt = PBN_NO_TARGET;
+          }
+          const uint32_t u2 = (uint32_t)(xr >> 32);   // = xhi
           if (u_fl & 4u) {
-            random_actions3<W>(E.w, E.z, N, a.n1_magic, m);
+            actions_from_draw<W>(c_act, N, a.n1_magic, m);
 #pragma unroll
             for (int w = 0; w < W; ++w) a.flipmask[CK(k * plane + (size_t)w * n + le, (size_t)n_steps * plane, 8)] = m[w];
           } else {
@@ -1015,29 +1059,26 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
           for (int w = 0; w < W; ++w) pc += __builtin_popcount(m[w]);
           int g0, g1, g2;
           if (u_gx == 2) {
-            g0 = gap_any(2, L, a, E.x); g1 = gap_any(2, L, a, E.y); g2 = gap_any(2, L, a, F.x);
+            g0 = gap_any(2, L, a, E.x); g1 = gap_any(2, L, a, E.y); g2 = gap_any(2, L, a, u2);
           } else if (u_gx) {
-            g0 = gap_of(cdf, a.cdf_len, E.x); g1 = gap_of(cdf, a.cdf_len, E.y); g2 = gap_of(cdf, a.cdf_len, F.x);
+            g0 = gap_of(cdf, a.cdf_len, E.x); g1 = gap_of(cdf, a.cdf_len, E.y); g2 = gap_of(cdf, a.cdf_len, u2);
           } else {
             g0 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.x);
             g1 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.y);
-            g2 = gap_est(cdf, a.cdf_len, a.inv_log2q, F.x);
+            g2 = gap_est(cdf, a.cdf_len, a.inv_log2q, u2);
           }
           const int p0 = g0 - 1, p1 = p0 + g1, p2 = p1 + g2;
           set_bit<W>(gam, p0, N);
           set_bit<W>(gam, p1, N);
           set_bit<W>(gam, p2, N);
-          if (p2 < N - 1) {   // rare: a fourth flip is possible (gap 3 = F.y, gap k >= 4: PERT call (k-4)>>2, word (k-4)&3)
-            Word4 P = F;
+          if (p2 < N - 1) {   // rare: a fourth flip is possible (gap k >= 3: PERT call (k-3)>>2, word (k-3)&3)
+            Word4 P = E;
             int pos = p2;
             for (int kk = 3; pos < N - 1; ++kk) {
-              uint32_t u = F.y;
-              if (kk >= 4) {
-                if (((kk - 4) & 3) == 0)
-                  P = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamPert << 28) | (uint32_t)((kk - 4) >> 2), ge_hi, u_k0, u_k1);
-                const int j4 = (kk - 4) & 3;
-                u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
-              }
+              if (((kk - 3) & 3) == 0)
+                P = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamPert << 28) | (uint32_t)((kk - 3) >> 2), ge_hi, u_k0, u_k1);
+              const int j4 = (kk - 3) & 3;
+              const uint32_t u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
               pos += gap_any(u_gx, L, a, u);
               set_bit<W>(gam, pos, N);
             }
@@ -1045,33 +1086,6 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
           bool pert = false;
 #pragma unroll
           for (int w = 0; w < W; ++w) pert = pert || gam[w] != 0;
-          // autoreset draw (used by wave 0 only if the env's episode ends): (start, target) in
-          // one draw over the A(A-1) pairs, then the state within the start attractor
-          uint32_t rt;
-          if (u_na >= 1) {
-            const int32_t* att_first = reinterpret_cast<const int32_t*>(L + a.att_off);
-            const uint32_t* att_words = L + a.att_off + u_na + 1;
-            const uint32_t A = (uint32_t)u_na;
-            uint32_t hi = F.w, lo = F.z, as = 0;
-            rt = 0;
-            if (A >= 2) {
-              const uint32_t c = ext64(hi, lo, A * (A - 1));
-              as = a.am1_magic ? __umulhi(c, a.am1_magic) : c;   // c / (A - 1)
-              rt = c - as * (A - 1);
-              rt += (rt >= as) ? 1u : 0u;
-            }
-            // (single-state attractors: the draw over one state is 0 and state a is attractor a's)
-            const int st0 = (u_fl & 16u) ? (int)as : att_first[as];
-            const uint32_t idx = (u_fl & 16u) ? 0u : ext64(hi, lo, (uint32_t)(att_first[as + 1] - st0));
-#pragma unroll
-            for (int w = 0; w < W; ++w) rs[w] = att_words[(size_t)(st0 + idx) * W + w];
-          } else {
-            const Word4 rr = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamReset << 28) | 1u, ge_hi, u_k0, u_k1);
-            const uint32_t rw4[4] = {rr.x, rr.y, rr.z, rr.w};
-#pragma unroll
-            for (int w = 0; w < W; ++w) rs[w] = rw4[w] & valid_word_mask(N, w);
-            rt = PBN_NO_TARGET;
-          }
 #pragma unroll
           for (int w = 0; w < W; ++w) {
             slot[w * 64 + lane] = m[w];
@@ -1451,6 +1465,7 @@ struct pbn_net {
   int n_gates = 0, n_glayers = 0, gate_off = 0, glayer_off = 0;   // lowered wide functions
   int max_nf = 0, lq = 1, slot_words = 0;
   uint32_t n1_magic = 0, am1_magic = 0;   // ceil(2^32 / (N + 1)), ceil(2^32 / (A - 1))
+  uint64_t x_mult = 0;
   int att_single = 0;                     // every attractor is a single state
   int force_roll = 0;        // PBN_ROLL env override: 2 = lean (wave kernel), 3 = pipe
   ResetFn reset = nullptr;
@@ -1889,10 +1904,11 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   net->wave_lean = pick_wave<2>(W, d->prob_bits);
   net->pipe = pick_pipe(W, d->prob_bits);
   net->reset = pick_reset(W);
-  // multiply-high divisors (exact for the operand ranges used: see random_actions3, autoreset)
+  // multiply-high divisors (exact for the operand ranges used: see actions_from_draw, autoreset)
   net->n1_magic = (uint32_t)(((1ull << 32) + (uint64_t)N) / (uint64_t)(N + 1));
   net->att_single = A >= 1 && S == A ? 1 : 0;
   net->am1_magic = A >= 3 ? (uint32_t)(((1ull << 32) + (uint64_t)(A - 2)) / (uint64_t)(A - 1)) : 0u;   // 0: A - 1 == 1
+  net->x_mult = (uint64_t)(N + 1) * (uint64_t)(N + 1) * (uint64_t)(N + 1) * (A >= 2 ? (uint64_t)A * (uint64_t)(A - 1) : 1ull);
   if (const char* env = getenv("PBN_ROLL")) {
     if (!strcmp(env, "lean")) net->force_roll = 2;
     if (!strcmp(env, "pipe")) net->force_roll = 3;
@@ -2041,6 +2057,7 @@ static int step_impl(pbn_net* net, uint64_t seed, uint64_t step, const uint64_t*
   a.n1_magic = net->n1_magic;
   a.att_single = net->att_single;
   a.am1_magic = net->am1_magic;
+  a.x_mult = net->x_mult;
   // launch shape: one thread per 32-env group once that fills the chip
   // (>= 4 waves per SIMD), else one wave per group (node loop across lanes)
   a.n_steps = 1;
@@ -2135,6 +2152,7 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
   a.n1_magic = net->n1_magic;
   a.att_single = net->att_single;
   a.am1_magic = net->am1_magic;
+  a.x_mult = net->x_mult;
 #ifdef PBN_STAMPS
   a.stamps = g_stamps;
 #endif

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--network", default="pbn28")
     ap.add_argument("--pipe", action="store_true", help="pipelined rollout kernel: per-role clocks of iteration 10")
     ap.add_argument("--plane", action="store_true", help="plane-resident rollout kernel (4 roles; implies --pipe)")
+    ap.add_argument("--lib", default=STAMP_LIB, help="a stamps build (default: the one --build makes)")
     ap.add_argument("--rollout", type=int, default=0,
                     help="stamp a pbn_rollout launch of this many steps (phases of its last step)")
     args = ap.parse_args()
@@ -34,7 +35,7 @@ def main():
         from pbn_rl_amd import _lib
         _lib.build(out=STAMP_LIB, defines=["PBN_STAMPS"], verbose=True)
         return
-    os.environ["PBN_LIB"] = STAMP_LIB
+    os.environ["PBN_LIB"] = args.lib
     if args.plane or args.pipe:
         os.environ["PBN_ROLL"] = "plane" if args.plane else "pipe"
     import numpy as np
