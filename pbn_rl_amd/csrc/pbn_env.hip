@@ -167,6 +167,24 @@ __device__ __noinline__ size_t pbn_ck(size_t i, size_t len, int site) {
 #endif
 
 // ---------------------------------------------------------------- helpers
+// Element (uniform base + lane element) of an output array addressed as a wave-uniform 64-bit
+// base (SGPRs, advanced per step on the SALU) plus the lane's 32-bit byte offset: the
+// global_store / global_load "saddr" form, with no 64-bit VGPR address pair and no per-step
+// VALU address arithmetic (lane_elem * sizeof(T) < 2^32: n_envs < 2^30).  Checked builds keep
+// the bounds-checked index.
+template <typename T>
+__device__ __forceinline__ T& lane_at(T* base, size_t uniform_elems, uint32_t lane_bytes) {
+  // laundered so that loop strength reduction cannot turn the sum into a 64-bit VGPR
+  // induction variable
+  asm volatile("" : "+s"(uniform_elems));
+  asm volatile("" : "+v"(lane_bytes));
+  return *reinterpret_cast<T*>(reinterpret_cast<char*>(base + uniform_elems) + lane_bytes);
+}
+#ifdef PBN_CHECKS
+#define LANE_AT(base, ubase, le_, len, site) (base)[CK((ubase) + (size_t)(le_), (len), (site))]
+#else
+#define LANE_AT(base, ubase, le_, len, site) lane_at((base), (ubase), (uint32_t)(le_) * (uint32_t)sizeof(*(base)))
+#endif
 __device__ __forceinline__ uint32_t valid_word_mask(int n, int w) {
   const int bits = n - 32 * w;
   return bits >= 32 ? 0xFFFFFFFFu : (bits <= 0 ? 0u : ((1u << bits) - 1u));
@@ -900,8 +918,16 @@ __device__ __forceinline__ uint32_t chain_padded(const uint4* __restrict__ rec, 
   return x;
 }
 
+// Waves per SIMD the register allocation must allow for single-word states: 6 (<= 80 VGPRs,
+// no spill in the step loops) runs 1M envs 10 % faster than the unconstrained 86 VGPRs (5 waves);
+// 7 and 8 spill to scratch in the state loop and lose (profiles/r02_ab_waves_per_eu.jsonl).
+// Wider states keep the compiler's choice.
+#ifndef PBN_PIPE_WAVES_PER_EU
+#define PBN_PIPE_WAVES_PER_EU 6
+#endif
+#define PBN_PIPE_ATTR __attribute__((amdgpu_waves_per_eu(W == 1 ? PBN_PIPE_WAVES_PER_EU : 1, 8)))
 template <int W, int B>
-__global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
+__global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a) {
   constexpr int CPN = B / 4;              // selection calls per node
   extern __shared__ uint32_t smem[];
   const int lane = threadIdx.x & 63;
@@ -1048,11 +1074,11 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
           if (u_fl & 4u) {
             actions_from_draw<W>(c_act, N, a.n1_magic, m);
 #pragma unroll
-            for (int w = 0; w < W; ++w) a.flipmask[CK(k * plane + (size_t)w * n + le, (size_t)n_steps * plane, 8)] = m[w];
+            for (int w = 0; w < W; ++w) LANE_AT(a.flipmask, k * plane + (size_t)w * n, le, (size_t)n_steps * plane, 8) = m[w];
           } else {
 #pragma unroll
             for (int w = 0; w < W; ++w)
-              m[w] = a.flipmask[CK(k * plane + (size_t)w * n + le, (size_t)n_steps * plane, 6)] & valid_word_mask(N, w);
+              m[w] = LANE_AT(a.flipmask, k * plane + (size_t)w * n, le, (size_t)n_steps * plane, 6) & valid_word_mask(N, w);
           }
           uint32_t pc = 0;
 #pragma unroll
@@ -1163,7 +1189,7 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
         info = slot[3 * W * 64 + lane];
         if (valid && (u_fl & 1u)) {
 #pragma unroll
-          for (int w = 0; w < W; ++w) a.obs[CK(t * plane + (size_t)w * n + le, (size_t)n_steps * plane, 7)] = st[w];
+          for (int w = 0; w < W; ++w) LANE_AT(a.obs, t * plane + (size_t)w * n, le, (size_t)n_steps * plane, 7) = st[w];
         }
 #pragma unroll
         for (int w = 0; w < W; ++w) Sg[32 * w + l32] = lane_transpose32(s1[w], lane);
@@ -1227,7 +1253,7 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
           for (int w = 0; w < W; ++w) sp[w] = pert ? (s1[w] ^ gam[w]) : sp[w];
           if (valid && (u_fl & 2u)) {
 #pragma unroll
-            for (int w = 0; w < W; ++w) a.final_state[CK(t * plane + (size_t)w * n + le, (size_t)n_steps * plane, 10)] = sp[w];
+            for (int w = 0; w < W; ++w) LANE_AT(a.final_state, t * plane + (size_t)w * n, le, (size_t)n_steps * plane, 10) = sp[w];
           }
           // reward candidates depend only on popcount(flipmask): read them beside the hash
           const float r_none = rtab[pc], r_wrong = rtab[(N + 1) + pc], r_term = rtab[2 * (N + 1) + pc];
@@ -1268,8 +1294,8 @@ __global__ void __launch_bounds__(192) pbn_rollout_pipe(StepArgs a) {
           const uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) |
                               ((uint32_t)pert << 3) | ((uint32_t)reset << 4);
           if (valid) {
-            a.reward[CK(t * n + le, n_steps * n, 11)] = term ? r_term : (wrong ? r_wrong : r_none);
-            a.flags[CK(t * n + le, n_steps * n, 15)] = (uint8_t)fl;
+            LANE_AT(a.reward, (size_t)t * n, le, (size_t)n_steps * n, 11) = term ? r_term : (wrong ? r_wrong : r_none);
+            LANE_AT(a.flags, (size_t)t * n, le, (size_t)n_steps * n, 15) = (uint8_t)fl;
           }
           tg0 = reset ? (info & 0xFFu) : tg0;
           tt0 = reset ? 0u : (uint32_t)tt;
