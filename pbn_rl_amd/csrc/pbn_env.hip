@@ -201,6 +201,36 @@ __device__ __forceinline__ uint32_t ext64(uint32_t& hi, uint32_t& lo, uint32_t K
   return (uint32_t)(y >> 32);
 }
 
+// LDS hash of the attractor states, slot-major: slot s holds its key words at [s * HS, s * HS +
+// W) and the attractor id (0xFFFFFFFF: empty) at s * HS + W, HS = W + 1 rounded up to a power
+// of two, so that one probe is one ds_read_b64 (W = 1) or ds_read_b128 (W = 2, 3)
+template <int W>
+struct HashStride {
+  static constexpr int value = W == 1 ? 2 : (W <= 3 ? 4 : 8);
+};
+
+// attractor id of the state sp at slot s, or -1
+template <int W>
+__device__ __forceinline__ int hash_probe(const uint32_t* __restrict__ htab, uint32_t s, const uint32_t (&sp)[W]) {
+  constexpr int HS = HashStride<W>::value;
+  const uint32_t* e = htab + (size_t)s * HS;
+  uint32_t ent[HS];
+  if constexpr (HS == 2) {
+    const uint2 v = *reinterpret_cast<const uint2*>(e);
+    ent[0] = v.x; ent[1] = v.y;
+  } else {
+#pragma unroll
+    for (int q = 0; q < HS / 4; ++q) {
+      const uint4 v = reinterpret_cast<const uint4*>(e)[q];
+      ent[4 * q] = v.x; ent[4 * q + 1] = v.y; ent[4 * q + 2] = v.z; ent[4 * q + 3] = v.w;
+    }
+  }
+  bool eq = ent[W] != 0xFFFFFFFFu;
+#pragma unroll
+  for (int w = 0; w < W; ++w) eq = eq && ent[w] == sp[w];
+  return eq ? (int)ent[W] : -1;
+}
+
 // Three actions uniform on [0, N]: the base-(N+1) digits of c, one draw over (N+1)^3.
 // Division by N+1 is a multiply-high by magic = ceil(2^32 / (N+1)), exact for c * (N+1) < 2^32
 // (c < (N+1)^3 <= 129^3).
@@ -753,8 +783,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   }
   int att = -1;
   if (a.hash_bits > 0) {
-    const int hmask = (1 << a.hash_bits) - 1;
-    const uint32_t* hid = htab + (size_t)W * (hmask + 1);
+    const uint32_t hmask = (1u << a.hash_bits) - 1u;
     uint32_t h = 0;
 #pragma unroll
     for (int w = 0; w < W; ++w) h += sp[w] * a.hash_mult[w];
@@ -762,20 +791,12 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
     // keys are unique: probe order does not matter; the first four probes are read side by side
 #pragma unroll
     for (int pr = 0; pr < 4; ++pr) {
-      const uint32_t slot = (h + pr) & hmask;
-      bool eq = pr < a.hash_probes;
-#pragma unroll
-      for (int w = 0; w < W; ++w) eq = eq && (htab[(size_t)w * (hmask + 1) + slot] == sp[w]);
-      const uint32_t id = hid[slot];
-      if (eq && id != 0xFFFFFFFFu) att = (int)id;
+      const int id = hash_probe<W>(htab, (h + pr) & hmask, sp);
+      if (pr < a.hash_probes && id >= 0) att = id;
     }
     for (int pr = 4; pr < a.hash_probes; ++pr) {
-      const uint32_t slot = (h + pr) & hmask;
-      bool eq = true;
-#pragma unroll
-      for (int w = 0; w < W; ++w) eq = eq && (htab[(size_t)w * (hmask + 1) + slot] == sp[w]);
-      const uint32_t id = hid[slot];
-      if (eq && id != 0xFFFFFFFFu) att = (int)id;
+      const int id = hash_probe<W>(htab, (h + pr) & hmask, sp);
+      if (id >= 0) att = id;
     }
   }
   const bool in_attr = att >= 0;
@@ -784,7 +805,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   int tt = (int)tt0 + 1;
   tt = tt > 255 ? 255 : tt;
   const bool trunc = a.horizon > 0 && tt >= a.horizon;
-  a.reward[CK(ks * n + le, n_steps * n, 11)] = rtab[(2 * (int)term + (int)wrong) * (N + 1) + (int)pc];
+  a.reward[CK(ks * n + le, n_steps * n, 11)] = rtab[(int)pc * 4 + 2 * (int)term + (int)wrong];
   uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) | ((uint32_t)pert << 3);
   if ((a.mode & PBN_MODE_AUTORESET) && (term || trunc)) {
     uint32_t nt;
@@ -921,11 +942,16 @@ __device__ __forceinline__ uint32_t chain_padded(const uint4* __restrict__ rec, 
 // Waves per SIMD the register allocation must allow for single-word states: 6 (<= 80 VGPRs,
 // no spill in the step loops) runs 1M envs 10 % faster than the unconstrained 86 VGPRs (5 waves);
 // 7 and 8 spill to scratch in the state loop and lose (profiles/r02_ab_waves_per_eu.jsonl).
-// Wider states keep the compiler's choice.
+// Three-word states (pbn70) are held to 3 waves (167 VGPRs, where the compiler's choice is 181:
+// 2 waves); two-word states fit 4 waves as they are.
 #ifndef PBN_PIPE_WAVES_PER_EU
 #define PBN_PIPE_WAVES_PER_EU 6
 #endif
-#define PBN_PIPE_ATTR __attribute__((amdgpu_waves_per_eu(W == 1 ? PBN_PIPE_WAVES_PER_EU : 1, 8)))
+#ifndef PBN_PIPE_WAVES_PER_EU_W3
+#define PBN_PIPE_WAVES_PER_EU_W3 3
+#endif
+#define PBN_PIPE_ATTR \
+  __attribute__((amdgpu_waves_per_eu(W == 1 ? PBN_PIPE_WAVES_PER_EU : (W == 3 ? PBN_PIPE_WAVES_PER_EU_W3 : 1), 8)))
 template <int W, int B>
 __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a) {
   constexpr int CPN = B / 4;              // selection calls per node
@@ -1025,10 +1051,10 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
         const uint32_t st_lo = (uint32_t)step;
         const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
         const uint32_t ge_lo = (uint32_t)ge;
+        // one ENV call: words 0, 1 = gaps 0, 1; X = words 3:2 gives, in order, the action draw
+        // (every mode), the autoreset draws and gap 2's uniform u2 (DESIGN.md "Step semantics")
+        const Word4 E = pbn::philox4x32_10(ge_lo, st_lo, pbn::kStreamEnv << 28, ge_hi, u_k0, u_k1);
         if (valid) {
-          // one ENV call: words 0, 1 = gaps 0, 1; X = words 3:2 gives, in order, the action draw
-          // (every mode), the autoreset draws and gap 2's uniform u2 (DESIGN.md "Step semantics")
-          const Word4 E = pbn::philox4x32_10(ge_lo, st_lo, pbn::kStreamEnv << 28, ge_hi, u_k0, u_k1);
           uint32_t m[W], gam[W], rs[W];
 #pragma unroll
           for (int w = 0; w < W; ++w) { m[w] = 0; gam[w] = 0; rs[w] = 0; }
@@ -1255,33 +1281,23 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
 #pragma unroll
             for (int w = 0; w < W; ++w) LANE_AT(a.final_state, t * plane + (size_t)w * n, le, (size_t)n_steps * plane, 10) = sp[w];
           }
-          // reward candidates depend only on popcount(flipmask): read them beside the hash
-          const float r_none = rtab[pc], r_wrong = rtab[(N + 1) + pc], r_term = rtab[2 * (N + 1) + pc];
+          // reward candidates depend only on popcount(flipmask): one 16-byte row {none, wrong,
+          // term, -} read beside the hash
+          const float4 r4 = reinterpret_cast<const float4*>(rtab)[pc];
+          const float r_none = r4.x, r_wrong = r4.y, r_term = r4.z;
           int att = -1;
           if (u_hb > 0) {
-            const int hmask = (1 << u_hb) - 1;
-            const uint32_t* hid = htab + (size_t)W * (hmask + 1);
+            const uint32_t hmask = (1u << u_hb) - 1u;
             uint32_t h = 0;
 #pragma unroll
             for (int w = 0; w < W; ++w) h += sp[w] * a.hash_mult[w];
             h >>= (32 - u_hb);
-            // the table is usually collision-free (one probe); keys are unique, so probe order
-            // does not matter
-            {
-              const uint32_t slot_i = h & hmask;
-              uint32_t eq = 1u;
-#pragma unroll
-              for (int w = 0; w < W; ++w) eq &= (htab[(size_t)w * (hmask + 1) + slot_i] == sp[w]) ? 1u : 0u;
-              const uint32_t id = hid[slot_i];
-              att = (eq != 0u && id != 0xFFFFFFFFu) ? (int)id : att;
-            }
+            // the table is usually collision-free (one probe, h < 2^bits needs no mask); keys
+            // are unique, so probe order does not matter
+            att = hash_probe<W>(htab, h, sp);
             for (int pr = 1; pr < u_hp; ++pr) {
-              const uint32_t slot_i = (h + pr) & hmask;
-              bool eq = true;
-#pragma unroll
-              for (int w = 0; w < W; ++w) eq = eq && (htab[(size_t)w * (hmask + 1) + slot_i] == sp[w]);
-              const uint32_t id = hid[slot_i];
-              if (eq && id != 0xFFFFFFFFu) att = (int)id;
+              const int id = hash_probe<W>(htab, (h + pr) & hmask, sp);
+              if (id >= 0) att = id;
             }
           }
           const bool in_attr = att >= 0;
@@ -1585,9 +1601,10 @@ bool build_hash(const std::vector<std::vector<uint32_t>>& states, const std::vec
     }
     const bool accept = best_probes == 1 || (best_probes <= 4 && bits >= std::min(min_bits + 4, kMaxHashBits));
     if (accept || bits == kMaxHashBits) {
-      image->assign((size_t)(W + 1) * size, 0u);
+      const int HS = W == 1 ? 2 : (W <= 3 ? 4 : 8);   // HashStride<W>
+      image->assign((size_t)HS * size, 0u);
       std::vector<int> used(size, 0);
-      for (uint32_t s = 0; s < size; ++s) (*image)[(size_t)W * size + s] = 0xFFFFFFFFu;
+      for (uint32_t s = 0; s < size; ++s) (*image)[(size_t)s * HS + W] = 0xFFFFFFFFu;
       for (size_t k = 0; k < S; ++k) {
         uint32_t h = 0;
         for (int w = 0; w < W; ++w) h += states[k][w] * best_mult[w];
@@ -1596,8 +1613,8 @@ bool build_hash(const std::vector<std::vector<uint32_t>>& states, const std::vec
         while (used[(h + p) & mask]) ++p;
         const uint32_t slot = (h + p) & mask;
         used[slot] = 1;
-        for (int w = 0; w < W; ++w) (*image)[(size_t)w * size + slot] = states[k][w];
-        (*image)[(size_t)W * size + slot] = ids[k];
+        for (int w = 0; w < W; ++w) (*image)[(size_t)slot * HS + w] = states[k][w];
+        (*image)[(size_t)slot * HS + W] = ids[k];
       }
       *bits_out = bits;
       *probes_out = best_probes;
@@ -1731,7 +1748,7 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
       return fail(PBN_EINVAL, "too many attractor states for the LDS hash");
     }
   }
-  // LDS table image: cdf[cdf_len] | reward[4(N+1)] | hash[(W+1) << bits]
+  // LDS table image: cdf[cdf_len] | reward[N+1][4] | hash[1 << bits][HashStride<W>]
   std::vector<uint32_t> tab(net->cdf_len, 0xFFFFFFFFu);
   for (int m = 0; m < N; ++m) tab[m] = d->perturb_cdf[m];
   for (int m = 1; m < N; ++m)
@@ -1739,11 +1756,13 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
       free_net(net);
       return fail(PBN_EINVAL, "perturb_cdf must be non-decreasing");
     }
-  for (int k = 0; k < 4 * (N + 1); ++k) {
-    uint32_t u;
-    memcpy(&u, &d->reward_table[k], 4);
-    tab.push_back(u);
-  }
+  // reward rows by popcount(flipmask): {none, wrong attractor, target, 0} (one 16-byte read)
+  for (int pc = 0; pc <= N; ++pc)
+    for (int c = 0; c < 4; ++c) {
+      uint32_t u = 0;
+      if (c < 3) memcpy(&u, &d->reward_table[c * (N + 1) + pc], 4);
+      tab.push_back(u);
+    }
   tab.insert(tab.end(), hash_img.begin(), hash_img.end());
   // attractor start[A+1] | states[S][W], read by autoreset in the wave kernel
   net->att_off = (int)tab.size();
