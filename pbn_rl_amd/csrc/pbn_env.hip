@@ -201,6 +201,21 @@ __device__ __forceinline__ uint32_t ext64(uint32_t& hi, uint32_t& lo, uint32_t K
   return (uint32_t)(y >> 32);
 }
 
+// The LDS table image from global memory, all of a thread's loads issued before its stores
+// (four loads in flight per thread, where a load-store loop waits once per element)
+__device__ __forceinline__ void copy_image(uint32_t* L, const StepArgs& a) {
+  const uint4* src = reinterpret_cast<const uint4*>(a.tab);
+  uint4* dst = reinterpret_cast<uint4*>(L);
+  const int n4 = a.tab_words >> 2, bd = (int)blockDim.x;
+  int k = (int)threadIdx.x;
+  for (; k + 3 * bd < n4; k += 4 * bd) {
+    const uint4 v0 = src[CK(k, n4, 5)], v1 = src[CK(k + bd, n4, 5)];
+    const uint4 v2 = src[CK(k + 2 * bd, n4, 5)], v3 = src[CK(k + 3 * bd, n4, 5)];
+    dst[k] = v0; dst[k + bd] = v1; dst[k + 2 * bd] = v2; dst[k + 3 * bd] = v3;
+  }
+  for (; k < n4; k += bd) dst[k] = src[CK(k, n4, 5)];
+}
+
 // LDS hash of the attractor states, slot-major: slot s holds its key words at [s * HS, s * HS +
 // W) and the attractor id (0xFFFFFFFF: empty) at s * HS + W, HS = W + 1 rounded up to a power
 // of two, so that one probe is one ds_read_b64 (W = 1) or ds_read_b128 (W = 2, 3)
@@ -544,11 +559,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
 #pragma unroll
     for (int q = 0; q < kNodeRecs; ++q) rec_[r][q] = a.nrec[CK((size_t)ic * kNodeRecs + q, N * kNodeRecs, 4)];
   }
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(a.tab);
-    uint4* dst = reinterpret_cast<uint4*>(L);
-    for (int k = threadIdx.x; k < (a.tab_words >> 2); k += blockDim.x) dst[k] = src[CK(k, a.tab_words >> 2, 5)];
-  }
+  copy_image(L, a);
   __syncthreads();   // the kernel's only block barrier
   if (g >= a.n_groups) return;  // whole wave
   const uint4* selq = reinterpret_cast<const uint4*>(L + a.sel_off);
@@ -984,21 +995,19 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
   const uint4* selq = reinterpret_cast<const uint4*>(L + a.sel_off);
   uint32_t* Sg = smem + a.tab_words + half * 32 * W;   // this half's group
   uint32_t* slots = smem + a.tab_words + 2 * 32 * W;
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(a.tab);
-    uint4* dst = reinterpret_cast<uint4*>(L);
-    for (int k = threadIdx.x; k < (a.tab_words >> 2); k += blockDim.x) dst[k] = src[CK(k, a.tab_words >> 2, 5)];
-  }
   uint32_t st[W];
   uint32_t tt0 = 0, tg0 = 0;
 #pragma unroll
   for (int w = 0; w < W; ++w) st[w] = 0;
-  if (role == 0 && valid) {
+  if (role == 0 && valid) {   // issued first: their latency overlaps the image copy
 #pragma unroll
-    for (int w = 0; w < W; ++w) st[w] = a.state[CK((size_t)w * n + le, plane, 1)] & valid_word_mask(N, w);
+    for (int w = 0; w < W; ++w) st[w] = a.state[CK((size_t)w * n + le, plane, 1)];
     tt0 = a.t[CK(le, n, 2)];
     tg0 = a.target[CK(le, n, 3)];
   }
+  copy_image(L, a);
+#pragma unroll
+  for (int w = 0; w < W; ++w) st[w] &= valid_word_mask(N, w);
   // node records live in LDS (L + nrec_off), record-major [kNodeRecs][32W] so that a wave's
   // lanes (nodes) read consecutive 16-byte records without bank conflicts: each role reads
   // what it needs per step, so no record is carried in VGPRs across the step loop
@@ -1020,11 +1029,19 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
   uint32_t* cm = slots + 2 * (size_t)a.slot_words;
   __syncthreads();
   if constexpr (W == 1) {
-    for (int idx = threadIdx.x; idx < (kNodeRecs - 1) * B * 32; idx += blockDim.x) {
-      const int i = idx % 32, d = (idx / 32) % B, q = idx / (32 * B);
+    // thread t: record (q, i) = p = t mod 96 and digits [h B/2, (h+1) B/2), h = t / 96 (192
+    // threads = two per record: two LDS reads, then B/2 independent writes)
+    static_assert((kNodeRecs - 1) * 32 * 2 == 192, "cm build assumes 192 threads");
+    {
+      const int p = (int)threadIdx.x % ((kNodeRecs - 1) * 32), h = (int)threadIdx.x / ((kNodeRecs - 1) * 32);
+      const int i = p & 31, q = p >> 5;
       uint32_t c = 0;
       if (i < N && q < (int)recL[i].w - 1) c = recL[q * 32 * W + i].z;
-      cm[idx] = ((c >> (B - 1 - d)) & 1u) ? ~0u : 0u;
+#pragma unroll
+      for (int dd = 0; dd < B / 2; ++dd) {
+        const int d = h * (B / 2) + dd;
+        cm[(q * B + d) * 32 + i] = ((c >> (B - 1 - d)) & 1u) ? ~0u : 0u;
+      }
     }
     __syncthreads();
   }
