@@ -1056,6 +1056,103 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
   // loop-carried values (hoisted invariants) occupy registers only in that role's loop
   if (role == PBN_DIAG_SKIP_ROLE) {
     for (int k = 0; k <= n_steps; ++k) lds_barrier();
+  } else if (role == 1 && (u_fl & 4u) && u_gx == 2 && u_na >= 2 && (u_fl & 16u)) {
+    // env draws, common configuration (random actions, gap bucket table, two or more
+    // single-state attractors): the same draws as the general loop below, branch-free apart from
+    // the rare fourth-flip tail and the guarded flip-mask store, so that the next step's ENV call
+    // (computed here, one step ahead) interleaves with this step's dependent draws and LDS reads
+    // instead of following them
+    const uint32_t A = (uint32_t)u_na;
+    const uint32_t n1 = (uint32_t)(N + 1);
+    const uint32_t* att_words = L + a.att_off + u_na + 1;
+    const uint2* lut = reinterpret_cast<const uint2*>(L + a.gap_lut_off);
+    auto env_call = [&](int k) {
+      const uint64_t step = a.step + (uint64_t)k;
+      const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
+      return pbn::philox4x32_10((uint32_t)ge, (uint32_t)step, pbn::kStreamEnv << 28, ge_hi, u_k0, u_k1);
+    };
+    Word4 E_next = env_call(0);
+    for (int k = 0; k <= n_steps; ++k) {
+      asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
+      asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
+      PBN_PSTAMP(k, 0);
+      if (k < n_steps) {
+        uint32_t* slot = slots + (size_t)(k & 1) * a.slot_words;
+        const Word4 E = E_next;
+        // part 1: the draws that feed LDS reads, and the reads themselves
+        uint32_t xhi = E.w, xlo = E.z;
+        const uint32_t c_act = ext64(xhi, xlo, n1 * n1 * n1);
+        const uint32_t u2 = (uint32_t)((((((uint64_t)E.w) << 32) | E.z) * a.x_mult) >> 32);
+        const uint32_t c = ext64(xhi, xlo, A * (A - 1));
+        const uint32_t as = a.am1_magic ? __umulhi(c, a.am1_magic) : c;   // c / (A - 1)
+        uint32_t rs[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) rs[w] = att_words[(size_t)as * W + w];
+        const uint2 e0 = lut[min(E.x >> a.gap_shift, (uint32_t)a.gap_nb)];
+        const uint2 e1 = lut[min(E.y >> a.gap_shift, (uint32_t)a.gap_nb)];
+        const uint2 e2 = lut[min(u2 >> a.gap_shift, (uint32_t)a.gap_nb)];
+        // part 2: the next step's ENV call runs while those reads are in flight (the scheduling
+        // barriers keep the compiler from hoisting it above them or sinking it to the latch)
+        asm volatile("" ::: "memory");   // the LDS reads above are issued here
+        __builtin_amdgcn_sched_barrier(0);
+        E_next = env_call(k + 1);   // (one unused call per launch)
+        asm volatile("" : "+v"(E_next.x), "+v"(E_next.y), "+v"(E_next.z), "+v"(E_next.w));
+        __builtin_amdgcn_sched_barrier(0);
+        // part 3: the rest of step k's draws
+        uint32_t rt = c - as * (A - 1);
+        rt += (rt >= as) ? 1u : 0u;
+        uint32_t m[W], gam[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) { m[w] = 0; gam[w] = 0; }
+        actions_from_draw<W>(c_act, N, a.n1_magic, m);
+        uint32_t pc = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) pc += __builtin_popcount(m[w]);
+        const int g0 = (int)e0.y + (E.x >= e0.x ? 1 : 0);   // gap_lut
+        const int g1 = (int)e1.y + (E.y >= e1.x ? 1 : 0);
+        const int g2 = (int)e2.y + (u2 >= e2.x ? 1 : 0);
+        const int p0 = g0 - 1, p1 = p0 + g1, p2 = p1 + g2;
+        set_bit<W>(gam, p0, N);
+        set_bit<W>(gam, p1, N);
+        set_bit<W>(gam, p2, N);
+        bool pert = false;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          pert = pert || gam[w] != 0;
+          slot[w * 64 + lane] = m[w];
+          slot[(W + w) * 64 + lane] = gam[w];
+          slot[(2 * W + w) * 64 + lane] = rs[w];
+        }
+        slot[3 * W * 64 + lane] = rt | (pc << 8) | ((uint32_t)pert << 16);
+        if (valid) {
+#pragma unroll
+          for (int w = 0; w < W; ++w) LANE_AT(a.flipmask, k * plane + (size_t)w * n, le, (size_t)n_steps * plane, 8) = m[w];
+        }
+        if (p2 < N - 1) {   // rare: a fourth flip is possible (gap k >= 3: PERT call (k-3)>>2, word (k-3)&3)
+          const uint64_t step = a.step + (uint64_t)k;
+          const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
+          Word4 P = E;
+          int pos = p2;
+          for (int kk = 3; pos < N - 1; ++kk) {
+            if (((kk - 3) & 3) == 0)
+              P = pbn::philox4x32_10((uint32_t)ge, (uint32_t)step, (pbn::kStreamPert << 28) | (uint32_t)((kk - 3) >> 2), ge_hi, u_k0, u_k1);
+            const int j4 = (kk - 3) & 3;
+            const uint32_t u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
+            pos += gap_lut(lut, a.gap_shift, a.gap_nb, u);
+            set_bit<W>(gam, pos, N);
+          }
+          pert = false;
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            pert = pert || gam[w] != 0;
+            slot[(W + w) * 64 + lane] = gam[w];
+          }
+          slot[3 * W * 64 + lane] = rt | (pc << 8) | ((uint32_t)pert << 16);
+        }
+      }
+      PBN_PSTAMP(k, 1);
+      lds_barrier();
+    }
   } else if (role == 1) {
     for (int k = 0; k <= n_steps; ++k) {
       asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
