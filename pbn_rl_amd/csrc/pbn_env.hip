@@ -24,6 +24,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <string>
 #include <vector>
 
@@ -1263,6 +1264,56 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
       }
       PBN_PSTAMP(k, 1);
       lds_barrier();
+    }
+  } else if (role == 2 && W == 1 && u_mnf >= 2 && u_mnf <= kNodeRecs) {
+    // selection, single-word states with at most kNodeRecs functions per node: branch-free over
+    // the lanes (lanes past N, single-function nodes and thresholds past a node's last compute
+    // values the padded chain ignores), one loop per threshold count, and the next step's
+    // SEL calls computed in the same block as this step's compares
+    auto sel_fast = [&](auto nq_c) {
+      constexpr int NQ = decltype(nq_c)::value;   // thresholds per node: max_nf - 1
+      const uint32_t* cmi = cm + l32;
+      uint32_t* lt_base = slots + (3 * W + 1) * 64 + half * 32 * W + l32;
+      auto sel_calls = [&](int k, uint32_t (&d)[16]) {
+        const uint64_t step = a.step + (uint64_t)k;
+        const uint32_t G_hi = (uint32_t)((G >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
+#pragma unroll
+        for (int c = 0; c < CPN; ++c) {
+          const Word4 o = pbn::philox4x32_10((uint32_t)G, (uint32_t)step, (pbn::kStreamSel << 28) | (uint32_t)(4 * l32 + c),
+                                             G_hi, u_k0, u_k1);
+          d[4 * c + 0] = o.x; d[4 * c + 1] = o.y; d[4 * c + 2] = o.z; d[4 * c + 3] = o.w;
+        }
+      };
+      // one step: this step's compares from `cur`, the next step's calls into `nxt`
+      auto sel_step = [&](int k, const uint32_t (&cur)[16], uint32_t (&nxt)[16]) {
+        asm volatile("" : "+s"(u_k0), "+s"(u_k1));
+        PBN_PSTAMP(k, 0);
+        if (k < n_steps) {
+          sel_calls(k + 1, nxt);   // (one unused set per launch)
+          uint32_t* lt_out = lt_base + (size_t)(k & 1) * a.slot_words;
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) lt_out[q * 64] = less_than_cm<B>(cur, cmi + (size_t)q * B * 32, 32);
+          // keeps the next calls in this block (LLVM would sink them to the loop latch)
+#pragma unroll
+          for (int d = 0; d < 16; ++d) asm volatile("" : "+v"(nxt[d]));
+        }
+        PBN_PSTAMP(k, 1);
+        lds_barrier();
+      };
+      // two steps per trip with the digit arrays swapping roles: no copies between steps
+      uint32_t dA[16], dB[16];
+#pragma unroll
+      for (int d = 0; d < 16; ++d) { dA[d] = 0; dB[d] = 0; }
+      sel_calls(0, dA);
+      for (int k = 0; k <= n_steps; k += 2) {
+        sel_step(k, dA, dB);
+        if (k + 1 <= n_steps) sel_step(k + 1, dB, dA);
+      }
+    };
+    switch (u_mnf) {
+      case 2: sel_fast(std::integral_constant<int, 1>{}); break;
+      case 3: sel_fast(std::integral_constant<int, 2>{}); break;
+      default: sel_fast(std::integral_constant<int, 3>{}); break;
     }
   } else if (role == 2) {
     for (int k = 0; k <= n_steps; ++k) {
