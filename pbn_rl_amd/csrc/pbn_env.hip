@@ -1360,6 +1360,116 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
       lds_barrier();
     }
   } else {
+    // the epilogue of step t (after the back-transpose): perturbed envs, outputs, attractor
+    // hash, reward, flags, autoreset
+    auto finish = [&](int t, uint32_t (&sp)[W], const uint32_t (&s1)[W], const uint32_t (&gam)[W],
+                      const uint32_t (&rs)[W], uint32_t info) {
+      {
+        // branch-free epilogue (this wave bounds the iteration): only the stores are guarded
+        const bool pert = (info >> 16) & 1u;
+        const uint32_t pc = (info >> 8) & 0xFFu;
+#pragma unroll
+        for (int w = 0; w < W; ++w) sp[w] = pert ? (s1[w] ^ gam[w]) : sp[w];
+        if (valid && (u_fl & 2u)) {
+#pragma unroll
+          for (int w = 0; w < W; ++w) LANE_AT(a.final_state, t * plane + (size_t)w * n, le, (size_t)n_steps * plane, 10) = sp[w];
+        }
+        // reward candidates depend only on popcount(flipmask): one 16-byte row {none, wrong,
+        // term, -} read beside the hash
+        const float4 r4 = reinterpret_cast<const float4*>(rtab)[pc];
+        const float r_none = r4.x, r_wrong = r4.y, r_term = r4.z;
+        int att = -1;
+        if (u_hb > 0) {
+          const uint32_t hmask = (1u << u_hb) - 1u;
+          uint32_t h = 0;
+#pragma unroll
+          for (int w = 0; w < W; ++w) h += sp[w] * a.hash_mult[w];
+          h >>= (32 - u_hb);
+          // the table is usually collision-free (one probe, h < 2^bits needs no mask); keys
+          // are unique, so probe order does not matter
+          att = hash_probe<W>(htab, h, sp);
+          for (int pr = 1; pr < u_hp; ++pr) {
+            const int id = hash_probe<W>(htab, (h + pr) & hmask, sp);
+            if (id >= 0) att = id;
+          }
+        }
+        const bool in_attr = att >= 0;
+        const bool term = in_attr && (uint32_t)att == tg0;
+        const bool wrong = in_attr && !term;
+        int tt = (int)tt0 + 1;
+        tt = tt > 255 ? 255 : tt;
+        const bool trunc = u_hz > 0 && tt >= u_hz;
+        const bool reset = (u_fl & 8u) && (term || trunc);
+        const uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) |
+                            ((uint32_t)pert << 3) | ((uint32_t)reset << 4);
+        if (valid) {
+          LANE_AT(a.reward, (size_t)t * n, le, (size_t)n_steps * n, 11) = term ? r_term : (wrong ? r_wrong : r_none);
+          LANE_AT(a.flags, (size_t)t * n, le, (size_t)n_steps * n, 15) = (uint8_t)fl;
+        }
+        tg0 = reset ? (info & 0xFFu) : tg0;
+        tt0 = reset ? 0u : (uint32_t)tt;
+#pragma unroll
+        for (int w = 0; w < W; ++w) st[w] = reset ? rs[w] : sp[w];
+      }
+    };
+    if (W == 1 && u_mnf >= 1 && u_mnf <= kNodeRecs) {
+      // single-word states with at most kNodeRecs functions per node: the loop-invariant record
+      // inputs held in VGPRs, and this step's selection masks and selectors read before the
+      // transpose, so that their LDS latency is off the chain slot -> transpose -> gathers ->
+      // mux trees -> back-transpose
+      auto state_fast = [&](auto k_c) {
+        constexpr int K = decltype(k_c)::value;
+        uint32_t ins[K];
+#pragma unroll
+        for (int q = 0; q < K; ++q) ins[q] = recL[q * 32 + l32].x;
+        for (int k = 0; k <= n_steps; ++k) {
+          asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
+          PBN_PSTAMP(k, 0);
+          if (k >= 1) {
+            const int t = k - 1;
+            const uint32_t* slot = slots + (size_t)(t & 1) * a.slot_words;
+            const uint32_t* lt_in = slot + 4 * 64 + half * 32 + l32;
+            uint32_t s1[W], gam[W], rs[W];
+            s1[0] = st[0] ^ slot[lane];
+            gam[0] = slot[64 + lane];
+            rs[0] = slot[2 * 64 + lane];
+            const uint32_t info = slot[3 * 64 + lane];
+            uint32_t ltv[K];
+            uint4 sa[K], sb[K];
+#pragma unroll
+            for (int q = 0; q < K; ++q) {
+              ltv[q] = q < K - 1 ? lt_in[q * 64] : 0u;
+              sa[q] = selq[(2 * q) * 32 + l32];
+              sb[q] = selq[(2 * q + 1) * 32 + l32];
+            }
+            if (valid && (u_fl & 1u)) LANE_AT(a.obs, (size_t)t * plane, le, (size_t)n_steps * plane, 7) = st[0];
+            Sg[l32] = lane_transpose32(s1[0], lane);
+            __builtin_amdgcn_wave_barrier();
+            uint32_t x = 0;
+#pragma unroll
+            for (int q = K - 1; q >= 0; --q) {
+              uint32_t xin[4];
+#pragma unroll
+              for (int kk = 0; kk < 4; ++kk) xin[kk] = plane_in<true>(Sg, ins[q], kk);
+              const uint32_t fj = eval_sel_in(xin, sa[q], sb[q]);
+              x = (q == K - 1) ? fj : bfi(ltv[q], fj, x);
+            }
+            uint32_t sp[W];
+            sp[0] = lane_transpose32(x, lane);
+            finish(t, sp, s1, gam, rs, info);
+          }
+          PBN_PSTAMP(k, 1);
+          lds_barrier();
+          PBN_PSTAMP(k, 2);
+        }
+      };
+      switch (u_mnf) {
+        case 1: state_fast(std::integral_constant<int, 1>{}); break;
+        case 2: state_fast(std::integral_constant<int, 2>{}); break;
+        case 3: state_fast(std::integral_constant<int, 3>{}); break;
+        default: state_fast(std::integral_constant<int, 4>{}); break;
+      }
+    } else
     for (int k = 0; k <= n_steps; ++k) {
       asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
       asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
@@ -1436,53 +1546,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
 #pragma unroll
         for (int w = 0; w < W; ++w) sp[w] = lane_transpose32(X[w], lane);
         PBN_PSTAMP_AT(k, 13);
-        {
-          // branch-free epilogue (this wave bounds the iteration): only the stores are guarded
-          const bool pert = (info >> 16) & 1u;
-          const uint32_t pc = (info >> 8) & 0xFFu;
-#pragma unroll
-          for (int w = 0; w < W; ++w) sp[w] = pert ? (s1[w] ^ gam[w]) : sp[w];
-          if (valid && (u_fl & 2u)) {
-#pragma unroll
-            for (int w = 0; w < W; ++w) LANE_AT(a.final_state, t * plane + (size_t)w * n, le, (size_t)n_steps * plane, 10) = sp[w];
-          }
-          // reward candidates depend only on popcount(flipmask): one 16-byte row {none, wrong,
-          // term, -} read beside the hash
-          const float4 r4 = reinterpret_cast<const float4*>(rtab)[pc];
-          const float r_none = r4.x, r_wrong = r4.y, r_term = r4.z;
-          int att = -1;
-          if (u_hb > 0) {
-            const uint32_t hmask = (1u << u_hb) - 1u;
-            uint32_t h = 0;
-#pragma unroll
-            for (int w = 0; w < W; ++w) h += sp[w] * a.hash_mult[w];
-            h >>= (32 - u_hb);
-            // the table is usually collision-free (one probe, h < 2^bits needs no mask); keys
-            // are unique, so probe order does not matter
-            att = hash_probe<W>(htab, h, sp);
-            for (int pr = 1; pr < u_hp; ++pr) {
-              const int id = hash_probe<W>(htab, (h + pr) & hmask, sp);
-              if (id >= 0) att = id;
-            }
-          }
-          const bool in_attr = att >= 0;
-          const bool term = in_attr && (uint32_t)att == tg0;
-          const bool wrong = in_attr && !term;
-          int tt = (int)tt0 + 1;
-          tt = tt > 255 ? 255 : tt;
-          const bool trunc = u_hz > 0 && tt >= u_hz;
-          const bool reset = (u_fl & 8u) && (term || trunc);
-          const uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) |
-                              ((uint32_t)pert << 3) | ((uint32_t)reset << 4);
-          if (valid) {
-            LANE_AT(a.reward, (size_t)t * n, le, (size_t)n_steps * n, 11) = term ? r_term : (wrong ? r_wrong : r_none);
-            LANE_AT(a.flags, (size_t)t * n, le, (size_t)n_steps * n, 15) = (uint8_t)fl;
-          }
-          tg0 = reset ? (info & 0xFFu) : tg0;
-          tt0 = reset ? 0u : (uint32_t)tt;
-#pragma unroll
-          for (int w = 0; w < W; ++w) st[w] = reset ? rs[w] : sp[w];
-        }
+        finish(t, sp, s1, gam, rs, info);
       }
       PBN_PSTAMP(k, 1);
       lds_barrier();
