@@ -114,6 +114,14 @@ def algorithmic_bytes_per_env(words: int) -> int:
     return 4 * words + 1 + 1 + 4 * words + 4 * words + 4 + 1 + 1
 
 
+def survey_bytes_per_env_step(n_nodes: int) -> int:
+    """SURVEY.md §8(d)'s algorithmic bytes per env-step, the figure roofline.achieved is priced on:
+    read s + flip mask + target id u8 + episode step u8, write s' + reward f32 + flags u8 + step u8,
+    with s packed in one u32 (N <= 32) or u64 words (N > 32): 20 B for Bittner-28, 56 B for pbn70."""
+    s = 4 if n_nodes <= 32 else 8 * ((n_nodes + 63) // 64)
+    return 3 * s + 8
+
+
 def rollout_bytes_per_env(words: int, steps: int) -> int:
     # per launch: read + write state 4W, t 1, target 1 once; per step write
     # obs 4W, flipmask (in-kernel actions) 4W, reward 4, flags 1
@@ -567,16 +575,23 @@ def main():
                         "traffic": None, "kernel": kernel, "launch_ms": frame_ms,
                         "note": "training frame (~150 launches): no single dominant kernel is priced"}
         elif rollout_mode:
-            bytes_run = sum(env.n_alloc * rollout_bytes_per_env(W, k) for k in plan)
+            per_step = survey_bytes_per_env_step(spec.n)
+            bytes_run = env.n_alloc * args.steps * per_step
+            moved_run = sum(env.n_alloc * rollout_bytes_per_env(W, k) for k in plan)
             achieved = bytes_run / elapsed / 1e9
             roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS,
                         "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
                         "kernel": "pbn_rollout (%s)" % ", ".join(f"{k} steps" for k in plan),
                         "launch_ms": dev_ms / len(plan), "bytes_per_launch": bytes_run / len(plan),
-                        "bytes_per_env_step": bytes_run / (env.n_alloc * args.steps),
-                        "note": "algorithmic bytes (DESIGN.md 'Algorithmic bytes') over HIP-event time; the "
-                                "kernel is compute/latency bound, see DESIGN.md 'What bounds it'"}
+                        "bytes_per_env_step": per_step,
+                        "moved_bytes_per_launch": moved_run / len(plan),
+                        "moved_bytes_per_env_step": moved_run / (env.n_alloc * args.steps),
+                        "note": "achieved = SURVEY.md 8(d)'s algorithmic bytes per env-step (a step kernel's "
+                                "minimal packed I/O) x env-steps / HIP-event time.  The rollout keeps the state "
+                                "on chip between steps and moves moved_bytes_per_launch, which `traffic` (PMC, "
+                                "per launch) measures.  The kernel is VALU-issue / latency bound, see DESIGN.md "
+                                "'What bounds it'"}
             if pmc:
                 roofline["traffic_source"] = {"file": pmc_path, "command": pmc.get("command")}
                 if pmc.get("valu_insts_per_launch"):
@@ -587,11 +602,13 @@ def main():
                                         "note": "SQ_INSTS_VALU of the same launch shape (traffic_source) over this "
                                                 "run's time; issue slots only"}
         else:
-            bytes_launch = env.n_alloc * algorithmic_bytes_per_env(W)
+            bytes_launch = env.n_alloc * survey_bytes_per_env_step(spec.n)
             achieved = bytes_launch / (frame_ms * 1e-3) / 1e9
             roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "pbn_step",
-                        "launch_ms": frame_ms, "bytes_per_launch": bytes_launch}
+                        "launch_ms": frame_ms, "bytes_per_launch": bytes_launch,
+                        "bytes_per_env_step": survey_bytes_per_env_step(spec.n),
+                        "moved_bytes_per_env_step": algorithmic_bytes_per_env(W)}
         out = {
             "metric": "env steps/sec (batched PBN transitions), Bittner-28 at 1/2/4/8 GPUs"
             if args.network == "pbn28" else f"env steps/sec (batched PBN transitions), {args.network}",

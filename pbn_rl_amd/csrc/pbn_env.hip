@@ -43,6 +43,7 @@ constexpr int kNodeRecs = 4;       // compact records prefetched per node by the
 #ifndef PBN_STATE_PRIO
 #define PBN_STATE_PRIO 2
 #endif
+
 constexpr int kWavesPerBlock = 4;  // wave kernel: waves (32-env groups) per block, sharing one LDS table image
 constexpr int kMaxHashBits = 12;
 
@@ -111,6 +112,8 @@ struct StepArgs {
   uint32_t am1_magic;  // ceil(2^32 / (A - 1)) for A >= 2: autoreset (start, target) split
   uint64_t x_mult;     // (N+1)^3 * A(A-1) (A >= 2) mod 2^64: what the ENV draws before gap 2 leave
                        // of X is X * x_mult (times the start attractor's size, multi-state nets)
+  int sel_prio;        // pipelined rollout: raise the selection wave's priority (grids of at most
+                       // four blocks per CU)
 };
 
 // In-kernel phase clocks (cdna_hip_programming.md section 7, "In-kernel stamps"):
@@ -262,6 +265,20 @@ __device__ __forceinline__ void actions_from_draw(uint32_t c, int N, uint32_t ma
     for (int w = 0; w < W; ++w)
       if (act > 0 && ((act - 1) >> 5) == w) m[w] |= 1u << ((act - 1) & 31);
   }
+}
+
+// actions_from_draw for one word with N <= 31: action a sets bit a - 1 as 1 << (a - 1), where
+// a = 0 shifts by 31 (the shift count's low five bits) onto a bit past the network that `vmask`
+// (valid_word_mask(N, 0)) clears once for all three: no per-action guard
+__device__ __forceinline__ uint32_t actions_mask31(uint32_t c, uint32_t n1, uint32_t magic, uint32_t vmask) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const uint32_t qt = __umulhi(c, magic);
+    m |= 1u << ((c - qt * n1 - 1u) & 31u);
+    c = qt;
+  }
+  return m & vmask;
 }
 
 // gap(u) = min{m in 1..N : u < C[m-1]} (N+1 or more if none); C padded with 0xFFFFFFFF.
@@ -973,6 +990,17 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
   // the state wave bounds every iteration: let it win VALU issue against the RNG waves of
   // other blocks sharing its SIMD
   if (role == 0) __builtin_amdgcn_s_setprio(PBN_STATE_PRIO);
+  // with one block per SIMD triple (every SIMD holds one wave of each role) the selection wave,
+  // the longest instruction stream, also goes ahead of the env-draw wave: -5 % per step at
+  // 65,536 envs; with more blocks resident it loses 4-8 % (profiles/r02_ab_wave_priority.jsonl)
+  if (role == 2 && a.sel_prio) __builtin_amdgcn_s_setprio(1);
+#ifdef PBN_STAMPS
+  // placement of this wave: HW_ID (wave, SIMD, CU, SH, SE) in the low word, XCC_ID above it
+  if (a.stamps && lane == 0)
+    a.stamps[(size_t)blockIdx.x * 16 + (role == 0 ? 14 : role * 4 + 3)] =
+        (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+        ((unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32);
+#endif
   const int half = lane >> 5;
   const int l32 = lane & 31;
   const int64_t g = (int64_t)blockIdx.x * 2 + half;
@@ -1057,7 +1085,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
   // loop-carried values (hoisted invariants) occupy registers only in that role's loop
   if (role == PBN_DIAG_SKIP_ROLE) {
     for (int k = 0; k <= n_steps; ++k) lds_barrier();
-  } else if (role == 1 && (u_fl & 4u) && u_gx == 2 && u_na >= 2 && (u_fl & 16u)) {
+  } else if (role == 1 && (u_fl & 4u) && u_gx == 2 && u_na >= 2 && (u_fl & 16u) && (W > 1 || N <= 31)) {
     // env draws, common configuration (random actions, gap bucket table, two or more
     // single-state attractors): the same draws as the general loop below, branch-free apart from
     // the rare fourth-flip tail and the guarded flip-mask store, so that the next step's ENV call
@@ -1072,14 +1100,13 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
       const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
       return pbn::philox4x32_10((uint32_t)ge, (uint32_t)step, pbn::kStreamEnv << 28, ge_hi, u_k0, u_k1);
     };
-    Word4 E_next = env_call(0);
-    for (int k = 0; k <= n_steps; ++k) {
+    // one step: this step's draws from E, the next step's ENV call into E_next
+    auto env_step = [&](int k, const Word4& E, Word4& E_next) {
       asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
       asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
       PBN_PSTAMP(k, 0);
       if (k < n_steps) {
         uint32_t* slot = slots + (size_t)(k & 1) * a.slot_words;
-        const Word4 E = E_next;
         // part 1: the draws that feed LDS reads, and the reads themselves
         uint32_t xhi = E.w, xlo = E.z;
         const uint32_t c_act = ext64(xhi, xlo, n1 * n1 * n1);
@@ -1105,7 +1132,8 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
         uint32_t m[W], gam[W];
 #pragma unroll
         for (int w = 0; w < W; ++w) { m[w] = 0; gam[w] = 0; }
-        actions_from_draw<W>(c_act, N, a.n1_magic, m);
+        if constexpr (W == 1) m[0] = actions_mask31(c_act, n1, a.n1_magic, valid_word_mask(N, 0));   // N <= 31
+        else actions_from_draw<W>(c_act, N, a.n1_magic, m);
         uint32_t pc = 0;
 #pragma unroll
         for (int w = 0; w < W; ++w) pc += __builtin_popcount(m[w]);
@@ -1113,9 +1141,16 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
         const int g1 = (int)e1.y + (E.y >= e1.x ? 1 : 0);
         const int g2 = (int)e2.y + (u2 >= e2.x ? 1 : 0);
         const int p0 = g0 - 1, p1 = p0 + g1, p2 = p1 + g2;
-        set_bit<W>(gam, p0, N);
-        set_bit<W>(gam, p1, N);
-        set_bit<W>(gam, p2, N);
+        if constexpr (W == 1) {
+          // N <= 31: a position past the network lands on a bit >= N (bit 31 at most), cleared by
+          // the word mask once
+          gam[0] = ((1u << min((uint32_t)p0, 31u)) | (1u << min((uint32_t)p1, 31u)) |
+                    (1u << min((uint32_t)p2, 31u))) & valid_word_mask(N, 0);
+        } else {
+          set_bit<W>(gam, p0, N);
+          set_bit<W>(gam, p1, N);
+          set_bit<W>(gam, p2, N);
+        }
         bool pert = false;
 #pragma unroll
         for (int w = 0; w < W; ++w) {
@@ -1153,6 +1188,12 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
       }
       PBN_PSTAMP(k, 1);
       lds_barrier();
+    };
+    // two steps per trip with the ENV words alternating between EA and EB: no copies between steps
+    Word4 EA = env_call(0), EB = EA;
+    for (int k = 0; k <= n_steps; k += 2) {
+      env_step(k, EA, EB);
+      if (k + 1 <= n_steps) env_step(k + 1, EB, EA);
     }
   } else if (role == 1) {
     for (int k = 0; k <= n_steps; ++k) {
@@ -1713,6 +1754,7 @@ ResetFn pick_reset(int W) {
 
 struct pbn_net {
   int device = 0;
+  int n_cus = 256;   // compute units of the device (the pipelined rollout's priority choice)
   int n_nodes = 0, W = 0, B = 0, horizon = 0, n_attr = 0, n_states = 0;
   int cdf_len = 0, hash_bits = 0, hash_probes = 0, tab_words = 0;
   uint32_t hash_mult[4] = {0, 0, 0, 0};
@@ -2192,6 +2234,9 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     free_net(net);
     return fail(PBN_EDEVICE, "no HIP device");
   }
+  if (hipDeviceGetAttribute(&net->n_cus, hipDeviceAttributeMultiprocessorCount, net->device) != hipSuccess ||
+      net->n_cus <= 0)
+    net->n_cus = 256;
   if ((rc = upload(&net->d_fcompact, fcomp.data(), fcomp.size())) ||
       (rc = upload(&net->d_nrec, nrec.data(), nrec.size())) ||
       (rc = upload(&net->d_tab, tab.data(), tab.size())) ||
@@ -2436,7 +2481,9 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
   bool pipe = net->lds_pipe <= 64 * 1024 && !net->n_gates;
   if (net->force_roll) pipe = net->force_roll == 3 && !net->n_gates;
   if (pipe) {   // one block of three waves per pair of groups
-    hipLaunchKernelGGL(net->pipe, dim3((unsigned)((a.n_groups + 1) / 2)), dim3(192), net->lds_pipe,
+    const int64_t pblocks = (a.n_groups + 1) / 2;
+    a.sel_prio = pblocks <= 4 * (int64_t)net->n_cus ? 1 : 0;
+    hipLaunchKernelGGL(net->pipe, dim3((unsigned)pblocks), dim3(192), net->lds_pipe,
                        (hipStream_t)stream, a);
     HIP_OK(hipGetLastError());
     return PBN_OK;

@@ -21,6 +21,14 @@ def test_step_bytes():
     assert bench.algorithmic_bytes_per_env(2) == 32
 
 
+def test_survey_bytes_price_the_roofline():
+    # 20 B/env-step up to 32 nodes (u32 state), 56 B for pbn70 (2 x u64 state)
+    assert bench.survey_bytes_per_env_step(7) == bench.survey_bytes_per_env_step(28) == 20
+    assert bench.survey_bytes_per_env_step(32) == 20
+    assert bench.survey_bytes_per_env_step(70) == bench.survey_bytes_per_env_step(128) == 56
+    assert bench.survey_bytes_per_env_step(33) == 3 * 8 + 8
+
+
 @pytest.mark.parametrize("steps,chunk", [(2000, 100), (250, 100), (7, 3), (5, 10), (0, 4)])
 def test_launch_plan(steps, chunk):
     plan = bench.launch_plan(steps, chunk)

@@ -20,6 +20,38 @@ STAMP_LIB = os.path.join(ROOT, "pbn_rl_amd", "libpbn_env_stamps.so")
 PHASES = ["tables+barrier", "philox", "per-env", "transpose+S", "node eval", "back-transpose", "epilogue"]
 
 
+def placement(full, it):
+    """Where the pipelined kernel's waves ran (HW_ID/XCC_ID words the stamps build stores at
+    kernel start: role 0 in column 14, roles 1, 2 in columns 7, 11): the role mix per SIMD and the
+    iteration time of blocks by the heaviest role mix among their waves' SIMDs."""
+    import numpy as np
+    from collections import Counter
+    hw = full[:, [14, 7, 11]].astype(np.uint64)
+    lo = (hw & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    xcc = ((hw >> np.uint64(32)) & np.uint64(0xF)).astype(np.int64)
+    simd = (lo >> 4) & 3
+    cu = (lo >> 8) & 15
+    sh = (lo >> 12) & 1
+    se = (lo >> 13) & 7
+    key = (((xcc * 8 + se) * 2 + sh) * 16 + cu) * 4 + simd          # [blocks, role]
+    cukey = key // 4
+    mix = {}
+    for role in range(3):
+        for k in key[:, role]:
+            mix.setdefault(int(k), [0, 0, 0])[role] += 1
+    comp = Counter(tuple(v) for v in mix.values())
+    same_cu = float(np.mean((cukey[:, 0] == cukey[:, 1]) & (cukey[:, 0] == cukey[:, 2])))
+    distinct = float(np.mean((key[:, 0] != key[:, 1]) & (key[:, 0] != key[:, 2]) & (key[:, 1] != key[:, 2])))
+    # per block: the most selection-heavy SIMD among its three waves
+    worst = np.array([max(mix[int(k)][2] for k in key[b]) for b in range(len(key))])
+    by_worst = {int(w): {"blocks": int((worst == w).sum()), "iteration_median": int(np.median(it[worst == w]))}
+                for w in np.unique(worst)}
+    return {"simds_used": len(mix), "cus_used": len(set(int(k) // 4 for k in mix)),
+            "role_mix_per_simd (state, env, sel): count": {str(k): v for k, v in comp.most_common(12)},
+            "block_waves_same_cu": same_cu, "block_waves_distinct_simds": distinct,
+            "by_max_selection_waves_on_a_block_simd": by_worst}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--build", action="store_true")
@@ -91,6 +123,7 @@ def main():
             "epilogue": int(np.median(full[:, 1] - full[:, 13]))}
         it = t[:, :, 2].max(axis=1) - t[:, :, 0].min(axis=1)
         rep["iteration_median"] = int(np.median(it))
+        rep["placement"] = placement(full, it)
         print(json.dumps(rep, indent=1))
         return
     t = buf.view(waves, 16)[:, :8].cpu().numpy().astype(np.int64)
