@@ -150,10 +150,22 @@ struct StepArgs {
       if (a.stamps && (threadIdx.x & 63) == 0) a.stamps[(size_t)blockIdx.x * 16 + (idx_)] = t_; \
     }                                                                                         \
   } while (0)
+// pipelined rollout, launch anatomy: the state wave's s_memrealtime (100 MHz, one clock for the
+// whole chip) at kernel entry, after the table image, at the loop start, after iterations 0 and
+// 1, after the loop and after its final stores have landed; row gridDim.x + block
+#define PBN_RSTAMP(idx_)                                                                      \
+  do {                                                                                        \
+    unsigned long long t_;                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)(gridDim.x + blockIdx.x) * 16 + (idx_)] = t_; \
+  } while (0)
 #else
 #define PBN_STAMP(k) do {} while (0)
 #define PBN_PSTAMP(k, slot_) do {} while (0)
 #define PBN_PSTAMP_AT(k, idx_) do {} while (0)
+#define PBN_RSTAMP(idx_) do {} while (0)
 #endif
 
 // Bounds-checked global indexing for the diagnostic library (-DPBN_CHECKS): an
@@ -989,6 +1001,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
   const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar branches
   // the state wave bounds every iteration: let it win VALU issue against the RNG waves of
   // other blocks sharing its SIMD
+  PBN_RSTAMP(0);
   if (role == 0) __builtin_amdgcn_s_setprio(PBN_STATE_PRIO);
   // with one block per SIMD triple (every SIMD holds one wave of each role) the selection wave,
   // the longest instruction stream, also goes ahead of the env-draw wave: -5 % per step at
@@ -1057,6 +1070,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
   // measured -15 % on pbn70 x 1M)
   uint32_t* cm = slots + 2 * (size_t)a.slot_words;
   __syncthreads();
+  PBN_RSTAMP(1);
   if constexpr (W == 1) {
     // thread t: record (q, i) = p = t mod 96 and digits [h B/2, (h+1) B/2), h = t / 96 (192
     // threads = two per record: two LDS reads, then B/2 independent writes)
@@ -1077,6 +1091,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
   // drain the initial state loads here: otherwise the loop-carried st / t / target copies at
   // the bottom of the loop wait on vmcnt(0), which also waits for every store of the step
   __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
+  PBN_RSTAMP(2);
 
 #ifndef PBN_DIAG_SKIP_ROLE
 #define PBN_DIAG_SKIP_ROLE -1   // diagnostic builds only: one role does no work (timing shares)
@@ -1502,6 +1517,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
           PBN_PSTAMP(k, 1);
           lds_barrier();
           PBN_PSTAMP(k, 2);
+          if (k <= 1) PBN_RSTAMP(3 + k);
         }
       };
       switch (u_mnf) {
@@ -1593,12 +1609,17 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
       lds_barrier();
       PBN_PSTAMP(k, 2);
     }
+    PBN_RSTAMP(5);
     if (valid) {
 #pragma unroll
       for (int w = 0; w < W; ++w) a.state_out[CK((size_t)w * n + le, plane, 16)] = st[w];
       a.t[CK(le, n, 17)] = (uint8_t)tt0;
       a.target[CK(le, n, 18)] = (uint8_t)tg0;
     }
+#ifdef PBN_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+    PBN_RSTAMP(6);
+#endif
   }
 }
 

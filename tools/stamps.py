@@ -52,6 +52,30 @@ def placement(full, it):
             "by_max_selection_waves_on_a_block_simd": by_worst}
 
 
+def anatomy(r, n_steps, hw=None):
+    """Launch anatomy from the state waves' s_memrealtime stamps (100 MHz): entry, image in LDS,
+    loop start, after iterations 0 and 1, loop end, final stores landed (columns 0..6)."""
+    import numpy as np
+    us = lambda x: round(float(x) / 100.0, 3)       # 100 MHz ticks -> us
+    med = lambda x: us(np.median(x))
+    t0 = r[:, 0].min()
+    return {"clock": "s_memrealtime, 100 MHz", "blocks": int(len(r)),
+            "entry_spread_us": us(r[:, 0].max() - t0),
+            "image_us": med(r[:, 1] - r[:, 0]), "digit_masks_us": med(r[:, 2] - r[:, 1]),
+            "iteration0_us": med(r[:, 3] - r[:, 2]), "iteration1_us": med(r[:, 4] - r[:, 3]),
+            "loop_us": med(r[:, 5] - r[:, 2]), "per_iteration_us": round(float(np.median(r[:, 5] - r[:, 2])) / 100.0 / (n_steps + 1), 4),
+            "final_stores_us": med(r[:, 6] - r[:, 5]),
+            "first_entry_to_last_exit_us": us(r[:, 6].max() - t0),
+            "loop_start_spread_us": us(r[:, 2].max() - r[:, 2].min()),
+            "last_loop_end_minus_first_us": us(r[:, 5].max() - r[:, 5].min()),
+            "loop_us_pcts": {p: us(np.percentile(r[:, 5] - r[:, 2], p)) for p in (0, 10, 50, 90, 99, 100)},
+            "by_xcc": None if hw is None else {
+                int(x): {"blocks": int((xcc == x).sum()), "loop_us_median": med((r[:, 5] - r[:, 2])[xcc == x]),
+                         "loop_us_max": us(((r[:, 5] - r[:, 2])[xcc == x]).max()),
+                         "loop_end_max_us": us((r[:, 5][xcc == x]).max() - t0)}
+                for xcc in [(hw.astype(np.uint64) >> np.uint64(32)).astype(np.int64) & 0xF] for x in np.unique(xcc)}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--build", action="store_true")
@@ -124,6 +148,9 @@ def main():
         it = t[:, :, 2].max(axis=1) - t[:, :, 0].min(axis=1)
         rep["iteration_median"] = int(np.median(it))
         rep["placement"] = placement(full, it)
+        if args.rollout:
+            rep["anatomy"] = anatomy(buf.view(-1, 16)[waves:2 * waves, :7].cpu().numpy().astype(np.int64),
+                                     args.rollout, full[:, 14])
         print(json.dumps(rep, indent=1))
         return
     t = buf.view(waves, 16)[:, :8].cpu().numpy().astype(np.int64)
