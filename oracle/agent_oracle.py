@@ -8,8 +8,8 @@ pbn_rl_amd/csrc/pbn_agent.hip.  Follows the frame loop of the reference:
     branch, branch k from EXPLORE word k + 1 by a 32-bit multiply-high (:74-76), else
     argmax of each branch's Q row (:95-96, torch.argmax: first maximum, NaN is the maximum);
   - env actions: list(action.unique()) (:176), a > 0 flips node a-1 (:81-84).
-The explore draws follow DESIGN.md (Philox4x32-10, stream EXPLORE = 4); Philox is vectorised
-here over envs and checked against oracle/pyoracle.philox4x32_10 by the tests.
+The explore draws follow DESIGN.md (Philox4x32-7, stream EXPLORE = 4); Philox is vectorised
+here over envs and checked against oracle/pyoracle.philox4x32 by the tests.
 """
 from __future__ import annotations
 
@@ -20,11 +20,14 @@ W0, W1 = 0x9E3779B9, 0xBB67AE85
 EXPLORE = 4
 
 
-def philox_vec(c0, c1, c2, c3, k0: int, k1: int):
-    """Philox4x32-10 over arrays of counters (uint32), scalar key."""
+PHILOX_ROUNDS = 7   # every stream (DESIGN.md "RNG"); = pyoracle.PHILOX_ROUNDS
+
+
+def philox_vec(c0, c1, c2, c3, k0: int, k1: int, rounds: int = PHILOX_ROUNDS):
+    """Philox4x32-R over arrays of counters (uint32), scalar key (R = 7 for every stream)."""
     c0, c1, c2, c3 = (np.asarray(c, dtype=np.uint64) & np.uint64(0xFFFFFFFF) for c in (c0, c1, c2, c3))
     mask = np.uint64(0xFFFFFFFF)
-    for _ in range(10):
+    for _ in range(rounds):
         p0 = M0 * c0
         p1 = M1 * c2
         n0 = (p1 >> np.uint64(32)) ^ c1 ^ np.uint64(k0)

@@ -36,6 +36,8 @@ def lib():
         L.oracle_reset.restype = i32
         L.oracle_philox4x32_10.argtypes = [vp, vp, vp]
         L.oracle_philox4x32_10.restype = None
+        L.oracle_philox4x32_r.argtypes = [vp, vp, vp, i32]
+        L.oracle_philox4x32_r.restype = None
         _lib = L
     return _lib
 
@@ -44,11 +46,15 @@ def _p(a):
     return None if a is None else a.ctypes.data
 
 
-def philox(ctr, key):
+def philox(ctr, key, rounds: int = 10):
+    """Philox4x32-R of the C oracle (10 = rocRAND's philox4x32_10; the streams draw R = 7)."""
     c = np.ascontiguousarray(ctr, dtype=np.uint32)
     k = np.ascontiguousarray(key, dtype=np.uint32)
     out = np.zeros(4, dtype=np.uint32)
-    lib().oracle_philox4x32_10(_p(c), _p(k), _p(out))
+    if rounds == 10:
+        lib().oracle_philox4x32_10(_p(c), _p(k), _p(out))
+    else:
+        lib().oracle_philox4x32_r(_p(c), _p(k), _p(out), rounds)
     return out
 
 

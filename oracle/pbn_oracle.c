@@ -18,9 +18,10 @@
  *   - termination = s' in the target attractor (model_tester.py:616 in_target);
  *   - wildcard '*' -> 0 in attractor states (model_tester.py:609), applied by
  *     the Python side before it builds the descriptor.
- * Philox4x32-10 follows the Random123 definition (Salmon et al., SC'11); it is
- * pinned by known-answer vectors and by rocRAND's philox4x32_10 engine in
- * tests/test_philox.py.
+ * Philox4x32-R follows the Random123 definition (Salmon et al., SC'11); every
+ * stream draws R = 7 rounds (DESIGN.md "RNG").  The round function is pinned by
+ * rocRAND's philox4x32_10 engine (R = 10) and Random123's known-answer vectors
+ * (R = 7 and 10) in tests/test_philox.py.
  *
  * Written for clarity: scalar per env, the group selection words recomputed
  * per group of 32 envs (the unit the semantics defines), OpenMP over groups.
@@ -36,9 +37,12 @@
 
 enum { STREAM_SEL = 0, STREAM_ENV = 1, STREAM_PERT = 2, STREAM_RESET = 3 };
 
-static void philox4x32_10(const uint32_t ctr_in[4], uint32_t k0, uint32_t k1, uint32_t out[4]) {
+/* every stream draws Philox4x32-7 (DESIGN.md "RNG"); the KAT export runs any round count */
+enum { PHILOX_ROUNDS = 7 };
+
+static void philox4x32_r(const uint32_t ctr_in[4], uint32_t k0, uint32_t k1, uint32_t out[4], int rounds) {
   uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
-  for (int r = 0; r < 10; ++r) {
+  for (int r = 0; r < rounds; ++r) {
     uint64_t p0 = (uint64_t)0xD2511F53u * c0;
     uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
     uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
@@ -53,7 +57,11 @@ static void philox4x32_10(const uint32_t ctr_in[4], uint32_t k0, uint32_t k1, ui
 }
 
 void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
-  philox4x32_10(ctr, key[0], key[1], out);
+  philox4x32_r(ctr, key[0], key[1], out, 10);
+}
+
+void oracle_philox4x32_r(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4], int rounds) {
+  philox4x32_r(ctr, key[0], key[1], out, rounds);
 }
 
 static void draw(uint64_t seed, uint64_t id, uint64_t step, uint32_t stream, uint32_t idx,
@@ -63,7 +71,7 @@ static void draw(uint64_t seed, uint64_t id, uint64_t step, uint32_t stream, uin
   ctr[1] = (uint32_t)step;
   ctr[2] = (stream << 28) | (idx & 0x0FFFFFFFu);
   ctr[3] = (uint32_t)((id >> 32) & 0xFFFFu) | (uint32_t)(((step >> 32) & 0xFFFFu) << 16);
-  philox4x32_10(ctr, (uint32_t)seed, (uint32_t)(seed >> 32), out);
+  philox4x32_r(ctr, (uint32_t)seed, (uint32_t)(seed >> 32), out, PHILOX_ROUNDS);
 }
 
 static int words_of(int n) { return (n + 31) / 32; }

@@ -19,10 +19,15 @@ SEL, ENV, PERT, RESET = 0, 1, 2, 3
 MODE_AUTORESET, MODE_RANDOM_ACTIONS = 1, 2
 
 
-def philox4x32_10(ctr: Sequence[int], key: Sequence[int]) -> Tuple[int, int, int, int]:
+# every stream draws Philox4x32-7 (DESIGN.md "RNG"); the round function is pinned at 7 and 10
+# rounds by known-answer vectors (tests/test_philox.py)
+PHILOX_ROUNDS = 7
+
+
+def philox4x32(ctr: Sequence[int], key: Sequence[int], rounds: int = PHILOX_ROUNDS) -> Tuple[int, int, int, int]:
     c0, c1, c2, c3 = (int(x) & MASK32 for x in ctr)
     k0, k1 = int(key[0]) & MASK32, int(key[1]) & MASK32
-    for _ in range(10):
+    for _ in range(rounds):
         p0 = M0 * c0
         p1 = M1 * c2
         c0, c1, c2, c3 = ((p1 >> 32) ^ c1 ^ k0) & MASK32, p1 & MASK32, ((p0 >> 32) ^ c3 ^ k1) & MASK32, p0 & MASK32
@@ -31,10 +36,14 @@ def philox4x32_10(ctr: Sequence[int], key: Sequence[int]) -> Tuple[int, int, int
     return c0, c1, c2, c3
 
 
+def philox4x32_10(ctr: Sequence[int], key: Sequence[int]) -> Tuple[int, int, int, int]:
+    return philox4x32(ctr, key, 10)
+
+
 def draw(seed: int, ident: int, step: int, stream: int, idx: int):
     ctr = (ident & MASK32, step & MASK32, (stream << 28) | (idx & 0x0FFFFFFF),
            ((ident >> 32) & 0xFFFF) | (((step >> 32) & 0xFFFF) << 16))
-    return philox4x32_10(ctr, (seed & MASK32, (seed >> 32) & MASK32))
+    return philox4x32(ctr, (seed & MASK32, (seed >> 32) & MASK32))
 
 
 def ext64(x: int, k: int) -> Tuple[int, int]:

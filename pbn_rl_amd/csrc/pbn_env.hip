@@ -648,7 +648,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
     } else {   // (upper list done: a discarded call)
       uc0 = ge_lo; uc2 = pbn::kStreamEnv << 28; uc3 = ge_hi;
     }
-    out[it] = pbn::philox4x32_10(lo ? lc0 : uc0, st_lo, lo ? lc2 : uc2, lo ? lc3 : uc3, kk0, kk1);
+    out[it] = pbn::philox(lo ? lc0 : uc0, st_lo, lo ? lc2 : uc2, lo ? lc3 : uc3, kk0, kk1);
   }
   // digits of node l32 + 32r: calls c < H from this lane, c >= H from lane + 32
   uint32_t dig[W][16];
@@ -727,7 +727,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
       int pos = p2;
       for (int kk = 3; pos < N - 1; ++kk) {
         if (((kk - 3) & 3) == 0)
-          P = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamPert << 28) | (uint32_t)((kk - 3) >> 2), ge_hi, kk0, kk1);
+          P = pbn::philox(ge_lo, st_lo, (pbn::kStreamPert << 28) | (uint32_t)((kk - 3) >> 2), ge_hi, kk0, kk1);
         const int j4 = (kk - 3) & 3;
         const uint32_t u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
         pos += gap_any(a.gap_exact, L, a, u);
@@ -856,7 +856,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
       for (int w = 0; w < W; ++w) sp[w] = att_words[(size_t)r_row * W + w];
       nt = r_nt;
     } else {
-      const Word4 rr = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamReset << 28) | 1u, ge_hi, kk0, kk1);
+      const Word4 rr = pbn::philox(ge_lo, st_lo, (pbn::kStreamReset << 28) | 1u, ge_hi, kk0, kk1);
       const uint32_t rw4[4] = {rr.x, rr.y, rr.z, rr.w};
 #pragma unroll
       for (int w = 0; w < W; ++w) sp[w] = rw4[w] & valid_word_mask(N, w);
@@ -1113,7 +1113,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
     auto env_call = [&](int k) {
       const uint64_t step = a.step + (uint64_t)k;
       const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
-      return pbn::philox4x32_10((uint32_t)ge, (uint32_t)step, pbn::kStreamEnv << 28, ge_hi, u_k0, u_k1);
+      return pbn::philox((uint32_t)ge, (uint32_t)step, pbn::kStreamEnv << 28, ge_hi, u_k0, u_k1);
     };
     // one step: this step's draws from E, the next step's ENV call into E_next
     auto env_step = [&](int k, const Word4& E, Word4& E_next) {
@@ -1186,7 +1186,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
           int pos = p2;
           for (int kk = 3; pos < N - 1; ++kk) {
             if (((kk - 3) & 3) == 0)
-              P = pbn::philox4x32_10((uint32_t)ge, (uint32_t)step, (pbn::kStreamPert << 28) | (uint32_t)((kk - 3) >> 2), ge_hi, u_k0, u_k1);
+              P = pbn::philox((uint32_t)ge, (uint32_t)step, (pbn::kStreamPert << 28) | (uint32_t)((kk - 3) >> 2), ge_hi, u_k0, u_k1);
             const int j4 = (kk - 3) & 3;
             const uint32_t u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
             pos += gap_lut(lut, a.gap_shift, a.gap_nb, u);
@@ -1224,7 +1224,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
         const uint32_t ge_lo = (uint32_t)ge;
         // one ENV call: words 0, 1 = gaps 0, 1; X = words 3:2 gives, in order, the action draw
         // (every mode), the autoreset draws and gap 2's uniform u2 (DESIGN.md "Step semantics")
-        const Word4 E = pbn::philox4x32_10(ge_lo, st_lo, pbn::kStreamEnv << 28, ge_hi, u_k0, u_k1);
+        const Word4 E = pbn::philox(ge_lo, st_lo, pbn::kStreamEnv << 28, ge_hi, u_k0, u_k1);
         if (valid) {
           uint32_t m[W], gam[W], rs[W];
 #pragma unroll
@@ -1261,7 +1261,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
 #pragma unroll
             for (int w = 0; w < W; ++w) rs[w] = att_words[(size_t)(st0 + idx) * W + w];
           } else {
-            const Word4 rr = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamReset << 28) | 1u, ge_hi, u_k0, u_k1);
+            const Word4 rr = pbn::philox(ge_lo, st_lo, (pbn::kStreamReset << 28) | 1u, ge_hi, u_k0, u_k1);
             const uint32_t rw4[4] = {rr.x, rr.y, rr.z, rr.w};
 #pragma unroll
             for (int w = 0; w < W; ++w) rs[w] = rw4[w] & valid_word_mask(N, w);
@@ -1299,7 +1299,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
             int pos = p2;
             for (int kk = 3; pos < N - 1; ++kk) {
               if (((kk - 3) & 3) == 0)
-                P = pbn::philox4x32_10(ge_lo, st_lo, (pbn::kStreamPert << 28) | (uint32_t)((kk - 3) >> 2), ge_hi, u_k0, u_k1);
+                P = pbn::philox(ge_lo, st_lo, (pbn::kStreamPert << 28) | (uint32_t)((kk - 3) >> 2), ge_hi, u_k0, u_k1);
               const int j4 = (kk - 3) & 3;
               const uint32_t u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
               pos += gap_any(u_gx, L, a, u);
@@ -1335,7 +1335,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
         const uint32_t G_hi = (uint32_t)((G >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
 #pragma unroll
         for (int c = 0; c < CPN; ++c) {
-          const Word4 o = pbn::philox4x32_10((uint32_t)G, (uint32_t)step, (pbn::kStreamSel << 28) | (uint32_t)(4 * l32 + c),
+          const Word4 o = pbn::philox((uint32_t)G, (uint32_t)step, (pbn::kStreamSel << 28) | (uint32_t)(4 * l32 + c),
                                              G_hi, u_k0, u_k1);
           d[4 * c + 0] = o.x; d[4 * c + 1] = o.y; d[4 * c + 2] = o.z; d[4 * c + 3] = o.w;
         }
@@ -1392,7 +1392,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
             uint32_t dig[16];
 #pragma unroll
             for (int c = 0; c < CPN; ++c) {
-              const Word4 o = pbn::philox4x32_10(G_lo, st_lo, (pbn::kStreamSel << 28) | (uint32_t)(4 * i + c), G_hi, u_k0, u_k1);
+              const Word4 o = pbn::philox(G_lo, st_lo, (pbn::kStreamSel << 28) | (uint32_t)(4 * i + c), G_hi, u_k0, u_k1);
               dig[4 * c + 0] = o.x; dig[4 * c + 1] = o.y; dig[4 * c + 2] = o.z; dig[4 * c + 3] = o.w;
             }
             const int nf = (int)r0.w;

@@ -55,7 +55,9 @@ def test_vectorised_philox_matches_scalar():
         ctr = rng.integers(0, 2 ** 32, size=4, dtype=np.uint64)
         key = rng.integers(0, 2 ** 32, size=2, dtype=np.uint64)
         got = agent_oracle.philox_vec(*[np.array([c]) for c in ctr], int(key[0]), int(key[1]))
-        assert tuple(int(g[0]) for g in got) == pyoracle.philox4x32_10(ctr, key)
+        assert tuple(int(g[0]) for g in got) == pyoracle.philox4x32(ctr, key)
+        got10 = agent_oracle.philox_vec(*[np.array([c]) for c in ctr], int(key[0]), int(key[1]), rounds=10)
+        assert tuple(int(g[0]) for g in got10) == pyoracle.philox4x32_10(ctr, key)
     w = agent_oracle.explore_words(7, 11, 64, 4)
     for e in range(4):
         assert tuple(int(x[e]) for x in w) == pyoracle.draw(7, 64 + e, 11, agent_oracle.EXPLORE, 0)

@@ -1,4 +1,8 @@
-"""Philox4x32-10 of the oracle (C and Python) against rocRAND + Random123 known answers."""
+"""Philox of the oracle (C and Python) against rocRAND + Random123 known answers.
+
+Every stream draws Philox4x32-7 (DESIGN.md "RNG"); the round function is pinned at 10 rounds by
+rocRAND's philox4x32_10 engine and Random123's kat_vectors, and at 7 rounds by Random123's
+kat_vectors (the "philox4x32 7" lines: same three inputs)."""
 import json
 import os
 
@@ -21,6 +25,19 @@ def test_random123_known_answers():
     assert c[2]["out"] == [0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]
 
 
+# Random123 kat_vectors, philox4x32 R = 7, on the inputs of cases()[0:3]
+R123_KAT7 = [[0x5F6FB709, 0x0D893F64, 0x4F121F81, 0x4F730A48],
+             [0x5207DDC2, 0x45165E59, 0x4D8EE751, 0x8C52F662],
+             [0x4DFCCABA, 0x190A87F0, 0xC47362BA, 0xB6B5242A]]
+
+
+def test_random123_known_answers_7_rounds():
+    for cs, want in zip(cases()[:3], R123_KAT7):
+        assert list(pyoracle.philox4x32(cs["ctr"], cs["key"], 7)) == want
+        assert list(oracle.philox(cs["ctr"], cs["key"], 7)) == want
+    assert pyoracle.PHILOX_ROUNDS == 7
+
+
 def test_c_oracle_matches_rocrand():
     for cs in cases():
         assert list(oracle.philox(cs["ctr"], cs["key"])) == cs["out"]
@@ -36,5 +53,5 @@ def test_counter_map():
     seed, ident, step = 0x0123456789ABCDEF, 0x0000_1234_89AB_CDEF, 0x0000_0042_0000_0007
     got = pyoracle.draw(seed, ident, step, 2, 5)
     ctr = [ident & 0xFFFFFFFF, step & 0xFFFFFFFF, (2 << 28) | 5, (ident >> 32) & 0xFFFF | ((step >> 32) & 0xFFFF) << 16]
-    assert got == pyoracle.philox4x32_10(ctr, [seed & 0xFFFFFFFF, seed >> 32])
-    assert list(oracle.philox(ctr, [seed & 0xFFFFFFFF, seed >> 32])) == list(got)
+    assert got == pyoracle.philox4x32(ctr, [seed & 0xFFFFFFFF, seed >> 32], 7)
+    assert list(oracle.philox(ctr, [seed & 0xFFFFFFFF, seed >> 32], 7)) == list(got)
