@@ -201,6 +201,17 @@ __device__ __forceinline__ T& lane_at(T* base, size_t uniform_elems, uint32_t la
 #else
 #define LANE_AT(base, ubase, le_, len, site) lane_at((base), (ubase), (uint32_t)(le_) * (uint32_t)sizeof(*(base)))
 #endif
+// Streaming store of a rollout output (pbn_rollout_pipe): non-temporal, so that the per-step
+// obs / flip-mask / reward / flags stream does not evict the table image from L2 between
+// launches (every launch re-reads it)
+#ifndef PBN_NT_STORES
+#define PBN_NT_STORES 1
+#endif
+#if PBN_NT_STORES && !defined(PBN_CHECKS)
+#define LANE_ST(base, ubase, le_, len, site, v) __builtin_nontemporal_store((v), &LANE_AT(base, ubase, le_, len, site))
+#else
+#define LANE_ST(base, ubase, le_, len, site, v) (LANE_AT(base, ubase, le_, len, site) = (v))
+#endif
 __device__ __forceinline__ uint32_t valid_word_mask(int n, int w) {
   const int bits = n - 32 * w;
   return bits >= 32 ? 0xFFFFFFFFu : (bits <= 0 ? 0u : ((1u << bits) - 1u));
@@ -1177,7 +1188,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
         slot[3 * W * 64 + lane] = rt | (pc << 8) | ((uint32_t)pert << 16);
         if (valid) {
 #pragma unroll
-          for (int w = 0; w < W; ++w) LANE_AT(a.flipmask, k * plane + (size_t)w * n, le, (size_t)n_steps * plane, 8) = m[w];
+          for (int w = 0; w < W; ++w) LANE_ST(a.flipmask, k * plane + (size_t)w * n, le, (size_t)n_steps * plane, 8, m[w]);
         }
         if (p2 < N - 1) {   // rare: a fourth flip is possible (gap k >= 3: PERT call (k-3)>>2, word (k-3)&3)
           const uint64_t step = a.step + (uint64_t)k;
@@ -1271,7 +1282,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
           if (u_fl & 4u) {
             actions_from_draw<W>(c_act, N, a.n1_magic, m);
 #pragma unroll
-            for (int w = 0; w < W; ++w) LANE_AT(a.flipmask, k * plane + (size_t)w * n, le, (size_t)n_steps * plane, 8) = m[w];
+            for (int w = 0; w < W; ++w) LANE_ST(a.flipmask, k * plane + (size_t)w * n, le, (size_t)n_steps * plane, 8, m[w]);
           } else {
 #pragma unroll
             for (int w = 0; w < W; ++w)
@@ -1428,7 +1439,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
         for (int w = 0; w < W; ++w) sp[w] = pert ? (s1[w] ^ gam[w]) : sp[w];
         if (valid && (u_fl & 2u)) {
 #pragma unroll
-          for (int w = 0; w < W; ++w) LANE_AT(a.final_state, t * plane + (size_t)w * n, le, (size_t)n_steps * plane, 10) = sp[w];
+          for (int w = 0; w < W; ++w) LANE_ST(a.final_state, t * plane + (size_t)w * n, le, (size_t)n_steps * plane, 10, sp[w]);
         }
         // reward candidates depend only on popcount(flipmask): one 16-byte row {none, wrong,
         // term, -} read beside the hash
@@ -1459,8 +1470,8 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
         const uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) |
                             ((uint32_t)pert << 3) | ((uint32_t)reset << 4);
         if (valid) {
-          LANE_AT(a.reward, (size_t)t * n, le, (size_t)n_steps * n, 11) = term ? r_term : (wrong ? r_wrong : r_none);
-          LANE_AT(a.flags, (size_t)t * n, le, (size_t)n_steps * n, 15) = (uint8_t)fl;
+          LANE_ST(a.reward, (size_t)t * n, le, (size_t)n_steps * n, 11, term ? r_term : (wrong ? r_wrong : r_none));
+          LANE_ST(a.flags, (size_t)t * n, le, (size_t)n_steps * n, 15, (uint8_t)fl);
         }
         tg0 = reset ? (info & 0xFFu) : tg0;
         tt0 = reset ? 0u : (uint32_t)tt;
@@ -1498,7 +1509,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
               sa[q] = selq[(2 * q) * 32 + l32];
               sb[q] = selq[(2 * q + 1) * 32 + l32];
             }
-            if (valid && (u_fl & 1u)) LANE_AT(a.obs, (size_t)t * plane, le, (size_t)n_steps * plane, 7) = st[0];
+            if (valid && (u_fl & 1u)) LANE_ST(a.obs, (size_t)t * plane, le, (size_t)n_steps * plane, 7, st[0]);
             Sg[l32] = lane_transpose32(s1[0], lane);
             __builtin_amdgcn_wave_barrier();
             uint32_t x = 0;
@@ -1547,7 +1558,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
         info = slot[3 * W * 64 + lane];
         if (valid && (u_fl & 1u)) {
 #pragma unroll
-          for (int w = 0; w < W; ++w) LANE_AT(a.obs, t * plane + (size_t)w * n, le, (size_t)n_steps * plane, 7) = st[w];
+          for (int w = 0; w < W; ++w) LANE_ST(a.obs, t * plane + (size_t)w * n, le, (size_t)n_steps * plane, 7, st[w]);
         }
 #pragma unroll
         for (int w = 0; w < W; ++w) Sg[32 * w + l32] = lane_transpose32(s1[w], lane);
