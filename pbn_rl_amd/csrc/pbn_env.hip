@@ -2515,6 +2515,9 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
   if (pipe) {   // one block of three waves per pair of groups
     const int64_t pblocks = (a.n_groups + 1) / 2;
     a.sel_prio = pblocks <= 4 * (int64_t)net->n_cus ? 1 : 0;
+#ifdef PBN_DIAG_SEL_PRIO   // diagnostic builds only: 0 never, 1 always
+    a.sel_prio = PBN_DIAG_SEL_PRIO;
+#endif
     hipLaunchKernelGGL(net->pipe, dim3((unsigned)pblocks), dim3(192), net->lds_pipe,
                        (hipStream_t)stream, a);
     HIP_OK(hipGetLastError());
