@@ -61,13 +61,14 @@
 extern "C" {
 #endif
 
-#define PBN_ABI_VERSION 2
+#define PBN_ABI_VERSION 3
 
 #define PBN_MAX_NODES 128
 #define PBN_MAX_ARITY 4
 #define PBN_MAX_FUNCS_PER_NODE 16
 #define PBN_MAX_ATTRACTORS 254
 #define PBN_MAX_GATES 224          /* and 32 * ceil(n_nodes / 32) + n_gates <= 256 */
+#define PBN_MAX_SETTLE 4096        /* cap of settle_max (synchronous updates per env step) */
 #define PBN_NO_TARGET 0xFF
 
 /* error codes */
@@ -87,6 +88,7 @@ extern "C" {
 #define PBN_FLAG_IN_ATTRACTOR 4u   /* s' is a state of some attractor */
 #define PBN_FLAG_PERTURBED 8u      /* a perturbation fired this step */
 #define PBN_FLAG_RESET 16u         /* autoreset happened: state_out is a fresh start */
+#define PBN_FLAG_UNSETTLED 32u     /* settle law: settle_max updates ran and s' is in no attractor */
 
 /*
  * Network description (semantic form; the library derives its kernel encodings).
@@ -99,6 +101,14 @@ extern "C" {
  * Attractor a owns states attractor_start[a] .. attractor_start[a+1]-1; state k
  * is words attractor_states[k*W .. k*W+W).  reward_table[(2*term + wrong)*(N+1) + k]
  * with k = popcount(flipmask), wrong = in some non-target attractor.
+ *
+ * Step law (settle_max).  0 or 1: one synchronous update per env step (DESIGN.md "Step
+ * semantics").  K >= 2, the settle law: after the intervention the network keeps updating
+ * synchronously until the state is a state of some attractor, at most K updates in all;
+ * flags carry PBN_FLAG_UNSETTLED when the K-th update still left it outside every attractor.
+ * That is the "intervene, then run to a (pseudo-)attractor" step that the reference's
+ * recorded bb33 evaluation pins (data/results/pbn_33_3.pkl under model_tester.py:587-658;
+ * DESIGN.md "Parity status").  Updates k >= 1 draw from the SETTLE_SEL / SETTLE_ENV streams.
  */
 typedef struct pbn_net_desc {
   int32_t n_nodes;
@@ -125,6 +135,7 @@ typedef struct pbn_net_desc {
   const int32_t* gate_arity;        /* [n_gates] 0..4 */
   const int32_t* gate_inputs;       /* [n_gates * 4], unused slots -1 */
   const uint32_t* gate_table;       /* [n_gates] */
+  int32_t settle_max;               /* 0..PBN_MAX_SETTLE, see "Step law" above (ABI 3) */
 } pbn_net_desc;
 
 typedef struct pbn_net pbn_net;
@@ -145,7 +156,8 @@ int pbn_reset(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, i
               uint32_t* d_state, uint8_t* d_target, uint8_t* d_t, void* stream);
 
 /*
- * One synchronous PBN transition of every env (the hot path).
+ * One env step of every env (the hot path): one synchronous PBN transition, or under the
+ * settle law (settle_max >= 2) the intervention followed by updates until an attractor.
  *   d_state        in   [W][n]  current observation s
  *   d_flipmask     in   [W][n]  intervention flips (bit a-1 for action a > 0);
  *                  out  with PBN_MODE_RANDOM_ACTIONS (the actions drawn)

@@ -24,7 +24,7 @@ from typing import Callable, Dict, List, Sequence, Tuple
 
 import numpy as np
 
-__all__ = ["transition_matrix", "flip_mask", "hitting_distribution", "pair_statistics"]
+__all__ = ["transition_matrix", "settle_matrix", "flip_mask", "hitting_distribution", "pair_statistics"]
 
 
 def _bits(s: int, n: int) -> List[int]:
@@ -63,6 +63,23 @@ def transition_matrix(net, p: float, prob_bits: int = 16) -> np.ndarray:
             probs *= np.where(bit == 1, p1[i], 1.0 - p1[i])
         T[s1] += ((1 - p) ** n) * probs
     return T
+
+
+def settle_matrix(T: np.ndarray, attractor_states: Sequence[int], settle: int) -> np.ndarray:
+    """The settle law's step matrix (include/pbn_env.h "Step law"): from s1, one update by T,
+    then further updates while the state is outside every attractor, at most ``settle``
+    updates in all.  M[s1, s'] = P(the step ends in s')."""
+    A = np.zeros(T.shape[0], bool)
+    A[list(attractor_states)] = True
+    M = np.zeros_like(T)
+    cur = T.copy()
+    for _ in range(1, max(settle, 1)):
+        M[:, A] += cur[:, A]
+        cur[:, A] = 0.0
+        if not cur.any():
+            break
+        cur = cur @ T
+    return M + cur
 
 
 def flip_mask(actions: Sequence[int], mode: str = "or") -> int:
@@ -129,10 +146,13 @@ def state_index(bits: Sequence[int]) -> int:
 
 
 def evaluate_protocol(net, attractors: List[List[Sequence[int]]], q_fn, p: float, prob_bits: int = 16,
-                      mode: str = "or", max_steps: int = 100) -> Dict[Tuple[int, int], np.ndarray]:
+                      mode: str = "or", max_steps: int = 100, settle: int = 0) -> Dict[Tuple[int, int], np.ndarray]:
     """Exact count distribution of every (start attractor, target attractor) pair of
-    model_tester.py:598 (itertools.product over the attractor indices)."""
+    model_tester.py:598 (itertools.product over the attractor indices); settle >= 2 uses the
+    settle law with ``attractors`` as the env's attractor set."""
     T = transition_matrix(net, p, prob_bits)
+    if settle >= 2:
+        T = settle_matrix(T, [state_index(s) for a in attractors for s in a], settle)
     out = {}
     for a, t in itertools.product(range(len(attractors)), repeat=2):
         start = state_index(attractors[a][0])

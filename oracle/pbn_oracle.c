@@ -35,7 +35,7 @@
 
 #include "../include/pbn_env.h"
 
-enum { STREAM_SEL = 0, STREAM_ENV = 1, STREAM_PERT = 2, STREAM_RESET = 3 };
+enum { STREAM_SEL = 0, STREAM_ENV = 1, STREAM_PERT = 2, STREAM_RESET = 3, STREAM_SETTLE_SEL = 5, STREAM_SETTLE_ENV = 6 };
 
 /* every stream draws Philox4x32-7 (DESIGN.md "RNG"); the KAT export runs any round count */
 enum { PHILOX_ROUNDS = 7 };
@@ -187,12 +187,85 @@ int oracle_reset(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t e
   return 0;
 }
 
+/* the rule update of every node of env bit b of its group from state s1, digit words D[i][d] */
+static void rule_update(const pbn_net_desc* d, const uint32_t* s1, uint32_t D[][16], int b, uint32_t* sp) {
+  const int N = d->n_nodes, W = words_of(N), B = d->prob_bits;
+  uint8_t gv[PBN_MAX_GATES];
+  eval_gates(d, s1, gv);
+  for (int w = 0; w < W; ++w) sp[w] = 0;
+  for (int i = 0; i < N; ++i) {
+    int f0 = d->node_func_start[i], nf = d->node_func_start[i + 1] - f0, x;
+    if (nf == 1) {
+      x = eval_func(d, f0, s1, gv);
+    } else {
+      uint32_t u = 0;
+      for (int dd = 0; dd < B; ++dd) u |= ((D[i][dd] >> b) & 1u) << (B - 1 - dd);
+      int j = 0;
+      while (j < nf - 1 && !(u < d->func_threshold[f0 + j])) ++j;
+      x = eval_func(d, f0 + j, s1, gv);
+    }
+    if (x) sp[i >> 5] |= 1u << (i & 31);
+  }
+}
+
+/* selection digit words of group G for update `sub` of a step: sub 0 = the SEL stream (the
+ * one-update law), sub k >= 1 = SETTLE_SEL with idx (k-1) << 9 | 4i + c */
+static void group_digits(const pbn_net_desc* d, uint64_t seed, uint64_t G, uint64_t step, int sub,
+                         uint32_t D[][16]) {
+  const int N = d->n_nodes, B = d->prob_bits;
+  for (int i = 0; i < N; ++i) {
+    int nf = d->node_func_start[i + 1] - d->node_func_start[i];
+    if (nf < 2) continue;
+    for (int c = 0; c < B / 4; ++c) {
+      if (sub == 0) draw(seed, G, step, STREAM_SEL, (uint32_t)(4 * i + c), &D[i][4 * c]);
+      else draw(seed, G, step, STREAM_SETTLE_SEL, ((uint32_t)(sub - 1) << 9) | (uint32_t)(4 * i + c), &D[i][4 * c]);
+    }
+  }
+}
+
+/* settle law (settle_max >= 2): updates k = 1 .. settle_max-1 of env e (group bit b) from sp
+ * until sp is a state of some attractor.  Update k: perturbation gaps j = 0, 1, ... from
+ * SETTLE_ENV call ((k-1) << 8 | j >> 2), word j & 3; unperturbed, the rule update with the
+ * group's SETTLE_SEL digits of update k (Dk[k-1], drawn on demand).  Returns 1 if still
+ * outside every attractor after the last update. */
+static int settle(const pbn_net_desc* d, uint64_t seed, uint64_t G, uint64_t e, uint64_t step, int b,
+                  uint32_t (*Dk)[PBN_MAX_NODES][16], int* have, uint32_t* sp, int* perturbed) {
+  const int N = d->n_nodes, W = words_of(N);
+  for (int k = 1; k < d->settle_max; ++k) {
+    if (attractor_of(d, sp, W) >= 0) return 0;
+    uint32_t gam[4] = {0, 0, 0, 0}, P[4];
+    int pos = -1;
+    for (int j = 0; pos < N - 1; ++j) {
+      if ((j & 3) == 0) draw(seed, e, step, STREAM_SETTLE_ENV, ((uint32_t)(k - 1) << 8) | (uint32_t)(j >> 2), P);
+      pos += gap_of(d, P[j & 3]);
+      if (pos >= N) break;
+      gam[pos >> 5] |= 1u << (pos & 31);
+    }
+    int pk = 0;
+    for (int w = 0; w < W; ++w) pk |= gam[w] != 0;
+    if (pk) {
+      for (int w = 0; w < W; ++w) sp[w] ^= gam[w];
+      *perturbed = 1;
+    } else {
+      if (!have[k - 1]) {
+        group_digits(d, seed, G, step, k, Dk[k - 1]);
+        have[k - 1] = 1;
+      }
+      uint32_t x[4];
+      rule_update(d, sp, Dk[k - 1], b, x);
+      for (int w = 0; w < W; ++w) sp[w] = x[w];
+    }
+  }
+  return attractor_of(d, sp, W) < 0;
+}
+
 int oracle_step(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n,
                 uint32_t mode, const uint32_t* state, uint32_t* flipmask, uint8_t* target, uint8_t* t,
                 uint32_t* state_out, uint32_t* final_state, float* reward, uint8_t* flags,
                 int n_threads) {
-  const int N = d->n_nodes, W = words_of(N), B = d->prob_bits;
+  const int N = d->n_nodes, W = words_of(N);
   if ((env_offset & 31u) || (n & 31)) return PBN_EINVAL;
+  if (d->settle_max < 0 || d->settle_max > PBN_MAX_SETTLE) return PBN_EINVAL;
   const int64_t n_groups = n / 32;
 #ifdef _OPENMP
   if (n_threads > 0) omp_set_num_threads(n_threads);
@@ -202,11 +275,11 @@ int oracle_step(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t en
     const uint64_t G = (env_offset >> 5) + (uint64_t)g;
     /* selection digit words of this group: D[i][d], digit d = 0 is the MSB of u */
     uint32_t D[PBN_MAX_NODES][16];
-    for (int i = 0; i < N; ++i) {
-      int nf = d->node_func_start[i + 1] - d->node_func_start[i];
-      if (nf < 2) continue;
-      for (int c = 0; c < B / 4; ++c) draw(seed, G, step, STREAM_SEL, (uint32_t)(4 * i + c), &D[i][4 * c]);
-    }
+    group_digits(d, seed, G, step, 0, D);
+    /* settle law: the group's digit words of updates 1.., drawn when an env first needs them */
+    const int n_sub = d->settle_max > 1 ? d->settle_max - 1 : 0;
+    uint32_t (*Dk)[PBN_MAX_NODES][16] = n_sub ? malloc((size_t)n_sub * sizeof *Dk) : NULL;
+    int* have = n_sub ? calloc((size_t)n_sub, sizeof(int)) : NULL;
     for (int b = 0; b < 32; ++b) {
       const int64_t li = g * 32 + b;
       const uint64_t e = env_offset + (uint64_t)li;
@@ -265,22 +338,9 @@ int oracle_step(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t en
       if (perturbed) {
         for (int w = 0; w < W; ++w) sp[w] = s1[w] ^ gam[w];
       } else {
-        uint8_t gv[PBN_MAX_GATES];
-        eval_gates(d, s1, gv);
-        for (int i = 0; i < N; ++i) {
-          int f0 = d->node_func_start[i], nf = d->node_func_start[i + 1] - f0, x;
-          if (nf == 1) {
-            x = eval_func(d, f0, s1, gv);
-          } else {
-            uint32_t u = 0;
-            for (int dd = 0; dd < B; ++dd) u |= ((D[i][dd] >> b) & 1u) << (B - 1 - dd);
-            int j = 0;
-            while (j < nf - 1 && !(u < d->func_threshold[f0 + j])) ++j;
-            x = eval_func(d, f0 + j, s1, gv);
-          }
-          if (x) sp[i >> 5] |= 1u << (i & 31);
-        }
+        rule_update(d, s1, D, b, sp);
       }
+      int unsettled = n_sub ? settle(d, seed, G, e, step, b, Dk, have, sp, &perturbed) : 0;
       /* 5. reward / termination */
       int a = attractor_of(d, sp, W);
       int in_attr = a >= 0;
@@ -292,7 +352,7 @@ int oracle_step(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t en
       int pc = 0;
       for (int w = 0; w < W; ++w) pc += __builtin_popcount(m[w]);
       reward[li] = d->reward_table[(2 * term + wrong) * (N + 1) + pc];
-      uint8_t fl = (uint8_t)(term | (trunc << 1) | (in_attr << 2) | (perturbed << 3));
+      uint8_t fl = (uint8_t)(term | (trunc << 1) | (in_attr << 2) | (perturbed << 3) | (unsettled << 5));
       if (final_state)
         for (int w = 0; w < W; ++w) final_state[(size_t)w * n + li] = sp[w];
       if ((mode & PBN_MODE_AUTORESET) && (term || trunc)) {
@@ -313,6 +373,8 @@ int oracle_step(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t en
       }
       flags[li] = fl;
     }
+    free(Dk);
+    free(have);
   }
   return 0;
 }

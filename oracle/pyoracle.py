@@ -15,7 +15,7 @@ from typing import Dict, List, Sequence, Tuple
 M0, M1 = 0xD2511F53, 0xCD9E8D57
 W0, W1 = 0x9E3779B9, 0xBB67AE85
 MASK32 = 0xFFFFFFFF
-SEL, ENV, PERT, RESET = 0, 1, 2, 3
+SEL, ENV, PERT, RESET, SETTLE_SEL, SETTLE_ENV = 0, 1, 2, 3, 5, 6
 MODE_AUTORESET, MODE_RANDOM_ACTIONS = 1, 2
 
 
@@ -102,6 +102,23 @@ class PyPBN:
         state, tgt = self.reset_from_words(seed, e, step, R[1], R[0])
         return state, tgt, 0
 
+    def rule_update(self, seed: int, G: int, b: int, step: int, s1: List[int], ctr) -> List[int]:
+        """Every node's rule update of env bit b of group G from s1; ctr(i, c) = (stream, idx) of
+        node i's selection call c."""
+        B = self.spec.prob_bits
+        sp = []
+        for i, fl in enumerate(self.net.nodes):
+            j = 0
+            if len(fl) > 1:
+                u = 0
+                for d in range(B):
+                    word = draw(seed, G, step, *ctr(i, d >> 2))[d & 3]
+                    u |= ((word >> b) & 1) << (B - 1 - d)
+                while j < len(fl) - 1 and not (u < self.thr[i][j]):
+                    j += 1
+            sp.append(fl[j](s1))
+        return sp
+
     def step(self, seed: int, step: int, e: int, state: List[int], flip: List[int], target: int, t: int,
              mode: int):
         n, B = self.n, self.spec.prob_bits
@@ -142,19 +159,29 @@ class PyPBN:
         if perturbed:
             sp = [s1[i] ^ gamma[i] for i in range(n)]
         else:
-            sp = []
-            for i, fl in enumerate(self.net.nodes):
-                if len(fl) == 1:
-                    j = 0
-                else:
-                    u = 0
-                    for d in range(B):
-                        word = draw(seed, G, step, SEL, 4 * i + (d >> 2))[d & 3]
-                        u |= ((word >> b) & 1) << (B - 1 - d)
-                    j = 0
-                    while j < len(fl) - 1 and not (u < self.thr[i][j]):
-                        j += 1
-                sp.append(fl[j](s1))
+            sp = self.rule_update(seed, G, b, step, s1, lambda i, c: (SEL, 4 * i + c))
+        # settle law (spec.settle >= 2): update k = 1.. from SETTLE_ENV gaps and SETTLE_SEL
+        # digits until sp is an attractor state, at most spec.settle updates in all
+        unsettled = False
+        for k in range(1, self.spec.settle):
+            if tuple(sp) in self.att_of:
+                break
+            gk, pos, j = [0] * n, -1, 0
+            while pos < n - 1:
+                if j % 4 == 0:
+                    P = draw(seed, e, step, SETTLE_ENV, ((k - 1) << 8) | (j // 4))
+                pos += self.gap(P[j % 4])
+                j += 1
+                if pos >= n:
+                    break
+                gk[pos] = 1
+            if any(gk):
+                sp = [sp[i] ^ gk[i] for i in range(n)]
+                perturbed = True
+            else:
+                sp = self.rule_update(seed, G, b, step, sp, lambda i, c, k=k: (SETTLE_SEL, ((k - 1) << 9) | (4 * i + c)))
+        else:
+            unsettled = self.spec.settle >= 2 and tuple(sp) not in self.att_of
         a = self.att_of.get(tuple(sp), -1)
         in_attr = a >= 0
         term = in_attr and a == target
@@ -162,7 +189,7 @@ class PyPBN:
         trunc = self.spec.horizon > 0 and tt >= self.spec.horizon
         wrong = in_attr and not term
         reward = self.spec.reward_value(term, wrong, sum(flip))
-        flags = int(term) | (int(trunc) << 1) | (int(in_attr) << 2) | (int(perturbed) << 3)
+        flags = int(term) | (int(trunc) << 1) | (int(in_attr) << 2) | (int(perturbed) << 3) | (int(unsettled) << 5)
         out = {"final_state": sp, "reward": reward, "flipmask": flip, "target": target}
         if (mode & MODE_AUTORESET) and (term or trunc):
             ns, tg = reset_to if reset_to is not None else self.random_state(seed, e, step)

@@ -22,6 +22,7 @@ FLAG_TRUNCATED = 2
 FLAG_IN_ATTRACTOR = 4
 FLAG_PERTURBED = 8
 FLAG_RESET = 16
+FLAG_UNSETTLED = 32
 
 EXPORTS = ["pbn_net_create", "pbn_net_destroy", "pbn_net_words", "pbn_reset", "pbn_step", "pbn_step_dev",
            "pbn_rollout", "pbn_state_histogram", "pbn_obs_unpack", "pbn_bilinear_targets", "pbn_q_to_flipmask",

@@ -114,6 +114,7 @@ struct StepArgs {
                        // of X is X * x_mult (times the start attractor's size, multi-state nets)
   int sel_prio;        // pipelined rollout: raise the selection wave's priority (grids of at most
                        // four blocks per CU)
+  int settle_max;      // step law: >= 2 = the settle law (wave kernel variants 3, 4)
 };
 
 // In-kernel phase clocks (cdna_hip_programming.md section 7, "In-kernel stamps"):
@@ -544,12 +545,182 @@ __device__ __forceinline__ void set_bit(uint32_t (&g)[W], int pos, int N) {
     if ((unsigned)pos < (unsigned)N && (pos >> 5) == w) g[w] |= 1u << (pos & 31);
 }
 
+// attractor id of the per-env state sp (open-addressing LDS hash; keys are unique, so the probe
+// order does not matter: the first four probes are read side by side), or -1
+template <int W>
+__device__ __forceinline__ int attractor_lookup(const StepArgs& a, const uint32_t* __restrict__ htab,
+                                                const uint32_t (&sp)[W]) {
+  int att = -1;
+  if (a.hash_bits > 0) {
+    const uint32_t hmask = (1u << a.hash_bits) - 1u;
+    uint32_t h = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) h += sp[w] * a.hash_mult[w];
+    h >>= (32 - a.hash_bits);
+#pragma unroll
+    for (int pr = 0; pr < 4; ++pr) {
+      const int id = hash_probe<W>(htab, (h + pr) & hmask, sp);
+      if (pr < a.hash_probes && id >= 0) att = id;
+    }
+    for (int pr = 4; pr < a.hash_probes; ++pr) {
+      const int id = hash_probe<W>(htab, (h + pr) & hmask, sp);
+      if (id >= 0) att = id;
+    }
+  }
+  return att;
+}
+
+// combinational gates of the lowered wide functions (lowering.py), level by level, all 64 lanes:
+// gate record {input S indices, 16-bit table, output S index}; one wave's LDS operations execute
+// in order, so level l + 1 reads what level l wrote
+__device__ __forceinline__ void eval_gate_levels(const StepArgs& a, const uint32_t* __restrict__ L, uint32_t* S,
+                                                 int lane) {
+  const uint4* grec = reinterpret_cast<const uint4*>(L + a.gate_off);
+  const int32_t* glev = reinterpret_cast<const int32_t*>(L + a.glayer_off);
+  for (int lv = 0; lv < a.n_glayers; ++lv) {
+    const int end = glev[lv + 1];
+    for (int gi = glev[lv] + lane; gi < end; gi += 64) {
+      const uint4 r = grec[gi];
+      S[r.z] = eval_compact(r.x, r.y, S);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// node l32 + 32r on lane l32: the rule update of every env of the group from the bit-sliced
+// planes S, the selection digit planes dig (perturbed envs are replaced by the caller)
+template <int W, int B>
+__device__ __forceinline__ void node_update(const StepArgs& a, const uint4 (&rec_)[W][kNodeRecs],
+                                            const uint4* __restrict__ selq, const uint32_t* __restrict__ S,
+                                            const uint32_t (&dig)[W][16], bool lo, int l32, uint32_t (&X)[W]) {
+  const int N = a.n_nodes;
+#pragma unroll
+  for (int r = 0; r < W; ++r) {
+    X[r] = 0;
+    const int i = l32 + 32 * r;
+    const int ii = lo && i < N ? i : 0;   // other lanes evaluate node 0 and discard it
+    uint32_t x = 0;
+    if (a.n_cls > 0 && a.max_nf <= kNodeRecs) {
+      // thresholds from a few wave-uniform classes (all kaban networks: 1/3, 2/3)
+      const int nf = (int)rec_[r][0].w;
+      uint32_t ltc[kNodeRecs];
+      class_masks<B>(dig[r], a.uthr, a.n_cls, ltc);
+#pragma unroll
+      for (int q = kNodeRecs - 1; q >= 0; --q) {
+        if (q < a.max_nf) {
+          const uint4 rc = rec_[r][q];
+          const uint32_t fj = eval_sel(rc.x, selq[(2 * q) * 32 * W + ii], selq[(2 * q + 1) * 32 * W + ii], S);
+          const uint32_t y = (q == nf - 1) ? fj : bfi(pick_class(ltc, rc.y), fj, x);
+          x = (q < nf) ? y : x;
+        }
+      }
+    } else {
+      const int nf = (int)rec_[r][0].w;
+      const int f0 = (int)rec_[r][1].w;
+      // selection chain from the last function down: x = F_{nf-1}; x = lt_j ? F_j : x
+      for (int j = nf - 1; j >= kNodeRecs; --j) {   // nodes with more than kNodeRecs functions (slow path)
+        const uint4 rc = a.fcompact[CK(f0 + j, a.n_funcs, 9)];
+        const uint32_t fj = eval_compact(rc.x, rc.y, S);
+        x = (j == nf - 1) ? fj : bfi(less_than(dig[r], rc.z, B), fj, x);
+      }
+#pragma unroll
+      for (int q = kNodeRecs - 1; q >= 0; --q) {
+        if (q < nf) {
+          const uint4 rc = rec_[r][q];
+          const uint32_t fj = eval_sel(rc.x, selq[(2 * q) * 32 * W + ii], selq[(2 * q + 1) * 32 * W + ii], S);
+          x = (q == nf - 1) ? fj : bfi(less_than(dig[r], rc.z, B), fj, x);
+        }
+      }
+    }
+    if (lo && i < N) X[r] = x;
+  }
+}
+
+// The settle law (settle_max >= 2, include/pbn_env.h "Step law"): updates k = 1 ..
+// settle_max - 1 of the envs (lower lanes) whose state sp is outside every attractor, until all
+// of the wave's envs are in one.  Update k: perturbation gaps j = 0, 1, ... from SETTLE_ENV call
+// ((k-1) << 8 | j >> 2), word j & 3 (per env); unperturbed envs take the rule update with the
+// group's SETTLE_SEL digit planes of update k (call idx (k-1) << 9 | 4i + c).  Every lane
+// computes the digit calls of its node (the upper half repeats the lower's: settle updates are
+// off the one-update hot path).  Returns true on lanes whose env is still outside after the
+// last update (PBN_FLAG_UNSETTLED).
+template <int W, int B>
+__device__ __forceinline__ bool settle_updates(const StepArgs& a, const uint32_t* __restrict__ L, uint32_t* S,
+                                            const uint4 (&rec_)[W][kNodeRecs], int lane, uint32_t ge_lo,
+                                            uint32_t ge_hi, uint32_t G_lo, uint32_t G_hi, uint32_t st_lo,
+                                            uint32_t (&sp)[W], int& att, bool& pert) {
+  constexpr int CPN = B / 4;
+  const bool lo = lane < 32;
+  const int l32 = lane & 31;
+  const int N = a.n_nodes;
+  const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+  const uint4* selq = reinterpret_cast<const uint4*>(L + a.sel_off);
+  const uint32_t* htab = L + a.cdf_len + 4 * (N + 1);
+  bool open = lo && att < 0;
+  for (int k = 1; k < a.settle_max; ++k) {
+    if (__ballot(open) == 0) return false;
+    const uint32_t sub = (uint32_t)(k - 1);
+    uint32_t dig[W][16];
+#pragma unroll
+    for (int r = 0; r < W; ++r) {
+#pragma unroll
+      for (int c = 0; c < CPN; ++c) {
+        const Word4 d = pbn::philox(G_lo, st_lo, (pbn::kStreamSettleSel << 28) | (sub << 9) |
+                                                     (uint32_t)(4 * (l32 + 32 * r) + c), G_hi, k0, k1);
+        dig[r][4 * c + 0] = d.x; dig[r][4 * c + 1] = d.y; dig[r][4 * c + 2] = d.z; dig[r][4 * c + 3] = d.w;
+      }
+    }
+    uint32_t gam[W];
+    bool pk = false;
+#pragma unroll
+    for (int w = 0; w < W; ++w) gam[w] = 0;
+    if (open) {
+      Word4 P = {0, 0, 0, 0};
+      int pos = -1;
+      for (int j = 0; pos < N - 1; ++j) {
+        if ((j & 3) == 0)
+          P = pbn::philox(ge_lo, st_lo, (pbn::kStreamSettleEnv << 28) | (sub << 8) | (uint32_t)(j >> 2), ge_hi, k0, k1);
+        const int j4 = j & 3;
+        const uint32_t u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
+        pos += gap_any(a.gap_exact, L, a, u);
+        set_bit<W>(gam, pos, N);
+      }
+#pragma unroll
+      for (int w = 0; w < W; ++w) pk = pk || gam[w] != 0;
+    }
+    // bit-slice sp (every lane takes part in the cross-lane transposes)
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      const uint32_t pl = lane_transpose32(sp[w], lane);
+      if (lo) S[32 * w + l32] = pl;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (a.n_glayers > 0) eval_gate_levels(a, L, S, lane);
+    uint32_t X[W], x[W];
+    node_update<W, B>(a, rec_, selq, S, dig, lo, l32, X);
+#pragma unroll
+    for (int w = 0; w < W; ++w) x[w] = lane_transpose32(X[w], lane);
+    if (open) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) sp[w] = pk ? sp[w] ^ gam[w] : x[w];
+      pert = pert || pk;
+      att = attractor_lookup<W>(a, htab, sp);
+      open = att < 0;
+    }
+  }
+  return open;
+}
+
 // VARIANT 1: exactly one step (pbn_step; no loop, lowest VGPR count);
 // 2: rollout with invariants recomputed per step (occupancy first; the rollout of networks
-//    with gates, which the pipelined kernel does not run).
+//    with gates, which the pipelined kernel does not run);
+// 3, 4: 1 and 2 under the settle law (settle_max >= 2: settle_updates after the first update).
 template <int W, int B, int VARIANT>
 __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a) {
-  constexpr bool LEAN = VARIANT == 2;
+  constexpr bool LEAN = VARIANT == 2 || VARIANT == 4;
+  constexpr bool SINGLE = VARIANT == 1 || VARIANT == 3;
+  constexpr bool SETTLE = VARIANT >= 3;
   constexpr int CPN = B / 4;               // selection calls per node
   constexpr int H = (CPN + 1) / 2;         // of which the lower half computes H
   constexpr int NLO = 1 + W * H;           // lower list: ENV, SEL(c < H)
@@ -605,7 +776,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   if (g >= a.n_groups) return;  // whole wave
   const uint4* selq = reinterpret_cast<const uint4*>(L + a.sel_off);
 
-  const int n_steps = VARIANT == 1 ? 1 : a.n_steps;
+  const int n_steps = SINGLE ? 1 : a.n_steps;
   // Random-action mode issues no global load inside the step loop (attractor tables live in
   // LDS), so stores never have to drain (vmcnt retires in issue order).  A given flip mask
   // is loaded and consumed inside its own branch, so the wait for it stays on that path.
@@ -623,7 +794,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   }
   const uint32_t kk0 = k0, kk1 = k1, ge_lo = (uint32_t)ge, G_lo = (uint32_t)G;
   uint64_t step = a.step + (uint64_t)ks;
-  if constexpr (VARIANT == 1) {
+  if constexpr (SINGLE) {
     if (a.step_ptr) step = *a.step_ptr;   // graph-replayable single step (pbn_step_dev)
   }
   const uint32_t st_lo = (uint32_t)step;
@@ -757,66 +928,13 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
     if (lo) S[32 * w + l32] = sp;
   }
   __builtin_amdgcn_wave_barrier();
-  if (a.n_glayers > 0) {
-    // combinational gates of the lowered wide functions (lowering.py), level by level, all
-    // 64 lanes: gate record {input S indices, 16-bit table, output S index}; one wave's LDS
-    // operations execute in order, so level l + 1 reads what level l wrote
-    const uint4* grec = reinterpret_cast<const uint4*>(L + a.gate_off);
-    const int32_t* glev = reinterpret_cast<const int32_t*>(L + a.glayer_off);
-    for (int lv = 0; lv < a.n_glayers; ++lv) {
-      const int end = glev[lv + 1];
-      for (int gi = glev[lv] + lane; gi < end; gi += 64) {
-        const uint4 r = grec[gi];
-        S[r.z] = eval_compact(r.x, r.y, S);
-      }
-      __builtin_amdgcn_wave_barrier();
-    }
-  }
+  if (a.n_glayers > 0) eval_gate_levels(a, L, S, lane);
 
   // ---- 4. node l32 + 32r on lane l32: X = rule update of every env (perturbed envs are
   // replaced after the back-transpose)
   PBN_STAMP(4);
   uint32_t X[W];
-#pragma unroll
-  for (int r = 0; r < W; ++r) {
-    X[r] = 0;
-    const int i = l32 + 32 * r;
-    const int ii = lo && i < N ? i : 0;   // other lanes evaluate node 0 and discard it
-    uint32_t x = 0;
-    if (a.n_cls > 0 && a.max_nf <= kNodeRecs) {
-      // thresholds from a few wave-uniform classes (all kaban networks: 1/3, 2/3)
-      const int nf = (int)rec_[r][0].w;
-      uint32_t ltc[kNodeRecs];
-      class_masks<B>(dig[r], a.uthr, a.n_cls, ltc);
-#pragma unroll
-      for (int q = kNodeRecs - 1; q >= 0; --q) {
-        if (q < a.max_nf) {
-          const uint4 rc = rec_[r][q];
-          const uint32_t fj = eval_sel(rc.x, selq[(2 * q) * 32 * W + ii], selq[(2 * q + 1) * 32 * W + ii], S);
-          const uint32_t y = (q == nf - 1) ? fj : bfi(pick_class(ltc, rc.y), fj, x);
-          x = (q < nf) ? y : x;
-        }
-      }
-    } else {
-      const int nf = (int)rec_[r][0].w;
-      const int f0 = (int)rec_[r][1].w;
-      // selection chain from the last function down: x = F_{nf-1}; x = lt_j ? F_j : x
-      for (int j = nf - 1; j >= kNodeRecs; --j) {   // nodes with more than kNodeRecs functions (slow path)
-        const uint4 rc = a.fcompact[CK(f0 + j, a.n_funcs, 9)];
-        const uint32_t fj = eval_compact(rc.x, rc.y, S);
-        x = (j == nf - 1) ? fj : bfi(less_than(dig[r], rc.z, B), fj, x);
-      }
-#pragma unroll
-      for (int q = kNodeRecs - 1; q >= 0; --q) {
-        if (q < nf) {
-          const uint4 rc = rec_[r][q];
-          const uint32_t fj = eval_sel(rc.x, selq[(2 * q) * 32 * W + ii], selq[(2 * q + 1) * 32 * W + ii], S);
-          x = (q == nf - 1) ? fj : bfi(less_than(dig[r], rc.z, B), fj, x);
-        }
-      }
-    }
-    if (lo && i < N) X[r] = x;
-  }
+  node_update<W, B>(a, rec_, selq, S, dig, lo, l32, X);
 
   // ---- 5. back to per-env words, reward, termination, autoreset, stores
   PBN_STAMP(5);
@@ -824,32 +942,19 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
 #pragma unroll
   for (int w = 0; w < W; ++w) sp[w] = lane_transpose32(X[w], lane);
   PBN_STAMP(6);
-  if (lo) {
-  if (pert) {
+  if (lo && pert) {
 #pragma unroll
     for (int w = 0; w < W; ++w) sp[w] = s1[w] ^ gam[w];
   }
+  int att = lo ? attractor_lookup<W>(a, htab, sp) : 0;
+  bool unsettled = false;
+  if constexpr (SETTLE) {   // the whole wave (cross-lane transposes)
+    unsettled = settle_updates<W, B>(a, L, S, rec_, lane, ge_lo, ge_hi, G_lo, G_hi, st_lo, sp, att, pert);
+  }
+  if (lo) {
   if (a.final_state) {
 #pragma unroll
     for (int w = 0; w < W; ++w) a.final_state[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 10)] = sp[w];
-  }
-  int att = -1;
-  if (a.hash_bits > 0) {
-    const uint32_t hmask = (1u << a.hash_bits) - 1u;
-    uint32_t h = 0;
-#pragma unroll
-    for (int w = 0; w < W; ++w) h += sp[w] * a.hash_mult[w];
-    h >>= (32 - a.hash_bits);
-    // keys are unique: probe order does not matter; the first four probes are read side by side
-#pragma unroll
-    for (int pr = 0; pr < 4; ++pr) {
-      const int id = hash_probe<W>(htab, (h + pr) & hmask, sp);
-      if (pr < a.hash_probes && id >= 0) att = id;
-    }
-    for (int pr = 4; pr < a.hash_probes; ++pr) {
-      const int id = hash_probe<W>(htab, (h + pr) & hmask, sp);
-      if (id >= 0) att = id;
-    }
   }
   const bool in_attr = att >= 0;
   const bool term = in_attr && (uint32_t)att == tg0;
@@ -858,7 +963,8 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   tt = tt > 255 ? 255 : tt;
   const bool trunc = a.horizon > 0 && tt >= a.horizon;
   a.reward[CK(ks * n + le, n_steps * n, 11)] = rtab[(int)pc * 4 + 2 * (int)term + (int)wrong];
-  uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) | ((uint32_t)pert << 3);
+  uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) | ((uint32_t)pert << 3) |
+                ((uint32_t)unsettled << 5);
   if ((a.mode & PBN_MODE_AUTORESET) && (term || trunc)) {
     uint32_t nt;
     if (a.n_attr >= 1) {   // the attractor draws of step 2 (attractor states from the LDS image)
@@ -1805,6 +1911,9 @@ struct pbn_net {
   size_t lds_wave = 0;
   StepFn wave1 = nullptr;       // single step (pbn_step)
   StepFn wave_lean = nullptr;   // rollout, one wave per group (networks with gates)
+  StepFn wave_settle = nullptr;       // pbn_step under the settle law (settle_max >= 2)
+  StepFn wave_settle_lean = nullptr;  // pbn_rollout under the settle law
+  int settle_max = 0;
   StepFn pipe = nullptr;        // rollout, three waves per group pair (every other network)
   size_t lds_pipe = 0;
   int n_gates = 0, n_glayers = 0, gate_off = 0, glayer_off = 0;   // lowered wide functions
@@ -1960,6 +2069,7 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   if (!(d->prob_bits == 4 || d->prob_bits == 8 || d->prob_bits == 12 || d->prob_bits == 16))
     return fail(PBN_EINVAL, "prob_bits must be 4, 8, 12 or 16");
   if (d->horizon < 0 || d->horizon > 255) return fail(PBN_EINVAL, "horizon out of range 0..255");
+  if (d->settle_max < 0 || d->settle_max > PBN_MAX_SETTLE) return fail(PBN_EINVAL, "settle_max out of range 0..4096");
   if (d->n_attractors < 0 || d->n_attractors > PBN_MAX_ATTRACTORS)
     return fail(PBN_EINVAL, "n_attractors out of range 0..254");
   if (!d->node_func_start || !d->func_arity || !d->func_inputs || !d->func_table || !d->func_threshold ||
@@ -2250,6 +2360,9 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   // compact records for the wave kernel: {inputs as bytes, 4-input truth table, threshold, 0}
   net->wave1 = pick_wave<1>(W, d->prob_bits);
   net->wave_lean = pick_wave<2>(W, d->prob_bits);
+  net->wave_settle = pick_wave<3>(W, d->prob_bits);
+  net->wave_settle_lean = pick_wave<4>(W, d->prob_bits);
+  net->settle_max = d->settle_max;
   net->pipe = pick_pipe(W, d->prob_bits);
   net->reset = pick_reset(W);
   // multiply-high divisors (exact for the operand ranges used: see actions_from_draw, autoreset)
@@ -2277,8 +2390,9 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     free_net(net);
     return rc;
   }
-  for (int ti = 2; ti < 5; ++ti) {
-    const StepFn fn = ti == 2 ? net->wave_lean : (ti == 3 ? net->wave1 : net->pipe);
+  for (int ti = 0; ti < 5; ++ti) {
+    const StepFn fns[5] = {net->wave_settle, net->wave_settle_lean, net->wave_lean, net->wave1, net->pipe};
+    const StepFn fn = fns[ti];
     const size_t bytes = ti == 4 ? net->lds_pipe : net->lds_wave;
     if (!fn || bytes > 160 * 1024) continue;  // variant unusable for this net; never picked
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2322,6 +2436,61 @@ static int check_common(pbn_net* net, uint64_t env_offset, int64_t n_envs) {
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
+// The launch arguments every step kernel shares: the net's tables and encodings, the key and
+// the env range (the caller adds its buffers, mode and step count)
+static void fill_args(const pbn_net* net, StepArgs* p, uint64_t seed, uint64_t step, uint64_t env_offset,
+                      int64_t n_envs) {
+  StepArgs& a = *p;
+  memset(&a, 0, sizeof a);
+  a.tab = net->d_tab;
+  a.att_start = net->d_att_start;
+  a.att_states = net->d_att_states;
+  a.seed = seed;
+  a.step = step;
+  a.env_offset = env_offset;
+  a.n_envs = n_envs;
+  a.n_groups = n_envs / 32;
+  a.n_steps = 1;
+  a.n_nodes = net->n_nodes;
+  a.n_attr = net->n_attr;
+  a.horizon = net->horizon;
+  a.cdf_len = net->cdf_len;
+  a.hash_bits = net->n_attr ? net->hash_bits : 0;
+  a.hash_probes = net->hash_probes;
+  a.tab_words = net->tab_words;
+  a.n_states = net->n_states;
+  a.att_off = net->att_off;
+  a.sel_off = net->sel_off;
+  a.nrec_off = net->nrec_off;
+  a.n_cls = net->n_cls;
+  a.max_nf = net->max_nf;
+  a.lq = net->lq;
+  a.slot_words = net->slot_words;
+  a.gate_off = net->gate_off;
+  a.glayer_off = net->glayer_off;
+  a.n_glayers = net->n_glayers;
+  memcpy(a.uthr, net->uthr, sizeof a.uthr);
+  memcpy(a.hash_mult, net->hash_mult, sizeof a.hash_mult);
+  a.prob_bits = net->B;
+  a.n_funcs = net->n_funcs;
+  a.wave_words = net->wave_words;
+  a.gap_exact = net->gap_exact;
+  a.gap_lut_off = net->gap_lut_off;
+  a.gap_shift = net->gap_shift;
+  a.gap_nb = net->gap_nb;
+  a.inv_log2q = net->inv_log2q;
+  a.fcompact = net->d_fcompact;
+  a.nrec = net->d_nrec;
+  a.n1_magic = net->n1_magic;
+  a.att_single = net->att_single;
+  a.am1_magic = net->am1_magic;
+  a.x_mult = net->x_mult;
+  a.settle_max = net->settle_max;
+#ifdef PBN_STAMPS
+  a.stamps = g_stamps;
+#endif
+}
+
 int pbn_reset(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs,
               uint32_t* d_state, uint8_t* d_target, uint8_t* d_t, void* stream) {
   int rc = check_common(net, env_offset, n_envs);
@@ -2353,69 +2522,21 @@ static int step_impl(pbn_net* net, uint64_t seed, uint64_t step, const uint64_t*
       (d_final_state && !aligned16(d_final_state)))
     return fail(PBN_EINVAL, "device buffers must be 16-byte aligned");
   StepArgs a;
-  memset(&a, 0, sizeof a);
-  a.tab = net->d_tab;
-  a.att_start = net->d_att_start;
-  a.att_states = net->d_att_states;
+  fill_args(net, &a, seed, step, env_offset, n_envs);
+  a.step_ptr = d_step;
   a.state = d_state;
+  a.state_out = d_state_out;
   a.flipmask = d_flipmask;
   a.target = d_target;
   a.t = d_t;
-  a.state_out = d_state_out;
   a.final_state = d_final_state;
   a.reward = d_reward;
   a.flags = d_flags;
-  a.seed = seed;
-  a.step = step;
-  a.step_ptr = d_step;
-  a.env_offset = env_offset;
-  a.n_envs = n_envs;
-  a.n_groups = n_envs / 32;
-  a.n_nodes = net->n_nodes;
-  a.n_attr = net->n_attr;
-  a.horizon = net->horizon;
   a.mode = (int)mode;
-  a.cdf_len = net->cdf_len;
-  a.hash_bits = net->n_attr ? net->hash_bits : 0;
-  a.hash_probes = net->hash_probes;
-  a.tab_words = net->tab_words;
-  a.n_states = net->n_states;
-  a.att_off = net->att_off;
-  a.sel_off = net->sel_off;
-  a.nrec_off = net->nrec_off;
-  a.n_cls = net->n_cls;
-  a.max_nf = net->max_nf;
-  a.lq = net->lq;
-  a.slot_words = net->slot_words;
-  a.gate_off = net->gate_off;
-  a.glayer_off = net->glayer_off;
-  a.n_glayers = net->n_glayers;
-  memcpy(a.uthr, net->uthr, sizeof a.uthr);
-  memcpy(a.hash_mult, net->hash_mult, sizeof a.hash_mult);
-#ifdef PBN_STAMPS
-  a.stamps = g_stamps;
-#endif
-  a.prob_bits = net->B;
-  a.n_funcs = net->n_funcs;
-  a.wave_words = net->wave_words;
-  a.gap_exact = net->gap_exact;
-  a.gap_lut_off = net->gap_lut_off;
-  a.gap_shift = net->gap_shift;
-  a.gap_nb = net->gap_nb;
-  a.inv_log2q = net->inv_log2q;
-  a.fcompact = net->d_fcompact;
-  a.nrec = net->d_nrec;
-  a.n1_magic = net->n1_magic;
-  a.att_single = net->att_single;
-  a.am1_magic = net->am1_magic;
-  a.x_mult = net->x_mult;
-  // launch shape: one thread per 32-env group once that fills the chip
-  // (>= 4 waves per SIMD), else one wave per group (node loop across lanes)
-  a.n_steps = 1;
-  a.obs = nullptr;
   if (net->lds_wave > 160 * 1024) return fail(PBN_EINVAL, "network too large for the step kernel's LDS");
   const unsigned blocks = (unsigned)((a.n_groups + kWavesPerBlock - 1) / kWavesPerBlock);  // one wave per group
-  hipLaunchKernelGGL(net->wave1, dim3(blocks), dim3(64 * kWavesPerBlock), net->lds_wave, (hipStream_t)stream, a);
+  const StepFn fn = net->settle_max >= 2 ? net->wave_settle : net->wave1;
+  hipLaunchKernelGGL(fn, dim3(blocks), dim3(64 * kWavesPerBlock), net->lds_wave, (hipStream_t)stream, a);
   HIP_OK(hipGetLastError());
   return PBN_OK;
 }
@@ -2450,10 +2571,7 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
   if (!d_state || !d_flipmask || !d_target || !d_t || !d_reward || !d_flags) return fail(PBN_EINVAL, "null buffer");
   if (net->lds_wave > 160 * 1024) return fail(PBN_EINVAL, "network too large for the rollout kernel's LDS");
   StepArgs a;
-  memset(&a, 0, sizeof a);
-  a.tab = net->d_tab;
-  a.att_start = net->d_att_start;
-  a.att_states = net->d_att_states;
+  fill_args(net, &a, seed, step, env_offset, n_envs);
   a.state = d_state;
   a.state_out = d_state;   // in place: every env is read and written by one lane only
   a.flipmask = d_flipmask;
@@ -2463,55 +2581,14 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
   a.obs = d_obs;
   a.reward = d_reward;
   a.flags = d_flags;
-  a.seed = seed;
-  a.step = step;
-  a.env_offset = env_offset;
-  a.n_envs = n_envs;
-  a.n_groups = n_envs / 32;
   a.n_steps = n_steps;
-  a.n_nodes = net->n_nodes;
-  a.n_attr = net->n_attr;
-  a.horizon = net->horizon;
   a.mode = (int)mode;
-  a.cdf_len = net->cdf_len;
-  a.hash_bits = net->n_attr ? net->hash_bits : 0;
-  a.hash_probes = net->hash_probes;
-  a.tab_words = net->tab_words;
-  a.n_states = net->n_states;
-  a.att_off = net->att_off;
-  a.sel_off = net->sel_off;
-  a.nrec_off = net->nrec_off;
-  a.n_cls = net->n_cls;
-  a.max_nf = net->max_nf;
-  a.lq = net->lq;
-  a.slot_words = net->slot_words;
-  a.gate_off = net->gate_off;
-  a.glayer_off = net->glayer_off;
-  a.n_glayers = net->n_glayers;
-  memcpy(a.uthr, net->uthr, sizeof a.uthr);
-  memcpy(a.hash_mult, net->hash_mult, sizeof a.hash_mult);
-  a.prob_bits = net->B;
-  a.n_funcs = net->n_funcs;
-  a.wave_words = net->wave_words;
-  a.gap_exact = net->gap_exact;
-  a.gap_lut_off = net->gap_lut_off;
-  a.gap_shift = net->gap_shift;
-  a.gap_nb = net->gap_nb;
-  a.inv_log2q = net->inv_log2q;
-  a.fcompact = net->d_fcompact;
-  a.nrec = net->d_nrec;
-  a.n1_magic = net->n1_magic;
-  a.att_single = net->att_single;
-  a.am1_magic = net->am1_magic;
-  a.x_mult = net->x_mult;
-#ifdef PBN_STAMPS
-  a.stamps = g_stamps;
-#endif
   // the pipelined kernel for every network it supports (it beats the one-wave-per-group
   // rollout at every measured size: profiles/r01_sweep_pbn28_variants_v4.jsonl); networks
   // with gates (lowered wide functions) run the wave kernel.  PBN_ROLL=lean|pipe forces one.
-  bool pipe = net->lds_pipe <= 64 * 1024 && !net->n_gates;
-  if (net->force_roll) pipe = net->force_roll == 3 && !net->n_gates;
+  // The settle law runs the wave kernel (variant 4).
+  bool pipe = net->lds_pipe <= 64 * 1024 && !net->n_gates && net->settle_max < 2;
+  if (net->force_roll) pipe = net->force_roll == 3 && !net->n_gates && net->settle_max < 2;
   if (pipe) {   // one block of three waves per pair of groups
     const int64_t pblocks = (a.n_groups + 1) / 2;
     a.sel_prio = pblocks <= 4 * (int64_t)net->n_cus ? 1 : 0;
@@ -2524,8 +2601,8 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
     return PBN_OK;
   }
   const unsigned blocks = (unsigned)((a.n_groups + kWavesPerBlock - 1) / kWavesPerBlock);  // one wave per group
-  hipLaunchKernelGGL(net->wave_lean, dim3(blocks), dim3(64 * kWavesPerBlock), net->lds_wave,
-                     (hipStream_t)stream, a);
+  hipLaunchKernelGGL(net->settle_max >= 2 ? net->wave_settle_lean : net->wave_lean, dim3(blocks),
+                     dim3(64 * kWavesPerBlock), net->lds_wave, (hipStream_t)stream, a);
   HIP_OK(hipGetLastError());
   return PBN_OK;
 }

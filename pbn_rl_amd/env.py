@@ -11,6 +11,9 @@ Drop-in for the env the reference builds with
   step(actions) -> (obs, reward, term, trunc, info)  bdq_model/__init__.py:177
       actions: list of ints / 0-d (CUDA) tensors, a tensor, an int, or []
       (0 = no-op, a > 0 flips node a-1, duplicates count once: bdq_model/__init__.py:76-84,176)
+      settle=K >= 2 selects the settle law (intervene, then update until an attractor state,
+      at most K updates; include/pbn_env.h "Step law"), the law data/results/pbn_33_3.pkl pins
+      (tests/test_bn_pin.py); the default 0 is one synchronous update per step
   observation_space.shape[0]                      train_BDQ.py:82
   attracting_states, all_attractors, real_attractors      bdq_model/__init__.py:60,182
   state_attractor_id, target_attractor_id         bdq_model/__init__.py:180
@@ -121,7 +124,7 @@ class PBNEnv:
                  prob_bits: int = 16, seed: Optional[int] = None, device=None, render_mode=None,
                  success_reward: float = 5.0, wrong_attractor_cost: float = 2.0, action_cost: float = 1.0,
                  step_cost: float = 0.0, name: Optional[str] = None, grow_attractors: bool = True,
-                 discovery: Optional[dict] = None):
+                 discovery: Optional[dict] = None, settle: int = 0):
         if isinstance(network, str):
             if attractors is None:
                 attractors = load_attractors(network)
@@ -148,7 +151,7 @@ class PBNEnv:
             warnings.warn(f"network has {len(attractors)} attractors < min_attractors={min_attractors}")
         self._spec_kwargs = dict(perturbation=perturbation, prob_bits=prob_bits, horizon=horizon,
                                  success_reward=success_reward, wrong_attractor_cost=wrong_attractor_cost,
-                                 action_cost=action_cost, step_cost=step_cost)
+                                 action_cost=action_cost, step_cost=step_cost, settle=settle)
         self.spec = EnvSpec(network, attractors, **self._spec_kwargs)
         self.N = network.n
         self.render_mode = render_mode
@@ -256,7 +259,7 @@ class PBNEnv:
             key = tuple(int(v) for v in obs)
             self._visits[key] = self._visits.get(key, 0) + 1
         info = {"perturbed": bool(fl & _lib.FLAG_PERTURBED), "in_attractor": bool(fl & _lib.FLAG_IN_ATTRACTOR),
-                "flags": fl}
+                "unsettled": bool(fl & _lib.FLAG_UNSETTLED), "flags": fl}
         return obs, r, bool(fl & _lib.FLAG_TERMINATED), bool(fl & _lib.FLAG_TRUNCATED), info
 
     # ------------------------------------------------------ attribute surface

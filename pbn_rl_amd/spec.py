@@ -29,6 +29,7 @@ __all__ = ["EnvSpec", "PbnNetDesc", "NO_TARGET"]
 
 NO_TARGET = 0xFF
 MAX_ATTRACTORS = 254
+MAX_SETTLE = 4096
 
 
 class PbnNetDesc(ctypes.Structure):
@@ -52,6 +53,7 @@ class PbnNetDesc(ctypes.Structure):
         ("gate_arity", ctypes.c_void_p),
         ("gate_inputs", ctypes.c_void_p),
         ("gate_table", ctypes.c_void_p),
+        ("settle_max", ctypes.c_int32),
     ]
 
 
@@ -64,7 +66,7 @@ class EnvSpec:
     def __init__(self, network: Network, attractors: Optional[Attractors] = None, *,
                  perturbation: float = 0.01, prob_bits: int = 16, horizon: int = 20,
                  success_reward: float = 5.0, wrong_attractor_cost: float = 2.0,
-                 action_cost: float = 1.0, step_cost: float = 0.0):
+                 action_cost: float = 1.0, step_cost: float = 0.0, settle: int = 0):
         self.network = network
         self.attractors: Attractors = [[clean_state(s) for s in a] for a in (attractors or [])]
         self.perturbation = float(perturbation)
@@ -74,6 +76,11 @@ class EnvSpec:
         self.wrong_attractor_cost = float(wrong_attractor_cost)
         self.action_cost = float(action_cost)
         self.step_cost = float(step_cost)
+        # step law: 0/1 = one synchronous update per env step; K >= 2 = the settle law (updates
+        # until an attractor state, at most K; include/pbn_env.h "Step law")
+        self.settle = int(settle or 0)
+        if not 0 <= self.settle <= MAX_SETTLE:
+            raise ValueError(f"settle must be in 0..{MAX_SETTLE}")
         if not 0 <= self.horizon <= 255:
             raise ValueError("horizon must be in 0..255 (0 = none)")
         if len(self.attractors) > MAX_ATTRACTORS:
@@ -154,6 +161,7 @@ class EnvSpec:
         d.gate_arity = _ptr(a["gate_arity"])
         d.gate_inputs = _ptr(a["gate_inputs"])
         d.gate_table = _ptr(a["gate_table"])
+        d.settle_max = self.settle
         return d
 
     @property
@@ -168,7 +176,7 @@ class EnvSpec:
         return {
             "network": self.network.name, "n_nodes": self.n, "words": self.words,
             "n_attractors": len(self.attractors), "perturbation": self.perturbation,
-            "prob_bits": self.prob_bits, "horizon": self.horizon,
+            "prob_bits": self.prob_bits, "horizon": self.horizon, "settle": self.settle,
             "reward": {"success": self.success_reward, "wrong_attractor": self.wrong_attractor_cost,
                        "action": self.action_cost, "step": self.step_cost},
         }

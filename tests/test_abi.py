@@ -41,14 +41,23 @@ def test_library_exports_every_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.pbn_abi_version() == 2
+    assert lib.pbn_abi_version() == 3
 
 
-def test_descriptor_layout_matches_header():
-    # pointer-sized fields follow four int32; same order as pbn_net_desc
-    assert PbnNetDesc.node_func_start.offset == 16
-    assert ctypes.sizeof(PbnNetDesc) == 16 + 6 * 8 + 8 + 3 * 8 + 8 + 3 * 8
-    assert PbnNetDesc.n_gates.offset == 96 and PbnNetDesc.gate_arity.offset == 104
+def test_descriptor_layout_matches_header(tmp_path):
+    """ctypes' pbn_net_desc == the C compiler's (sizeof and every offsetof, from the header)."""
+    import subprocess
+    fields = [f for f, _ in PbnNetDesc._fields_]
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "pbn_env.h"\nint main(void) {\n'
+                   '  printf("%zu\\n", sizeof(pbn_net_desc));\n' +
+                   "".join(f'  printf("%zu\\n", offsetof(pbn_net_desc, {f}));\n' for f in fields) + "  return 0;\n}\n")
+    exe = tmp_path / "layout"
+    inc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "include")
+    subprocess.run(["gcc", "-I", inc, "-o", str(exe), str(src)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    assert got[0] == ctypes.sizeof(PbnNetDesc)
+    assert got[1:] == [getattr(PbnNetDesc, f).offset for f in fields]
 
 
 def _create(lib, spec):
@@ -60,6 +69,7 @@ def _create(lib, spec):
 @pytest.mark.parametrize("field,value,msg", [
     ("prob_bits", 5, "prob_bits"),
     ("horizon", 300, "horizon"),
+    ("settle_max", 5000, "settle_max"),
     ("n_nodes", 0, "n_nodes"),
     ("n_attractors", 255, "n_attractors"),
 ])

@@ -199,3 +199,34 @@ def test_wide_random_network_c_oracle_equals_python_oracle():
     assert net.max_arity > 4
     spec = EnvSpec(net, random_state_targets(12, 4, 8), perturbation=0.01, horizon=4)
     _wide_pair(spec, 96, 4, 3)
+
+
+@pytest.mark.parametrize("name,settle,p", [("pbn7", 2, 0.08), ("pbn28", 7, 0.02), ("bb33", 7, 0.01),
+                                           ("pbn70", 3, 0.3)])
+def test_settle_law_c_oracle_equals_python_oracle(name, settle, p):
+    """The settle law (include/pbn_env.h "Step law") restated twice: the C oracle and the
+    per-env Python oracle agree on every output, flags (UNSETTLED) included."""
+    spec = spec_for(name, perturbation=p, horizon=4, settle=settle)
+    net = spec.network
+    n, seed, off = 64, 4242, 96
+    W = spec.words
+    py = pyoracle.PyPBN(spec)
+    st, tg, t = oracle.reset(spec, seed, 0, off, n)
+    rng = np.random.default_rng(9)
+    st = rng.integers(0, 2 ** 32, size=(W, n), dtype=np.uint64).astype(np.uint32)
+    if spec.n % 32:
+        st[W - 1] &= np.uint32((1 << (spec.n % 32)) - 1)
+    seen = 0
+    for step in range(1, 4):
+        res = oracle.step(spec, seed, step, off, st, np.zeros((W, n), np.uint32), tg, t, 3)
+        for i in range(n):
+            bits = net.unpack([int(st[w, i]) for w in range(W)])
+            r = py.step(seed, step, off + i, bits, [0] * net.n, int(tg[i]), int(t[i]), 3)
+            assert net.pack(r["final_state"]) == [int(res["final_state"][w, i]) for w in range(W)], (step, i)
+            assert net.pack(r["state_out"]) == [int(res["state_out"][w, i]) for w in range(W)]
+            assert r["flags"] == res["flags"][i] and r["t"] == res["t"][i] and r["target"] == res["target"][i]
+            assert np.float32(r["reward"]) == res["reward"][i]
+        seen |= int(np.bitwise_or.reduce(res["flags"]))
+        st, tg, t = res["state_out"], res["target"], res["t"]
+    if name == "pbn70":
+        assert seen & 32, "the cap path (UNSETTLED) was not exercised"
