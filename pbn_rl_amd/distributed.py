@@ -5,8 +5,21 @@ owns the contiguous env ids [offset_r, offset_r + count_r) (multiples of 32);
 because the RNG is keyed by global env id, the union of the shards is
 bit-identical to a single-GPU run of all envs.  There is no exchange inside a
 step.  The only collective is the hand-off of a rollout's transitions to the
-learner: one ``all_gather_into_tensor`` (RCCL over xGMI on MI355X, gloo in
-the CPU tests) of the shard's record buffer per rollout of T steps.
+learner, once per rollout of T steps (RCCL over xGMI on MI355X, gloo in the CPU
+tests), in one of two forms:
+
+  * ``dst=r`` (the learner's rank): every other rank sends its record buffer to
+    rank r point to point (``batch_isend_irecv``); rank r keeps its own records
+    where the kernel wrote them.  Each rank's link to the learner carries its own
+    shard only, the 7 x 153 GB/s fan-in SURVEY.md 8(e) prices (17 B per env-step:
+    ~6.3e10 env-steps/s delivered across 8 GPUs);
+  * ``dst=None``: ``all_gather_into_tensor``, every rank receives every shard.
+
+``ShardedRollout.run`` overlaps the hand-off with the next rollout: records live
+in a ring of ``buffers`` slots (two by default), the collective of rollout k is
+issued asynchronously behind rollout k on the communicator's own stream, and
+rollout k + buffers waits (stream-side, no host sync) only for the collective
+that last read its slot.
 
 Wire format (``TransitionRecords``): one flat byte buffer per shard and rollout,
 field-major so that ``pbn_rollout`` writes every field in place (no packing
@@ -88,52 +101,157 @@ class TransitionRecords:
 
 
 class ShardedRollout:
-    """Drive one env shard per rank and gather (s, a, s', r, flags) every rollout.
+    """Drive one env shard per rank and hand (s, a, s', r, flags) to the learner every rollout.
 
     ``env_factory(env_offset, count)`` builds the shard's env (VectorPBNEnv on the
     rank's GPU in production; any object with the same ``rollout`` contract in tests).
-    Shards must be equal-sized (all_gather_into_tensor), i.e. n_total / 32 divisible by the
-    world size.
+    Shards must be equal-sized, i.e. n_total / 32 divisible by the world size.
+
+    Records are a ring of ``buffers`` TransitionRecords per rollout length: the records a
+    ``rollout`` returns stay valid until ``buffers`` further rollouts of that length have been
+    issued; received records (``gather``) likewise live in a ring of ``buffers`` receive slots.
+    Callers that keep records longer copy them out (e.g. into a replay ring).
     """
 
     def __init__(self, n_total: int, env_factory: Callable[[int, int], object],
-                 group: Optional[dist.ProcessGroup] = None):
+                 group: Optional[dist.ProcessGroup] = None, buffers: int = 2):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.n_total = n_total
         if (n_total // 32) % self.world:
             raise ValueError("equal shards required: (n_total/32) must divide by the world size")
+        if buffers < 1:
+            raise ValueError("buffers must be >= 1")
+        self.buffers = int(buffers)
         self.offset, self.count = shard_range(n_total, self.world, self.rank)
         self.env = env_factory(self.offset, self.count)
         self.words = self.env.words
-        self._rec: Optional[TransitionRecords] = None
-        self._all: Optional[torch.Tensor] = None
+        self._ring: Dict[int, List[TransitionRecords]] = {}
+        self._recv: Dict[Tuple[int, Optional[int]], List[torch.Tensor]] = {}
+        self._pending: Dict[int, List[Optional[object]]] = {}   # slot -> the collective reading it
+        self._issued: Dict[int, int] = {}
+        self._gathered: Dict[Tuple[int, Optional[int]], int] = {}
+
+    @property
+    def _device(self):
+        return getattr(self.env, "device", None) or self.env.state.device
+
+    def _slot(self, steps: int) -> int:
+        return self._issued.get(steps, 0) % self.buffers
 
     def rollout(self, steps: int, random_actions: bool = True, flipmasks: Optional[torch.Tensor] = None
                 ) -> TransitionRecords:
         """``steps`` transitions on the local shard, in one ``rollout`` call whose outputs land
-        directly in the record buffer (reused across calls of the same length)."""
-        dev = getattr(self.env, "device", None) or self.env.state.device
-        if self._rec is None or self._rec.steps != steps:
-            self._rec = TransitionRecords(steps, self.words, self.count, device=dev)
+        directly in the next record slot of the ring.  If an asynchronous hand-off of that slot
+        is still in flight, the rollout is ordered after it on the device (work.wait())."""
+        ring = self._ring.setdefault(steps, [])
+        k = self._slot(steps)
+        if len(ring) <= k:
+            ring.append(TransitionRecords(steps, self.words, self.count, device=self._device))
+        rec = ring[k]
+        pend = self._pending.setdefault(steps, [None] * self.buffers)
+        if pend[k] is not None:
+            _wait(pend[k])
+            pend[k] = None
         self.env.rollout(steps, flipmasks=flipmasks, random_actions=random_actions, keep_obs=True,
-                         keep_final=True, out=self._rec.rollout_out())
-        return self._rec
+                         keep_final=True, out=rec.rollout_out())
+        self._issued[steps] = self._issued.get(steps, 0) + 1
+        rec._slot = k
+        return rec
 
-    def gather(self, rec: TransitionRecords) -> List[TransitionRecords]:
-        """One ``all_gather_into_tensor`` of the flat record buffers; every rank receives the
-        records of every rank (rank r's envs are offset_r + i: rank-major = global order)."""
-        if not dist.is_initialized():
-            return [rec]
+    def gather(self, rec: TransitionRecords, dst: Optional[int] = None, async_op: bool = False):
+        """Hand the records of one rollout to the learner.
+
+        dst = None: ``all_gather_into_tensor``; every rank receives every rank's records
+        (rank r's envs are offset_r + i: rank-major = global order).  dst = r: point-to-point
+        sends to rank r; rank r receives the other shards and uses its own in place, the
+        other ranks receive nothing (an empty list).  Returns the list of per-rank records
+        (valid until ``buffers`` further gathers of this shape and form) or, with async_op,
+        (records, work): the records are readable on the current stream after ``work.wait()``.
+        """
+        if not dist.is_initialized() or (self.world == 1 and dst is not None):
+            # the learner's own shard: already where the kernel wrote it (all_gather still runs
+            # at world 1, so the collective path is exercised on a one-GPU box)
+            return ([rec], None) if async_op else [rec]
         nbytes = rec.flat.numel()
-        if self._all is None or self._all.numel() != self.world * nbytes or self._all.device != rec.flat.device:
-            self._all = torch.empty(self.world * nbytes, dtype=torch.uint8, device=rec.flat.device)
-        dist.all_gather_into_tensor(self._all, rec.flat, group=self.group)
-        return [TransitionRecords(rec.steps, rec.words, rec.n, flat=self._all[r * nbytes:(r + 1) * nbytes])
-                for r in range(self.world)]
+        key = (rec.steps, dst)
+        recv = self._recv.setdefault(key, [])
+        k = self._gathered.get(key, 0) % self.buffers
+        self._gathered[key] = self._gathered.get(key, 0) + 1
+        if dst is None:
+            if len(recv) <= k:
+                recv.append(torch.empty(self.world * nbytes, dtype=torch.uint8, device=rec.flat.device))
+            out = recv[k]
+            work = _Works([dist.all_gather_into_tensor(out, rec.flat, group=self.group, async_op=True)])
+            parts = [TransitionRecords(rec.steps, rec.words, rec.n, flat=out[r * nbytes:(r + 1) * nbytes])
+                     for r in range(self.world)]
+        else:
+            gdst = dist.get_global_rank(self.group, dst) if self.group is not None else dst
+            if self.rank == dst:
+                if len(recv) <= k:
+                    recv.append(torch.empty(self.world * nbytes, dtype=torch.uint8, device=rec.flat.device))
+                out = recv[k]
+                ops = [dist.P2POp(dist.irecv, out[r * nbytes:(r + 1) * nbytes],
+                                  dist.get_global_rank(self.group, r) if self.group is not None else r, self.group)
+                       for r in range(self.world) if r != dst]
+                parts = [rec if r == dst else
+                         TransitionRecords(rec.steps, rec.words, rec.n, flat=out[r * nbytes:(r + 1) * nbytes])
+                         for r in range(self.world)]
+            else:
+                ops = [dist.P2POp(dist.isend, rec.flat, gdst, self.group)]
+                parts = []
+            works = dist.batch_isend_irecv(ops)
+            work = _Works(works)
+        slot = getattr(rec, "_slot", None)
+        if slot is not None:   # the slot's next rollout must wait for this read of it
+            self._pending.setdefault(rec.steps, [None] * self.buffers)[slot] = work
+        if async_op:
+            return parts, work
+        _wait(work)
+        return parts
+
+    def run(self, n_rollouts: int, steps: int, dst: Optional[int] = None, consume=None,
+            random_actions: bool = True) -> None:
+        """``n_rollouts`` rollouts with the hand-off of rollout k overlapped with rollout k + 1.
+        ``consume(k, parts)`` is called on the learner (every rank for dst=None) once rollout
+        k's records are readable on the current stream (after the device-side wait)."""
+        prev = None
+        for k in range(n_rollouts):
+            rec = self.rollout(steps, random_actions=random_actions)
+            parts, work = self.gather(rec, dst=dst, async_op=True)
+            if prev is not None:
+                _finish(prev, consume)
+            prev = (k, parts, work)
+        if prev is not None:
+            _finish(prev, consume)
 
     @staticmethod
     def to_global(parts: List[TransitionRecords]) -> Dict[str, torch.Tensor]:
         """Per-rank records -> per-field tensors over all envs in global order (env = last axis)."""
         return {name: torch.cat([p[name] for p in parts], dim=-1) for name, _, _ in _FIELDS}
+
+
+class _Works:
+    """The works of one hand-off, waited together, at most once (a second wait on a finished
+    gloo receive blocks)."""
+
+    def __init__(self, works):
+        self.works = list(works or [])
+
+    def wait(self):
+        works, self.works = self.works, []
+        for w in works:
+            w.wait()
+
+
+def _wait(work) -> None:
+    if work is not None:
+        work.wait()
+
+
+def _finish(item, consume) -> None:
+    k, parts, work = item
+    _wait(work)
+    if consume is not None and parts:
+        consume(k, parts)

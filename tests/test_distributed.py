@@ -28,7 +28,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n_total, steps, result_path):
+def _worker(rank, world, port, n_total, steps, result_path, form="all"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from pbn_rl_amd.attractors import load_attractors
@@ -38,15 +38,31 @@ def _worker(rank, world, port, n_total, steps, result_path):
 
     spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.05)
     ro = ShardedRollout(n_total, lambda off, cnt: OracleVectorEnv(spec, off, cnt, seed=11))
-    rec = ro.rollout(steps)
-    glob = ShardedRollout.to_global(ro.gather(rec))
-    if rank == 0:
-        torch.save({k: v.clone() for k, v in glob.items()}, result_path)
+    if form == "run":
+        # three rollouts, each hand-off to rank 0 overlapped with the next rollout
+        got = {}
+        ro.run(3, steps, dst=0, consume=lambda k, parts: got.__setitem__(
+            k, {n: v.clone() for n, v in ShardedRollout.to_global(parts).items()}))
+        if rank == 0:
+            torch.save(got, result_path)
+        else:
+            assert got == {}
+    else:
+        rec = ro.rollout(steps)
+        parts = ro.gather(rec, dst=0 if form == "dst" else None)
+        if form == "dst" and rank != 0:
+            assert parts == []
+        if rank == 0:
+            glob = ShardedRollout.to_global(parts)
+            torch.save({k: v.clone() for k, v in glob.items()}, result_path)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_two_rank_gather_equals_single_run(tmp_path):
+@pytest.mark.parametrize("form", ["all", "dst"])
+def test_two_rank_gather_equals_single_run(tmp_path, form):
+    """all_gather (every rank receives) and the point-to-point hand-off to the learner (rank 0
+    keeps its shard in place, rank 1 sends): the union equals one process's run."""
     from pbn_rl_amd.attractors import load_attractors
     from pbn_rl_amd.network import load_network
     from pbn_rl_amd.spec import EnvSpec
@@ -54,7 +70,7 @@ def test_two_rank_gather_equals_single_run(tmp_path):
 
     n_total, steps = 256, 4
     out = str(tmp_path / "gathered.pt")
-    mp.spawn(_worker, args=(2, _free_port(), n_total, steps, out), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), n_total, steps, out, form), nprocs=2, join=True)
     got = torch.load(out, weights_only=True)
     spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.05)
     single = ShardedRollout(n_total, lambda off, cnt: OracleVectorEnv(spec, off, cnt, seed=11))
@@ -75,3 +91,43 @@ def test_record_wire_format():
     assert rec2.flat.numel() == 2 * 32 * (12 * 3 + 5)
     with pytest.raises(ValueError):
         TransitionRecords(1, 1, 48)
+
+
+def test_two_rank_overlapped_run_equals_single_run(tmp_path):
+    """ShardedRollout.run: three rollouts with the hand-off of rollout k to rank 0 in flight
+    while rollout k + 1 runs (two record slots): rank 0 receives all three, equal to three
+    successive rollouts of one process."""
+    from pbn_rl_amd.attractors import load_attractors
+    from pbn_rl_amd.network import load_network
+    from pbn_rl_amd.spec import EnvSpec
+    from tests.oracle_env import OracleVectorEnv
+
+    n_total, steps = 256, 3
+    out = str(tmp_path / "run.pt")
+    mp.spawn(_worker, args=(2, _free_port(), n_total, steps, out, "run"), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.05)
+    single = ShardedRollout(n_total, lambda off, cnt: OracleVectorEnv(spec, off, cnt, seed=11), buffers=1)
+    assert sorted(got) == [0, 1, 2]
+    for k in range(3):
+        want = single.rollout(steps)
+        for name in ("obs", "flipmask", "final_state", "reward", "flags"):
+            assert torch.equal(got[k][name], want[name]), (k, name)
+
+
+def test_record_ring_keeps_previous_rollout():
+    """With two slots the records of rollout k survive rollout k + 1 (and are overwritten by
+    rollout k + 2)."""
+    from pbn_rl_amd.attractors import load_attractors
+    from pbn_rl_amd.network import load_network
+    from pbn_rl_amd.spec import EnvSpec
+    from tests.oracle_env import OracleVectorEnv
+
+    spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.05)
+    ro = ShardedRollout(64, lambda off, cnt: OracleVectorEnv(spec, off, cnt, seed=3), buffers=2)
+    a = ro.rollout(2)
+    snap = a["obs"].clone()
+    b = ro.rollout(2)
+    assert a.flat.data_ptr() != b.flat.data_ptr() and torch.equal(a["obs"], snap)
+    c = ro.rollout(2)
+    assert c.flat.data_ptr() == a.flat.data_ptr()

@@ -1,7 +1,8 @@
-"""The per-rollout transition gather through RCCL ("nccl" backend) on the GPU: a world-1
+"""The per-rollout transition hand-off through RCCL ("nccl" backend) on the GPU: a world-1
 process group on cuda:0 (the box has one GPU; RCCL refuses two ranks on one device).  The
 gathered records must equal the C oracle stepped over the same envs; the
-2-rank exchange itself is covered over gloo in tests/test_distributed.py."""
+2-rank exchange itself (all_gather and the point-to-point hand-off to the learner) is covered
+over gloo in tests/test_distributed.py."""
 import socket
 
 import numpy as np
@@ -18,39 +19,84 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_rccl_world1_gather_matches_oracle():
-    from pbn_rl_amd.attractors import load_attractors
-    from pbn_rl_amd.distributed import ShardedRollout
-    from pbn_rl_amd.network import load_network
-    from pbn_rl_amd.spec import EnvSpec
-    from pbn_rl_amd.vector_env import VectorPBNEnv
-    from tests.oracle_env import OracleVectorEnv
-
+@pytest.fixture
+def rccl_world1():
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
     try:
         assert dist.get_backend() == "nccl"
-        spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.05)
-        n_total, steps = 2048, 6
-
-        def factory(off, cnt):
-            env = VectorPBNEnv(spec, cnt, seed=11, device="cuda:0", env_offset=off)
-            env.reset()
-            return env
-
-        ro = ShardedRollout(n_total, factory)
-        parts = ro.gather(ro.rollout(steps))
-        torch.cuda.synchronize()
-        assert len(parts) == 1 and parts[0].flat.data_ptr() != ro._rec.flat.data_ptr()   # went through RCCL
-        got = ShardedRollout.to_global(parts)
-        want = OracleVectorEnv(spec, 0, n_total, seed=11).rollout(steps)
-        for name in ("obs", "flipmask", "final_state", "reward", "flags"):
-            g = got[name].cpu()
-            w = want[name]
-            if name == "reward":
-                assert np.array_equal(g.numpy().view(np.uint32), w.numpy().view(np.uint32)), name
-            else:
-                assert torch.equal(g, w), name
+        yield
     finally:
         dist.destroy_process_group()
+
+
+def _spec(p=0.05):
+    from pbn_rl_amd.attractors import load_attractors
+    from pbn_rl_amd.network import load_network
+    from pbn_rl_amd.spec import EnvSpec
+    return EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=p)
+
+
+def _factory(spec, seed, base=0):
+    from pbn_rl_amd.vector_env import VectorPBNEnv
+
+    def make(off, cnt):
+        env = VectorPBNEnv(spec, cnt, seed=seed, device="cuda:0", env_offset=base + off)
+        env.reset()
+        return env
+    return make
+
+
+def _check_against_oracle(spec, seed, got, env_offset, n, steps, lo, hi):
+    """Records of envs [lo, hi) of the shard (global ids env_offset + lo ..) == the oracle."""
+    from tests.oracle_env import OracleVectorEnv
+    want = OracleVectorEnv(spec, env_offset + lo, hi - lo, seed=seed).rollout(steps)
+    for name in ("obs", "flipmask", "final_state", "reward", "flags"):
+        g = got[name][..., lo:hi].cpu()
+        w = want[name]
+        if name == "reward":
+            assert np.array_equal(g.numpy().view(np.uint32), w.numpy().view(np.uint32)), name
+        else:
+            assert torch.equal(g, w), (name, lo)
+
+
+def test_rccl_world1_gather_matches_oracle(rccl_world1):
+    from pbn_rl_amd.distributed import ShardedRollout
+    spec = _spec()
+    n_total, steps = 2048, 6
+    ro = ShardedRollout(n_total, _factory(spec, 11))
+    parts = ro.gather(ro.rollout(steps))
+    torch.cuda.synchronize()
+    assert len(parts) == 1 and parts[0].flat.data_ptr() != ro._ring[steps][0].flat.data_ptr()   # via RCCL
+    _check_against_oracle(spec, 11, ShardedRollout.to_global(parts), 0, n_total, steps, 0, n_total)
+
+
+def test_rccl_config4_shard_at_size(rccl_world1):
+    """BASELINE config 4's per-GPU shard: 1,048,576 Bittner-28 envs at env_offset 3 * 2^20 (rank
+    3 of 8), one 16-step rollout (config 4 gathers every T = 16 steps) through the RCCL
+    all_gather, then the overlapped hand-off loop of ShardedRollout.run; four 4,096-env windows
+    across the shard (start, two interior, end) against the oracle."""
+    from pbn_rl_amd.distributed import ShardedRollout
+    spec = _spec(0.01)
+    n, steps, base = 1 << 20, 16, 3 << 20
+    ro = ShardedRollout(n, _factory(spec, 0, base))
+    got = ShardedRollout.to_global(ro.gather(ro.rollout(steps)))
+    torch.cuda.synchronize()
+    for lo in (0, 262144 + 4096, 786432 - 8192, n - 4096):
+        _check_against_oracle(spec, 0, got, base, n, steps, lo, lo + 4096)
+    # the overlapped loop continues the same envs: rollouts 2 and 3 (steps 17-48), the window of
+    # the shard's last 4,096 envs copied out by the learner's consume callback
+    from tests.oracle_env import OracleVectorEnv
+    seen = []
+    ro.run(2, steps, dst=None, consume=lambda k, parts: seen.append(
+        {f: v[..., n - 4096:].cpu().clone() for f, v in ShardedRollout.to_global(parts).items()}))
+    torch.cuda.synchronize()
+    assert len(seen) == 2
+    ref = OracleVectorEnv(spec, base + n - 4096, 4096, seed=0)
+    ref.rollout(steps)
+    for k in range(2):
+        want = ref.rollout(steps)
+        for name in ("obs", "flipmask", "final_state", "flags"):
+            assert torch.equal(seen[k][name], want[name]), (k, name)
+        assert np.array_equal(seen[k]["reward"].numpy().view(np.uint32), want["reward"].numpy().view(np.uint32))
