@@ -17,9 +17,10 @@ fixture attractors), 65,536 envs per GPU, horizon 20, p = 0.01.
 One process per GPU, RCCL ("nccl") process group over all ranks (world 1 too).
 Multi-GPU is weak scaling: every rank owns its own env range (env_offset =
 rank * envs).  ``value`` times the steps alone; ``value_with_gather`` times the
-same steps with one ``all_gather_into_tensor`` of the rollout's (s, a, s', r,
-flags) records (17 B per env-step for Bittner-28) after every rollout launch
-(SURVEY.md 8(e), config 4).  Each timed region is bracketed by barrier +
+same steps with the rollout's (s, a, s', r, flags) records (17 B per env-step for
+Bittner-28) handed to the learner (rank 0) after every rollout launch, overlapped
+with the next launch (``gather.all_gather`` times the
+all-gather form).  Each timed region is bracketed by barrier +
 synchronize, timed with HIP events on the launch stream, and the max over ranks
 is reported.  Inputs are resident in HBM before timing.  Before the timed region
 the captured run is replayed untimed for at least --clock-warm seconds so the
@@ -80,6 +81,9 @@ def parse():
                         "queued behind the spin gate; a graph replay adds ~8 us of device-side overhead per "
                         "replay on this stack, profiles/r02_chunk_fit_pbn28_65536.jsonl)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-final-state", action="store_true",
+                   help="rollout workload: do not write s' (final_state) per step; the next step's obs is s' "
+                        "except for envs that autoreset, whose s' is then not stored")
     p.add_argument("--no-gather", action="store_true",
                    help="skip the second timed pass (rollouts + one RCCL all_gather of their (s, a, s', r, "
                         "flags) records per launch, SURVEY.md 8(e)) reported as value_with_gather")
@@ -122,10 +126,10 @@ def survey_bytes_per_env_step(n_nodes: int) -> int:
     return 3 * s + 8
 
 
-def rollout_bytes_per_env(words: int, steps: int) -> int:
+def rollout_bytes_per_env(words: int, steps: int, final: bool = False) -> int:
     # per launch: read + write state 4W, t 1, target 1 once; per step write
-    # obs 4W, flipmask (in-kernel actions) 4W, reward 4, flags 1
-    return 2 * (4 * words + 1 + 1) + steps * (4 * words + 4 * words + 4 + 1)
+    # obs 4W, flipmask (in-kernel actions) 4W, reward 4, flags 1 (+ s' 4W with final)
+    return 2 * (4 * words + 1 + 1) + steps * (4 * words + 4 * words + 4 + 1 + (4 * words if final else 0))
 
 
 def usable_cpus() -> dict:
@@ -296,9 +300,11 @@ def workload_text(args, chunk: int, rollout_mode: bool) -> str:
                 f"(eps={args.epsilon}), the envs' transitions into the device replay, one update_policy step "
                 f"(batch 256, Adam, double-DQN target), "
                 f"{'one captured hipGraph per frame' if args.learn_graph else 'eager launches'}, {common}")
+    stored = "obs/actions/rewards/flags" + ("" if args.no_final_state else "/s'")
     return (f"{args.network} x {args.envs} envs per GPU, in-kernel random interventions (3 uniform actions/env/step), "
             f"autoreset, {common}; "
-            + (f"pbn_rollout, launches of up to {chunk} steps, per-step obs/actions/rewards/flags written to HBM"
+            + (f"pbn_rollout, launches of up to {chunk} steps, per-step {stored} written to HBM"
+               + (" (s' of autoreset envs not stored)" if args.no_final_state else "")
                if rollout_mode else "pbn_step per step"))
 
 
@@ -345,38 +351,72 @@ def timed(fn, stream, dev, world, local):
     return max_over_ranks(ev0.elapsed_time(ev1), world, dev), max_over_ranks(host_s, world, dev)
 
 
-def gather_pass(env, plan, world, local, dev, stream):
-    """The timed steps again, each rollout launch followed by one all_gather_into_tensor (RCCL)
-    of its (s, a, s', r, flags) records, written in place by the kernel (TransitionRecords):
-    device ms, max over ranks."""
-    from pbn_rl_amd.distributed import TransitionRecords
+def gather_pass(env, plan, world, local, dev, stream, dst):
+    """The timed steps again, the records of every rollout launch handed to the learner
+    (ShardedRollout: a ring of two record slots the kernel writes in place; the hand-off of
+    launch k runs on the communicator's stream while launch k + 1 runs).  dst = 0: point to
+    point to rank 0, which keeps its own shard in place; dst = None: all_gather_into_tensor.
+    Device ms, max over ranks."""
+    from pbn_rl_amd.distributed import ShardedRollout
 
-    recs = {k: TransitionRecords(k, env.words, env.n_alloc, device=dev) for k in set(plan)}
-    outs = {k: torch.empty(world * r.flat.numel(), dtype=torch.uint8, device=dev) for k, r in recs.items()}
+    ro = ShardedRollout(world * env.n_alloc, lambda off, cnt: env)
+    assert ro.offset == env.env_offset and ro.count == env.n_alloc
 
     def run():
         for k in plan:
-            env.rollout(k, random_actions=True, keep_obs=True, keep_final=True, out=recs[k].rollout_out())
-            torch.distributed.all_gather_into_tensor(outs[k], recs[k].flat)
+            ro.gather(ro.rollout(k), dst=dst, async_op=True)
+        for works in ro._pending.values():   # the last hand-offs, before the end event
+            for w in works:
+                if w is not None:
+                    w.wait()
 
     with torch.cuda.stream(stream):
         run()
         torch.cuda.synchronize(dev)
         ms, _ = timed(run, stream, dev, world, local)
-    wire = sum(recs[k].flat.numel() for k in plan)
+    wire = sum(env.n_alloc * k * (12 * env.words + 5) for k in plan)
     return ms, wire
 
 
 def pmc_profile(args, plan):
     """The rocprofv3 PMC summary of the same launch shape, if one is committed under profiles/
-    (network, envs, steps per launch): HBM bytes and VALU instructions per launch."""
+    (network, envs, steps per launch, s' stored or not): HBM bytes and VALU instructions per
+    launch (tools/pmc_summary.py)."""
     if len(set(plan)) != 1:
         return None, None
-    path = os.path.join(ROOT, "profiles", f"pmc_{args.network}_{args.envs}_{args.mode}_T{plan[0]}.json")
+    tail = "_nofinal" if args.no_final_state else ""
+    path = os.path.join(ROOT, "profiles", f"pmc_{args.network}_{args.envs}_{args.mode}_T{plan[0]}{tail}.json")
     if not os.path.exists(path):
         return None, None
     with open(path) as f:
         return json.load(f), os.path.relpath(path, ROOT)
+
+
+def visible_gpu_count() -> int:
+    """GPUs this process may use, counted without touching HIP: the KFD topology in sysfs
+    (nodes with SIMDs are GPUs), narrowed by ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES /
+    CUDA_VISIBLE_DEVICES.  The parent of ``--gpus N`` calls this before it starts the ranks,
+    so it must not initialise the GPU (a process that has may not hand the device to children
+    cleanly, and on this pool must not exec)."""
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    n = 0
+    try:
+        for node in os.listdir(root):
+            try:
+                with open(os.path.join(root, node, "properties")) as f:
+                    props = dict(line.split(None, 1) for line in f if line.strip())
+            except OSError:
+                continue
+            if int(props.get("simd_count", "0").strip() or 0) > 0:
+                n += 1
+    except OSError:
+        n = 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        val = os.environ.get(var)
+        if val is not None:
+            ids = [v for v in val.split(",") if v.strip() != ""]
+            n = min(n, len(ids))
+    return n
 
 
 def spawn_ranks(args) -> int:
@@ -385,7 +425,7 @@ def spawn_ranks(args) -> int:
     import socket
     import subprocess
 
-    n_dev = torch.cuda.device_count()   # does not initialise the GPU on this image
+    n_dev = visible_gpu_count()
     if args.gpus > n_dev:
         print(f"bench.py: --gpus {args.gpus} but only {n_dev} GPU(s) visible; refusing to run "
               f"several ranks on one GPU", file=sys.stderr, flush=True)
@@ -457,13 +497,14 @@ def main():
 
     rollout_mode = args.mode == "rollout" and agent is None
     chunk = args.chunk if rollout_mode else 1
+    keep_final = not args.no_final_state
     bufs = {}   # rollout outputs per launch length; captured graphs write into them, so they live
                 # as long as the graphs (torch.cuda.graph empties the allocator cache on entry)
 
     def launch(k: int):
         """One kernel launch covering k steps of every env."""
         if rollout_mode:
-            bufs[k] = env.rollout(k, random_actions=True, keep_obs=True, keep_final=False, out=bufs.get(k))
+            bufs[k] = env.rollout(k, random_actions=True, keep_obs=True, keep_final=keep_final, out=bufs.get(k))
         elif args.workload == "bdq-learn":
             learner.frame()
         elif agent is not None:
@@ -480,7 +521,7 @@ def main():
         # output buffers of every launch length exist before the capture, so the graph holds
         # the rollout launches alone (no allocation or fill kernels in the timed region)
         for k in set(plan) | set(launch_plan(args.warmup, chunk)):
-            bufs[k] = env.rollout_buffers(k, keep_obs=True, keep_final=False)
+            bufs[k] = env.rollout_buffers(k, keep_obs=True, keep_final=keep_final)
     with torch.cuda.stream(stream):
         for k in launch_plan(args.warmup, chunk):
             launch(k)
@@ -522,11 +563,18 @@ def main():
 
     with_gather = None
     if rollout_mode and not args.no_gather:
-        gms, wire = gather_pass(env, plan, world, local, dev, stream)
-        with_gather = {"value": total_env_steps / (gms * 1e-3), "ms_per_step": gms / args.steps,
-                       "collective": "torch.distributed.all_gather_into_tensor (RCCL) once per rollout launch",
-                       "launches": len(plan), "wire_bytes_per_rank": wire,
-                       "wire_bytes_per_env_step": wire // (env.n_alloc * args.steps)}
+        with_gather = {}
+        for key, dst, what in (("learner", 0, "point-to-point sends of every shard to rank 0 (the learner keeps "
+                                              "its own shard in place; nothing moves at world 1)"),
+                               ("all_gather", None, "torch.distributed.all_gather_into_tensor (RCCL): every "
+                                                    "rank receives every shard")):
+            gms, wire = gather_pass(env, plan, world, local, dev, stream, dst)
+            with_gather[key] = {"value": total_env_steps / (gms * 1e-3), "ms_per_step": gms / args.steps,
+                                "collective": what + "; one hand-off per rollout launch, overlapped with the "
+                                              "next launch (two record slots)",
+                                "launches": len(plan), "wire_bytes_per_rank": wire,
+                                "wire_bytes_per_env_step": wire // (env.n_alloc * args.steps),
+                                "records": "s, a, s' (final_state), r, flags of every env-step"}
 
     bil_ms = None
     if args.workload == "bdq":
@@ -577,7 +625,7 @@ def main():
         elif rollout_mode:
             per_step = survey_bytes_per_env_step(spec.n)
             bytes_run = env.n_alloc * args.steps * per_step
-            moved_run = sum(env.n_alloc * rollout_bytes_per_env(W, k) for k in plan)
+            moved_run = sum(env.n_alloc * rollout_bytes_per_env(W, k, keep_final) for k in plan)
             achieved = bytes_run / elapsed / 1e9
             roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS,
@@ -635,7 +683,7 @@ def main():
                        "host_ms_per_step": host_s * 1e3 / args.steps, "clock_warm_runs": warm_reps},
         }
         if with_gather is not None:
-            out["value_with_gather"] = with_gather["value"]
+            out["value_with_gather"] = with_gather["learner"]["value"]
             out["gather"] = with_gather
         if world == 1 and not args.no_cpu_baseline:
             host = host_info()

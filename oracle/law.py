@@ -9,7 +9,11 @@ restatement of DESIGN.md "Step semantics", as probabilities instead of draws:
 with P(node i -> 1 | s1) = sum over the functions f_ij with f_ij(s1) = 1 of their quantised
 weight (network.thresholds(prob_bits), the integer thresholds the kernels compare against)
 / 2^prob_bits.  The perturbation is Bernoulli(p) per node exactly (the kernels draw it as
-geometric gaps against a 32-bit CDF: the same law to 2^-32).
+geometric gaps against a 32-bit CDF: the same law to 2^-32 per threshold, except gap 2,
+whose uniform is the top word of what the action and reset draws leave of the 64-bit X:
+uniform on its own, and within K / 2^64 per threshold of uniform given those draws,
+K = (N+1)^3 * A(A-1) * |start attractor| -- 7.5e-9 at N = 128 with 254 single-state
+attractors, DESIGN.md "Step semantics").
 
 It is used to pin the law against the one reference artefact that constrains it: the trained
 pbn7 agent (models/pbn7/bdq_final.pt) and the strategy lengths model_tester.py:587-658 recorded

@@ -30,7 +30,8 @@ import numpy as np
 from .attractors import Attractors
 from .network import Network
 
-__all__ = ["successor_boxes", "bottom_sccs", "discover_attractors", "discover_attractors_escalating"]
+__all__ = ["successor_boxes", "explore", "bottom_sccs", "simulate_visits", "discover_attractors",
+           "discover_attractors_escalating", "reached_stg"]
 
 
 def successor_boxes(net: Network, bits: np.ndarray, prob_bits: int = 16) -> Tuple[np.ndarray, np.ndarray]:
@@ -60,13 +61,11 @@ def _key(bits_row: np.ndarray) -> bytes:
     return np.packbits(bits_row.astype(np.uint8), bitorder="little").tobytes()
 
 
-def bottom_sccs(net: Network, candidates: np.ndarray, *, prob_bits: int = 16, max_box: int = 1 << 12,
-                max_states: int = 1 << 20) -> Attractors:
-    """Bottom SCCs reachable from ``candidates`` ((S, N) 0/1 rows), found exactly.
-
-    The candidate set is closed under successors breadth-first (at most ``max_states`` states;
-    a state with more than ``max_box`` successors is not expanded).  An SCC containing a state
-    whose successors were not all enumerated is never reported."""
+def explore(net: Network, candidates: np.ndarray, *, prob_bits: int = 16, max_box: int = 1 << 12,
+            max_states: int = 1 << 20) -> Tuple[List[np.ndarray], List[Optional[List[int]]]]:
+    """The candidate set ((S, N) 0/1 rows) closed under successors breadth-first: (rows, succ),
+    succ[v] = the row indices of v's successors, or None where they were not enumerated (a box
+    of more than ``max_box`` states, or ``max_states`` reached)."""
     N = net.n
     index: Dict[bytes, int] = {}
     rows: List[np.ndarray] = []
@@ -103,9 +102,20 @@ def bottom_sccs(net: Network, candidates: np.ndarray, *, prob_bits: int = 16, ma
                     frontier.append(w)
                 outs.append(w)
             succ[v] = outs
-    total = len(rows)
-    while len(succ) < total:
+    while len(succ) < len(rows):
         succ.append(None)
+    return rows, succ
+
+
+def bottom_sccs(net: Network, candidates: np.ndarray, *, prob_bits: int = 16, max_box: int = 1 << 12,
+                max_states: int = 1 << 20) -> Attractors:
+    """Bottom SCCs reachable from ``candidates`` ((S, N) 0/1 rows), found exactly.
+
+    The candidate set is closed under successors breadth-first (``explore``: at most
+    ``max_states`` states; a state with more than ``max_box`` successors is not expanded).  An
+    SCC containing a state whose successors were not all enumerated is never reported."""
+    rows, succ = explore(net, candidates, prob_bits=prob_bits, max_box=max_box, max_states=max_states)
+    total = len(rows)
     # iterative Tarjan over the explored graph
     idx = [-1] * total
     low = [0] * total
@@ -162,10 +172,11 @@ def bottom_sccs(net: Network, candidates: np.ndarray, *, prob_bits: int = 16, ma
     return out
 
 
-def discover_attractors(net: Network, *, chains: int = 65536, burn_in: int = 1000, window: int = 64, seed: int = 0,
-                        prob_bits: int = 16, device=None, chunk: int = 250, max_box: int = 1 << 14,
-                        max_states: int = 1 << 20) -> Attractors:
-    """Bottom SCCs of ``net``'s STG that ``chains`` GPU chains reach within ``burn_in`` steps."""
+def simulate_visits(net: Network, *, chains: int = 65536, burn_in: int = 1000, window: int = 64, seed: int = 0,
+                    prob_bits: int = 16, device=None, chunk: int = 250) -> np.ndarray:
+    """The distinct states ((S, N) 0/1 rows) that ``chains`` GPU chains of ``net`` (uniform
+    random starts, no perturbation or interventions) visit in the ``window`` steps after
+    ``burn_in`` steps."""
     import torch
 
     from .spec import EnvSpec
@@ -176,7 +187,7 @@ def discover_attractors(net: Network, *, chains: int = 65536, burn_in: int = 100
     env = VectorPBNEnv(spec, chains, seed=seed, device=dev, autoreset=False, keep_final_state=False)
     try:
         env.reset()   # no attractors: uniform random start states
-        left, buf = burn_in, None
+        left, buf = burn_in, None   # (burn_in 0: the window starts at the random start states)
         with torch.cuda.device(dev):
             while left > 0:
                 k = min(chunk, left)
@@ -189,14 +200,42 @@ def discover_attractors(net: Network, *, chains: int = 65536, burn_in: int = 100
     finally:
         env.close()
     shifts = np.arange(32, dtype=np.uint32)
-    bits = ((words[:, :, None] >> shifts) & 1).reshape(len(words), -1)[:, :net.n].astype(np.uint8)
+    return ((words[:, :, None] >> shifts) & 1).reshape(len(words), -1)[:, :net.n].astype(np.uint8)
+
+
+def discover_attractors(net: Network, *, chains: int = 65536, burn_in: int = 1000, window: int = 64, seed: int = 0,
+                        prob_bits: int = 16, device=None, chunk: int = 250, max_box: int = 1 << 14,
+                        max_states: int = 1 << 20) -> Attractors:
+    """Bottom SCCs of ``net``'s STG that ``chains`` GPU chains reach within ``burn_in`` steps."""
+    bits = simulate_visits(net, chains=chains, burn_in=burn_in, window=window, seed=seed, prob_bits=prob_bits,
+                           device=device, chunk=chunk)
     return bottom_sccs(net, bits, prob_bits=prob_bits, max_box=max_box, max_states=max_states)
 
 
-def discover_attractors_escalating(net: Network, *, burn_ins=(1000, 5000, 20000), **kwargs) -> Attractors:
+def reached_stg(net: Network, *, chains: int = 4096, steps: int = 64, seed: int = 0, prob_bits: int = 16,
+                device=None, max_box: int = 1 << 12, max_states: int = 1 << 16) -> Dict[Tuple[int, ...], set]:
+    """``graph.genSTG()`` for networks too large to enumerate (print_graph.py:15-34 calls it on
+    the reference's networks, bb33 has 33 nodes): the states ``chains`` GPU chains visit in
+    their first ``steps`` steps from uniform random starts, closed under successors (at most
+    ``max_states`` states), as {state: set of successor states} -- the exact successor relation
+    of that region.  States whose successors were not enumerated (past ``max_states`` or a box
+    of more than ``max_box``) are left out, as are edges into them."""
+    bits = simulate_visits(net, chains=chains, burn_in=0, window=steps, seed=seed, prob_bits=prob_bits,
+                           device=device)
+    rows, succ = explore(net, bits, prob_bits=prob_bits, max_box=max_box, max_states=max_states)
+    keys = [tuple(int(x) for x in r) for r in rows]
+    done = {v for v, s in enumerate(succ) if s is not None}
+    return {keys[v]: {keys[w] for w in succ[v] if w in done} for v in sorted(done)}
+
+
+def discover_attractors_escalating(net: Network, *, burn_ins=None, **kwargs) -> Attractors:
     """``discover_attractors`` with a growing burn-in until a bottom SCC is certified: 1,000
     steps suffice for pbn28 but not pbn70 (20,000 certify its bottom SCC).  Returns
-    the first non-empty result (empty if every burn-in fails)."""
+    the first non-empty result (empty if every burn-in fails).  A caller's ``burn_in`` (e.g.
+    ``PBNEnv(discovery={"burn_in": 50000})``) is used as given, alone; ``burn_ins`` sets the
+    ladder; the default ladder is (1000, 5000, 20000)."""
+    if burn_ins is None:
+        burn_ins = (kwargs.pop("burn_in"),) if "burn_in" in kwargs else (1000, 5000, 20000)
     kwargs.pop("burn_in", None)
     found: Attractors = []
     for b in burn_ins:

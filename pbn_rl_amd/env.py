@@ -99,12 +99,16 @@ class _Graph:
     def getState(self):
         return self._env.render()
 
-    def genSTG(self):
-        """State-transition graph {state: set(successor states)} for small networks."""
+    def genSTG(self, **reached):
+        """State-transition graph {state: set(successor states)} (print_graph.py:15-34): every
+        state for networks of at most 20 nodes; beyond that the region GPU chains reach from
+        random starts, closed under successors, with its exact successor relation
+        (``discovery.reached_stg``; keyword arguments go to it)."""
         from .attractors import _successor_options  # exhaustive, N <= 20
         net = self._env.spec.network
         if net.n > 20:
-            raise ValueError("genSTG is exhaustive; limited to 20 nodes")
+            from .discovery import reached_stg
+            return reached_stg(net, prob_bits=self._env.spec.prob_bits, device=self._env._venv.device, **reached)
         stg = {}
         for s in range(1 << net.n):
             opts = _successor_options(net, s, self._env.spec.prob_bits)
@@ -180,6 +184,7 @@ class PBNEnv:
         # attractor growth (bdq_model/__init__.py:182-184): states revisited outside the known
         # attractors are verified as bottom SCCs (discovery.bottom_sccs) at episode ends
         self.grow_attractors = grow_attractors
+        self.visit_cap = 1 << 16     # bound on the host-side visit table (packed-state keys)
         self._visits: dict = {}
         self._checked: set = set()
         # rework_probas (bdq_model/__init__.py:203): per (start, target) pair weights
@@ -256,8 +261,10 @@ class PBNEnv:
                        dtype=np.int64)
         self.n_steps += 1
         if self.grow_attractors and not fl & _lib.FLAG_IN_ATTRACTOR:
-            key = tuple(int(v) for v in obs)
+            key = int.from_bytes(self._pin_state.numpy()[:, 0].view(np.uint32).tobytes(), "little")
             self._visits[key] = self._visits.get(key, 0) + 1
+            if len(self._visits) > self.visit_cap:
+                self._prune_visits()
         info = {"perturbed": bool(fl & _lib.FLAG_PERTURBED), "in_attractor": bool(fl & _lib.FLAG_IN_ATTRACTOR),
                 "unsettled": bool(fl & _lib.FLAG_UNSETTLED), "flags": fl}
         return obs, r, bool(fl & _lib.FLAG_TERMINATED), bool(fl & _lib.FLAG_TRUNCATED), info
@@ -344,25 +351,37 @@ class PBNEnv:
         from .discovery import bottom_sccs
         from .spec import MAX_ATTRACTORS
 
-        cand = [s for s, c in self._visits.items() if c >= min_visits and s not in self._checked]
+        cand = [k for k, c in self._visits.items() if c >= min_visits and k not in self._checked]
         if not cand or len(self.all_attractors) >= MAX_ATTRACTORS:
             return 0
+        if len(self._checked) + len(cand) > self.visit_cap:
+            self._checked.clear()
         self._checked.update(cand)
-        found = bottom_sccs(self.spec.network, np.array(cand, dtype=np.uint8), prob_bits=self.spec.prob_bits,
-                            max_states=max_states)
+        W = self.spec.words
+        rows = np.array([self.spec.network.unpack([(k >> (32 * w)) & 0xFFFFFFFF for w in range(W)]) for k in cand],
+                        dtype=np.uint8)
+        found = bottom_sccs(self.spec.network, rows, prob_bits=self.spec.prob_bits, max_states=max_states)
         known = {s for a in self.all_attractors for s in a}
         new = [a for a in found if not any(s in known for s in a)]
         new = new[:MAX_ATTRACTORS - len(self.all_attractors)]
+        for k in cand:   # checked: their visit counts are no longer needed
+            self._visits.pop(k, None)
         if not new:
             return 0
         self.all_attractors.extend([list(a) for a in new])
         self.attracting_states = [s for a in self.all_attractors for s in a]
         self.spec = EnvSpec(self.spec.network, self.all_attractors, **self._spec_kwargs)
         self._venv.set_spec(self.spec)
-        for a in new:
-            for s in a:
-                self._visits.pop(s, None)
         return len(new)
+
+    def _prune_visits(self) -> None:
+        """Keep the visit table within visit_cap: drop the states seen once (a revisit is what
+        makes a candidate), then, if still full, the oldest half."""
+        self._visits = {k: c for k, c in self._visits.items() if c > 1}
+        if len(self._visits) > self.visit_cap // 2:
+            keys = list(self._visits)
+            for k in keys[:len(keys) // 2]:
+                del self._visits[k]
 
     def close(self) -> None:
         self._venv.close()

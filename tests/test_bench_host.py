@@ -75,3 +75,26 @@ def test_usable_cpus():
     assert 1 <= info["usable"] <= info["affinity"] <= info["cpu_count"]
     if info["cgroup_quota"] is not None:
         assert info["usable"] <= max(1, -(-info["cgroup_quota"] // 1))
+
+
+def test_visible_gpu_count_does_not_initialise_hip(tmp_path, monkeypatch):
+    """The parent of `bench.py --gpus N` counts GPUs from sysfs and the visibility variables,
+    never through HIP (torch.cuda stays uninitialised), and honours the variables."""
+    import torch
+    n = bench.visible_gpu_count()
+    assert n >= 0 and not torch.cuda.is_initialized()
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
+    assert bench.visible_gpu_count() == 0
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0")
+    assert bench.visible_gpu_count() <= 1
+
+
+def test_spawn_path_in_a_fresh_interpreter_never_touches_hip():
+    """Run the parent's pre-spawn code in a clean interpreter: after counting, torch.cuda is not
+    initialised (the ranks get the device)."""
+    import subprocess
+    code = ("import sys; sys.argv=['bench.py']; import bench, torch; bench.visible_gpu_count(); "
+            "print(torch.cuda.is_initialized())")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       cwd=str(__import__('pathlib').Path(bench.__file__).parent))
+    assert r.returncode == 0 and r.stdout.strip().endswith("False"), r.stderr

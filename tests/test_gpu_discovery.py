@@ -55,3 +55,42 @@ def test_pbnenv_uses_discovery_beyond_exhaustive_size():
     (state, target), info = env.reset()
     assert tuple(target) in {s for a in env.all_attractors for s in a}
     env.close()
+
+
+def test_genstg_beyond_exhaustive_size_bb33():
+    """graph.genSTG() (print_graph.py:15-34) on the reference's 33-node bb33: the region GPU
+    chains reach, with its exact successor relation (one function per node: every state has
+    exactly one successor), which contains the network's bottom SCCs."""
+    from pbn_rl_amd.env import make
+    from pbn_rl_amd.discovery import successor_boxes
+    import numpy as np
+
+    env = make("gym-PBN/PBNEnv", network="bb33", perturbation=0.0, grow_attractors=False)
+    stg = env.graph.genSTG(chains=2048, steps=48)
+    assert len(stg) > 2048
+    net = env.spec.network
+    some = list(stg)[:500]
+    can0, can1 = successor_boxes(net, np.array(some, dtype=np.uint8))
+    for s, c1 in zip(some, can1):
+        assert stg[s] <= {tuple(int(x) for x in c1)} and len(stg[s]) <= 1
+    present = [s for att in env.real_attractors for s in att if s in stg]
+    assert present
+    for att in env.real_attractors:
+        for s in att:
+            if s in stg:
+                assert stg[s] <= set(att)     # a bottom SCC's successors stay inside it
+    env.close()
+
+
+def test_discovery_honours_a_callers_burn_in(monkeypatch):
+    """PBNEnv(discovery={"burn_in": ...}) reaches discover_attractors unchanged."""
+    from pbn_rl_amd import discovery
+    seen = []
+    real = discovery.discover_attractors
+
+    def spy(net, **kw):
+        seen.append(kw["burn_in"])
+        return real(net, **kw)
+    monkeypatch.setattr(discovery, "discover_attractors", spy)
+    discovery.discover_attractors_escalating(load_network("pbn7"), burn_in=123, chains=256)
+    assert seen == [123]

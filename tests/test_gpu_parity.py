@@ -217,7 +217,7 @@ def test_rollout_high_perturbation_and_no_attractors(variant, monkeypatch):
 
 
 # ---------------------------------------------------------------- synthetic networks
-SYNTH = [(5, 11), (33, 12), (80, 13), (128, 14)]   # 1, 2, 3, 4 state words
+SYNTH = [(5, 11), (32, 15), (33, 12), (80, 13), (128, 14)]   # 1, 1 (full word), 2, 3, 4 state words
 
 
 @pytest.mark.parametrize("n_nodes,seed", SYNTH)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # On the GPU box: bench line + rocprofv3 kernel stats + three PMC passes (FETCH_SIZE, WRITE_SIZE,
-# SQ instruction counts)
+# SQ instruction counts with the VALU-busy / wave-state cycle counters and GRBM_GUI_ACTIVE)
 # for the same bench command.  Usage: tools/gpu_bench_profile.sh TAG [bench args...]
 # Outputs under gpurun_out/TAG/.  Every GPU step has its own time limit; the first failure ends the script.
 set -euo pipefail
@@ -21,7 +21,8 @@ echo "fetch done"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats --output-format csv -d "$out/pmc_write" -o run -- \
   python bench.py --no-cpu-baseline "$@" > /dev/null 2> "$out/pmc_write.err"
 echo "write done"
-timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_BUSY_CYCLES --kernel-trace --stats \
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES \
+  SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --kernel-trace --stats \
   --output-format csv -d "$out/pmc_sq" -o run -- \
   python bench.py --no-cpu-baseline "$@" > /dev/null 2> "$out/pmc_sq.err"
 echo "sq done"

@@ -1,0 +1,51 @@
+#!/bin/bash
+# One gpurun session on the GPU box, as a list of steps (replaces round 2's one-script-per-call
+# tools/gpu_r02_*.sh).  Usage:
+#   tools/gpu_session.sh TAG STEP [STEP ...]
+# Outputs under gpurun_out/TAG/.  Every GPU step runs under its own time limit; the first
+# failure ends the session (no retries).  Steps:
+#   tests            the -m gpu suite (tools/gpu_tests.sh) + smoke()
+#   driver           the driver's bench command (--gpus 1 --steps 20 --warmup 5) + kernel trace + PMC
+#   s2000            2,000 steps at 65,536 envs (100-step launches) + kernel trace + PMC
+#   1m               pbn28 x 1,048,576 envs, 500 steps
+#   8m               pbn28 x 8,388,608 envs, 200 steps
+#   pbn70            config 3: pbn70 x 1,048,576 envs, 200 steps
+#   bdq              config 5: the BDQ frame at 32,768 envs (+ kernel trace)
+#   bdq-learn        BDQ training frames at 32,768 envs
+#   ubench           tools/ubench_valu_issue (VALU issue rates by instruction and waves per SIMD)
+#   nofinal          the driver's command and 2,000 steps without s' (--no-final-state)
+set -o pipefail
+tag=$1; shift
+cd "$GRAFT_REPO_ROOT" || exit 1
+out=gpurun_out/$tag
+mkdir -p "$out"
+export TMPDIR=/tmp
+fail() { echo "STEP $1 FAILED"; exit 1; }
+bench() {   # bench NAME ARGS... : one bench line
+  local name=$1; shift
+  timeout -k 10 300 python bench.py "$@" > "$out/$name.json" 2> "$out/$name.err" || fail "$name"
+  echo "$name: $(python -c "import json,sys; d=json.load(open('$out/$name.json')); print(d['value'], d.get('roofline',{}).get('frac'))")"
+}
+for step in "$@"; do
+  case $step in
+    tests) bash tools/gpu_tests.sh "$tag/tests" || fail tests ;;
+    driver) bash tools/gpu_bench_profile.sh "$tag/driver" --gpus 1 --steps 20 --warmup 5 || fail driver ;;
+    s2000) bash tools/gpu_bench_profile.sh "$tag/s2000" --gpus 1 --steps 2000 --warmup 200 || fail s2000 ;;
+    1m) bench bench_1m --envs 1048576 --steps 500 --warmup 100 --no-cpu-baseline ;;
+    8m) bench bench_8m --envs 8388608 --steps 200 --warmup 20 --no-cpu-baseline --no-gather ;;
+    pbn70) bench bench_pbn70 --network pbn70 --envs 1048576 --steps 200 --warmup 20 ;;
+    bdq)
+      bench bench_bdq --workload bdq
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/bdq_trace" -o run -- \
+        python bench.py --workload bdq --no-cpu-baseline > "$out/bdq_trace.json" 2> "$out/bdq_trace.err" || fail bdq-trace ;;
+    bdq-learn) bench bench_bdq_learn --workload bdq-learn ;;
+    ubench)
+      timeout -k 10 300 tools/ubench_valu_issue > "$out/ubench_valu_issue.jsonl" 2> "$out/ubench.err" || fail ubench
+      echo "ubench done" ;;
+    nofinal)
+      bench bench_driver_nofinal --gpus 1 --steps 20 --warmup 5 --no-final-state --no-cpu-baseline
+      bench bench_s2000_nofinal --steps 2000 --warmup 200 --no-final-state --no-cpu-baseline ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "SESSION $tag DONE"

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--mode", default="rollout")
     ap.add_argument("--steps-per-launch", type=int, default=100)
     ap.add_argument("--words", type=int, default=1)
+    ap.add_argument("--no-final", action="store_true", help="the run did not store s' (bench.py --no-final-state)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--command", default=None, help="the profiled command, recorded in the summary")
     args = ap.parse_args()
@@ -38,7 +39,7 @@ def main():
     w, _, _ = mean_counter(os.path.join(args.run_dir, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
     W, T = args.words, args.steps_per_launch
     if args.mode == "rollout":
-        alg = args.envs * (2 * (4 * W + 2) + T * (8 * W + 5))
+        alg = args.envs * (2 * (4 * W + 2) + T * ((8 if args.no_final else 12) * W + 5))
     else:
         alg = args.envs * (12 * W + 8)
     out = {"kernel": name, "mode": args.mode, "envs": args.envs, "launches": n,
@@ -50,10 +51,24 @@ def main():
            "command": args.command, "steps_per_launch": args.steps_per_launch}
     sq = os.path.join(args.run_dir, "pmc_sq", "run_counter_collection.csv")
     if os.path.exists(sq):
-        for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES", "SQ_BUSY_CYCLES"):
-            out[c + "_per_launch"] = mean_counter(sq, c)[0]
+        for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_ACTIVE_INST_VALU", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES",
+                  "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "GRBM_GUI_ACTIVE"):
+            try:
+                out[c + "_per_launch"] = mean_counter(sq, c)[0]
+            except ZeroDivisionError:   # counter not in this pass
+                pass
         out["valu_insts_per_launch"] = out["SQ_INSTS_VALU_per_launch"]
-    path = args.out or os.path.join("profiles", f"pmc_{args.network}_{args.envs}_{args.mode}_T{args.steps_per_launch}.json")
+        if "SQ_WAVE_CYCLES_per_launch" in out:
+            wc = out["SQ_WAVE_CYCLES_per_launch"]
+            out["wave_state"] = {
+                "note": "fractions of SQ_WAVE_CYCLES (disjoint: MI355X_MICROARCH.md PMC table); quad-cycle units",
+                "active_any": out["SQ_ACTIVE_INST_ANY_per_launch"] / wc,
+                "active_valu": out["SQ_ACTIVE_INST_VALU_per_launch"] / wc,
+                "wait_any (s_waitcnt / barrier)": out["SQ_WAIT_ANY_per_launch"] / wc,
+                "wait_inst_any (issue stall)": out["SQ_WAIT_INST_ANY_per_launch"] / wc}
+    tail = "_nofinal" if args.no_final else ""
+    path = args.out or os.path.join("profiles",
+                                    f"pmc_{args.network}_{args.envs}_{args.mode}_T{args.steps_per_launch}{tail}.json")
     with open(path, "w") as fo:
         json.dump(out, fo, indent=1)
     print(json.dumps(out))
