@@ -330,7 +330,7 @@ def barrier(world: int, local: int) -> None:
 GATE_CYCLES = 250_000
 
 
-def timed(fn, stream, dev, world, local):
+def timed(fn, stream, dev, world, local, gate_cycles: int = None):
     """Device milliseconds of fn() (launches on `stream`), bracketed by barrier + synchronize,
     max over ranks.  A spin kernel is queued on the stream ahead of the start event (the
     "blocking kernel" of nvbench): while it runs the host enqueues the start event, fn's
@@ -340,7 +340,7 @@ def timed(fn, stream, dev, world, local):
     torch.cuda.synchronize(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     with torch.cuda.stream(stream):
-        torch.cuda._sleep(GATE_CYCLES)
+        torch.cuda._sleep(gate_cycles or GATE_CYCLES)
     t0 = time.perf_counter()
     ev0.record(stream)
     fn()
@@ -371,9 +371,12 @@ def gather_pass(env, plan, world, local, dev, stream, dst):
                     w.wait()
 
     with torch.cuda.stream(stream):
-        run()
+        for _ in range(2):   # both record slots (and receive slots) allocated before timing
+            run()
         torch.cuda.synchronize(dev)
-        ms, _ = timed(run, stream, dev, world, local)
+        # the host enqueues every launch and hand-off of the plan while the gate spins (the
+        # ring's Python bookkeeping costs more host time per launch than a bare rollout)
+        ms, _ = timed(run, stream, dev, world, local, gate_cycles=GATE_CYCLES * (1 + len(plan)))
     wire = sum(env.n_alloc * k * (12 * env.words + 5) for k in plan)
     return ms, wire
 

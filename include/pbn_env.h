@@ -18,6 +18,7 @@
  *   compute_ssd_hist(env, model, resets, iters) train_pbn_28.py:257 -> pbn_rollout + pbn_state_histogram
  *   BranchingDQN.predict + list(action.unique())
  *        bdq_model/__init__.py:69-98,176                       -> pbn_bilinear_targets (first layer),
+ *                                                                 pbn_qnet_heads (the other layers),
  *                                                                 pbn_heads_to_flipmask / pbn_q_to_flipmask
  *   update_policy's np.stack of sampled Transitions
  *        bdq_model/__init__.py:100-109                         -> pbn_obs_unpack
@@ -280,6 +281,25 @@ int pbn_heads_to_flipmask(const pbn_net* net, uint64_t seed, uint64_t step, cons
                           uint64_t env_offset, int64_t n_envs, int32_t n_branches, int32_t n_actions,
                           const float* d_heads, float epsilon, const float* d_epsilon, uint32_t* d_flipmask,
                           int32_t* d_actions, void* stream);
+
+/*
+ * The layers of BranchingQNetwork after the bilinear one (bdq_model/network.py:35-61), fused
+ * into one MFMA kernel (v_mfma_f32_32x32x2_f32, exact f32 k-ordered fmaf chains):
+ *   d_y     in   float [n][256]: the bilinear layer after its LeakyReLU (pbn_bilinear_targets
+ *                with leaky != 0)
+ *   d_w1 [128][256], d_b1 [128]; d_w2 [64][128], d_b2 [64]; d_w3 [32][64], d_b3 [32]: the trunk
+ *                Linear layers (torch's (out, in) layout), each followed by LeakyReLU(slope)
+ *   d_wh1 [64 H][32], d_bh1 [64 H]: the H = n_heads first head layers stacked (value head
+ *                first), each followed by LeakyReLU; d_wh2 [H][A][64], d_bh2 [H][A]: the
+ *                second head layers (the value head zero-padded to A outputs)
+ *   d_heads out  float [H][n][A]: the raw head outputs pbn_heads_to_flipmask consumes
+ * n_envs a multiple of 32; n_heads 1..8; n_actions (A) 1..128; d_y and the weight matrices
+ * 16-byte aligned.  Summation order differs from a GEMM library's: compare with a tolerance.
+ */
+int pbn_qnet_heads(const pbn_net* net, int64_t n_envs, const float* d_y, const float* d_w1, const float* d_b1,
+                   const float* d_w2, const float* d_b2, const float* d_w3, const float* d_b3, const float* d_wh1,
+                   const float* d_bh1, const float* d_wh2, const float* d_bh2, int32_t n_heads, int32_t n_actions,
+                   float slope, float* d_heads, void* stream);
 
 const char* pbn_last_error(void);
 int pbn_abi_version(void);

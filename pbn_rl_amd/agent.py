@@ -7,9 +7,11 @@ flips node a-1 for every action a > 0 (:81-84,176-177).  Here one frame covers a
 ``VectorPBNEnv`` batch, and nothing leaves HBM (BatchedBDQ.step):
 
     pbn_bilinear_targets   packed state + target id -> the bilinear layer (+ LeakyReLU)   (HIP)
-    BranchingQNetwork      the rest of the network -> raw head outputs (4, n, N+1)         (PyTorch-ROCm)
+    pbn_qnet_heads         the rest of the network -> raw head outputs (4, n, N+1)         (HIP, MFMA)
     pbn_heads_to_flipmask  dueling combination + epsilon-greedy -> flip-mask words (W, n)  (HIP)
     pbn_step               the PBN transition                                             (HIP)
+
+(``fused_tail=False`` runs the layers after the bilinear one in PyTorch instead.)
 
 ``BranchingQNetwork`` keeps the reference module tree (bdq_model/network.py:24-63), so the
 reference's checkpoints load into it with ``load_state_dict``; its own forward (used for
@@ -144,7 +146,7 @@ class BatchedBDQ:
     pbn_step, all on the env's device and the current stream (graph-capturable)."""
 
     def __init__(self, env: VectorPBNEnv, qnet: Optional[BranchingQNetwork] = None, *, branches: int = 3,
-                 epsilon: float = 0.0):
+                 epsilon: float = 0.0, fused_tail: bool = True):
         self.env = env
         N = env.n_nodes
         self.branches = int(branches)
@@ -165,6 +167,23 @@ class BatchedBDQ:
         self._pack, self._pack_key = None, None
         self._y = torch.empty(n, self.q.model[0].output_dim if self.fast else 1, dtype=torch.float32,
                               device=env.device)
+        self.fused_tail = bool(fused_tail) and self._tail_fusable()
+        self._heads = (torch.empty(self.branches + 1, n, env.n_nodes + 1, dtype=torch.float32, device=env.device)
+                       if self.fused_tail else None)
+
+    def _tail_fusable(self) -> bool:
+        """pbn_qnet_heads implements exactly BranchingQNetwork's layers after the bilinear one
+        (256-128-64-32 trunk, 32-64-A heads, one LeakyReLU slope)."""
+        m = self.q.model
+        if not (self.fast and self._act and len(m) == 8 and m[0].output_dim == 256):
+            return False
+        dims = [(m[2], 256, 128), (m[4], 128, 64), (m[6], 64, 32)]
+        if any(not isinstance(l, nn.Linear) or (l.in_features, l.out_features) != (i, o) for l, i, o in dims):
+            return False
+        acts = [m[1], m[3], m[5], m[7], self.q.value_head[1]] + [hd[1] for hd in self.q.adv_heads]
+        if any(not isinstance(a, nn.LeakyReLU) or float(a.negative_slope) != self._slope for a in acts):
+            return False
+        return self.q.n == self.branches and self.branches + 1 <= 8 and self.q.ac_dim <= 128
 
     def observe(self) -> torch.Tensor:
         """(2, n, N) fp32: env states and their target attractors' first states."""
@@ -266,8 +285,25 @@ class BatchedBDQ:
             return self.q.forward_heads(y) if heads else self.q.forward_tail(y)
         hw = self.bilinear()
         # the kernel applied model[1] (LeakyReLU) when _act
-        out = self.q.forward_heads(self._y, skip_act=self._act, weights=hw)
+        if self.fused_tail and not (torch.is_grad_enabled() and self.q.training):   # (no autograd through it)
+            out = self._tail_kernel(hw)
+        else:
+            out = self.q.forward_heads(self._y, skip_act=self._act, weights=hw)
         return out if heads else self.q.dueling(out)
+
+    def _tail_kernel(self, hw) -> torch.Tensor:
+        """pbn_qnet_heads on self._y -> self._heads (K+1, n, A)."""
+        env, m = self.env, self.q.model
+        w1, b1, w2, b2 = hw
+        ts = [m[2].weight, m[2].bias, m[4].weight, m[4].bias, m[6].weight, m[6].bias,
+              w1, b1, w2, b2]
+        ts = [t.detach().contiguous() for t in ts]
+        L = _lib.load()
+        with torch.cuda.device(env.device):
+            _lib.check(L.pbn_qnet_heads(env.net.handle, env.n_alloc, self._y.data_ptr(),
+                                        *[t.data_ptr() for t in ts], self.branches + 1, env.n_nodes + 1,
+                                        self._slope, self._heads.data_ptr(), env._stream()), "pbn_qnet_heads")
+        return self._heads
 
     def act_heads(self, heads: torch.Tensor, epsilon: Optional[float] = None,
                   step_t: Optional[torch.Tensor] = None, epsilon_t: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -1,0 +1,201 @@
+// pbn_qnet.hip -- the layers of BranchingQNetwork after the bilinear one, fused into one MFMA
+// kernel (config 5's acting frame).
+//
+// bdq_model/network.py:35-61: model = Bilinear(N, N, 256), LeakyReLU, Linear(256, 128),
+// LeakyReLU, Linear(128, 64), LeakyReLU, Linear(64, 32), LeakyReLU; value head Linear(32, 64),
+// LeakyReLU, Linear(64, 1); K advantage heads Linear(32, 64), LeakyReLU, Linear(64, A).  The
+// bilinear layer (+ its LeakyReLU) comes from pbn_bilinear_targets; this kernel takes its
+// output y (n, 256) and writes the raw head outputs (K+1, n, A) that pbn_heads_to_flipmask
+// combines (dueling) and argmaxes -- in one launch where PyTorch spends four GEMMs and three
+// elementwise launches.
+//
+// Layout: one wave per 32 envs, feature-major.  Every layer is out^T = W . in^T on
+// v_mfma_f32_32x32x2_f32 (exact f32: a k-ordered fmaf chain): the envs are the 32 MFMA
+// columns (lane & 31), the output features the rows, so an accumulator tile of one layer is
+// the B operand of the next with no data movement: register r of a 32-feature tile holds
+// feature row(r, h) = (r & 3) + 8 (r >> 2) + 4 h on lane half h, and k-step (tile p, register
+// r) of the next layer takes lane half h's element from there.  The A operand (weights) is
+// then W[out][32 p + row(r, h)], i.e. for r = 4q .. 4q+3 four consecutive inputs: one float4
+// load of the weight row per four MFMAs, straight from the natural (out, in) layout in L2.
+// Biases initialise the accumulators; LeakyReLU (x > 0 ? x : x * slope, torch's form) is
+// applied in registers between layers.  y is read in the same feature order (four float4 per
+// lane per 32-feature tile).
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include "../../include/pbn_env.h"
+#include "net_view.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kD0 = 256, kD1 = 128, kD2 = 64, kD3 = 32, kDH = 64;   // BranchingQNetwork widths
+constexpr int kMaxHeads = 8;                                         // value + up to 7 branches
+constexpr int kMaxActTiles = 4;                                      // A <= 128 (pbn70: 71)
+constexpr int kWaves = 4;                                            // waves (32-env tiles) per block
+
+struct QnetArgs {
+  const float* y;                  // [n][256]
+  const float *w1, *b1, *w2, *b2, *w3, *b3;
+  const float *wh1, *bh1;          // [64 H][32], [64 H]
+  const float *wh2, *bh2;          // [H][A][64], [H][A]
+  float* heads;                    // [H][n][A]
+  int64_t n;
+  int n_heads, n_act;
+  float slope;
+};
+
+__device__ __forceinline__ int feat_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+__device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// acc = bias of the 32 output features 32 m + row(r, h) (0 past n_out)
+__device__ __forceinline__ f32x16 bias_tile(const float* __restrict__ b, int m, int h, int n_out) {
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int o = 32 * m + feat_row(r, h);
+    acc[r] = o < n_out ? b[o] : 0.f;
+  }
+  return acc;
+}
+
+__device__ __forceinline__ f32x16 leaky(f32x16 x, float slope) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) x[r] = x[r] > 0.f ? x[r] : x[r] * slope;
+  return x;
+}
+
+// acc += W[32 m + (lane & 31)][32 p + row(., h)] . X  over the 16 k-steps of input tile p
+// (W row-major [n_out][ld]; rows >= n_out read as 0)
+__device__ __forceinline__ f32x16 tile_step(f32x16 acc, const float* __restrict__ W, int ld, int n_out, int m,
+                                            int p, int lane, const f32x16& X) {
+  const int o = 32 * m + (lane & 31);
+  const int h = lane >> 5;
+  const float* wr = W + (size_t)(o < n_out ? o : 0) * ld + 32 * p + 4 * h;
+  float4 w[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    w[q] = *reinterpret_cast<const float4*>(wr + 8 * q);
+    if (o >= n_out) w[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    acc = mfma(w[q].x, X[4 * q + 0], acc);
+    acc = mfma(w[q].y, X[4 * q + 1], acc);
+    acc = mfma(w[q].z, X[4 * q + 2], acc);
+    acc = mfma(w[q].w, X[4 * q + 3], acc);
+  }
+  return acc;
+}
+
+__global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int h = lane >> 5;
+  const int64_t e0 = ((int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6)) * 32;
+  if (e0 >= a.n) return;   // whole wave (n is a multiple of 32)
+  const int64_t e = e0 + (lane & 31);
+
+  // ---- Linear(256, 128): input tiles from y, feature order row(r, h) (four float4 per tile)
+  f32x16 x1[kD1 / 32];
+#pragma unroll
+  for (int m = 0; m < kD1 / 32; ++m) x1[m] = bias_tile(a.b1, m, h, kD1);
+  const float* yrow = a.y + (size_t)e * kD0 + 4 * h;
+  float4 yv[4], yn[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) yv[q] = *reinterpret_cast<const float4*>(yrow + 8 * q);
+#pragma unroll
+  for (int p = 0; p < kD0 / 32; ++p) {
+    if (p + 1 < kD0 / 32) {   // the next tile's loads in flight under this tile's MFMAs
+#pragma unroll
+      for (int q = 0; q < 4; ++q) yn[q] = *reinterpret_cast<const float4*>(yrow + 32 * (p + 1) + 8 * q);
+    }
+    f32x16 X;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      X[4 * q + 0] = yv[q].x; X[4 * q + 1] = yv[q].y; X[4 * q + 2] = yv[q].z; X[4 * q + 3] = yv[q].w;
+    }
+#pragma unroll
+    for (int m = 0; m < kD1 / 32; ++m) x1[m] = tile_step(x1[m], a.w1, kD0, kD1, m, p, lane, X);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) yv[q] = yn[q];
+  }
+#pragma unroll
+  for (int m = 0; m < kD1 / 32; ++m) x1[m] = leaky(x1[m], a.slope);
+
+  // ---- Linear(128, 64), Linear(64, 32)
+  f32x16 x2[kD2 / 32];
+#pragma unroll
+  for (int m = 0; m < kD2 / 32; ++m) {
+    x2[m] = bias_tile(a.b2, m, h, kD2);
+#pragma unroll
+    for (int p = 0; p < kD1 / 32; ++p) x2[m] = tile_step(x2[m], a.w2, kD1, kD2, m, p, lane, x1[p]);
+    x2[m] = leaky(x2[m], a.slope);
+  }
+  f32x16 x3 = bias_tile(a.b3, 0, h, kD3);
+#pragma unroll
+  for (int p = 0; p < kD2 / 32; ++p) x3 = tile_step(x3, a.w3, kD2, kD3, 0, p, lane, x2[p]);
+  x3 = leaky(x3, a.slope);
+
+  // ---- heads: Linear(32, 64) + LeakyReLU per head (stacked rows 64 k .. 64 k + 63), then
+  // Linear(64, A) of that head's 64 features; raw outputs to heads[k][e][a]
+  const int A = a.n_act;
+  const int atiles = (A + 31) / 32;
+  for (int k = 0; k < a.n_heads; ++k) {
+    f32x16 z[kDH / 32];
+#pragma unroll
+    for (int m = 0; m < kDH / 32; ++m) {
+      z[m] = bias_tile(a.bh1 + kDH * k, m, h, kDH);
+      z[m] = tile_step(z[m], a.wh1 + (size_t)kDH * k * kD3, kD3, kDH, m, 0, lane, x3);
+      z[m] = leaky(z[m], a.slope);
+    }
+    float* out = a.heads + ((size_t)k * a.n + e) * A;
+    for (int m = 0; m < atiles; ++m) {
+      f32x16 o = bias_tile(a.bh2 + (size_t)A * k, m, h, A);
+#pragma unroll
+      for (int p = 0; p < kDH / 32; ++p) o = tile_step(o, a.wh2 + (size_t)A * kDH * k, kDH, A, m, p, lane, z[p]);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int act = 32 * m + feat_row(r, h);
+        if (act < A) out[act] = o[r];
+      }
+    }
+  }
+}
+
+bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int pbn_qnet_heads(const pbn_net* net, int64_t n_envs, const float* d_y, const float* d_w1, const float* d_b1,
+                   const float* d_w2, const float* d_b2, const float* d_w3, const float* d_b3, const float* d_wh1,
+                   const float* d_bh1, const float* d_wh2, const float* d_bh2, int32_t n_heads, int32_t n_actions,
+                   float slope, float* d_heads, void* stream) {
+  int rc = pbn::check_device(net);
+  if (rc) return rc;
+  if (n_envs < 0 || (n_envs & 31)) return pbn::set_error(PBN_EINVAL, "n_envs must be a non-negative multiple of 32");
+  if (n_heads < 1 || n_heads > kMaxHeads) return pbn::set_error(PBN_EINVAL, "n_heads must be 1..8");
+  if (n_actions < 1 || n_actions > 32 * kMaxActTiles) return pbn::set_error(PBN_EINVAL, "n_actions must be 1..128");
+  if (n_envs == 0) return PBN_OK;
+  if (!d_y || !d_w1 || !d_b1 || !d_w2 || !d_b2 || !d_w3 || !d_b3 || !d_wh1 || !d_bh1 || !d_wh2 || !d_bh2 || !d_heads)
+    return pbn::set_error(PBN_EINVAL, "null buffer");
+  // float4 weight-row and y loads: rows of 256 / 128 / 64 / 32 floats start 16-byte aligned
+  // when the base is; the second head layer's rows are 64 floats
+  if (!al16(d_y) || !al16(d_w1) || !al16(d_w2) || !al16(d_w3) || !al16(d_wh1) || !al16(d_wh2))
+    return pbn::set_error(PBN_EINVAL, "y and weight buffers must be 16-byte aligned");
+  QnetArgs a{d_y, d_w1, d_b1, d_w2, d_b2, d_w3, d_b3, d_wh1, d_bh1, d_wh2, d_bh2, d_heads, n_envs, n_heads,
+             n_actions, slope};
+  const int64_t waves = n_envs / 32;
+  const unsigned blocks = (unsigned)((waves + kWaves - 1) / kWaves);
+  hipLaunchKernelGGL(qnet_tail_kernel, dim3(blocks), dim3(64 * kWaves), 0, (hipStream_t)stream, a);
+  if (hipGetLastError() != hipSuccess) return pbn::set_error(PBN_EDEVICE, "qnet_tail_kernel launch failed");
+  return PBN_OK;
+}
+
+}  // extern "C"

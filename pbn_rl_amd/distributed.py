@@ -95,9 +95,10 @@ class TransitionRecords:
 
     def rollout_out(self) -> dict:
         """The ``out=`` dict of ``VectorPBNEnv.rollout``: the kernel writes the fields in place."""
-        d = dict(self.fields)
-        d["_n_steps"] = self.steps
-        return d
+        if getattr(self, "_out", None) is None:
+            self._out = dict(self.fields)
+            self._out["_n_steps"] = self.steps
+        return self._out
 
 
 class ShardedRollout:

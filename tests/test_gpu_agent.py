@@ -259,3 +259,47 @@ def test_prepacked_weights_follow_in_place_updates():
     torch.cuda.synchronize()
     assert agent._pack_key != key
     assert torch.allclose(q_fast, q_ref, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("name,n", [("pbn28", 32768), ("pbn7", 96), ("pbn70", 2080)])
+def test_fused_tail_matches_module(name, n):
+    """pbn_qnet_heads (the layers after the bilinear one, one MFMA kernel) against the PyTorch
+    layers on the same bilinear output: fp32, rtol 1e-5 / atol 1e-5 (summation order differs
+    from hipBLASLt's); and the flip masks it leads to equal the PyTorch tail's except where fp32
+    summation order splits a near-tie (> 99.9 %)."""
+    spec = make_spec(name)
+    torch.manual_seed(11)
+    env = VectorPBNEnv(spec, n, seed=2)
+    qnet = BranchingQNetwork((spec.n, spec.n), spec.n + 1, 3)
+    fused = BatchedBDQ(env, qnet)
+    plain = BatchedBDQ(env, qnet, fused_tail=False)
+    assert fused.fused_tail and not plain.fused_tail
+    env.reset()
+    with torch.no_grad():
+        hf = fused.q_heads().clone()
+        hp = plain.q_heads().clone()
+        torch.cuda.synchronize()
+        assert torch.allclose(hf, hp, rtol=1e-5, atol=1e-5), (hf - hp).abs().max().item()
+        fused.act_heads(hf, 0.0)
+        fm_f = env.flipmask.clone()
+        plain.act_heads(hp, 0.0)
+        same = (env.flipmask == fm_f).float().mean().item()
+    assert same > 0.999, same
+
+
+def test_fused_tail_with_reference_checkpoint():
+    """The reference's trained pbn7 agent (models/pbn7/bdq_final.pt via tests/golden): fused
+    tail == the module's forward on the unpacked observation, within fp32 tolerance."""
+    import os
+    w = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "pbn7_bdq_final.npz"))
+    qnet = BranchingQNetwork((7, 7), 8, 3)
+    qnet.load_state_dict({k: torch.from_numpy(w[k]) for k in w.files})
+    spec = make_spec("pbn7")
+    env = VectorPBNEnv(spec, 256, seed=4)
+    agent = BatchedBDQ(env, qnet)
+    env.reset()
+    with torch.no_grad():
+        q_fast = agent.q_values()
+        q_ref = agent.q(agent.observe())
+    torch.cuda.synchronize()
+    assert torch.allclose(q_fast, q_ref, rtol=1e-5, atol=1e-5)

@@ -24,7 +24,7 @@ fail() { echo "STEP $1 FAILED"; exit 1; }
 bench() {   # bench NAME ARGS... : one bench line
   local name=$1; shift
   timeout -k 10 300 python bench.py "$@" > "$out/$name.json" 2> "$out/$name.err" || fail "$name"
-  echo "$name: $(python -c "import json,sys; d=json.load(open('$out/$name.json')); print(d['value'], d.get('roofline',{}).get('frac'))")"
+  echo "$name: $(python -c "import json; d=[json.loads(l) for l in open('$out/$name.json') if l.startswith('{')][-1]; print(d['value'], d.get('roofline',{}).get('frac'))")"
 }
 for step in "$@"; do
   case $step in

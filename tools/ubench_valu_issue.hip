@@ -2,10 +2,12 @@
 // weak" 2: calibrate the rollout kernel's VALU ceiling).  Each lane runs 8 independent chains of
 // one instruction with VGPR-only operands (no literal, no SGPR: the VOP encodings the kernel
 // issues), kIters x 8 instructions per wave.  Every wave reads the shader clock (s_memtime, one
-// tick = one shader cycle) around its loop and the 100 MHz real-time clock (s_memrealtime), so
-// the line gives cycles per wave-instruction per SIMD without assuming a clock:
-//   simd_cycles_per_inst = median wave's loop cycles / (instructions per wave x waves per SIMD)
-// and the shader clock the load ran at (cycles / real time).
+// tick = one shader cycle) and the 100 MHz real-time clock (s_memrealtime) around its loop.
+// Two rates per line:
+//   simd_cycles_per_inst   = the chip-wide span of the loops (first start to last end, real
+//                            time x the median shader clock) x SIMDs / wave-instructions issued:
+//                            the SIMD issue cost, whatever the waves' co-residency;
+//   cycles_per_wave_inst   = one wave's own loop cycles per instruction (its issue interval).
 //
 //   hipcc --offload-arch=gfx950 -O3 -o tools/ubench_valu_issue tools/ubench_valu_issue.hip
 //   tools/ubench_valu_issue > profiles/r03_ubench_valu_issue.jsonl
@@ -82,8 +84,10 @@ __global__ void __launch_bounds__(256) issue_kernel(const uint32_t* __restrict__
   out[tid] = r;
   if ((threadIdx.x & 63) == 0) {
     const int w = tid >> 6;
-    stamps[2 * w] = t1 - t0;
-    stamps[2 * w + 1] = r1 - r0;
+    stamps[4 * w] = t1 - t0;
+    stamps[4 * w + 1] = r1 - r0;
+    stamps[4 * w + 2] = r0;
+    stamps[4 * w + 3] = r1;
   }
 }
 
@@ -97,20 +101,26 @@ void run(int cus, int waves_per_simd, const uint32_t* d_in, uint32_t* d_out, uns
   hipLaunchKernelGGL(issue_kernel<OP>, dim3(blocks), dim3(256), 0, 0, d_in, d_out, d_st);   // warm
   hipLaunchKernelGGL(issue_kernel<OP>, dim3(blocks), dim3(256), 0, 0, d_in, d_out, d_st);
   hipDeviceSynchronize();
-  std::vector<unsigned long long> st(2 * (size_t)n_waves);
+  std::vector<unsigned long long> st(4 * (size_t)n_waves);
   hipMemcpy(st.data(), d_st, st.size() * 8, hipMemcpyDeviceToHost);
   std::vector<double> cyc(n_waves), mhz(n_waves);
+  unsigned long long first = ~0ull, last = 0;
   for (int w = 0; w < n_waves; ++w) {
-    cyc[w] = (double)st[2 * w];
-    mhz[w] = (double)st[2 * w] / ((double)st[2 * w + 1] / 100.0);   // real-time clock: 100 MHz
+    cyc[w] = (double)st[4 * w];
+    mhz[w] = (double)st[4 * w] / ((double)st[4 * w + 1] / 100.0);   // real-time clock: 100 MHz
+    first = std::min(first, st[4 * w + 2]);
+    last = std::max(last, st[4 * w + 3]);
   }
   std::sort(cyc.begin(), cyc.end());
   std::sort(mhz.begin(), mhz.end());
   const double inst = (double)kIters * kChains * kInstPer[OP];
   const double med = cyc[n_waves / 2];
+  const double span_cycles = (double)(last - first) / 100.0 * mhz[n_waves / 2];   // 100 MHz ticks x MHz
+  const double simd_rate = span_cycles * (4.0 * cus) / (inst * n_waves);
   printf("{\"op\": \"%s\", \"waves_per_simd\": %d, \"wave_loop_cycles_median\": %.0f, "
-         "\"cycles_per_wave_inst\": %.3f, \"simd_cycles_per_inst\": %.3f, \"shader_mhz_median\": %.0f}\n",
-         kNames[OP], waves_per_simd, med, med / inst, med / inst / waves_per_simd, mhz[n_waves / 2]);
+         "\"cycles_per_wave_inst\": %.3f, \"span_cycles\": %.0f, \"simd_cycles_per_inst\": %.3f, "
+         "\"shader_mhz_median\": %.0f}\n",
+         kNames[OP], waves_per_simd, med, med / inst, span_cycles, simd_rate, mhz[n_waves / 2]);
 }
 
 template <int OP>
@@ -128,7 +138,7 @@ int main() {
   hipMalloc(&d_in, 1024 * 4);
   hipMemcpy(d_in, h.data(), 1024 * 4, hipMemcpyHostToDevice);
   hipMalloc(&d_out, (size_t)cus * 8 * 256 * 4);
-  hipMalloc(&d_st, (size_t)cus * 8 * 4 * 16);
+  hipMalloc(&d_st, (size_t)cus * 8 * 4 * 32);
   sweep<kBitop3>(cus, d_in, d_out, d_st);
   sweep<kXor>(cus, d_in, d_out, d_st);
   sweep<kAdd>(cus, d_in, d_out, d_st);
