@@ -28,7 +28,7 @@ EXPORTS = ["pbn_net_create", "pbn_net_destroy", "pbn_net_words", "pbn_reset", "p
            "pbn_rollout", "pbn_state_histogram", "pbn_obs_unpack", "pbn_bilinear_targets", "pbn_q_to_flipmask",
            "pbn_q_to_flipmask_dev",
            "pbn_heads_to_flipmask", "pbn_qnet_heads", "pbn_last_error", "pbn_abi_version"]
-SOURCES = ["pbn_env.hip", "pbn_agent.hip", "pbn_qnet.hip"]
+SOURCES = ["pbn_env.hip", "pbn_settle.hip", "pbn_agent.hip", "pbn_qnet.hip"]
 
 _lib: Optional[ctypes.CDLL] = None
 
@@ -38,14 +38,29 @@ class PbnError(RuntimeError):
 
 
 def build(verbose: bool = False, out: str = LIB_PATH, defines=()) -> str:
-    """Compile csrc/pbn_env.hip for gfx950 into pbn_rl_amd/libpbn_env.so (in-tree).
-    ``defines`` builds a diagnostic variant (e.g. PBN_STAMPS) into another path."""
-    srcs = [os.path.join(SRC_DIR, f) for f in SOURCES]
-    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-unused-result", *[f"-D{d}" for d in defines], "-o", out + ".tmp", *srcs]
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+    """Compile csrc/*.hip for gfx950 into pbn_rl_amd/libpbn_env.so (in-tree): one object per
+    source, compiled in parallel, then one link.  ``defines`` builds a diagnostic variant (e.g.
+    PBN_STAMPS) into another path."""
+    import tempfile
+    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result",
+             *[f"-D{d}" for d in defines]]
+    with tempfile.TemporaryDirectory(prefix="pbn_build_") as tmp:
+        objs, procs = [], []
+        for f in SOURCES:
+            obj = os.path.join(tmp, f.replace(".hip", ".o"))
+            cmd = ["hipcc", *flags, "-c", "-o", obj, os.path.join(SRC_DIR, f)]
+            if verbose:
+                print(" ".join(cmd))
+            procs.append((subprocess.Popen(cmd), cmd))
+            objs.append(obj)
+        rcs = [(p.wait(), cmd) for p, cmd in procs]   # all of them, before the directory goes
+        for rc, cmd in rcs:
+            if rc != 0:
+                raise subprocess.CalledProcessError(rc, cmd)
+        cmd = ["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out + ".tmp", *objs]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
     os.replace(out + ".tmp", out)
     return out
 

@@ -1,0 +1,25 @@
+// pbn_settle.hip -- the settle-law instances of the wave step kernel (pbn_step_wave variants 3
+// and 4, include/pbn_env.h "Step law"), compiled beside pbn_env.hip so that the two halves of
+// the kernel instances build in parallel.
+#include "step_kernels.h"
+
+namespace {
+
+template <int V>
+void* pick_settle(int W, int B) {
+#define PBN_SETTLE_CASE(w, b) \
+  if (W == w && B == b) return reinterpret_cast<void*>(&pbn_step_wave<w, b, V>);
+#define PBN_SETTLE_W(w) PBN_SETTLE_CASE(w, 4) PBN_SETTLE_CASE(w, 8) PBN_SETTLE_CASE(w, 12) PBN_SETTLE_CASE(w, 16)
+  PBN_SETTLE_W(1) PBN_SETTLE_W(2) PBN_SETTLE_W(3) PBN_SETTLE_W(4)
+#undef PBN_SETTLE_W
+#undef PBN_SETTLE_CASE
+  return nullptr;
+}
+
+}  // namespace
+
+namespace pbn {
+
+void* settle_kernel(int W, int B, int lean) { return lean ? pick_settle<4>(W, B) : pick_settle<3>(W, B); }
+
+}  // namespace pbn

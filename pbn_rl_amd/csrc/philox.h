@@ -36,12 +36,7 @@ __host__ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32
 #endif
 }
 
-// PBN_DIAG_PHILOX_ROUNDS: diagnostic builds only (timing the RNG's share of a kernel; the
-// results are then wrong); the product is always Philox4x32-7
-#ifndef PBN_DIAG_PHILOX_ROUNDS
-#define PBN_DIAG_PHILOX_ROUNDS 7
-#endif
-constexpr int kPhiloxRounds = PBN_DIAG_PHILOX_ROUNDS;
+constexpr int kPhiloxRounds = 7;
 
 // ctr = (c0, c1, c2, c3), key = (k0, k1); one round: two 32x32->64 products, two 3-input xors,
 // the Weyl key bump (SALU: the key is wave-uniform)

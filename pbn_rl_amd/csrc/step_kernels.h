@@ -1,0 +1,1782 @@
+// step_kernels.h -- the device side of libpbn_env.so: the step / rollout / reset / histogram
+// kernels and their helpers (library-internal).  Included by pbn_env.hip (host side, the
+// one-update instances) and pbn_settle.hip (the settle-law instances), so the two halves of
+// the template instances compile in parallel.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../../include/pbn_env.h"
+#include "bitslice.h"
+#include "philox.h"
+
+using pbn::bfi;
+using pbn::Word4;
+
+namespace {
+
+constexpr int kFuncRecWords = 24;  // in[4], leaf[16], thr, pad[3]
+constexpr int kNodeRecs = 4;       // compact records prefetched per node by the wave kernel
+constexpr int kStatePrio = 2;      // s_setprio of the pipelined rollout's state wave
+
+constexpr int kWavesPerBlock = 4;  // wave kernel: waves (32-env groups) per block, sharing one LDS table image
+constexpr int kMaxHashBits = 12;
+
+struct FuncRec {   // host-side function record (validation, leaf tables for the selectors)
+  uint32_t in[4];      // input node index per mux level (padded with 0)
+  uint32_t leaf[16];   // leaf[m] = d_m (x0 mask), leaf[8+m] = beta_m
+  uint32_t thr;        // cumulative selection threshold c_f (prob_bits units)
+  uint32_t pad[3];
+};
+static_assert(sizeof(FuncRec) == kFuncRecWords * 4, "FuncRec layout");
+
+struct StepArgs {
+  const uint32_t* tab;          // packed LDS image (cdf | reward | hash)
+  const int32_t* att_start;     // [A+1]
+  const uint32_t* att_states;   // [S*W]
+  const uint32_t* state;
+  uint32_t* flipmask;
+  uint8_t* target;
+  uint8_t* t;
+  uint32_t* state_out;
+  uint32_t* final_state;
+  float* reward;
+  uint8_t* flags;
+  uint64_t seed, step, env_offset;
+  const uint64_t* step_ptr;     // single-step kernel: step index read from device memory (nullable)
+  int64_t n_envs;
+  int64_t n_groups;
+  int n_nodes;
+  int n_attr;
+  int horizon;
+  int mode;
+  int cdf_len;       // power of two >= N (LDS cdf table length, padded with 0xFFFFFFFF)
+  int hash_bits;     // 0 = no attractors
+  int hash_probes;   // max probe count (>= 1 when attractors exist)
+  int tab_words;     // words of the LDS table image
+  int prob_bits;
+  int n_funcs;
+  int wave_words;    // wave kernel: per-wave LDS words of S planes (after the shared table image)
+  int gap_exact;     // 1: binary search for gaps (p == 0 or tiny); 0: log estimate + fix-up;
+                     // 2: bucket table (gap_lut_off)
+  int gap_lut_off;   // LDS image offset of the gap bucket table, uint2 [gap_nb + 1] {threshold, gap}
+  int gap_shift;     // bucket of u = u >> gap_shift
+  int gap_nb;        // buckets below C[N-1]; entry gap_nb is the sentinel {0xFFFFFFFF, N+1}
+  float inv_log2q;   // 1 / log2(1 - p)
+  const uint4* fcompact;   // [n_funcs] {inputs (4 x u8), truth table, threshold, 0}
+  const uint4* nrec;       // [N * kNodeRecs] node-major copy of the first records (+ nf, f0 in .w)
+  uint32_t hash_mult[4];
+  unsigned long long* stamps;  // diagnostic builds (-DPBN_STAMPS) only: per-wave phase clocks
+  int n_steps;       // steps per launch (wave kernel); outputs are [n_steps][...] arrays
+  uint32_t* obs;     // [n_steps][W][n] observation before each step (nullable)
+  int n_states;      // attractor states (bounds of att_states; checked builds)
+  int att_off;       // LDS image offset of attractor start[A+1] | states[S][W] (wave kernel)
+  int sel_off;       // LDS image offset of the leaf selectors, uint4 [kNodeRecs][2][32W] (wave kernel)
+  int nrec_off;      // LDS image offset of the node records, record-major uint4 [kNodeRecs][32W]
+  int n_cls;         // 1..4: the first kNodeRecs thresholds of every node take one of n_cls values
+                     // uthr[0..n_cls) (record .y = class index); 0: per-node thresholds
+  uint32_t uthr[kNodeRecs];
+  int max_nf;        // largest function count of a node
+  int lq;            // pipelined rollout: selection masks per node in a slot (max(max_nf - 1, 1))
+  int slot_words;    // pipelined rollout: words of one step slot
+  int gate_off;      // wave kernel: LDS image offset of the gate records, uint4 [n_gates] by level
+  int glayer_off;    // LDS image offset of the level starts, int32 [n_glayers + 1]
+  int n_glayers;     // 0: no gates
+  int att_single;    // every attractor is one state: the reset state is attractor a's state a
+  uint32_t n1_magic; // ceil(2^32 / (N + 1)): random-action digits
+  uint32_t am1_magic;  // ceil(2^32 / (A - 1)) for A >= 2: autoreset (start, target) split
+  uint64_t x_mult;     // (N+1)^3 * A(A-1) (A >= 2) mod 2^64: what the ENV draws before gap 2 leave
+                       // of X is X * x_mult (times the start attractor's size, multi-state nets)
+  int sel_prio;        // pipelined rollout: raise the selection wave's priority (grids of at most
+                       // four blocks per CU)
+  int settle_max;      // step law: >= 2 = the settle law (wave kernel variants 3, 4)
+};
+
+// In-kernel phase clocks (cdna_hip_programming.md section 7, "In-kernel stamps"):
+// compiled only into the diagnostic library (-DPBN_STAMPS), never the product.
+#ifdef PBN_STAMPS
+#define PBN_STAMP(k)                                                                          \
+  do {                                                                                        \
+    unsigned long long t_;                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    if (a.stamps && (threadIdx.x & 63) == 0)                                                  \
+      a.stamps[(size_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + (k)] = t_; \
+  } while (0)
+// pipelined rollout: per role, clocks at the start of iteration 10, after its work, after the barrier
+#define PBN_PSTAMP(k, slot_)                                                                  \
+  do {                                                                                        \
+    if ((k) == 10) {                                                                          \
+      unsigned long long t_;                                                                  \
+      __builtin_amdgcn_sched_barrier(0);                                                      \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");             \
+      __builtin_amdgcn_sched_barrier(0);                                                      \
+      if (a.stamps && (threadIdx.x & 63) == 0)                                                \
+        a.stamps[(size_t)blockIdx.x * 16 + (threadIdx.x >> 6) * 4 + (slot_)] = t_;            \
+    }                                                                                         \
+  } while (0)
+#define PBN_PSTAMP_AT(k, idx_)                                                                \
+  do {                                                                                        \
+    if ((k) == 10) {                                                                          \
+      unsigned long long t_;                                                                  \
+      __builtin_amdgcn_sched_barrier(0);                                                      \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");             \
+      __builtin_amdgcn_sched_barrier(0);                                                      \
+      if (a.stamps && (threadIdx.x & 63) == 0) a.stamps[(size_t)blockIdx.x * 16 + (idx_)] = t_; \
+    }                                                                                         \
+  } while (0)
+// pipelined rollout, launch anatomy: the state wave's s_memrealtime (100 MHz, one clock for the
+// whole chip) at kernel entry, after the table image, at the loop start, after iterations 0 and
+// 1, after the loop and after its final stores have landed; row gridDim.x + block
+#define PBN_RSTAMP(idx_)                                                                      \
+  do {                                                                                        \
+    unsigned long long t_;                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)(gridDim.x + blockIdx.x) * 16 + (idx_)] = t_; \
+  } while (0)
+#else
+#define PBN_STAMP(k) do {} while (0)
+#define PBN_PSTAMP(k, slot_) do {} while (0)
+#define PBN_PSTAMP_AT(k, idx_) do {} while (0)
+#define PBN_RSTAMP(idx_) do {} while (0)
+#endif
+
+// Bounds-checked global indexing for the diagnostic library (-DPBN_CHECKS): an
+// out-of-range index is printed and redirected to element 0 instead of faulting.
+#ifdef PBN_CHECKS
+__device__ __noinline__ size_t pbn_ck(size_t i, size_t len, int site) {
+  if (i < len) return i;
+  printf("pbn OOB site %d idx %llu len %llu block %u thread %u\n", site, (unsigned long long)i,
+         (unsigned long long)len, blockIdx.x, threadIdx.x);
+  return 0;
+}
+#define CK(i, len, site) pbn_ck((size_t)(i), (size_t)(len), (site))
+#else
+#define CK(i, len, site) (i)
+#endif
+
+// ---------------------------------------------------------------- helpers
+// Element (uniform base + lane element) of an output array addressed as a wave-uniform 64-bit
+// base (SGPRs, advanced per step on the SALU) plus the lane's 32-bit byte offset: the
+// global_store / global_load "saddr" form, with no 64-bit VGPR address pair and no per-step
+// VALU address arithmetic (lane_elem * sizeof(T) < 2^32: n_envs < 2^30).  Checked builds keep
+// the bounds-checked index.
+template <typename T>
+__device__ __forceinline__ T& lane_at(T* base, size_t uniform_elems, uint32_t lane_bytes) {
+  // laundered so that loop strength reduction cannot turn the sum into a 64-bit VGPR
+  // induction variable
+  asm volatile("" : "+s"(uniform_elems));
+  asm volatile("" : "+v"(lane_bytes));
+  return *reinterpret_cast<T*>(reinterpret_cast<char*>(base + uniform_elems) + lane_bytes);
+}
+#ifdef PBN_CHECKS
+#define LANE_AT(base, ubase, le_, len, site) (base)[CK((ubase) + (size_t)(le_), (len), (site))]
+#else
+#define LANE_AT(base, ubase, le_, len, site) lane_at((base), (ubase), (uint32_t)(le_) * (uint32_t)sizeof(*(base)))
+#endif
+// Streaming store of a rollout output (pbn_rollout_pipe): non-temporal, so that the per-step
+// obs / flip-mask / reward / flags stream does not evict the table image from L2 between
+// launches (every launch re-reads it)
+#ifndef PBN_CHECKS
+#define LANE_ST(base, ubase, le_, len, site, v) __builtin_nontemporal_store((v), &LANE_AT(base, ubase, le_, len, site))
+#else
+#define LANE_ST(base, ubase, le_, len, site, v) (LANE_AT(base, ubase, le_, len, site) = (v))
+#endif
+__device__ __forceinline__ uint32_t valid_word_mask(int n, int w) {
+  const int bits = n - 32 * w;
+  return bits >= 32 ? 0xFFFFFFFFu : (bits <= 0 ? 0u : ((1u << bits) - 1u));
+}
+
+// One bounded draw from the 64-bit uniform X = (hi:lo), keeping the rest of X: v =
+// floor(X * K / 2^64) in [0, K), X <- X * K mod 2^64 (two v_mad_u64_u32; bias <= K / 2^64;
+// oracle/pbn_oracle.c ext64).
+__device__ __forceinline__ uint32_t ext64(uint32_t& hi, uint32_t& lo, uint32_t K) {
+  const uint64_t x = (uint64_t)lo * K;
+  const uint64_t y = (uint64_t)hi * K + (x >> 32);
+  lo = (uint32_t)x;
+  hi = (uint32_t)y;
+  return (uint32_t)(y >> 32);
+}
+
+// The LDS table image from global memory, all of a thread's loads issued before its stores
+// (four loads in flight per thread, where a load-store loop waits once per element)
+__device__ __forceinline__ void copy_image(uint32_t* L, const StepArgs& a) {
+  const uint4* src = reinterpret_cast<const uint4*>(a.tab);
+  uint4* dst = reinterpret_cast<uint4*>(L);
+  const int n4 = a.tab_words >> 2, bd = (int)blockDim.x;
+  int k = (int)threadIdx.x;
+  for (; k + 3 * bd < n4; k += 4 * bd) {
+    const uint4 v0 = src[CK(k, n4, 5)], v1 = src[CK(k + bd, n4, 5)];
+    const uint4 v2 = src[CK(k + 2 * bd, n4, 5)], v3 = src[CK(k + 3 * bd, n4, 5)];
+    dst[k] = v0; dst[k + bd] = v1; dst[k + 2 * bd] = v2; dst[k + 3 * bd] = v3;
+  }
+  for (; k < n4; k += bd) dst[k] = src[CK(k, n4, 5)];
+}
+
+// LDS hash of the attractor states, slot-major: slot s holds its key words at [s * HS, s * HS +
+// W) and the attractor id (0xFFFFFFFF: empty) at s * HS + W, HS = W + 1 rounded up to a power
+// of two, so that one probe is one ds_read_b64 (W = 1) or ds_read_b128 (W = 2, 3)
+template <int W>
+struct HashStride {
+  static constexpr int value = W == 1 ? 2 : (W <= 3 ? 4 : 8);
+};
+
+// attractor id of the state sp at slot s, or -1
+template <int W>
+__device__ __forceinline__ int hash_probe(const uint32_t* __restrict__ htab, uint32_t s, const uint32_t (&sp)[W]) {
+  constexpr int HS = HashStride<W>::value;
+  const uint32_t* e = htab + (size_t)s * HS;
+  uint32_t ent[HS];
+  if constexpr (HS == 2) {
+    const uint2 v = *reinterpret_cast<const uint2*>(e);
+    ent[0] = v.x; ent[1] = v.y;
+  } else {
+#pragma unroll
+    for (int q = 0; q < HS / 4; ++q) {
+      const uint4 v = reinterpret_cast<const uint4*>(e)[q];
+      ent[4 * q] = v.x; ent[4 * q + 1] = v.y; ent[4 * q + 2] = v.z; ent[4 * q + 3] = v.w;
+    }
+  }
+  bool eq = ent[W] != 0xFFFFFFFFu;
+#pragma unroll
+  for (int w = 0; w < W; ++w) eq = eq && ent[w] == sp[w];
+  return eq ? (int)ent[W] : -1;
+}
+
+// Three actions uniform on [0, N]: the base-(N+1) digits of c, one draw over (N+1)^3.
+// Division by N+1 is a multiply-high by magic = ceil(2^32 / (N+1)), exact for c * (N+1) < 2^32
+// (c < (N+1)^3 <= 129^3).
+template <int W>
+__device__ __forceinline__ void actions_from_draw(uint32_t c, int N, uint32_t magic, uint32_t (&m)[W]) {
+  const uint32_t n1 = (uint32_t)(N + 1);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {   // action a in [0, N]: 0 = no-op, else flip node a-1
+    const uint32_t qt = __umulhi(c, magic);
+    const int act = (int)(c - qt * n1);
+    c = qt;
+#pragma unroll
+    for (int w = 0; w < W; ++w)
+      if (act > 0 && ((act - 1) >> 5) == w) m[w] |= 1u << ((act - 1) & 31);
+  }
+}
+
+// actions_from_draw for one word with N <= 31: action a sets bit a - 1 as 1 << (a - 1), where
+// a = 0 shifts by 31 (the shift count's low five bits) onto a bit past the network that `vmask`
+// (valid_word_mask(N, 0)) clears once for all three: no per-action guard
+__device__ __forceinline__ uint32_t actions_mask31(uint32_t c, uint32_t n1, uint32_t magic, uint32_t vmask) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const uint32_t qt = __umulhi(c, magic);
+    m |= 1u << ((c - qt * n1 - 1u) & 31u);
+    c = qt;
+  }
+  return m & vmask;
+}
+
+// gap(u) = min{m in 1..N : u < C[m-1]} (N+1 or more if none); C padded with 0xFFFFFFFF.
+__device__ __forceinline__ int gap_of(const uint32_t* __restrict__ cdf, int len, uint32_t u) {
+  int cnt = 0;
+  for (int s = len >> 1; s >= 1; s >>= 1)
+    if (cdf[cnt + s - 1] <= u) cnt += s;
+  if (cdf[cnt] <= u) cnt += 1;
+  return cnt + 1;
+}
+
+// lanes-of-32-envs bit mask of (u < c), u = digits dig[0..B) MSB first (B = prob_bits).
+// From the least significant digit up: lt' = c_d ? (u_d ? lt : 1) : (u_d ? 0 : lt),
+// one v_bitop3_b32 per digit over (u_d, lt, C_d) with LUT 0x8E.
+__device__ __forceinline__ uint32_t less_than(const uint32_t (&dig)[16], uint32_t c, int B) {
+  uint32_t lt = 0;
+#pragma unroll
+  for (int d = 15; d >= 0; --d) {
+    if (d < B) {
+      const uint32_t C = (uint32_t)__builtin_amdgcn_sbfe((int)c, B - 1 - d, 1);
+      lt = __builtin_amdgcn_bitop3_b32(dig[d], lt, C, 0x8E);
+    }
+  }
+  return lt;
+}
+
+// less_than with the threshold's digit masks read from LDS: cmq[d * stride] = ~0 if bit
+// (B-1-d) of the threshold is set, else 0 (built once per block; saves a v_bfe per digit)
+template <int B>
+__device__ __forceinline__ uint32_t less_than_cm(const uint32_t (&dig)[16], const uint32_t* __restrict__ cmq,
+                                                 int stride) {
+  uint32_t lt = 0;
+#pragma unroll
+  for (int d = 15; d >= 0; --d) {
+    if (d < B) lt = __builtin_amdgcn_bitop3_b32(dig[d], lt, cmq[d * stride], 0x8E);
+  }
+  return lt;
+}
+
+// ------------------------------------------- step kernel, one wave per 32-env group
+//
+// Lane j of the wave is env j (lanes 0-31) for the per-env work and node j (+32r) for
+// the node work.  Blocks of kWavesPerBlock waves share one LDS copy of the tables; all
+// global loads are issued before the Philox batch so their latency hides under it.
+//   1. Philox: the lower half computes each env's ENV call and the first half of
+//      its node's selection calls, the upper half the other selection calls plus
+//      each env's first continuation-gap call; results meet via lane swaps;
+//   2. per env (lower lanes): interventions, perturbation (gap = linear count
+//      against the CDF in SGPRs for N <= 32), reset word;
+//   3. 32x32 bit transposes as 5-stage cross-lane butterflies on DPP
+//      (quad_perm, row_ror) and v_permlane16_swap: lane p ends up holding plane p;
+//   4. lane i evaluates node i; selection digits stay in its registers;
+//   5. butterfly back to per-env words, reward/termination/autoreset, stores.
+
+// y = a of lane ^ J (J in 1, 2, 4, 8, 16), within 32-lane halves, without LDS
+// ~0 on lanes with bit J of the lane index set, else 0 (a VGPR value: selecting with it
+// needs no exec mask or SGPR pair, which the step loops cannot spare)
+template <int J>
+__device__ __forceinline__ uint32_t lane_bit_mask(int lane) {
+  return 0u - (uint32_t)((lane & J) != 0);
+}
+
+// (every lane's DPP source is inside its row for these controls, so each lane is written and
+// the "old" operand is never used: mov_dpp leaves it undefined, which saves the v_mov that
+// update_dpp(0, ...) spends initialising the destination)
+template <int J>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t a, int lane) {
+  if constexpr (J == 1) {
+    return __builtin_amdgcn_mov_dpp(a, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
+  } else if constexpr (J == 2) {
+    return __builtin_amdgcn_mov_dpp(a, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
+  } else if constexpr (J == 4) {
+    const uint32_t r4 = __builtin_amdgcn_mov_dpp(a, 0x124, 0xF, 0xF, true);   // row_ror:4
+    const uint32_t r12 = __builtin_amdgcn_mov_dpp(a, 0x12C, 0xF, 0xF, true);  // row_ror:12
+    return pbn::bfi3(lane_bit_mask<4>(lane), r4, r12);
+  } else if constexpr (J == 8) {
+    return __builtin_amdgcn_mov_dpp(a, 0x128, 0xF, 0xF, true);  // row_ror:8
+  } else {
+    const auto r = __builtin_amdgcn_permlane16_swap(a, a, false, false);
+    return pbn::bfi3(lane_bit_mask<16>(lane), r[0], r[1]);
+  }
+}
+
+// one butterfly stage: lanes without bit J keep their M bits and take the partner's M bits
+// shifted up by J; lanes with bit J take the partner's ~M bits shifted down.  Branch-free: the
+// shift is a per-lane rotate (v_alignbit_b32; wrapped bits land outside the kept field) and
+// the field a per-lane mask.
+template <int J>
+__device__ __forceinline__ uint32_t transpose_step(uint32_t a, int lane) {
+  constexpr uint32_t M = J == 16 ? 0x0000FFFFu : (J == 8 ? 0x00FF00FFu : (J == 4 ? 0x0F0F0F0Fu : (J == 2 ? 0x33333333u : 0x55555555u)));
+  const uint32_t y = xor_lane<J>(a, lane);
+  const uint32_t up = lane_bit_mask<J>(lane);
+  const uint32_t rot = __builtin_amdgcn_alignbit(y, y, (32u - J) ^ (up & ((32u - J) ^ (uint32_t)J)));
+  return pbn::bfi3(M ^ ~up, rot, a);
+}
+
+// the partner value of lane ^ J within 32-lane halves through the LDS crossbar (ds_swizzle,
+// bit mode: and 0x1F, xor J): no VALU issue slot, where DPP cannot cross rows of 16 lanes
+template <int J>
+__device__ __forceinline__ uint32_t swizzle_xor(uint32_t a) {
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)a, (J << 10) | 0x1F);
+}
+
+// byte-granular stages (J = 16, 8) as one v_perm_b32 with a per-lane selector: the shift and
+// the field select of transpose_step in one instruction.  perm(y, a, sel): bytes 0-3 are a's,
+// 4-7 the partner's.
+//   J = 16: low lanes [a0 a1 y0 y1], high lanes [y2 y3 a2 a3]
+//   J = 8:  low lanes [a0 y0 a2 y2], high lanes [y1 a1 y3 a3]
+template <int J>
+__device__ __forceinline__ uint32_t perm_sel(int lane) {
+  if constexpr (J == 16) return (lane & 16) ? 0x03020706u : 0x05040100u;
+  else return (lane & 8) ? 0x03070105u : 0x06020400u;
+}
+
+// lane k holds row k of a 32x32 bit matrix (per 32-lane half); afterwards lane c holds column c.
+// 11 VALU (J = 16: swizzle + perm; 8: DPP + perm; 4: swizzle + alignbit + bitop3; 2, 1: DPP +
+// alignbit + bitop3) where five transpose_step spend 20.
+__device__ __forceinline__ uint32_t lane_transpose32(uint32_t a, int lane) {
+  a = __builtin_amdgcn_perm(swizzle_xor<16>(a), a, perm_sel<16>(lane));
+  a = __builtin_amdgcn_perm(xor_lane<8>(a, lane), a, perm_sel<8>(lane));
+  {
+    const uint32_t y = swizzle_xor<4>(a);
+    const uint32_t up = lane_bit_mask<4>(lane);
+    const uint32_t rot = __builtin_amdgcn_alignbit(y, y, 28u ^ (up & (28u ^ 4u)));
+    a = pbn::bfi3(0x0F0F0F0Fu ^ ~up, rot, a);
+  }
+  a = transpose_step<2>(a, lane);
+  a = transpose_step<1>(a, lane);
+  return a;
+}
+
+// eval of a lane-varying function from its compact record: 4 input planes, 16-bit
+// truth table T; leaf masks are sign-extended table bits (v_bfe_i32).
+__device__ __forceinline__ uint32_t eval_compact(uint32_t ins, uint32_t T, const uint32_t* __restrict__ S) {
+  const uint32_t x0 = S[ins & 0xFFu], x1 = S[(ins >> 8) & 0xFFu], x2 = S[(ins >> 16) & 0xFFu], x3 = S[ins >> 24];
+  uint32_t v[8];
+#pragma unroll
+  for (int mm = 0; mm < 8; ++mm) {
+    const uint32_t l0 = (uint32_t)__builtin_amdgcn_sbfe((int)T, 2 * mm, 1);
+    const uint32_t l1 = (uint32_t)__builtin_amdgcn_sbfe((int)T, 2 * mm + 1, 1);
+    v[mm] = bfi(x0, l1, l0);
+  }
+  const uint32_t w0 = bfi(x1, v[1], v[0]), w1 = bfi(x1, v[3], v[2]), w2 = bfi(x1, v[5], v[4]), w3 = bfi(x1, v[7], v[6]);
+  return bfi(x3, bfi(x2, w3, w2), bfi(x2, w1, w0));
+}
+
+// eval from per-lane leaf selectors: leaf m = (T bit 2m, T bit 2m+1) = (value at x0 = 0,
+// value at x0 = 1) is one of {0, x0, ~x0, ~0}, i.e. per byte one v_perm_b32 of {~x0 : x0}
+// with selector byte j, 4 + j, 12 (0x00) or 13 (0xFF); the selectors are built on the host.
+__device__ __forceinline__ uint32_t eval_sel(uint32_t ins, uint4 sa, uint4 sb, const uint32_t* __restrict__ S) {
+  const uint32_t x0 = S[ins & 0xFFu], x1 = S[(ins >> 8) & 0xFFu], x2 = S[(ins >> 16) & 0xFFu], x3 = S[ins >> 24];
+  const uint32_t nx0 = ~x0;
+  const uint32_t v0 = __builtin_amdgcn_perm(nx0, x0, sa.x), v1 = __builtin_amdgcn_perm(nx0, x0, sa.y);
+  const uint32_t v2 = __builtin_amdgcn_perm(nx0, x0, sa.z), v3 = __builtin_amdgcn_perm(nx0, x0, sa.w);
+  const uint32_t v4 = __builtin_amdgcn_perm(nx0, x0, sb.x), v5 = __builtin_amdgcn_perm(nx0, x0, sb.y);
+  const uint32_t v6 = __builtin_amdgcn_perm(nx0, x0, sb.z), v7 = __builtin_amdgcn_perm(nx0, x0, sb.w);
+  const uint32_t w0 = bfi(x1, v1, v0), w1 = bfi(x1, v3, v2), w2 = bfi(x1, v5, v4), w3 = bfi(x1, v7, v6);
+  return bfi(x3, bfi(x2, w3, w2), bfi(x2, w1, w0));
+}
+
+// eval_sel with the four input planes already read
+__device__ __forceinline__ uint32_t eval_sel_in(const uint32_t (&x)[4], uint4 sa, uint4 sb) {
+  const uint32_t x0 = x[0], nx0 = ~x0;
+  const uint32_t v0 = __builtin_amdgcn_perm(nx0, x0, sa.x), v1 = __builtin_amdgcn_perm(nx0, x0, sa.y);
+  const uint32_t v2 = __builtin_amdgcn_perm(nx0, x0, sa.z), v3 = __builtin_amdgcn_perm(nx0, x0, sa.w);
+  const uint32_t v4 = __builtin_amdgcn_perm(nx0, x0, sb.x), v5 = __builtin_amdgcn_perm(nx0, x0, sb.y);
+  const uint32_t v6 = __builtin_amdgcn_perm(nx0, x0, sb.z), v7 = __builtin_amdgcn_perm(nx0, x0, sb.w);
+  const uint32_t w0 = bfi(x[1], v1, v0), w1 = bfi(x[1], v3, v2), w2 = bfi(x[1], v5, v4), w3 = bfi(x[1], v7, v6);
+  return bfi(x[3], bfi(x[2], w3, w2), bfi(x[2], w1, w0));
+}
+
+// gap(u) = min{m : u < C[m-1]} from a float estimate of log(1-x)/log(1-p) corrected
+// exactly (+-1) against the integer CDF in LDS; C padded with 0xFFFFFFFF.
+__device__ __forceinline__ int gap_est(const uint32_t* __restrict__ cdf, int len, float inv_log2q, uint32_t u) {
+  const float x = (float)u * 2.3283064365386963e-10f;   // u / 2^32
+  const float l2 = __builtin_amdgcn_logf(1.0f - x);     // v_log_f32: log2
+  float est = floorf(l2 * inv_log2q) + 1.0f;
+  est = fminf(fmaxf(est, 1.0f), (float)len);
+  int g = (int)est;
+  // C[g-2] and C[g-1] as one pair of adjacent reads (no branch: g == 1 reads C[0], C[1])
+  const int base = g >= 2 ? g - 2 : 0;
+  const uint32_t c0 = cdf[base], c1 = cdf[base + 1];
+  const uint32_t hi = g >= 2 ? c1 : c0;                 // C[g-1]
+  const uint32_t lo = g >= 2 ? c0 : 0u;                 // C[g-2]
+  g += (u >= hi) ? 1 : 0;
+  g -= (g >= 2 && u < lo) ? 1 : 0;
+  return g;
+}
+
+// gap(u) from the bucket table: within a bucket of u (its top bits) the gap takes at most two
+// values, lo and lo + 1, split at threshold C[lo-1]; buckets from C[N-1] on share one sentinel
+// entry (gap N+1, no flip).  One LDS read and two VALU ops, where gap_est spends ~22.
+__device__ __forceinline__ int gap_lut(const uint2* __restrict__ lut, int shift, int nb, uint32_t u) {
+  const uint32_t b = min(u >> shift, (uint32_t)nb);
+  const uint2 e = lut[b];
+  return (int)e.y + (u >= e.x ? 1 : 0);
+}
+
+// one gap by the net's method (mode: 0 estimate, 1 binary search, 2 bucket table)
+__device__ __forceinline__ int gap_any(int mode, const uint32_t* __restrict__ L, const StepArgs& a, uint32_t u) {
+  if (mode == 2) return gap_lut(reinterpret_cast<const uint2*>(L + a.gap_lut_off), a.gap_shift, a.gap_nb, u);
+  return mode ? gap_of(L, a.cdf_len, u) : gap_est(L, a.cdf_len, a.inv_log2q, u);
+}
+
+// (u < c_q) for the wave-uniform threshold classes: one bit-sliced comparison per class with
+// SGPR digit masks, then a per-lane pick by class index (record .y)
+template <int B>
+__device__ __forceinline__ void class_masks(const uint32_t (&dig)[16], const uint32_t (&uthr)[kNodeRecs], int n_cls,
+                                            uint32_t (&ltc)[kNodeRecs]) {
+#pragma unroll
+  for (int v = 0; v < kNodeRecs; ++v) {
+    ltc[v] = 0;
+    if (v < n_cls) {
+      uint32_t c = uthr[v];
+      asm volatile("" : "+s"(c));   // digits re-extracted per step on the SALU (hoisted: SGPR spills)
+      ltc[v] = less_than(dig, c, B);
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t pick_class(const uint32_t (&ltc)[kNodeRecs], uint32_t cls) {
+  return cls == 0 ? ltc[0] : (cls == 1 ? ltc[1] : (cls == 2 ? ltc[2] : ltc[3]));
+}
+
+// Lower lanes receive the upper lanes' four words (upper lanes end with junk): per pair of
+// words two v_permlane32_swap and no copies.  swap(X, Y) moves X's upper half into Y's
+// lower half; swap(Y', X') then moves Y's upper half into X''s lower half.
+__device__ __forceinline__ pbn::Word4 upper_to_lower(pbn::Word4 v) {
+  const auto a1 = __builtin_amdgcn_permlane32_swap(v.x, v.y, false, false);
+  const auto a2 = __builtin_amdgcn_permlane32_swap(a1[1], a1[0], false, false);
+  const auto b1 = __builtin_amdgcn_permlane32_swap(v.z, v.w, false, false);
+  const auto b2 = __builtin_amdgcn_permlane32_swap(b1[1], b1[0], false, false);
+  return pbn::Word4{a2[0], a2[1], b2[0], b2[1]};
+}
+
+template <int W>
+__device__ __forceinline__ void set_bit(uint32_t (&g)[W], int pos, int N) {
+#pragma unroll
+  for (int w = 0; w < W; ++w)
+    if ((unsigned)pos < (unsigned)N && (pos >> 5) == w) g[w] |= 1u << (pos & 31);
+}
+
+// attractor id of the per-env state sp (open-addressing LDS hash; keys are unique, so the probe
+// order does not matter: the first four probes are read side by side), or -1
+template <int W>
+__device__ __forceinline__ int attractor_lookup(const StepArgs& a, const uint32_t* __restrict__ htab,
+                                                const uint32_t (&sp)[W]) {
+  int att = -1;
+  if (a.hash_bits > 0) {
+    const uint32_t hmask = (1u << a.hash_bits) - 1u;
+    uint32_t h = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) h += sp[w] * a.hash_mult[w];
+    h >>= (32 - a.hash_bits);
+#pragma unroll
+    for (int pr = 0; pr < 4; ++pr) {
+      const int id = hash_probe<W>(htab, (h + pr) & hmask, sp);
+      if (pr < a.hash_probes && id >= 0) att = id;
+    }
+    for (int pr = 4; pr < a.hash_probes; ++pr) {
+      const int id = hash_probe<W>(htab, (h + pr) & hmask, sp);
+      if (id >= 0) att = id;
+    }
+  }
+  return att;
+}
+
+// combinational gates of the lowered wide functions (lowering.py), level by level, all 64 lanes:
+// gate record {input S indices, 16-bit table, output S index}; one wave's LDS operations execute
+// in order, so level l + 1 reads what level l wrote
+__device__ __forceinline__ void eval_gate_levels(const StepArgs& a, const uint32_t* __restrict__ L, uint32_t* S,
+                                                 int lane) {
+  const uint4* grec = reinterpret_cast<const uint4*>(L + a.gate_off);
+  const int32_t* glev = reinterpret_cast<const int32_t*>(L + a.glayer_off);
+  for (int lv = 0; lv < a.n_glayers; ++lv) {
+    const int end = glev[lv + 1];
+    for (int gi = glev[lv] + lane; gi < end; gi += 64) {
+      const uint4 r = grec[gi];
+      S[r.z] = eval_compact(r.x, r.y, S);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// node l32 + 32r on lane l32: the rule update of every env of the group from the bit-sliced
+// planes S, the selection digit planes dig (perturbed envs are replaced by the caller)
+template <int W, int B>
+__device__ __forceinline__ void node_update(const StepArgs& a, const uint4 (&rec_)[W][kNodeRecs],
+                                            const uint4* __restrict__ selq, const uint32_t* __restrict__ S,
+                                            const uint32_t (&dig)[W][16], bool lo, int l32, uint32_t (&X)[W]) {
+  const int N = a.n_nodes;
+#pragma unroll
+  for (int r = 0; r < W; ++r) {
+    X[r] = 0;
+    const int i = l32 + 32 * r;
+    const int ii = lo && i < N ? i : 0;   // other lanes evaluate node 0 and discard it
+    uint32_t x = 0;
+    if (a.n_cls > 0 && a.max_nf <= kNodeRecs) {
+      // thresholds from a few wave-uniform classes (all kaban networks: 1/3, 2/3)
+      const int nf = (int)rec_[r][0].w;
+      uint32_t ltc[kNodeRecs];
+      class_masks<B>(dig[r], a.uthr, a.n_cls, ltc);
+#pragma unroll
+      for (int q = kNodeRecs - 1; q >= 0; --q) {
+        if (q < a.max_nf) {
+          const uint4 rc = rec_[r][q];
+          const uint32_t fj = eval_sel(rc.x, selq[(2 * q) * 32 * W + ii], selq[(2 * q + 1) * 32 * W + ii], S);
+          const uint32_t y = (q == nf - 1) ? fj : bfi(pick_class(ltc, rc.y), fj, x);
+          x = (q < nf) ? y : x;
+        }
+      }
+    } else {
+      const int nf = (int)rec_[r][0].w;
+      const int f0 = (int)rec_[r][1].w;
+      // selection chain from the last function down: x = F_{nf-1}; x = lt_j ? F_j : x
+      for (int j = nf - 1; j >= kNodeRecs; --j) {   // nodes with more than kNodeRecs functions (slow path)
+        const uint4 rc = a.fcompact[CK(f0 + j, a.n_funcs, 9)];
+        const uint32_t fj = eval_compact(rc.x, rc.y, S);
+        x = (j == nf - 1) ? fj : bfi(less_than(dig[r], rc.z, B), fj, x);
+      }
+#pragma unroll
+      for (int q = kNodeRecs - 1; q >= 0; --q) {
+        if (q < nf) {
+          const uint4 rc = rec_[r][q];
+          const uint32_t fj = eval_sel(rc.x, selq[(2 * q) * 32 * W + ii], selq[(2 * q + 1) * 32 * W + ii], S);
+          x = (q == nf - 1) ? fj : bfi(less_than(dig[r], rc.z, B), fj, x);
+        }
+      }
+    }
+    if (lo && i < N) X[r] = x;
+  }
+}
+
+// The settle law (settle_max >= 2, include/pbn_env.h "Step law"): updates k = 1 ..
+// settle_max - 1 of the envs (lower lanes) whose state sp is outside every attractor, until all
+// of the wave's envs are in one.  Update k: perturbation gaps j = 0, 1, ... from SETTLE_ENV call
+// ((k-1) << 8 | j >> 2), word j & 3 (per env); unperturbed envs take the rule update with the
+// group's SETTLE_SEL digit planes of update k (call idx (k-1) << 9 | 4i + c).  Every lane
+// computes the digit calls of its node (the upper half repeats the lower's: settle updates are
+// off the one-update hot path).  Returns true on lanes whose env is still outside after the
+// last update (PBN_FLAG_UNSETTLED).
+template <int W, int B>
+__device__ __forceinline__ bool settle_updates(const StepArgs& a, const uint32_t* __restrict__ L, uint32_t* S,
+                                            const uint4 (&rec_)[W][kNodeRecs], int lane, uint32_t ge_lo,
+                                            uint32_t ge_hi, uint32_t G_lo, uint32_t G_hi, uint32_t st_lo,
+                                            uint32_t (&sp)[W], int& att, bool& pert) {
+  constexpr int CPN = B / 4;
+  const bool lo = lane < 32;
+  const int l32 = lane & 31;
+  const int N = a.n_nodes;
+  const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+  const uint4* selq = reinterpret_cast<const uint4*>(L + a.sel_off);
+  const uint32_t* htab = L + a.cdf_len + 4 * (N + 1);
+  bool open = lo && att < 0;
+  for (int k = 1; k < a.settle_max; ++k) {
+    if (__ballot(open) == 0) return false;
+    const uint32_t sub = (uint32_t)(k - 1);
+    uint32_t dig[W][16];
+#pragma unroll
+    for (int r = 0; r < W; ++r) {
+#pragma unroll
+      for (int c = 0; c < CPN; ++c) {
+        const Word4 d = pbn::philox(G_lo, st_lo, (pbn::kStreamSettleSel << 28) | (sub << 9) |
+                                                     (uint32_t)(4 * (l32 + 32 * r) + c), G_hi, k0, k1);
+        dig[r][4 * c + 0] = d.x; dig[r][4 * c + 1] = d.y; dig[r][4 * c + 2] = d.z; dig[r][4 * c + 3] = d.w;
+      }
+    }
+    uint32_t gam[W];
+    bool pk = false;
+#pragma unroll
+    for (int w = 0; w < W; ++w) gam[w] = 0;
+    if (open) {
+      Word4 P = {0, 0, 0, 0};
+      int pos = -1;
+      for (int j = 0; pos < N - 1; ++j) {
+        if ((j & 3) == 0)
+          P = pbn::philox(ge_lo, st_lo, (pbn::kStreamSettleEnv << 28) | (sub << 8) | (uint32_t)(j >> 2), ge_hi, k0, k1);
+        const int j4 = j & 3;
+        const uint32_t u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
+        pos += gap_any(a.gap_exact, L, a, u);
+        set_bit<W>(gam, pos, N);
+      }
+#pragma unroll
+      for (int w = 0; w < W; ++w) pk = pk || gam[w] != 0;
+    }
+    // bit-slice sp (every lane takes part in the cross-lane transposes)
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      const uint32_t pl = lane_transpose32(sp[w], lane);
+      if (lo) S[32 * w + l32] = pl;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (a.n_glayers > 0) eval_gate_levels(a, L, S, lane);
+    uint32_t X[W], x[W];
+    node_update<W, B>(a, rec_, selq, S, dig, lo, l32, X);
+#pragma unroll
+    for (int w = 0; w < W; ++w) x[w] = lane_transpose32(X[w], lane);
+    if (open) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) sp[w] = pk ? sp[w] ^ gam[w] : x[w];
+      pert = pert || pk;
+      att = attractor_lookup<W>(a, htab, sp);
+      open = att < 0;
+    }
+  }
+  return open;
+}
+
+// VARIANT 1: exactly one step (pbn_step; no loop, lowest VGPR count);
+// 2: rollout with invariants recomputed per step (occupancy first; the rollout of networks
+//    with gates, which the pipelined kernel does not run);
+// 3, 4: 1 and 2 under the settle law (settle_max >= 2: settle_updates after the first update).
+template <int W, int B, int VARIANT>
+__global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a) {
+  constexpr bool LEAN = VARIANT == 2 || VARIANT == 4;
+  constexpr bool SINGLE = VARIANT == 1 || VARIANT == 3;
+  constexpr bool SETTLE = VARIANT >= 3;
+  constexpr int CPN = B / 4;               // selection calls per node
+  constexpr int H = (CPN + 1) / 2;         // of which the lower half computes H
+  constexpr int NLO = 1 + W * H;           // lower list: ENV, SEL(c < H)
+  constexpr int NUP = W * (CPN - H);       // upper list: SEL(c >= H)
+  constexpr int IT = NLO > NUP ? NLO : NUP;
+  constexpr int UPC = (CPN - H) > 0 ? (CPN - H) : 1;  // divisor guard (B = 4: no upper calls)
+  extern __shared__ uint32_t smem[];
+  PBN_STAMP(0);
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int64_t g = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  const int N = a.n_nodes;
+  // LDS: the block's table image [cdf | reward | hash | attractors | leaf selectors], then
+  // each wave's S planes
+  uint32_t* L = smem;
+  uint32_t* S = smem + a.tab_words + (size_t)wv * a.wave_words;
+  const uint32_t* cdf = L;
+  const float* rtab = reinterpret_cast<const float*>(L + a.cdf_len);
+  const uint32_t* htab = L + a.cdf_len + 4 * (N + 1);
+  const int64_t n = a.n_envs;
+  const bool lo = lane < 32;
+  const int l32 = lane & 31;
+  const int64_t le = g * 32 + l32;
+  const uint64_t ge = a.env_offset + (uint64_t)le;
+  const uint64_t G = ge >> 5;
+  const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+  const bool random_actions = (a.mode & PBN_MODE_RANDOM_ACTIONS) != 0;
+  const size_t plane = (size_t)W * n;   // words per step of a [steps][W][n] output
+
+  // ---- 0. issue the one-time global loads: env state, node records, tables
+  uint32_t st[W];      // current observation s of env l32 (lower lanes), carried across steps
+  uint32_t tt0 = 0, tg0 = 0;
+#pragma unroll
+  for (int w = 0; w < W; ++w) st[w] = 0;
+  if (lo && g < a.n_groups) {   // (waves past the end only help copy the tables)
+#pragma unroll
+    for (int w = 0; w < W; ++w) st[w] = a.state[CK((size_t)w * n + le, plane, 1)] & valid_word_mask(N, w);
+    tt0 = a.t[CK(le, n, 2)];
+    tg0 = a.target[CK(le, n, 3)];
+  }
+  // node l32 + 32r: its first kNodeRecs compact records {inputs, table, threshold, meta}
+  // (node-major, fixed stride: no dependent load); meta of record 0 = nf, of record 1 = f0
+  uint4 rec_[W][kNodeRecs];
+#pragma unroll
+  for (int r = 0; r < W; ++r) {
+    const int i = l32 + 32 * r;
+    const int ic = i < N ? i : 0;
+#pragma unroll
+    for (int q = 0; q < kNodeRecs; ++q) rec_[r][q] = a.nrec[CK((size_t)ic * kNodeRecs + q, N * kNodeRecs, 4)];
+  }
+  copy_image(L, a);
+  __syncthreads();   // the kernel's only block barrier
+  if (g >= a.n_groups) return;  // whole wave
+  const uint4* selq = reinterpret_cast<const uint4*>(L + a.sel_off);
+
+  const int n_steps = SINGLE ? 1 : a.n_steps;
+  // Random-action mode issues no global load inside the step loop (attractor tables live in
+  // LDS), so stores never have to drain (vmcnt retires in issue order).  A given flip mask
+  // is loaded and consumed inside its own branch, so the wait for it stays on that path.
+  for (int ks = 0; ks < n_steps; ++ks) {
+  if constexpr (LEAN) {
+    // keep loop-invariant expansions (leaf masks, threshold digits, key schedule, first-round
+    // products) inside the loop so VGPRs stay low and occupancy high
+#pragma unroll
+    for (int r = 0; r < W; ++r) {
+#pragma unroll
+      for (int q = 0; q < kNodeRecs; ++q) {
+        asm volatile("" : "+v"(rec_[r][q].x), "+v"(rec_[r][q].z));
+      }
+    }
+  }
+  const uint32_t kk0 = k0, kk1 = k1, ge_lo = (uint32_t)ge, G_lo = (uint32_t)G;
+  uint64_t step = a.step + (uint64_t)ks;
+  if constexpr (SINGLE) {
+    if (a.step_ptr) step = *a.step_ptr;   // graph-replayable single step (pbn_step_dev)
+  }
+  const uint32_t st_lo = (uint32_t)step;
+  const uint32_t st_hi = (uint32_t)((step >> 32) & 0xFFFFu) << 16;
+  const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | st_hi;
+  const uint32_t G_hi = (uint32_t)((G >> 32) & 0xFFFFu) | st_hi;
+  uint32_t m[W], s1[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) { m[w] = 0; s1[w] = st[w]; }
+  if (lo && a.obs) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) a.obs[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 7)] = st[w];
+  }
+
+  // ---- 1. all Philox calls of the group, two half-wave work lists
+  PBN_STAMP(1);
+  Word4 out[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    uint32_t lc0, lc2, lc3, uc0, uc2, uc3;
+    if (it == 0) {
+      lc0 = ge_lo; lc2 = pbn::kStreamEnv << 28; lc3 = ge_hi;
+    } else {
+      const int idx = it - 1;
+      const int r = (idx / H) < W ? idx / H : W - 1;
+      const int c = idx % H;
+      lc0 = G_lo; lc2 = (pbn::kStreamSel << 28) | (uint32_t)(4 * (l32 + 32 * r) + c); lc3 = G_hi;
+    }
+    if (it < W * (CPN - H)) {
+      const int r = it / UPC;
+      const int c = H + it % UPC;
+      uc0 = G_lo; uc2 = (pbn::kStreamSel << 28) | (uint32_t)(4 * (l32 + 32 * r) + c); uc3 = G_hi;
+    } else {   // (upper list done: a discarded call)
+      uc0 = ge_lo; uc2 = pbn::kStreamEnv << 28; uc3 = ge_hi;
+    }
+    out[it] = pbn::philox(lo ? lc0 : uc0, st_lo, lo ? lc2 : uc2, lo ? lc3 : uc3, kk0, kk1);
+  }
+  // digits of node l32 + 32r: calls c < H from this lane, c >= H from lane + 32
+  uint32_t dig[W][16];
+#pragma unroll
+  for (int r = 0; r < W; ++r) {
+#pragma unroll
+    for (int c = 0; c < CPN; ++c) {
+      const Word4 d = c < H ? out[(1 + r * H + c) < IT ? (1 + r * H + c) : 0]
+                            : upper_to_lower(out[r * (CPN - H) + (c - H)]);
+      dig[r][4 * c + 0] = d.x; dig[r][4 * c + 1] = d.y; dig[r][4 * c + 2] = d.z; dig[r][4 * c + 3] = d.w;
+    }
+  }
+  const Word4 E = out[0];
+
+  // ---- 2. per env (lower lanes): interventions, perturbation, reset word
+  PBN_STAMP(2);
+  uint32_t gam[W];
+  uint32_t pc = 0;
+  bool pert = false;
+#pragma unroll
+  for (int w = 0; w < W; ++w) gam[w] = 0;
+  // ENV words 3:2 = a 64-bit uniform X: the action draw (every mode), the autoreset draws,
+  // then gap 2's uniform u2 = what remains of X's top word (DESIGN.md "Step semantics")
+  uint32_t r_row = 0, r_nt = 0, u2 = 0;
+  if (lo) {
+    uint32_t xhi = E.w, xlo = E.z;
+    const uint32_t n1 = (uint32_t)(N + 1);
+    const uint32_t c_act = ext64(xhi, xlo, n1 * n1 * n1);
+    if (a.n_attr >= 1) {
+      const int32_t* att_first = reinterpret_cast<const int32_t*>(L + a.att_off);
+      const uint32_t A = (uint32_t)a.n_attr;
+      uint32_t as = 0;
+      if (A >= 2) {
+        const uint32_t c = ext64(xhi, xlo, A * (A - 1));
+        as = a.am1_magic ? __umulhi(c, a.am1_magic) : c;   // c / (A - 1)
+        r_nt = c - as * (A - 1);
+        r_nt += (r_nt >= as) ? 1u : 0u;
+      }
+      // (single-state attractors: the draw over one state is 0 and state a is attractor a's)
+      const int st0 = a.att_single ? (int)as : att_first[as];
+      r_row = (uint32_t)st0 + (a.att_single ? 0u : ext64(xhi, xlo, (uint32_t)(att_first[as + 1] - st0)));
+    }
+    u2 = xhi;
+    if (random_actions) {
+      actions_from_draw<W>(c_act, N, a.n1_magic, m);
+#pragma unroll
+      for (int w = 0; w < W; ++w) a.flipmask[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 8)] = m[w];
+    } else {
+#pragma unroll
+      for (int w = 0; w < W; ++w)
+        m[w] = a.flipmask[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 6)] & valid_word_mask(N, w);
+    }
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      pc += __builtin_popcount(m[w]);
+      s1[w] ^= m[w];
+    }
+    // perturbation positions are prefix sums of geometric gaps; the first three gaps
+    // (u = E.x, E.y, u2) are independent, so they are computed side by side
+    int g0, g1, g2;
+    if (a.gap_exact == 2) {
+      g0 = gap_any(2, L, a, E.x); g1 = gap_any(2, L, a, E.y); g2 = gap_any(2, L, a, u2);
+    } else if (a.gap_exact) {
+      g0 = gap_of(cdf, a.cdf_len, E.x); g1 = gap_of(cdf, a.cdf_len, E.y); g2 = gap_of(cdf, a.cdf_len, u2);
+    } else {
+      g0 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.x);
+      g1 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.y);
+      g2 = gap_est(cdf, a.cdf_len, a.inv_log2q, u2);
+    }
+    const int p0 = g0 - 1, p1 = p0 + g1, p2 = p1 + g2;
+    set_bit<W>(gam, p0, N);
+    set_bit<W>(gam, p1, N);
+    set_bit<W>(gam, p2, N);
+    if (p2 < N - 1) {   // rare: a fourth flip is possible (gap k >= 3: PERT call (k-3)>>2, word (k-3)&3)
+      Word4 P = E;
+      int pos = p2;
+      for (int kk = 3; pos < N - 1; ++kk) {
+        if (((kk - 3) & 3) == 0)
+          P = pbn::philox(ge_lo, st_lo, (pbn::kStreamPert << 28) | (uint32_t)((kk - 3) >> 2), ge_hi, kk0, kk1);
+        const int j4 = (kk - 3) & 3;
+        const uint32_t u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
+        pos += gap_any(a.gap_exact, L, a, u);
+        set_bit<W>(gam, pos, N);
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < W; ++w) pert = pert || gam[w] != 0;
+  }
+
+  // ---- 3. bit-slice s1: lane p <- plane p (node p over the 32 envs), to LDS
+  PBN_STAMP(3);
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    const uint32_t sp = lane_transpose32(s1[w], lane);
+    if (lo) S[32 * w + l32] = sp;
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (a.n_glayers > 0) eval_gate_levels(a, L, S, lane);
+
+  // ---- 4. node l32 + 32r on lane l32: X = rule update of every env (perturbed envs are
+  // replaced after the back-transpose)
+  PBN_STAMP(4);
+  uint32_t X[W];
+  node_update<W, B>(a, rec_, selq, S, dig, lo, l32, X);
+
+  // ---- 5. back to per-env words, reward, termination, autoreset, stores
+  PBN_STAMP(5);
+  uint32_t sp[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) sp[w] = lane_transpose32(X[w], lane);
+  PBN_STAMP(6);
+  if (lo && pert) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) sp[w] = s1[w] ^ gam[w];
+  }
+  int att = lo ? attractor_lookup<W>(a, htab, sp) : 0;
+  bool unsettled = false;
+  if constexpr (SETTLE) {   // the whole wave (cross-lane transposes)
+    unsettled = settle_updates<W, B>(a, L, S, rec_, lane, ge_lo, ge_hi, G_lo, G_hi, st_lo, sp, att, pert);
+  }
+  if (lo) {
+  if (a.final_state) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) a.final_state[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 10)] = sp[w];
+  }
+  const bool in_attr = att >= 0;
+  const bool term = in_attr && (uint32_t)att == tg0;
+  const bool wrong = in_attr && !term;
+  int tt = (int)tt0 + 1;
+  tt = tt > 255 ? 255 : tt;
+  const bool trunc = a.horizon > 0 && tt >= a.horizon;
+  a.reward[CK(ks * n + le, n_steps * n, 11)] = rtab[(int)pc * 4 + 2 * (int)term + (int)wrong];
+  uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) | ((uint32_t)pert << 3) |
+                ((uint32_t)unsettled << 5);
+  if ((a.mode & PBN_MODE_AUTORESET) && (term || trunc)) {
+    uint32_t nt;
+    if (a.n_attr >= 1) {   // the attractor draws of step 2 (attractor states from the LDS image)
+      const uint32_t* att_words = L + a.att_off + a.n_attr + 1;
+#pragma unroll
+      for (int w = 0; w < W; ++w) sp[w] = att_words[(size_t)r_row * W + w];
+      nt = r_nt;
+    } else {
+      const Word4 rr = pbn::philox(ge_lo, st_lo, (pbn::kStreamReset << 28) | 1u, ge_hi, kk0, kk1);
+      const uint32_t rw4[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+      for (int w = 0; w < W; ++w) sp[w] = rw4[w] & valid_word_mask(N, w);
+      nt = PBN_NO_TARGET;
+    }
+    tg0 = nt;
+    tt = 0;
+    fl |= PBN_FLAG_RESET;
+  }
+  a.flags[CK(ks * n + le, n_steps * n, 15)] = (uint8_t)fl;
+  tt0 = (uint32_t)tt;
+#pragma unroll
+  for (int w = 0; w < W; ++w) st[w] = sp[w];
+  }  // lo
+  PBN_STAMP(7);
+  }  // steps
+
+  if (lo) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) a.state_out[CK((size_t)w * n + le, plane, 16)] = st[w];
+    a.t[CK(le, n, 17)] = (uint8_t)tt0;
+    a.target[CK(le, n, 18)] = (uint8_t)tg0;
+  }
+}
+
+
+// Block barrier ordering LDS only.  __syncthreads() is a workgroup fence on every address
+// space, so each wave would first wait (s_waitcnt vmcnt(0)) for its global stores -- the
+// per-step obs / reward / flags / flip-mask stores -- to complete.  The step loops
+// communicate through LDS alone and never read back what they store to HBM in the loop.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// ------------------------------- rollout kernel, three waves per pair of 32-env groups
+// Block = two groups (64 envs; lanes 32h..32h+31 of every wave work on group 2*block + h).
+// The step splits into work that depends only on the counter-based RNG and work that
+// depends on the state, so different waves run different steps:
+//   wave 1 (env draws): ENV + PERT call 0 of env `lane` -> actions / given flip mask,
+//     perturbation mask, autoreset draw;
+//   wave 2 (selection): SEL calls of node `lane & 31` -> the (u < c_j) masks of its thresholds;
+//   wave 0 (state): s1 = s ^ m, bit-slice, node evaluation from the masks, back-transpose,
+//     attractor lookup, reward, flags, autoreset, stores.
+// Iteration k: waves 1 and 2 produce step k into slot k&1 while wave 0 consumes step k-1
+// from the other slot; the block barrier ends the iteration.  Same results as pbn_step_wave.
+// Each wave alone is latency-bound, so the split (three instruction streams per group pair)
+// is what fills the SIMDs at small batches.
+
+// input plane k of a record's input word: byte k is a plane index, or with BY (the pipelined
+// kernel's LDS records for W <= 2) the plane's byte offset, so that the address is one add of
+// a byte field (v_add_u32 with an SDWA byte select) instead of extract + shift-add
+template <bool BY>
+__device__ __forceinline__ uint32_t plane_in(const uint32_t* __restrict__ S, uint32_t ins, int k) {
+  const uint32_t f = k == 3 ? ins >> 24 : (ins >> (8 * k)) & 0xFFu;
+  if constexpr (BY) return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(S) + f);
+  else return S[f];
+}
+
+// node chain from precomputed selection masks: x = F_{nf-1}; x = lt_j ? F_j : x, with every
+// LDS read of the K records issued before any use (K = wave-uniform bound, nf per lane)
+template <int K, bool BY>
+__device__ __forceinline__ uint32_t chain_from_masks(const uint4 (&rec)[kNodeRecs], const uint4* __restrict__ sel,
+                                                     int stride, const uint32_t* __restrict__ S,
+                                                     const uint32_t* __restrict__ lt, int lt_stride, int nf,
+                                                     bool tail, uint32_t x) {
+  uint32_t xin[K][4], ltv[K];
+  uint4 sa[K], sb[K];
+#pragma unroll
+  for (int q = 0; q < K; ++q) {
+    const uint32_t ins = rec[q].x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) xin[q][k] = plane_in<BY>(S, ins, k);
+    sa[q] = sel[(2 * q) * stride];
+    sb[q] = sel[(2 * q + 1) * stride];
+    // mask q exists for q < K - 1, and for q = K - 1 too when some node has more than K
+    // (= kNodeRecs) functions
+    ltv[q] = (q < K - 1 || tail) ? lt[q * lt_stride] : 0u;
+  }
+#pragma unroll
+  for (int q = K - 1; q >= 0; --q) {
+    const uint32_t x0 = xin[q][0], x1 = xin[q][1], x2 = xin[q][2], x3 = xin[q][3];
+    const uint32_t nx0 = ~x0;
+    const uint32_t v0 = __builtin_amdgcn_perm(nx0, x0, sa[q].x), v1 = __builtin_amdgcn_perm(nx0, x0, sa[q].y);
+    const uint32_t v2 = __builtin_amdgcn_perm(nx0, x0, sa[q].z), v3 = __builtin_amdgcn_perm(nx0, x0, sa[q].w);
+    const uint32_t v4 = __builtin_amdgcn_perm(nx0, x0, sb[q].x), v5 = __builtin_amdgcn_perm(nx0, x0, sb[q].y);
+    const uint32_t v6 = __builtin_amdgcn_perm(nx0, x0, sb[q].z), v7 = __builtin_amdgcn_perm(nx0, x0, sb[q].w);
+    const uint32_t w0 = bfi(x1, v1, v0), w1 = bfi(x1, v3, v2), w2 = bfi(x1, v5, v4), w3 = bfi(x1, v7, v6);
+    const uint32_t fj = bfi(x3, bfi(x2, w3, w2), bfi(x2, w1, w0));
+    const uint32_t y = (q == nf - 1) ? fj : bfi(ltv[q], fj, x);
+    x = (q < nf) ? y : x;
+  }
+  return x;
+}
+
+// chain over padded records (every node has max_nf <= kNodeRecs records, the last function
+// repeated; lanes past N have all-zero selectors and evaluate to 0): x = F_{K-1}; x = lt_q ? F_q
+// : x, with no per-lane function count
+template <int K, bool BY>
+__device__ __forceinline__ uint32_t chain_padded(const uint4* __restrict__ rec, const uint4* __restrict__ sel,
+                                                 int stride, const uint32_t* __restrict__ S,
+                                                 const uint32_t* __restrict__ lt, int lt_stride) {
+  uint32_t xin[K][4], ltv[K];
+  uint4 sa[K], sb[K];
+#pragma unroll
+  for (int q = 0; q < K; ++q) {
+    const uint32_t ins = rec[q * stride].x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) xin[q][k] = plane_in<BY>(S, ins, k);
+    sa[q] = sel[(2 * q) * stride];
+    sb[q] = sel[(2 * q + 1) * stride];
+    ltv[q] = q < K - 1 ? lt[q * lt_stride] : 0u;
+  }
+  uint32_t x = 0;
+#pragma unroll
+  for (int q = K - 1; q >= 0; --q) {
+    const uint32_t fj = eval_sel_in(xin[q], sa[q], sb[q]);
+    x = (q == K - 1) ? fj : bfi(ltv[q], fj, x);
+  }
+  return x;
+}
+
+// Waves per SIMD the register allocation must allow for single-word states: 6 (<= 80 VGPRs,
+// no spill in the step loops) runs 1M envs 10 % faster than the unconstrained 86 VGPRs (5 waves);
+// 7 and 8 spill to scratch in the state loop and lose (profiles/r02_ab_waves_per_eu.jsonl).
+// Three-word states (pbn70) are held to 3 waves (167 VGPRs, where the compiler's choice is 181:
+// 2 waves); two-word states fit 4 waves as they are.
+#define PBN_PIPE_ATTR __attribute__((amdgpu_waves_per_eu(W == 1 ? 6 : (W == 3 ? 3 : 1), 8)))
+template <int W, int B>
+__global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a) {
+  constexpr int CPN = B / 4;              // selection calls per node
+  extern __shared__ uint32_t smem[];
+  const int lane = threadIdx.x & 63;
+  const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar branches
+  // the state wave bounds every iteration: let it win VALU issue against the RNG waves of
+  // other blocks sharing its SIMD
+  PBN_RSTAMP(0);
+  if (role == 0) __builtin_amdgcn_s_setprio(kStatePrio);
+  // with one block per SIMD triple (every SIMD holds one wave of each role) the selection wave,
+  // the longest instruction stream, also goes ahead of the env-draw wave: -5 % per step at
+  // 65,536 envs; with more blocks resident it loses 4-8 % (profiles/r02_ab_wave_priority.jsonl)
+  if (role == 2 && a.sel_prio) __builtin_amdgcn_s_setprio(1);
+#ifdef PBN_STAMPS
+  // placement of this wave: HW_ID (wave, SIMD, CU, SH, SE) in the low word, XCC_ID above it
+  if (a.stamps && lane == 0)
+    a.stamps[(size_t)blockIdx.x * 16 + (role == 0 ? 14 : role * 4 + 3)] =
+        (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+        ((unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32);
+#endif
+  const int half = lane >> 5;
+  const int l32 = lane & 31;
+  const int64_t g = (int64_t)blockIdx.x * 2 + half;
+  const bool valid = g < a.n_groups;
+  const int N = a.n_nodes;
+  const int64_t n = a.n_envs;
+  const int64_t le = g * 32 + l32;
+  const uint64_t ge = a.env_offset + (uint64_t)le;
+  const uint64_t G = ge >> 5;
+  const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+  const bool random_actions = (a.mode & PBN_MODE_RANDOM_ACTIONS) != 0;
+  const size_t plane = (size_t)W * n;
+  const int n_steps = a.n_steps;
+  const int LQ = a.lq;
+  // LDS: table image | S planes [2][32W] | two slots
+  //   slot = m[W][64] | gam[W][64] | rs[W][64] | info[64] | lt[LQ][2][32W]
+  uint32_t* L = smem;
+  const uint32_t* cdf = L;
+  const float* rtab = reinterpret_cast<const float*>(L + a.cdf_len);
+  const uint32_t* htab = L + a.cdf_len + 4 * (N + 1);
+  const uint4* selq = reinterpret_cast<const uint4*>(L + a.sel_off);
+  uint32_t* Sg = smem + a.tab_words + half * 32 * W;   // this half's group
+  uint32_t* slots = smem + a.tab_words + 2 * 32 * W;
+  uint32_t st[W];
+  uint32_t tt0 = 0, tg0 = 0;
+#pragma unroll
+  for (int w = 0; w < W; ++w) st[w] = 0;
+  if (role == 0 && valid) {   // issued first: their latency overlaps the image copy
+#pragma unroll
+    for (int w = 0; w < W; ++w) st[w] = a.state[CK((size_t)w * n + le, plane, 1)];
+    tt0 = a.t[CK(le, n, 2)];
+    tg0 = a.target[CK(le, n, 3)];
+  }
+  copy_image(L, a);
+#pragma unroll
+  for (int w = 0; w < W; ++w) st[w] &= valid_word_mask(N, w);
+  // node records live in LDS (L + nrec_off), record-major [kNodeRecs][32W] so that a wave's
+  // lanes (nodes) read consecutive 16-byte records without bank conflicts: each role reads
+  // what it needs per step, so no record is carried in VGPRs across the step loop
+  const uint4* recL = reinterpret_cast<const uint4*>(L + a.nrec_off);
+  // wave-uniform parameters, re-defined (laundered) every iteration: hoisted out of the step
+  // loop, the conditions built from them occupy SGPR pairs and spill to VGPR lanes
+  uint32_t u_k0 = k0, u_k1 = k1;
+  int u_gx = a.gap_exact, u_na = a.n_attr,  u_mnf = a.max_nf, u_hb = a.hash_bits,
+      u_hp = a.hash_probes, u_hz = a.horizon;
+  uint32_t u_fl = __builtin_amdgcn_readfirstlane((a.obs ? 1u : 0u) | (a.final_state ? 2u : 0u) |
+                                                 (random_actions ? 4u : 0u) | ((a.mode & PBN_MODE_AUTORESET) ? 8u : 0u) |
+                                                 (a.att_single ? 16u : 0u));
+  // digit masks of the first kNodeRecs - 1 thresholds of every node, [q][d][32W], for the
+  // selection wave's compares, built from the LDS copy of the node records once it has
+  // landed (from the global records this was two dependent L2 round trips per entry, eight
+  // entries per thread: most of the launch's fixed cost)
+  // (single-word states only: for W > 1 the extra LDS costs more occupancy than it saves,
+  // measured -15 % on pbn70 x 1M)
+  uint32_t* cm = slots + 2 * (size_t)a.slot_words;
+  __syncthreads();
+  PBN_RSTAMP(1);
+  if constexpr (W == 1) {
+    // thread t: record (q, i) = p = t mod 96 and digits [h B/2, (h+1) B/2), h = t / 96 (192
+    // threads = two per record: two LDS reads, then B/2 independent writes)
+    static_assert((kNodeRecs - 1) * 32 * 2 == 192, "cm build assumes 192 threads");
+    {
+      const int p = (int)threadIdx.x % ((kNodeRecs - 1) * 32), h = (int)threadIdx.x / ((kNodeRecs - 1) * 32);
+      const int i = p & 31, q = p >> 5;
+      uint32_t c = 0;
+      if (i < N && q < (int)recL[i].w - 1) c = recL[q * 32 * W + i].z;
+#pragma unroll
+      for (int dd = 0; dd < B / 2; ++dd) {
+        const int d = h * (B / 2) + dd;
+        cm[(q * B + d) * 32 + i] = ((c >> (B - 1 - d)) & 1u) ? ~0u : 0u;
+      }
+    }
+    __syncthreads();
+  }
+  // drain the initial state loads here: otherwise the loop-carried st / t / target copies at
+  // the bottom of the loop wait on vmcnt(0), which also waits for every store of the step
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
+  PBN_RSTAMP(2);
+
+  // one loop per role: every wave passes the same n_steps + 1 block barriers, and each role's
+  // loop-carried values (hoisted invariants) occupy registers only in that role's loop
+  if (role == 1 && (u_fl & 4u) && u_gx == 2 && u_na >= 2 && (u_fl & 16u) && (W > 1 || N <= 31)) {
+    // env draws, common configuration (random actions, gap bucket table, two or more
+    // single-state attractors): the same draws as the general loop below, branch-free apart from
+    // the rare fourth-flip tail and the guarded flip-mask store, so that the next step's ENV call
+    // (computed here, one step ahead) interleaves with this step's dependent draws and LDS reads
+    // instead of following them
+    const uint32_t A = (uint32_t)u_na;
+    const uint32_t n1 = (uint32_t)(N + 1);
+    const uint32_t* att_words = L + a.att_off + u_na + 1;
+    const uint2* lut = reinterpret_cast<const uint2*>(L + a.gap_lut_off);
+    auto env_call = [&](int k) {
+      const uint64_t step = a.step + (uint64_t)k;
+      const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
+      return pbn::philox((uint32_t)ge, (uint32_t)step, pbn::kStreamEnv << 28, ge_hi, u_k0, u_k1);
+    };
+    // one step: this step's draws from E, the next step's ENV call into E_next
+    auto env_step = [&](int k, const Word4& E, Word4& E_next) {
+      asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
+      asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
+      PBN_PSTAMP(k, 0);
+      if (k < n_steps) {
+        uint32_t* slot = slots + (size_t)(k & 1) * a.slot_words;
+        // part 1: the draws that feed LDS reads, and the reads themselves
+        uint32_t xhi = E.w, xlo = E.z;
+        const uint32_t c_act = ext64(xhi, xlo, n1 * n1 * n1);
+        const uint32_t u2 = (uint32_t)((((((uint64_t)E.w) << 32) | E.z) * a.x_mult) >> 32);
+        const uint32_t c = ext64(xhi, xlo, A * (A - 1));
+        const uint32_t as = a.am1_magic ? __umulhi(c, a.am1_magic) : c;   // c / (A - 1)
+        uint32_t rs[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) rs[w] = att_words[(size_t)as * W + w];
+        const uint2 e0 = lut[min(E.x >> a.gap_shift, (uint32_t)a.gap_nb)];
+        const uint2 e1 = lut[min(E.y >> a.gap_shift, (uint32_t)a.gap_nb)];
+        const uint2 e2 = lut[min(u2 >> a.gap_shift, (uint32_t)a.gap_nb)];
+        // part 2: the next step's ENV call runs while those reads are in flight (the scheduling
+        // barriers keep the compiler from hoisting it above them or sinking it to the latch)
+        asm volatile("" ::: "memory");   // the LDS reads above are issued here
+        __builtin_amdgcn_sched_barrier(0);
+        E_next = env_call(k + 1);   // (one unused call per launch)
+        asm volatile("" : "+v"(E_next.x), "+v"(E_next.y), "+v"(E_next.z), "+v"(E_next.w));
+        __builtin_amdgcn_sched_barrier(0);
+        // part 3: the rest of step k's draws
+        uint32_t rt = c - as * (A - 1);
+        rt += (rt >= as) ? 1u : 0u;
+        uint32_t m[W], gam[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) { m[w] = 0; gam[w] = 0; }
+        if constexpr (W == 1) m[0] = actions_mask31(c_act, n1, a.n1_magic, valid_word_mask(N, 0));   // N <= 31
+        else actions_from_draw<W>(c_act, N, a.n1_magic, m);
+        uint32_t pc = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) pc += __builtin_popcount(m[w]);
+        const int g0 = (int)e0.y + (E.x >= e0.x ? 1 : 0);   // gap_lut
+        const int g1 = (int)e1.y + (E.y >= e1.x ? 1 : 0);
+        const int g2 = (int)e2.y + (u2 >= e2.x ? 1 : 0);
+        const int p0 = g0 - 1, p1 = p0 + g1, p2 = p1 + g2;
+        if constexpr (W == 1) {
+          // N <= 31: a position past the network lands on a bit >= N (bit 31 at most), cleared by
+          // the word mask once
+          gam[0] = ((1u << min((uint32_t)p0, 31u)) | (1u << min((uint32_t)p1, 31u)) |
+                    (1u << min((uint32_t)p2, 31u))) & valid_word_mask(N, 0);
+        } else {
+          set_bit<W>(gam, p0, N);
+          set_bit<W>(gam, p1, N);
+          set_bit<W>(gam, p2, N);
+        }
+        bool pert = false;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          pert = pert || gam[w] != 0;
+          slot[w * 64 + lane] = m[w];
+          slot[(W + w) * 64 + lane] = gam[w];
+          slot[(2 * W + w) * 64 + lane] = rs[w];
+        }
+        slot[3 * W * 64 + lane] = rt | (pc << 8) | ((uint32_t)pert << 16);
+        if (valid) {
+#pragma unroll
+          for (int w = 0; w < W; ++w) LANE_ST(a.flipmask, k * plane + (size_t)w * n, le, (size_t)n_steps * plane, 8, m[w]);
+        }
+        if (p2 < N - 1) {   // rare: a fourth flip is possible (gap k >= 3: PERT call (k-3)>>2, word (k-3)&3)
+          const uint64_t step = a.step + (uint64_t)k;
+          const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
+          Word4 P = E;
+          int pos = p2;
+          for (int kk = 3; pos < N - 1; ++kk) {
+            if (((kk - 3) & 3) == 0)
+              P = pbn::philox((uint32_t)ge, (uint32_t)step, (pbn::kStreamPert << 28) | (uint32_t)((kk - 3) >> 2), ge_hi, u_k0, u_k1);
+            const int j4 = (kk - 3) & 3;
+            const uint32_t u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
+            pos += gap_lut(lut, a.gap_shift, a.gap_nb, u);
+            set_bit<W>(gam, pos, N);
+          }
+          pert = false;
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            pert = pert || gam[w] != 0;
+            slot[(W + w) * 64 + lane] = gam[w];
+          }
+          slot[3 * W * 64 + lane] = rt | (pc << 8) | ((uint32_t)pert << 16);
+        }
+      }
+      PBN_PSTAMP(k, 1);
+      lds_barrier();
+    };
+    // two steps per trip with the ENV words alternating between EA and EB: no copies between steps
+    Word4 EA = env_call(0), EB = EA;
+    for (int k = 0; k <= n_steps; k += 2) {
+      env_step(k, EA, EB);
+      if (k + 1 <= n_steps) env_step(k + 1, EB, EA);
+    }
+  } else if (role == 1) {
+    for (int k = 0; k <= n_steps; ++k) {
+      asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
+      asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
+      PBN_PSTAMP(k, 0);
+      if (k < n_steps) {
+        // ---- env draws of step k, env `lane`
+        uint32_t* slot = slots + (size_t)(k & 1) * a.slot_words;
+        const uint64_t step = a.step + (uint64_t)k;
+        const uint32_t st_lo = (uint32_t)step;
+        const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
+        const uint32_t ge_lo = (uint32_t)ge;
+        // one ENV call: words 0, 1 = gaps 0, 1; X = words 3:2 gives, in order, the action draw
+        // (every mode), the autoreset draws and gap 2's uniform u2 (DESIGN.md "Step semantics")
+        const Word4 E = pbn::philox(ge_lo, st_lo, pbn::kStreamEnv << 28, ge_hi, u_k0, u_k1);
+        if (valid) {
+          uint32_t m[W], gam[W], rs[W];
+#pragma unroll
+          for (int w = 0; w < W; ++w) { m[w] = 0; gam[w] = 0; rs[w] = 0; }
+          uint32_t xhi = E.w, xlo = E.z;
+          const uint32_t n1 = (uint32_t)(N + 1);
+          const uint32_t c_act = ext64(xhi, xlo, n1 * n1 * n1);
+          // X after the action and pair draws, X * x_mult mod 2^64, as one product off the
+          // draws' dependency chain
+          uint64_t xr = ((((uint64_t)E.w) << 32) | E.z) * a.x_mult;
+          // autoreset draw (used by wave 0 only if the env's episode ends): (start, target) in
+          // one draw over the A(A-1) pairs, then the state within the start attractor
+          uint32_t rt;
+          if (u_na >= 1) {
+            const int32_t* att_first = reinterpret_cast<const int32_t*>(L + a.att_off);
+            const uint32_t* att_words = L + a.att_off + u_na + 1;
+            const uint32_t A = (uint32_t)u_na;
+            uint32_t as = 0;
+            rt = 0;
+            if (A >= 2) {
+              const uint32_t c = ext64(xhi, xlo, A * (A - 1));
+              as = a.am1_magic ? __umulhi(c, a.am1_magic) : c;   // c / (A - 1)
+              rt = c - as * (A - 1);
+              rt += (rt >= as) ? 1u : 0u;
+            }
+            // (single-state attractors: the draw over one state is 0 and state a is attractor a's)
+            const int st0 = (u_fl & 16u) ? (int)as : att_first[as];
+            uint32_t idx = 0;
+            if (!(u_fl & 16u)) {
+              const uint32_t size = (uint32_t)(att_first[as + 1] - st0);
+              idx = ext64(xhi, xlo, size);
+              xr *= size;
+            }
+#pragma unroll
+            for (int w = 0; w < W; ++w) rs[w] = att_words[(size_t)(st0 + idx) * W + w];
+          } else {
+            const Word4 rr = pbn::philox(ge_lo, st_lo, (pbn::kStreamReset << 28) | 1u, ge_hi, u_k0, u_k1);
+            const uint32_t rw4[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+            for (int w = 0; w < W; ++w) rs[w] = rw4[w] & valid_word_mask(N, w);
+            rt = PBN_NO_TARGET;
+          }
+          const uint32_t u2 = (uint32_t)(xr >> 32);   // = xhi
+          if (u_fl & 4u) {
+            actions_from_draw<W>(c_act, N, a.n1_magic, m);
+#pragma unroll
+            for (int w = 0; w < W; ++w) LANE_ST(a.flipmask, k * plane + (size_t)w * n, le, (size_t)n_steps * plane, 8, m[w]);
+          } else {
+#pragma unroll
+            for (int w = 0; w < W; ++w)
+              m[w] = LANE_AT(a.flipmask, k * plane + (size_t)w * n, le, (size_t)n_steps * plane, 6) & valid_word_mask(N, w);
+          }
+          uint32_t pc = 0;
+#pragma unroll
+          for (int w = 0; w < W; ++w) pc += __builtin_popcount(m[w]);
+          int g0, g1, g2;
+          if (u_gx == 2) {
+            g0 = gap_any(2, L, a, E.x); g1 = gap_any(2, L, a, E.y); g2 = gap_any(2, L, a, u2);
+          } else if (u_gx) {
+            g0 = gap_of(cdf, a.cdf_len, E.x); g1 = gap_of(cdf, a.cdf_len, E.y); g2 = gap_of(cdf, a.cdf_len, u2);
+          } else {
+            g0 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.x);
+            g1 = gap_est(cdf, a.cdf_len, a.inv_log2q, E.y);
+            g2 = gap_est(cdf, a.cdf_len, a.inv_log2q, u2);
+          }
+          const int p0 = g0 - 1, p1 = p0 + g1, p2 = p1 + g2;
+          set_bit<W>(gam, p0, N);
+          set_bit<W>(gam, p1, N);
+          set_bit<W>(gam, p2, N);
+          if (p2 < N - 1) {   // rare: a fourth flip is possible (gap k >= 3: PERT call (k-3)>>2, word (k-3)&3)
+            Word4 P = E;
+            int pos = p2;
+            for (int kk = 3; pos < N - 1; ++kk) {
+              if (((kk - 3) & 3) == 0)
+                P = pbn::philox(ge_lo, st_lo, (pbn::kStreamPert << 28) | (uint32_t)((kk - 3) >> 2), ge_hi, u_k0, u_k1);
+              const int j4 = (kk - 3) & 3;
+              const uint32_t u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
+              pos += gap_any(u_gx, L, a, u);
+              set_bit<W>(gam, pos, N);
+            }
+          }
+          bool pert = false;
+#pragma unroll
+          for (int w = 0; w < W; ++w) pert = pert || gam[w] != 0;
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            slot[w * 64 + lane] = m[w];
+            slot[(W + w) * 64 + lane] = gam[w];
+            slot[(2 * W + w) * 64 + lane] = rs[w];
+          }
+          slot[3 * W * 64 + lane] = rt | (pc << 8) | ((uint32_t)pert << 16);
+        }
+      }
+      PBN_PSTAMP(k, 1);
+      lds_barrier();
+    }
+  } else if (role == 2 && W == 1 && u_mnf >= 2 && u_mnf <= kNodeRecs) {
+    // selection, single-word states with at most kNodeRecs functions per node: branch-free over
+    // the lanes (lanes past N, single-function nodes and thresholds past a node's last compute
+    // values the padded chain ignores), one loop per threshold count, and the next step's
+    // SEL calls computed in the same block as this step's compares
+    auto sel_fast = [&](auto nq_c) {
+      constexpr int NQ = decltype(nq_c)::value;   // thresholds per node: max_nf - 1
+      const uint32_t* cmi = cm + l32;
+      uint32_t* lt_base = slots + (3 * W + 1) * 64 + half * 32 * W + l32;
+      auto sel_calls = [&](int k, uint32_t (&d)[16]) {
+        const uint64_t step = a.step + (uint64_t)k;
+        const uint32_t G_hi = (uint32_t)((G >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
+#pragma unroll
+        for (int c = 0; c < CPN; ++c) {
+          const Word4 o = pbn::philox((uint32_t)G, (uint32_t)step, (pbn::kStreamSel << 28) | (uint32_t)(4 * l32 + c),
+                                             G_hi, u_k0, u_k1);
+          d[4 * c + 0] = o.x; d[4 * c + 1] = o.y; d[4 * c + 2] = o.z; d[4 * c + 3] = o.w;
+        }
+      };
+      // one step: this step's compares from `cur`, the next step's calls into `nxt`
+      auto sel_step = [&](int k, const uint32_t (&cur)[16], uint32_t (&nxt)[16]) {
+        asm volatile("" : "+s"(u_k0), "+s"(u_k1));
+        PBN_PSTAMP(k, 0);
+        if (k < n_steps) {
+          sel_calls(k + 1, nxt);   // (one unused set per launch)
+          uint32_t* lt_out = lt_base + (size_t)(k & 1) * a.slot_words;
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) lt_out[q * 64] = less_than_cm<B>(cur, cmi + (size_t)q * B * 32, 32);
+          // keeps the next calls in this block (LLVM would sink them to the loop latch)
+#pragma unroll
+          for (int d = 0; d < 16; ++d) asm volatile("" : "+v"(nxt[d]));
+        }
+        PBN_PSTAMP(k, 1);
+        lds_barrier();
+      };
+      // two steps per trip with the digit arrays swapping roles: no copies between steps
+      uint32_t dA[16], dB[16];
+#pragma unroll
+      for (int d = 0; d < 16; ++d) { dA[d] = 0; dB[d] = 0; }
+      sel_calls(0, dA);
+      for (int k = 0; k <= n_steps; k += 2) {
+        sel_step(k, dA, dB);
+        if (k + 1 <= n_steps) sel_step(k + 1, dB, dA);
+      }
+    };
+    switch (u_mnf) {
+      case 2: sel_fast(std::integral_constant<int, 1>{}); break;
+      case 3: sel_fast(std::integral_constant<int, 2>{}); break;
+      default: sel_fast(std::integral_constant<int, 3>{}); break;
+    }
+  } else if (role == 2) {
+    for (int k = 0; k <= n_steps; ++k) {
+      asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
+      asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
+      PBN_PSTAMP(k, 0);
+      if (k < n_steps) {
+        // ---- selection masks of step k: node l32 + 32r of group g
+        uint32_t* lt_out = slots + (size_t)(k & 1) * a.slot_words + (3 * W + 1) * 64 + half * 32 * W;
+        const uint64_t step = a.step + (uint64_t)k;
+        const uint32_t st_lo = (uint32_t)step;
+        const uint32_t G_hi = (uint32_t)((G >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
+        const uint32_t G_lo = (uint32_t)G;
+#pragma unroll
+        for (int r = 0; r < W; ++r) {
+          const int i = l32 + 32 * r;
+          const int ic = i < N ? i : 0;
+          const uint4 r0 = recL[ic];
+          if (valid && i < N && (int)r0.w > 1) {
+            uint32_t dig[16];
+#pragma unroll
+            for (int c = 0; c < CPN; ++c) {
+              const Word4 o = pbn::philox(G_lo, st_lo, (pbn::kStreamSel << 28) | (uint32_t)(4 * i + c), G_hi, u_k0, u_k1);
+              dig[4 * c + 0] = o.x; dig[4 * c + 1] = o.y; dig[4 * c + 2] = o.z; dig[4 * c + 3] = o.w;
+            }
+            const int nf = (int)r0.w;
+            {   // per-lane thresholds: the selection wave has slack, the SGPRs are scarce
+#pragma unroll
+              for (int q = 0; q < kNodeRecs - 1; ++q)
+                if (q < nf - 1) {
+                  if constexpr (W == 1)
+                    lt_out[q * 64 * W + i] = less_than_cm<B>(dig, cm + (size_t)q * B * 32 + i, 32);
+                  else
+                    lt_out[q * 64 * W + i] = less_than(dig, recL[q * 32 * W + ic].z, B);
+                }
+              const int f0 = (int)recL[32 * W + ic].w;
+              for (int j = kNodeRecs - 1; j < nf - 1; ++j)   // nodes with more than kNodeRecs functions
+                lt_out[j * 64 * W + i] = less_than(dig, a.fcompact[CK(f0 + j, a.n_funcs, 9)].z, B);
+            }
+          }
+        }
+      }
+      PBN_PSTAMP(k, 1);
+      lds_barrier();
+    }
+  } else {
+    // the epilogue of step t (after the back-transpose): perturbed envs, outputs, attractor
+    // hash, reward, flags, autoreset
+    auto finish = [&](int t, uint32_t (&sp)[W], const uint32_t (&s1)[W], const uint32_t (&gam)[W],
+                      const uint32_t (&rs)[W], uint32_t info) {
+      {
+        // branch-free epilogue (this wave bounds the iteration): only the stores are guarded
+        const bool pert = (info >> 16) & 1u;
+        const uint32_t pc = (info >> 8) & 0xFFu;
+#pragma unroll
+        for (int w = 0; w < W; ++w) sp[w] = pert ? (s1[w] ^ gam[w]) : sp[w];
+        if (valid && (u_fl & 2u)) {
+#pragma unroll
+          for (int w = 0; w < W; ++w) LANE_ST(a.final_state, t * plane + (size_t)w * n, le, (size_t)n_steps * plane, 10, sp[w]);
+        }
+        // reward candidates depend only on popcount(flipmask): one 16-byte row {none, wrong,
+        // term, -} read beside the hash
+        const float4 r4 = reinterpret_cast<const float4*>(rtab)[pc];
+        const float r_none = r4.x, r_wrong = r4.y, r_term = r4.z;
+        int att = -1;
+        if (u_hb > 0) {
+          const uint32_t hmask = (1u << u_hb) - 1u;
+          uint32_t h = 0;
+#pragma unroll
+          for (int w = 0; w < W; ++w) h += sp[w] * a.hash_mult[w];
+          h >>= (32 - u_hb);
+          // the table is usually collision-free (one probe, h < 2^bits needs no mask); keys
+          // are unique, so probe order does not matter
+          att = hash_probe<W>(htab, h, sp);
+          for (int pr = 1; pr < u_hp; ++pr) {
+            const int id = hash_probe<W>(htab, (h + pr) & hmask, sp);
+            if (id >= 0) att = id;
+          }
+        }
+        const bool in_attr = att >= 0;
+        const bool term = in_attr && (uint32_t)att == tg0;
+        const bool wrong = in_attr && !term;
+        int tt = (int)tt0 + 1;
+        tt = tt > 255 ? 255 : tt;
+        const bool trunc = u_hz > 0 && tt >= u_hz;
+        const bool reset = (u_fl & 8u) && (term || trunc);
+        const uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) |
+                            ((uint32_t)pert << 3) | ((uint32_t)reset << 4);
+        if (valid) {
+          LANE_ST(a.reward, (size_t)t * n, le, (size_t)n_steps * n, 11, term ? r_term : (wrong ? r_wrong : r_none));
+          LANE_ST(a.flags, (size_t)t * n, le, (size_t)n_steps * n, 15, (uint8_t)fl);
+        }
+        tg0 = reset ? (info & 0xFFu) : tg0;
+        tt0 = reset ? 0u : (uint32_t)tt;
+#pragma unroll
+        for (int w = 0; w < W; ++w) st[w] = reset ? rs[w] : sp[w];
+      }
+    };
+    if (W == 1 && u_mnf >= 1 && u_mnf <= kNodeRecs) {
+      // single-word states with at most kNodeRecs functions per node: the loop-invariant record
+      // inputs held in VGPRs, and this step's selection masks and selectors read before the
+      // transpose, so that their LDS latency is off the chain slot -> transpose -> gathers ->
+      // mux trees -> back-transpose
+      auto state_fast = [&](auto k_c) {
+        constexpr int K = decltype(k_c)::value;
+        uint32_t ins[K];
+#pragma unroll
+        for (int q = 0; q < K; ++q) ins[q] = recL[q * 32 + l32].x;
+        for (int k = 0; k <= n_steps; ++k) {
+          asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
+          PBN_PSTAMP(k, 0);
+          if (k >= 1) {
+            const int t = k - 1;
+            const uint32_t* slot = slots + (size_t)(t & 1) * a.slot_words;
+            const uint32_t* lt_in = slot + 4 * 64 + half * 32 + l32;
+            uint32_t s1[W], gam[W], rs[W];
+            s1[0] = st[0] ^ slot[lane];
+            gam[0] = slot[64 + lane];
+            rs[0] = slot[2 * 64 + lane];
+            const uint32_t info = slot[3 * 64 + lane];
+            uint32_t ltv[K];
+            uint4 sa[K], sb[K];
+#pragma unroll
+            for (int q = 0; q < K; ++q) {
+              ltv[q] = q < K - 1 ? lt_in[q * 64] : 0u;
+              sa[q] = selq[(2 * q) * 32 + l32];
+              sb[q] = selq[(2 * q + 1) * 32 + l32];
+            }
+            if (valid && (u_fl & 1u)) LANE_ST(a.obs, (size_t)t * plane, le, (size_t)n_steps * plane, 7, st[0]);
+            Sg[l32] = lane_transpose32(s1[0], lane);
+            __builtin_amdgcn_wave_barrier();
+            uint32_t x = 0;
+#pragma unroll
+            for (int q = K - 1; q >= 0; --q) {
+              uint32_t xin[4];
+#pragma unroll
+              for (int kk = 0; kk < 4; ++kk) xin[kk] = plane_in<true>(Sg, ins[q], kk);
+              const uint32_t fj = eval_sel_in(xin, sa[q], sb[q]);
+              x = (q == K - 1) ? fj : bfi(ltv[q], fj, x);
+            }
+            uint32_t sp[W];
+            sp[0] = lane_transpose32(x, lane);
+            finish(t, sp, s1, gam, rs, info);
+          }
+          PBN_PSTAMP(k, 1);
+          lds_barrier();
+          PBN_PSTAMP(k, 2);
+          if (k <= 1) PBN_RSTAMP(3 + k);
+        }
+      };
+      switch (u_mnf) {
+        case 1: state_fast(std::integral_constant<int, 1>{}); break;
+        case 2: state_fast(std::integral_constant<int, 2>{}); break;
+        case 3: state_fast(std::integral_constant<int, 3>{}); break;
+        default: state_fast(std::integral_constant<int, 4>{}); break;
+      }
+    } else
+    for (int k = 0; k <= n_steps; ++k) {
+      asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
+      asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
+      PBN_PSTAMP(k, 0);
+      if (k >= 1) {
+        // ---- state part of step t = k - 1
+        const int t = k - 1;
+        const uint32_t* slot = slots + (size_t)(t & 1) * a.slot_words;
+        const uint32_t* lt_in = slot + (3 * W + 1) * 64 + half * 32 * W;
+        uint32_t s1[W], gam[W], rs[W];
+        uint32_t info = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          s1[w] = st[w] ^ slot[w * 64 + lane];
+          gam[w] = slot[(W + w) * 64 + lane];
+          rs[w] = slot[(2 * W + w) * 64 + lane];
+        }
+        info = slot[3 * W * 64 + lane];
+        if (valid && (u_fl & 1u)) {
+#pragma unroll
+          for (int w = 0; w < W; ++w) LANE_ST(a.obs, t * plane + (size_t)w * n, le, (size_t)n_steps * plane, 7, st[w]);
+        }
+#pragma unroll
+        for (int w = 0; w < W; ++w) Sg[32 * w + l32] = lane_transpose32(s1[w], lane);
+        __builtin_amdgcn_wave_barrier();
+        PBN_PSTAMP_AT(k, 3);
+        uint32_t X[W];
+        if (u_mnf <= kNodeRecs) {
+#pragma unroll
+          for (int r = 0; r < W; ++r) {
+            int i = l32 + 32 * r;
+            asm volatile("" : "+v"(i));   // selector and record reads stay in the step loop
+            const uint4* rc = recL + i;
+            const uint4* sel = selq + i;
+            const uint32_t* lti = lt_in + i;
+            switch (u_mnf) {
+              case 1: X[r] = chain_padded<1, (W <= 2)>(rc, sel, 32 * W, Sg, lti, 64 * W); break;
+              case 2: X[r] = chain_padded<2, (W <= 2)>(rc, sel, 32 * W, Sg, lti, 64 * W); break;
+              case 3: X[r] = chain_padded<3, (W <= 2)>(rc, sel, 32 * W, Sg, lti, 64 * W); break;
+              default: X[r] = chain_padded<4, (W <= 2)>(rc, sel, 32 * W, Sg, lti, 64 * W); break;
+            }
+          }
+        } else
+#pragma unroll
+        for (int r = 0; r < W; ++r) {
+          const int i = l32 + 32 * r;
+          int ii = i < N ? i : 0;
+          asm volatile("" : "+v"(ii));   // selector and record reads stay in the step loop
+          uint4 rec_r[kNodeRecs];
+#pragma unroll
+          for (int q = 0; q < kNodeRecs; ++q) rec_r[q] = recL[q * 32 * W + ii];
+          const int nf = (int)rec_r[0].w;
+          uint32_t x = 0;
+          if (u_mnf > kNodeRecs) {   // chain tail of nodes with more than kNodeRecs functions
+            const int f0 = (int)rec_r[1].w;
+            for (int j = nf - 1; j >= kNodeRecs; --j) {
+              const uint4 rc = a.fcompact[CK(f0 + j, a.n_funcs, 9)];
+              const uint32_t fj = eval_compact(rc.x, rc.y, Sg);
+              x = (j == nf - 1) ? fj : bfi(lt_in[j * 64 * W + ii], fj, x);
+            }
+          }
+          const uint4* sel = selq + ii;
+          const uint32_t* lti = lt_in + ii;
+          switch (u_mnf) {
+            case 1: x = chain_from_masks<1, (W <= 2)>(rec_r, sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
+            case 2: x = chain_from_masks<2, (W <= 2)>(rec_r, sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
+            case 3: x = chain_from_masks<3, (W <= 2)>(rec_r, sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
+            default: x = chain_from_masks<4, (W <= 2)>(rec_r, sel, 32 * W, Sg, lti, 64 * W, nf, u_mnf > kNodeRecs, x); break;
+          }
+          X[r] = i < N ? x : 0u;
+        }
+        PBN_PSTAMP_AT(k, 12);
+        uint32_t sp[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) sp[w] = lane_transpose32(X[w], lane);
+        PBN_PSTAMP_AT(k, 13);
+        finish(t, sp, s1, gam, rs, info);
+      }
+      PBN_PSTAMP(k, 1);
+      lds_barrier();
+      PBN_PSTAMP(k, 2);
+    }
+    PBN_RSTAMP(5);
+    if (valid) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) a.state_out[CK((size_t)w * n + le, plane, 16)] = st[w];
+      a.t[CK(le, n, 17)] = (uint8_t)tt0;
+      a.target[CK(le, n, 18)] = (uint8_t)tg0;
+    }
+#ifdef PBN_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+    PBN_RSTAMP(6);
+#endif
+  }
+}
+
+// ------------------------------------------------------------- state histogram
+// Visits per state for the steady-state distribution.  States of a steady-state chain
+// concentrate on a few attractor basins, so a wave first merges equal values (a few
+// ballot rounds: the leader adds the count of its value) before per-lane atomics.
+__global__ void __launch_bounds__(256) pbn_hist_kernel(const uint32_t* __restrict__ states, int64_t n_rows,
+                                                       int64_t n_cols, int64_t row_stride, uint32_t mask,
+                                                       uint32_t* __restrict__ hist) {
+  const int64_t total = n_rows * n_cols;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < total; base += stride) {
+    const int64_t i = base + threadIdx.x;
+    const bool have = i < total;
+    uint32_t v = 0;
+    if (have) {
+      const int64_t r = i / n_cols, c = i - r * n_cols;
+      v = states[r * row_stride + c] & mask;
+    }
+    bool pending = have;
+#pragma unroll
+    for (int round = 0; round < 4; ++round) {
+      const uint64_t act = __ballot(pending);
+      if (act == 0) break;
+      const int leader = __builtin_ctzll(act);
+      const uint32_t lv = __shfl(v, leader);
+      const uint64_t same = __ballot(pending && v == lv);
+      if ((threadIdx.x & 63) == leader) atomicAdd(&hist[lv], (uint32_t)__popcll(same));
+      if (pending && v == lv) pending = false;
+    }
+    if (pending) atomicAdd(&hist[v], 1u);
+  }
+}
+
+// ---------------------------------------------------------------- reset kernel
+template <int W>
+__global__ void __launch_bounds__(256) pbn_reset_kernel(const int32_t* __restrict__ att_start,
+                                                        const uint32_t* __restrict__ att_states,
+                                                        int n_attr, int n_states, int N, uint64_t seed, uint64_t step,
+                                                        uint64_t env_offset, int64_t n, uint32_t* state,
+                                                        uint8_t* target, uint8_t* t) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t ge = env_offset + (uint64_t)i;
+  const Word4 r0 = pbn::draw(seed, ge, step, pbn::kStreamReset, 0);
+  uint32_t ns[W];
+  uint32_t nt;
+  if (n_attr >= 1) {
+    // (start, target != start) in one draw over the A(A-1) pairs, then the start state
+    // uniformly within the start attractor, from the 64-bit value (word 1 : word 0)
+    uint32_t hi = r0.y, lo = r0.x;
+    const uint32_t A = (uint32_t)n_attr;
+    uint32_t as = 0;
+    nt = 0;
+    if (A >= 2) {
+      const uint32_t c = ext64(hi, lo, A * (A - 1));
+      as = c / (A - 1);
+      nt = c - as * (A - 1);
+      nt += (nt >= as) ? 1u : 0u;
+    }
+    const int st0 = att_start[CK(as, n_attr + 1, 20)];
+    const uint32_t size = (uint32_t)(att_start[CK(as + 1, n_attr + 1, 21)] - st0);
+    const uint32_t idx = ext64(hi, lo, size);
+#pragma unroll
+    for (int w = 0; w < W; ++w) ns[w] = att_states[CK((size_t)(st0 + idx) * W + w, (size_t)n_states * W, 22)];
+  } else {
+    const Word4 r1 = pbn::draw(seed, ge, step, pbn::kStreamReset, 1);
+    const uint32_t rw[4] = {r1.x, r1.y, r1.z, r1.w};
+#pragma unroll
+    for (int w = 0; w < W; ++w) ns[w] = rw[w] & valid_word_mask(N, w);
+    nt = PBN_NO_TARGET;
+  }
+#pragma unroll
+  for (int w = 0; w < W; ++w) state[(size_t)w * n + i] = ns[w];
+  target[i] = (uint8_t)nt;
+  t[i] = 0;
+}
+
+}  // namespace

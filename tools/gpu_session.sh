@@ -5,6 +5,7 @@
 # Outputs under gpurun_out/TAG/.  Every GPU step runs under its own time limit; the first
 # failure ends the session (no retries).  Steps:
 #   tests            the -m gpu suite (tools/gpu_tests.sh) + smoke()
+#   pytest:F1,F2     the -m gpu tests of those files only (e.g. pytest:tests/test_gpu_agent.py)
 #   driver           the driver's bench command (--gpus 1 --steps 20 --warmup 5) + kernel trace + PMC
 #   s2000            2,000 steps at 65,536 envs (100-step launches) + kernel trace + PMC
 #   1m               pbn28 x 1,048,576 envs, 500 steps
@@ -29,6 +30,11 @@ bench() {   # bench NAME ARGS... : one bench line
 for step in "$@"; do
   case $step in
     tests) bash tools/gpu_tests.sh "$tag/tests" || fail tests ;;
+    pytest:*)
+      files=${step#pytest:}
+      timeout -k 10 600 python -u -m pytest ${files//,/ } -m gpu -x -v --timeout 240 --timeout-method thread \
+        > "$out/pytest.log" 2>&1 || { tail -40 "$out/pytest.log"; fail "$step"; }
+      tail -2 "$out/pytest.log" ;;
     driver) bash tools/gpu_bench_profile.sh "$tag/driver" --gpus 1 --steps 20 --warmup 5 || fail driver ;;
     s2000) bash tools/gpu_bench_profile.sh "$tag/s2000" --gpus 1 --steps 2000 --warmup 200 || fail s2000 ;;
     1m) bench bench_1m --envs 1048576 --steps 500 --warmup 100 --no-cpu-baseline ;;
