@@ -16,7 +16,7 @@
 // feature row(r, h) = (r & 3) + 8 (r >> 2) + 4 h on lane half h, and k-step (tile p, register
 // r) of the next layer takes lane half h's element from there.  The A operand (weights) is
 // then W[out][32 p + row(r, h)], i.e. for r = 4q .. 4q+3 four consecutive inputs: one float4
-// load of the weight row per four MFMAs, straight from the natural (out, in) layout in L2.
+// read of the weight row per four MFMAs (from LDS: the weight stream below).
 // Biases initialise the accumulators; LeakyReLU (x > 0 ? x : x * slope, torch's form) is
 // applied in registers between layers.  y is read in the same feature order (four float4 per
 // lane per 32-feature tile).
@@ -70,35 +70,109 @@ __device__ __forceinline__ f32x16 leaky(f32x16 x, float slope) {
   return x;
 }
 
-// acc += W[32 m + (lane & 31)][32 p + row(., h)] . X  over the 16 k-steps of input tile p
-// (W row-major [n_out][ld]; rows >= n_out read as 0)
-__device__ __forceinline__ f32x16 tile_step(f32x16 acc, const float* __restrict__ W, int ld, int n_out, int m,
-                                            int p, int lane, const f32x16& X) {
-  const int o = 32 * m + (lane & 31);
-  const int h = lane >> 5;
-  const float* wr = W + (size_t)(o < n_out ? o : 0) * ld + 32 * p + 4 * h;
+// The A operand of k-steps (tile p, registers 4q .. 4q+3), q = 0..3: one float4 of weight row
+// 32 m + (lane & 31) at column 32 p + 8 q + 4 h
+struct WTile {
   float4 w[4];
+};
+
+// acc += W-tile . X over the 16 k-steps of one input tile
+__device__ __forceinline__ f32x16 mfma_tile(f32x16 acc, const WTile& t, const f32x16& X) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    w[q] = *reinterpret_cast<const float4*>(wr + 8 * q);
-    if (o >= n_out) w[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    acc = mfma(w[q].x, X[4 * q + 0], acc);
-    acc = mfma(w[q].y, X[4 * q + 1], acc);
-    acc = mfma(w[q].z, X[4 * q + 2], acc);
-    acc = mfma(w[q].w, X[4 * q + 3], acc);
+    acc = mfma(t.w[q].x, X[4 * q + 0], acc);
+    acc = mfma(t.w[q].y, X[4 * q + 1], acc);
+    acc = mfma(t.w[q].z, X[4 * q + 2], acc);
+    acc = mfma(t.w[q].w, X[4 * q + 3], acc);
   }
   return acc;
 }
 
+// The weights reach the MFMAs through LDS as one stream of chunks, double-buffered: a chunk
+// is 32 input columns of one layer's weight matrix, all its rows (<= 128; rows past n_out are
+// zero).  The block's four waves share every chunk (a quarter of the L2 reads of per-wave
+// loads), the next chunk's global loads are in flight under the current chunk's MFMAs, and an
+// operand read is one ds_read_b128 at LDS latency.  Rows are padded to 36 floats, so the 16
+// rows one read's quarter-wave touches start on 16 distinct 4-bank groups.  The stream:
+//   Linear(256, 128): 8 chunks | Linear(128, 64): 4 | Linear(64, 32): 2 |
+//   per head k: Linear(32, 64): 1, Linear(64, A): 2
+constexpr int kPitch = 36;
+constexpr int kBufFloats = 128 * kPitch;   // one buffer: up to 128 rows
+
+struct Chunk {
+  const float* src;   // column 0 of the chunk in the row-major weight matrix
+  int ld, rows;       // row stride (floats), valid rows (the rest of the 32 * tiles read 0)
+};
+
+__device__ __forceinline__ Chunk chunk_of(const QnetArgs& a, int c) {
+  if (c < 8) return {a.w1 + 32 * c, kD0, kD1};
+  if (c < 12) return {a.w2 + 32 * (c - 8), kD1, kD2};
+  if (c < 14) return {a.w3 + 32 * (c - 12), kD2, kD3};
+  const int k = (c - 14) / 3, j = (c - 14) % 3;
+  if (j == 0) return {a.wh1 + (size_t)kDH * k * kD3, kD3, kDH};
+  return {a.wh2 + (size_t)a.n_act * kDH * k + 32 * (j - 1), kDH, a.n_act};
+}
+
+__device__ __forceinline__ WTile lds_w(const float* __restrict__ buf, int m, int lane) {
+  const float* r = buf + (32 * m + (lane & 31)) * kPitch + 4 * (lane >> 5);
+  WTile t;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) t.w[q] = *reinterpret_cast<const float4*>(r + 8 * q);
+  return t;
+}
+
+template <int AT>   // output tiles of the second head layers: A <= 32 AT
 __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
+  __shared__ __attribute__((aligned(16))) float wbuf[2 * kBufFloats];
   const int lane = threadIdx.x & 63;
   const int h = lane >> 5;
   const int64_t e0 = ((int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6)) * 32;
-  if (e0 >= a.n) return;   // whole wave (n is a multiple of 32)
-  const int64_t e = e0 + (lane & 31);
+  const bool live = e0 < a.n;   // (a wave past the end still stages weights and meets the barriers)
+  const int64_t e = live ? e0 + (lane & 31) : 0;
+  const int A = a.n_act;
+  const int n_chunks = 14 + 3 * a.n_heads;
+
+  // staging: thread t moves float4 (row (t >> 3) + 32 j, columns 4 (t & 7) .. +3), j = 0..3
+  const int t = threadIdx.x;
+  const int srow = t >> 3, scol = 4 * (t & 7);
+  float4 s0, s1, s2, s3;
+#define PBN_FETCH(c_)                                                                              \
+  do {                                                                                             \
+    const Chunk ch_ = chunk_of(a, (c_));                                                           \
+    const float4 z_ = make_float4(0.f, 0.f, 0.f, 0.f);                                             \
+    const float* p_ = ch_.src + scol;                                                              \
+    const int last_ = ch_.rows - 1; /* rows past the matrix load its last row, then read as 0 */   \
+    s0 = *reinterpret_cast<const float4*>(p_ + (size_t)min(srow, last_) * ch_.ld);                 \
+    s1 = *reinterpret_cast<const float4*>(p_ + (size_t)min(srow + 32, last_) * ch_.ld);            \
+    s2 = *reinterpret_cast<const float4*>(p_ + (size_t)min(srow + 64, last_) * ch_.ld);            \
+    s3 = *reinterpret_cast<const float4*>(p_ + (size_t)min(srow + 96, last_) * ch_.ld);            \
+    if (srow >= ch_.rows) s0 = z_;                                                                 \
+    if (srow + 32 >= ch_.rows) s1 = z_;                                                            \
+    if (srow + 64 >= ch_.rows) s2 = z_;                                                            \
+    if (srow + 96 >= ch_.rows) s3 = z_;                                                            \
+  } while (0)
+#define PBN_PUT(b_)                                                                                \
+  do {                                                                                             \
+    float* d_ = wbuf + (b_) * kBufFloats + srow * kPitch + scol;                                   \
+    *reinterpret_cast<float4*>(d_) = s0;                                                           \
+    *reinterpret_cast<float4*>(d_ + 32 * kPitch) = s1;                                             \
+    *reinterpret_cast<float4*>(d_ + 64 * kPitch) = s2;                                             \
+    *reinterpret_cast<float4*>(d_ + 96 * kPitch) = s3;                                             \
+  } while (0)
+  // one chunk step: the next chunk's loads, this chunk's MFMAs (BODY reads `buf`), the next
+  // chunk into the other buffer (the waves left it at the previous barrier), barrier
+#define PBN_CHUNK(c_, BODY)                                                                        \
+  do {                                                                                             \
+    const int cc_ = (c_);                                                                          \
+    if (cc_ + 1 < n_chunks) PBN_FETCH(cc_ + 1);                                                    \
+    const float* buf = wbuf + (cc_ & 1) * kBufFloats;                                              \
+    if (live) { BODY }                                                                             \
+    if (cc_ + 1 < n_chunks) PBN_PUT((cc_ + 1) & 1);                                                \
+    __syncthreads();                                                                               \
+  } while (0)
+
+  PBN_FETCH(0);
+  PBN_PUT(0);
 
   // ---- Linear(256, 128): input tiles from y, feature order row(r, h) (four float4 per tile)
   f32x16 x1[kD1 / 32];
@@ -108,9 +182,10 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
   float4 yv[4], yn[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) yv[q] = *reinterpret_cast<const float4*>(yrow + 8 * q);
+  __syncthreads();
 #pragma unroll
   for (int p = 0; p < kD0 / 32; ++p) {
-    if (p + 1 < kD0 / 32) {   // the next tile's loads in flight under this tile's MFMAs
+    if (p + 1 < kD0 / 32) {   // the next y tile's loads fly under this tile's MFMAs
 #pragma unroll
       for (int q = 0; q < 4; ++q) yn[q] = *reinterpret_cast<const float4*>(yrow + 32 * (p + 1) + 8 * q);
     }
@@ -119,8 +194,10 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
     for (int q = 0; q < 4; ++q) {
       X[4 * q + 0] = yv[q].x; X[4 * q + 1] = yv[q].y; X[4 * q + 2] = yv[q].z; X[4 * q + 3] = yv[q].w;
     }
-#pragma unroll
-    for (int m = 0; m < kD1 / 32; ++m) x1[m] = tile_step(x1[m], a.w1, kD0, kD1, m, p, lane, X);
+    PBN_CHUNK(p, {
+_Pragma("unroll")
+      for (int m = 0; m < kD1 / 32; ++m) x1[m] = mfma_tile(x1[m], lds_w(buf, m, lane), X);
+    });
 #pragma unroll
     for (int q = 0; q < 4; ++q) yv[q] = yn[q];
   }
@@ -130,41 +207,60 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
   // ---- Linear(128, 64), Linear(64, 32)
   f32x16 x2[kD2 / 32];
 #pragma unroll
-  for (int m = 0; m < kD2 / 32; ++m) {
-    x2[m] = bias_tile(a.b2, m, h, kD2);
+  for (int m = 0; m < kD2 / 32; ++m) x2[m] = bias_tile(a.b2, m, h, kD2);
 #pragma unroll
-    for (int p = 0; p < kD1 / 32; ++p) x2[m] = tile_step(x2[m], a.w2, kD1, kD2, m, p, lane, x1[p]);
-    x2[m] = leaky(x2[m], a.slope);
+  for (int p = 0; p < kD1 / 32; ++p) {
+    PBN_CHUNK(8 + p, {
+_Pragma("unroll")
+      for (int m = 0; m < kD2 / 32; ++m) x2[m] = mfma_tile(x2[m], lds_w(buf, m, lane), x1[p]);
+    });
   }
+#pragma unroll
+  for (int m = 0; m < kD2 / 32; ++m) x2[m] = leaky(x2[m], a.slope);
   f32x16 x3 = bias_tile(a.b3, 0, h, kD3);
 #pragma unroll
-  for (int p = 0; p < kD2 / 32; ++p) x3 = tile_step(x3, a.w3, kD2, kD3, 0, p, lane, x2[p]);
+  for (int p = 0; p < kD2 / 32; ++p) {
+    PBN_CHUNK(12 + p, { x3 = mfma_tile(x3, lds_w(buf, 0, lane), x2[p]); });
+  }
   x3 = leaky(x3, a.slope);
 
   // ---- heads: Linear(32, 64) + LeakyReLU per head (stacked rows 64 k .. 64 k + 63), then
   // Linear(64, A) of that head's 64 features; raw outputs to heads[k][e][a]
-  const int A = a.n_act;
-  const int atiles = (A + 31) / 32;
   for (int k = 0; k < a.n_heads; ++k) {
     f32x16 z[kDH / 32];
 #pragma unroll
-    for (int m = 0; m < kDH / 32; ++m) {
-      z[m] = bias_tile(a.bh1 + kDH * k, m, h, kDH);
-      z[m] = tile_step(z[m], a.wh1 + (size_t)kDH * k * kD3, kD3, kDH, m, 0, lane, x3);
-      z[m] = leaky(z[m], a.slope);
+    for (int m = 0; m < kDH / 32; ++m) z[m] = bias_tile(a.bh1 + kDH * k, m, h, kDH);
+    PBN_CHUNK(14 + 3 * k, {
+_Pragma("unroll")
+      for (int m = 0; m < kDH / 32; ++m) z[m] = mfma_tile(z[m], lds_w(buf, m, lane), x3);
+    });
+#pragma unroll
+    for (int m = 0; m < kDH / 32; ++m) z[m] = leaky(z[m], a.slope);
+    f32x16 o[AT];
+#pragma unroll
+    for (int m = 0; m < AT; ++m) o[m] = bias_tile(a.bh2 + (size_t)A * k, m, h, A);
+#pragma unroll
+    for (int p = 0; p < kDH / 32; ++p) {
+      PBN_CHUNK(15 + 3 * k + p, {
+_Pragma("unroll")
+        for (int m = 0; m < AT; ++m) o[m] = mfma_tile(o[m], lds_w(buf, m, lane), z[p]);
+      });
     }
-    float* out = a.heads + ((size_t)k * a.n + e) * A;
-    for (int m = 0; m < atiles; ++m) {
-      f32x16 o = bias_tile(a.bh2 + (size_t)A * k, m, h, A);
+    if (live) {
+      float* out = a.heads + ((size_t)k * a.n + e) * A;
 #pragma unroll
-      for (int p = 0; p < kDH / 32; ++p) o = tile_step(o, a.wh2 + (size_t)A * kDH * k, kDH, A, m, p, lane, z[p]);
+      for (int m = 0; m < AT; ++m) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int act = 32 * m + feat_row(r, h);
-        if (act < A) out[act] = o[r];
+        for (int r = 0; r < 16; ++r) {
+          const int act = 32 * m + feat_row(r, h);
+          if (act < A) out[act] = o[m][r];
+        }
       }
     }
   }
+#undef PBN_CHUNK
+#undef PBN_PUT
+#undef PBN_FETCH
 }
 
 bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
@@ -193,7 +289,9 @@ int pbn_qnet_heads(const pbn_net* net, int64_t n_envs, const float* d_y, const f
              n_actions, slope};
   const int64_t waves = n_envs / 32;
   const unsigned blocks = (unsigned)((waves + kWaves - 1) / kWaves);
-  hipLaunchKernelGGL(qnet_tail_kernel, dim3(blocks), dim3(64 * kWaves), 0, (hipStream_t)stream, a);
+  void (*kernels[kMaxActTiles])(QnetArgs) = {qnet_tail_kernel<1>, qnet_tail_kernel<2>, qnet_tail_kernel<3>,
+                                              qnet_tail_kernel<4>};
+  hipLaunchKernelGGL(kernels[(n_actions + 31) / 32 - 1], dim3(blocks), dim3(64 * kWaves), 0, (hipStream_t)stream, a);
   if (hipGetLastError() != hipSuccess) return pbn::set_error(PBN_EDEVICE, "qnet_tail_kernel launch failed");
   return PBN_OK;
 }
