@@ -35,6 +35,7 @@ constexpr int kD0 = 256, kD1 = 128, kD2 = 64, kD3 = 32, kDH = 64;   // Branching
 constexpr int kMaxHeads = 8;                                         // value + up to 7 branches
 constexpr int kMaxActTiles = 4;                                      // A <= 128 (pbn70: 71)
 constexpr int kWaves = 4;                                            // waves (32-env tiles) per block
+constexpr int kBiasFloats = kD1 + kD2 + kD3 + (kDH + 32 * kMaxActTiles) * kMaxHeads;
 
 struct QnetArgs {
   const float* y;                  // [n][256]
@@ -53,7 +54,7 @@ __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
-// acc = bias of the 32 output features 32 m + row(r, h) (0 past n_out)
+// acc = bias of the 32 output features 32 m + row(r, h) (0 past n_out; b in LDS)
 __device__ __forceinline__ f32x16 bias_tile(const float* __restrict__ b, int m, int h, int n_out) {
   f32x16 acc;
 #pragma unroll
@@ -136,53 +137,74 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
   const int t = threadIdx.x;
   const int srow = t >> 3, scol = 4 * (t & 7);
   float4 s0, s1, s2, s3;
+  int srows = 0;
 #define PBN_FETCH(c_)                                                                              \
   do {                                                                                             \
     const Chunk ch_ = chunk_of(a, (c_));                                                           \
-    const float4 z_ = make_float4(0.f, 0.f, 0.f, 0.f);                                             \
     const float* p_ = ch_.src + scol;                                                              \
     const int last_ = ch_.rows - 1; /* rows past the matrix load its last row, then read as 0 */   \
     s0 = *reinterpret_cast<const float4*>(p_ + (size_t)min(srow, last_) * ch_.ld);                 \
     s1 = *reinterpret_cast<const float4*>(p_ + (size_t)min(srow + 32, last_) * ch_.ld);            \
     s2 = *reinterpret_cast<const float4*>(p_ + (size_t)min(srow + 64, last_) * ch_.ld);            \
     s3 = *reinterpret_cast<const float4*>(p_ + (size_t)min(srow + 96, last_) * ch_.ld);            \
-    if (srow >= ch_.rows) s0 = z_;                                                                 \
-    if (srow + 32 >= ch_.rows) s1 = z_;                                                            \
-    if (srow + 64 >= ch_.rows) s2 = z_;                                                            \
-    if (srow + 96 >= ch_.rows) s3 = z_;                                                            \
+    srows = ch_.rows;                                                                              \
   } while (0)
 #define PBN_PUT(b_)                                                                                \
   do {                                                                                             \
     float* d_ = wbuf + (b_) * kBufFloats + srow * kPitch + scol;                                   \
+    const float4 z_ = make_float4(0.f, 0.f, 0.f, 0.f); /* masked here, not at the load: a select */ \
+    if (srow >= srows) s0 = z_;                        /* on the loaded value would wait for it */ \
+    if (srow + 32 >= srows) s1 = z_;                                                               \
+    if (srow + 64 >= srows) s2 = z_;                                                               \
+    if (srow + 96 >= srows) s3 = z_;                                                               \
     *reinterpret_cast<float4*>(d_) = s0;                                                           \
     *reinterpret_cast<float4*>(d_ + 32 * kPitch) = s1;                                             \
     *reinterpret_cast<float4*>(d_ + 64 * kPitch) = s2;                                             \
     *reinterpret_cast<float4*>(d_ + 96 * kPitch) = s3;                                             \
   } while (0)
-  // one chunk step: the next chunk's loads, this chunk's MFMAs (BODY reads `buf`), the next
+  // one chunk step: the next chunk's loads (kept above the MFMAs by the scheduling barriers:
+  // LLVM would sink them to their LDS stores and expose their L2 round trip), this chunk's
+  // MFMAs (BODY reads `buf`; waves past the end compute on env 0 and store nothing), the next
   // chunk into the other buffer (the waves left it at the previous barrier), barrier
 #define PBN_CHUNK(c_, BODY)                                                                        \
   do {                                                                                             \
     const int cc_ = (c_);                                                                          \
-    if (cc_ + 1 < n_chunks) PBN_FETCH(cc_ + 1);                                                    \
+    PBN_FETCH(min(cc_ + 1, n_chunks - 1)); /* unconditional: a branch here makes the wait */    \
+    __builtin_amdgcn_sched_barrier(0);                                                             \
     const float* buf = wbuf + (cc_ & 1) * kBufFloats;                                              \
-    if (live) { BODY }                                                                             \
-    if (cc_ + 1 < n_chunks) PBN_PUT((cc_ + 1) & 1);                                                \
+    BODY                                                                                           \
+    __builtin_amdgcn_sched_barrier(0);                                                             \
+    PBN_PUT((cc_ + 1) & 1); /* counters assume loads pending at the MFMAs (after the last */    \
+                            /* chunk this rewrites the idle buffer) */                            \
     __syncthreads();                                                                               \
   } while (0)
+
+  // every bias, staged once in LDS (a per-head bias load from L2 sat in front of the head's
+  // first MFMA): b1 | b2 | b3 | bh1 [64 H] | bh2 [H][A]
+  __shared__ float bias[kBiasFloats];
+  float* const bs1 = bias;
+  float* const bs2 = bs1 + kD1;
+  float* const bs3 = bs2 + kD2;
+  float* const bsh1 = bs3 + kD3;
+  float* const bsh2 = bsh1 + kDH * kMaxHeads;
+  for (int i = t; i < kD1; i += 64 * kWaves) bs1[i] = a.b1[i];
+  if (t < kD2) bs2[t] = a.b2[t];
+  if (t < kD3) bs3[t] = a.b3[t];
+  for (int i = t; i < kDH * a.n_heads; i += 64 * kWaves) bsh1[i] = a.bh1[i];
+  for (int i = t; i < A * a.n_heads; i += 64 * kWaves) bsh2[i] = a.bh2[i];
 
   PBN_FETCH(0);
   PBN_PUT(0);
 
   // ---- Linear(256, 128): input tiles from y, feature order row(r, h) (four float4 per tile)
-  f32x16 x1[kD1 / 32];
-#pragma unroll
-  for (int m = 0; m < kD1 / 32; ++m) x1[m] = bias_tile(a.b1, m, h, kD1);
   const float* yrow = a.y + (size_t)e * kD0 + 4 * h;
   float4 yv[4], yn[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) yv[q] = *reinterpret_cast<const float4*>(yrow + 8 * q);
-  __syncthreads();
+  __syncthreads();   // chunk 0 and the biases are in LDS
+  f32x16 x1[kD1 / 32];
+#pragma unroll
+  for (int m = 0; m < kD1 / 32; ++m) x1[m] = bias_tile(bs1, m, h, kD1);
 #pragma unroll
   for (int p = 0; p < kD0 / 32; ++p) {
     if (p + 1 < kD0 / 32) {   // the next y tile's loads fly under this tile's MFMAs
@@ -207,7 +229,7 @@ _Pragma("unroll")
   // ---- Linear(128, 64), Linear(64, 32)
   f32x16 x2[kD2 / 32];
 #pragma unroll
-  for (int m = 0; m < kD2 / 32; ++m) x2[m] = bias_tile(a.b2, m, h, kD2);
+  for (int m = 0; m < kD2 / 32; ++m) x2[m] = bias_tile(bs2, m, h, kD2);
 #pragma unroll
   for (int p = 0; p < kD1 / 32; ++p) {
     PBN_CHUNK(8 + p, {
@@ -217,7 +239,7 @@ _Pragma("unroll")
   }
 #pragma unroll
   for (int m = 0; m < kD2 / 32; ++m) x2[m] = leaky(x2[m], a.slope);
-  f32x16 x3 = bias_tile(a.b3, 0, h, kD3);
+  f32x16 x3 = bias_tile(bs3, 0, h, kD3);
 #pragma unroll
   for (int p = 0; p < kD2 / 32; ++p) {
     PBN_CHUNK(12 + p, { x3 = mfma_tile(x3, lds_w(buf, 0, lane), x2[p]); });
@@ -229,7 +251,7 @@ _Pragma("unroll")
   for (int k = 0; k < a.n_heads; ++k) {
     f32x16 z[kDH / 32];
 #pragma unroll
-    for (int m = 0; m < kDH / 32; ++m) z[m] = bias_tile(a.bh1 + kDH * k, m, h, kDH);
+    for (int m = 0; m < kDH / 32; ++m) z[m] = bias_tile(bsh1 + kDH * k, m, h, kDH);
     PBN_CHUNK(14 + 3 * k, {
 _Pragma("unroll")
       for (int m = 0; m < kDH / 32; ++m) z[m] = mfma_tile(z[m], lds_w(buf, m, lane), x3);
@@ -238,7 +260,7 @@ _Pragma("unroll")
     for (int m = 0; m < kDH / 32; ++m) z[m] = leaky(z[m], a.slope);
     f32x16 o[AT];
 #pragma unroll
-    for (int m = 0; m < AT; ++m) o[m] = bias_tile(a.bh2 + (size_t)A * k, m, h, A);
+    for (int m = 0; m < AT; ++m) o[m] = bias_tile(bsh2 + A * k, m, h, A);
 #pragma unroll
     for (int p = 0; p < kDH / 32; ++p) {
       PBN_CHUNK(15 + 3 * k + p, {

@@ -6,7 +6,8 @@ REV=${1:-HEAD}
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 TMP=$(mktemp -d)
 git -C "$ROOT" archive "$REV" pbn_rl_amd/csrc include | tar -x -C "$TMP"
+srcs=("$TMP"/pbn_rl_amd/csrc/*.hip)   # every translation unit of that revision
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wno-unused-result \
-  -o "$ROOT/pbn_rl_amd/libpbn_env_diag_base.so" "$TMP/pbn_rl_amd/csrc/pbn_env.hip" "$TMP/pbn_rl_amd/csrc/pbn_agent.hip"
+  -o "$ROOT/pbn_rl_amd/libpbn_env_diag_base.so" "${srcs[@]}"
 rm -rf "$TMP"
 echo "built $REV -> pbn_rl_amd/libpbn_env_diag_base.so"

@@ -15,6 +15,8 @@
 #   bdq-learn        BDQ training frames at 32,768 envs
 #   ubench           tools/ubench_valu_issue (VALU issue rates by instruction and waves per SIMD)
 #   nofinal          the driver's command and 2,000 steps without s' (--no-final-state)
+#   ab               A/B: the driver's command, 2,000 steps and the BDQ frame, first with
+#                    pbn_rl_amd/libpbn_env_diag_base.so (tools/ab_build.sh REV), then this tree
 set -o pipefail
 tag=$1; shift
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -51,6 +53,14 @@ for step in "$@"; do
     nofinal)
       bench bench_driver_nofinal --gpus 1 --steps 20 --warmup 5 --no-final-state --no-cpu-baseline
       bench bench_s2000_nofinal --steps 2000 --warmup 200 --no-final-state --no-cpu-baseline ;;
+    ab)
+      for side in base tree; do
+        if [ $side = base ]; then export PBN_LIB=$PWD/pbn_rl_amd/libpbn_env_diag_base.so; else unset PBN_LIB; fi
+        bench ab_${side}_driver --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-gather
+        bench ab_${side}_s2000 --steps 2000 --warmup 200 --no-cpu-baseline --no-gather
+        bench ab_${side}_bdq --workload bdq --no-cpu-baseline
+      done
+      unset PBN_LIB ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
