@@ -42,6 +42,8 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FP32_MATRIX_TFLOPS = 157.3  # MI355X FP32 MFMA/vector peak (MI355X_MICROARCH.md)
+L2_PEAK_GBS = 34500.0  # aggregate L2 bandwidth, 8 XCDs (MI355X_MICROARCH.md L2 section)
+BDQ_PMC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_bdq_pbn28_32768.json")
 # VALU issue: 256 CUs x 4 SIMD-32 x 2.4 GHz, one wave64 instruction per 2 cycles per SIMD
 # (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles")
 VALU_WAVE_INSTS_PER_S = 256 * 4 * 2.4e9 / 2
@@ -621,6 +623,18 @@ def main():
                                                     "note": "the reference forward's FLOPs (bilinear as N*N*256 "
                                                             "MACs/env) over the whole frame time; the frame "
                                                             "executes ~4x fewer"}}
+            # what bounds it: the per-set-bit table rows, read from L2.  Algorithmic L2 bytes =
+            # envs x mean set bits of s x one 256-float row
+            st = env.state[:, : env.num_envs]
+            set_bits = sum(int(((st >> b) & 1).sum().item()) for b in range(32)) / env.num_envs
+            l2_bytes = n * set_bits * out_dim * 4
+            l2 = l2_bytes / (bil_ms * 1e-3) / 1e9
+            roofline["l2"] = {"achieved": l2, "peak": L2_PEAK_GBS, "unit": "GB/s", "frac": l2 / L2_PEAK_GBS,
+                              "bytes_per_launch": l2_bytes, "mean_set_bits": set_bits,
+                              "note": "table-row bytes the kernel sums (envs x set bits x 1 KB) over its launch time"}
+            if os.path.exists(BDQ_PMC) and spec.n == 28 and n == 32768:
+                with open(BDQ_PMC) as f:
+                    roofline["l2"]["counters"] = json.load(f)["kernels"].get("bilinear_targets_kernel")
         elif agent is not None:
             roofline = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                         "traffic": None, "kernel": kernel, "launch_ms": frame_ms,

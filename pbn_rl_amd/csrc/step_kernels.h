@@ -207,16 +207,16 @@ __device__ __forceinline__ uint32_t ext64(uint32_t& hi, uint32_t& lo, uint32_t K
 // The LDS table image from global memory, all of a thread's loads issued before its stores
 // (four loads in flight per thread, where a load-store loop waits once per element)
 __device__ __forceinline__ void copy_image(uint32_t* L, const StepArgs& a) {
+  // LDS-DMA (global_load_lds_dwordx4): every wave issues its share of the image at once, with no
+  // VGPR round trip; the destination of a wave-instruction is base + 16 B x lane, so wave w
+  // moves uint4s [base, base + 64) of each blockDim-wide stripe.  The caller's barrier waits for it.
+  const int n4 = a.tab_words >> 2, lane = (int)threadIdx.x & 63;
   const uint4* src = reinterpret_cast<const uint4*>(a.tab);
-  uint4* dst = reinterpret_cast<uint4*>(L);
-  const int n4 = a.tab_words >> 2, bd = (int)blockDim.x;
-  int k = (int)threadIdx.x;
-  for (; k + 3 * bd < n4; k += 4 * bd) {
-    const uint4 v0 = src[CK(k, n4, 5)], v1 = src[CK(k + bd, n4, 5)];
-    const uint4 v2 = src[CK(k + 2 * bd, n4, 5)], v3 = src[CK(k + 3 * bd, n4, 5)];
-    dst[k] = v0; dst[k + bd] = v1; dst[k + 2 * bd] = v2; dst[k + 3 * bd] = v3;
+  for (int base = (int)threadIdx.x - lane; base < n4; base += (int)blockDim.x) {
+    if (base + lane < n4)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + base + lane),
+                                       (__attribute__((address_space(3))) void*)(L + 4 * base), 16, 0, 0);
   }
-  for (; k < n4; k += bd) dst[k] = src[CK(k, n4, 5)];
 }
 
 // LDS hash of the attractor states, slot-major: slot s holds its key words at [s * HS, s * HS +

@@ -13,8 +13,11 @@
 #   pbn70            config 3: pbn70 x 1,048,576 envs, 200 steps
 #   bdq              config 5: the BDQ frame at 32,768 envs (+ kernel trace)
 #   bdq-learn        BDQ training frames at 32,768 envs
+#   bdqpmc           the BDQ frame under two PMC passes: L2 hits / misses / requests, HBM fetch + write
 #   ubench           tools/ubench_valu_issue (VALU issue rates by instruction and waves per SIMD)
 #   nofinal          the driver's command and 2,000 steps without s' (--no-final-state)
+#   abenv            every pbn_rl_amd/libpbn_env_diag_*.so, then this tree: tests/test_gpu_parity.py,
+#                    the driver's command and 2,000 steps (env rollout variants)
 #   ab               A/B: the driver's command, 2,000 steps and the BDQ frame, first with
 #                    pbn_rl_amd/libpbn_env_diag_base.so (tools/ab_build.sh REV), then this tree
 set -o pipefail
@@ -46,6 +49,14 @@ for step in "$@"; do
       bench bench_bdq --workload bdq
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/bdq_trace" -o run -- \
         python bench.py --workload bdq --no-cpu-baseline > "$out/bdq_trace.json" 2> "$out/bdq_trace.err" || fail bdq-trace ;;
+    bdqpmc)
+      timeout -k 10 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum --kernel-trace --stats --output-format csv \
+        -d "$out/bdq_pmc_l2" -o run -- python bench.py --workload bdq --no-cpu-baseline > /dev/null 2> "$out/bdq_pmc_l2.err" || fail bdqpmc-l2
+      timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --stats --output-format csv \
+        -d "$out/bdq_pmc_fetch" -o run -- python bench.py --workload bdq --no-cpu-baseline > /dev/null 2> "$out/bdq_pmc_fetch.err" || fail bdqpmc-fetch
+      timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats --output-format csv \
+        -d "$out/bdq_pmc_write" -o run -- python bench.py --workload bdq --no-cpu-baseline > /dev/null 2> "$out/bdq_pmc_write.err" || fail bdqpmc-write
+      echo "bdqpmc done" ;;
     bdq-learn) bench bench_bdq_learn --workload bdq-learn ;;
     ubench)
       timeout -k 10 300 tools/ubench_valu_issue > "$out/ubench_valu_issue.jsonl" 2> "$out/ubench.err" || fail ubench
@@ -59,6 +70,16 @@ for step in "$@"; do
         bench ab_${side}_driver --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-gather
         bench ab_${side}_s2000 --steps 2000 --warmup 200 --no-cpu-baseline --no-gather
         bench ab_${side}_bdq --workload bdq --no-cpu-baseline
+      done
+      unset PBN_LIB ;;
+    abenv)
+      for lib in pbn_rl_amd/libpbn_env_diag_*.so tree; do
+        side=$(basename "$lib" .so); side=${side#libpbn_env_diag_}
+        if [ "$lib" = tree ]; then unset PBN_LIB; else export PBN_LIB=$PWD/$lib; fi
+        timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread \
+          > "$out/abenv_${side}_parity.log" 2>&1 || { tail -20 "$out/abenv_${side}_parity.log"; fail "abenv $side parity"; }
+        bench abenv_${side}_driver --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-gather
+        bench abenv_${side}_s2000 --steps 2000 --warmup 200 --no-cpu-baseline --no-gather
       done
       unset PBN_LIB ;;
     *) echo "unknown step $step"; exit 2 ;;
