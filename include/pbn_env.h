@@ -19,7 +19,8 @@
  *   BranchingDQN.predict + list(action.unique())
  *        bdq_model/__init__.py:69-98,176                       -> pbn_bilinear_targets (first layer),
  *                                                                 pbn_qnet_heads (the other layers),
- *                                                                 pbn_heads_to_flipmask / pbn_q_to_flipmask
+ *                                                                 pbn_heads_to_flipmask / pbn_q_to_flipmask,
+ *                                                                 or pbn_qnet_flipmask (both in one)
  *   update_policy's np.stack of sampled Transitions
  *        bdq_model/__init__.py:100-109                         -> pbn_obs_unpack
  *   a frame loop captured once and replayed (no reference counterpart)
@@ -300,6 +301,21 @@ int pbn_qnet_heads(const pbn_net* net, int64_t n_envs, const float* d_y, const f
                    const float* d_w2, const float* d_b2, const float* d_w3, const float* d_b3, const float* d_wh1,
                    const float* d_bh1, const float* d_wh2, const float* d_bh2, int32_t n_heads, int32_t n_actions,
                    float slope, float* d_heads, void* stream);
+
+/*
+ * pbn_qnet_heads and pbn_heads_to_flipmask in one launch: the same layers, then, per env, the
+ * dueling combination, epsilon-greedy and flip masks exactly as pbn_heads_to_flipmask computes
+ * them (same q_a order, same EXPLORE draws), without the (K+1, n, A) head outputs in HBM.
+ * Arguments as those two functions (n_branches = K, the heads are K + 1; n_actions = N + 1);
+ * d_step / d_epsilon, when non-null, are read when the kernel runs (graph replays).
+ *   bdq_model/__init__.py:69-98,176 (predict + list(action.unique())) after the bilinear layer
+ */
+int pbn_qnet_flipmask(const pbn_net* net, uint64_t seed, uint64_t step, const uint64_t* d_step, uint64_t env_offset,
+                      int64_t n_envs, const float* d_y, const float* d_w1, const float* d_b1, const float* d_w2,
+                      const float* d_b2, const float* d_w3, const float* d_b3, const float* d_wh1, const float* d_bh1,
+                      const float* d_wh2, const float* d_bh2, int32_t n_branches, int32_t n_actions, float slope,
+                      float epsilon, const float* d_epsilon, uint32_t* d_flipmask, int32_t* d_actions,
+                      void* stream);
 
 const char* pbn_last_error(void);
 int pbn_abi_version(void);

@@ -9,6 +9,7 @@ flips node a-1 for every action a > 0 (:81-84,176-177).  Here one frame covers a
     pbn_bilinear_targets   packed state + target id -> the bilinear layer (+ LeakyReLU)   (HIP)
     pbn_qnet_heads         the rest of the network -> raw head outputs (4, n, N+1)         (HIP, MFMA)
     pbn_heads_to_flipmask  dueling combination + epsilon-greedy -> flip-mask words (W, n)  (HIP)
+    pbn_qnet_flipmask      the two above in one launch (act_q, BatchedBDQ.step)           (HIP)
     pbn_step               the PBN transition                                             (HIP)
 
 (``fused_tail=False`` runs the layers after the bilinear one in PyTorch instead.)
@@ -327,9 +328,39 @@ class BatchedBDQ:
         return env.flipmask
 
     @torch.no_grad()
+    def act_q(self, epsilon: Optional[float] = None, step_t: Optional[torch.Tensor] = None,
+              epsilon_t: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``predict`` + epsilon-greedy for every env (bdq_model/__init__.py:69-98): Q of the
+        current observations -> env.flipmask and self.actions.  With the fused tail this is
+        pbn_bilinear_targets + pbn_qnet_flipmask (no head outputs in HBM), else q_heads() +
+        act_heads(); both give the same actions.  ``step_t`` / ``epsilon_t`` as act_heads."""
+        if not (self.fast and self.fused_tail):
+            return self.act_heads(self.q_heads(), epsilon, step_t=step_t, epsilon_t=epsilon_t)
+        env, m = self.env, self.q.model
+        if step_t is not None and (step_t.dtype != torch.int64 or step_t.numel() != 1):
+            raise ValueError("step_t must be a one-element int64 tensor")
+        if epsilon_t is not None and (epsilon_t.dtype != torch.float32 or epsilon_t.numel() != 1):
+            raise ValueError("epsilon_t must be a one-element float32 tensor")
+        w1, b1, w2, b2 = self.bilinear()
+        ts = [m[2].weight, m[2].bias, m[4].weight, m[4].bias, m[6].weight, m[6].bias, w1, b1, w2, b2]
+        ts = [t.detach().contiguous() for t in ts]
+        eps = self.epsilon if epsilon is None else float(epsilon)
+        L = _lib.load()
+        with torch.cuda.device(env.device):
+            _lib.check(L.pbn_qnet_flipmask(env.net.handle, env.seed, env.step_index,
+                                           step_t.data_ptr() if step_t is not None else None,
+                                           env.env_offset, env.n_alloc, self._y.data_ptr(),
+                                           *[t.data_ptr() for t in ts], self.branches, env.n_nodes + 1,
+                                           self._slope, eps,
+                                           epsilon_t.data_ptr() if epsilon_t is not None else None,
+                                           env.flipmask.data_ptr(), self.actions.data_ptr(), env._stream()),
+                       "pbn_qnet_flipmask")
+        return env.flipmask
+
+    @torch.no_grad()
     def step(self, epsilon: Optional[float] = None):
         """One frame for every env; returns (state', reward, flags) views as VectorPBNEnv.step_flipmask."""
-        self.act_heads(self.q_heads(), epsilon)
+        self.act_q(epsilon)
         return self.env.step_flipmask(use_current=True)
 
 

@@ -26,6 +26,7 @@
 
 #include "../../include/pbn_env.h"
 #include "net_view.h"
+#include "philox.h"
 
 namespace {
 
@@ -42,11 +43,21 @@ struct QnetArgs {
   const float *w1, *b1, *w2, *b2, *w3, *b3;
   const float *wh1, *bh1;          // [64 H][32], [64 H]
   const float *wh2, *bh2;          // [H][A][64], [H][A]
-  float* heads;                    // [H][n][A]
+  float* heads;                    // [H][n][A] (FLIP = false)
   int64_t n;
   int n_heads, n_act;
   float slope;
+  // FLIP = true: the acting epilogue of pbn_heads_to_flipmask in place of the head outputs
+  uint64_t seed, step, env_offset, eps_u;
+  const uint64_t* d_step;          // step index in device memory (graph replays), or null
+  const float* d_eps;              // epsilon in device memory, or null
+  uint32_t* flipmask;              // [W][n]
+  int32_t* actions;                // [n][H - 1], or null
+  int n_nodes, W;
 };
+
+constexpr int kPitch = 36;                 // weight-chunk row pitch in LDS (floats)
+constexpr int kBufFloats = 128 * kPitch;   // one buffer: up to 128 rows
 
 __device__ __forceinline__ int feat_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
@@ -71,22 +82,36 @@ __device__ __forceinline__ f32x16 leaky(f32x16 x, float slope) {
   return x;
 }
 
-// The A operand of k-steps (tile p, registers 4q .. 4q+3), q = 0..3: one float4 of weight row
-// 32 m + (lane & 31) at column 32 p + 8 q + 4 h
-struct WTile {
-  float4 w[4];
-};
-
-// acc += W-tile . X over the 16 k-steps of one input tile
-__device__ __forceinline__ f32x16 mfma_tile(f32x16 acc, const WTile& t, const f32x16& X) {
+// acc[m] += W[32 m .., chunk] . X over the 16 k-steps of one 32-column chunk, m < MT.  The A
+// operand of k-steps (registers 4q .. 4q+3) is one float4 of weight row 32 m + (lane & 31) at
+// column 8 q + 4 h.  The MT tiles' float4s of group q + 1 are read while group q's MFMAs run,
+// and the MT accumulators interleave, so no MFMA waits on its LDS read or on the MFMA before it.
+template <int MT>
+__device__ __forceinline__ void mfma_chunk(f32x16 (&acc)[MT], const float* __restrict__ buf, int lane,
+                                           const f32x16& X) {
+  const float* r = buf + (lane & 31) * kPitch + 4 * (lane >> 5);
+  float4 w[MT], wn[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) w[m] = *reinterpret_cast<const float4*>(r + 32 * m * kPitch);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    acc = mfma(t.w[q].x, X[4 * q + 0], acc);
-    acc = mfma(t.w[q].y, X[4 * q + 1], acc);
-    acc = mfma(t.w[q].z, X[4 * q + 2], acc);
-    acc = mfma(t.w[q].w, X[4 * q + 3], acc);
+    if (q < 3) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) wn[m] = *reinterpret_cast<const float4*>(r + 32 * m * kPitch + 8 * (q + 1));
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = mfma(w[m].x, X[4 * q + 0], acc[m]);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = mfma(w[m].y, X[4 * q + 1], acc[m]);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = mfma(w[m].z, X[4 * q + 2], acc[m]);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = mfma(w[m].w, X[4 * q + 3], acc[m]);
+    if (q < 3) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) w[m] = wn[m];
+    }
   }
-  return acc;
 }
 
 // The weights reach the MFMAs through LDS as one stream of chunks, double-buffered: a chunk
@@ -97,8 +122,6 @@ __device__ __forceinline__ f32x16 mfma_tile(f32x16 acc, const WTile& t, const f3
 // rows one read's quarter-wave touches start on 16 distinct 4-bank groups.  The stream:
 //   Linear(256, 128): 8 chunks | Linear(128, 64): 4 | Linear(64, 32): 2 |
 //   per head k: Linear(32, 64): 1, Linear(64, A): 2
-constexpr int kPitch = 36;
-constexpr int kBufFloats = 128 * kPitch;   // one buffer: up to 128 rows
 
 struct Chunk {
   const float* src;   // column 0 of the chunk in the row-major weight matrix
@@ -114,15 +137,48 @@ __device__ __forceinline__ Chunk chunk_of(const QnetArgs& a, int c) {
   return {a.wh2 + (size_t)a.n_act * kDH * k + 32 * (j - 1), kDH, a.n_act};
 }
 
-__device__ __forceinline__ WTile lds_w(const float* __restrict__ buf, int m, int lane) {
-  const float* r = buf + (32 * m + (lane & 31)) * kPitch + 4 * (lane >> 5);
-  WTile t;
+
+// The dueling combination and argmax of one advantage head, as pbn_heads_to_flipmask computes
+// them (pbn_agent.hip, q_to_flipmask_kernel): q_a = (v + adv_a) - mean, mean = the left-to-right
+// float32 sum of adv_0 .. adv_{A-1} over A, torch.argmax's first maximum with NaN maximal.
+// Action a = 32 m + f of the env sits in register (f & 3) + 4 (f >> 3) of tile m on lane half
+// (f >> 2) & 1; the halves swap their registers once, so both walk the row in order.
+template <int AT>
+__device__ __forceinline__ int dueling_argmax(const f32x16 (&o)[AT], int h, int A, float v) {
+  float oth[AT][16];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) t.w[q] = *reinterpret_cast<const float4*>(r + 8 * q);
-  return t;
+  for (int m = 0; m < AT; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) oth[m][r] = __shfl_xor(o[m][r], 32);
+  auto at = [&](int m, int f) {
+    const int r = (f & 3) + 4 * (f >> 3);
+    return ((f >> 2) & 1) == h ? o[m][r] : oth[m][r];
+  };
+  float sum = 0.f;
+#pragma unroll
+  for (int m = 0; m < AT; ++m)
+#pragma unroll
+    for (int f = 0; f < 32; ++f)
+      if (32 * m + f < A) sum += at(m, f);
+  const float mean = sum / (float)A;
+  float best = (v + at(0, 0)) - mean;
+  int bi = 0;
+#pragma unroll
+  for (int m = 0; m < AT; ++m)
+#pragma unroll
+    for (int f = 0; f < 32; ++f) {
+      const int act = 32 * m + f;
+      if (act >= 1 && act < A) {
+        const float qa = (v + at(m, f)) - mean;
+        const bool take = !isnan(best) && (isnan(qa) || qa > best);
+        best = take ? qa : best;
+        bi = take ? act : bi;
+      }
+    }
+  return bi;
 }
 
-template <int AT>   // output tiles of the second head layers: A <= 32 AT
+template <int AT, bool FLIP>   // AT: output tiles of the second head layers, A <= 32 AT
 __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
   __shared__ __attribute__((aligned(16))) float wbuf[2 * kBufFloats];
   const int lane = threadIdx.x & 63;
@@ -217,8 +273,7 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
       X[4 * q + 0] = yv[q].x; X[4 * q + 1] = yv[q].y; X[4 * q + 2] = yv[q].z; X[4 * q + 3] = yv[q].w;
     }
     PBN_CHUNK(p, {
-_Pragma("unroll")
-      for (int m = 0; m < kD1 / 32; ++m) x1[m] = mfma_tile(x1[m], lds_w(buf, m, lane), X);
+      mfma_chunk<kD1 / 32>(x1, buf, lane, X);
     });
 #pragma unroll
     for (int q = 0; q < 4; ++q) yv[q] = yn[q];
@@ -233,28 +288,43 @@ _Pragma("unroll")
 #pragma unroll
   for (int p = 0; p < kD1 / 32; ++p) {
     PBN_CHUNK(8 + p, {
-_Pragma("unroll")
-      for (int m = 0; m < kD2 / 32; ++m) x2[m] = mfma_tile(x2[m], lds_w(buf, m, lane), x1[p]);
+      mfma_chunk<kD2 / 32>(x2, buf, lane, x1[p]);
     });
   }
 #pragma unroll
   for (int m = 0; m < kD2 / 32; ++m) x2[m] = leaky(x2[m], a.slope);
-  f32x16 x3 = bias_tile(bs3, 0, h, kD3);
+  f32x16 x3[1] = {bias_tile(bs3, 0, h, kD3)};
 #pragma unroll
   for (int p = 0; p < kD2 / 32; ++p) {
-    PBN_CHUNK(12 + p, { x3 = mfma_tile(x3, lds_w(buf, 0, lane), x2[p]); });
+    PBN_CHUNK(12 + p, { mfma_chunk<1>(x3, buf, lane, x2[p]); });
   }
-  x3 = leaky(x3, a.slope);
+  x3[0] = leaky(x3[0], a.slope);
 
   // ---- heads: Linear(32, 64) + LeakyReLU per head (stacked rows 64 k .. 64 k + 63), then
-  // Linear(64, A) of that head's 64 features; raw outputs to heads[k][e][a]
+  // Linear(64, A) of that head's 64 features; raw outputs to heads[k][e][a], or (FLIP) the
+  // value, then each branch's action into the flip mask
+  float v = 0.f;
+  bool explore = false;
+  pbn::Word4 r0{0u, 0u, 0u, 0u}, r1{0u, 0u, 0u, 0u};
+  uint32_t mk[4] = {0u, 0u, 0u, 0u};
+  if constexpr (FLIP) {   // the EXPLORE draws of env e (both lane halves draw the same)
+    const uint64_t ge = a.env_offset + (uint64_t)e;
+    const uint64_t st = a.d_step ? *a.d_step : a.step;
+    uint64_t eps_u = a.eps_u;
+    if (a.d_eps) {   // device epsilon (graph replays): clamped to [0, 1], NaN -> 0
+      const float ef = fminf(fmaxf(*a.d_eps, 0.f), 1.f);
+      eps_u = (uint64_t)floor((double)ef * 4294967296.0);
+    }
+    r0 = pbn::draw(a.seed, ge, st, pbn::kStreamExplore, 0);
+    if (a.n_heads > 4) r1 = pbn::draw(a.seed, ge, st, pbn::kStreamExplore, 1);
+    explore = (uint64_t)r0.x < eps_u;
+  }
   for (int k = 0; k < a.n_heads; ++k) {
     f32x16 z[kDH / 32];
 #pragma unroll
     for (int m = 0; m < kDH / 32; ++m) z[m] = bias_tile(bsh1 + kDH * k, m, h, kDH);
     PBN_CHUNK(14 + 3 * k, {
-_Pragma("unroll")
-      for (int m = 0; m < kDH / 32; ++m) z[m] = mfma_tile(z[m], lds_w(buf, m, lane), x3);
+      mfma_chunk<kDH / 32>(z, buf, lane, x3[0]);
     });
 #pragma unroll
     for (int m = 0; m < kDH / 32; ++m) z[m] = leaky(z[m], a.slope);
@@ -264,11 +334,30 @@ _Pragma("unroll")
 #pragma unroll
     for (int p = 0; p < kDH / 32; ++p) {
       PBN_CHUNK(15 + 3 * k + p, {
-_Pragma("unroll")
-        for (int m = 0; m < AT; ++m) o[m] = mfma_tile(o[m], lds_w(buf, m, lane), z[p]);
+        mfma_chunk<AT>(o, buf, lane, z[p]);
       });
     }
-    if (live) {
+    if constexpr (FLIP) {
+      if (k == 0) {
+        v = __shfl(o[0][0], lane & 31);   // value head output 0: register 0 of lane half 0
+      } else {
+        const int b = k - 1;   // branch
+        int act;
+        if (explore) {   // branch b: EXPLORE word b + 1 across calls 0 and 1, onto [0, N]
+          const uint32_t rw = b == 0 ? r0.y : b == 1 ? r0.z : b == 2 ? r0.w : b == 3 ? r1.x
+                            : b == 4 ? r1.y : b == 5 ? r1.z : r1.w;
+          act = (int)__umulhi(rw, (uint32_t)(a.n_nodes + 1));
+        } else {
+          act = dueling_argmax<AT>(o, h, A, v);
+        }
+        if (act > 0 && act <= a.n_nodes) {   // a > 0 flips node a - 1, once however often
+#pragma unroll
+          for (int w = 0; w < 4; ++w)
+            if (w == ((act - 1) >> 5)) mk[w] |= 1u << ((act - 1) & 31);
+        }
+        if (a.actions && live && h == 0) a.actions[e * (a.n_heads - 1) + b] = act;
+      }
+    } else if (live) {
       float* out = a.heads + ((size_t)k * a.n + e) * A;
 #pragma unroll
       for (int m = 0; m < AT; ++m) {
@@ -280,12 +369,48 @@ _Pragma("unroll")
       }
     }
   }
+  if constexpr (FLIP) {
+    if (live && h == 0) {
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+        if (w < a.W) a.flipmask[(size_t)w * a.n + e] = mk[w];
+    }
+  }
 #undef PBN_CHUNK
 #undef PBN_PUT
 #undef PBN_FETCH
 }
 
 bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+int qnet_check(const pbn_net* net, int64_t n_envs, const float* d_y, const float* d_w1, const float* d_b1,
+                      const float* d_w2, const float* d_b2, const float* d_w3, const float* d_b3, const float* d_wh1,
+                      const float* d_bh1, const float* d_wh2, const float* d_bh2, int32_t n_heads, int32_t n_actions) {
+  int rc = pbn::check_device(net);
+  if (rc) return rc;
+  if (n_envs < 0 || (n_envs & 31)) return pbn::set_error(PBN_EINVAL, "n_envs must be a non-negative multiple of 32");
+  if (n_heads < 1 || n_heads > kMaxHeads) return pbn::set_error(PBN_EINVAL, "n_heads must be 1..8");
+  if (n_actions < 1 || n_actions > 32 * kMaxActTiles) return pbn::set_error(PBN_EINVAL, "n_actions must be 1..128");
+  if (n_envs == 0) return PBN_OK;
+  if (!d_y || !d_w1 || !d_b1 || !d_w2 || !d_b2 || !d_w3 || !d_b3 || !d_wh1 || !d_bh1 || !d_wh2 || !d_bh2)
+    return pbn::set_error(PBN_EINVAL, "null buffer");
+  // float4 weight-row and y loads: rows of 256 / 128 / 64 / 32 floats start 16-byte aligned
+  // when the base is; the second head layer's rows are 64 floats
+  if (!al16(d_y) || !al16(d_w1) || !al16(d_w2) || !al16(d_w3) || !al16(d_wh1) || !al16(d_wh2))
+    return pbn::set_error(PBN_EINVAL, "y and weight buffers must be 16-byte aligned");
+  return PBN_OK;
+}
+
+template <bool FLIP>
+int qnet_launch(const QnetArgs& a, void* stream) {
+  const int64_t waves = a.n / 32;
+  const unsigned blocks = (unsigned)((waves + kWaves - 1) / kWaves);
+  void (*kernels[kMaxActTiles])(QnetArgs) = {qnet_tail_kernel<1, FLIP>, qnet_tail_kernel<2, FLIP>,
+                                              qnet_tail_kernel<3, FLIP>, qnet_tail_kernel<4, FLIP>};
+  hipLaunchKernelGGL(kernels[(a.n_act + 31) / 32 - 1], dim3(blocks), dim3(64 * kWaves), 0, (hipStream_t)stream, a);
+  if (hipGetLastError() != hipSuccess) return pbn::set_error(PBN_EDEVICE, "qnet_tail_kernel launch failed");
+  return PBN_OK;
+}
 
 }  // namespace
 
@@ -295,27 +420,46 @@ int pbn_qnet_heads(const pbn_net* net, int64_t n_envs, const float* d_y, const f
                    const float* d_w2, const float* d_b2, const float* d_w3, const float* d_b3, const float* d_wh1,
                    const float* d_bh1, const float* d_wh2, const float* d_bh2, int32_t n_heads, int32_t n_actions,
                    float slope, float* d_heads, void* stream) {
-  int rc = pbn::check_device(net);
+  int rc = qnet_check(net, n_envs, d_y, d_w1, d_b1, d_w2, d_b2, d_w3, d_b3, d_wh1, d_bh1, d_wh2, d_bh2, n_heads,
+                      n_actions);
+  if (rc || n_envs == 0) return rc;
+  if (!d_heads) return pbn::set_error(PBN_EINVAL, "null buffer");
+  QnetArgs a{};
+  a.y = d_y; a.w1 = d_w1; a.b1 = d_b1; a.w2 = d_w2; a.b2 = d_b2; a.w3 = d_w3; a.b3 = d_b3;
+  a.wh1 = d_wh1; a.bh1 = d_bh1; a.wh2 = d_wh2; a.bh2 = d_bh2; a.heads = d_heads;
+  a.n = n_envs; a.n_heads = n_heads; a.n_act = n_actions; a.slope = slope;
+  return qnet_launch<false>(a, stream);
+}
+
+int pbn_qnet_flipmask(const pbn_net* net, uint64_t seed, uint64_t step, const uint64_t* d_step, uint64_t env_offset,
+                      int64_t n_envs, const float* d_y, const float* d_w1, const float* d_b1, const float* d_w2,
+                      const float* d_b2, const float* d_w3, const float* d_b3, const float* d_wh1, const float* d_bh1,
+                      const float* d_wh2, const float* d_bh2, int32_t n_branches, int32_t n_actions, float slope,
+                      float epsilon, const float* d_epsilon, uint32_t* d_flipmask, int32_t* d_actions,
+                      void* stream) {
+  pbn::NetView v;
+  int rc = pbn::net_view(net, &v);
   if (rc) return rc;
-  if (n_envs < 0 || (n_envs & 31)) return pbn::set_error(PBN_EINVAL, "n_envs must be a non-negative multiple of 32");
-  if (n_heads < 1 || n_heads > kMaxHeads) return pbn::set_error(PBN_EINVAL, "n_heads must be 1..8");
-  if (n_actions < 1 || n_actions > 32 * kMaxActTiles) return pbn::set_error(PBN_EINVAL, "n_actions must be 1..128");
+  if (n_branches < 1 || n_branches > kMaxHeads - 1) return pbn::set_error(PBN_EINVAL, "n_branches must be 1..7");
+  if ((rc = qnet_check(net, n_envs, d_y, d_w1, d_b1, d_w2, d_b2, d_w3, d_b3, d_wh1, d_bh1, d_wh2, d_bh2,
+                       n_branches + 1, n_actions)))
+    return rc;
+  if (env_offset & 31) return pbn::set_error(PBN_EINVAL, "env_offset must be a multiple of 32");
+  if (n_actions != v.n_nodes + 1) return pbn::set_error(PBN_EINVAL, "n_actions must be n_nodes + 1");
+  if (!(epsilon >= 0.f && epsilon <= 1.f)) return pbn::set_error(PBN_EINVAL, "epsilon must be in [0, 1]");
+  if (d_step && ((uintptr_t)d_step & 7u) != 0) return pbn::set_error(PBN_EINVAL, "d_step must be 8-byte aligned");
+  if (d_epsilon && ((uintptr_t)d_epsilon & 3u) != 0) return pbn::set_error(PBN_EINVAL, "d_epsilon misaligned");
   if (n_envs == 0) return PBN_OK;
-  if (!d_y || !d_w1 || !d_b1 || !d_w2 || !d_b2 || !d_w3 || !d_b3 || !d_wh1 || !d_bh1 || !d_wh2 || !d_bh2 || !d_heads)
-    return pbn::set_error(PBN_EINVAL, "null buffer");
-  // float4 weight-row and y loads: rows of 256 / 128 / 64 / 32 floats start 16-byte aligned
-  // when the base is; the second head layer's rows are 64 floats
-  if (!al16(d_y) || !al16(d_w1) || !al16(d_w2) || !al16(d_w3) || !al16(d_wh1) || !al16(d_wh2))
-    return pbn::set_error(PBN_EINVAL, "y and weight buffers must be 16-byte aligned");
-  QnetArgs a{d_y, d_w1, d_b1, d_w2, d_b2, d_w3, d_b3, d_wh1, d_bh1, d_wh2, d_bh2, d_heads, n_envs, n_heads,
-             n_actions, slope};
-  const int64_t waves = n_envs / 32;
-  const unsigned blocks = (unsigned)((waves + kWaves - 1) / kWaves);
-  void (*kernels[kMaxActTiles])(QnetArgs) = {qnet_tail_kernel<1>, qnet_tail_kernel<2>, qnet_tail_kernel<3>,
-                                              qnet_tail_kernel<4>};
-  hipLaunchKernelGGL(kernels[(n_actions + 31) / 32 - 1], dim3(blocks), dim3(64 * kWaves), 0, (hipStream_t)stream, a);
-  if (hipGetLastError() != hipSuccess) return pbn::set_error(PBN_EDEVICE, "qnet_tail_kernel launch failed");
-  return PBN_OK;
+  if (!d_flipmask) return pbn::set_error(PBN_EINVAL, "null buffer");
+  QnetArgs a{};
+  a.y = d_y; a.w1 = d_w1; a.b1 = d_b1; a.w2 = d_w2; a.b2 = d_b2; a.w3 = d_w3; a.b3 = d_b3;
+  a.wh1 = d_wh1; a.bh1 = d_bh1; a.wh2 = d_wh2; a.bh2 = d_bh2;
+  a.n = n_envs; a.n_heads = n_branches + 1; a.n_act = n_actions; a.slope = slope;
+  // explore iff EXPLORE word 0 < floor(epsilon * 2^32), as pbn_q_to_flipmask
+  a.seed = seed; a.step = step; a.env_offset = env_offset; a.eps_u = (uint64_t)floor((double)epsilon * 4294967296.0);
+  a.d_step = d_step; a.d_eps = d_epsilon; a.flipmask = d_flipmask; a.actions = d_actions;
+  a.n_nodes = v.n_nodes; a.W = v.W;
+  return qnet_launch<true>(a, stream);
 }
 
 }  // extern "C"

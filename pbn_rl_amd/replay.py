@@ -201,9 +201,7 @@ class BDQLearner:
         env = self.env
         state = env.state.clone()
         target = env.target.clone()
-        with torch.no_grad():
-            heads = self.agent.q_heads()
-        self.agent.act_heads(heads, self.epsilon)
+        self.agent.act_q(self.epsilon)
         _, reward, flags = env.step_flipmask(use_current=True)
         done_all = (env.flags & (_lib.FLAG_TERMINATED | _lib.FLAG_TRUNCATED)) != 0
         # all n_alloc envs are stored (the padding envs of a ragged batch are real envs too)
@@ -263,9 +261,7 @@ class BDQLearner:
         env = self.env
         state = env.state.clone()
         target = env.target.clone()
-        with torch.no_grad():
-            heads = self.agent.q_heads()
-        self.agent.act_heads(heads, step_t=self._step_t, epsilon_t=self._eps32)
+        self.agent.act_q(step_t=self._step_t, epsilon_t=self._eps32)
         env.step_flipmask_dev(self._step_t)
         self._step_t.add_(1)
         done_all = (env.flags & (_lib.FLAG_TERMINATED | _lib.FLAG_TRUNCATED)) != 0

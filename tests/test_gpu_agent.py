@@ -303,3 +303,67 @@ def test_fused_tail_with_reference_checkpoint():
         q_ref = agent.q(agent.observe())
     torch.cuda.synchronize()
     assert torch.allclose(q_fast, q_ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("name,n,K,eps", [("pbn28", 32768, 3, 0.0), ("pbn28", 4096, 3, 0.3), ("pbn70", 2080, 3, 0.25),
+                                          ("pbn7", 96, 5, 0.0), ("pbn7", 512, 1, 0.5), ("pbn28", 1024, 3, 1.0)])
+def test_qnet_flipmask_equals_heads_path(name, n, K, eps):
+    """pbn_qnet_flipmask (the tail + dueling + epsilon-greedy in one launch, act_q) against
+    pbn_qnet_heads -> pbn_heads_to_flipmask on the same observations: flip masks and actions bit
+    for bit, and both against the oracle's restatement of the heads arithmetic; then the device
+    step / epsilon forms."""
+    spec = make_spec(name)
+    A, seed, step = spec.n + 1, 13, 29
+    torch.manual_seed(17)
+    env = VectorPBNEnv(spec, n, seed=seed)
+    agent = BatchedBDQ(env, BranchingQNetwork((spec.n, spec.n), A, K), branches=K)
+    assert agent.fused_tail
+    env.reset()
+    for _ in range(2):
+        env.step_flipmask(random_actions=True)
+    env.step_index = step
+    with torch.no_grad():
+        heads = agent.q_heads().clone()
+        agent.act_heads(heads, eps)
+        fm_ref, act_ref = env.flipmask.clone(), agent.actions.clone()
+        env.flipmask.zero_()
+        agent.actions.zero_()
+        agent.act_q(eps)
+    torch.cuda.synchronize()
+    assert torch.equal(env.flipmask, fm_ref)
+    assert torch.equal(agent.actions, act_ref)
+    flip, acts = agent_oracle.q_to_flipmask(spec, agent_oracle.heads_q(heads.cpu().numpy()), seed, step, 0, eps)
+    assert np.array_equal(u32(env.flipmask), flip) and np.array_equal(agent.actions.cpu().numpy(), acts)
+    step_t = torch.full((1,), step, dtype=torch.int64, device="cuda")
+    eps_t = torch.full((1,), eps, dtype=torch.float32, device="cuda")
+    env.flipmask.zero_()
+    env.step_index = step + 5          # ignored: the device step wins
+    agent.act_q(0.77, step_t=step_t, epsilon_t=eps_t)
+    torch.cuda.synchronize()
+    assert torch.equal(env.flipmask, fm_ref)
+
+
+def test_qnet_flipmask_rejects_bad_arguments():
+    spec = make_spec("pbn28")
+    env = VectorPBNEnv(spec, 64, seed=1)
+    agent = BatchedBDQ(env, BranchingQNetwork((28, 28), 29, 3))
+    L = _lib.load()
+    m = agent.q.model
+    w1, b1, w2, b2 = agent.q.head_weights()
+    ts = [agent._y, m[2].weight, m[2].bias, m[4].weight, m[4].bias, m[6].weight, m[6].bias, w1, b1, w2, b2]
+    ptrs = [t.data_ptr() for t in ts]
+    fm = env.flipmask.data_ptr()
+    h = env.net.handle
+    ok = (h, 1, 0, None, 0, 64, *ptrs, 3, 29, 0.01, 0.0, None, fm, None, None)
+    assert L.pbn_qnet_flipmask(*ok) == 0
+    bad = list(ok); bad[17] = 0                      # n_branches
+    assert L.pbn_qnet_flipmask(*bad) == -22
+    bad = list(ok); bad[18] = 30                     # n_actions != N + 1
+    assert L.pbn_qnet_flipmask(*bad) == -22
+    bad = list(ok); bad[20] = 1.5                    # epsilon
+    assert L.pbn_qnet_flipmask(*bad) == -22
+    bad = list(ok); bad[4] = 16                      # env_offset
+    assert L.pbn_qnet_flipmask(*bad) == -22
+    bad = list(ok); bad[22] = None                   # flipmask
+    assert L.pbn_qnet_flipmask(*bad) == -22
+    torch.cuda.synchronize()
