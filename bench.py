@@ -114,6 +114,13 @@ def qnet_flops_per_env(n: int, branches: int = 3) -> int:
     return 2 * macs
 
 
+def qnet_tail_flops_per_env(n: int, branches: int = 3) -> int:
+    """FLOPs of the layers after the bilinear one per env (pbn_qnet_flipmask): trunk 256-128-64-32,
+    K + 1 first head layers 32-64, value 64-1, K advantage layers 64-(N+1)."""
+    macs = 256 * 128 + 128 * 64 + 64 * 32 + (branches + 1) * 32 * 64 + 64 + branches * 64 * (n + 1)
+    return 2 * macs
+
+
 def algorithmic_bytes_per_env(words: int) -> int:
     # read: state 4W, t 1, target 1 ; write: flipmask (in-kernel actions) 4W,
     # state_out 4W, reward 4, flags 1, t 1   (target is rewritten only on reset)
@@ -581,60 +588,74 @@ def main():
                                 "wire_bytes_per_env_step": wire // (env.n_alloc * args.steps),
                                 "records": "s, a, s' (final_state), r, flags of every env-step"}
 
-    bil_ms = None
-    if args.workload == "bdq":
+    bil_ms = tail_ms = None
+    if args.workload == "bdq":   # the frame's two long launches, each timed alone (50 back to back)
         def bil():
             for _ in range(50):
                 agent.bilinear()
         with torch.cuda.stream(stream):
-            agent.bilinear()
+            hw = agent.bilinear()
             bil_ms, _ = timed(bil, stream, dev, world, local)
             bil_ms /= 50
+            if agent.fused_tail:
+                def tail():
+                    for _ in range(50):
+                        agent.tail_flipmask(hw, args.epsilon)
+                agent.tail_flipmask(hw, args.epsilon)
+                tail_ms, _ = timed(tail, stream, dev, world, local)
+                tail_ms /= 50
 
     if rank == 0:
         W = spec.words
         pmc, pmc_path = (None, None) if agent is not None else pmc_profile(args, plan)
         if agent is not None:
-            kernel = ("BDQ frame (pbn_bilinear_targets, BranchingQNetwork fp32 layers after the bilinear, "
-                      "pbn_heads_to_flipmask, pbn_step)")
+            kernel = ("BDQ frame (pbn_bilinear_targets, pbn_qnet_flipmask: the fp32 MFMA layers after the "
+                      "bilinear + dueling + epsilon-greedy, pbn_step)")
             if args.workload == "bdq-learn":
                 kernel += " + replay store + update_policy (batch 256)"
                 kernel += ", one hipGraph replay per frame" if args.learn_graph else ", eager"
         frame_ms = dev_ms / args.steps
         if args.workload == "bdq":
-            # dominant launch: pbn_bilinear_targets.  HBM bytes it must move per frame: the packed
-            # state and target id in, the (n, 256) fp32 layer out, the per-target table and bias
-            # once; the table rows it sums come from L2 (a few hundred KB, re-read by every env)
+            # dominant launch: pbn_qnet_flipmask, MFMA-bound.  Algorithmic FLOPs = the layers after
+            # the bilinear one (qnet_tail_flops_per_env), fp32 MFMA peak
             out_dim = agent.q.model[0].output_dim
             n = env.n_alloc
             A = max(1, len(spec.attractors))
-            bil_bytes = n * (4 * W + 1) + n * out_dim * 4 + A * spec.n * out_dim * 4 + out_dim * 4
-            achieved = bil_bytes / (bil_ms * 1e-3) / 1e9
             flops = env.n_alloc * qnet_flops_per_env(spec.n)
-            roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                        "kernel": "pbn_bilinear_targets (the frame's longest launch)", "launch_ms": bil_ms,
-                        "bytes_per_launch": bil_bytes,
-                        "note": "bytes = state+target in, the (n,256) fp32 layer out, the per-target table once; "
-                                "the per-set-bit row sums are L2 reads (the kernel is L2-bound), so the HBM "
-                                "fraction understates how busy it is",
-                        "model_flops_utilisation": {"achieved_tflops": flops / (frame_ms * 1e-3) / 1e12,
-                                                    "peak_tflops": FP32_MATRIX_TFLOPS,
-                                                    "note": "the reference forward's FLOPs (bilinear as N*N*256 "
-                                                            "MACs/env) over the whole frame time; the frame "
-                                                            "executes ~4x fewer"}}
-            # what bounds it: the per-set-bit table rows, read from L2.  Algorithmic L2 bytes =
-            # envs x mean set bits of s x one 256-float row
+            mfu = {"achieved_tflops": flops / (frame_ms * 1e-3) / 1e12, "peak_tflops": FP32_MATRIX_TFLOPS,
+                   "note": "the reference forward's FLOPs (bilinear as N*N*256 MACs/env) over the whole frame "
+                           "time; the frame executes ~4x fewer"}
+            if tail_ms is not None:
+                tail_flops = n * qnet_tail_flops_per_env(spec.n, agent.branches)
+                tf = tail_flops / (tail_ms * 1e-3) / 1e12
+                roofline = {"bound": "mfma", "achieved": tf, "peak": FP32_MATRIX_TFLOPS, "unit": "TFLOP/s",
+                            "frac": tf / FP32_MATRIX_TFLOPS, "traffic": None,
+                            "kernel": "pbn_qnet_flipmask (the frame's longest launch)", "launch_ms": tail_ms,
+                            "flops_per_launch": tail_flops,
+                            "note": "v_mfma_f32_32x32x2_f32 (exact f32), one wave per 32 envs; FLOPs = the "
+                                    "Linear layers after the bilinear one (trunk 256-128-64-32, K+1 heads 32-64-A)",
+                            "model_flops_utilisation": mfu}
+            else:
+                roofline = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                            "traffic": None, "kernel": "frame (PyTorch tail)", "launch_ms": frame_ms,
+                            "model_flops_utilisation": mfu}
+            # the second launch, pbn_bilinear_targets: the per-set-bit table rows it sums are L2
+            # reads.  Algorithmic L2 bytes = envs x mean set bits of s x one 256-float row
+            bil_bytes = n * (4 * W + 1) + n * out_dim * 4 + A * spec.n * out_dim * 4 + out_dim * 4
             st = env.state[:, : env.num_envs]
             set_bits = sum(int(((st >> b) & 1).sum().item()) for b in range(32)) / env.num_envs
             l2_bytes = n * set_bits * out_dim * 4
             l2 = l2_bytes / (bil_ms * 1e-3) / 1e9
-            roofline["l2"] = {"achieved": l2, "peak": L2_PEAK_GBS, "unit": "GB/s", "frac": l2 / L2_PEAK_GBS,
-                              "bytes_per_launch": l2_bytes, "mean_set_bits": set_bits,
-                              "note": "table-row bytes the kernel sums (envs x set bits x 1 KB) over its launch time"}
+            roofline["bilinear"] = {"launch_ms": bil_ms, "hbm_GBps": bil_bytes / (bil_ms * 1e-3) / 1e9,
+                                    "hbm_bytes_per_launch": bil_bytes,
+                                    "l2": {"achieved": l2, "peak": L2_PEAK_GBS, "unit": "GB/s",
+                                           "frac": l2 / L2_PEAK_GBS, "bytes_per_launch": l2_bytes,
+                                           "mean_set_bits": set_bits,
+                                           "note": "table-row bytes the kernel sums (envs x set bits x 1 KB) "
+                                                   "over its launch time"}}
             if os.path.exists(BDQ_PMC) and spec.n == 28 and n == 32768:
                 with open(BDQ_PMC) as f:
-                    roofline["l2"]["counters"] = json.load(f)["kernels"].get("bilinear_targets_kernel")
+                    roofline["bilinear"]["counters"] = json.load(f)["kernels"].get("bilinear_targets_kernel")
         elif agent is not None:
             roofline = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                         "traffic": None, "kernel": kernel, "launch_ms": frame_ms,

@@ -336,12 +336,18 @@ class BatchedBDQ:
         act_heads(); both give the same actions.  ``step_t`` / ``epsilon_t`` as act_heads."""
         if not (self.fast and self.fused_tail):
             return self.act_heads(self.q_heads(), epsilon, step_t=step_t, epsilon_t=epsilon_t)
-        env, m = self.env, self.q.model
         if step_t is not None and (step_t.dtype != torch.int64 or step_t.numel() != 1):
             raise ValueError("step_t must be a one-element int64 tensor")
         if epsilon_t is not None and (epsilon_t.dtype != torch.float32 or epsilon_t.numel() != 1):
             raise ValueError("epsilon_t must be a one-element float32 tensor")
-        w1, b1, w2, b2 = self.bilinear()
+        return self.tail_flipmask(self.bilinear(), epsilon, step_t, epsilon_t)
+
+    def tail_flipmask(self, hw, epsilon: Optional[float] = None, step_t: Optional[torch.Tensor] = None,
+                      epsilon_t: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """The ``pbn_qnet_flipmask`` launch of act_q on the current bilinear output self._y
+        (``hw``: the head weights bilinear() returned)."""
+        env, m = self.env, self.q.model
+        w1, b1, w2, b2 = hw
         ts = [m[2].weight, m[2].bias, m[4].weight, m[4].bias, m[6].weight, m[6].bias, w1, b1, w2, b2]
         ts = [t.detach().contiguous() for t in ts]
         eps = self.epsilon if epsilon is None else float(epsilon)

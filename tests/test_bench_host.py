@@ -98,3 +98,12 @@ def test_spawn_path_in_a_fresh_interpreter_never_touches_hip():
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
                        cwd=str(__import__('pathlib').Path(bench.__file__).parent))
     assert r.returncode == 0 and r.stdout.strip().endswith("False"), r.stderr
+
+
+def test_qnet_tail_flops_count_the_layers_after_the_bilinear():
+    import bench
+    # Bittner-28, 3 branches: trunk 256*128 + 128*64 + 64*32, 4 first head layers 32*64,
+    # value 64*1, 3 advantage layers 64*29 multiply-adds
+    macs = 32768 + 8192 + 2048 + 4 * 2048 + 64 + 3 * 64 * 29
+    assert bench.qnet_tail_flops_per_env(28, 3) == 2 * macs
+    assert bench.qnet_flops_per_env(28, 3) - bench.qnet_tail_flops_per_env(28, 3) == 2 * 28 * 28 * 256
