@@ -17,7 +17,7 @@
 #   ubench           tools/ubench_valu_issue (VALU issue rates by instruction and waves per SIMD)
 #   nofinal          the driver's command and 2,000 steps without s' (--no-final-state)
 #   abenv            every pbn_rl_amd/libpbn_env_diag_*.so, then this tree: tests/test_gpu_parity.py,
-#                    the driver's command and 2,000 steps (env rollout variants)
+#                    the driver's command, 2,000 steps and 1M envs (env rollout variants)
 #   ab               A/B: the driver's command, 2,000 steps and the BDQ frame, first with
 #                    pbn_rl_amd/libpbn_env_diag_base.so (tools/ab_build.sh REV), then this tree
 set -o pipefail
@@ -80,6 +80,7 @@ for step in "$@"; do
           > "$out/abenv_${side}_parity.log" 2>&1 || { tail -20 "$out/abenv_${side}_parity.log"; fail "abenv $side parity"; }
         bench abenv_${side}_driver --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-gather
         bench abenv_${side}_s2000 --steps 2000 --warmup 200 --no-cpu-baseline --no-gather
+        bench abenv_${side}_1m --envs 1048576 --steps 300 --warmup 50 --no-cpu-baseline --no-gather
       done
       unset PBN_LIB ;;
     *) echo "unknown step $step"; exit 2 ;;
