@@ -16,6 +16,8 @@
 
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
 
@@ -135,6 +137,117 @@ __global__ void __launch_bounds__(kBilThreads) bilinear_targets_kernel(const uin
       y4[o4] = acc;
     }
   }
+}
+
+// The same layer with the table staged in LDS.  The rows an env sums are T[target][i] for its
+// set bits i, 1 KB each: read from L2 that is ~750 MB per 32,768 Bittner-28 envs, and the kernel
+// above runs at two thirds of the L2 bandwidth.  A block of kBlEnvs envs instead walks the
+// outputs in 32-wide tiles and stages tile p's slice of the whole table, T[.][.][32p, 32p + 32)
+// (A N rows of 128 B, 50 KB for Bittner-28), in LDS once: L2 reads drop to A N x 1 KB per
+// block, and the gathers hit LDS.  The slices are copied by LDS-DMA (global_load_lds_dwordx4: a
+// wave-instruction fills 1 KB of LDS linearly, eight rows, with no VGPR round trip) and
+// double-buffered, so the next slice lands while this tile is summed; the bias is staged once
+// beside them (an ordinary global load in the loop would make the compiler drain the DMA).
+// TPE threads per env, each owning 32 / TPE outputs of the tile; the sum order is the kernel
+// above's (bias, then the rows in ascending i), so the two agree bit for bit.
+constexpr int kBlEnvs = 128;
+constexpr int kBlBatch = 4;   // set bits whose rows are read before they are added
+constexpr int kBlTpe = 4;     // threads per env (2 measured 46 us against 29.6 us at 32,768 envs)
+
+template <int W, int TPE>
+__global__ void __launch_bounds__(kBlEnvs * TPE) bilinear_lds_kernel(const uint32_t* __restrict__ state,
+                                                                      const uint8_t* __restrict__ target,
+                                                                      const float* __restrict__ T,
+                                                                      const float* __restrict__ bias, int N, int A,
+                                                                      int O, uint32_t n, int leaky, float slope,
+                                                                      float* __restrict__ y) {
+  constexpr int kThreads = kBlEnvs * TPE;
+  constexpr int Q = 8 / TPE;   // float4s of the tile per thread
+  extern __shared__ __attribute__((aligned(16))) float sl[];   // [2][A N][32] | bias [O]
+  const int rows = A * N;
+  const int slice = rows * 32;
+  float* sbias = sl + 2 * slice;
+  const int t = (int)threadIdx.x;
+  const int lane = t & 63;
+  const int sub = t % TPE;
+  const uint32_t e = blockIdx.x * kBlEnvs + (uint32_t)(t / TPE);
+  const bool live = e < n;
+  const uint32_t tg = live ? (uint32_t)target[e] : 0xFFu;
+  const bool has_t = tg < (uint32_t)A;
+  uint32_t words[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) words[w] = (live && has_t) ? state[(size_t)w * n + e] : 0u;
+  for (int i = t; i < O; i += kThreads) sbias[i] = bias[i];
+  // the state word has landed before any DMA is issued (its first use behind one would drain it)
+#pragma unroll
+  for (int w = 0; w < W; ++w) asm volatile("" ::"v"(words[w]));
+  const int rowbase = has_t ? (int)tg * N : 0;
+  const int n_items = rows * 8;   // float4s of one slice
+  const float4* T4 = reinterpret_cast<const float4*>(T);
+  // slice p into buffer b: LDS float4 P = 64 j' + lane of the wave's stripes holds row P >> 3,
+  // columns 32p + 4 (P & 7) .. + 3
+#define PBN_BL_STAGE(p_, b_)                                                                       \
+  for (int base = t - lane; base < n_items; base += kThreads) {                                    \
+    const int P = base + lane;                                                                     \
+    if (P < n_items)                                                                               \
+      __builtin_amdgcn_global_load_lds(                                                            \
+          (__attribute__((address_space(1))) void*)(T4 + (size_t)(P >> 3) * (O >> 2) + 8 * (p_) + (P & 7)), \
+          (__attribute__((address_space(3))) void*)(sl + (b_) * slice + 4 * base), 16, 0, 0);      \
+  }
+  const int n_tiles = O >> 5;
+  PBN_BL_STAGE(0, 0)
+  __syncthreads();
+  for (int p = 0; p < n_tiles; ++p) {
+    if (p + 1 < n_tiles) { PBN_BL_STAGE(p + 1, (p + 1) & 1) }
+    const float* S = sl + (p & 1) * slice + 4 * Q * sub;
+    float4 acc[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) acc[q] = *reinterpret_cast<const float4*>(sbias + 32 * p + 4 * (Q * sub + q));
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      uint32_t b = words[w];
+      while (b) {
+        int idx[kBlBatch];
+#pragma unroll
+        for (int k = 0; k < kBlBatch; ++k) {
+          idx[k] = b ? 32 * w + __builtin_ctz(b) : -1;
+          b = b ? (b & (b - 1u)) : 0u;
+        }
+        float4 v[kBlBatch][Q];
+#pragma unroll
+        for (int k = 0; k < kBlBatch; ++k) {
+          const float4* r = reinterpret_cast<const float4*>(S + (rowbase + (idx[k] >= 0 ? idx[k] : 0)) * 32);
+#pragma unroll
+          for (int q = 0; q < Q; ++q) v[k][q] = r[q];
+        }
+#pragma unroll
+        for (int k = 0; k < kBlBatch; ++k) {
+          if (idx[k] >= 0) {
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+              acc[q].x += v[k][q].x; acc[q].y += v[k][q].y; acc[q].z += v[k][q].z; acc[q].w += v[k][q].w;
+            }
+          }
+        }
+      }
+    }
+    if (live) {
+      float4* yo = reinterpret_cast<float4*>(y + (size_t)e * O) + 8 * p + Q * sub;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        float4 a = acc[q];
+        if (leaky) {   // torch's LeakyReLU: x > 0 ? x : x * slope
+          a.x = a.x > 0.f ? a.x : a.x * slope;
+          a.y = a.y > 0.f ? a.y : a.y * slope;
+          a.z = a.z > 0.f ? a.z : a.z * slope;
+          a.w = a.w > 0.f ? a.w : a.w * slope;
+        }
+        yo[q] = a;
+      }
+    }
+    __syncthreads();   // (waits for the next slice's DMA: vmcnt(0))
+  }
+#undef PBN_BL_STAGE
 }
 
 // torch.argmax semantics: the first maximal index; NaN counts as the maximum
@@ -283,8 +396,37 @@ int pbn_bilinear_targets(const pbn_net* net, int64_t n_envs, const uint32_t* d_s
   if (!d_state || !d_target || !d_bias || !d_y || (v.n_attr > 0 && !d_T)) return pbn::set_error(PBN_EINVAL, "null buffer");
   if (!aligned16(d_bias) || !aligned16(d_y) || (d_T && !aligned16(d_T)))
     return pbn::set_error(PBN_EINVAL, "d_T, d_bias and d_y must be 16-byte aligned");
-  const unsigned blocks = (unsigned)((n_envs + kBilEnvs - 1) / kBilEnvs);
   const uint32_t n = (uint32_t)n_envs;
+  // the LDS-staged kernel when both table slices fit (A N <= 556 rows: Bittner-28's 14 x 28 and
+  // pbn7's; not pbn70's 16 x 70) and the outputs come in 32-wide tiles; PBN_BILINEAR=l2 forces
+  // the L2 kernel (tests compare the two)
+  const size_t lds = (2 * (size_t)v.n_attr * v.n_nodes * 32 + (size_t)out_dim) * sizeof(float);
+  const char* force = getenv("PBN_BILINEAR");
+  if (v.n_attr > 0 && (out_dim & 31) == 0 && lds <= 140 * 1024 && !(force && !strcmp(force, "l2"))) {
+    using K = void (*)(const uint32_t*, const uint8_t*, const float*, const float*, int, int, int, uint32_t, int,
+                       float, float*);
+    static const K kerns[4] = {bilinear_lds_kernel<1, kBlTpe>, bilinear_lds_kernel<2, kBlTpe>,
+                               bilinear_lds_kernel<3, kBlTpe>, bilinear_lds_kernel<4, kBlTpe>};
+    const K kern = kerns[v.W - 1];
+    if (lds > 64 * 1024) {
+      static bool raised[64] = {};
+      const int dv = v.device >= 0 && v.device < 64 ? v.device : 0;
+      if (!raised[dv]) {
+        for (int w = 0; w < 4; ++w)
+          if (hipFuncSetAttribute(reinterpret_cast<const void*>(kerns[w]), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024) != hipSuccess)
+            return pbn::set_error(PBN_EDEVICE, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+        raised[dv] = true;
+      }
+    }
+    const unsigned bl = (unsigned)((n_envs + kBlEnvs - 1) / kBlEnvs);
+    hipLaunchKernelGGL(kern, dim3(bl), dim3(kBlEnvs * kBlTpe), lds, (hipStream_t)stream, d_state, d_target, d_T, d_bias,
+                       v.n_nodes, v.n_attr, out_dim, n, leaky, slope, d_y);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return pbn::set_error(PBN_EDEVICE, hipGetErrorString(e));
+    return PBN_OK;
+  }
+  const unsigned blocks = (unsigned)((n_envs + kBilEnvs - 1) / kBilEnvs);
   switch (v.W) {
     case 1: hipLaunchKernelGGL(bilinear_targets_kernel<1>, dim3(blocks), dim3(kBilThreads), 0, (hipStream_t)stream,
                                d_state, d_target, d_T, d_bias, v.n_nodes, v.n_attr, out_dim, n, leaky, slope, d_y); break;

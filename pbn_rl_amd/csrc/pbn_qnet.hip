@@ -36,6 +36,9 @@ constexpr int kD0 = 256, kD1 = 128, kD2 = 64, kD3 = 32, kDH = 64;   // Branching
 constexpr int kMaxHeads = 8;                                         // value + up to 7 branches
 constexpr int kMaxActTiles = 4;                                      // A <= 128 (pbn70: 71)
 constexpr int kWaves = 4;                                            // waves (32-env tiles) per block
+constexpr int kStageRows = 8 * kWaves;                               // weight rows per staging pass
+constexpr int kStagePasses = 128 / kStageRows;                       // 4 or 8
+static_assert(kStagePasses == 4 || kStagePasses == 8, "staging covers 128 rows in 4 or 8 passes");
 constexpr int kBiasFloats = kD1 + kD2 + kD3 + (kDH + 32 * kMaxActTiles) * kMaxHeads;
 
 struct QnetArgs {
@@ -189,34 +192,34 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
   const int A = a.n_act;
   const int n_chunks = 14 + 3 * a.n_heads;
 
-  // staging: thread t moves float4 (row (t >> 3) + 32 j, columns 4 (t & 7) .. +3), j = 0..3
+  // staging: thread t moves float4 (row (t >> 3) + kStageRows j, columns 4 (t & 7) .. +3), j <
+  // kStagePasses (128 rows in all)
   const int t = threadIdx.x;
   const int srow = t >> 3, scol = 4 * (t & 7);
-  float4 s0, s1, s2, s3;
+  float4 s0, s1, s2, s3, s4, s5, s6, s7;
   int srows = 0;
+#define PBN_LD(sj, j)                                                                              \
+  sj = *reinterpret_cast<const float4*>(p_ + (size_t)min(srow + kStageRows * (j), last_) * ch_.ld)
 #define PBN_FETCH(c_)                                                                              \
   do {                                                                                             \
     const Chunk ch_ = chunk_of(a, (c_));                                                           \
     const float* p_ = ch_.src + scol;                                                              \
     const int last_ = ch_.rows - 1; /* rows past the matrix load its last row, then read as 0 */   \
-    s0 = *reinterpret_cast<const float4*>(p_ + (size_t)min(srow, last_) * ch_.ld);                 \
-    s1 = *reinterpret_cast<const float4*>(p_ + (size_t)min(srow + 32, last_) * ch_.ld);            \
-    s2 = *reinterpret_cast<const float4*>(p_ + (size_t)min(srow + 64, last_) * ch_.ld);            \
-    s3 = *reinterpret_cast<const float4*>(p_ + (size_t)min(srow + 96, last_) * ch_.ld);            \
+    PBN_LD(s0, 0); PBN_LD(s1, 1); PBN_LD(s2, 2); PBN_LD(s3, 3);                                    \
+    if constexpr (kStagePasses > 4) { PBN_LD(s4, 4); PBN_LD(s5, 5); PBN_LD(s6, 6); PBN_LD(s7, 7); } \
     srows = ch_.rows;                                                                              \
+  } while (0)
+#define PBN_ST(sj, j)                                                                              \
+  do {                                                                                             \
+    if (srow + kStageRows * (j) >= srows) sj = z_;                                                 \
+    *reinterpret_cast<float4*>(d_ + kStageRows * (j) * kPitch) = sj;                               \
   } while (0)
 #define PBN_PUT(b_)                                                                                \
   do {                                                                                             \
     float* d_ = wbuf + (b_) * kBufFloats + srow * kPitch + scol;                                   \
     const float4 z_ = make_float4(0.f, 0.f, 0.f, 0.f); /* masked here, not at the load: a select */ \
-    if (srow >= srows) s0 = z_;                        /* on the loaded value would wait for it */ \
-    if (srow + 32 >= srows) s1 = z_;                                                               \
-    if (srow + 64 >= srows) s2 = z_;                                                               \
-    if (srow + 96 >= srows) s3 = z_;                                                               \
-    *reinterpret_cast<float4*>(d_) = s0;                                                           \
-    *reinterpret_cast<float4*>(d_ + 32 * kPitch) = s1;                                             \
-    *reinterpret_cast<float4*>(d_ + 64 * kPitch) = s2;                                             \
-    *reinterpret_cast<float4*>(d_ + 96 * kPitch) = s3;                                             \
+    PBN_ST(s0, 0); PBN_ST(s1, 1); PBN_ST(s2, 2); PBN_ST(s3, 3); /* on the loaded value waits */    \
+    if constexpr (kStagePasses > 4) { PBN_ST(s4, 4); PBN_ST(s5, 5); PBN_ST(s6, 6); PBN_ST(s7, 7); } \
   } while (0)
   // one chunk step: the next chunk's loads (kept above the MFMAs by the scheduling barriers:
   // LLVM would sink them to their LDS stores and expose their L2 round trip), this chunk's
@@ -378,7 +381,9 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
   }
 #undef PBN_CHUNK
 #undef PBN_PUT
+#undef PBN_ST
 #undef PBN_FETCH
+#undef PBN_LD
 }
 
 bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }

@@ -367,3 +367,26 @@ def test_qnet_flipmask_rejects_bad_arguments():
     bad = list(ok); bad[22] = None                   # flipmask
     assert L.pbn_qnet_flipmask(*bad) == -22
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("name,n", [("pbn28", 32768), ("pbn7", 4096), ("pbn28", 96)])
+def test_bilinear_lds_equals_l2_kernel(name, n, monkeypatch):
+    """pbn_bilinear_targets' LDS-staged kernel (the default where the table slices fit) against
+    its L2 kernel (PBN_BILINEAR=l2): the same sums in the same order, bit for bit; ragged last
+    block, envs without a target (bias only) included."""
+    spec = make_spec(name)
+    torch.manual_seed(21)
+    env = VectorPBNEnv(spec, n, seed=3)
+    agent = BatchedBDQ(env, BranchingQNetwork((spec.n, spec.n), spec.n + 1, 3))
+    env.reset()
+    for _ in range(2):
+        env.step_flipmask(random_actions=True)
+    env.target[::7] = 0xFF
+    with torch.no_grad():
+        agent.bilinear()
+        y_lds = agent._y.clone()
+        monkeypatch.setenv("PBN_BILINEAR", "l2")
+        agent.bilinear()
+        y_l2 = agent._y.clone()
+    torch.cuda.synchronize()
+    assert torch.equal(y_lds, y_l2)
