@@ -9,17 +9,19 @@
 // combines (dueling) and argmaxes -- in one launch where PyTorch spends four GEMMs and three
 // elementwise launches.
 //
-// Layout: one wave per 32 envs, feature-major.  Every layer is out^T = W . in^T on
-// v_mfma_f32_32x32x2_f32 (exact f32: a k-ordered fmaf chain): the envs are the 32 MFMA
-// columns (lane & 31), the output features the rows, so an accumulator tile of one layer is
-// the B operand of the next with no data movement: register r of a 32-feature tile holds
-// feature row(r, h) = (r & 3) + 8 (r >> 2) + 4 h on lane half h, and k-step (tile p, register
-// r) of the next layer takes lane half h's element from there.  The A operand (weights) is
-// then W[out][32 p + row(r, h)], i.e. for r = 4q .. 4q+3 four consecutive inputs: one float4
-// read of the weight row per four MFMAs (from LDS: the weight stream below).
+// Layout: one wave per 16 envs, feature-major.  Every layer is out^T = W . in^T on
+// v_mfma_f32_16x16x4_f32 (exact f32): the envs are the 16 MFMA columns (lane & 15), the output
+// features the rows, so an accumulator tile of one layer is the B operand of the next with no
+// data movement: register i of a 16-feature tile holds feature 4 g + i on lane group g = lane >> 4,
+// and k-step (tile p, register i) of the next layer takes group g's element from there, i.e.
+// inputs 16 p + 4 g + i.  The A operand (weights) is then W[out][16 p + 4 g + i] for i = 0..3:
+// one float4 of the weight row per four MFMAs (from LDS: the weight stream below).  Sixteen envs
+// per wave make 2,048 waves at config 5's 32,768 envs, two per SIMD: one wave's barriers, LDS
+// reads and epilogue run under the other's MFMAs (with 32 envs per wave on the 32x32x2 form, one
+// wave per SIMD, the kernel took 51 us against 28 us of MFMA issue).
 // Biases initialise the accumulators; LeakyReLU (x > 0 ? x : x * slope, torch's form) is
-// applied in registers between layers.  y is read in the same feature order (four float4 per
-// lane per 32-feature tile).
+// applied in registers between layers.  y is read in the same feature order (one float4 per lane
+// per 16-feature tile).
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -30,15 +32,16 @@
 
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kD0 = 256, kD1 = 128, kD2 = 64, kD3 = 32, kDH = 64;   // BranchingQNetwork widths
 constexpr int kMaxHeads = 8;                                         // value + up to 7 branches
-constexpr int kMaxActTiles = 4;                                      // A <= 128 (pbn70: 71)
-constexpr int kWaves = 4;                                            // waves (32-env tiles) per block
+constexpr int kMaxActTiles = 4;                                      // A <= 128 (pbn70: 71), 32 per tile
+constexpr int kEnvs = 16;                                            // envs per wave
+constexpr int kWaves = 8;                                            // waves per block (128 envs)
 constexpr int kStageRows = 8 * kWaves;                               // weight rows per staging pass
-constexpr int kStagePasses = 128 / kStageRows;                       // 4 or 8
-static_assert(kStagePasses == 4 || kStagePasses == 8, "staging covers 128 rows in 4 or 8 passes");
+constexpr int kStagePasses = 128 / kStageRows;                       // 2, 4 or 8
+static_assert(kStagePasses == 2 || kStagePasses == 4 || kStagePasses == 8, "staging covers 128 rows");
 constexpr int kBiasFloats = kD1 + kD2 + kD3 + (kDH + 32 * kMaxActTiles) * kMaxHeads;
 
 struct QnetArgs {
@@ -62,59 +65,56 @@ struct QnetArgs {
 constexpr int kPitch = 36;                 // weight-chunk row pitch in LDS (floats)
 constexpr int kBufFloats = 128 * kPitch;   // one buffer: up to 128 rows
 
-__device__ __forceinline__ int feat_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
-
-__device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+__device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// acc = bias of the 32 output features 32 m + row(r, h) (0 past n_out; b in LDS)
-__device__ __forceinline__ f32x16 bias_tile(const float* __restrict__ b, int m, int h, int n_out) {
-  f32x16 acc;
+// acc = bias of the output features 16 m + 4 g + i (0 past n_out; b in LDS)
+__device__ __forceinline__ f32x4 bias_tile(const float* __restrict__ b, int m, int g, int n_out) {
+  f32x4 acc;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int o = 32 * m + feat_row(r, h);
-    acc[r] = o < n_out ? b[o] : 0.f;
+  for (int i = 0; i < 4; ++i) {
+    const int o = 16 * m + 4 * g + i;
+    acc[i] = o < n_out ? b[o] : 0.f;
   }
   return acc;
 }
 
-__device__ __forceinline__ f32x16 leaky(f32x16 x, float slope) {
+__device__ __forceinline__ f32x4 leaky(f32x4 x, float slope) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) x[r] = x[r] > 0.f ? x[r] : x[r] * slope;
+  for (int i = 0; i < 4; ++i) x[i] = x[i] > 0.f ? x[i] : x[i] * slope;
   return x;
 }
 
-// acc[m] += W[32 m .., chunk] . X over the 16 k-steps of one 32-column chunk, m < MT.  The A
-// operand of k-steps (registers 4q .. 4q+3) is one float4 of weight row 32 m + (lane & 31) at
-// column 8 q + 4 h.  The MT tiles' float4s of group q + 1 are read while group q's MFMAs run,
-// and the MT accumulators interleave, so no MFMA waits on its LDS read or on the MFMA before it.
+// acc[m] += W[16 m .., chunk] . X over the 8 k-steps of one 32-column chunk (input tiles X0,
+// X1), m < MT.  The A operand of tile p's k-steps is one float4 of weight row 16 m + (lane & 15)
+// at column 16 p + 4 g; tile 1's float4s are read while tile 0's MFMAs run, and the MT
+// accumulators interleave.
 template <int MT>
-__device__ __forceinline__ void mfma_chunk(f32x16 (&acc)[MT], const float* __restrict__ buf, int lane,
-                                           const f32x16& X) {
-  const float* r = buf + (lane & 31) * kPitch + 4 * (lane >> 5);
+__device__ __forceinline__ void mfma_chunk(f32x4 (&acc)[MT], const float* __restrict__ buf, int lane,
+                                           const f32x4& X0, const f32x4& X1) {
+  const float* r = buf + (lane & 15) * kPitch + 4 * (lane >> 4);
   float4 w[MT], wn[MT];
 #pragma unroll
-  for (int m = 0; m < MT; ++m) w[m] = *reinterpret_cast<const float4*>(r + 32 * m * kPitch);
+  for (int m = 0; m < MT; ++m) w[m] = *reinterpret_cast<const float4*>(r + 16 * m * kPitch);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    if (q < 3) {
+  for (int m = 0; m < MT; ++m) wn[m] = *reinterpret_cast<const float4*>(r + 16 * m * kPitch + 16);
 #pragma unroll
-      for (int m = 0; m < MT; ++m) wn[m] = *reinterpret_cast<const float4*>(r + 32 * m * kPitch + 8 * (q + 1));
-    }
+  for (int m = 0; m < MT; ++m) acc[m] = mfma(w[m].x, X0[0], acc[m]);
 #pragma unroll
-    for (int m = 0; m < MT; ++m) acc[m] = mfma(w[m].x, X[4 * q + 0], acc[m]);
+  for (int m = 0; m < MT; ++m) acc[m] = mfma(w[m].y, X0[1], acc[m]);
 #pragma unroll
-    for (int m = 0; m < MT; ++m) acc[m] = mfma(w[m].y, X[4 * q + 1], acc[m]);
+  for (int m = 0; m < MT; ++m) acc[m] = mfma(w[m].z, X0[2], acc[m]);
 #pragma unroll
-    for (int m = 0; m < MT; ++m) acc[m] = mfma(w[m].z, X[4 * q + 2], acc[m]);
+  for (int m = 0; m < MT; ++m) acc[m] = mfma(w[m].w, X0[3], acc[m]);
 #pragma unroll
-    for (int m = 0; m < MT; ++m) acc[m] = mfma(w[m].w, X[4 * q + 3], acc[m]);
-    if (q < 3) {
+  for (int m = 0; m < MT; ++m) acc[m] = mfma(wn[m].x, X1[0], acc[m]);
 #pragma unroll
-      for (int m = 0; m < MT; ++m) w[m] = wn[m];
-    }
-  }
+  for (int m = 0; m < MT; ++m) acc[m] = mfma(wn[m].y, X1[1], acc[m]);
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acc[m] = mfma(wn[m].z, X1[2], acc[m]);
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acc[m] = mfma(wn[m].w, X1[3], acc[m]);
 }
 
 // The weights reach the MFMAs through LDS as one stream of chunks, double-buffered: a chunk
@@ -144,35 +144,33 @@ __device__ __forceinline__ Chunk chunk_of(const QnetArgs& a, int c) {
 // The dueling combination and argmax of one advantage head, as pbn_heads_to_flipmask computes
 // them (pbn_agent.hip, q_to_flipmask_kernel): q_a = (v + adv_a) - mean, mean = the left-to-right
 // float32 sum of adv_0 .. adv_{A-1} over A, torch.argmax's first maximum with NaN maximal.
-// Action a = 32 m + f of the env sits in register (f & 3) + 4 (f >> 3) of tile m on lane half
-// (f >> 2) & 1; the halves swap their registers once, so both walk the row in order.
-template <int AT>
-__device__ __forceinline__ int dueling_argmax(const f32x16 (&o)[AT], int h, int A, float v) {
-  float oth[AT][16];
+// Action a = 16 m + 4 g + i of the env sits in register i of tile m on lane group g; every lane
+// gathers its env's row from the four groups, so all four walk it in order.
+template <int T16>
+__device__ __forceinline__ int dueling_argmax(const f32x4 (&o)[T16], int lane, int A, float v) {
+  float row[T16][4][4];   // [m][g][i]
 #pragma unroll
-  for (int m = 0; m < AT; ++m)
+  for (int m = 0; m < T16; ++m)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) oth[m][r] = __shfl_xor(o[m][r], 32);
-  auto at = [&](int m, int f) {
-    const int r = (f & 3) + 4 * (f >> 3);
-    return ((f >> 2) & 1) == h ? o[m][r] : oth[m][r];
-  };
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) row[m][g][i] = __shfl(o[m][i], (lane & 15) + 16 * g);
   float sum = 0.f;
 #pragma unroll
-  for (int m = 0; m < AT; ++m)
+  for (int m = 0; m < T16; ++m)
 #pragma unroll
-    for (int f = 0; f < 32; ++f)
-      if (32 * m + f < A) sum += at(m, f);
+    for (int f = 0; f < 16; ++f)
+      if (16 * m + f < A) sum += row[m][f >> 2][f & 3];
   const float mean = sum / (float)A;
-  float best = (v + at(0, 0)) - mean;
+  float best = (v + row[0][0][0]) - mean;
   int bi = 0;
 #pragma unroll
-  for (int m = 0; m < AT; ++m)
+  for (int m = 0; m < T16; ++m)
 #pragma unroll
-    for (int f = 0; f < 32; ++f) {
-      const int act = 32 * m + f;
+    for (int f = 0; f < 16; ++f) {
+      const int act = 16 * m + f;
       if (act >= 1 && act < A) {
-        const float qa = (v + at(m, f)) - mean;
+        const float qa = (v + row[m][f >> 2][f & 3]) - mean;
         const bool take = !isnan(best) && (isnan(qa) || qa > best);
         best = take ? qa : best;
         bi = take ? act : bi;
@@ -181,14 +179,15 @@ __device__ __forceinline__ int dueling_argmax(const f32x16 (&o)[AT], int h, int 
   return bi;
 }
 
-template <int AT, bool FLIP>   // AT: output tiles of the second head layers, A <= 32 AT
+template <int AT, bool FLIP>   // AT: the second head layers' outputs in 32-row units, A <= 32 AT
 __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
+  constexpr int T16 = 2 * AT;   // 16-feature output tiles of the second head layers
   __shared__ __attribute__((aligned(16))) float wbuf[2 * kBufFloats];
   const int lane = threadIdx.x & 63;
-  const int h = lane >> 5;
-  const int64_t e0 = ((int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6)) * 32;
+  const int g = lane >> 4;
+  const int64_t e0 = ((int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6)) * kEnvs;
   const bool live = e0 < a.n;   // (a wave past the end still stages weights and meets the barriers)
-  const int64_t e = live ? e0 + (lane & 31) : 0;
+  const int64_t e = live ? e0 + (lane & 15) : 0;
   const int A = a.n_act;
   const int n_chunks = 14 + 3 * a.n_heads;
 
@@ -205,7 +204,8 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
     const Chunk ch_ = chunk_of(a, (c_));                                                           \
     const float* p_ = ch_.src + scol;                                                              \
     const int last_ = ch_.rows - 1; /* rows past the matrix load its last row, then read as 0 */   \
-    PBN_LD(s0, 0); PBN_LD(s1, 1); PBN_LD(s2, 2); PBN_LD(s3, 3);                                    \
+    PBN_LD(s0, 0); PBN_LD(s1, 1);                                                                  \
+    if constexpr (kStagePasses > 2) { PBN_LD(s2, 2); PBN_LD(s3, 3); }                              \
     if constexpr (kStagePasses > 4) { PBN_LD(s4, 4); PBN_LD(s5, 5); PBN_LD(s6, 6); PBN_LD(s7, 7); } \
     srows = ch_.rows;                                                                              \
   } while (0)
@@ -218,7 +218,8 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
   do {                                                                                             \
     float* d_ = wbuf + (b_) * kBufFloats + srow * kPitch + scol;                                   \
     const float4 z_ = make_float4(0.f, 0.f, 0.f, 0.f); /* masked here, not at the load: a select */ \
-    PBN_ST(s0, 0); PBN_ST(s1, 1); PBN_ST(s2, 2); PBN_ST(s3, 3); /* on the loaded value waits */    \
+    PBN_ST(s0, 0); PBN_ST(s1, 1);                      /* on the loaded value would wait for it */ \
+    if constexpr (kStagePasses > 2) { PBN_ST(s2, 2); PBN_ST(s3, 3); }                              \
     if constexpr (kStagePasses > 4) { PBN_ST(s4, 4); PBN_ST(s5, 5); PBN_ST(s6, 6); PBN_ST(s7, 7); } \
   } while (0)
   // one chunk step: the next chunk's loads (kept above the MFMAs by the scheduling barriers:
@@ -247,61 +248,61 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
   float* const bsh1 = bs3 + kD3;
   float* const bsh2 = bsh1 + kDH * kMaxHeads;
   for (int i = t; i < kD1; i += 64 * kWaves) bs1[i] = a.b1[i];
-  if (t < kD2) bs2[t] = a.b2[t];
-  if (t < kD3) bs3[t] = a.b3[t];
+  for (int i = t; i < kD2; i += 64 * kWaves) bs2[i] = a.b2[i];
+  for (int i = t; i < kD3; i += 64 * kWaves) bs3[i] = a.b3[i];
   for (int i = t; i < kDH * a.n_heads; i += 64 * kWaves) bsh1[i] = a.bh1[i];
   for (int i = t; i < A * a.n_heads; i += 64 * kWaves) bsh2[i] = a.bh2[i];
 
   PBN_FETCH(0);
   PBN_PUT(0);
 
-  // ---- Linear(256, 128): input tiles from y, feature order row(r, h) (four float4 per tile)
-  const float* yrow = a.y + (size_t)e * kD0 + 4 * h;
-  float4 yv[4], yn[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) yv[q] = *reinterpret_cast<const float4*>(yrow + 8 * q);
+  // ---- Linear(256, 128): input tiles from y, features 16 p + 4 g .. + 3 (one float4 per tile);
+  // a chunk is two tiles, whose loads fly one chunk ahead
+  const float* yrow = a.y + (size_t)e * kD0 + 4 * g;
+  f32x4 yv0, yv1, yn0, yn1;
+  {
+    const float4 u0 = *reinterpret_cast<const float4*>(yrow), u1 = *reinterpret_cast<const float4*>(yrow + 16);
+    yv0 = f32x4{u0.x, u0.y, u0.z, u0.w};
+    yv1 = f32x4{u1.x, u1.y, u1.z, u1.w};
+  }
   __syncthreads();   // chunk 0 and the biases are in LDS
-  f32x16 x1[kD1 / 32];
+  f32x4 x1[kD1 / 16];
 #pragma unroll
-  for (int m = 0; m < kD1 / 32; ++m) x1[m] = bias_tile(bs1, m, h, kD1);
+  for (int m = 0; m < kD1 / 16; ++m) x1[m] = bias_tile(bs1, m, g, kD1);
 #pragma unroll
   for (int p = 0; p < kD0 / 32; ++p) {
-    if (p + 1 < kD0 / 32) {   // the next y tile's loads fly under this tile's MFMAs
-#pragma unroll
-      for (int q = 0; q < 4; ++q) yn[q] = *reinterpret_cast<const float4*>(yrow + 32 * (p + 1) + 8 * q);
+    if (p + 1 < kD0 / 32) {   // the next chunk's y tiles fly under this chunk's MFMAs
+      const float4 u0 = *reinterpret_cast<const float4*>(yrow + 32 * (p + 1));
+      const float4 u1 = *reinterpret_cast<const float4*>(yrow + 32 * (p + 1) + 16);
+      yn0 = f32x4{u0.x, u0.y, u0.z, u0.w};
+      yn1 = f32x4{u1.x, u1.y, u1.z, u1.w};
     }
-    f32x16 X;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      X[4 * q + 0] = yv[q].x; X[4 * q + 1] = yv[q].y; X[4 * q + 2] = yv[q].z; X[4 * q + 3] = yv[q].w;
-    }
-    PBN_CHUNK(p, {
-      mfma_chunk<kD1 / 32>(x1, buf, lane, X);
-    });
-#pragma unroll
-    for (int q = 0; q < 4; ++q) yv[q] = yn[q];
+    PBN_CHUNK(p, { mfma_chunk<kD1 / 16>(x1, buf, lane, yv0, yv1); });
+    yv0 = yn0;
+    yv1 = yn1;
   }
 #pragma unroll
-  for (int m = 0; m < kD1 / 32; ++m) x1[m] = leaky(x1[m], a.slope);
+  for (int m = 0; m < kD1 / 16; ++m) x1[m] = leaky(x1[m], a.slope);
 
   // ---- Linear(128, 64), Linear(64, 32)
-  f32x16 x2[kD2 / 32];
+  f32x4 x2[kD2 / 16];
 #pragma unroll
-  for (int m = 0; m < kD2 / 32; ++m) x2[m] = bias_tile(bs2, m, h, kD2);
+  for (int m = 0; m < kD2 / 16; ++m) x2[m] = bias_tile(bs2, m, g, kD2);
 #pragma unroll
   for (int p = 0; p < kD1 / 32; ++p) {
-    PBN_CHUNK(8 + p, {
-      mfma_chunk<kD2 / 32>(x2, buf, lane, x1[p]);
-    });
+    PBN_CHUNK(8 + p, { mfma_chunk<kD2 / 16>(x2, buf, lane, x1[2 * p], x1[2 * p + 1]); });
   }
 #pragma unroll
-  for (int m = 0; m < kD2 / 32; ++m) x2[m] = leaky(x2[m], a.slope);
-  f32x16 x3[1] = {bias_tile(bs3, 0, h, kD3)};
+  for (int m = 0; m < kD2 / 16; ++m) x2[m] = leaky(x2[m], a.slope);
+  f32x4 x3[kD3 / 16];
+#pragma unroll
+  for (int m = 0; m < kD3 / 16; ++m) x3[m] = bias_tile(bs3, m, g, kD3);
 #pragma unroll
   for (int p = 0; p < kD2 / 32; ++p) {
-    PBN_CHUNK(12 + p, { mfma_chunk<1>(x3, buf, lane, x2[p]); });
+    PBN_CHUNK(12 + p, { mfma_chunk<kD3 / 16>(x3, buf, lane, x2[2 * p], x2[2 * p + 1]); });
   }
-  x3[0] = leaky(x3[0], a.slope);
+#pragma unroll
+  for (int m = 0; m < kD3 / 16; ++m) x3[m] = leaky(x3[m], a.slope);
 
   // ---- heads: Linear(32, 64) + LeakyReLU per head (stacked rows 64 k .. 64 k + 63), then
   // Linear(64, A) of that head's 64 features; raw outputs to heads[k][e][a], or (FLIP) the
@@ -310,7 +311,7 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
   bool explore = false;
   pbn::Word4 r0{0u, 0u, 0u, 0u}, r1{0u, 0u, 0u, 0u};
   uint32_t mk[4] = {0u, 0u, 0u, 0u};
-  if constexpr (FLIP) {   // the EXPLORE draws of env e (both lane halves draw the same)
+  if constexpr (FLIP) {   // the EXPLORE draws of env e (the four lane groups draw the same)
     const uint64_t ge = a.env_offset + (uint64_t)e;
     const uint64_t st = a.d_step ? *a.d_step : a.step;
     uint64_t eps_u = a.eps_u;
@@ -323,26 +324,22 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
     explore = (uint64_t)r0.x < eps_u;
   }
   for (int k = 0; k < a.n_heads; ++k) {
-    f32x16 z[kDH / 32];
+    f32x4 z[kDH / 16];
 #pragma unroll
-    for (int m = 0; m < kDH / 32; ++m) z[m] = bias_tile(bsh1 + kDH * k, m, h, kDH);
-    PBN_CHUNK(14 + 3 * k, {
-      mfma_chunk<kDH / 32>(z, buf, lane, x3[0]);
-    });
+    for (int m = 0; m < kDH / 16; ++m) z[m] = bias_tile(bsh1 + kDH * k, m, g, kDH);
+    PBN_CHUNK(14 + 3 * k, { mfma_chunk<kDH / 16>(z, buf, lane, x3[0], x3[1]); });
 #pragma unroll
-    for (int m = 0; m < kDH / 32; ++m) z[m] = leaky(z[m], a.slope);
-    f32x16 o[AT];
+    for (int m = 0; m < kDH / 16; ++m) z[m] = leaky(z[m], a.slope);
+    f32x4 o[T16];
 #pragma unroll
-    for (int m = 0; m < AT; ++m) o[m] = bias_tile(bsh2 + A * k, m, h, A);
+    for (int m = 0; m < T16; ++m) o[m] = bias_tile(bsh2 + A * k, m, g, A);
 #pragma unroll
     for (int p = 0; p < kDH / 32; ++p) {
-      PBN_CHUNK(15 + 3 * k + p, {
-        mfma_chunk<AT>(o, buf, lane, z[p]);
-      });
+      PBN_CHUNK(15 + 3 * k + p, { mfma_chunk<T16>(o, buf, lane, z[2 * p], z[2 * p + 1]); });
     }
     if constexpr (FLIP) {
       if (k == 0) {
-        v = __shfl(o[0][0], lane & 31);   // value head output 0: register 0 of lane half 0
+        v = __shfl(o[0][0], lane & 15);   // value head output 0: register 0 of lane group 0
       } else {
         const int b = k - 1;   // branch
         int act;
@@ -351,29 +348,29 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
                             : b == 4 ? r1.y : b == 5 ? r1.z : r1.w;
           act = (int)__umulhi(rw, (uint32_t)(a.n_nodes + 1));
         } else {
-          act = dueling_argmax<AT>(o, h, A, v);
+          act = dueling_argmax<T16>(o, lane, A, v);
         }
         if (act > 0 && act <= a.n_nodes) {   // a > 0 flips node a - 1, once however often
 #pragma unroll
           for (int w = 0; w < 4; ++w)
             if (w == ((act - 1) >> 5)) mk[w] |= 1u << ((act - 1) & 31);
         }
-        if (a.actions && live && h == 0) a.actions[e * (a.n_heads - 1) + b] = act;
+        if (a.actions && live && g == 0) a.actions[e * (a.n_heads - 1) + b] = act;
       }
     } else if (live) {
       float* out = a.heads + ((size_t)k * a.n + e) * A;
 #pragma unroll
-      for (int m = 0; m < AT; ++m) {
+      for (int m = 0; m < T16; ++m) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int act = 32 * m + feat_row(r, h);
-          if (act < A) out[act] = o[m][r];
+        for (int i = 0; i < 4; ++i) {
+          const int act = 16 * m + 4 * g + i;
+          if (act < A) out[act] = o[m][i];
         }
       }
     }
   }
   if constexpr (FLIP) {
-    if (live && h == 0) {
+    if (live && g == 0) {
 #pragma unroll
       for (int w = 0; w < 4; ++w)
         if (w < a.W) a.flipmask[(size_t)w * a.n + e] = mk[w];
@@ -408,7 +405,7 @@ int qnet_check(const pbn_net* net, int64_t n_envs, const float* d_y, const float
 
 template <bool FLIP>
 int qnet_launch(const QnetArgs& a, void* stream) {
-  const int64_t waves = a.n / 32;
+  const int64_t waves = a.n / kEnvs;
   const unsigned blocks = (unsigned)((waves + kWaves - 1) / kWaves);
   void (*kernels[kMaxActTiles])(QnetArgs) = {qnet_tail_kernel<1, FLIP>, qnet_tail_kernel<2, FLIP>,
                                               qnet_tail_kernel<3, FLIP>, qnet_tail_kernel<4, FLIP>};

@@ -18,9 +18,12 @@
 #   nofinal          the driver's command and 2,000 steps without s' (--no-final-state)
 #   abenv            every pbn_rl_amd/libpbn_env_diag_*.so, then this tree: tests/test_gpu_parity.py,
 #                    the driver's command, 2,000 steps and 1M envs (env rollout variants)
+#   abbdq            every pbn_rl_amd/libpbn_env_diag_q*.so, then this tree: tests/test_gpu_agent.py
+#                    and the BDQ frame (frame and tail-launch times; Q-network tail variants)
 #   ab               A/B: the driver's command, 2,000 steps and the BDQ frame, first with
 #                    pbn_rl_amd/libpbn_env_diag_base.so (tools/ab_build.sh REV), then this tree
 set -o pipefail
+shopt -s nullglob   # a variant glob with no match expands to nothing
 tag=$1; shift
 cd "$GRAFT_REPO_ROOT" || exit 1
 out=gpurun_out/$tag
@@ -64,6 +67,17 @@ for step in "$@"; do
     nofinal)
       bench bench_driver_nofinal --gpus 1 --steps 20 --warmup 5 --no-final-state --no-cpu-baseline
       bench bench_s2000_nofinal --steps 2000 --warmup 200 --no-final-state --no-cpu-baseline ;;
+    abbdq)
+      for lib in pbn_rl_amd/libpbn_env_diag_q*.so tree; do
+        side=$(basename "$lib" .so); side=${side#libpbn_env_diag_}
+        if [ "$lib" = tree ]; then unset PBN_LIB; else export PBN_LIB=$PWD/$lib; fi
+        timeout -k 10 300 python -u -m pytest tests/test_gpu_agent.py -m gpu -x -q --timeout 120 --timeout-method thread \
+          > "$out/abbdq_${side}_agent.log" 2>&1 || { tail -20 "$out/abbdq_${side}_agent.log"; fail "abbdq $side agent"; }
+        timeout -k 10 300 python bench.py --workload bdq --no-cpu-baseline > "$out/abbdq_$side.json" 2> "$out/abbdq_$side.err" \
+          || fail "abbdq $side"
+        python -c "import json; d=[json.loads(l) for l in open('$out/abbdq_$side.json') if l.startswith('{')][-1]; r=d['roofline']; print('$side frame_ms', d['ms_per_step'], 'tail_ms', r['launch_ms'], 'bilinear_ms', r['bilinear']['launch_ms'])"
+      done
+      unset PBN_LIB ;;
     ab)
       for side in base tree; do
         if [ $side = base ]; then export PBN_LIB=$PWD/pbn_rl_amd/libpbn_env_diag_base.so; else unset PBN_LIB; fi
