@@ -42,8 +42,6 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FP32_MATRIX_TFLOPS = 157.3  # MI355X FP32 MFMA/vector peak (MI355X_MICROARCH.md)
-L2_PEAK_GBS = 34500.0  # aggregate L2 bandwidth, 8 XCDs (MI355X_MICROARCH.md L2 section)
-BDQ_PMC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_bdq_pbn28_32768.json")
 # VALU issue: 256 CUs x 4 SIMD-32 x 2.4 GHz, one wave64 instruction per 2 cycles per SIMD
 # (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles")
 VALU_WAVE_INSTS_PER_S = 256 * 4 * 2.4e9 / 2
@@ -588,79 +586,54 @@ def main():
                                 "wire_bytes_per_env_step": wire // (env.n_alloc * args.steps),
                                 "records": "s, a, s' (final_state), r, flags of every env-step"}
 
-    bil_ms = tail_ms = None
-    if args.workload == "bdq":   # the frame's two long launches, each timed alone (50 back to back)
-        def bil():
-            for _ in range(50):
-                agent.bilinear()
+    tail_ms = None
+    if args.workload == "bdq" and agent.fused_tail:
+        # the frame's long launch timed alone: 50 back to back, replayed from one hipGraph (eager,
+        # the host's ctypes calls would set the pace)
         with torch.cuda.stream(stream):
-            hw = agent.bilinear()
-            bil_ms, _ = timed(bil, stream, dev, world, local)
-            bil_ms /= 50
-            if agent.fused_tail:
-                def tail():
-                    for _ in range(50):
-                        agent.tail_flipmask(hw, args.epsilon)
-                agent.tail_flipmask(hw, args.epsilon)
-                tail_ms, _ = timed(tail, stream, dev, world, local)
-                tail_ms /= 50
+            agent.act_q(args.epsilon)
+            tg = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(tg, stream=stream):
+                for _ in range(50):
+                    agent.act_q(args.epsilon)
+            tg.replay()
+            tail_ms, _ = timed(tg.replay, stream, dev, world, local)
+            tail_ms /= 50
 
     if rank == 0:
         W = spec.words
         pmc, pmc_path = (None, None) if agent is not None else pmc_profile(args, plan)
         if agent is not None:
-            kernel = ("BDQ frame (pbn_bilinear_targets, pbn_qnet_flipmask: the fp32 MFMA layers after the "
-                      "bilinear + dueling + epsilon-greedy, pbn_step)")
+            kernel = ("BDQ frame (pbn_qnet_flipmask_from_state: the whole BranchingQNetwork on fp32 MFMAs from "
+                      "the packed state + dueling + epsilon-greedy; pbn_step)")
             if args.workload == "bdq-learn":
                 kernel += " + replay store + update_policy (batch 256)"
                 kernel += ", one hipGraph replay per frame" if args.learn_graph else ", eager"
         frame_ms = dev_ms / args.steps
         if args.workload == "bdq":
-            # dominant launch: pbn_qnet_flipmask, MFMA-bound.  Algorithmic FLOPs = the layers after
-            # the bilinear one (qnet_tail_flops_per_env), fp32 MFMA peak
-            out_dim = agent.q.model[0].output_dim
+            # dominant launch: pbn_qnet_flipmask_from_state, MFMA-bound.  Algorithmic FLOPs = the
+            # bilinear layer as the target-contracted product (N x 256 MACs per env) + the layers
+            # after it (qnet_tail_flops_per_env), fp32 MFMA peak
             n = env.n_alloc
-            A = max(1, len(spec.attractors))
             flops = env.n_alloc * qnet_flops_per_env(spec.n)
             mfu = {"achieved_tflops": flops / (frame_ms * 1e-3) / 1e12, "peak_tflops": FP32_MATRIX_TFLOPS,
                    "note": "the reference forward's FLOPs (bilinear as N*N*256 MACs/env) over the whole frame "
                            "time; the frame executes ~4x fewer"}
             if tail_ms is not None:
-                tail_flops = n * qnet_tail_flops_per_env(spec.n, agent.branches)
+                tail_flops = n * (qnet_tail_flops_per_env(spec.n, agent.branches) + 2 * spec.n * 256)
                 tf = tail_flops / (tail_ms * 1e-3) / 1e12
                 roofline = {"bound": "mfma", "achieved": tf, "peak": FP32_MATRIX_TFLOPS, "unit": "TFLOP/s",
                             "frac": tf / FP32_MATRIX_TFLOPS, "traffic": None,
-                            "kernel": "pbn_qnet_flipmask (the frame's longest launch)", "launch_ms": tail_ms,
-                            "flops_per_launch": tail_flops,
-                            "note": "v_mfma_f32_32x32x2_f32 (exact f32), one wave per 32 envs; FLOPs = the "
-                                    "Linear layers after the bilinear one (trunk 256-128-64-32, K+1 heads 32-64-A)",
+                            "kernel": "pbn_qnet_flipmask_from_state (the frame's longest launch)",
+                            "launch_ms": tail_ms, "flops_per_launch": tail_flops,
+                            "note": "v_mfma_f32_16x16x4_f32 (exact f32), one wave per 16 envs; FLOPs = the bilinear "
+                                    "layer contracted with the target (N x 256 MACs) + the Linear layers after it "
+                                    "(trunk 256-128-64-32, K+1 heads 32-64-A)",
                             "model_flops_utilisation": mfu}
             else:
                 roofline = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                             "traffic": None, "kernel": "frame (PyTorch tail)", "launch_ms": frame_ms,
                             "model_flops_utilisation": mfu}
-            # the second launch, pbn_bilinear_targets: it sums envs x mean set bits x one 256-float
-            # row of the per-target table; where the table's 32-column slices fit in LDS (Bittner-28)
-            # each block of 128 envs stages all of them once (A N rows x 1 KB), else the rows come
-            # from L2
-            bil_bytes = n * (4 * W + 1) + n * out_dim * 4 + A * spec.n * out_dim * 4 + out_dim * 4
-            st = env.state[:, : env.num_envs]
-            set_bits = sum(int(((st >> b) & 1).sum().item()) for b in range(32)) / env.num_envs
-            rows_bytes = n * set_bits * out_dim * 4
-            lds_path = 2 * A * spec.n * 32 * 4 + out_dim * 4 <= 140 * 1024 and os.environ.get("PBN_BILINEAR") != "l2"
-            staged = ((n + 127) // 128) * A * spec.n * out_dim * 4 if lds_path else None
-            roofline["bilinear"] = {"launch_ms": bil_ms, "path": "lds" if lds_path else "l2",
-                                    "hbm_GBps": bil_bytes / (bil_ms * 1e-3) / 1e9, "hbm_bytes_per_launch": bil_bytes,
-                                    "rows_bytes_per_launch": rows_bytes, "mean_set_bits": set_bits,
-                                    "rows_GBps": rows_bytes / (bil_ms * 1e-3) / 1e9,
-                                    "staged_bytes_per_launch": staged,
-                                    "staged_GBps": staged / (bil_ms * 1e-3) / 1e9 if staged else None,
-                                    "note": "rows = table-row bytes summed (from LDS on the lds path, L2 on the l2 "
-                                            "path; L2 peak 34.5 TB/s); staged = the LDS-DMA copies of the table "
-                                            "slices (MI355X_MICROARCH.md: LDS-DMA fills reach ~6.4 TB/s chip-wide)"}
-            if os.path.exists(BDQ_PMC) and spec.n == 28 and n == 32768:
-                with open(BDQ_PMC) as f:
-                    roofline["bilinear"]["counters_l2_path"] = json.load(f)["kernels"].get("bilinear_targets_kernel")
         elif agent is not None:
             roofline = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                         "traffic": None, "kernel": kernel, "launch_ms": frame_ms,

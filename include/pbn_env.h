@@ -317,6 +317,29 @@ int pbn_qnet_flipmask(const pbn_net* net, uint64_t seed, uint64_t step, const ui
                       float epsilon, const float* d_epsilon, uint32_t* d_flipmask, int32_t* d_actions,
                       void* stream);
 
+/*
+ * pbn_qnet_heads / pbn_qnet_flipmask with the bilinear layer (+ LeakyReLU) computed in the same
+ * launch from the packed state, in place of d_y: the arguments of pbn_bilinear_targets (d_state,
+ * d_target, d_T, d_b0 = the layer's bias [256], out_dim 256) followed by those of the function
+ * it extends.  Each block sorts its envs by target, so a wave's 16 envs share one or two
+ * targets' tables, and the layer runs on the MFMAs (k = node, 0/1 state bits as the B operand);
+ * its sums are exact f32 but grouped differently from pbn_bilinear_targets' sequential adds:
+ * compare with a tolerance.  This is config 5's acting frame in one launch before pbn_step.
+ */
+int pbn_qnet_heads_from_state(const pbn_net* net, int64_t n_envs, const uint32_t* d_state, const uint8_t* d_target,
+                              const float* d_T, const float* d_b0, const float* d_w1, const float* d_b1,
+                              const float* d_w2, const float* d_b2, const float* d_w3, const float* d_b3,
+                              const float* d_wh1, const float* d_bh1, const float* d_wh2, const float* d_bh2,
+                              int32_t n_heads, int32_t n_actions, float slope, float* d_heads, void* stream);
+int pbn_qnet_flipmask_from_state(const pbn_net* net, uint64_t seed, uint64_t step, const uint64_t* d_step,
+                                 uint64_t env_offset, int64_t n_envs, const uint32_t* d_state,
+                                 const uint8_t* d_target, const float* d_T, const float* d_b0, const float* d_w1,
+                                 const float* d_b1, const float* d_w2, const float* d_b2, const float* d_w3,
+                                 const float* d_b3, const float* d_wh1, const float* d_bh1, const float* d_wh2,
+                                 const float* d_bh2, int32_t n_branches, int32_t n_actions, float slope,
+                                 float epsilon, const float* d_epsilon, uint32_t* d_flipmask, int32_t* d_actions,
+                                 void* stream);
+
 const char* pbn_last_error(void);
 int pbn_abi_version(void);
 

@@ -27,7 +27,8 @@ FLAG_UNSETTLED = 32
 EXPORTS = ["pbn_net_create", "pbn_net_destroy", "pbn_net_words", "pbn_reset", "pbn_step", "pbn_step_dev",
            "pbn_rollout", "pbn_state_histogram", "pbn_obs_unpack", "pbn_bilinear_targets", "pbn_q_to_flipmask",
            "pbn_q_to_flipmask_dev",
-           "pbn_heads_to_flipmask", "pbn_qnet_heads", "pbn_qnet_flipmask", "pbn_last_error", "pbn_abi_version"]
+           "pbn_heads_to_flipmask", "pbn_qnet_heads", "pbn_qnet_flipmask", "pbn_qnet_heads_from_state",
+           "pbn_qnet_flipmask_from_state", "pbn_last_error", "pbn_abi_version"]
 SOURCES = ["pbn_env.hip", "pbn_settle.hip", "pbn_agent.hip", "pbn_qnet.hip"]
 
 _lib: Optional[ctypes.CDLL] = None
@@ -109,6 +110,13 @@ def load() -> ctypes.CDLL:
     L.pbn_qnet_flipmask.argtypes = ([vp, u64, u64, vp, u64, i64] + [vp] * 11 +
                                     [ctypes.c_int32, ctypes.c_int32, ctypes.c_float, ctypes.c_float, vp, vp, vp, vp])
     L.pbn_qnet_flipmask.restype = ctypes.c_int
+    L.pbn_qnet_heads_from_state.argtypes = [vp, i64] + [vp] * 14 + [ctypes.c_int32, ctypes.c_int32, ctypes.c_float,
+                                                                     vp, vp]
+    L.pbn_qnet_heads_from_state.restype = ctypes.c_int
+    L.pbn_qnet_flipmask_from_state.argtypes = ([vp, u64, u64, vp, u64, i64] + [vp] * 14 +
+                                               [ctypes.c_int32, ctypes.c_int32, ctypes.c_float, ctypes.c_float,
+                                                vp, vp, vp, vp])
+    L.pbn_qnet_flipmask_from_state.restype = ctypes.c_int
     L.pbn_last_error.argtypes = []
     L.pbn_last_error.restype = ctypes.c_char_p
     L.pbn_abi_version.argtypes = []

@@ -9,7 +9,8 @@ flips node a-1 for every action a > 0 (:81-84,176-177).  Here one frame covers a
     pbn_bilinear_targets   packed state + target id -> the bilinear layer (+ LeakyReLU)   (HIP)
     pbn_qnet_heads         the rest of the network -> raw head outputs (4, n, N+1)         (HIP, MFMA)
     pbn_heads_to_flipmask  dueling combination + epsilon-greedy -> flip-mask words (W, n)  (HIP)
-    pbn_qnet_flipmask      the two above in one launch (act_q, BatchedBDQ.step)           (HIP)
+    pbn_qnet_flipmask      the two above in one launch                                    (HIP)
+    pbn_qnet_flipmask_from_state  all of it from the packed state, one launch (act_q, step) (HIP, MFMA)
     pbn_step               the PBN transition                                             (HIP)
 
 (``fused_tail=False`` runs the layers after the bilinear one in PyTorch instead.)
@@ -284,26 +285,34 @@ class BatchedBDQ:
         if not self.fast:
             y = self.q.model[0](self.observe())
             return self.q.forward_heads(y) if heads else self.q.forward_tail(y)
-        hw = self.bilinear()
-        # the kernel applied model[1] (LeakyReLU) when _act
         if self.fused_tail and not (torch.is_grad_enabled() and self.q.training):   # (no autograd through it)
-            out = self._tail_kernel(hw)
+            out = self._tail_kernel()
         else:
+            hw = self.bilinear()
+            # the kernel applied model[1] (LeakyReLU) when _act
             out = self.q.forward_heads(self._y, skip_act=self._act, weights=hw)
         return out if heads else self.q.dueling(out)
 
-    def _tail_kernel(self, hw) -> torch.Tensor:
-        """pbn_qnet_heads on self._y -> self._heads (K+1, n, A)."""
-        env, m = self.env, self.q.model
-        w1, b1, w2, b2 = hw
-        ts = [m[2].weight, m[2].bias, m[4].weight, m[4].bias, m[6].weight, m[6].bias,
-              w1, b1, w2, b2]
+    def _tail_operands(self):
+        """Device pointers of the fused kernels' operands after the state: the bilinear layer's
+        target table and bias, then the trunk and the stacked head weights."""
+        m = self.q.model
+        T, bias, (w1, b1, w2, b2) = self._packed()
+        ts = [bias, m[2].weight, m[2].bias, m[4].weight, m[4].bias, m[6].weight, m[6].bias, w1, b1, w2, b2]
         ts = [t.detach().contiguous() for t in ts]
+        return [T.data_ptr() if T is not None else None] + [t.data_ptr() for t in ts], ts
+
+    def _tail_kernel(self) -> torch.Tensor:
+        """pbn_qnet_heads_from_state: the whole network from the packed state -> self._heads
+        (K+1, n, A), one launch."""
+        env = self.env
+        ptrs, _keep = self._tail_operands()
         L = _lib.load()
         with torch.cuda.device(env.device):
-            _lib.check(L.pbn_qnet_heads(env.net.handle, env.n_alloc, self._y.data_ptr(),
-                                        *[t.data_ptr() for t in ts], self.branches + 1, env.n_nodes + 1,
-                                        self._slope, self._heads.data_ptr(), env._stream()), "pbn_qnet_heads")
+            _lib.check(L.pbn_qnet_heads_from_state(env.net.handle, env.n_alloc, env.state.data_ptr(),
+                                                   env.target.data_ptr(), *ptrs, self.branches + 1,
+                                                   env.n_nodes + 1, self._slope, self._heads.data_ptr(),
+                                                   env._stream()), "pbn_qnet_heads_from_state")
         return self._heads
 
     def act_heads(self, heads: torch.Tensor, epsilon: Optional[float] = None,
@@ -331,36 +340,29 @@ class BatchedBDQ:
     def act_q(self, epsilon: Optional[float] = None, step_t: Optional[torch.Tensor] = None,
               epsilon_t: Optional[torch.Tensor] = None) -> torch.Tensor:
         """``predict`` + epsilon-greedy for every env (bdq_model/__init__.py:69-98): Q of the
-        current observations -> env.flipmask and self.actions.  With the fused tail this is
-        pbn_bilinear_targets + pbn_qnet_flipmask (no head outputs in HBM), else q_heads() +
-        act_heads(); both give the same actions.  ``step_t`` / ``epsilon_t`` as act_heads."""
+        current observations -> env.flipmask and self.actions.  With the fused tail this is one
+        launch, pbn_qnet_flipmask_from_state (the whole network from the packed state, no
+        activations in HBM), else q_heads() + act_heads().  ``step_t`` / ``epsilon_t`` as act_heads."""
         if not (self.fast and self.fused_tail):
             return self.act_heads(self.q_heads(), epsilon, step_t=step_t, epsilon_t=epsilon_t)
         if step_t is not None and (step_t.dtype != torch.int64 or step_t.numel() != 1):
             raise ValueError("step_t must be a one-element int64 tensor")
         if epsilon_t is not None and (epsilon_t.dtype != torch.float32 or epsilon_t.numel() != 1):
             raise ValueError("epsilon_t must be a one-element float32 tensor")
-        return self.tail_flipmask(self.bilinear(), epsilon, step_t, epsilon_t)
-
-    def tail_flipmask(self, hw, epsilon: Optional[float] = None, step_t: Optional[torch.Tensor] = None,
-                      epsilon_t: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """The ``pbn_qnet_flipmask`` launch of act_q on the current bilinear output self._y
-        (``hw``: the head weights bilinear() returned)."""
-        env, m = self.env, self.q.model
-        w1, b1, w2, b2 = hw
-        ts = [m[2].weight, m[2].bias, m[4].weight, m[4].bias, m[6].weight, m[6].bias, w1, b1, w2, b2]
-        ts = [t.detach().contiguous() for t in ts]
+        env = self.env
+        ptrs, _keep = self._tail_operands()
         eps = self.epsilon if epsilon is None else float(epsilon)
         L = _lib.load()
         with torch.cuda.device(env.device):
-            _lib.check(L.pbn_qnet_flipmask(env.net.handle, env.seed, env.step_index,
-                                           step_t.data_ptr() if step_t is not None else None,
-                                           env.env_offset, env.n_alloc, self._y.data_ptr(),
-                                           *[t.data_ptr() for t in ts], self.branches, env.n_nodes + 1,
-                                           self._slope, eps,
-                                           epsilon_t.data_ptr() if epsilon_t is not None else None,
-                                           env.flipmask.data_ptr(), self.actions.data_ptr(), env._stream()),
-                       "pbn_qnet_flipmask")
+            _lib.check(L.pbn_qnet_flipmask_from_state(env.net.handle, env.seed, env.step_index,
+                                                      step_t.data_ptr() if step_t is not None else None,
+                                                      env.env_offset, env.n_alloc, env.state.data_ptr(),
+                                                      env.target.data_ptr(), *ptrs, self.branches, env.n_nodes + 1,
+                                                      self._slope, eps,
+                                                      epsilon_t.data_ptr() if epsilon_t is not None else None,
+                                                      env.flipmask.data_ptr(), self.actions.data_ptr(),
+                                                      env._stream()),
+                       "pbn_qnet_flipmask_from_state")
         return env.flipmask
 
     @torch.no_grad()

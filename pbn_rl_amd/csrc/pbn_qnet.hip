@@ -60,6 +60,13 @@ struct QnetArgs {
   uint32_t* flipmask;              // [W][n]
   int32_t* actions;                // [n][H - 1], or null
   int n_nodes, W;
+  // BIL = true: the bilinear layer (+ LeakyReLU) computed here from the packed state, in place of y
+  const uint32_t* state;           // [W][n]
+  const uint8_t* target;           // [n]
+  const float* T;                  // [n_attr][n_nodes][256]: the layer's weight contracted with each
+                                   // attractor's first state (MyBilinear.target_table)
+  const float* b0;                 // [256]
+  int n_attr;
 };
 
 constexpr int kPitch = 36;                 // weight-chunk row pitch in LDS (floats)
@@ -179,17 +186,49 @@ __device__ __forceinline__ int dueling_argmax(const f32x4 (&o)[T16], int lane, i
   return bi;
 }
 
-template <int AT, bool FLIP>   // AT: the second head layers' outputs in 32-row units, A <= 32 AT
+template <int AT, bool FLIP, bool BIL>   // AT: the second head layers' outputs in 32-row units, A <= 32 AT
 __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
   constexpr int T16 = 2 * AT;   // 16-feature output tiles of the second head layers
   __shared__ __attribute__((aligned(16))) float wbuf[2 * kBufFloats];
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4;
-  const int64_t e0 = ((int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6)) * kEnvs;
-  const bool live = e0 < a.n;   // (a wave past the end still stages weights and meets the barriers)
-  const int64_t e = live ? e0 + (lane & 15) : 0;
   const int A = a.n_act;
   const int n_chunks = 14 + 3 * a.n_heads;
+  // this lane's env: the wave's 16 envs in order (y input), or (BIL) the wave's 16 of the block's
+  // envs stably sorted by target, so that a wave's envs share one or two targets' tables
+  int64_t e;
+  bool live;
+  int key = 0;   // BIL: target id, n_attr = none, 255 = past the end
+  if constexpr (!BIL) {
+    const int64_t e0 = ((int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6)) * kEnvs;
+    live = e0 < a.n;   // (a wave past the end still stages weights and meets the barriers)
+    e = live ? e0 + (lane & 15) : 0;
+  } else {
+    __shared__ uint8_t skey[kWaves * kEnvs];
+    __shared__ uint8_t sperm[kWaves * kEnvs];
+    const int64_t eb = (int64_t)blockIdx.x * kWaves * kEnvs;
+    const int tt = threadIdx.x;
+    if (tt < kWaves * kEnvs) {
+      const bool lv = eb + tt < a.n;
+      const uint32_t tg = lv ? (uint32_t)a.target[eb + tt] : 255u;
+      skey[tt] = (uint8_t)(lv ? (tg < (uint32_t)a.n_attr ? tg : (uint32_t)a.n_attr) : 255u);
+    }
+    __syncthreads();
+    if (tt < kWaves * kEnvs) {   // stable counting sort: position = keys below + equal keys before
+      const int k = skey[tt];
+      int pos = 0;
+      for (int u = 0; u < kWaves * kEnvs; ++u) {
+        const int ku = skey[u];
+        pos += (ku < k || (ku == k && u < tt)) ? 1 : 0;
+      }
+      sperm[pos] = (uint8_t)tt;
+    }
+    __syncthreads();
+    const int li = sperm[(threadIdx.x >> 6) * kEnvs + (lane & 15)];
+    key = skey[li];
+    live = key != 255;
+    e = live ? eb + li : 0;
+  }
 
   // staging: thread t moves float4 (row (t >> 3) + kStageRows j, columns 4 (t & 7) .. +3), j <
   // kStagePasses (128 rows in all)
@@ -258,28 +297,86 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
 
   // ---- Linear(256, 128): input tiles from y, features 16 p + 4 g .. + 3 (one float4 per tile);
   // a chunk is two tiles, whose loads fly one chunk ahead
-  const float* yrow = a.y + (size_t)e * kD0 + 4 * g;
-  f32x4 yv0, yv1, yn0, yn1;
-  {
-    const float4 u0 = *reinterpret_cast<const float4*>(yrow), u1 = *reinterpret_cast<const float4*>(yrow + 16);
-    yv0 = f32x4{u0.x, u0.y, u0.z, u0.w};
-    yv1 = f32x4{u1.x, u1.y, u1.z, u1.w};
-  }
-  __syncthreads();   // chunk 0 and the biases are in LDS
   f32x4 x1[kD1 / 16];
-#pragma unroll
-  for (int m = 0; m < kD1 / 16; ++m) x1[m] = bias_tile(bs1, m, g, kD1);
-#pragma unroll
-  for (int p = 0; p < kD0 / 32; ++p) {
-    if (p + 1 < kD0 / 32) {   // the next chunk's y tiles fly under this chunk's MFMAs
-      const float4 u0 = *reinterpret_cast<const float4*>(yrow + 32 * (p + 1));
-      const float4 u1 = *reinterpret_cast<const float4*>(yrow + 32 * (p + 1) + 16);
-      yn0 = f32x4{u0.x, u0.y, u0.z, u0.w};
-      yn1 = f32x4{u1.x, u1.y, u1.z, u1.w};
+  if constexpr (!BIL) {
+    const float* yrow = a.y + (size_t)e * kD0 + 4 * g;
+    f32x4 yv0, yv1, yn0, yn1;
+    {
+      const float4 u0 = *reinterpret_cast<const float4*>(yrow), u1 = *reinterpret_cast<const float4*>(yrow + 16);
+      yv0 = f32x4{u0.x, u0.y, u0.z, u0.w};
+      yv1 = f32x4{u1.x, u1.y, u1.z, u1.w};
     }
-    PBN_CHUNK(p, { mfma_chunk<kD1 / 16>(x1, buf, lane, yv0, yv1); });
-    yv0 = yn0;
-    yv1 = yn1;
+    __syncthreads();   // chunk 0 and the biases are in LDS
+#pragma unroll
+    for (int m = 0; m < kD1 / 16; ++m) x1[m] = bias_tile(bs1, m, g, kD1);
+#pragma unroll
+    for (int p = 0; p < kD0 / 32; ++p) {
+      if (p + 1 < kD0 / 32) {   // the next chunk's y tiles fly under this chunk's MFMAs
+        const float4 u0 = *reinterpret_cast<const float4*>(yrow + 32 * (p + 1));
+        const float4 u1 = *reinterpret_cast<const float4*>(yrow + 32 * (p + 1) + 16);
+        yn0 = f32x4{u0.x, u0.y, u0.z, u0.w};
+        yn1 = f32x4{u1.x, u1.y, u1.z, u1.w};
+      }
+      PBN_CHUNK(p, { mfma_chunk<kD1 / 16>(x1, buf, lane, yv0, yv1); });
+      yv0 = yn0;
+      yv1 = yn1;
+    }
+  } else {
+    // the bilinear layer of the wave's 16 envs, all 256 outputs, in registers: y^T = b0 +
+    // sum over the targets a present of T[a]^T . S_a, S_a[i][j] = bit i of env j's state if env
+    // j's target is a, else 0 (on v_mfma_f32_16x16x4_f32: k = node, A = T[a][node][out], B = the
+    // 0/1 bits); then LeakyReLU.  Register tile q = outputs 16 q + 4 g + i: layer 1's B operand.
+    const int N = a.n_nodes;
+    uint32_t sw[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+      if (w < a.W && live) sw[w] = a.state[(size_t)w * a.n + e];
+    f32x4 yt[kD0 / 16];
+#pragma unroll
+    for (int q = 0; q < kD0 / 16; ++q) {
+      const float4 b4 = *reinterpret_cast<const float4*>(a.b0 + 16 * q + 4 * g);
+      yt[q] = f32x4{b4.x, b4.y, b4.z, b4.w};
+    }
+    const int klo = __shfl(key, 0), khi = __shfl(key, 15);   // the wave's keys are sorted
+    const int kend = khi < a.n_attr ? khi : a.n_attr - 1;
+    for (int ta = klo; ta <= kend; ++ta) {
+      if (!__any(key == ta)) continue;
+      const float* Ta = a.T + (size_t)ta * N * kD0 + (lane & 15);
+      const bool mine = key == ta;
+      // k-step s4: nodes s4 .. s4 + 3, this lane's s4 + g; the next step's 16 table loads are
+      // issued before this step's 16 MFMAs (rows past N load row N - 1 and meet a 0 operand)
+      float av[kD0 / 16], an[kD0 / 16];
+      {
+        const float* Tn = Ta + (size_t)min(g, N - 1) * kD0;
+#pragma unroll
+        for (int q = 0; q < kD0 / 16; ++q) av[q] = Tn[16 * q];
+      }
+      for (int s4 = 0; s4 < N; s4 += 4) {
+        const float* Tn = Ta + (size_t)min(s4 + 4 + g, N - 1) * kD0;
+#pragma unroll
+        for (int q = 0; q < kD0 / 16; ++q) an[q] = Tn[16 * q];
+        __builtin_amdgcn_sched_barrier(0);
+        const int node = s4 + g;
+        uint32_t wsel = sw[0];
+#pragma unroll
+        for (int w = 1; w < 4; ++w) wsel = (node >> 5) == w ? sw[w] : wsel;
+        const float bv = (mine && node < N && ((wsel >> (node & 31)) & 1u)) ? 1.f : 0.f;
+#pragma unroll
+        for (int q = 0; q < kD0 / 16; ++q) yt[q] = mfma(av[q], bv, yt[q]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < kD0 / 16; ++q) av[q] = an[q];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kD0 / 16; ++q) yt[q] = leaky(yt[q], a.slope);
+    __syncthreads();   // chunk 0 and the biases are in LDS
+#pragma unroll
+    for (int m = 0; m < kD1 / 16; ++m) x1[m] = bias_tile(bs1, m, g, kD1);
+#pragma unroll
+    for (int p = 0; p < kD0 / 32; ++p) {
+      PBN_CHUNK(p, { mfma_chunk<kD1 / 16>(x1, buf, lane, yt[2 * p], yt[2 * p + 1]); });
+    }
   }
 #pragma unroll
   for (int m = 0; m < kD1 / 16; ++m) x1[m] = leaky(x1[m], a.slope);
@@ -403,14 +500,27 @@ int qnet_check(const pbn_net* net, int64_t n_envs, const float* d_y, const float
   return PBN_OK;
 }
 
-template <bool FLIP>
+template <bool FLIP, bool BIL>
 int qnet_launch(const QnetArgs& a, void* stream) {
   const int64_t waves = a.n / kEnvs;
   const unsigned blocks = (unsigned)((waves + kWaves - 1) / kWaves);
-  void (*kernels[kMaxActTiles])(QnetArgs) = {qnet_tail_kernel<1, FLIP>, qnet_tail_kernel<2, FLIP>,
-                                              qnet_tail_kernel<3, FLIP>, qnet_tail_kernel<4, FLIP>};
+  void (*kernels[kMaxActTiles])(QnetArgs) = {qnet_tail_kernel<1, FLIP, BIL>, qnet_tail_kernel<2, FLIP, BIL>,
+                                              qnet_tail_kernel<3, FLIP, BIL>, qnet_tail_kernel<4, FLIP, BIL>};
   hipLaunchKernelGGL(kernels[(a.n_act + 31) / 32 - 1], dim3(blocks), dim3(64 * kWaves), 0, (hipStream_t)stream, a);
   if (hipGetLastError() != hipSuccess) return pbn::set_error(PBN_EDEVICE, "qnet_tail_kernel launch failed");
+  return PBN_OK;
+}
+
+// the bilinear layer's inputs of the _from_state forms; on success fills a's BIL fields
+int bil_check(const pbn_net* net, const uint32_t* d_state, const uint8_t* d_target, const float* d_T,
+              const float* d_b0, QnetArgs& a) {
+  pbn::NetView v;
+  int rc = pbn::net_view(net, &v);
+  if (rc) return rc;
+  if (!d_state || !d_target || !d_b0 || (v.n_attr > 0 && !d_T)) return pbn::set_error(PBN_EINVAL, "null buffer");
+  if (!al16(d_b0)) return pbn::set_error(PBN_EINVAL, "d_b0 must be 16-byte aligned");
+  a.state = d_state; a.target = d_target; a.T = d_T; a.b0 = d_b0;
+  a.n_attr = v.n_attr; a.n_nodes = v.n_nodes; a.W = v.W;
   return PBN_OK;
 }
 
@@ -430,7 +540,7 @@ int pbn_qnet_heads(const pbn_net* net, int64_t n_envs, const float* d_y, const f
   a.y = d_y; a.w1 = d_w1; a.b1 = d_b1; a.w2 = d_w2; a.b2 = d_b2; a.w3 = d_w3; a.b3 = d_b3;
   a.wh1 = d_wh1; a.bh1 = d_bh1; a.wh2 = d_wh2; a.bh2 = d_bh2; a.heads = d_heads;
   a.n = n_envs; a.n_heads = n_heads; a.n_act = n_actions; a.slope = slope;
-  return qnet_launch<false>(a, stream);
+  return qnet_launch<false, false>(a, stream);
 }
 
 int pbn_qnet_flipmask(const pbn_net* net, uint64_t seed, uint64_t step, const uint64_t* d_step, uint64_t env_offset,
@@ -461,7 +571,56 @@ int pbn_qnet_flipmask(const pbn_net* net, uint64_t seed, uint64_t step, const ui
   a.seed = seed; a.step = step; a.env_offset = env_offset; a.eps_u = (uint64_t)floor((double)epsilon * 4294967296.0);
   a.d_step = d_step; a.d_eps = d_epsilon; a.flipmask = d_flipmask; a.actions = d_actions;
   a.n_nodes = v.n_nodes; a.W = v.W;
-  return qnet_launch<true>(a, stream);
+  return qnet_launch<true, false>(a, stream);
+}
+
+int pbn_qnet_heads_from_state(const pbn_net* net, int64_t n_envs, const uint32_t* d_state, const uint8_t* d_target,
+                              const float* d_T, const float* d_b0, const float* d_w1, const float* d_b1,
+                              const float* d_w2, const float* d_b2, const float* d_w3, const float* d_b3,
+                              const float* d_wh1, const float* d_bh1, const float* d_wh2, const float* d_bh2,
+                              int32_t n_heads, int32_t n_actions, float slope, float* d_heads, void* stream) {
+  QnetArgs a{};
+  int rc = qnet_check(net, n_envs, d_b0, d_w1, d_b1, d_w2, d_b2, d_w3, d_b3, d_wh1, d_bh1, d_wh2, d_bh2, n_heads,
+                      n_actions);
+  if (rc || n_envs == 0) return rc;
+  if ((rc = bil_check(net, d_state, d_target, d_T, d_b0, a))) return rc;
+  if (!d_heads) return pbn::set_error(PBN_EINVAL, "null buffer");
+  a.w1 = d_w1; a.b1 = d_b1; a.w2 = d_w2; a.b2 = d_b2; a.w3 = d_w3; a.b3 = d_b3;
+  a.wh1 = d_wh1; a.bh1 = d_bh1; a.wh2 = d_wh2; a.bh2 = d_bh2; a.heads = d_heads;
+  a.n = n_envs; a.n_heads = n_heads; a.n_act = n_actions; a.slope = slope;
+  return qnet_launch<false, true>(a, stream);
+}
+
+int pbn_qnet_flipmask_from_state(const pbn_net* net, uint64_t seed, uint64_t step, const uint64_t* d_step,
+                                 uint64_t env_offset, int64_t n_envs, const uint32_t* d_state,
+                                 const uint8_t* d_target, const float* d_T, const float* d_b0, const float* d_w1,
+                                 const float* d_b1, const float* d_w2, const float* d_b2, const float* d_w3,
+                                 const float* d_b3, const float* d_wh1, const float* d_bh1, const float* d_wh2,
+                                 const float* d_bh2, int32_t n_branches, int32_t n_actions, float slope,
+                                 float epsilon, const float* d_epsilon, uint32_t* d_flipmask, int32_t* d_actions,
+                                 void* stream) {
+  pbn::NetView v;
+  int rc = pbn::net_view(net, &v);
+  if (rc) return rc;
+  if (n_branches < 1 || n_branches > kMaxHeads - 1) return pbn::set_error(PBN_EINVAL, "n_branches must be 1..7");
+  if ((rc = qnet_check(net, n_envs, d_b0, d_w1, d_b1, d_w2, d_b2, d_w3, d_b3, d_wh1, d_bh1, d_wh2, d_bh2,
+                       n_branches + 1, n_actions)))
+    return rc;
+  if (env_offset & 31) return pbn::set_error(PBN_EINVAL, "env_offset must be a multiple of 32");
+  if (n_actions != v.n_nodes + 1) return pbn::set_error(PBN_EINVAL, "n_actions must be n_nodes + 1");
+  if (!(epsilon >= 0.f && epsilon <= 1.f)) return pbn::set_error(PBN_EINVAL, "epsilon must be in [0, 1]");
+  if (d_step && ((uintptr_t)d_step & 7u) != 0) return pbn::set_error(PBN_EINVAL, "d_step must be 8-byte aligned");
+  if (d_epsilon && ((uintptr_t)d_epsilon & 3u) != 0) return pbn::set_error(PBN_EINVAL, "d_epsilon misaligned");
+  if (n_envs == 0) return PBN_OK;
+  QnetArgs a{};
+  if ((rc = bil_check(net, d_state, d_target, d_T, d_b0, a))) return rc;
+  if (!d_flipmask) return pbn::set_error(PBN_EINVAL, "null buffer");
+  a.w1 = d_w1; a.b1 = d_b1; a.w2 = d_w2; a.b2 = d_b2; a.w3 = d_w3; a.b3 = d_b3;
+  a.wh1 = d_wh1; a.bh1 = d_bh1; a.wh2 = d_wh2; a.bh2 = d_bh2;
+  a.n = n_envs; a.n_heads = n_branches + 1; a.n_act = n_actions; a.slope = slope;
+  a.seed = seed; a.step = step; a.env_offset = env_offset; a.eps_u = (uint64_t)floor((double)epsilon * 4294967296.0);
+  a.d_step = d_step; a.d_eps = d_epsilon; a.flipmask = d_flipmask; a.actions = d_actions;
+  return qnet_launch<true, true>(a, stream);
 }
 
 }  // extern "C"

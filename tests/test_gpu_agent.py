@@ -169,6 +169,7 @@ def test_bilinear_targets_matches_module(name):
         env.step_flipmask(random_actions=True)
     with torch.no_grad():
         q_fast = agent.q_values().clone()
+        agent.bilinear()                    # pbn_bilinear_targets into agent._y
         y_fast = agent._y.clone()
         assert agent._act                   # the kernel applied the LeakyReLU
         obs = agent.observe()
@@ -186,6 +187,7 @@ def test_bilinear_targets_without_attractors_is_bias():
     env.reset()
     with torch.no_grad():
         agent.q_values()
+        agent.bilinear()
         obs = agent.observe()
         y_ref = agent.q.model[1](agent.q.model[0](obs))
         act_bias = agent.q.model[1](agent.q.model[0].bilinear.bias)
@@ -390,3 +392,38 @@ def test_bilinear_lds_equals_l2_kernel(name, n, monkeypatch):
         y_l2 = agent._y.clone()
     torch.cuda.synchronize()
     assert torch.equal(y_lds, y_l2)
+
+
+@pytest.mark.parametrize("name,n", [("pbn28", 32768), ("pbn7", 96), ("pbn70", 2080), ("pbn28", 160)])
+def test_qnet_from_state_matches_y_path(name, n):
+    """pbn_qnet_heads_from_state (the bilinear layer on the MFMAs inside the tail, envs sorted by
+    target per block) against pbn_bilinear_targets -> pbn_qnet_heads on the same state: fp32,
+    rtol 1e-5 / atol 1e-5 (the bilinear sums are grouped differently); envs without a target and a
+    ragged last block included.  Both acting paths then pick the same flip masks except where
+    fp32 rounding splits a near-tie (> 99.9 %)."""
+    spec = make_spec(name)
+    torch.manual_seed(23)
+    env = VectorPBNEnv(spec, n, seed=5)
+    qnet = BranchingQNetwork((spec.n, spec.n), spec.n + 1, 3)
+    agent = BatchedBDQ(env, qnet)
+    env.reset()
+    for _ in range(2):
+        env.step_flipmask(random_actions=True)
+    env.target[::11] = 0xFF
+    L = _lib.load()
+    with torch.no_grad():
+        h_state = agent.q_heads().clone()
+        hw = agent.bilinear()                      # y through pbn_bilinear_targets
+        m = agent.q.model
+        ts = [t.detach().contiguous() for t in (m[2].weight, m[2].bias, m[4].weight, m[4].bias, m[6].weight,
+                                                m[6].bias, *hw)]
+        h_y = torch.empty_like(h_state)
+        _lib.check(L.pbn_qnet_heads(env.net.handle, env.n_alloc, agent._y.data_ptr(), *[t.data_ptr() for t in ts],
+                                    4, spec.n + 1, agent._slope, h_y.data_ptr(), None), "pbn_qnet_heads")
+        torch.cuda.synchronize()
+        assert torch.allclose(h_state, h_y, rtol=1e-5, atol=1e-5), (h_state - h_y).abs().max().item()
+        agent.act_q(0.0)
+        fm_state = env.flipmask.clone()
+        agent.act_heads(h_y, 0.0)
+        same = (env.flipmask == fm_state).float().mean().item()
+    assert same > 0.999, same

@@ -75,7 +75,7 @@ for step in "$@"; do
           > "$out/abbdq_${side}_agent.log" 2>&1 || { tail -20 "$out/abbdq_${side}_agent.log"; fail "abbdq $side agent"; }
         timeout -k 10 300 python bench.py --workload bdq --no-cpu-baseline > "$out/abbdq_$side.json" 2> "$out/abbdq_$side.err" \
           || fail "abbdq $side"
-        python -c "import json; d=[json.loads(l) for l in open('$out/abbdq_$side.json') if l.startswith('{')][-1]; r=d['roofline']; print('$side frame_ms', d['ms_per_step'], 'tail_ms', r['launch_ms'], 'bilinear_ms', r['bilinear']['launch_ms'])"
+        python -c "import json; d=[json.loads(l) for l in open('$out/abbdq_$side.json') if l.startswith('{')][-1]; r=d['roofline']; print('$side frame_ms', d['ms_per_step'], 'tail_ms', r['launch_ms'], 'bilinear_ms', r.get('bilinear', {}).get('launch_ms'))"
       done
       unset PBN_LIB ;;
     ab)
