@@ -427,3 +427,30 @@ def test_qnet_from_state_matches_y_path(name, n):
         agent.act_heads(h_y, 0.0)
         same = (env.flipmask == fm_state).float().mean().item()
     assert same > 0.999, same
+
+
+def test_qnet_from_state_rejects_bad_arguments():
+    spec = make_spec("pbn28")
+    env = VectorPBNEnv(spec, 64, seed=1)
+    agent = BatchedBDQ(env, BranchingQNetwork((28, 28), 29, 3))
+    L = _lib.load()
+    ptrs, _keep = agent._tail_operands()             # T, b0, trunk, stacked heads
+    st, tg, fm = env.state.data_ptr(), env.target.data_ptr(), env.flipmask.data_ptr()
+    h = env.net.handle
+    ok = [h, 1, 0, None, 0, 64, st, tg, *ptrs, 3, 29, 0.01, 0.0, None, fm, None, None]
+    assert L.pbn_qnet_flipmask_from_state(*ok) == 0
+    for idx, val in [(8, None),                       # T with attractors
+                     (9, ptrs[1] + 4),                # b0 misaligned
+                     (6, None),                       # state
+                     (20, 0),                         # n_branches
+                     (21, 30),                        # n_actions != N + 1
+                     (5, 40)]:                        # n_envs not a multiple of 32
+        bad = list(ok)
+        bad[idx] = val
+        assert L.pbn_qnet_flipmask_from_state(*bad) == -22, idx
+    heads = torch.empty(4, 64, 29, device="cuda")
+    okh = [h, 64, st, tg, *ptrs, 4, 29, 0.01, heads.data_ptr(), None]
+    assert L.pbn_qnet_heads_from_state(*okh) == 0
+    bad = list(okh); bad[3] = None
+    assert L.pbn_qnet_heads_from_state(*bad) == -22
+    torch.cuda.synchronize()
