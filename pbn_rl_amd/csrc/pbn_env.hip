@@ -82,23 +82,24 @@ StepFn pick_wave(int W, int B) {
   return nullptr;
 }
 
-template <int W>
+template <int W, bool MANY>
 StepFn pick_pipe_w(int B) {
   switch (B) {
-    case 4: return pbn_rollout_pipe<W, 4>;
-    case 8: return pbn_rollout_pipe<W, 8>;
-    case 12: return pbn_rollout_pipe<W, 12>;
-    case 16: return pbn_rollout_pipe<W, 16>;
+    case 4: return pbn_rollout_pipe<W, 4, MANY>;
+    case 8: return pbn_rollout_pipe<W, 8, MANY>;
+    case 12: return pbn_rollout_pipe<W, 12, MANY>;
+    case 16: return pbn_rollout_pipe<W, 16, MANY>;
   }
   return nullptr;
 }
 
-StepFn pick_pipe(int W, int B) {
+// many: some node has more than kNodeRecs functions (the instance that carries those chains)
+StepFn pick_pipe(int W, int B, bool many) {
   switch (W) {
-    case 1: return pick_pipe_w<1>(B);
-    case 2: return pick_pipe_w<2>(B);
-    case 3: return pick_pipe_w<3>(B);
-    case 4: return pick_pipe_w<4>(B);
+    case 1: return many ? pick_pipe_w<1, true>(B) : pick_pipe_w<1, false>(B);
+    case 2: return many ? pick_pipe_w<2, true>(B) : pick_pipe_w<2, false>(B);
+    case 3: return many ? pick_pipe_w<3, true>(B) : pick_pipe_w<3, false>(B);
+    case 4: return many ? pick_pipe_w<4, true>(B) : pick_pipe_w<4, false>(B);
   }
   return nullptr;
 }
@@ -411,17 +412,23 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     tab.insert(tab.end(), d->attractor_states, d->attractor_states + (size_t)S * W);
   }
   while (tab.size() & 3) tab.push_back(0u);  // 16-byte aligned uint4 selectors
-  // leaf selectors of the first kNodeRecs functions of every node, uint4 [kNodeRecs][2][32W]
+  for (int i = 0; i < N; ++i)
+    net->max_nf = std::max(net->max_nf, d->node_func_start[i + 1] - d->node_func_start[i]);
+  // records per node in the LDS image: no kernel reads record q >= max_nf (the chains stop at a
+  // node's function count, the padded ones at max_nf), so the image holds min(max_nf, kNodeRecs)
+  // of them at the [kNodeRecs]-layout's strides (pbn70: 4.6 KB less LDS per block)
+  const int Q = std::min(std::max(net->max_nf, 1), kNodeRecs);
+  // leaf selectors of the first Q functions of every node, uint4 [Q][2][32W]
   // (lane-consecutive 16-byte reads); see eval_sel
   net->sel_off = (int)tab.size();
   {
-    std::vector<uint32_t> sel((size_t)kNodeRecs * 2 * 32 * W * 4, 0x0C0C0C0Cu);
+    std::vector<uint32_t> sel((size_t)Q * 2 * 32 * W * 4, 0x0C0C0C0Cu);
     for (int i = 0; i < N; ++i) {
       const int f0 = d->node_func_start[i], nf = d->node_func_start[i + 1] - f0;
-      // records beyond a node's last function (up to kNodeRecs) repeat the last one: the
+      // records beyond a node's last function (up to Q) repeat the last one: the
       // pipelined kernel's chain then needs no per-lane function count (x = lt ? f : x with
       // f == x is x)
-      for (int q = 0; q < kNodeRecs; ++q) {
+      for (int q = 0; q < Q; ++q) {
         const int qf = std::min(q, nf - 1);
         const uint32_t T = d->func_table[f0 + qf];
         const int k = d->func_arity[f0 + qf];
@@ -462,8 +469,6 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     }
     net->n_cls = ok ? (int)vals.size() : 0;
     for (int q = 0; q < kNodeRecs; ++q) net->uthr[q] = (ok && q < (int)vals.size()) ? vals[q] : 0u;
-    for (int i = 0; i < N; ++i)
-      net->max_nf = std::max(net->max_nf, d->node_func_start[i + 1] - d->node_func_start[i]);
     net->lq = std::max(net->max_nf - 1, 1);
   }
   std::vector<uint4> fcomp(d->n_funcs);
@@ -487,12 +492,12 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     nrec[(size_t)i * kNodeRecs + 0].w = (uint32_t)nf;
     nrec[(size_t)i * kNodeRecs + 1].w = (uint32_t)f0;
   }
-  // the records in the LDS image too, record-major uint4 [kNodeRecs][32W] (the pipelined
+  // the records in the LDS image too, record-major uint4 [Q][32W] (the pipelined
   // kernel reads them per step instead of keeping them in VGPRs across its loop; lane = node,
   // so consecutive lanes read consecutive 16-byte records: no LDS bank conflicts, where the
   // node-major layout's 64-byte lane stride conflicted 4 ways)
   net->nrec_off = (int)tab.size();
-  for (int q = 0; q < kNodeRecs; ++q)
+  for (int q = 0; q < Q; ++q)
     for (int i = 0; i < 32 * W; ++i) {
       uint4 r4 = i < N ? nrec[(size_t)i * kNodeRecs + q] : make_uint4(0, 0, 0, 0);
       if (i < N) {   // padded inputs as the selectors above (the .w metadata stays)
@@ -590,7 +595,7 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   net->wave_settle = reinterpret_cast<StepFn>(pbn::settle_kernel(W, d->prob_bits, 0));
   net->wave_settle_lean = reinterpret_cast<StepFn>(pbn::settle_kernel(W, d->prob_bits, 1));
   net->settle_max = d->settle_max;
-  net->pipe = pick_pipe(W, d->prob_bits);
+  net->pipe = pick_pipe(W, d->prob_bits, net->max_nf > kNodeRecs);
   net->reset = pick_reset(W);
   // multiply-high divisors (exact for the operand ranges used: see actions_from_draw, autoreset)
   net->n1_magic = (uint32_t)(((1ull << 32) + (uint64_t)N) / (uint64_t)(N + 1));

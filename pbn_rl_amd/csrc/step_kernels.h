@@ -1072,13 +1072,18 @@ __device__ __forceinline__ uint32_t chain_padded(const uint4* __restrict__ rec, 
   return x;
 }
 
+// MANY: some node has more than kNodeRecs functions.  Those chains read records past the LDS
+// copy (global fcompact) and hold every record of a node in registers; compiled out of the
+// common instances (every bundled network has at most 3 functions per node), they no longer set
+// the register allocation of the whole kernel: 167 -> 88 VGPRs at three state words (pbn70),
+// 121 -> 83 at two, 242 -> 93 at four.
 // Waves per SIMD the register allocation must allow for single-word states: 6 (<= 80 VGPRs,
 // no spill in the step loops) runs 1M envs 10 % faster than the unconstrained 86 VGPRs (5 waves);
 // 7 and 8 spill to scratch in the state loop and lose (profiles/r02_ab_waves_per_eu.jsonl).
-// Three-word states (pbn70) are held to 3 waves (167 VGPRs, where the compiler's choice is 181:
-// 2 waves); two-word states fit 4 waves as they are.
-#define PBN_PIPE_ATTR __attribute__((amdgpu_waves_per_eu(W == 1 ? 6 : (W == 3 ? 3 : 1), 8)))
-template <int W, int B>
+// Multi-word states: 5 waves without MANY; with MANY, three words are held to 3 waves (167 VGPRs,
+// where the compiler's choice is 181: 2 waves) and two words fit 4 waves as they are.
+#define PBN_PIPE_ATTR __attribute__((amdgpu_waves_per_eu(W == 1 ? 6 : (MANY ? (W == 3 ? 3 : 1) : 5), 8)))
+template <int W, int B, bool MANY>
 __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a) {
   constexpr int CPN = B / 4;              // selection calls per node
   extern __shared__ uint32_t smem[];
@@ -1485,9 +1490,11 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
                   else
                     lt_out[q * 64 * W + i] = less_than(dig, recL[q * 32 * W + ic].z, B);
                 }
-              const int f0 = (int)recL[32 * W + ic].w;
-              for (int j = kNodeRecs - 1; j < nf - 1; ++j)   // nodes with more than kNodeRecs functions
-                lt_out[j * 64 * W + i] = less_than(dig, a.fcompact[CK(f0 + j, a.n_funcs, 9)].z, B);
+              if constexpr (MANY) {   // nodes with more than kNodeRecs functions
+                const int f0 = (int)recL[32 * W + ic].w;
+                for (int j = kNodeRecs - 1; j < nf - 1; ++j)
+                  lt_out[j * 64 * W + i] = less_than(dig, a.fcompact[CK(f0 + j, a.n_funcs, 9)].z, B);
+              }
             }
           }
         }
@@ -1634,7 +1641,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
         __builtin_amdgcn_wave_barrier();
         PBN_PSTAMP_AT(k, 3);
         uint32_t X[W];
-        if (u_mnf <= kNodeRecs) {
+        if (!MANY || u_mnf <= kNodeRecs) {
 #pragma unroll
           for (int r = 0; r < W; ++r) {
             int i = l32 + 32 * r;

@@ -20,6 +20,7 @@
 #                    the driver's command, 2,000 steps and 1M envs (env rollout variants)
 #   abbdq            every pbn_rl_amd/libpbn_env_diag_q*.so, then this tree: tests/test_gpu_agent.py
 #                    and the BDQ frame (frame and tail-launch times; Q-network tail variants)
+#   ab70             A/B: pbn70 x 1M and pbn28 x 1M, pbn_rl_amd/libpbn_env_diag_base.so, then this tree
 #   ab               A/B: the driver's command, 2,000 steps and the BDQ frame, first with
 #                    pbn_rl_amd/libpbn_env_diag_base.so (tools/ab_build.sh REV), then this tree
 set -o pipefail
@@ -84,6 +85,13 @@ for step in "$@"; do
         bench ab_${side}_driver --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-gather
         bench ab_${side}_s2000 --steps 2000 --warmup 200 --no-cpu-baseline --no-gather
         bench ab_${side}_bdq --workload bdq --no-cpu-baseline
+      done
+      unset PBN_LIB ;;
+    ab70)
+      for side in base tree; do
+        if [ $side = base ]; then export PBN_LIB=$PWD/pbn_rl_amd/libpbn_env_diag_base.so; else unset PBN_LIB; fi
+        bench ab70_${side}_pbn70 --network pbn70 --envs 1048576 --steps 200 --warmup 20 --no-cpu-baseline --no-gather
+        bench ab70_${side}_1m --envs 1048576 --steps 300 --warmup 50 --no-cpu-baseline --no-gather
       done
       unset PBN_LIB ;;
     abenv)
