@@ -655,7 +655,13 @@ def main():
                                 "minimal packed I/O) x env-steps / HIP-event time.  The rollout keeps the state "
                                 "on chip between steps and moves moved_bytes_per_launch, which `traffic` (PMC, "
                                 "per launch) measures.  The kernel is VALU-issue / latency bound, see DESIGN.md "
-                                "'What bounds it'"}
+                                "'What bounds it'",
+                        # what the counters show bounds the kernel ("bound" is the contract's pricing
+                        # axis, the bytes): VALU issue well below its rate, the waves waiting on LDS
+                        # round trips and the per-step block barrier (DESIGN.md "What bounds the env
+                        # kernel, from counters")
+                        "limiter": "latency: VALU issue below its rate, waves parked on s_waitcnt / the "
+                                   "per-step block barrier (roofline.valu, traffic_source's wave_state)"}
             if pmc:
                 roofline["traffic_source"] = {"file": pmc_path, "command": pmc.get("command")}
                 if pmc.get("valu_insts_per_launch"):
