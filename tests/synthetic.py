@@ -36,6 +36,6 @@ def random_network(n_nodes: int, seed: int, max_funcs: int = 6, max_arity: int =
     return Network([f"g{i}" for i in range(n_nodes)], nodes, name=f"rand{n_nodes}_{seed}")
 
 
-def random_spec(n_nodes: int, seed: int, n_targets: int = 8, **kw) -> EnvSpec:
-    net = random_network(n_nodes, seed)
+def random_spec(n_nodes: int, seed: int, n_targets: int = 8, max_funcs: int = 6, **kw) -> EnvSpec:
+    net = random_network(n_nodes, seed, max_funcs=max_funcs)
     return EnvSpec(net, random_state_targets(n_nodes, n_targets, seed + 1), **kw)

@@ -61,12 +61,13 @@ def test_c_oracle_equals_python_oracle(name, mode):
         st, tg, t = res["state_out"], res["target"], res["t"]
 
 
-@pytest.mark.parametrize("n_nodes,seed", [(5, 21), (40, 22)])
+@pytest.mark.parametrize("n_nodes,seed,max_funcs", [(5, 21, 6), (40, 22, 6), (9, 21, 3), (70, 24, 4)])
 @pytest.mark.parametrize("mode", [1, 3])
-def test_c_oracle_equals_python_oracle_synthetic(n_nodes, seed, mode):
-    """Random networks: up to 6 functions per node, arbitrary weights, 1-2 state words."""
+def test_c_oracle_equals_python_oracle_synthetic(n_nodes, seed, max_funcs, mode):
+    """Random networks: up to max_funcs functions per node, arbitrary weights, 1-3 state words
+    (the few-function ones are the GPU parity cases of test_synthetic_few_functions_rollout)."""
     from .synthetic import random_spec
-    spec = random_spec(n_nodes, seed, perturbation=0.1, horizon=3)
+    spec = random_spec(n_nodes, seed, max_funcs=max_funcs, perturbation=0.1, horizon=3)
     net = spec.network
     n, sd, off = 32, 777, 32
     W = spec.words
