@@ -237,6 +237,19 @@ def test_synthetic_networks_rollout(n_nodes, seed, variant, monkeypatch):
     run_rollout_pair(spec, 96, 5, 1)
 
 
+@pytest.mark.parametrize("n_nodes,seed", [(9, 21), (31, 22), (45, 23), (70, 24), (100, 25)])
+@pytest.mark.parametrize("max_funcs", [3, 4])
+def test_synthetic_few_functions_rollout(n_nodes, seed, max_funcs):
+    """At most kNodeRecs functions per node with per-node weights: the pipelined kernel's
+    common instances (no long chains) with per-lane thresholds (the selection's LDS digit-mask
+    table at one state word, the per-lane compares above it), where every kaban network takes
+    the wave-uniform threshold path."""
+    spec = random_spec(n_nodes, seed, max_funcs=max_funcs, perturbation=0.05, horizon=6)
+    assert max(len(f) for f in spec.network.nodes) <= 4
+    run_rollout_pair(spec, 2080, 7, 3)
+    run_rollout_pair(spec, 96, 4, 1)
+
+
 @pytest.mark.parametrize("variant", ["pipe", "lean"])
 def test_rollout_long(variant, monkeypatch):
     """Many steps (horizons, resets, slots wrapping) in one launch: the pipelined kernel and
