@@ -21,8 +21,9 @@ same steps with the rollout's (s, a, s', r, flags) records (17 B per env-step fo
 Bittner-28) handed to the learner (rank 0) after every rollout launch, overlapped
 with the next launch (``gather.all_gather`` times the
 all-gather form).  Each timed region is bracketed by barrier +
-synchronize, timed with HIP events on the launch stream, and the max over ranks
-is reported.  Inputs are resident in HBM before timing.  Before the timed region
+synchronize, timed with HIP events on the launch stream (created without the
+system-scope fence: the interval is the device's work; timing.default_events times
+the same run between torch's default events), and the max over ranks is reported.  Inputs are resident in HBM before timing.  Before the timed region
 the captured run is replayed untimed for at least --clock-warm seconds so the
 GPU clocks have ramped (the W warmup steps alone are microseconds of GPU work).
 """
@@ -337,15 +338,56 @@ def barrier(world: int, local: int) -> None:
 GATE_CYCLES = 250_000
 
 
-def timed(fn, stream, dev, world, local, gate_cycles: int = None):
+HIP_EVENT_DISABLE_SYSTEM_FENCE = 0x20000000   # hip_runtime_api.h
+_HIP = None
+
+
+class DeviceEvent:
+    """A timing HIP event created with hipEventDisableSystemFence: recording it does not
+    release device memory to system scope (no write-back of the outputs for the host), so the
+    interval between two of them is the device's work on the stream.  The outputs stay in HBM
+    for their consumer on the device (the learner); host visibility comes with the
+    synchronize after the end event.  torch.cuda.Event records with the system fence, which
+    adds ~1.5-2 us to each timed region (tools/event_probe.py, profiles/r03_zh_event_probe.jsonl)."""
+
+    def __init__(self):
+        global _HIP
+        import ctypes
+        if _HIP is None:
+            _HIP = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+        self._c = ctypes
+        self.ev = ctypes.c_void_p()
+        if _HIP.hipEventCreateWithFlags(ctypes.byref(self.ev), HIP_EVENT_DISABLE_SYSTEM_FENCE) != 0:
+            raise RuntimeError("hipEventCreateWithFlags failed")
+
+    def record(self, stream):
+        if _HIP.hipEventRecord(self.ev, self._c.c_void_p(stream.cuda_stream)) != 0:
+            raise RuntimeError("hipEventRecord failed")
+
+    def elapsed_time(self, end) -> float:
+        ms = self._c.c_float()
+        if _HIP.hipEventSynchronize(end.ev) != 0 or _HIP.hipEventElapsedTime(self._c.byref(ms), self.ev, end.ev) != 0:
+            raise RuntimeError("hipEventElapsedTime failed")
+        return float(ms.value)
+
+    def __del__(self):
+        if _HIP is not None and self.ev:
+            _HIP.hipEventDestroy(self.ev)
+
+
+def timed(fn, stream, dev, world, local, gate_cycles: int = None, system_fence: bool = False):
     """Device milliseconds of fn() (launches on `stream`), bracketed by barrier + synchronize,
     max over ranks.  A spin kernel is queued on the stream ahead of the start event (the
     "blocking kernel" of nvbench): while it runs the host enqueues the start event, fn's
     launches and the end event, so the events time the GPU work of fn and not the host's
-    graph-launch latency in front of it.  The spin itself lies outside the two events."""
+    graph-launch latency in front of it.  The spin itself lies outside the two events.
+    Events: DeviceEvent (no system-scope fence), or torch's default events (system_fence)."""
     barrier(world, local)
     torch.cuda.synchronize(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if system_fence:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    else:
+        ev0, ev1 = DeviceEvent(), DeviceEvent()
     with torch.cuda.stream(stream):
         torch.cuda._sleep(gate_cycles or GATE_CYCLES)
     t0 = time.perf_counter()
@@ -564,9 +606,13 @@ def main():
             if time.perf_counter() >= t_end:
                 break
         dev_ms, host_s = timed(run, stream, dev, world, local)
+        # the same run between torch's default events (system-scope fence at each event)
+        fenced_ms, _ = timed(run, stream, dev, world, local, system_fence=True)
         # the floor of this timing method: the same gate + event pair around a one-element kernel
         tiny = torch.zeros(1, device=dev)
         floor_ms = min(timed(lambda: tiny.add_(1.0), stream, dev, world, local)[0] for _ in range(5))
+        floor_fenced_ms = min(timed(lambda: tiny.add_(1.0), stream, dev, world, local, system_fence=True)[0]
+                              for _ in range(5))
     elapsed = dev_ms * 1e-3
     total_env_steps = world * args.envs * args.steps
     value = total_env_steps / elapsed
@@ -698,8 +744,14 @@ def main():
                        "parallelism": f"env-shard x{world} (RCCL process group)",
                        "launch": "hipGraph" if (use_graph or args.learn_graph) else "eager"},
             "roofline": roofline,
-            "timing": {"clock": "HIP events on the launch stream behind a spin gate, max over ranks",
+            "timing": {"clock": "HIP events (hipEventDisableSystemFence) on the launch stream behind a spin gate, "
+                                "max over ranks",
                        "event_floor_us": floor_ms * 1e3,
+                       "default_events": {"value": total_env_steps / (fenced_ms * 1e-3),
+                                          "ms_per_step": fenced_ms / args.steps,
+                                          "event_floor_us": floor_fenced_ms * 1e3,
+                                          "note": "the same run between torch.cuda.Event pairs, whose records "
+                                                  "release device memory to system scope (host visibility)"},
                        "note": "event_floor_us: the same gate + event pair around a one-element kernel (dispatch "
                                "and event overhead, part of every timed region)",
                        "host_ms_per_step": host_s * 1e3 / args.steps, "clock_warm_runs": warm_reps},
