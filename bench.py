@@ -55,8 +55,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=None, help="untimed steps (default 200; bdq workload 20)")
     p.add_argument("--workload", choices=["env", "bdq", "bdq-learn"], default="env",
                    help="env: BASELINE config 2, the env step alone (in-kernel random interventions); "
-                        "bdq: config 5, the full BDQ frame per step (BranchingQNetwork forward: bilinear layer "
-                        "by pbn_bilinear_targets, the rest in PyTorch -> pbn_q_to_flipmask -> pbn_step); "
+                        "bdq: config 5, the full BDQ frame per step (the whole BranchingQNetwork forward, "
+                        "dueling and epsilon-greedy in one fp32 MFMA launch from the packed state, "
+                        "pbn_qnet_flipmask_from_state -> pbn_step); "
                         "bdq-learn: that frame plus "
                         "storing the transitions in the device replay and one update_policy step of "
                         "batch 256 (one hipGraph per frame: step index, epsilon and ring position live on "
