@@ -87,8 +87,17 @@ def parse():
                    help="rollout workload: do not write s' (final_state) per step; the next step's obs is s' "
                         "except for envs that autoreset, whose s' is then not stored")
     p.add_argument("--no-gather", action="store_true",
-                   help="skip the second timed pass (rollouts + one RCCL all_gather of their (s, a, s', r, "
-                        "flags) records per launch, SURVEY.md 8(e)) reported as value_with_gather")
+                   help="skip the timed hand-off passes (SURVEY.md 8(e)): the rollouts again with their (s, a, "
+                        "s', r, flags) records handed to the learner after every launch, point to point to rank "
+                        "0 (value_with_gather; at world 1 the learner's shard is copied into its receive slot) "
+                        "and as an RCCL all_gather (gather.all_gather)")
+    p.add_argument("--settle", type=int, default=0,
+                   help="step law of the whole line: 0 = one synchronous update per env step (the headline "
+                        "unit, SURVEY.md 8(d)); K >= 2 = the settle law (intervene, then update until an "
+                        "attractor state, at most K updates: PBNEnv's default, include/pbn_env.h)")
+    p.add_argument("--settle-line", type=int, default=64,
+                   help="env workload under the one-update law: also time the same steps under the settle "
+                        "law with this cap (PBNEnv's default, 64) and report them as settle_law; 0 = skip")
     p.add_argument("--clock-warm", type=float, default=0.3,
                    help="seconds of untimed replays of the captured run before timing (GPU clock ramp)")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -246,7 +255,8 @@ def config1_line(dev, seconds: float = 2.0) -> dict:
     el = time.perf_counter() - t0
     spec7 = env.spec
     env.close()
-    return {"workload": "pbn7 single env through the gym facade, random interventions, reset on done",
+    return {"workload": f"pbn7 single env through the gym facade (its default step law: settle <= {spec7.settle} "
+                        f"updates), random interventions, reset on done",
             "facade_gpu": {"value": k / el, "unit": "env-steps/s", "us_per_step": el / k * 1e6,
                            "sample": f"PBNEnv(network='pbn7').step x {k}"},
             "cpu_python": python_baseline(spec7, seconds)}
@@ -315,6 +325,28 @@ def workload_text(args, chunk: int, rollout_mode: bool) -> str:
             + (f"pbn_rollout, launches of up to {chunk} steps, per-step {stored} written to HBM"
                + (" (s' of autoreset envs not stored)" if args.no_final_state else "")
                if rollout_mode else "pbn_step per step"))
+
+
+def settle_stats(updates, elapsed_s: float, env_steps: int) -> dict:
+    """Settle lengths (pbn_rollout_ex's d_updates) of every env-step of a timed run: the
+    synchronous updates applied per second and their distribution."""
+    u = torch.cat([x.reshape(-1) for x in updates]).to(torch.int64)
+    total = int(u.sum().item())
+    hist = torch.bincount(u).cpu().tolist()
+    n = u.numel()
+    cum, q = 0, {}
+    for length, c in enumerate(hist):
+        cum += c
+        for p in (0.5, 0.9, 0.99):
+            if p not in q and cum >= p * n:
+                q[p] = length
+    return {"updates_per_s": total / elapsed_s, "mean_updates_per_env_step": total / n,
+            "updates_quantiles": {"p50": q.get(0.5), "p90": q.get(0.9), "p99": q.get(0.99), "max": len(hist) - 1},
+            "settle_length_histogram": {str(k): c for k, c in enumerate(hist) if c},
+            "env_steps_sampled": n, "env_steps_timed": env_steps,
+            "note": "updates = synchronous updates applied per env-step (1 + the settle updates), read from "
+                    "pbn_rollout_ex's d_updates of every timed launch; a 32-env group runs until its last env "
+                    "settles, so the kernel's update slots are at least the sum of these"}
 
 
 def launch_plan(steps: int, chunk: int):
@@ -401,12 +433,13 @@ def timed(fn, stream, dev, world, local, gate_cycles: int = None, system_fence: 
     return max_over_ranks(ev0.elapsed_time(ev1), world, dev), max_over_ranks(host_s, world, dev)
 
 
-def gather_pass(env, plan, world, local, dev, stream, dst):
+def gather_pass(env, plan, world, local, dev, stream, dst, copy_own=False):
     """The timed steps again, the records of every rollout launch handed to the learner
     (ShardedRollout: a ring of two record slots the kernel writes in place; the hand-off of
     launch k runs on the communicator's stream while launch k + 1 runs).  dst = 0: point to
-    point to rank 0, which keeps its own shard in place; dst = None: all_gather_into_tensor.
-    Device ms, max over ranks."""
+    point to rank 0, which keeps its own shard in place, or with copy_own copies it into its
+    receive slot on a side stream (world 1: the whole hand-off); dst = None:
+    all_gather_into_tensor.  Device ms, max over ranks."""
     from pbn_rl_amd.distributed import ShardedRollout
 
     ro = ShardedRollout(world * env.n_alloc, lambda off, cnt: env)
@@ -414,7 +447,7 @@ def gather_pass(env, plan, world, local, dev, stream, dst):
 
     def run():
         for k in plan:
-            ro.gather(ro.rollout(k), dst=dst, async_op=True)
+            ro.gather(ro.rollout(k), dst=dst, async_op=True, copy_own=copy_own)
         for works in ro._pending.values():   # the last hand-offs, before the end event
             for w in works:
                 if w is not None:
@@ -429,6 +462,64 @@ def gather_pass(env, plan, world, local, dev, stream, dst):
         ms, _ = timed(run, stream, dev, world, local, gate_cycles=GATE_CYCLES * (1 + len(plan)))
     wire = sum(env.n_alloc * k * (12 * env.words + 5) for k in plan)
     return ms, wire
+
+
+def settle_line(args, dev, stream, world, local, plan, K):
+    """The timed steps again under the settle law (cap K, PBNEnv's default law): a fresh env
+    of the same network, envs and seed, the same launch plan; env-steps/s, the synchronous
+    updates applied per second and the settle-length distribution of every timed env-step."""
+    from pbn_rl_amd.attractors import load_attractors
+    from pbn_rl_amd.network import load_network
+    from pbn_rl_amd.spec import EnvSpec
+    from pbn_rl_amd.vector_env import VectorPBNEnv
+
+    rank = int(os.environ.get("RANK", "0"))
+    spec = EnvSpec(load_network(args.network), load_attractors(args.network), perturbation=args.perturbation,
+                   prob_bits=args.prob_bits, horizon=args.horizon, settle=K)
+    env = VectorPBNEnv(spec, args.envs, seed=args.seed, device=dev, env_offset=rank * args.envs,
+                       keep_final_state=False)
+    env.reset()
+    keep_final = not args.no_final_state
+    kw = dict(random_actions=True, keep_obs=True, keep_final=keep_final, keep_updates=True)
+    bufs = [env.rollout_buffers(k, keep_obs=True, keep_final=keep_final, keep_updates=True) for k in plan]
+    wplan = launch_plan(args.warmup, args.chunk)
+    wbufs = {k: env.rollout_buffers(k, keep_obs=True, keep_final=keep_final, keep_updates=True) for k in set(wplan)}
+
+    def run():
+        for i, k in enumerate(plan):
+            env.rollout(k, out=bufs[i], **kw)
+
+    with torch.cuda.stream(stream):
+        for k in wplan:
+            env.rollout(k, out=wbufs[k], **kw)
+        t_end = time.perf_counter() + args.clock_warm
+        while True:
+            run()
+            torch.cuda.synchronize(dev)
+            if time.perf_counter() >= t_end:
+                break
+        ms, _ = timed(run, stream, dev, world, local)
+    elapsed = ms * 1e-3
+    total = world * args.envs * args.steps
+    stats = settle_stats([b["updates"] for b in bufs], elapsed, total)
+    if world > 1:   # every rank's updates
+        t = torch.tensor([stats["updates_per_s"]], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t)
+        stats["updates_per_s"] = float(t.item())
+    per_step = survey_bytes_per_env_step(spec.n)
+    achieved = env.n_alloc * world * args.steps * per_step / elapsed / 1e9
+    line = {"value": total / elapsed, "unit": "env-steps/s", "ms_per_step": ms / args.steps, "settle_max": K,
+            "step_law": f"settle: the intervention, then synchronous updates until every state is an attractor "
+                        f"state, at most {K} updates (PBNEnv's default; include/pbn_env.h 'Step law')",
+            "kernel": "pbn_rollout_settle (%s)" % ", ".join(f"{k} steps" for k in plan),
+            "launch_ms": ms / len(plan),
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "bytes_per_env_step": per_step,
+                         "note": "the same per-env-step I/O as the headline; a settle step applies "
+                                 "mean_updates_per_env_step updates on chip for it"},
+            **stats}
+    env.close()
+    return line, spec
 
 
 def pmc_profile(args, plan):
@@ -526,7 +617,7 @@ def main():
     from pbn_rl_amd.vector_env import VectorPBNEnv
 
     spec = EnvSpec(load_network(args.network), load_attractors(args.network), perturbation=args.perturbation,
-                   prob_bits=args.prob_bits, horizon=args.horizon)
+                   prob_bits=args.prob_bits, horizon=args.horizon, settle=args.settle)
     env = VectorPBNEnv(spec, args.envs, seed=args.seed, device=dev, env_offset=rank * args.envs,
                        keep_final_state=args.workload == "bdq-learn")
     env.reset()
@@ -554,10 +645,18 @@ def main():
     bufs = {}   # rollout outputs per launch length; captured graphs write into them, so they live
                 # as long as the graphs (torch.cuda.graph empties the allocator cache on entry)
 
-    def launch(k: int):
-        """One kernel launch covering k steps of every env."""
+    settle_law = rollout_mode and args.settle >= 2
+    bufs_t = {}   # settle law: outputs per launch of the timed plan (every launch's settle lengths kept)
+
+    def launch(k: int, i: int = None):
+        """One kernel launch covering k steps of every env (i: index in the timed plan)."""
         if rollout_mode:
-            bufs[k] = env.rollout(k, random_actions=True, keep_obs=True, keep_final=keep_final, out=bufs.get(k))
+            if settle_law and i is not None:
+                env.rollout(k, random_actions=True, keep_obs=True, keep_final=keep_final, out=bufs_t[i],
+                            keep_updates=True)
+            else:
+                bufs[k] = env.rollout(k, random_actions=True, keep_obs=True, keep_final=keep_final, out=bufs.get(k),
+                                      keep_updates=settle_law)
         elif args.workload == "bdq-learn":
             learner.frame()
         elif agent is not None:
@@ -574,7 +673,10 @@ def main():
         # output buffers of every launch length exist before the capture, so the graph holds
         # the rollout launches alone (no allocation or fill kernels in the timed region)
         for k in set(plan) | set(launch_plan(args.warmup, chunk)):
-            bufs[k] = env.rollout_buffers(k, keep_obs=True, keep_final=keep_final)
+            bufs[k] = env.rollout_buffers(k, keep_obs=True, keep_final=keep_final, keep_updates=settle_law)
+        if settle_law:
+            for i, k in enumerate(plan):
+                bufs_t[i] = env.rollout_buffers(k, keep_obs=True, keep_final=keep_final, keep_updates=True)
     with torch.cuda.stream(stream):
         for k in launch_plan(args.warmup, chunk):
             launch(k)
@@ -587,16 +689,16 @@ def main():
             # the whole timed run as distinct launches
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph, stream=stream):
-                for k in plan:
-                    launch(k)
+                for i, k in enumerate(plan):
+                    launch(k, i)
             torch.cuda.synchronize(dev)
 
         def run():
             if use_graph:
                 graph.replay()
             else:
-                for k in plan:
-                    launch(k)
+                for i, k in enumerate(plan):
+                    launch(k, i)
 
         # untimed clock ramp: replays of the captured run (no timing, no results kept)
         warm_reps, t_end = 0, time.perf_counter() + args.clock_warm
@@ -618,18 +720,31 @@ def main():
     total_env_steps = world * args.envs * args.steps
     value = total_env_steps / elapsed
 
+    settle = None
+    if settle_law:
+        settle = settle_stats([bufs_t[i]["updates"] for i in range(len(plan))], elapsed, total_env_steps)
+    settle_other, settle_spec = None, None
+    if rollout_mode and not settle_law and args.workload == "env" and args.settle_line >= 2:
+        settle_other, settle_spec = settle_line(args, dev, stream, world, local, plan, args.settle_line)
+
     with_gather = None
     if rollout_mode and not args.no_gather:
         with_gather = {}
-        for key, dst, what in (("learner", 0, "point-to-point sends of every shard to rank 0 (the learner keeps "
-                                              "its own shard in place; nothing moves at world 1)"),
+        # the hand-off of launch k overlaps launch k + 1: a one-launch plan (the driver's 20 steps) is
+        # split in two so that there is something to overlap
+        gplan = plan if len(plan) >= 2 else launch_plan(args.steps, max(1, (args.steps + 1) // 2))
+        own = world == 1
+        for key, dst, what in (("learner", 0, "point-to-point sends of every shard to rank 0" +
+                                              (" (world 1: the learner's own shard copied into its receive slot "
+                                               "on a side stream, device to device)" if own else
+                                               " (the learner keeps its own shard in place)")),
                                ("all_gather", None, "torch.distributed.all_gather_into_tensor (RCCL): every "
                                                     "rank receives every shard")):
-            gms, wire = gather_pass(env, plan, world, local, dev, stream, dst)
+            gms, wire = gather_pass(env, gplan, world, local, dev, stream, dst, copy_own=own and dst == 0)
             with_gather[key] = {"value": total_env_steps / (gms * 1e-3), "ms_per_step": gms / args.steps,
                                 "collective": what + "; one hand-off per rollout launch, overlapped with the "
                                               "next launch (two record slots)",
-                                "launches": len(plan), "wire_bytes_per_rank": wire,
+                                "launches": len(gplan), "plan": gplan, "wire_bytes_per_rank": wire,
                                 "wire_bytes_per_env_step": wire // (env.n_alloc * args.steps),
                                 "records": "s, a, s' (final_state), r, flags of every env-step"}
 
@@ -728,7 +843,8 @@ def main():
                         "moved_bytes_per_env_step": algorithmic_bytes_per_env(W)}
         out = {
             "metric": "env steps/sec (batched PBN transitions), Bittner-28 at 1/2/4/8 GPUs"
-            if args.network == "pbn28" else f"env steps/sec (batched PBN transitions), {args.network}",
+            if args.network == "pbn28" and not settle_law else
+            f"env steps/sec (batched PBN transitions{', settle law' if settle_law else ''}), {args.network}",
             "value": value,
             "unit": "env-steps/s",
             "n_gpus": world,
@@ -757,6 +873,13 @@ def main():
                                "and event overhead, part of every timed region)",
                        "host_ms_per_step": host_s * 1e3 / args.steps, "clock_warm_runs": warm_reps},
         }
+        if settle is not None:
+            out["config"]["step_law"] = f"settle (at most {args.settle} updates per env step)"
+            out["settle"] = settle
+        elif rollout_mode:
+            out["config"]["step_law"] = "one synchronous update per env step (SURVEY.md 8(d)'s unit of work)"
+        if settle_other is not None:
+            out["settle_law"] = settle_other
         if with_gather is not None:
             out["value_with_gather"] = with_gather["learner"]["value"]
             out["gather"] = with_gather
@@ -767,6 +890,9 @@ def main():
                 out["cpu_baseline"] = cpu_baseline_bdq(spec, agent.q, args.cpu_seconds, threads)
             else:
                 out["cpu_baseline"] = cpu_baseline(spec, args.envs, args.cpu_seconds, threads)
+                if settle_other is not None:
+                    out["settle_law"]["cpu_baseline"] = cpu_baseline(settle_spec, args.envs, args.cpu_seconds / 2,
+                                                                     threads)
                 out["cpu_baseline_python"] = python_baseline(spec)
                 out["cpu_baseline_numpy"] = numpy_baseline(spec, args.envs)
                 out["config1"] = config1_line(dev)

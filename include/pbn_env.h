@@ -63,7 +63,7 @@
 extern "C" {
 #endif
 
-#define PBN_ABI_VERSION 3
+#define PBN_ABI_VERSION 4
 
 #define PBN_MAX_NODES 128
 #define PBN_MAX_ARITY 4
@@ -199,6 +199,22 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
                 int32_t n_steps, uint32_t mode, uint32_t* d_state, uint32_t* d_flipmask, uint8_t* d_target,
                 uint8_t* d_t, uint32_t* d_obs, uint32_t* d_final_state, float* d_reward, uint8_t* d_flags,
                 void* stream);
+
+/*
+ * pbn_rollout with one more output (ABI 4):
+ *   d_updates  [n_steps][n] uint16 out (nullable): the synchronous updates applied in each
+ *              env-step, 1 under the one-update law, 1..settle_max under the settle law (the
+ *              settle length; the env-step carries PBN_FLAG_UNSETTLED when it reached settle_max
+ *              outside every attractor).
+ * Under the settle law the pipelined kernel runs one update per iteration for each 32-env group
+ * and continues a group's step while any of its envs is outside every attractor.
+ *   the frame loop bdq_model/__init__.py:172-213 on the env constructed at train_BDQ.py:50 /
+ *   model_tester.py:409-413, whose step runs to an attractor (model_tester.py:616-626)
+ */
+int pbn_rollout_ex(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs,
+                   int32_t n_steps, uint32_t mode, uint32_t* d_state, uint32_t* d_flipmask, uint8_t* d_target,
+                   uint8_t* d_t, uint32_t* d_obs, uint32_t* d_final_state, float* d_reward, uint8_t* d_flags,
+                   uint16_t* d_updates, void* stream);
 
 /*
  * State histogram, the accumulation step of the steady-state distribution

@@ -32,6 +32,8 @@ def lib():
         vp, u64, i64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64, ctypes.c_uint32, ctypes.c_int
         L.oracle_step.argtypes = [vp, u64, u64, u64, i64, u32, vp, vp, vp, vp, vp, vp, vp, vp, i32]
         L.oracle_step.restype = i32
+        L.oracle_step_ex.argtypes = [vp, u64, u64, u64, i64, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32]
+        L.oracle_step_ex.restype = i32
         L.oracle_reset.argtypes = [vp, u64, u64, u64, i64, vp, vp, vp]
         L.oracle_reset.restype = i32
         L.oracle_philox4x32_10.argtypes = [vp, vp, vp]
@@ -71,7 +73,8 @@ def reset(spec, seed: int, step: int, env_offset: int, n: int):
 
 def step(spec, seed: int, step: int, env_offset: int, state, flipmask, target, t, mode: int,
          want_final: bool = True, n_threads: int = 0):
-    """Returns dict of outputs; target/t are returned updated (inputs are not modified)."""
+    """Returns dict of outputs; target/t are returned updated (inputs are not modified).
+    ``updates``: the synchronous updates applied per env (the settle length under the settle law)."""
     W, n = state.shape
     state = np.ascontiguousarray(state, dtype=np.uint32)
     flip = np.ascontiguousarray(flipmask, dtype=np.uint32).copy()
@@ -81,10 +84,11 @@ def step(spec, seed: int, step: int, env_offset: int, state, flipmask, target, t
     final = np.zeros((W, n), dtype=np.uint32) if want_final else None
     reward = np.zeros(n, dtype=np.float32)
     flags = np.zeros(n, dtype=np.uint8)
-    rc = lib().oracle_step(ctypes.addressof(spec.desc), seed, step, env_offset, n, mode,
-                           _p(state), _p(flip), _p(tgt), _p(tt), _p(out), _p(final), _p(reward),
-                           _p(flags), n_threads)
+    updates = np.zeros(n, dtype=np.uint16)
+    rc = lib().oracle_step_ex(ctypes.addressof(spec.desc), seed, step, env_offset, n, mode,
+                              _p(state), _p(flip), _p(tgt), _p(tt), _p(out), _p(final), _p(reward),
+                              _p(flags), _p(updates), n_threads)
     if rc != 0:
         raise ValueError(f"oracle_step failed ({rc})")
     return {"state_out": out, "final_state": final, "reward": reward, "flags": flags,
-            "target": tgt, "t": tt, "flipmask": flip}
+            "target": tgt, "t": tt, "flipmask": flip, "updates": updates}

@@ -227,9 +227,9 @@ static void group_digits(const pbn_net_desc* d, uint64_t seed, uint64_t G, uint6
  * until sp is a state of some attractor.  Update k: perturbation gaps j = 0, 1, ... from
  * SETTLE_ENV call ((k-1) << 8 | j >> 2), word j & 3; unperturbed, the rule update with the
  * group's SETTLE_SEL digits of update k (Dk[k-1], drawn on demand).  Returns 1 if still
- * outside every attractor after the last update. */
+ * outside every attractor after the last update; *nupd counts the updates applied. */
 static int settle(const pbn_net_desc* d, uint64_t seed, uint64_t G, uint64_t e, uint64_t step, int b,
-                  uint32_t (*Dk)[PBN_MAX_NODES][16], int* have, uint32_t* sp, int* perturbed) {
+                  uint32_t (*Dk)[PBN_MAX_NODES][16], int* have, uint32_t* sp, int* perturbed, int* nupd) {
   const int N = d->n_nodes, W = words_of(N);
   for (int k = 1; k < d->settle_max; ++k) {
     if (attractor_of(d, sp, W) >= 0) return 0;
@@ -255,14 +255,17 @@ static int settle(const pbn_net_desc* d, uint64_t seed, uint64_t G, uint64_t e, 
       rule_update(d, sp, Dk[k - 1], b, x);
       for (int w = 0; w < W; ++w) sp[w] = x[w];
     }
+    ++*nupd;
   }
   return attractor_of(d, sp, W) < 0;
 }
 
-int oracle_step(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n,
-                uint32_t mode, const uint32_t* state, uint32_t* flipmask, uint8_t* target, uint8_t* t,
-                uint32_t* state_out, uint32_t* final_state, float* reward, uint8_t* flags,
-                int n_threads) {
+/* one env step of every env; updates (nullable) = the synchronous updates applied per env
+ * (1, or the settle length under the settle law: pbn_rollout_ex's d_updates) */
+int oracle_step_ex(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n,
+                   uint32_t mode, const uint32_t* state, uint32_t* flipmask, uint8_t* target, uint8_t* t,
+                   uint32_t* state_out, uint32_t* final_state, float* reward, uint8_t* flags, uint16_t* updates,
+                   int n_threads) {
   const int N = d->n_nodes, W = words_of(N);
   if ((env_offset & 31u) || (n & 31)) return PBN_EINVAL;
   if (d->settle_max < 0 || d->settle_max > PBN_MAX_SETTLE) return PBN_EINVAL;
@@ -340,7 +343,9 @@ int oracle_step(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t en
       } else {
         rule_update(d, s1, D, b, sp);
       }
-      int unsettled = n_sub ? settle(d, seed, G, e, step, b, Dk, have, sp, &perturbed) : 0;
+      int nupd = 1;
+      int unsettled = n_sub ? settle(d, seed, G, e, step, b, Dk, have, sp, &perturbed, &nupd) : 0;
+      if (updates) updates[li] = (uint16_t)nupd;
       /* 5. reward / termination */
       int a = attractor_of(d, sp, W);
       int in_attr = a >= 0;
@@ -377,4 +382,11 @@ int oracle_step(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t en
     free(have);
   }
   return 0;
+}
+
+int oracle_step(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n,
+                uint32_t mode, const uint32_t* state, uint32_t* flipmask, uint8_t* target, uint8_t* t,
+                uint32_t* state_out, uint32_t* final_state, float* reward, uint8_t* flags, int n_threads) {
+  return oracle_step_ex(d, seed, step, env_offset, n, mode, state, flipmask, target, t, state_out, final_state,
+                        reward, flags, NULL, n_threads);
 }

@@ -25,7 +25,7 @@ FLAG_RESET = 16
 FLAG_UNSETTLED = 32
 
 EXPORTS = ["pbn_net_create", "pbn_net_destroy", "pbn_net_words", "pbn_reset", "pbn_step", "pbn_step_dev",
-           "pbn_rollout", "pbn_state_histogram", "pbn_obs_unpack", "pbn_bilinear_targets", "pbn_q_to_flipmask",
+           "pbn_rollout", "pbn_rollout_ex", "pbn_state_histogram", "pbn_obs_unpack", "pbn_bilinear_targets", "pbn_q_to_flipmask",
            "pbn_q_to_flipmask_dev",
            "pbn_heads_to_flipmask", "pbn_qnet_heads", "pbn_qnet_flipmask", "pbn_qnet_heads_from_state",
            "pbn_qnet_flipmask_from_state", "pbn_last_error", "pbn_abi_version"]
@@ -89,6 +89,9 @@ def load() -> ctypes.CDLL:
     L.pbn_step_dev.restype = ctypes.c_int
     L.pbn_rollout.argtypes = [vp, u64, u64, u64, i64, ctypes.c_int32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.pbn_rollout.restype = ctypes.c_int
+    L.pbn_rollout_ex.argtypes = [vp, u64, u64, u64, i64, ctypes.c_int32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                 vp]
+    L.pbn_rollout_ex.restype = ctypes.c_int
     L.pbn_state_histogram.argtypes = [vp, i64, i64, i64, ctypes.c_int32, vp, vp]
     L.pbn_state_histogram.restype = ctypes.c_int
     L.pbn_obs_unpack.argtypes = [vp, i64, vp, vp, vp, vp]

@@ -39,6 +39,8 @@ namespace pbn {
 // pbn_settle.hip: pbn_step_wave<W, B, 3> (lean = 0, pbn_step) or <W, B, 4> (lean = 1,
 // pbn_rollout) under the settle law, as an untyped host stub pointer (nullptr: no such W, B)
 void* settle_kernel(int W, int B, int lean);
+// pbn_settle.hip: pbn_rollout_settle<W, B> (pbn_rollout under the settle law, pipelined)
+void* settle_pipe_kernel(int W, int B);
 }  // namespace pbn
 
 namespace {
@@ -140,7 +142,9 @@ struct pbn_net {
   StepFn wave1 = nullptr;       // single step (pbn_step)
   StepFn wave_lean = nullptr;   // rollout, one wave per group (networks with gates)
   StepFn wave_settle = nullptr;       // pbn_step under the settle law (settle_max >= 2)
-  StepFn wave_settle_lean = nullptr;  // pbn_rollout under the settle law
+  StepFn wave_settle_lean = nullptr;  // pbn_rollout under the settle law (networks with gates)
+  StepFn pipe_settle = nullptr;       // pbn_rollout under the settle law, three waves per group pair
+  size_t lds_settle = 0;
   int settle_max = 0;
   StepFn pipe = nullptr;        // rollout, three waves per group pair (every other network)
   size_t lds_pipe = 0;
@@ -595,6 +599,9 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   net->wave_settle = reinterpret_cast<StepFn>(pbn::settle_kernel(W, d->prob_bits, 0));
   net->wave_settle_lean = reinterpret_cast<StepFn>(pbn::settle_kernel(W, d->prob_bits, 1));
   net->settle_max = d->settle_max;
+  net->pipe_settle = net->max_nf <= kNodeRecs ? reinterpret_cast<StepFn>(pbn::settle_pipe_kernel(W, d->prob_bits))
+                                              : nullptr;
+  net->lds_settle = net->lds_pipe + 8 * 4;   // + the per-half update plan [parity][half]{t, k}
   net->pipe = pick_pipe(W, d->prob_bits, net->max_nf > kNodeRecs);
   net->reset = pick_reset(W);
   // multiply-high divisors (exact for the operand ranges used: see actions_from_draw, autoreset)
@@ -622,10 +629,11 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     free_net(net);
     return rc;
   }
-  for (int ti = 0; ti < 5; ++ti) {
-    const StepFn fns[5] = {net->wave_settle, net->wave_settle_lean, net->wave_lean, net->wave1, net->pipe};
+  for (int ti = 0; ti < 6; ++ti) {
+    const StepFn fns[6] = {net->wave_settle, net->wave_settle_lean, net->wave_lean, net->wave1, net->pipe,
+                           net->pipe_settle};
     const StepFn fn = fns[ti];
-    const size_t bytes = ti == 4 ? net->lds_pipe : net->lds_wave;
+    const size_t bytes = ti == 5 ? net->lds_settle : (ti == 4 ? net->lds_pipe : net->lds_wave);
     if (!fn || bytes > 160 * 1024) continue;  // variant unusable for this net; never picked
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)bytes) != hipSuccess) {
@@ -795,6 +803,14 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
                 int32_t n_steps, uint32_t mode, uint32_t* d_state, uint32_t* d_flipmask, uint8_t* d_target,
                 uint8_t* d_t, uint32_t* d_obs, uint32_t* d_final_state, float* d_reward, uint8_t* d_flags,
                 void* stream) {
+  return pbn_rollout_ex(net, seed, step, env_offset, n_envs, n_steps, mode, d_state, d_flipmask, d_target, d_t,
+                        d_obs, d_final_state, d_reward, d_flags, nullptr, stream);
+}
+
+int pbn_rollout_ex(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs,
+                   int32_t n_steps, uint32_t mode, uint32_t* d_state, uint32_t* d_flipmask, uint8_t* d_target,
+                   uint8_t* d_t, uint32_t* d_obs, uint32_t* d_final_state, float* d_reward, uint8_t* d_flags,
+                   uint16_t* d_updates, void* stream) {
   int rc = check_common(net, env_offset, n_envs);
   if (rc) return rc;
   if (n_steps < 0) return fail(PBN_EINVAL, "n_steps < 0");
@@ -815,14 +831,23 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
   a.flags = d_flags;
   a.n_steps = n_steps;
   a.mode = (int)mode;
-  // the pipelined kernel for every network it supports (it beats the one-wave-per-group
+  a.updates = d_updates;
+  // the pipelined kernels for every network they support (they beat the one-wave-per-group
   // rollout at every measured size: profiles/r01_sweep_pbn28_variants_v4.jsonl); networks
   // with gates (lowered wide functions) run the wave kernel.  PBN_ROLL=lean|pipe forces one.
-  // The settle law runs the wave kernel (variant 4).
-  bool pipe = net->lds_pipe <= 64 * 1024 && !net->n_gates && net->settle_max < 2;
-  if (net->force_roll) pipe = net->force_roll == 3 && !net->n_gates && net->settle_max < 2;
+  const bool settle = net->settle_max >= 2;
+  bool pipe = (settle ? net->lds_settle : net->lds_pipe) <= 64 * 1024 && !net->n_gates && (!settle || net->pipe_settle);
+  if (net->force_roll) pipe = net->force_roll == 3 && !net->n_gates && (!settle || net->pipe_settle);
   if (pipe) {   // one block of three waves per pair of groups
     const int64_t pblocks = (a.n_groups + 1) / 2;
+    if (settle) {
+      hipLaunchKernelGGL(net->pipe_settle, dim3((unsigned)pblocks), dim3(192), net->lds_settle,
+                         (hipStream_t)stream, a);
+      HIP_OK(hipGetLastError());
+      return PBN_OK;
+    }
+    // the one-update law applies exactly one synchronous update per env-step
+    if (d_updates) HIP_OK(hipMemsetD16Async(d_updates, 1, (size_t)n_steps * (size_t)n_envs, (hipStream_t)stream));
     a.sel_prio = pblocks <= 4 * (int64_t)net->n_cus ? 1 : 0;
     hipLaunchKernelGGL(net->pipe, dim3((unsigned)pblocks), dim3(192), net->lds_pipe,
                        (hipStream_t)stream, a);

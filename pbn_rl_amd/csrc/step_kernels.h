@@ -92,7 +92,9 @@ struct StepArgs {
                        // of X is X * x_mult (times the start attractor's size, multi-state nets)
   int sel_prio;        // pipelined rollout: raise the selection wave's priority (grids of at most
                        // four blocks per CU)
-  int settle_max;      // step law: >= 2 = the settle law (wave kernel variants 3, 4)
+  int settle_max;      // step law: >= 2 = the settle law (wave kernel variants 3, 4,
+                       // pbn_rollout_settle)
+  uint16_t* updates;   // rollouts: [n_steps][n] synchronous updates applied per env-step (nullable)
 };
 
 // In-kernel phase clocks (cdna_hip_programming.md section 7, "In-kernel stamps"):
@@ -188,6 +190,9 @@ __device__ __forceinline__ T& lane_at(T* base, size_t uniform_elems, uint32_t la
 #else
 #define LANE_ST(base, ubase, le_, len, site, v) (LANE_AT(base, ubase, le_, len, site) = (v))
 #endif
+// LANE_ST with a per-lane element index (pbn_rollout_settle: the two halves of a wave may be
+// at different steps, so the step's base is not wave-uniform)
+#define LANE_STV(base, idx, len, site, v) __builtin_nontemporal_store((v), &(base)[CK((idx), (len), (site))])
 __device__ __forceinline__ uint32_t valid_word_mask(int n, int w) {
   const int bits = n - 32 * w;
   return bits >= 32 ? 0xFFFFFFFFu : (bits <= 0 ? 0u : ((1u << bits) - 1u));
@@ -623,7 +628,7 @@ template <int W, int B>
 __device__ __forceinline__ bool settle_updates(const StepArgs& a, const uint32_t* __restrict__ L, uint32_t* S,
                                             const uint4 (&rec_)[W][kNodeRecs], int lane, uint32_t ge_lo,
                                             uint32_t ge_hi, uint32_t G_lo, uint32_t G_hi, uint32_t st_lo,
-                                            uint32_t (&sp)[W], int& att, bool& pert) {
+                                            uint32_t (&sp)[W], int& att, bool& pert, uint32_t& nupd) {
   constexpr int CPN = B / 4;
   const bool lo = lane < 32;
   const int l32 = lane & 31;
@@ -680,6 +685,7 @@ __device__ __forceinline__ bool settle_updates(const StepArgs& a, const uint32_t
 #pragma unroll
       for (int w = 0; w < W; ++w) sp[w] = pk ? sp[w] ^ gam[w] : x[w];
       pert = pert || pk;
+      ++nupd;
       att = attractor_lookup<W>(a, htab, sp);
       open = att < 0;
     }
@@ -923,10 +929,14 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   }
   int att = lo ? attractor_lookup<W>(a, htab, sp) : 0;
   bool unsettled = false;
+  uint32_t nupd = 1;   // synchronous updates applied this step
   if constexpr (SETTLE) {   // the whole wave (cross-lane transposes)
-    unsettled = settle_updates<W, B>(a, L, S, rec_, lane, ge_lo, ge_hi, G_lo, G_hi, st_lo, sp, att, pert);
+    unsettled = settle_updates<W, B>(a, L, S, rec_, lane, ge_lo, ge_hi, G_lo, G_hi, st_lo, sp, att, pert, nupd);
   }
   if (lo) {
+  if constexpr (!SINGLE) {
+    if (a.updates) a.updates[CK(ks * n + le, n_steps * n, 23)] = (uint16_t)min(nupd, 0xFFFFu);
+  }
   if (a.final_state) {
 #pragma unroll
     for (int w = 0; w < W; ++w) a.final_state[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 10)] = sp[w];
@@ -1707,6 +1717,404 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
     __builtin_amdgcn_s_waitcnt(0);
     PBN_RSTAMP(6);
 #endif
+  }
+}
+
+// ------------------------------- settle-law rollout, three waves per pair of 32-env groups
+// pbn_rollout under the settle law (settle_max = K >= 2, include/pbn_env.h "Step law"): the
+// intervention, then synchronous updates until every env of the group is in an attractor or K
+// updates have run.  Same roles as pbn_rollout_pipe, but one iteration is one UPDATE (t, k) of a
+// step t (k = 0 the one-update law's draws; k >= 1 the SETTLE_ENV / SETTLE_SEL draws), and each
+// of the block's two groups (halves) runs its own sequence of updates:
+//   wave 1 (env draws): k = 0: ENV (+ PERT) call -> flip mask, autoreset draw, gaps;
+//                       k >= 1: the SETTLE_ENV gaps of update k (per env);
+//   wave 2 (selection): SEL (k = 0) or SETTLE_SEL (k >= 1) digit planes -> (u < c_j) masks;
+//   wave 0 (state):     the update of the envs still outside every attractor (all at k = 0),
+//                       the group's decision (continue or end the step), the step's epilogue.
+// Iteration i: the RNG waves produce update R(i) into slot i & 1 while the state wave applies
+// R(i-1).  Whether a group needs (t, k+1) or (t+1, 0) after R(i-1) is only known at the end of
+// iteration i, so R(i) is speculated as (t, k+1) (k + 1 < K) and re-issued as the state wave's
+// decision C when the speculation was wrong: one idle iteration of that group per step that ends
+// before the cap.  C is published in LDS per half and iteration parity; every wave derives the
+// same R, validity and loop exit from it, so all waves pass the same number of block barriers.
+// Results are bit-identical to pbn_step_wave's settle variants and to oracle/pbn_oracle.c.
+// The per-half update plan of pbn_rollout_settle, wave-uniform (SGPRs), identical in every wave.
+// P = R(i-1), the update produced in the previous iteration (t = ~0: none); C = C(i-2), the
+// state wave's decision after the update it applied in iteration i-1 (the next update each group
+// needs); R = R(i), the update the RNG waves produce in iteration i.  R(i-1) is valid (the state
+// wave applies it in iteration i) iff it equals C; R(i) continues a valid R(i-1) speculatively
+// ((t, k+1), or (t+1, 0) at the cap), else re-issues C.
+struct SettlePlan {
+  uint32_t Pt0 = ~0u, Pk0 = 0, Pt1 = ~0u, Pk1 = 0;
+  uint32_t Ct0 = 0, Ck0 = 0, Ct1 = 0, Ck1 = 0;
+  uint32_t Rt0 = 0, Rk0 = 0, Rt1 = 0, Rk1 = 0;
+  bool v0 = false, v1 = false;
+  // false once both groups have finished all steps (the loop's exit, the same in every wave)
+  __device__ __forceinline__ bool next(const uint32_t* ctl, uint32_t it, uint32_t K, uint32_t n_steps) {
+    const uint32_t* cin = ctl + ((it + 1) & 1) * 4;   // written in iteration i-1
+    Ct0 = __builtin_amdgcn_readfirstlane(cin[0]);
+    Ck0 = __builtin_amdgcn_readfirstlane(cin[1]);
+    Ct1 = __builtin_amdgcn_readfirstlane(cin[2]);
+    Ck1 = __builtin_amdgcn_readfirstlane(cin[3]);
+    if (Ct0 >= n_steps && Ct1 >= n_steps) return false;
+    v0 = Pt0 == Ct0 && Pk0 == Ck0;
+    v1 = Pt1 == Ct1 && Pk1 == Ck1;
+    Rt0 = v0 ? (Pk0 + 1 < K ? Pt0 : Pt0 + 1) : Ct0;
+    Rk0 = v0 ? (Pk0 + 1 < K ? Pk0 + 1 : 0u) : Ck0;
+    Rt1 = v1 ? (Pk1 + 1 < K ? Pt1 : Pt1 + 1) : Ct1;
+    Rk1 = v1 ? (Pk1 + 1 < K ? Pk1 + 1 : 0u) : Ck1;
+    return true;
+  }
+  __device__ __forceinline__ void done() {
+    Pt0 = Rt0; Pk0 = Rk0; Pt1 = Rt1; Pk1 = Rk1;
+  }
+};
+
+template <int W, int B>
+__global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(4, 8)))
+pbn_rollout_settle(StepArgs a) {
+  constexpr int CPN = B / 4;              // selection calls per node
+  extern __shared__ uint32_t smem[];
+  const int lane = threadIdx.x & 63;
+  const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (role == 0) __builtin_amdgcn_s_setprio(kStatePrio);
+  const int half = lane >> 5;
+  const int l32 = lane & 31;
+  const int64_t g = (int64_t)blockIdx.x * 2 + half;
+  const bool valid = g < a.n_groups;
+  const int N = a.n_nodes;
+  const int64_t n = a.n_envs;
+  const int64_t le = g * 32 + l32;
+  const uint64_t ge = a.env_offset + (uint64_t)le;
+  const uint64_t G = ge >> 5;
+  const size_t plane = (size_t)W * n;
+  const uint32_t n_steps = (uint32_t)a.n_steps;
+  const uint32_t K = (uint32_t)a.settle_max;
+  uint32_t* L = smem;
+  const float* rtab = reinterpret_cast<const float*>(L + a.cdf_len);
+  const uint32_t* htab = L + a.cdf_len + 4 * (N + 1);
+  const uint4* selq = reinterpret_cast<const uint4*>(L + a.sel_off);
+  const uint4* recL = reinterpret_cast<const uint4*>(L + a.nrec_off);
+  uint32_t* Sg = smem + a.tab_words + half * 32 * W;
+  uint32_t* slots = smem + a.tab_words + 2 * 32 * W;
+  uint32_t* cm = slots + 2 * (size_t)a.slot_words;                      // W == 1: threshold digit masks
+  uint32_t* ctl = cm + (W == 1 ? (kNodeRecs - 1) * B * 32 : 0);         // [parity][half]{t, k}
+  uint32_t st[W];
+  uint32_t tt0 = 0, tg0 = 0;
+#pragma unroll
+  for (int w = 0; w < W; ++w) st[w] = 0;
+  if (role == 0 && valid) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) st[w] = a.state[CK((size_t)w * n + le, plane, 1)];
+    tt0 = a.t[CK(le, n, 2)];
+    tg0 = a.target[CK(le, n, 3)];
+  }
+  copy_image(L, a);
+  if (threadIdx.x < 4) ctl[4 + threadIdx.x] = 0u;   // C before iteration 0: (t, k) = (0, 0) for both halves
+#pragma unroll
+  for (int w = 0; w < W; ++w) st[w] &= valid_word_mask(N, w);
+  uint32_t u_k0 = (uint32_t)a.seed, u_k1 = (uint32_t)(a.seed >> 32);
+  const uint32_t u_fl = __builtin_amdgcn_readfirstlane((a.obs ? 1u : 0u) | (a.final_state ? 2u : 0u) |
+                                                       ((a.mode & PBN_MODE_RANDOM_ACTIONS) ? 4u : 0u) |
+                                                       ((a.mode & PBN_MODE_AUTORESET) ? 8u : 0u) |
+                                                       (a.updates ? 32u : 0u));
+  __syncthreads();
+  if constexpr (W == 1) {   // threshold digit masks [q][d][32], as pbn_rollout_pipe
+    const int p = (int)threadIdx.x % ((kNodeRecs - 1) * 32), h = (int)threadIdx.x / ((kNodeRecs - 1) * 32);
+    const int i = p & 31, q = p >> 5;
+    uint32_t c = 0;
+    if (i < N && q < (int)recL[i].w - 1) c = recL[q * 32 + i].z;
+#pragma unroll
+    for (int dd = 0; dd < B / 2; ++dd) {
+      const int d = h * (B / 2) + dd;
+      cm[(q * B + d) * 32 + i] = ((c >> (B - 1 - d)) & 1u) ? ~0u : 0u;
+    }
+    __syncthreads();
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the initial state loads (see pbn_rollout_pipe)
+
+  const int mnf = __builtin_amdgcn_readfirstlane(a.max_nf);
+  // one loop per role (each role's loop-carried values occupy registers in that loop only);
+  // every role derives the same update plan from the LDS words, so all leave at the same iteration
+  if (role == 1) {
+    SettlePlan p;
+    for (uint32_t it = 0; p.next(ctl, it, K, n_steps); ++it) {
+      asm volatile("" : "+s"(u_k0), "+s"(u_k1));
+      const uint32_t Rt0 = p.Rt0, Rk0 = p.Rk0, Rt1 = p.Rt1, Rk1 = p.Rk1;
+      // ---- env draws of update R(i), env `lane`
+      const uint32_t t = half ? Rt1 : Rt0, k = half ? Rk1 : Rk0;
+      uint32_t* slot = slots + (size_t)(it & 1) * a.slot_words;
+      const uint64_t step = a.step + (uint64_t)t;
+      const uint32_t st_lo = (uint32_t)step;
+      const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
+      const uint32_t ge_lo = (uint32_t)ge;
+      if (valid && t < n_steps) {
+        uint32_t gam[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) gam[w] = 0;
+        if (k == 0) {
+          // the one-update law's draws of step t (pbn_rollout_pipe's general env loop)
+          const Word4 E = pbn::philox(ge_lo, st_lo, pbn::kStreamEnv << 28, ge_hi, u_k0, u_k1);
+          uint32_t m[W], rsv[W];
+#pragma unroll
+          for (int w = 0; w < W; ++w) { m[w] = 0; rsv[w] = 0; }
+          uint32_t xhi = E.w, xlo = E.z;
+          const uint32_t n1 = (uint32_t)(N + 1);
+          const uint32_t c_act = ext64(xhi, xlo, n1 * n1 * n1);
+          uint64_t xr = ((((uint64_t)E.w) << 32) | E.z) * a.x_mult;
+          uint32_t rtv;
+          if (a.n_attr >= 1) {
+            const int32_t* att_first = reinterpret_cast<const int32_t*>(L + a.att_off);
+            const uint32_t* att_words = L + a.att_off + a.n_attr + 1;
+            const uint32_t A = (uint32_t)a.n_attr;
+            uint32_t as = 0;
+            rtv = 0;
+            if (A >= 2) {
+              const uint32_t c = ext64(xhi, xlo, A * (A - 1));
+              as = a.am1_magic ? __umulhi(c, a.am1_magic) : c;
+              rtv = c - as * (A - 1);
+              rtv += (rtv >= as) ? 1u : 0u;
+            }
+            const int st0 = a.att_single ? (int)as : att_first[as];
+            uint32_t idx = 0;
+            if (!a.att_single) {
+              const uint32_t size = (uint32_t)(att_first[as + 1] - st0);
+              idx = ext64(xhi, xlo, size);
+              xr *= size;
+            }
+#pragma unroll
+            for (int w = 0; w < W; ++w) rsv[w] = att_words[(size_t)(st0 + idx) * W + w];
+          } else {
+            const Word4 rr = pbn::philox(ge_lo, st_lo, (pbn::kStreamReset << 28) | 1u, ge_hi, u_k0, u_k1);
+            const uint32_t rw4[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+            for (int w = 0; w < W; ++w) rsv[w] = rw4[w] & valid_word_mask(N, w);
+            rtv = PBN_NO_TARGET;
+          }
+          const uint32_t u2 = (uint32_t)(xr >> 32);
+          if (u_fl & 4u) {
+            actions_from_draw<W>(c_act, N, a.n1_magic, m);
+#pragma unroll
+            for (int w = 0; w < W; ++w) LANE_STV(a.flipmask, (t * plane + (size_t)w * n) + (size_t)le, (size_t)n_steps * plane, 8, m[w]);
+          } else {
+#pragma unroll
+            for (int w = 0; w < W; ++w)
+              m[w] = a.flipmask[CK((t * plane + (size_t)w * n) + (size_t)le, (size_t)n_steps * plane, 6)] & valid_word_mask(N, w);
+          }
+          uint32_t pcv = 0;
+#pragma unroll
+          for (int w = 0; w < W; ++w) pcv += __builtin_popcount(m[w]);
+          const int g0 = gap_any(a.gap_exact, L, a, E.x), g1 = gap_any(a.gap_exact, L, a, E.y),
+                    g2 = gap_any(a.gap_exact, L, a, u2);
+          const int p0 = g0 - 1, p1 = p0 + g1, p2 = p1 + g2;
+          set_bit<W>(gam, p0, N);
+          set_bit<W>(gam, p1, N);
+          set_bit<W>(gam, p2, N);
+          if (p2 < N - 1) {   // rare: a fourth flip (gap k >= 3: PERT call (k-3)>>2, word (k-3)&3)
+            Word4 P = E;
+            int pos = p2;
+            for (int kk = 3; pos < N - 1; ++kk) {
+              if (((kk - 3) & 3) == 0)
+                P = pbn::philox(ge_lo, st_lo, (pbn::kStreamPert << 28) | (uint32_t)((kk - 3) >> 2), ge_hi, u_k0, u_k1);
+              const int j4 = (kk - 3) & 3;
+              const uint32_t u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
+              pos += gap_any(a.gap_exact, L, a, u);
+              set_bit<W>(gam, pos, N);
+            }
+          }
+          bool pert = false;
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            pert = pert || gam[w] != 0;
+            slot[w * 64 + lane] = m[w];
+            slot[(2 * W + w) * 64 + lane] = rsv[w];
+          }
+          slot[3 * W * 64 + lane] = rtv | (pcv << 8) | ((uint32_t)pert << 16);
+        } else {
+          // update k >= 1: perturbation gaps j = 0, 1, ... from SETTLE_ENV call ((k-1) << 8 | j >> 2), word j & 3
+          const uint32_t sub = k - 1;
+          Word4 P = {0, 0, 0, 0};
+          int pos = -1;
+          for (int j = 0; pos < N - 1; ++j) {
+            if ((j & 3) == 0)
+              P = pbn::philox(ge_lo, st_lo, (pbn::kStreamSettleEnv << 28) | (sub << 8) | (uint32_t)(j >> 2), ge_hi,
+                              u_k0, u_k1);
+            const int j4 = j & 3;
+            const uint32_t u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
+            pos += gap_any(a.gap_exact, L, a, u);
+            set_bit<W>(gam, pos, N);
+          }
+          bool pert = false;
+#pragma unroll
+          for (int w = 0; w < W; ++w) pert = pert || gam[w] != 0;
+          slot[3 * W * 64 + lane] = (uint32_t)pert << 16;
+        }
+#pragma unroll
+        for (int w = 0; w < W; ++w) slot[(W + w) * 64 + lane] = gam[w];
+      }
+      lds_barrier();
+      p.done();
+    }
+  } else if (role == 2) {
+    SettlePlan p;
+    for (uint32_t it = 0; p.next(ctl, it, K, n_steps); ++it) {
+      asm volatile("" : "+s"(u_k0), "+s"(u_k1));
+      const uint32_t Rt0 = p.Rt0, Rk0 = p.Rk0, Rt1 = p.Rt1, Rk1 = p.Rk1;
+      // ---- selection masks of update R(i): node l32 + 32r of group g
+      const uint32_t t = half ? Rt1 : Rt0, k = half ? Rk1 : Rk0;
+      uint32_t* lt_out = slots + (size_t)(it & 1) * a.slot_words + (3 * W + 1) * 64 + half * 32 * W;
+      const uint64_t step = a.step + (uint64_t)t;
+      const uint32_t st_lo = (uint32_t)step;
+      const uint32_t G_hi = (uint32_t)((G >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
+      const uint32_t G_lo = (uint32_t)G;
+      // SEL (k = 0) or SETTLE_SEL idx (k-1) << 9 | 4i + c (k >= 1)
+      const uint32_t base = k == 0 ? (pbn::kStreamSel << 28) : ((pbn::kStreamSettleSel << 28) | ((k - 1) << 9));
+      if (valid && t < n_steps) {
+#pragma unroll
+        for (int r = 0; r < W; ++r) {
+          const int i = l32 + 32 * r;
+          const int ic = i < N ? i : 0;
+          const uint4 r0 = recL[ic];
+          if (i < N && (int)r0.w > 1) {
+            uint32_t dig[16];
+#pragma unroll
+            for (int c = 0; c < CPN; ++c) {
+              const Word4 o = pbn::philox(G_lo, st_lo, base | (uint32_t)(4 * i + c), G_hi, u_k0, u_k1);
+              dig[4 * c + 0] = o.x; dig[4 * c + 1] = o.y; dig[4 * c + 2] = o.z; dig[4 * c + 3] = o.w;
+            }
+            const int nf = (int)r0.w;
+#pragma unroll
+            for (int q = 0; q < kNodeRecs - 1; ++q)
+              if (q < nf - 1) {
+                if constexpr (W == 1)
+                  lt_out[q * 64 * W + i] = less_than_cm<B>(dig, cm + (size_t)q * B * 32 + i, 32);
+                else
+                  lt_out[q * 64 * W + i] = less_than(dig, recL[q * 32 * W + ic].z, B);
+              }
+          }
+        }
+      }
+      lds_barrier();
+      p.done();
+    }
+  } else {
+    // per-env state of the step in progress
+    uint32_t cur[W], rs[W];
+    uint32_t rt = 0, pc = 0, nupd = 0;
+    bool open = false, pacc = false;
+    int att = -1;
+#pragma unroll
+    for (int w = 0; w < W; ++w) { cur[w] = 0; rs[w] = 0; }
+    SettlePlan p;
+    for (uint32_t it = 0; p.next(ctl, it, K, n_steps); ++it) {
+      const uint32_t Pt0 = p.Pt0, Pk0 = p.Pk0, Pt1 = p.Pt1, Pk1 = p.Pk1;
+      const uint32_t Ct0 = p.Ct0, Ck0 = p.Ck0, Ct1 = p.Ct1, Ck1 = p.Ck1;
+      const bool v0 = p.v0, v1 = p.v1;
+      // ---- state: apply R(i-1) (slot (i-1) & 1) to the groups for which it is valid
+      const bool proc0 = v0 && Pt0 < n_steps, proc1 = v1 && Pt1 < n_steps;
+      const bool proc = half ? proc1 : proc0;
+      const uint32_t t = half ? Pt1 : Pt0, k = half ? Pk1 : Pk0;
+      const uint32_t* slot = slots + (size_t)((it + 1) & 1) * a.slot_words;
+      const uint32_t* lt_in = slot + (3 * W + 1) * 64 + half * 32 * W;
+      uint32_t s1[W], gam[W];
+      const uint32_t info = slot[3 * W * 64 + lane];
+      const bool pk = (info >> 16) & 1u;
+      if (k == 0) {
+        if (proc && valid && (u_fl & 1u)) {
+#pragma unroll
+          for (int w = 0; w < W; ++w) LANE_STV(a.obs, (t * plane + (size_t)w * n) + (size_t)le, (size_t)n_steps * plane, 7, st[w]);
+        }
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          s1[w] = st[w] ^ slot[w * 64 + lane];
+          if (proc) rs[w] = slot[(2 * W + w) * 64 + lane];
+        }
+        if (proc) {
+          rt = info & 0xFFu;
+          pc = (info >> 8) & 0xFFu;
+          open = valid;
+          pacc = false;
+          nupd = 0;
+        }
+      } else {
+#pragma unroll
+        for (int w = 0; w < W; ++w) s1[w] = cur[w];
+      }
+#pragma unroll
+      for (int w = 0; w < W; ++w) gam[w] = slot[(W + w) * 64 + lane];
+#pragma unroll
+      for (int w = 0; w < W; ++w) Sg[32 * w + l32] = lane_transpose32(s1[w], lane);
+      __builtin_amdgcn_wave_barrier();
+      uint32_t X[W];
+#pragma unroll
+      for (int r = 0; r < W; ++r) {
+        int i = l32 + 32 * r;
+        asm volatile("" : "+v"(i));   // selector and record reads stay in the loop
+        const uint4* rc = recL + i;
+        const uint4* sel = selq + i;
+        const uint32_t* lti = lt_in + i;
+        switch (mnf) {
+          case 1: X[r] = chain_padded<1, (W <= 2)>(rc, sel, 32 * W, Sg, lti, 64 * W); break;
+          case 2: X[r] = chain_padded<2, (W <= 2)>(rc, sel, 32 * W, Sg, lti, 64 * W); break;
+          case 3: X[r] = chain_padded<3, (W <= 2)>(rc, sel, 32 * W, Sg, lti, 64 * W); break;
+          default: X[r] = chain_padded<4, (W <= 2)>(rc, sel, 32 * W, Sg, lti, 64 * W); break;
+        }
+      }
+      uint32_t sp[W];
+#pragma unroll
+      for (int w = 0; w < W; ++w) sp[w] = lane_transpose32(X[w], lane);
+      if (proc && open) {
+#pragma unroll
+        for (int w = 0; w < W; ++w) cur[w] = pk ? (s1[w] ^ gam[w]) : sp[w];
+        pacc = pacc || pk;
+        ++nupd;
+        att = attractor_lookup<W>(a, htab, cur);
+        open = att < 0;
+      }
+      // the group's decision: the step ends when no env of the group is open or the cap is reached
+      const uint64_t ob = __ballot(proc && open);
+      const bool end0 = proc0 && ((uint32_t)ob == 0u || Pk0 + 1 >= K);
+      const bool end1 = proc1 && ((uint32_t)(ob >> 32) == 0u || Pk1 + 1 >= K);
+      if (lane == 0) {
+        uint32_t* cout = ctl + (it & 1) * 4;
+        cout[0] = proc0 ? (end0 ? Pt0 + 1 : Pt0) : Ct0;
+        cout[1] = proc0 ? (end0 ? 0u : Pk0 + 1) : Ck0;
+        cout[2] = proc1 ? (end1 ? Pt1 + 1 : Pt1) : Ct1;
+        cout[3] = proc1 ? (end1 ? 0u : Pk1 + 1) : Ck1;
+      }
+      if ((half ? end1 : end0) && valid) {
+        // epilogue of step t
+        if (u_fl & 2u) {
+#pragma unroll
+          for (int w = 0; w < W; ++w) LANE_STV(a.final_state, (t * plane + (size_t)w * n) + (size_t)le, (size_t)n_steps * plane, 10, cur[w]);
+        }
+        if (u_fl & 32u) LANE_STV(a.updates, ((size_t)t * n) + (size_t)le, (size_t)n_steps * n, 23, (uint16_t)min(nupd, 0xFFFFu));
+        const float4 r4 = reinterpret_cast<const float4*>(rtab)[pc];
+        const bool in_attr = att >= 0;
+        const bool term = in_attr && (uint32_t)att == tg0;
+        const bool wrong = in_attr && !term;
+        int tt = (int)tt0 + 1;
+        tt = tt > 255 ? 255 : tt;
+        const bool trunc = a.horizon > 0 && tt >= a.horizon;
+        const bool reset = (u_fl & 8u) && (term || trunc);
+        const uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) |
+                            ((uint32_t)pacc << 3) | ((uint32_t)reset << 4) | ((uint32_t)open << 5);
+        LANE_STV(a.reward, ((size_t)t * n) + (size_t)le, (size_t)n_steps * n, 11, term ? r4.z : (wrong ? r4.y : r4.x));
+        LANE_STV(a.flags, ((size_t)t * n) + (size_t)le, (size_t)n_steps * n, 15, (uint8_t)fl);
+        tg0 = reset ? rt : tg0;
+        tt0 = reset ? 0u : (uint32_t)tt;
+#pragma unroll
+        for (int w = 0; w < W; ++w) st[w] = reset ? rs[w] : cur[w];
+      }
+      lds_barrier();
+      p.done();
+    }
+    if (valid) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) a.state_out[CK((size_t)w * n + le, plane, 16)] = st[w];
+      a.t[CK(le, n, 17)] = (uint8_t)tt0;
+      a.target[CK(le, n, 18)] = (uint8_t)tg0;
+    }
   }
 }
 

@@ -19,7 +19,13 @@ tests), in one of two forms:
 in a ring of ``buffers`` slots (two by default), the collective of rollout k is
 issued asynchronously behind rollout k on the communicator's own stream, and
 rollout k + buffers waits (stream-side, no host sync) only for the collective
-that last read its slot.
+that last read its slot.  With one slot there is nothing to overlap: each
+rollout is consumed before the next one overwrites the slot.
+
+``gather(rec, dst, copy_own=True)`` also copies the learner's own shard into its
+receive slot (on a side stream, overlapped like the collective), so that every
+shard ends in a learner-owned buffer; at world 1 that copy is the whole
+hand-off (bench.py's ``value_with_gather``).
 
 Wire format (``TransitionRecords``): one flat byte buffer per shard and rollout,
 field-major so that ``pbn_rollout`` writes every field in place (no packing
@@ -161,22 +167,24 @@ class ShardedRollout:
         rec._slot = k
         return rec
 
-    def gather(self, rec: TransitionRecords, dst: Optional[int] = None, async_op: bool = False):
+    def gather(self, rec: TransitionRecords, dst: Optional[int] = None, async_op: bool = False,
+               copy_own: bool = False):
         """Hand the records of one rollout to the learner.
 
         dst = None: ``all_gather_into_tensor``; every rank receives every rank's records
         (rank r's envs are offset_r + i: rank-major = global order).  dst = r: point-to-point
-        sends to rank r; rank r receives the other shards and uses its own in place, the
-        other ranks receive nothing (an empty list).  Returns the list of per-rank records
-        (valid until ``buffers`` further gathers of this shape and form) or, with async_op,
-        (records, work): the records are readable on the current stream after ``work.wait()``.
+        sends to rank r; rank r receives the other shards and uses its own in place (or, with
+        ``copy_own``, copies it into its receive slot too), the other ranks receive nothing (an
+        empty list).  Returns the list of per-rank records (valid until ``buffers`` further
+        gathers of this shape and form) or, with async_op, (records, work): the records are
+        readable on the current stream after ``work.wait()``.
         """
-        if not dist.is_initialized() or (self.world == 1 and dst is not None):
+        if dst is not None and not copy_own and (not dist.is_initialized() or self.world == 1):
             # the learner's own shard: already where the kernel wrote it (all_gather still runs
             # at world 1, so the collective path is exercised on a one-GPU box)
             return ([rec], None) if async_op else [rec]
         nbytes = rec.flat.numel()
-        key = (rec.steps, dst)
+        key = (rec.steps, dst, copy_own)
         recv = self._recv.setdefault(key, [])
         k = self._gathered.get(key, 0) % self.buffers
         self._gathered[key] = self._gathered.get(key, 0) + 1
@@ -188,7 +196,8 @@ class ShardedRollout:
             parts = [TransitionRecords(rec.steps, rec.words, rec.n, flat=out[r * nbytes:(r + 1) * nbytes])
                      for r in range(self.world)]
         else:
-            gdst = dist.get_global_rank(self.group, dst) if self.group is not None else dst
+            gdst = (dist.get_global_rank(self.group, dst) if self.group is not None else dst) if self.world > 1 else dst
+            works = []
             if self.rank == dst:
                 if len(recv) <= k:
                     recv.append(torch.empty(self.world * nbytes, dtype=torch.uint8, device=rec.flat.device))
@@ -196,13 +205,16 @@ class ShardedRollout:
                 ops = [dist.P2POp(dist.irecv, out[r * nbytes:(r + 1) * nbytes],
                                   dist.get_global_rank(self.group, r) if self.group is not None else r, self.group)
                        for r in range(self.world) if r != dst]
-                parts = [rec if r == dst else
+                if copy_own:
+                    works.append(self._copy_async(out[dst * nbytes:(dst + 1) * nbytes], rec.flat))
+                parts = [rec if (r == dst and not copy_own) else
                          TransitionRecords(rec.steps, rec.words, rec.n, flat=out[r * nbytes:(r + 1) * nbytes])
                          for r in range(self.world)]
             else:
                 ops = [dist.P2POp(dist.isend, rec.flat, gdst, self.group)]
                 parts = []
-            works = dist.batch_isend_irecv(ops)
+            if ops:
+                works.extend(dist.batch_isend_irecv(ops))
             work = _Works(works)
         slot = getattr(rec, "_slot", None)
         if slot is not None:   # the slot's next rollout must wait for this read of it
@@ -212,15 +224,34 @@ class ShardedRollout:
         _wait(work)
         return parts
 
+    def _copy_async(self, out: torch.Tensor, src: torch.Tensor):
+        """out <- src on a side stream ordered after the current stream's work so far; the
+        returned work's wait() orders the current stream after the copy (as a collective's)."""
+        cur = torch.cuda.current_stream(src.device)
+        side = getattr(self, "_side", None)
+        if side is None:
+            side = self._side = torch.cuda.Stream(device=src.device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            out.copy_(src, non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(side)
+        return _StreamWork(done, src.device)
+
     def run(self, n_rollouts: int, steps: int, dst: Optional[int] = None, consume=None,
-            random_actions: bool = True) -> None:
-        """``n_rollouts`` rollouts with the hand-off of rollout k overlapped with rollout k + 1.
-        ``consume(k, parts)`` is called on the learner (every rank for dst=None) once rollout
-        k's records are readable on the current stream (after the device-side wait)."""
+            random_actions: bool = True, copy_own: bool = False) -> None:
+        """``n_rollouts`` rollouts with the hand-off of rollout k overlapped with rollout k + 1
+        (two or more record slots; with one slot, rollout k is consumed before rollout k + 1
+        overwrites it).  ``consume(k, parts)`` is called on the learner (every rank for dst=None)
+        once rollout k's records are readable on the current stream (after the device-side
+        wait)."""
         prev = None
         for k in range(n_rollouts):
             rec = self.rollout(steps, random_actions=random_actions)
-            parts, work = self.gather(rec, dst=dst, async_op=True)
+            parts, work = self.gather(rec, dst=dst, async_op=True, copy_own=copy_own)
+            if self.buffers < 2:
+                _finish((k, parts, work), consume)
+                continue
             if prev is not None:
                 _finish(prev, consume)
             prev = (k, parts, work)
@@ -244,6 +275,17 @@ class _Works:
         works, self.works = self.works, []
         for w in works:
             w.wait()
+
+
+class _StreamWork:
+    """A side-stream copy's completion as a work object: wait() orders the current stream
+    after it (no host synchronisation)."""
+
+    def __init__(self, event, device):
+        self.event, self.device = event, device
+
+    def wait(self):
+        torch.cuda.current_stream(self.device).wait_event(self.event)
 
 
 def _wait(work) -> None:

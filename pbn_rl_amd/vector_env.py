@@ -203,31 +203,35 @@ class VectorPBNEnv:
         k = self.num_envs
         return self.state[:, :k], self.reward[:k], self.flags[:k]
 
-    def rollout_buffers(self, n_steps: int, keep_obs: bool = False, keep_final: bool = True) -> dict:
+    def rollout_buffers(self, n_steps: int, keep_obs: bool = False, keep_final: bool = True,
+                        keep_updates: bool = False) -> dict:
         """Output buffers of an ``n_steps`` rollout.  Uninitialised: the kernel writes every
         element of every buffer it is given (all ``n_alloc`` envs, all steps), and ``rollout``
         writes the flip masks itself when it does not draw them.  Allocate them before a
-        hipGraph capture so that the graph holds the rollout launch alone."""
+        hipGraph capture so that the graph holds the rollout launch alone.  ``keep_updates``:
+        the synchronous updates of every env-step (uint16; the settle length under the settle law)."""
         W, n, dev = self.words, self.n_alloc, self.device
         return {"_n_steps": n_steps,
                 "flipmask": torch.empty(n_steps, W, n, dtype=torch.int32, device=dev),
                 "reward": torch.empty(n_steps, n, dtype=torch.float32, device=dev),
                 "flags": torch.empty(n_steps, n, dtype=torch.uint8, device=dev),
                 "obs": torch.empty(n_steps, W, n, dtype=torch.int32, device=dev) if keep_obs else None,
-                "final_state": torch.empty(n_steps, W, n, dtype=torch.int32, device=dev) if keep_final else None}
+                "final_state": torch.empty(n_steps, W, n, dtype=torch.int32, device=dev) if keep_final else None,
+                "updates": torch.empty(n_steps, n, dtype=torch.int16, device=dev) if keep_updates else None}
 
     def rollout(self, n_steps: int, flipmasks: Optional[torch.Tensor] = None, random_actions: bool = True,
-                keep_obs: bool = False, keep_final: bool = True, out: Optional[dict] = None) -> dict:
-        """``n_steps`` transitions in one ``pbn_rollout`` launch (state kept on chip).
+                keep_obs: bool = False, keep_final: bool = True, out: Optional[dict] = None,
+                keep_updates: bool = False) -> dict:
+        """``n_steps`` env steps in one ``pbn_rollout_ex`` launch (state kept on chip).
 
         flipmasks: optional (n_steps, W, num_envs) interventions (else in-kernel random
         actions when ``random_actions``, else none).  Returns views of
-        ``flipmask`` / ``reward`` / ``flags`` (+ ``obs`` / ``final_state``) shaped
+        ``flipmask`` / ``reward`` / ``flags`` (+ ``obs`` / ``final_state`` / ``updates``) shaped
         (n_steps, ...); pass ``out`` (a previous result) to reuse its buffers."""
         L = _lib.load()
         n, k = self.n_alloc, self.num_envs
         if out is None or out["_n_steps"] != n_steps:
-            out = self.rollout_buffers(n_steps, keep_obs, keep_final)
+            out = self.rollout_buffers(n_steps, keep_obs, keep_final, keep_updates)
         mode = _lib.MODE_AUTORESET if self.autoreset else 0
         if flipmasks is not None:
             out["flipmask"][:, :, :k].copy_(flipmasks)
@@ -238,11 +242,12 @@ class VectorPBNEnv:
             out["flipmask"].zero_()
         ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
         with torch.cuda.device(self.device):
-            _lib.check(L.pbn_rollout(self.net.handle, self.seed, self.step_index, self.env_offset, n, n_steps, mode,
-                                     self.state.data_ptr(), out["flipmask"].data_ptr(), self.target.data_ptr(),
-                                     self.t.data_ptr(), ptr(out["obs"]), ptr(out["final_state"]),
-                                     out["reward"].data_ptr(), out["flags"].data_ptr(), self._stream()),
-                       "pbn_rollout")
+            _lib.check(L.pbn_rollout_ex(self.net.handle, self.seed, self.step_index, self.env_offset, n, n_steps,
+                                        mode, self.state.data_ptr(), out["flipmask"].data_ptr(),
+                                        self.target.data_ptr(), self.t.data_ptr(), ptr(out["obs"]),
+                                        ptr(out["final_state"]), out["reward"].data_ptr(), out["flags"].data_ptr(),
+                                        ptr(out.get("updates")), self._stream()),
+                       "pbn_rollout_ex")
         self.step_index += n_steps
         return out
 

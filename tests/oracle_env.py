@@ -28,6 +28,7 @@ class OracleVectorEnv:
         self.state = torch.from_numpy(out["state_out"].view(np.int32).copy())
         self.flipmask = torch.from_numpy(out["flipmask"].view(np.int32).copy())
         self.final_state = torch.from_numpy(out["final_state"].view(np.int32).copy())
+        self.updates = torch.from_numpy(out["updates"].view(np.int16).copy())
         return self.state, torch.from_numpy(out["reward"]), torch.from_numpy(out["flags"])
 
     def rollout(self, n_steps, flipmasks=None, random_actions=True, keep_obs=True, keep_final=True, out=None):
@@ -38,7 +39,8 @@ class OracleVectorEnv:
             "flipmask": torch.empty((n_steps, W, n), dtype=torch.int32),
             "final_state": torch.empty((n_steps, W, n), dtype=torch.int32),
             "reward": torch.empty((n_steps, n), dtype=torch.float32),
-            "flags": torch.empty((n_steps, n), dtype=torch.uint8)}
+            "flags": torch.empty((n_steps, n), dtype=torch.uint8),
+            "updates": torch.empty((n_steps, n), dtype=torch.int16)}
         for k in range(n_steps):
             rec["obs"][k] = self.state
             fm = None if flipmasks is None else flipmasks[k]
@@ -47,4 +49,6 @@ class OracleVectorEnv:
             rec["final_state"][k] = self.final_state
             rec["reward"][k] = reward
             rec["flags"][k] = flags
+            if "updates" in rec:
+                rec["updates"][k] = self.updates
         return rec

@@ -37,8 +37,9 @@ def _worker(rank, world, port, n_total, steps, result_path, form="all"):
     from tests.oracle_env import OracleVectorEnv
 
     spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.05)
-    ro = ShardedRollout(n_total, lambda off, cnt: OracleVectorEnv(spec, off, cnt, seed=11))
-    if form == "run":
+    ro = ShardedRollout(n_total, lambda off, cnt: OracleVectorEnv(spec, off, cnt, seed=11),
+                        buffers=1 if form == "run1" else 2)
+    if form in ("run", "run1"):
         # three rollouts, each hand-off to rank 0 overlapped with the next rollout
         got = {}
         ro.run(3, steps, dst=0, consume=lambda k, parts: got.__setitem__(
@@ -93,10 +94,12 @@ def test_record_wire_format():
         TransitionRecords(1, 1, 48)
 
 
-def test_two_rank_overlapped_run_equals_single_run(tmp_path):
+@pytest.mark.parametrize("form", ["run", "run1"])
+def test_two_rank_overlapped_run_equals_single_run(tmp_path, form):
     """ShardedRollout.run: three rollouts with the hand-off of rollout k to rank 0 in flight
-    while rollout k + 1 runs (two record slots): rank 0 receives all three, equal to three
-    successive rollouts of one process."""
+    while rollout k + 1 runs (two record slots; "run1": one slot, each rollout consumed before
+    the next overwrites it): rank 0 receives all three, equal to three successive rollouts of
+    one process."""
     from pbn_rl_amd.attractors import load_attractors
     from pbn_rl_amd.network import load_network
     from pbn_rl_amd.spec import EnvSpec
@@ -104,7 +107,7 @@ def test_two_rank_overlapped_run_equals_single_run(tmp_path):
 
     n_total, steps = 256, 3
     out = str(tmp_path / "run.pt")
-    mp.spawn(_worker, args=(2, _free_port(), n_total, steps, out, "run"), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), n_total, steps, out, form), nprocs=2, join=True)
     got = torch.load(out, weights_only=True)
     spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.05)
     single = ShardedRollout(n_total, lambda off, cnt: OracleVectorEnv(spec, off, cnt, seed=11), buffers=1)

@@ -169,11 +169,12 @@ def run_rollout_pair(spec, n, R, mode, *, seed=4242, env_offset=2048):
         if spec.n % 32:
             flips[:, W - 1] &= np.uint32((1 << (spec.n % 32)) - 1)
         fm = torch.from_numpy(flips.view(np.int32)).to(env.device)
-    out = env.rollout(R, flipmasks=fm, random_actions=bool(mode & 2), keep_obs=True)
+    out = env.rollout(R, flipmasks=fm, random_actions=bool(mode & 2), keep_obs=True, keep_updates=True)
     for k in range(R):
         flip = np.zeros((W, n), np.uint32) if flips is None else flips[k]
         ref = oracle.step(spec, seed, 1 + k, env_offset, st, flip, tg, t, mode)
         assert np.array_equal(u32(out["obs"][k])[:, :n], st), k
+        assert np.array_equal(out["updates"][k].cpu().numpy().view(np.uint16)[:n], ref["updates"]), k
         assert np.array_equal(u32(out["final_state"][k])[:, :n], ref["final_state"]), k
         assert np.array_equal(out["flags"][k].cpu().numpy()[:n], ref["flags"]), k
         assert np.array_equal(out["reward"][k].cpu().numpy()[:n].view(np.uint32), ref["reward"].view(np.uint32)), k
@@ -183,6 +184,7 @@ def run_rollout_pair(spec, n, R, mode, *, seed=4242, env_offset=2048):
     assert np.array_equal(env.target.cpu().numpy()[:n], tg)
     assert np.array_equal(env.t.cpu().numpy()[:n], t)
     env.close()
+    return ref
 
 
 @pytest.mark.parametrize("variant", ["pipe", "lean"])

@@ -1,23 +1,31 @@
 """The settle law on the GPU (include/pbn_env.h "Step law"): kernels == oracle bit for bit, and
 the reference's bb33 evaluation replayed through the gym facade on the device.
 
-pbn_step and pbn_rollout run the wave kernel's settle variants (3, 4) when the descriptor's
-settle_max >= 2; every output is compared with oracle/pbn_oracle.c, including the
-PBN_FLAG_UNSETTLED bit of envs that hit the cap.
+pbn_step runs the wave kernel's settle variant 3 when the descriptor's settle_max >= 2;
+pbn_rollout runs the pipelined settle kernel (pbn_rollout_settle: one update per iteration, a
+group's step continues while any env is outside every attractor) for networks without gates,
+and the wave kernel's variant 4 for networks with gates or under PBN_ROLL=lean.  Every output is
+compared with oracle/pbn_oracle.c, including the PBN_FLAG_UNSETTLED bit of envs that hit the cap
+and the per-env-step update counts (pbn_rollout_ex's d_updates, the settle lengths).
 """
 import numpy as np
 import pytest
 
+import torch
+
+from oracle import oracle
 from pbn_rl_amd import _lib
 from pbn_rl_amd.attractors import load_attractors
 from pbn_rl_amd.env import PBNEnv
 from pbn_rl_amd.network import load_network
 from pbn_rl_amd.spec import EnvSpec
+from pbn_rl_amd.vector_env import VectorPBNEnv
 
 from .protocol import load_agent, replay, summary
 from .synthetic import random_spec
 from .test_bn_pin import reference_result
-from .test_gpu_parity import run_pair, run_rollout_pair
+from .oracle_env import OracleVectorEnv
+from .test_gpu_parity import run_pair, run_rollout_pair, u32
 
 pytestmark = pytest.mark.gpu
 
@@ -34,11 +42,70 @@ def test_settle_step_matches_oracle(name, settle):
     run_pair(spec, 1024, 4, mode=0, start_random=True)
 
 
-@pytest.mark.parametrize("name", ["pbn28", "pbn70", "bb33"])
-def test_settle_rollout_matches_oracle(name):
+@pytest.mark.parametrize("variant", ["pipe", "lean"])
+@pytest.mark.parametrize("name", ["pbn7", "pbn10", "pbn28", "pbn70", "bb33"])
+def test_settle_rollout_matches_oracle(name, variant, monkeypatch):
+    monkeypatch.setenv("PBN_ROLL", variant)
     spec = settle_spec(name, 12, perturbation=0.05, horizon=7)
     run_rollout_pair(spec, 2080, 8, 3)
     run_rollout_pair(spec, 1024, 5, 1)
+
+
+@pytest.mark.parametrize("settle", [2, 3, 64])
+@pytest.mark.parametrize("n_envs", [32, 96, 4128])
+def test_settle_pipe_caps_and_odd_groups(settle, n_envs):
+    """The pipelined settle kernel at caps 2 (every step ends at the cap or earlier), 3 and the
+    facade's 64, with an odd group count (a phantom half in the last block) and p = 0 (groups
+    that settle early: the speculated update is dropped and re-issued)."""
+    for p in (0.0, 0.01):
+        spec = settle_spec("pbn28", settle, perturbation=p, horizon=20)
+        run_rollout_pair(spec, n_envs, 7, 3, env_offset=0)
+
+
+def test_settle_pipe_config2_100_steps_at_65536():
+    """Config 2 under the facade's default law (settle = 64): pbn28 x 65,536 envs, one 100-step
+    pbn_rollout launch (bench.py --settle 64's launch), every output of every step and the
+    settle length of every env-step, against the C oracle."""
+    spec = settle_spec("pbn28", 64, perturbation=0.01, horizon=20)
+    n, T, seed = 65536, 100, 0
+    env = VectorPBNEnv(spec, n, seed=seed)
+    env.reset()
+    out = env.rollout(T, random_actions=True, keep_obs=True, keep_final=True, keep_updates=True)
+    torch.cuda.synchronize()
+    st, tg, t = oracle.reset(spec, seed, 0, 0, n)
+    zero = np.zeros_like(st)
+    upd = 0
+    for k in range(T):
+        ref = oracle.step(spec, seed, 1 + k, 0, st, zero, tg, t, 3)
+        assert np.array_equal(u32(out["obs"][k]), st), k
+        assert np.array_equal(u32(out["flipmask"][k]), ref["flipmask"]), k
+        assert np.array_equal(u32(out["final_state"][k]), ref["final_state"]), k
+        assert np.array_equal(out["reward"][k].cpu().numpy().view(np.uint32), ref["reward"].view(np.uint32)), k
+        assert np.array_equal(out["flags"][k].cpu().numpy(), ref["flags"]), k
+        assert np.array_equal(out["updates"][k].cpu().numpy().view(np.uint16), ref["updates"]), k
+        upd += int(ref["updates"].sum())
+        st, tg, t = ref["state_out"], ref["target"], ref["t"]
+    assert np.array_equal(u32(env.state), st)
+    assert np.array_equal(env.target.cpu().numpy(), tg) and np.array_equal(env.t.cpu().numpy(), t)
+    assert upd > 2 * n * T        # the settle law ran (the mean settle length is well above 2)
+
+
+def test_settle_pipe_config3_pbn70_at_1m():
+    """Config 3's size under the settle law: pbn70 x 1,048,576 envs, one 20-step launch, four
+    4,096-env windows of every output against the oracle run on those envs."""
+    spec = settle_spec("pbn70", 16, perturbation=0.01, horizon=20)
+    n, T, seed = 1 << 20, 20, 1
+    env = VectorPBNEnv(spec, n, seed=seed)
+    env.reset()
+    out = env.rollout(T, random_actions=True, keep_obs=True, keep_final=True, keep_updates=True)
+    torch.cuda.synchronize()
+    for lo in (0, 333 * 1024, 700 * 1024 + 2048, n - 4096):
+        hi = lo + 4096
+        want = OracleVectorEnv(spec, lo, 4096, seed=seed).rollout(T)
+        for name in ("obs", "flipmask", "final_state", "flags", "updates"):
+            assert torch.equal(out[name][..., lo:hi].cpu(), want[name]), (name, lo)
+        assert np.array_equal(out["reward"][:, lo:hi].cpu().numpy().view(np.uint32),
+                              want["reward"].numpy().view(np.uint32)), lo
 
 
 def test_settle_unsettled_flag_and_high_perturbation():
@@ -87,6 +154,25 @@ def test_gpu_bb33_evaluation_reproduces_reference():
     chosen = [atts[i] for i in (0, 2, 1)]
     env = PBNEnv(network=net, attractors=chosen, perturbation=0.0, horizon=0, settle=64, seed=5,
                  grow_attractors=False)
+    env.reset()
+    res = replay(facade_step_fn(env, net), load_agent("bb33", 33), chosen, n_runs=10)
+    mat, same, data = summary(res)
+    ref, ref_data = reference_result()
+    assert same and np.array_equal(mat / 10, ref)
+    assert data == {k: v for k, v in ref_data.items() if k != 101}
+    env.close()
+
+
+def test_gpu_bb33_evaluation_on_default_constructor():
+    """The same replay through PBNEnv as the reference builds it (model_tester.py:409-413: no
+    step-law argument): the facade's default law (DEFAULT_SETTLE) reproduces the fixture."""
+    from pbn_rl_amd.env import DEFAULT_SETTLE
+    net = load_network("bb33")
+    atts = load_attractors("bb33")
+    chosen = [atts[i] for i in (0, 2, 1)]
+    env = PBNEnv(N=net.n, genes=net.genes, logic_functions=net.logic_functions, attractors=chosen,
+                 perturbation=0.0, horizon=0, seed=5, grow_attractors=False)
+    assert env.spec.settle == DEFAULT_SETTLE >= 2
     env.reset()
     res = replay(facade_step_fn(env, net), load_agent("bb33", 33), chosen, n_runs=10)
     mat, same, data = summary(res)

@@ -13,6 +13,8 @@
 #   pbn70            config 3: pbn70 x 1,048,576 envs, 200 steps
 #   bdq              config 5: the BDQ frame at 32,768 envs (+ kernel trace)
 #   bdq-learn        BDQ training frames at 32,768 envs
+#   settle           the driver's command (with its settle_law and hand-off fields) and config 2 under the
+#                    settle law alone (--settle 64, 200 steps) + its kernel trace
 #   bdqpmc           the BDQ frame under two PMC passes: L2 hits / misses / requests, HBM fetch + write
 #   ubench           tools/ubench_valu_issue (VALU issue rates by instruction and waves per SIMD)
 #   nofinal          the driver's command and 2,000 steps without s' (--no-final-state)
@@ -62,6 +64,12 @@ for step in "$@"; do
         -d "$out/bdq_pmc_write" -o run -- python bench.py --workload bdq --no-cpu-baseline > /dev/null 2> "$out/bdq_pmc_write.err" || fail bdqpmc-write
       echo "bdqpmc done" ;;
     bdq-learn) bench bench_bdq_learn --workload bdq-learn ;;
+    settle)
+      bench bench_driver --gpus 1 --steps 20 --warmup 5
+      bench bench_settle64 --settle 64 --steps 200 --warmup 20 --no-cpu-baseline --no-gather
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/settle_trace" -o run -- \
+        python bench.py --settle 64 --steps 200 --warmup 20 --no-cpu-baseline --no-gather \
+        > "$out/settle_trace.json" 2> "$out/settle_trace.err" || fail settle-trace ;;
     ubench)
       timeout -k 10 300 tools/ubench_valu_issue > "$out/ubench_valu_issue.jsonl" 2> "$out/ubench.err" || fail ubench
       echo "ubench done" ;;
