@@ -1749,7 +1749,9 @@ struct SettlePlan {
   uint32_t Ct0 = 0, Ck0 = 0, Ct1 = 0, Ck1 = 0;
   uint32_t Rt0 = 0, Rk0 = 0, Rt1 = 0, Rk1 = 0;
   bool v0 = false, v1 = false;
-  // false once both groups have finished all steps (the loop's exit, the same in every wave)
+  // false once both groups have finished all steps (the loop's exit, the same in every wave).
+  // A step takes at most K updates and one dropped speculation, so n_steps (K + 1) + 1
+  // iterations always suffice: the bound is a guard that every wave reaches, never the exit.
   __device__ __forceinline__ bool next(const uint32_t* ctl, uint32_t it, uint32_t K, uint32_t n_steps) {
     const uint32_t* cin = ctl + ((it + 1) & 1) * 4;   // written in iteration i-1
     Ct0 = __builtin_amdgcn_readfirstlane(cin[0]);
@@ -1757,6 +1759,7 @@ struct SettlePlan {
     Ct1 = __builtin_amdgcn_readfirstlane(cin[2]);
     Ck1 = __builtin_amdgcn_readfirstlane(cin[3]);
     if (Ct0 >= n_steps && Ct1 >= n_steps) return false;
+    if ((uint64_t)it > (uint64_t)n_steps * (K + 1) + 1) return false;
     v0 = Pt0 == Ct0 && Pk0 == Ck0;
     v1 = Pt1 == Ct1 && Pk1 == Ck1;
     Rt0 = v0 ? (Pk0 + 1 < K ? Pt0 : Pt0 + 1) : Ct0;
