@@ -107,9 +107,11 @@ struct StepArgs {
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
     __builtin_amdgcn_sched_barrier(0);                                                        \
     if (a.stamps && (threadIdx.x & 63) == 0)                                                  \
-      a.stamps[(size_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + (k)] = t_; \
+      a.stamps[(size_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 32 + (k)] = t_; \
   } while (0)
-// pipelined rollout: per role, clocks at the start of iteration 10, after its work, after the barrier
+// pipelined rollout: per role, clocks at the start of iteration 10, after its work, after the barrier;
+// rows of 32 per block (tools/stamps.py): role r at 4r + {0, 1, 2}, HW_ID at 14 / 7 / 11, the
+// segment clocks of the single-word fast paths at 15, 3, 12, 13 (state), 16, 17 (env), 18 (selection)
 #define PBN_PSTAMP(k, slot_)                                                                  \
   do {                                                                                        \
     if ((k) == 10) {                                                                          \
@@ -118,7 +120,7 @@ struct StepArgs {
       asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");             \
       __builtin_amdgcn_sched_barrier(0);                                                      \
       if (a.stamps && (threadIdx.x & 63) == 0)                                                \
-        a.stamps[(size_t)blockIdx.x * 16 + (threadIdx.x >> 6) * 4 + (slot_)] = t_;            \
+        a.stamps[(size_t)blockIdx.x * 32 + (threadIdx.x >> 6) * 4 + (slot_)] = t_;            \
     }                                                                                         \
   } while (0)
 #define PBN_PSTAMP_AT(k, idx_)                                                                \
@@ -128,7 +130,7 @@ struct StepArgs {
       __builtin_amdgcn_sched_barrier(0);                                                      \
       asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");             \
       __builtin_amdgcn_sched_barrier(0);                                                      \
-      if (a.stamps && (threadIdx.x & 63) == 0) a.stamps[(size_t)blockIdx.x * 16 + (idx_)] = t_; \
+      if (a.stamps && (threadIdx.x & 63) == 0) a.stamps[(size_t)blockIdx.x * 32 + (idx_)] = t_; \
     }                                                                                         \
   } while (0)
 // pipelined rollout, launch anatomy: the state wave's s_memrealtime (100 MHz, one clock for the
@@ -140,7 +142,7 @@ struct StepArgs {
     __builtin_amdgcn_sched_barrier(0);                                                        \
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
     __builtin_amdgcn_sched_barrier(0);                                                        \
-    if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)(gridDim.x + blockIdx.x) * 16 + (idx_)] = t_; \
+    if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)(gridDim.x + blockIdx.x) * 32 + (idx_)] = t_; \
   } while (0)
 #else
 #define PBN_STAMP(k) do {} while (0)
@@ -1110,7 +1112,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
 #ifdef PBN_STAMPS
   // placement of this wave: HW_ID (wave, SIMD, CU, SH, SE) in the low word, XCC_ID above it
   if (a.stamps && lane == 0)
-    a.stamps[(size_t)blockIdx.x * 16 + (role == 0 ? 14 : role * 4 + 3)] =
+    a.stamps[(size_t)blockIdx.x * 32 + (role == 0 ? 14 : role * 4 + 3)] =
         (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
         ((unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32);
 #endif
@@ -1233,9 +1235,11 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
         // barriers keep the compiler from hoisting it above them or sinking it to the latch)
         asm volatile("" ::: "memory");   // the LDS reads above are issued here
         __builtin_amdgcn_sched_barrier(0);
+        PBN_PSTAMP_AT(k, 16);
         E_next = env_call(k + 1);   // (one unused call per launch)
         asm volatile("" : "+v"(E_next.x), "+v"(E_next.y), "+v"(E_next.z), "+v"(E_next.w));
         __builtin_amdgcn_sched_barrier(0);
+        PBN_PSTAMP_AT(k, 17);
         // part 3: the rest of step k's draws
         uint32_t rt = c - as * (A - 1);
         rt += (rt >= as) ? 1u : 0u;
@@ -1298,6 +1302,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
       }
       PBN_PSTAMP(k, 1);
       lds_barrier();
+      PBN_PSTAMP(k, 2);
     };
     // two steps per trip with the ENV words alternating between EA and EB: no copies between steps
     Word4 EA = env_call(0), EB = EA;
@@ -1441,6 +1446,11 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
         PBN_PSTAMP(k, 0);
         if (k < n_steps) {
           sel_calls(k + 1, nxt);   // (one unused set per launch)
+#ifdef PBN_STAMPS
+#pragma unroll
+          for (int d = 0; d < 16; ++d) asm volatile("" : "+v"(nxt[d]));
+#endif
+          PBN_PSTAMP_AT(k, 18);
           uint32_t* lt_out = lt_base + (size_t)(k & 1) * a.slot_words;
 #pragma unroll
           for (int q = 0; q < NQ; ++q) lt_out[q * 64] = less_than_cm<B>(cur, cmi + (size_t)q * B * 32, 32);
@@ -1450,6 +1460,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
         }
         PBN_PSTAMP(k, 1);
         lds_barrier();
+        PBN_PSTAMP(k, 2);
       };
       // two steps per trip with the digit arrays swapping roles: no copies between steps
       uint32_t dA[16], dB[16];
@@ -1596,8 +1607,10 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
               sb[q] = selq[(2 * q + 1) * 32 + l32];
             }
             if (valid && (u_fl & 1u)) LANE_ST(a.obs, (size_t)t * plane, le, (size_t)n_steps * plane, 7, st[0]);
+            PBN_PSTAMP_AT(k, 15);
             Sg[l32] = lane_transpose32(s1[0], lane);
             __builtin_amdgcn_wave_barrier();
+            PBN_PSTAMP_AT(k, 3);
             uint32_t x = 0;
 #pragma unroll
             for (int q = K - 1; q >= 0; --q) {
@@ -1607,8 +1620,10 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
               const uint32_t fj = eval_sel_in(xin, sa[q], sb[q]);
               x = (q == K - 1) ? fj : bfi(ltv[q], fj, x);
             }
+            PBN_PSTAMP_AT(k, 12);
             uint32_t sp[W];
             sp[0] = lane_transpose32(x, lane);
+            PBN_PSTAMP_AT(k, 13);
             finish(t, sp, s1, gam, rs, info);
           }
           PBN_PSTAMP(k, 1);

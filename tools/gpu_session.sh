@@ -13,6 +13,8 @@
 #   pbn70            config 3: pbn70 x 1,048,576 envs, 200 steps
 #   bdq              config 5: the BDQ frame at 32,768 envs (+ kernel trace)
 #   bdq-learn        BDQ training frames at 32,768 envs
+#   stamps           the pipelined kernel's per-role segment clocks at iteration 10 (diagnostic build
+#                    pbn_rl_amd/libpbn_env_stamps.so: tools/stamps.py --build), 20- and 100-step launches
 #   settle           the driver's command (with its settle_law and hand-off fields) and config 2 under the
 #                    settle law alone (--settle 64, 200 steps) + its kernel trace
 #   bdqpmc           the BDQ frame under two PMC passes: L2 hits / misses / requests, HBM fetch + write
@@ -64,6 +66,12 @@ for step in "$@"; do
         -d "$out/bdq_pmc_write" -o run -- python bench.py --workload bdq --no-cpu-baseline > /dev/null 2> "$out/bdq_pmc_write.err" || fail bdqpmc-write
       echo "bdqpmc done" ;;
     bdq-learn) bench bench_bdq_learn --workload bdq-learn ;;
+    stamps)
+      for T in 20 100; do
+        timeout -k 10 120 python tools/stamps.py --pipe --rollout $T > "$out/stamps_T$T.json" 2> "$out/stamps_T$T.err" \
+          || fail "stamps T$T"
+      done
+      echo "stamps done" ;;
     settle)
       bench bench_driver --gpus 1 --steps 20 --warmup 5
       bench bench_settle64 --settle 64 --steps 200 --warmup 20 --no-cpu-baseline --no-gather

@@ -18,6 +18,36 @@ ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path.insert(0, ROOT)
 STAMP_LIB = os.path.join(ROOT, "pbn_rl_amd", "libpbn_env_stamps.so")
 PHASES = ["tables+barrier", "philox", "per-env", "transpose+S", "node eval", "back-transpose", "epilogue"]
+ROW = 32   # stamp words per block (pipelined kernel) or per wave (wave kernel), step_kernels.h PBN_PSTAMP
+
+
+def segments(full, it):
+    """Critical-path table of iteration 10 of the pipelined kernel's single-word fast paths, per
+    role: cycles of each segment between consecutive stamps (medians over blocks), the role's
+    wait at the block barrier, and the share of the iteration each accounts for."""
+    import numpy as np
+    med = lambda x: int(np.median(x))
+    c = lambda i: full[:, i]
+    roles = {
+        "state": [("slot reads + obs store", 0, 15), ("transpose to planes", 15, 3), ("gathers + mux chains", 3, 12),
+                  ("back-transpose", 12, 13), ("epilogue (hash, reward, flags, stores)", 13, 1),
+                  ("barrier wait", 1, 2)],
+        "env draws": [("draws + LDS reads (this step)", 4, 16), ("ENV Philox call (next step)", 16, 17),
+                      ("masks, slot writes, flip-mask store", 17, 5), ("barrier wait", 5, 6)],
+        "selection": [("SEL Philox calls (next step)", 8, 18), ("threshold compares + slot writes", 18, 9),
+                      ("barrier wait", 9, 10)],
+    }
+    out = {"iteration_median": med(it)}
+    for role, segs in roles.items():
+        have = all(np.all(c(a) > 0) and np.all(c(b) > 0) for _, a, b in segs)
+        if not have:
+            continue
+        total = med(c(segs[-1][2]) - c(segs[0][1]))
+        rows = {name: {"cycles": med(c(b) - c(a)), "share": round(med(c(b) - c(a)) / max(med(it), 1), 3)}
+                for name, a, b in segs}
+        out[role] = {"segments": rows, "span_median": total,
+                     "accounted": round(sum(r["cycles"] for r in rows.values()) / max(med(it), 1), 3)}
+    return out
 
 
 def placement(full, it):
@@ -109,7 +139,7 @@ def main():
     env = VectorPBNEnv(spec, args.envs, seed=1, keep_final_state=False)
     env.reset()
     waves = env.n_alloc // 32
-    buf = torch.zeros(waves * 16, dtype=torch.int64, device="cuda")
+    buf = torch.zeros(waves * ROW, dtype=torch.int64, device="cuda")
     for _ in range(10):
         env.step_flipmask(random_actions=True)
     torch.cuda.synchronize()
@@ -125,7 +155,7 @@ def main():
     if args.pipe or args.plane:
         waves = (waves + 1) // 2   # one block per pair of groups
         nr = 4 if args.plane else 3
-        t = buf.view(-1, 16)[:waves, :4 * nr].cpu().numpy().astype(np.int64).reshape(waves, nr, 4)[:, :, :3]
+        t = buf.view(-1, ROW)[:waves, :4 * nr].cpu().numpy().astype(np.int64).reshape(waves, nr, 4)[:, :, :3]
         rep = {"envs": args.envs, "blocks": waves, "rollout_steps": args.rollout}
         names = ["state", "env draws", "selection", "planes+outputs"][:nr]
         for role, name in enumerate(names):
@@ -133,7 +163,7 @@ def main():
             wait = t[:, role, 2] - t[:, role, 1]
             rep[name] = {"work_median": int(np.median(work)), "work_p90": int(np.percentile(work, 90)),
                          "barrier_wait_median": int(np.median(wait))}
-        full = buf.view(-1, 16)[:waves].cpu().numpy().astype(np.int64)
+        full = buf.view(-1, ROW)[:waves].cpu().numpy().astype(np.int64)
         st0 = full[:, 0]
         if args.plane:
             it = t[:, :, 2].max(axis=1) - t[:, :, 0].min(axis=1)
@@ -147,13 +177,14 @@ def main():
             "epilogue": int(np.median(full[:, 1] - full[:, 13]))}
         it = t[:, :, 2].max(axis=1) - t[:, :, 0].min(axis=1)
         rep["iteration_median"] = int(np.median(it))
+        rep["critical_path"] = segments(full, it)
         rep["placement"] = placement(full, it)
         if args.rollout:
-            rep["anatomy"] = anatomy(buf.view(-1, 16)[waves:2 * waves, :7].cpu().numpy().astype(np.int64),
+            rep["anatomy"] = anatomy(buf.view(-1, ROW)[waves:2 * waves, :7].cpu().numpy().astype(np.int64),
                                      args.rollout, full[:, 14])
         print(json.dumps(rep, indent=1))
         return
-    t = buf.view(waves, 16)[:, :8].cpu().numpy().astype(np.int64)
+    t = buf.view(waves, ROW)[:, :8].cpu().numpy().astype(np.int64)
     d = np.diff(t, axis=1)
     rep = {"envs": args.envs, "waves": waves, "rollout_steps": args.rollout,
            "start_spread_cycles": int(t[:, 0].max() - t[:, 0].min()),
