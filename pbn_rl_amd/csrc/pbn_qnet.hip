@@ -33,15 +33,14 @@
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kD0 = 256, kD1 = 128, kD2 = 64, kD3 = 32, kDH = 64;   // BranchingQNetwork widths
 constexpr int kMaxHeads = 8;                                         // value + up to 7 branches
 constexpr int kMaxActTiles = 4;                                      // A <= 128 (pbn70: 71), 32 per tile
 constexpr int kEnvs = 16;                                            // envs per wave
 constexpr int kWaves = 8;                                            // waves per block (128 envs)
-constexpr int kStageRows = 8 * kWaves;                               // weight rows per staging pass
-constexpr int kStagePasses = 128 / kStageRows;                       // 2, 4 or 8
-static_assert(kStagePasses == 2 || kStagePasses == 4 || kStagePasses == 8, "staging covers 128 rows");
+static_assert(kWaves == 8, "stage loads: 512 threads = 64 rows x 8 float4 columns per pass");
 constexpr int kBiasFloats = kD1 + kD2 + kD3 + (kDH + 32 * kMaxActTiles) * kMaxHeads;
 
 struct QnetArgs {
@@ -69,8 +68,9 @@ struct QnetArgs {
   int n_attr;
 };
 
-constexpr int kPitch = 36;                 // weight-chunk row pitch in LDS (floats)
-constexpr int kBufFloats = 128 * kPitch;   // one buffer: up to 128 rows
+constexpr int kPitch = 36;                   // weight row pitch in LDS (floats): conflict-free float4 reads
+constexpr int kBufFloats = 5 * 64 * kPitch;  // one stage buffer: 320 rows (the largest stage, below)
+constexpr int kMaxPieces = 5;
 
 __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -124,29 +124,90 @@ __device__ __forceinline__ void mfma_chunk(f32x4 (&acc)[MT], const float* __rest
   for (int m = 0; m < MT; ++m) acc[m] = mfma(wn[m].w, X1[3], acc[m]);
 }
 
-// The weights reach the MFMAs through LDS as one stream of chunks, double-buffered: a chunk
-// is 32 input columns of one layer's weight matrix, all its rows (<= 128; rows past n_out are
-// zero).  The block's four waves share every chunk (a quarter of the L2 reads of per-wave
-// loads), the next chunk's global loads are in flight under the current chunk's MFMAs, and an
-// operand read is one ds_read_b128 at LDS latency.  Rows are padded to 36 floats, so the 16
-// rows one read's quarter-wave touches start on 16 distinct 4-bank groups.  The stream:
-//   Linear(256, 128): 8 chunks | Linear(128, 64): 4 | Linear(64, 32): 2 |
-//   per head k: Linear(32, 64): 1, Linear(64, A): 2
+// The weights reach the MFMAs through LDS as a stream of STAGES, double-buffered: while the
+// block's waves run one stage's MFMAs from one buffer, every thread holds the next stage's global
+// loads in registers and stores them into the other buffer after the MFMAs; one block barrier per
+// stage.  A stage is a few 32-column pieces of weight matrices, each row padded to 36 floats (the
+// 16 rows one quarter-wave reads start on 16 distinct 4-bank groups):
+//   stages 0-7   Linear(256, 128), 32 input columns each (128 rows)
+//   stage 8      Linear(128, 64), all of it (four 64-row pieces)
+//   stage 9      Linear(64, 32) (two 32-row pieces), and head 0 when it fits beside it
+//   then         one stage per head k: Linear(32, 64) (64 rows) and Linear(64, A) (two pieces of
+//                32 AT rows, rows past A read as 0)
+// Round 3 streamed 32-column chunks only (26 stages and barriers at Bittner-28); each of the small
+// layers' chunks carried 512-1,024 MFMA cycles per wave, too few to cover the next chunk's L2
+// round trip and the barrier.  Now every stage after layer 1 carries at least 2,048.
+// Stage kinds; row r of a stage occupies rows r of its buffer (float offset r * kPitch), so only
+// the source of a row depends on the kind.
+enum StageKind { kL1 = 0, kL2 = 1, kS9 = 2, kHead = 3 };
 
-struct Chunk {
-  const float* src;   // column 0 of the chunk in the row-major weight matrix
-  int ld, rows;       // row stride (floats), valid rows (the rest of the 32 * tiles read 0)
+template <int AT>
+struct StagePlan {
+  // layer 3 and head 0 share stage 9 when they fit in one buffer
+  static constexpr bool kMerge = 64 + (64 + 64 * AT) <= kBufFloats / kPitch;
+  static constexpr int kFirstHeadStage = kMerge ? 9 : 10;
+  static constexpr int kHeadRows = 64 + 64 * AT;        // Linear(32, 64), then Linear(64, A) as two
+                                                        // pieces of 32 AT rows (32 input columns each)
+  static constexpr int kS9Rows = 64 + (kMerge ? kHeadRows : 0);
+  static constexpr int kHeadPasses = kHeadRows / 64;
+  static constexpr int kS9Passes = kS9Rows / 64;
 };
 
-__device__ __forceinline__ Chunk chunk_of(const QnetArgs& a, int c) {
-  if (c < 8) return {a.w1 + 32 * c, kD0, kD1};
-  if (c < 12) return {a.w2 + 32 * (c - 8), kD1, kD2};
-  if (c < 14) return {a.w3 + 32 * (c - 12), kD2, kD3};
-  const int k = (c - 14) / 3, j = (c - 14) % 3;
-  if (j == 0) return {a.wh1 + (size_t)kDH * k * kD3, kD3, kDH};
-  return {a.wh2 + (size_t)a.n_act * kDH * k + 32 * (j - 1), kDH, a.n_act};
+// row r of head k's stage rows: its source and whether it is a row of the matrix (rows past A
+// load row A - 1 and are stored as 0)
+__device__ __forceinline__ const float* head_row(const QnetArgs& a, int k, int r, int at32, bool& real) {
+  if (r < 64) {
+    real = true;
+    return a.wh1 + (size_t)kDH * kD3 * k + (size_t)r * kD3;
+  }
+  const int r2 = r - 64, j = r2 >= at32 ? 1 : 0, row = r2 - j * at32;
+  real = row < a.n_act;
+  return a.wh2 + (size_t)a.n_act * kDH * k + 32 * j + (size_t)min(row, a.n_act - 1) * kDH;
 }
 
+// row r of a stage of kind KIND (idx = the layer-1 chunk, or the head)
+template <int AT, int KIND>
+__device__ __forceinline__ const float* stage_row(const QnetArgs& a, int idx, int r, bool& real) {
+  if constexpr (KIND == kL1) {
+    real = true;
+    return a.w1 + 32 * idx + (size_t)r * kD0;
+  } else if constexpr (KIND == kL2) {
+    real = true;
+    return a.w2 + 32 * (r >> 6) + (size_t)(r & 63) * kD1;
+  } else if constexpr (KIND == kS9) {
+    if (r < 64) {
+      real = true;
+      return a.w3 + 32 * (r >> 5) + (size_t)(r & 31) * kD2;
+    }
+    return head_row(a, 0, r - 64, 32 * AT, real);
+  } else {
+    return head_row(a, idx, r, 32 * AT, real);
+  }
+}
+
+// thread t's share of a stage: rows (t >> 3) + 64 j, columns 4 (t & 7) .. + 3 (PASSES x 64 rows)
+template <int AT, int KIND, int PASSES>
+__device__ __forceinline__ void fetch_stage(const QnetArgs& a, int idx, int t, f32x4 (&sv)[kMaxPieces]) {
+  const int srow = t >> 3, scol = 4 * (t & 7);
+#pragma unroll
+  for (int j = 0; j < PASSES; ++j) {
+    bool real;
+    sv[j] = *reinterpret_cast<const f32x4*>(stage_row<AT, KIND>(a, idx, srow + 64 * j, real) + scol);
+  }
+}
+
+template <int AT, int KIND, int PASSES>
+__device__ __forceinline__ void put_stage(const QnetArgs& a, int idx, int t, float* buf, f32x4 (&sv)[kMaxPieces]) {
+  const int srow = t >> 3, scol = 4 * (t & 7);
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};   // masked here, not at the load (a select on
+                                           // the loaded value would wait for it)
+#pragma unroll
+  for (int j = 0; j < PASSES; ++j) {
+    bool real;
+    (void)stage_row<AT, KIND>(a, idx, srow + 64 * j, real);
+    *reinterpret_cast<f32x4*>(buf + (srow + 64 * j) * kPitch + scol) = real ? sv[j] : z;
+  }
+}
 
 // The dueling combination and argmax of one advantage head, as pbn_heads_to_flipmask computes
 // them (pbn_agent.hip, q_to_flipmask_kernel): q_a = (v + adv_a) - mean, mean = the left-to-right
@@ -189,11 +250,13 @@ __device__ __forceinline__ int dueling_argmax(const f32x4 (&o)[T16], int lane, i
 template <int AT, bool FLIP, bool BIL>   // AT: the second head layers' outputs in 32-row units, A <= 32 AT
 __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
   constexpr int T16 = 2 * AT;   // 16-feature output tiles of the second head layers
+  using Plan = StagePlan<AT>;
   __shared__ __attribute__((aligned(16))) float wbuf[2 * kBufFloats];
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4;
   const int A = a.n_act;
-  const int n_chunks = 14 + 3 * a.n_heads;
+  const int H = a.n_heads;
+  const int n_stages = Plan::kFirstHeadStage + H - (Plan::kMerge ? 1 : 0);
   // this lane's env: the wave's 16 envs in order (y input), or (BIL) the wave's 16 of the block's
   // envs stably sorted by target, so that a wave's envs share one or two targets' tables
   int64_t e;
@@ -230,52 +293,25 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
     e = live ? eb + li : 0;
   }
 
-  // staging: thread t moves float4 (row (t >> 3) + kStageRows j, columns 4 (t & 7) .. +3), j <
-  // kStagePasses (128 rows in all)
   const int t = threadIdx.x;
-  const int srow = t >> 3, scol = 4 * (t & 7);
-  float4 s0, s1, s2, s3, s4, s5, s6, s7;
-  int srows = 0;
-#define PBN_LD(sj, j)                                                                              \
-  sj = *reinterpret_cast<const float4*>(p_ + (size_t)min(srow + kStageRows * (j), last_) * ch_.ld)
-#define PBN_FETCH(c_)                                                                              \
+  f32x4 sv[kMaxPieces];   // the next stage's loads in flight
+  // one stage step: the next stage's loads (kept above the MFMAs by the scheduling barriers: LLVM
+  // would sink them to their LDS stores and expose their L2 round trip), this stage's MFMAs (BODY
+  // reads `buf`; waves past the end compute on env 0 and store nothing), the next stage into the
+  // other buffer (the waves left it at the previous barrier), barrier.  NEXT_PASSES = 0: the last
+  // stage, nothing to fetch.
+#define PBN_STAGE(s_, NEXT_KIND, NEXT_IDX, NEXT_PASSES, BODY)                                      \
   do {                                                                                             \
-    const Chunk ch_ = chunk_of(a, (c_));                                                           \
-    const float* p_ = ch_.src + scol;                                                              \
-    const int last_ = ch_.rows - 1; /* rows past the matrix load its last row, then read as 0 */   \
-    PBN_LD(s0, 0); PBN_LD(s1, 1);                                                                  \
-    if constexpr (kStagePasses > 2) { PBN_LD(s2, 2); PBN_LD(s3, 3); }                              \
-    if constexpr (kStagePasses > 4) { PBN_LD(s4, 4); PBN_LD(s5, 5); PBN_LD(s6, 6); PBN_LD(s7, 7); } \
-    srows = ch_.rows;                                                                              \
-  } while (0)
-#define PBN_ST(sj, j)                                                                              \
-  do {                                                                                             \
-    if (srow + kStageRows * (j) >= srows) sj = z_;                                                 \
-    *reinterpret_cast<float4*>(d_ + kStageRows * (j) * kPitch) = sj;                               \
-  } while (0)
-#define PBN_PUT(b_)                                                                                \
-  do {                                                                                             \
-    float* d_ = wbuf + (b_) * kBufFloats + srow * kPitch + scol;                                   \
-    const float4 z_ = make_float4(0.f, 0.f, 0.f, 0.f); /* masked here, not at the load: a select */ \
-    PBN_ST(s0, 0); PBN_ST(s1, 1);                      /* on the loaded value would wait for it */ \
-    if constexpr (kStagePasses > 2) { PBN_ST(s2, 2); PBN_ST(s3, 3); }                              \
-    if constexpr (kStagePasses > 4) { PBN_ST(s4, 4); PBN_ST(s5, 5); PBN_ST(s6, 6); PBN_ST(s7, 7); } \
-  } while (0)
-  // one chunk step: the next chunk's loads (kept above the MFMAs by the scheduling barriers:
-  // LLVM would sink them to their LDS stores and expose their L2 round trip), this chunk's
-  // MFMAs (BODY reads `buf`; waves past the end compute on env 0 and store nothing), the next
-  // chunk into the other buffer (the waves left it at the previous barrier), barrier
-#define PBN_CHUNK(c_, BODY)                                                                        \
-  do {                                                                                             \
-    const int cc_ = (c_);                                                                          \
-    PBN_FETCH(min(cc_ + 1, n_chunks - 1)); /* unconditional: a branch here makes the wait */    \
+    const int ss_ = (s_);                                                                          \
+    if constexpr ((NEXT_PASSES) > 0) fetch_stage<AT, (NEXT_KIND), (NEXT_PASSES)>(a, (NEXT_IDX), t, sv); \
     __builtin_amdgcn_sched_barrier(0);                                                             \
-    const float* buf = wbuf + (cc_ & 1) * kBufFloats;                                              \
+    const float* buf = wbuf + (ss_ & 1) * kBufFloats;                                              \
     BODY                                                                                           \
     __builtin_amdgcn_sched_barrier(0);                                                             \
-    PBN_PUT((cc_ + 1) & 1); /* counters assume loads pending at the MFMAs (after the last */    \
-                            /* chunk this rewrites the idle buffer) */                            \
-    __syncthreads();                                                                               \
+    if constexpr ((NEXT_PASSES) > 0) {                                                             \
+      put_stage<AT, (NEXT_KIND), (NEXT_PASSES)>(a, (NEXT_IDX), t, wbuf + ((ss_ + 1) & 1) * kBufFloats, sv); \
+      __syncthreads();                                                                             \
+    }                                                                                              \
   } while (0)
 
   // every bias, staged once in LDS (a per-head bias load from L2 sat in front of the head's
@@ -289,14 +325,14 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
   for (int i = t; i < kD1; i += 64 * kWaves) bs1[i] = a.b1[i];
   for (int i = t; i < kD2; i += 64 * kWaves) bs2[i] = a.b2[i];
   for (int i = t; i < kD3; i += 64 * kWaves) bs3[i] = a.b3[i];
-  for (int i = t; i < kDH * a.n_heads; i += 64 * kWaves) bsh1[i] = a.bh1[i];
-  for (int i = t; i < A * a.n_heads; i += 64 * kWaves) bsh2[i] = a.bh2[i];
+  for (int i = t; i < kDH * H; i += 64 * kWaves) bsh1[i] = a.bh1[i];
+  for (int i = t; i < A * H; i += 64 * kWaves) bsh2[i] = a.bh2[i];
 
-  PBN_FETCH(0);
-  PBN_PUT(0);
+  fetch_stage<AT, kL1, 2>(a, 0, t, sv);
+  put_stage<AT, kL1, 2>(a, 0, t, wbuf, sv);
 
   // ---- Linear(256, 128): input tiles from y, features 16 p + 4 g .. + 3 (one float4 per tile);
-  // a chunk is two tiles, whose loads fly one chunk ahead
+  // a stage is two tiles, whose loads fly one stage ahead
   f32x4 x1[kD1 / 16];
   if constexpr (!BIL) {
     const float* yrow = a.y + (size_t)e * kD0 + 4 * g;
@@ -306,18 +342,19 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
       yv0 = f32x4{u0.x, u0.y, u0.z, u0.w};
       yv1 = f32x4{u1.x, u1.y, u1.z, u1.w};
     }
-    __syncthreads();   // chunk 0 and the biases are in LDS
+    __syncthreads();   // stage 0 and the biases are in LDS
 #pragma unroll
     for (int m = 0; m < kD1 / 16; ++m) x1[m] = bias_tile(bs1, m, g, kD1);
 #pragma unroll
     for (int p = 0; p < kD0 / 32; ++p) {
-      if (p + 1 < kD0 / 32) {   // the next chunk's y tiles fly under this chunk's MFMAs
+      if (p + 1 < kD0 / 32) {   // the next stage's y tiles fly under this stage's MFMAs
         const float4 u0 = *reinterpret_cast<const float4*>(yrow + 32 * (p + 1));
         const float4 u1 = *reinterpret_cast<const float4*>(yrow + 32 * (p + 1) + 16);
         yn0 = f32x4{u0.x, u0.y, u0.z, u0.w};
         yn1 = f32x4{u1.x, u1.y, u1.z, u1.w};
       }
-      PBN_CHUNK(p, { mfma_chunk<kD1 / 16>(x1, buf, lane, yv0, yv1); });
+      if (p + 1 < kD0 / 32) PBN_STAGE(p, kL1, p + 1, 2, { mfma_chunk<kD1 / 16>(x1, buf, lane, yv0, yv1); });
+      else PBN_STAGE(p, kL2, 0, 4, { mfma_chunk<kD1 / 16>(x1, buf, lane, yv0, yv1); });
       yv0 = yn0;
       yv1 = yn1;
     }
@@ -370,36 +407,29 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
     }
 #pragma unroll
     for (int q = 0; q < kD0 / 16; ++q) yt[q] = leaky(yt[q], a.slope);
-    __syncthreads();   // chunk 0 and the biases are in LDS
+    __syncthreads();   // stage 0 and the biases are in LDS
 #pragma unroll
     for (int m = 0; m < kD1 / 16; ++m) x1[m] = bias_tile(bs1, m, g, kD1);
 #pragma unroll
     for (int p = 0; p < kD0 / 32; ++p) {
-      PBN_CHUNK(p, { mfma_chunk<kD1 / 16>(x1, buf, lane, yt[2 * p], yt[2 * p + 1]); });
+      if (p + 1 < kD0 / 32) PBN_STAGE(p, kL1, p + 1, 2, { mfma_chunk<kD1 / 16>(x1, buf, lane, yt[2 * p], yt[2 * p + 1]); });
+      else PBN_STAGE(p, kL2, 0, 4, { mfma_chunk<kD1 / 16>(x1, buf, lane, yt[2 * p], yt[2 * p + 1]); });
     }
   }
 #pragma unroll
   for (int m = 0; m < kD1 / 16; ++m) x1[m] = leaky(x1[m], a.slope);
 
-  // ---- Linear(128, 64), Linear(64, 32)
+  // ---- Linear(128, 64): stage 8, its four 64-row pieces of 32 input columns
   f32x4 x2[kD2 / 16];
 #pragma unroll
   for (int m = 0; m < kD2 / 16; ++m) x2[m] = bias_tile(bs2, m, g, kD2);
+  auto layer2 = [&](const float* buf) __attribute__((always_inline)) {
 #pragma unroll
-  for (int p = 0; p < kD1 / 32; ++p) {
-    PBN_CHUNK(8 + p, { mfma_chunk<kD2 / 16>(x2, buf, lane, x1[2 * p], x1[2 * p + 1]); });
-  }
+    for (int p = 0; p < kD1 / 32; ++p) mfma_chunk<kD2 / 16>(x2, buf + p * 64 * kPitch, lane, x1[2 * p], x1[2 * p + 1]);
+  };
+  PBN_STAGE(8, kS9, 0, Plan::kS9Passes, { layer2(buf); });
 #pragma unroll
   for (int m = 0; m < kD2 / 16; ++m) x2[m] = leaky(x2[m], a.slope);
-  f32x4 x3[kD3 / 16];
-#pragma unroll
-  for (int m = 0; m < kD3 / 16; ++m) x3[m] = bias_tile(bs3, m, g, kD3);
-#pragma unroll
-  for (int p = 0; p < kD2 / 32; ++p) {
-    PBN_CHUNK(12 + p, { mfma_chunk<kD3 / 16>(x3, buf, lane, x2[2 * p], x2[2 * p + 1]); });
-  }
-#pragma unroll
-  for (int m = 0; m < kD3 / 16; ++m) x3[m] = leaky(x3[m], a.slope);
 
   // ---- heads: Linear(32, 64) + LeakyReLU per head (stacked rows 64 k .. 64 k + 63), then
   // Linear(64, A) of that head's 64 features; raw outputs to heads[k][e][a], or (FLIP) the
@@ -407,7 +437,7 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
   float v = 0.f;
   bool explore = false;
   pbn::Word4 r0{0u, 0u, 0u, 0u}, r1{0u, 0u, 0u, 0u};
-  uint32_t mk[4] = {0u, 0u, 0u, 0u};
+  u32x4 mk = {0u, 0u, 0u, 0u};   // flip-mask words (a vector: no per-thread array in memory)
   if constexpr (FLIP) {   // the EXPLORE draws of env e (the four lane groups draw the same)
     const uint64_t ge = a.env_offset + (uint64_t)e;
     const uint64_t st = a.d_step ? *a.d_step : a.step;
@@ -417,23 +447,24 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
       eps_u = (uint64_t)floor((double)ef * 4294967296.0);
     }
     r0 = pbn::draw(a.seed, ge, st, pbn::kStreamExplore, 0);
-    if (a.n_heads > 4) r1 = pbn::draw(a.seed, ge, st, pbn::kStreamExplore, 1);
+    if (H > 4) r1 = pbn::draw(a.seed, ge, st, pbn::kStreamExplore, 1);
     explore = (uint64_t)r0.x < eps_u;
   }
-  for (int k = 0; k < a.n_heads; ++k) {
+  // head k from its stage buffer: the Linear(32, 64) piece at h1, the Linear(64, A) pieces at h2
+  // and h2 + 32 AT rows; then its output (FLIP: the value or the branch's action)
+  f32x4 x3[kD3 / 16];
+  auto head = [&](int k, const float* h1, const float* h2) __attribute__((always_inline)) {
     f32x4 z[kDH / 16];
 #pragma unroll
     for (int m = 0; m < kDH / 16; ++m) z[m] = bias_tile(bsh1 + kDH * k, m, g, kDH);
-    PBN_CHUNK(14 + 3 * k, { mfma_chunk<kDH / 16>(z, buf, lane, x3[0], x3[1]); });
+    mfma_chunk<kDH / 16>(z, h1, lane, x3[0], x3[1]);
 #pragma unroll
     for (int m = 0; m < kDH / 16; ++m) z[m] = leaky(z[m], a.slope);
     f32x4 o[T16];
 #pragma unroll
     for (int m = 0; m < T16; ++m) o[m] = bias_tile(bsh2 + A * k, m, g, A);
-#pragma unroll
-    for (int p = 0; p < kDH / 32; ++p) {
-      PBN_CHUNK(15 + 3 * k + p, { mfma_chunk<T16>(o, buf, lane, z[2 * p], z[2 * p + 1]); });
-    }
+    mfma_chunk<T16>(o, h2, lane, z[0], z[1]);
+    mfma_chunk<T16>(o, h2 + 32 * AT * kPitch, lane, z[2], z[3]);
     if constexpr (FLIP) {
       if (k == 0) {
         v = __shfl(o[0][0], lane & 15);   // value head output 0: register 0 of lane group 0
@@ -452,7 +483,7 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
           for (int w = 0; w < 4; ++w)
             if (w == ((act - 1) >> 5)) mk[w] |= 1u << ((act - 1) & 31);
         }
-        if (a.actions && live && g == 0) a.actions[e * (a.n_heads - 1) + b] = act;
+        if (a.actions && live && g == 0) a.actions[e * (H - 1) + b] = act;
       }
     } else if (live) {
       float* out = a.heads + ((size_t)k * a.n + e) * A;
@@ -465,6 +496,24 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
         }
       }
     }
+  };
+
+  // ---- Linear(64, 32) (stage 9, with head 0 when it fits)
+#pragma unroll
+  for (int m = 0; m < kD3 / 16; ++m) x3[m] = bias_tile(bs3, m, g, kD3);
+  auto stage9 = [&](const float* buf) __attribute__((always_inline)) {
+    mfma_chunk<kD3 / 16>(x3, buf, lane, x2[0], x2[1]);
+    mfma_chunk<kD3 / 16>(x3, buf + 32 * kPitch, lane, x2[2], x2[3]);
+#pragma unroll
+    for (int m = 0; m < kD3 / 16; ++m) x3[m] = leaky(x3[m], a.slope);
+    if constexpr (Plan::kMerge) head(0, buf + 64 * kPitch, buf + 128 * kPitch);
+  };
+  if (n_stages > 10) PBN_STAGE(9, kHead, 10 - Plan::kFirstHeadStage, Plan::kHeadPasses, { stage9(buf); });
+  else PBN_STAGE(9, kHead, 0, 0, { stage9(buf); });
+  for (int s = 10; s < n_stages; ++s) {
+    const int k = s - Plan::kFirstHeadStage;
+    if (s + 1 < n_stages) PBN_STAGE(s, kHead, k + 1, Plan::kHeadPasses, { head(k, buf, buf + 64 * kPitch); });
+    else PBN_STAGE(s, kHead, 0, 0, { head(k, buf, buf + 64 * kPitch); });
   }
   if constexpr (FLIP) {
     if (live && g == 0) {
@@ -473,11 +522,7 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
         if (w < a.W) a.flipmask[(size_t)w * a.n + e] = mk[w];
     }
   }
-#undef PBN_CHUNK
-#undef PBN_PUT
-#undef PBN_ST
-#undef PBN_FETCH
-#undef PBN_LD
+#undef PBN_STAGE
 }
 
 bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
