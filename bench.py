@@ -536,6 +536,21 @@ def pmc_profile(args, plan):
         return json.load(f), os.path.relpath(path, ROOT)
 
 
+def kernel_trace(args, plan):
+    """The rocprofv3 kernel-trace average of the same launch shape, if committed under profiles/
+    (tools/trace_summary.py): the kernel's own device time beside the two event clocks."""
+    if len(set(plan)) != 1:
+        return None
+    tail = ("_nofinal" if args.no_final_state else "") + (f"_settle{args.settle}" if args.settle >= 2 else "")
+    path = os.path.join(ROOT, "profiles", f"kernel_trace_{args.network}_{args.envs}_T{plan[0]}{tail}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    return {"avg_launch_us": d["avg_us"], "source": d.get("source"), "file": os.path.relpath(path, ROOT),
+            "command": d.get("command")}
+
+
 def visible_gpu_count() -> int:
     """GPUs this process may use, counted without touching HIP: the KFD topology in sysfs
     (nodes with SIMDs are GPUs), narrowed by ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES /
@@ -873,6 +888,13 @@ def main():
                                "and event overhead, part of every timed region)",
                        "host_ms_per_step": host_s * 1e3 / args.steps, "clock_warm_runs": warm_reps},
         }
+        if rollout_mode:
+            kt = kernel_trace(args, plan)
+            out["timing"]["launch_us"] = dev_ms * 1e3 / len(plan)
+            out["timing"]["default_events"]["launch_us"] = fenced_ms * 1e3 / len(plan)
+            if kt is not None:
+                kt["value"] = total_env_steps / (kt["avg_launch_us"] * 1e-6 * len(plan))
+                out["timing"]["kernel_trace"] = kt
         if settle is not None:
             out["config"]["step_law"] = f"settle (at most {args.settle} updates per env step)"
             out["settle"] = settle
