@@ -45,7 +45,7 @@ for step in "$@"; do
     tests) bash tools/gpu_tests.sh "$tag/tests" || fail tests ;;
     pytest:*)
       files=${step#pytest:}
-      timeout -k 10 600 python -u -m pytest ${files//,/ } -m gpu -x -v --timeout 240 --timeout-method thread \
+      timeout -k 10 ${PYTEST_TIMEOUT:-600} python -u -m pytest ${files//,/ } -m gpu -x -v --timeout 240 --timeout-method thread \
         > "$out/pytest.log" 2>&1 || { tail -40 "$out/pytest.log"; fail "$step"; }
       tail -2 "$out/pytest.log" ;;
     driver) bash tools/gpu_bench_profile.sh "$tag/driver" --gpus 1 --steps 20 --warmup 5 || fail driver ;;
