@@ -214,15 +214,34 @@ __device__ __forceinline__ void put_stage(const QnetArgs& a, int idx, int t, flo
 // float32 sum of adv_0 .. adv_{A-1} over A, torch.argmax's first maximum with NaN maximal.
 // Action a = 16 m + 4 g + i of the env sits in register i of tile m on lane group g; every lane
 // gathers its env's row from the four groups, so all four walk it in order.
+// scr: the wave's LDS scratch row block [16 envs][16 T16 actions] (nullptr: gather by __shfl,
+// the lane-to-lane path for heads too wide for a scratch block): each lane writes its T16 float4s
+// and reads its env's whole row back, T16 + 4 T16 LDS operations where the shuffles spend 16 T16.
 template <int T16>
-__device__ __forceinline__ int dueling_argmax(const f32x4 (&o)[T16], int lane, int A, float v) {
+__device__ __forceinline__ int dueling_argmax(const f32x4 (&o)[T16], int lane, int A, float v, float* scr) {
   float row[T16][4][4];   // [m][g][i]
+  if (scr) {
+    float* mine = scr + (lane & 15) * 16 * T16;
 #pragma unroll
-  for (int m = 0; m < T16; ++m)
+    for (int m = 0; m < T16; ++m) *reinterpret_cast<f32x4*>(mine + 16 * m + 4 * (lane >> 4)) = o[m];
+    __builtin_amdgcn_wave_barrier();   // one wave's LDS operations execute in order
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
+    for (int m = 0; m < T16; ++m)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) row[m][g][i] = __shfl(o[m][i], (lane & 15) + 16 * g);
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 q = *reinterpret_cast<const f32x4*>(mine + 16 * m + 4 * g);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) row[m][g][i] = q[i];
+      }
+    __builtin_amdgcn_wave_barrier();   // (the next head's writes follow these reads)
+  } else {
+#pragma unroll
+    for (int m = 0; m < T16; ++m)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) row[m][g][i] = __shfl(o[m][i], (lane & 15) + 16 * g);
+  }
   float sum = 0.f;
 #pragma unroll
   for (int m = 0; m < T16; ++m)
@@ -252,6 +271,9 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
   constexpr int T16 = 2 * AT;   // 16-feature output tiles of the second head layers
   using Plan = StagePlan<AT>;
   __shared__ __attribute__((aligned(16))) float wbuf[2 * kBufFloats];
+  // FLIP: per-wave scratch rows of the dueling epilogue (AT <= 2: 16 KB or 32 KB per block)
+  constexpr int kScr = (FLIP && AT <= 2) ? kWaves * 16 * 16 * T16 : 1;
+  __shared__ __attribute__((aligned(16))) float escr[kScr];
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4;
   const int A = a.n_act;
@@ -476,7 +498,8 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
                             : b == 4 ? r1.y : b == 5 ? r1.z : r1.w;
           act = (int)__umulhi(rw, (uint32_t)(a.n_nodes + 1));
         } else {
-          act = dueling_argmax<T16>(o, lane, A, v);
+          act = dueling_argmax<T16>(o, lane, A, v,
+                                    (FLIP && AT <= 2) ? escr + (threadIdx.x >> 6) * 16 * 16 * T16 : nullptr);
         }
         if (act > 0 && act <= a.n_nodes) {   // a > 0 flips node a - 1, once however often
 #pragma unroll
