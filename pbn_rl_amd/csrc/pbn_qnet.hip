@@ -278,7 +278,7 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
   const int g = lane >> 4;
   const int A = a.n_act;
   const int H = a.n_heads;
-  const int n_stages = Plan::kFirstHeadStage + H - (Plan::kMerge ? 1 : 0);
+  const int n_stages = Plan::kFirstHeadStage + H;   // head k in stage kFirstHeadStage + k
   // this lane's env: the wave's 16 envs in order (y input), or (BIL) the wave's 16 of the block's
   // envs stably sorted by target, so that a wave's envs share one or two targets' tables
   int64_t e;
