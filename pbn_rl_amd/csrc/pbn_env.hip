@@ -591,8 +591,7 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   net->lds_wave = ((size_t)net->tab_words + (size_t)kWavesPerBlock * net->wave_words) * 4;
   net->slot_words = (3 * W + 1) * 64 + net->lq * 64 * W;
   // + the selection wave's threshold digit masks [kNodeRecs - 1][B][32] (W == 1)
-  // (three step slots for single-word states: the pipelined kernel's lag-2 state wave)
-  net->lds_pipe = ((size_t)net->tab_words + 64 * (size_t)W + (W == 1 ? 3 : 2) * (size_t)net->slot_words +
+  net->lds_pipe = ((size_t)net->tab_words + 64 * (size_t)W + 2 * (size_t)net->slot_words +
                    (W == 1 ? (size_t)(kNodeRecs - 1) * d->prob_bits * 32 : 0)) * 4;
   // compact records for the wave kernel: {inputs as bytes, 4-input truth table, threshold, 0}
   net->wave1 = pick_wave<1>(W, d->prob_bits);

@@ -1170,10 +1170,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
   // entries per thread: most of the launch's fixed cost)
   // (single-word states only: for W > 1 the extra LDS costs more occupancy than it saves,
   // measured -15 % on pbn70 x 1M)
-  // step slots: three for single-word states (the lag-2 state wave below reads step t's slot
-  // in iteration t + 2, while the RNG waves write step t + 2's), two otherwise
-  constexpr int kSlots = W == 1 ? 3 : 2;
-  uint32_t* cm = slots + kSlots * (size_t)a.slot_words;
+  uint32_t* cm = slots + 2 * (size_t)a.slot_words;
   __syncthreads();
   PBN_RSTAMP(1);
   if constexpr (W == 1) {
@@ -1198,12 +1195,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
   __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
   PBN_RSTAMP(2);
 
-  // the state wave of single-word states with at most kNodeRecs functions per node (the fast
-  // path below) runs two iterations behind the RNG waves: it reads step t's slot one iteration
-  // before it applies step t, so the slot's LDS round trip is off its chain s_t -> s_t+1
-  const bool lag2 = W == 1 && u_mnf >= 1 && u_mnf <= kNodeRecs;
-  const int n_it = n_steps + (lag2 ? 2 : 1);
-  // one loop per role: every wave passes the same n_it block barriers, and each role's
+  // one loop per role: every wave passes the same n_steps + 1 block barriers, and each role's
   // loop-carried values (hoisted invariants) occupy registers only in that role's loop
   if (role == 1 && (u_fl & 4u) && u_gx == 2 && u_na >= 2 && (u_fl & 16u) && (W > 1 || N <= 31)) {
     // env draws, common configuration (random actions, gap bucket table, two or more
@@ -1226,7 +1218,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
       asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
       PBN_PSTAMP(k, 0);
       if (k < n_steps) {
-        uint32_t* slot = slots + (size_t)(k % kSlots) * a.slot_words;
+        uint32_t* slot = slots + (size_t)(k & 1) * a.slot_words;
         // part 1: the draws that feed LDS reads, and the reads themselves
         uint32_t xhi = E.w, xlo = E.z;
         const uint32_t c_act = ext64(xhi, xlo, n1 * n1 * n1);
@@ -1314,18 +1306,18 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
     };
     // two steps per trip with the ENV words alternating between EA and EB: no copies between steps
     Word4 EA = env_call(0), EB = EA;
-    for (int k = 0; k < n_it; k += 2) {
+    for (int k = 0; k <= n_steps; k += 2) {
       env_step(k, EA, EB);
-      if (k + 1 < n_it) env_step(k + 1, EB, EA);
+      if (k + 1 <= n_steps) env_step(k + 1, EB, EA);
     }
   } else if (role == 1) {
-    for (int k = 0; k < n_it; ++k) {
+    for (int k = 0; k <= n_steps; ++k) {
       asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
       asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
       PBN_PSTAMP(k, 0);
       if (k < n_steps) {
         // ---- env draws of step k, env `lane`
-        uint32_t* slot = slots + (size_t)(k % kSlots) * a.slot_words;
+        uint32_t* slot = slots + (size_t)(k & 1) * a.slot_words;
         const uint64_t step = a.step + (uint64_t)k;
         const uint32_t st_lo = (uint32_t)step;
         const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
@@ -1459,7 +1451,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
           for (int d = 0; d < 16; ++d) asm volatile("" : "+v"(nxt[d]));
 #endif
           PBN_PSTAMP_AT(k, 18);
-          uint32_t* lt_out = lt_base + (size_t)(k % kSlots) * a.slot_words;
+          uint32_t* lt_out = lt_base + (size_t)(k & 1) * a.slot_words;
 #pragma unroll
           for (int q = 0; q < NQ; ++q) lt_out[q * 64] = less_than_cm<B>(cur, cmi + (size_t)q * B * 32, 32);
           // keeps the next calls in this block (LLVM would sink them to the loop latch)
@@ -1475,9 +1467,9 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
 #pragma unroll
       for (int d = 0; d < 16; ++d) { dA[d] = 0; dB[d] = 0; }
       sel_calls(0, dA);
-      for (int k = 0; k < n_it; k += 2) {
+      for (int k = 0; k <= n_steps; k += 2) {
         sel_step(k, dA, dB);
-        if (k + 1 < n_it) sel_step(k + 1, dB, dA);
+        if (k + 1 <= n_steps) sel_step(k + 1, dB, dA);
       }
     };
     switch (u_mnf) {
@@ -1486,13 +1478,13 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
       default: sel_fast(std::integral_constant<int, 3>{}); break;
     }
   } else if (role == 2) {
-    for (int k = 0; k < n_it; ++k) {
+    for (int k = 0; k <= n_steps; ++k) {
       asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
       asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
       PBN_PSTAMP(k, 0);
       if (k < n_steps) {
         // ---- selection masks of step k: node l32 + 32r of group g
-        uint32_t* lt_out = slots + (size_t)(k % kSlots) * a.slot_words + (3 * W + 1) * 64 + half * 32 * W;
+        uint32_t* lt_out = slots + (size_t)(k & 1) * a.slot_words + (3 * W + 1) * 64 + half * 32 * W;
         const uint64_t step = a.step + (uint64_t)k;
         const uint32_t st_lo = (uint32_t)step;
         const uint32_t G_hi = (uint32_t)((G >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
@@ -1594,21 +1586,15 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
         uint32_t ins[K];
 #pragma unroll
         for (int q = 0; q < K; ++q) ins[q] = recL[q * 32 + l32].x;
-        // step t's flip mask, read in iteration t + 1 (right after the barrier that makes it
-        // visible, beside step t - 1's chain) and applied in iteration t + 2: s1 = s ^ m is the head
-        // of the chain, the rest of step t's slot is read under the transpose
-        uint32_t pm = 0;
-        for (int k = 0; k < n_it; ++k) {
+        for (int k = 0; k <= n_steps; ++k) {
           asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
           PBN_PSTAMP(k, 0);
-          uint32_t nm = 0;
-          if (k >= 1 && k - 1 < n_steps) nm = slots[(size_t)((k - 1) % kSlots) * a.slot_words + lane];
-          if (k >= 2) {
-            const int t = k - 2;
-            const uint32_t* slot = slots + (size_t)(t % kSlots) * a.slot_words;
+          if (k >= 1) {
+            const int t = k - 1;
+            const uint32_t* slot = slots + (size_t)(t & 1) * a.slot_words;
             const uint32_t* lt_in = slot + 4 * 64 + half * 32 + l32;
             uint32_t s1[W], gam[W], rs[W];
-            s1[0] = st[0] ^ pm;
+            s1[0] = st[0] ^ slot[lane];
             gam[0] = slot[64 + lane];
             rs[0] = slot[2 * 64 + lane];
             const uint32_t info = slot[3 * 64 + lane];
@@ -1640,11 +1626,10 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
             PBN_PSTAMP_AT(k, 13);
             finish(t, sp, s1, gam, rs, info);
           }
-          pm = nm;
           PBN_PSTAMP(k, 1);
           lds_barrier();
           PBN_PSTAMP(k, 2);
-          if (k == 0 || k == 2) PBN_RSTAMP(3 + k / 2);
+          if (k <= 1) PBN_RSTAMP(3 + k);
         }
       };
       switch (u_mnf) {
@@ -1654,14 +1639,14 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
         default: state_fast(std::integral_constant<int, 4>{}); break;
       }
     } else
-    for (int k = 0; k < n_it; ++k) {
+    for (int k = 0; k <= n_steps; ++k) {
       asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
       asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
       PBN_PSTAMP(k, 0);
       if (k >= 1) {
         // ---- state part of step t = k - 1
         const int t = k - 1;
-        const uint32_t* slot = slots + (size_t)(t % kSlots) * a.slot_words;
+        const uint32_t* slot = slots + (size_t)(t & 1) * a.slot_words;
         const uint32_t* lt_in = slot + (3 * W + 1) * 64 + half * 32 * W;
         uint32_t s1[W], gam[W], rs[W];
         uint32_t info = 0;
