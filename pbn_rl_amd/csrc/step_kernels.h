@@ -1588,6 +1588,11 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
         for (int q = 0; q < K; ++q) ins[q] = recL[q * 32 + l32].x;
         for (int k = 0; k <= n_steps; ++k) {
           asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
+          // the 4K plane addresses of the gathers are re-derived from ins[] every step: hoisted
+          // out of the loop they are 4K more live VGPRs, one was spilled, and its reload's
+          // s_waitcnt vmcnt(0) waited on the step's streaming stores in the middle of the chain
+#pragma unroll
+          for (int q = 0; q < K; ++q) asm volatile("" : "+v"(ins[q]));
           PBN_PSTAMP(k, 0);
           if (k >= 1) {
             const int t = k - 1;
