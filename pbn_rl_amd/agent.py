@@ -261,7 +261,9 @@ class BatchedBDQ:
                 return self._pack
         bil = self.q.model[0]
         T = bil.target_table(self.targets).contiguous() if self.targets.shape[0] else None
-        pack = (T, bil.bilinear.bias.contiguous(), self.q.head_weights())
+        # the fused kernels' layout of the same table: [a][i][j][q] = T[a][i][16 q + j]
+        Tq = T.view(T.shape[0], T.shape[1], 16, 16).transpose(2, 3).contiguous() if T is not None else None
+        pack = (T, bil.bilinear.bias.contiguous(), self.q.head_weights(), Tq)
         if key is not None:
             self._pack, self._pack_key = pack, key
         return pack
@@ -271,7 +273,7 @@ class BatchedBDQ:
         fast forward); returns the head weights of the same pack."""
         env = self.env
         bil = self.q.model[0]
-        T, bias, hw = self._packed()
+        T, bias, hw, _ = self._packed()
         L = _lib.load()
         with torch.cuda.device(env.device):
             _lib.check(L.pbn_bilinear_targets(env.net.handle, env.n_alloc, env.state.data_ptr(),
@@ -297,7 +299,7 @@ class BatchedBDQ:
         """Device pointers of the fused kernels' operands after the state: the bilinear layer's
         target table and bias, then the trunk and the stacked head weights."""
         m = self.q.model
-        T, bias, (w1, b1, w2, b2) = self._packed()
+        _, bias, (w1, b1, w2, b2), T = self._packed()
         ts = [bias, m[2].weight, m[2].bias, m[4].weight, m[4].bias, m[6].weight, m[6].bias, w1, b1, w2, b2]
         ts = [t.detach().contiguous() for t in ts]
         return [T.data_ptr() if T is not None else None] + [t.data_ptr() for t in ts], ts

@@ -24,6 +24,7 @@
 // per 16-feature tile).
 #include <hip/hip_runtime.h>
 
+#include <limits.h>
 #include <stdint.h>
 
 #include "../../include/pbn_env.h"
@@ -66,7 +67,22 @@ struct QnetArgs {
                                    // attractor's first state (MyBilinear.target_table)
   const float* b0;                 // [256]
   int n_attr;
+  unsigned long long* stamps;      // diagnostic builds (PBN_STAMPS): [block][wave][kQStampRow] s_memtime
 };
+
+// Diagnostic phase clocks (tools/qnet_stamps.py): lane 0 of every wave stores s_memtime at
+// 0 entry, 1 after the block's target sort, 2 after the bilinear layer, 3 stage 0 in LDS, and for
+// stage s at 4 + 3 s (its MFMA body starts), 5 + 3 s (body done), 6 + 3 s (past its barrier)
+constexpr int kQStampRow = 64;
+#ifdef PBN_STAMPS
+#define PBN_QSTAMP(i)                                                                                       \
+  do {                                                                                                    \
+    if (a.stamps && (threadIdx.x & 63) == 0)                                                              \
+      a.stamps[((size_t)blockIdx.x * kWaves + (threadIdx.x >> 6)) * kQStampRow + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define PBN_QSTAMP(i) do {} while (0)
+#endif
 
 constexpr int kPitch = 36;                   // weight row pitch in LDS (floats): conflict-free float4 reads
 constexpr int kBufFloats = 5 * 64 * kPitch;  // one stage buffer: 320 rows (the largest stage, below)
@@ -127,30 +143,35 @@ __device__ __forceinline__ void mfma_chunk(f32x4 (&acc)[MT], const float* __rest
 // The weights reach the MFMAs through LDS as a stream of STAGES, double-buffered: while the
 // block's waves run one stage's MFMAs from one buffer, every thread holds the next stage's global
 // loads in registers and stores them into the other buffer after the MFMAs; one block barrier per
-// stage.  A stage is a few 32-column pieces of weight matrices, each row padded to 36 floats (the
-// 16 rows one quarter-wave reads start on 16 distinct 4-bank groups):
-//   stages 0-7   Linear(256, 128), 32 input columns each (128 rows)
-//   stage 8      Linear(128, 64), all of it (four 64-row pieces)
-//   stage 9      Linear(64, 32) (two 32-row pieces), and head 0 when it fits beside it
-//   then         one stage per head k: Linear(32, 64) (64 rows) and Linear(64, A) (two pieces of
-//                32 AT rows, rows past A read as 0)
-// Round 3 streamed 32-column chunks only (26 stages and barriers at Bittner-28); each of the small
-// layers' chunks carried 512-1,024 MFMA cycles per wave, too few to cover the next chunk's L2
-// round trip and the barrier.  Now every stage after layer 1 carries at least 2,048.
+// stage.  A stage is a few 32-column pieces of weight matrices (up to 320 rows), each row padded to
+// 36 floats (the 16 rows one quarter-wave reads start on 16 distinct 4-bank groups):
+//   stages 0-3   Linear(256, 128), 64 input columns each (two 128-row pieces)
+//   stage 4      Linear(128, 64), all of it (four 64-row pieces)
+//   stage 5      Linear(64, 32) (two 32-row pieces), and the first heads that fit beside it
+//   then         the other heads, as many per stage as fit: per head Linear(32, 64) (64 rows) and
+//                Linear(64, A) (two pieces of 32 AT rows, rows past A read as 0)
+// Round 3 streamed 32-column chunks only (26 stages and barriers at Bittner-28); round 4 began with
+// 13 stages, whose LDS stores, barrier and first LDS reads cost ≈ 1,300 cycles each
+// (tools/qnet_stamps.py); Bittner-28 now runs 7.
 // Stage kinds; row r of a stage occupies rows r of its buffer (float offset r * kPitch), so only
 // the source of a row depends on the kind.
 enum StageKind { kL1 = 0, kL2 = 1, kS9 = 2, kHead = 3 };
+constexpr int kRows = kBufFloats / kPitch;   // rows per stage buffer (320)
+constexpr int kL1Cols = 64;                  // layer-1 input columns per stage
+constexpr int kL1Stages = kD0 / kL1Cols;
 
 template <int AT>
 struct StagePlan {
-  // layer 3 and head 0 share stage 9 when they fit in one buffer
-  static constexpr bool kMerge = 64 + (64 + 64 * AT) <= kBufFloats / kPitch;
-  static constexpr int kFirstHeadStage = kMerge ? 9 : 10;
   static constexpr int kHeadRows = 64 + 64 * AT;        // Linear(32, 64), then Linear(64, A) as two
                                                         // pieces of 32 AT rows (32 input columns each)
-  static constexpr int kS9Rows = 64 + (kMerge ? kHeadRows : 0);
-  static constexpr int kHeadPasses = kHeadRows / 64;
+  static constexpr int kHPS = kRows / kHeadRows;        // heads per head stage
+  static constexpr int kS9Heads = (kRows - 64) / kHeadRows < kHPS ? (kRows - 64) / kHeadRows : kHPS;
+  static constexpr int kS9Rows = 64 + kS9Heads * kHeadRows;
   static constexpr int kS9Passes = kS9Rows / 64;
+  static constexpr int kHeadPasses = kHPS * kHeadRows / 64;
+  static constexpr int kL2Stage = kL1Stages, kS9Stage = kL1Stages + 1, kFirstHeadStage = kL1Stages + 2;
+  static_assert(kHPS >= 1 && kS9Rows % 64 == 0 && (kHPS * kHeadRows) % 64 == 0, "stage rows");
+  static_assert(kS9Passes <= kMaxPieces && kHeadPasses <= kMaxPieces && 2 * 128 / 64 <= kMaxPieces, "passes");
 };
 
 // row r of head k's stage rows: its source and whether it is a row of the matrix (rows past A
@@ -165,12 +186,14 @@ __device__ __forceinline__ const float* head_row(const QnetArgs& a, int k, int r
   return a.wh2 + (size_t)a.n_act * kDH * k + 32 * j + (size_t)min(row, a.n_act - 1) * kDH;
 }
 
-// row r of a stage of kind KIND (idx = the layer-1 chunk, or the head)
+// row r of a stage of kind KIND (idx = the layer-1 stage, or the stage's first head); heads past
+// the last (the last head stage's unused slots) read head H - 1's rows and are stored as 0
 template <int AT, int KIND>
 __device__ __forceinline__ const float* stage_row(const QnetArgs& a, int idx, int r, bool& real) {
+  constexpr int HR = StagePlan<AT>::kHeadRows;
   if constexpr (KIND == kL1) {
     real = true;
-    return a.w1 + 32 * idx + (size_t)r * kD0;
+    return a.w1 + kL1Cols * idx + 32 * (r >> 7) + (size_t)(r & 127) * kD0;
   } else if constexpr (KIND == kL2) {
     real = true;
     return a.w2 + 32 * (r >> 6) + (size_t)(r & 63) * kD1;
@@ -179,9 +202,15 @@ __device__ __forceinline__ const float* stage_row(const QnetArgs& a, int idx, in
       real = true;
       return a.w3 + 32 * (r >> 5) + (size_t)(r & 31) * kD2;
     }
-    return head_row(a, 0, r - 64, 32 * AT, real);
+    const int j = (r - 64) / HR;
+    const float* p = head_row(a, min(j, a.n_heads - 1), r - 64 - j * HR, 32 * AT, real);
+    real = real && j < a.n_heads;
+    return p;
   } else {
-    return head_row(a, idx, r, 32 * AT, real);
+    const int j = r / HR, k = idx + j;
+    const float* p = head_row(a, min(k, a.n_heads - 1), r - j * HR, 32 * AT, real);
+    real = real && k < a.n_heads;
+    return p;
   }
 }
 
@@ -212,18 +241,36 @@ __device__ __forceinline__ void put_stage(const QnetArgs& a, int idx, int t, flo
 // The dueling combination and argmax of one advantage head, as pbn_heads_to_flipmask computes
 // them (pbn_agent.hip, q_to_flipmask_kernel): q_a = (v + adv_a) - mean, mean = the left-to-right
 // float32 sum of adv_0 .. adv_{A-1} over A, torch.argmax's first maximum with NaN maximal.
-// Action a = 16 m + 4 g + i of the env sits in register i of tile m on lane group g; every lane
-// gathers its env's row from the four groups, so all four walk it in order.
-// scr: the wave's LDS scratch row block [16 envs][16 T16 actions] (nullptr: gather by __shfl,
-// the lane-to-lane path for heads too wide for a scratch block): each lane writes its T16 float4s
-// and reads its env's whole row back, T16 + 4 T16 LDS operations where the shuffles spend 16 T16.
-template <int T16>
-__device__ __forceinline__ int dueling_argmax(const f32x4 (&o)[T16], int lane, int A, float v, float* scr) {
+// Action a = 16 m + 4 g + i of the env sits in register i of tile m on lane group g.  Branch-free
+// over A: vm (this lane group's bit 4 m + i = action 16 m + 4 g + i < A) pads the actions past A
+// with -0.0 for the sum (x + -0.0 == x for every x, so the walk over all 16 T16 entries is the
+// walk over the first A) and with -inf for the argmax (below every number; a tie goes to the lower,
+// real, index).
+// The sum: every lane gathers its env's row from the four groups and walks it in order, through
+// the wave's LDS scratch row block [16 envs][16 T16 actions] (SCR: T16 + 4 T16 LDS operations) or
+// by __shfl (heads too wide for a scratch block).
+// The argmax: each lane group walks its own actions in ascending order in registers, then the four
+// groups' candidates meet in two xor butterflies.  The rule -- a NaN before any number, the lower
+// index among NaNs, else the larger value, the lower index on a tie -- picks what the left-to-right
+// walk picks and is associative, so the split is exact.
+__device__ __forceinline__ float pad_if(uint32_t vm, int bit, float x, uint32_t pad) {
+  const uint32_t mk = (uint32_t)__builtin_amdgcn_sbfe((int)vm, bit, 1);
+  return __builtin_bit_cast(float, (__builtin_bit_cast(uint32_t, x) & mk) | (pad & ~mk));
+}
+
+template <int T16, bool SCR>
+__device__ __forceinline__ int dueling_argmax(const f32x4 (&o)[T16], int lane, int A, uint32_t vm, float v,
+                                              float* scr) {
+  f32x4 op[T16];   // -0.0 past A
+#pragma unroll
+  for (int m = 0; m < T16; ++m)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) op[m][i] = pad_if(vm, 4 * m + i, o[m][i], 0x80000000u);
   float row[T16][4][4];   // [m][g][i]
-  if (scr) {
+  if constexpr (SCR) {
     float* mine = scr + (lane & 15) * 16 * T16;
 #pragma unroll
-    for (int m = 0; m < T16; ++m) *reinterpret_cast<f32x4*>(mine + 16 * m + 4 * (lane >> 4)) = o[m];
+    for (int m = 0; m < T16; ++m) *reinterpret_cast<f32x4*>(mine + 16 * m + 4 * (lane >> 4)) = op[m];
     __builtin_amdgcn_wave_barrier();   // one wave's LDS operations execute in order
 #pragma unroll
     for (int m = 0; m < T16; ++m)
@@ -240,29 +287,36 @@ __device__ __forceinline__ int dueling_argmax(const f32x4 (&o)[T16], int lane, i
 #pragma unroll
       for (int g = 0; g < 4; ++g)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) row[m][g][i] = __shfl(o[m][i], (lane & 15) + 16 * g);
+        for (int i = 0; i < 4; ++i) row[m][g][i] = __shfl(op[m][i], (lane & 15) + 16 * g);
   }
   float sum = 0.f;
 #pragma unroll
   for (int m = 0; m < T16; ++m)
 #pragma unroll
-    for (int f = 0; f < 16; ++f)
-      if (16 * m + f < A) sum += row[m][f >> 2][f & 3];
+    for (int f = 0; f < 16; ++f) sum += row[m][f >> 2][f & 3];
   const float mean = sum / (float)A;
-  float best = (v + row[0][0][0]) - mean;
+  const int g = lane >> 4;
+  float best = 0.f;
   int bi = 0;
 #pragma unroll
   for (int m = 0; m < T16; ++m)
 #pragma unroll
-    for (int f = 0; f < 16; ++f) {
-      const int act = 16 * m + f;
-      if (act >= 1 && act < A) {
-        const float qa = (v + row[m][f >> 2][f & 3]) - mean;
-        const bool take = !isnan(best) && (isnan(qa) || qa > best);
-        best = take ? qa : best;
-        bi = take ? act : bi;
-      }
+    for (int i = 0; i < 4; ++i) {
+      const float qa = pad_if(vm, 4 * m + i, (v + o[m][i]) - mean, 0xFF800000u);   // -inf past A
+      // (bitwise & and |: the short-circuit forms compile to exec-mask branches)
+      const bool take = (m == 0 && i == 0) || ((!isnan(best)) & (isnan(qa) | (qa > best)));
+      best = take ? qa : best;
+      bi = take ? 16 * m + 4 * g + i : bi;
     }
+#pragma unroll
+  for (int x = 16; x <= 32; x <<= 1) {
+    const float ob = __shfl_xor(best, x);
+    const int oi = __shfl_xor(bi, x);
+    const bool nm = isnan(best), no = isnan(ob);
+    const bool take = (nm & no) ? oi < bi : (no ? true : (nm ? false : ((ob > best) | ((ob == best) & (oi < bi)))));
+    best = take ? ob : best;
+    bi = take ? oi : bi;
+  }
   return bi;
 }
 
@@ -278,7 +332,9 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
   const int g = lane >> 4;
   const int A = a.n_act;
   const int H = a.n_heads;
-  const int n_stages = Plan::kFirstHeadStage + H;   // head k in stage kFirstHeadStage + k
+  // heads kS9Heads + kHPS j .. in head stage kFirstHeadStage + j
+  const int n_stages = Plan::kFirstHeadStage + (H - Plan::kS9Heads + Plan::kHPS - 1) / Plan::kHPS;
+  PBN_QSTAMP(0);
   // this lane's env: the wave's 16 envs in order (y input), or (BIL) the wave's 16 of the block's
   // envs stably sorted by target, so that a wave's envs share one or two targets' tables
   int64_t e;
@@ -291,24 +347,56 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
   } else {
     __shared__ uint8_t skey[kWaves * kEnvs];
     __shared__ uint8_t sperm[kWaves * kEnvs];
+    __shared__ uint16_t wcnt[2][256];   // keys per sorting wave (waves 0, 1 hold one key per lane)
+    __shared__ uint16_t kbase[256];     // keys below, block-wide (exclusive prefix)
+    static_assert(kWaves * kEnvs == 128, "the block's keys are the lanes of waves 0 and 1");
     const int64_t eb = (int64_t)blockIdx.x * kWaves * kEnvs;
     const int tt = threadIdx.x;
+    const int wv = tt >> 6;
+    if (tt < 256) reinterpret_cast<uint32_t*>(&wcnt[0][0])[tt] = 0u;
+    int k = 255, rank = 0;
     if (tt < kWaves * kEnvs) {
       const bool lv = eb + tt < a.n;
       const uint32_t tg = lv ? (uint32_t)a.target[eb + tt] : 255u;
-      skey[tt] = (uint8_t)(lv ? (tg < (uint32_t)a.n_attr ? tg : (uint32_t)a.n_attr) : 255u);
+      k = lv ? (int)(tg < (uint32_t)a.n_attr ? tg : (uint32_t)a.n_attr) : 255;
+      skey[tt] = (uint8_t)k;
     }
     __syncthreads();
-    if (tt < kWaves * kEnvs) {   // stable counting sort: position = keys below + equal keys before
-      const int k = skey[tt];
-      int pos = 0;
-      for (int u = 0; u < kWaves * kEnvs; ++u) {
-        const int ku = skey[u];
-        pos += (ku < k || (ku == k && u < tt)) ? 1 : 0;
+    // stable counting sort in three barriers: each of waves 0, 1 ranks its lanes among equal keys
+    // (one ballot per distinct key of the wave) and counts them; wave 0 scans the counts; every
+    // key's position = keys below + equal keys in wave 0 (for wave 1) + equal keys on lower lanes
+    if (wv < 2) {
+      uint64_t rem = __ballot(1);
+      while (rem) {
+        const int l = __builtin_ctzll(rem);
+        const int kk = __builtin_amdgcn_readlane(k, l);
+        const uint64_t m = __ballot(k == kk);
+        if (k == kk) rank = __builtin_popcountll(m & ((1ull << lane) - 1ull));
+        if (lane == l) wcnt[wv][kk] = (uint16_t)__builtin_popcountll(m);
+        rem &= ~m;
       }
-      sperm[pos] = (uint8_t)tt;
     }
     __syncthreads();
+    if (wv == 0) {   // exclusive prefix over the 256 keys: four per lane, then across lanes
+      int c[4], tot = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        c[j] = tot;
+        tot += (int)wcnt[0][4 * lane + j] + (int)wcnt[1][4 * lane + j];
+      }
+      int inc = tot;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(inc, d);
+        inc += lane >= d ? y : 0;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) kbase[4 * lane + j] = (uint16_t)(inc - tot + c[j]);
+    }
+    __syncthreads();
+    if (tt < kWaves * kEnvs) sperm[(int)kbase[k] + (wv == 1 ? (int)wcnt[0][k] : 0) + rank] = (uint8_t)tt;
+    __syncthreads();
+    PBN_QSTAMP(1);
     const int li = sperm[(threadIdx.x >> 6) * kEnvs + (lane & 15)];
     key = skey[li];
     live = key != 255;
@@ -327,13 +415,16 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
     const int ss_ = (s_);                                                                          \
     if constexpr ((NEXT_PASSES) > 0) fetch_stage<AT, (NEXT_KIND), (NEXT_PASSES)>(a, (NEXT_IDX), t, sv); \
     __builtin_amdgcn_sched_barrier(0);                                                             \
+    PBN_QSTAMP(4 + 3 * ss_);                                                                       \
     const float* buf = wbuf + (ss_ & 1) * kBufFloats;                                              \
     BODY                                                                                           \
     __builtin_amdgcn_sched_barrier(0);                                                             \
+    PBN_QSTAMP(5 + 3 * ss_);                                                                       \
     if constexpr ((NEXT_PASSES) > 0) {                                                             \
       put_stage<AT, (NEXT_KIND), (NEXT_PASSES)>(a, (NEXT_IDX), t, wbuf + ((ss_ + 1) & 1) * kBufFloats, sv); \
       __syncthreads();                                                                             \
     }                                                                                              \
+    PBN_QSTAMP(6 + 3 * ss_);                                                                       \
   } while (0)
 
   // every bias, staged once in LDS (a per-head bias load from L2 sat in front of the head's
@@ -348,37 +439,46 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
   for (int i = t; i < kD2; i += 64 * kWaves) bs2[i] = a.b2[i];
   for (int i = t; i < kD3; i += 64 * kWaves) bs3[i] = a.b3[i];
   for (int i = t; i < kDH * H; i += 64 * kWaves) bsh1[i] = a.bh1[i];
-  for (int i = t; i < A * H; i += 64 * kWaves) bsh2[i] = a.bh2[i];
+  // bh2 as [H][32 AT], zero past A: the head's bias tiles read it with no per-element test
+  for (int i = t; i < 32 * AT * H; i += 64 * kWaves) {
+    const int kk = i / (32 * AT), aa = i - kk * 32 * AT;
+    bsh2[i] = aa < A ? a.bh2[kk * A + aa] : 0.f;
+  }
 
-  fetch_stage<AT, kL1, 2>(a, 0, t, sv);
-  put_stage<AT, kL1, 2>(a, 0, t, wbuf, sv);
+  fetch_stage<AT, kL1, 4>(a, 0, t, sv);
+  put_stage<AT, kL1, 4>(a, 0, t, wbuf, sv);
 
   // ---- Linear(256, 128): input tiles from y, features 16 p + 4 g .. + 3 (one float4 per tile);
   // a stage is two tiles, whose loads fly one stage ahead
   f32x4 x1[kD1 / 16];
   if constexpr (!BIL) {
     const float* yrow = a.y + (size_t)e * kD0 + 4 * g;
-    f32x4 yv0, yv1, yn0, yn1;
-    {
-      const float4 u0 = *reinterpret_cast<const float4*>(yrow), u1 = *reinterpret_cast<const float4*>(yrow + 16);
-      yv0 = f32x4{u0.x, u0.y, u0.z, u0.w};
-      yv1 = f32x4{u1.x, u1.y, u1.z, u1.w};
+    f32x4 yv[4], yn[4];   // a stage's four input tiles: columns 64 p + 16 j + 4 g .. + 3
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4 u = *reinterpret_cast<const float4*>(yrow + 16 * j);
+      yv[j] = f32x4{u.x, u.y, u.z, u.w};
     }
     __syncthreads();   // stage 0 and the biases are in LDS
 #pragma unroll
     for (int m = 0; m < kD1 / 16; ++m) x1[m] = bias_tile(bs1, m, g, kD1);
 #pragma unroll
-    for (int p = 0; p < kD0 / 32; ++p) {
-      if (p + 1 < kD0 / 32) {   // the next stage's y tiles fly under this stage's MFMAs
-        const float4 u0 = *reinterpret_cast<const float4*>(yrow + 32 * (p + 1));
-        const float4 u1 = *reinterpret_cast<const float4*>(yrow + 32 * (p + 1) + 16);
-        yn0 = f32x4{u0.x, u0.y, u0.z, u0.w};
-        yn1 = f32x4{u1.x, u1.y, u1.z, u1.w};
+    for (int p = 0; p < kL1Stages; ++p) {
+      if (p + 1 < kL1Stages) {   // the next stage's y tiles fly under this stage's MFMAs
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float4 u = *reinterpret_cast<const float4*>(yrow + kL1Cols * (p + 1) + 16 * j);
+          yn[j] = f32x4{u.x, u.y, u.z, u.w};
+        }
       }
-      if (p + 1 < kD0 / 32) PBN_STAGE(p, kL1, p + 1, 2, { mfma_chunk<kD1 / 16>(x1, buf, lane, yv0, yv1); });
-      else PBN_STAGE(p, kL2, 0, 4, { mfma_chunk<kD1 / 16>(x1, buf, lane, yv0, yv1); });
-      yv0 = yn0;
-      yv1 = yn1;
+      if (p + 1 < kL1Stages)
+        PBN_STAGE(p, kL1, p + 1, 4, { mfma_chunk<kD1 / 16>(x1, buf, lane, yv[0], yv[1]);
+                                      mfma_chunk<kD1 / 16>(x1, buf + 128 * kPitch, lane, yv[2], yv[3]); });
+      else
+        PBN_STAGE(p, kL2, 0, 4, { mfma_chunk<kD1 / 16>(x1, buf, lane, yv[0], yv[1]);
+                                  mfma_chunk<kD1 / 16>(x1, buf + 128 * kPitch, lane, yv[2], yv[3]); });
+#pragma unroll
+      for (int j = 0; j < 4; ++j) yv[j] = yn[j];
     }
   } else {
     // the bilinear layer of the wave's 16 envs, all 256 outputs, in registers: y^T = b0 +
@@ -400,20 +500,22 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
     const int kend = khi < a.n_attr ? khi : a.n_attr - 1;
     for (int ta = klo; ta <= kend; ++ta) {
       if (!__any(key == ta)) continue;
-      const float* Ta = a.T + (size_t)ta * N * kD0 + (lane & 15);
+      // T in the from_state layout [a][node][j][q] = T[a][node][16 q + j]: lane j's 16 A operands
+      // of a k-step (outputs 16 q + j, q = 0..15) are 64 contiguous bytes, four 16-byte loads
+      const float* Ta = a.T + (size_t)ta * N * kD0 + 16 * (lane & 15);
       const bool mine = key == ta;
-      // k-step s4: nodes s4 .. s4 + 3, this lane's s4 + g; the next step's 16 table loads are
+      // k-step s4: nodes s4 .. s4 + 3, this lane's s4 + g; the next step's 4 table loads are
       // issued before this step's 16 MFMAs (rows past N load row N - 1 and meet a 0 operand)
-      float av[kD0 / 16], an[kD0 / 16];
+      f32x4 av[4], an[4];
       {
         const float* Tn = Ta + (size_t)min(g, N - 1) * kD0;
 #pragma unroll
-        for (int q = 0; q < kD0 / 16; ++q) av[q] = Tn[16 * q];
+        for (int u = 0; u < 4; ++u) av[u] = *reinterpret_cast<const f32x4*>(Tn + 4 * u);
       }
       for (int s4 = 0; s4 < N; s4 += 4) {
         const float* Tn = Ta + (size_t)min(s4 + 4 + g, N - 1) * kD0;
 #pragma unroll
-        for (int q = 0; q < kD0 / 16; ++q) an[q] = Tn[16 * q];
+        for (int u = 0; u < 4; ++u) an[u] = *reinterpret_cast<const f32x4*>(Tn + 4 * u);
         __builtin_amdgcn_sched_barrier(0);
         const int node = s4 + g;
         uint32_t wsel = sw[0];
@@ -421,21 +523,27 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
         for (int w = 1; w < 4; ++w) wsel = (node >> 5) == w ? sw[w] : wsel;
         const float bv = (mine && node < N && ((wsel >> (node & 31)) & 1u)) ? 1.f : 0.f;
 #pragma unroll
-        for (int q = 0; q < kD0 / 16; ++q) yt[q] = mfma(av[q], bv, yt[q]);
+        for (int q = 0; q < kD0 / 16; ++q) yt[q] = mfma(av[q >> 2][q & 3], bv, yt[q]);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int q = 0; q < kD0 / 16; ++q) av[q] = an[q];
+        for (int u = 0; u < 4; ++u) av[u] = an[u];
       }
     }
 #pragma unroll
     for (int q = 0; q < kD0 / 16; ++q) yt[q] = leaky(yt[q], a.slope);
+    PBN_QSTAMP(2);
     __syncthreads();   // stage 0 and the biases are in LDS
+    PBN_QSTAMP(3);
 #pragma unroll
     for (int m = 0; m < kD1 / 16; ++m) x1[m] = bias_tile(bs1, m, g, kD1);
 #pragma unroll
-    for (int p = 0; p < kD0 / 32; ++p) {
-      if (p + 1 < kD0 / 32) PBN_STAGE(p, kL1, p + 1, 2, { mfma_chunk<kD1 / 16>(x1, buf, lane, yt[2 * p], yt[2 * p + 1]); });
-      else PBN_STAGE(p, kL2, 0, 4, { mfma_chunk<kD1 / 16>(x1, buf, lane, yt[2 * p], yt[2 * p + 1]); });
+    for (int p = 0; p < kL1Stages; ++p) {
+      if (p + 1 < kL1Stages)
+        PBN_STAGE(p, kL1, p + 1, 4, { mfma_chunk<kD1 / 16>(x1, buf, lane, yt[4 * p], yt[4 * p + 1]);
+                                      mfma_chunk<kD1 / 16>(x1, buf + 128 * kPitch, lane, yt[4 * p + 2], yt[4 * p + 3]); });
+      else
+        PBN_STAGE(p, kL2, 0, 4, { mfma_chunk<kD1 / 16>(x1, buf, lane, yt[4 * p], yt[4 * p + 1]);
+                                  mfma_chunk<kD1 / 16>(x1, buf + 128 * kPitch, lane, yt[4 * p + 2], yt[4 * p + 3]); });
     }
   }
 #pragma unroll
@@ -449,7 +557,7 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
 #pragma unroll
     for (int p = 0; p < kD1 / 32; ++p) mfma_chunk<kD2 / 16>(x2, buf + p * 64 * kPitch, lane, x1[2 * p], x1[2 * p + 1]);
   };
-  PBN_STAGE(8, kS9, 0, Plan::kS9Passes, { layer2(buf); });
+  PBN_STAGE(Plan::kL2Stage, kS9, 0, Plan::kS9Passes, { layer2(buf); });
 #pragma unroll
   for (int m = 0; m < kD2 / 16; ++m) x2[m] = leaky(x2[m], a.slope);
 
@@ -460,6 +568,11 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
   bool explore = false;
   pbn::Word4 r0{0u, 0u, 0u, 0u}, r1{0u, 0u, 0u, 0u};
   u32x4 mk = {0u, 0u, 0u, 0u};   // flip-mask words (a vector: no per-thread array in memory)
+  uint32_t vm = 0;                // bit 4 m + i: this lane group's action 16 m + 4 g + i < A
+#pragma unroll
+  for (int m = 0; m < T16; ++m)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) vm |= (16 * m + 4 * g + i < A ? 1u : 0u) << (4 * m + i);
   if constexpr (FLIP) {   // the EXPLORE draws of env e (the four lane groups draw the same)
     const uint64_t ge = a.env_offset + (uint64_t)e;
     const uint64_t st = a.d_step ? *a.d_step : a.step;
@@ -484,7 +597,7 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
     for (int m = 0; m < kDH / 16; ++m) z[m] = leaky(z[m], a.slope);
     f32x4 o[T16];
 #pragma unroll
-    for (int m = 0; m < T16; ++m) o[m] = bias_tile(bsh2 + A * k, m, g, A);
+    for (int m = 0; m < T16; ++m) o[m] = bias_tile(bsh2 + 32 * AT * k, m, g, 32 * AT);
     mfma_chunk<T16>(o, h2, lane, z[0], z[1]);
     mfma_chunk<T16>(o, h2 + 32 * AT * kPitch, lane, z[2], z[3]);
     if constexpr (FLIP) {
@@ -498,8 +611,10 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
                             : b == 4 ? r1.y : b == 5 ? r1.z : r1.w;
           act = (int)__umulhi(rw, (uint32_t)(a.n_nodes + 1));
         } else {
-          act = dueling_argmax<T16>(o, lane, A, v,
-                                    (FLIP && AT <= 2) ? escr + (threadIdx.x >> 6) * 16 * 16 * T16 : nullptr);
+          uint32_t vmk = vm;
+          asm volatile("" : "+v"(vmk));   // (per head: hoisted, its selects were SGPR pairs that spilled)
+          act = dueling_argmax<T16, (AT <= 2)>(o, lane, A, vmk, v,
+                                               (AT <= 2) ? escr + (threadIdx.x >> 6) * 16 * 16 * T16 : nullptr);
         }
         if (act > 0 && act <= a.n_nodes) {   // a > 0 flips node a - 1, once however often
 #pragma unroll
@@ -529,14 +644,24 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
     mfma_chunk<kD3 / 16>(x3, buf + 32 * kPitch, lane, x2[2], x2[3]);
 #pragma unroll
     for (int m = 0; m < kD3 / 16; ++m) x3[m] = leaky(x3[m], a.slope);
-    if constexpr (Plan::kMerge) head(0, buf + 64 * kPitch, buf + 128 * kPitch);
+#pragma unroll
+    for (int j = 0; j < Plan::kS9Heads; ++j)
+      if (j < H) head(j, buf + (64 + j * Plan::kHeadRows) * kPitch, buf + (128 + j * Plan::kHeadRows) * kPitch);
   };
-  if (n_stages > 10) PBN_STAGE(9, kHead, 10 - Plan::kFirstHeadStage, Plan::kHeadPasses, { stage9(buf); });
-  else PBN_STAGE(9, kHead, 0, 0, { stage9(buf); });
-  for (int s = 10; s < n_stages; ++s) {
-    const int k = s - Plan::kFirstHeadStage;
-    if (s + 1 < n_stages) PBN_STAGE(s, kHead, k + 1, Plan::kHeadPasses, { head(k, buf, buf + 64 * kPitch); });
-    else PBN_STAGE(s, kHead, 0, 0, { head(k, buf, buf + 64 * kPitch); });
+  // the heads of one head stage (those past H, in the last stage's unused slots, are skipped)
+  auto heads = [&](int k0, const float* buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < Plan::kHPS; ++j)
+      if (k0 + j < H) head(k0 + j, buf + j * Plan::kHeadRows * kPitch, buf + (64 + j * Plan::kHeadRows) * kPitch);
+  };
+  if (n_stages > Plan::kFirstHeadStage)
+    PBN_STAGE(Plan::kS9Stage, kHead, Plan::kS9Heads, Plan::kHeadPasses, { stage9(buf); });
+  else
+    PBN_STAGE(Plan::kS9Stage, kHead, 0, 0, { stage9(buf); });
+  for (int s = Plan::kFirstHeadStage; s < n_stages; ++s) {
+    const int k0 = Plan::kS9Heads + (s - Plan::kFirstHeadStage) * Plan::kHPS;
+    if (s + 1 < n_stages) PBN_STAGE(s, kHead, k0 + Plan::kHPS, Plan::kHeadPasses, { heads(k0, buf); });
+    else PBN_STAGE(s, kHead, 0, 0, { heads(k0, buf); });
   }
   if constexpr (FLIP) {
     if (live && g == 0) {
@@ -568,8 +693,16 @@ int qnet_check(const pbn_net* net, int64_t n_envs, const float* d_y, const float
   return PBN_OK;
 }
 
+#ifdef PBN_STAMPS
+unsigned long long* g_qstamps = nullptr;   // pbn_debug_set_qnet_stamps
+#endif
+
 template <bool FLIP, bool BIL>
-int qnet_launch(const QnetArgs& a, void* stream) {
+int qnet_launch(const QnetArgs& a_in, void* stream) {
+  QnetArgs a = a_in;
+#ifdef PBN_STAMPS
+  a.stamps = g_qstamps;
+#endif
   const int64_t waves = a.n / kEnvs;
   const unsigned blocks = (unsigned)((waves + kWaves - 1) / kWaves);
   void (*kernels[kMaxActTiles])(QnetArgs) = {qnet_tail_kernel<1, FLIP, BIL>, qnet_tail_kernel<2, FLIP, BIL>,
@@ -586,7 +719,7 @@ int bil_check(const pbn_net* net, const uint32_t* d_state, const uint8_t* d_targ
   int rc = pbn::net_view(net, &v);
   if (rc) return rc;
   if (!d_state || !d_target || !d_b0 || (v.n_attr > 0 && !d_T)) return pbn::set_error(PBN_EINVAL, "null buffer");
-  if (!al16(d_b0)) return pbn::set_error(PBN_EINVAL, "d_b0 must be 16-byte aligned");
+  if (!al16(d_b0) || !al16(d_T)) return pbn::set_error(PBN_EINVAL, "d_b0 and d_T must be 16-byte aligned");
   a.state = d_state; a.target = d_target; a.T = d_T; a.b0 = d_b0;
   a.n_attr = v.n_attr; a.n_nodes = v.n_nodes; a.W = v.W;
   return PBN_OK;
@@ -595,6 +728,13 @@ int bil_check(const pbn_net* net, const uint32_t* d_state, const uint8_t* d_targ
 }  // namespace
 
 extern "C" {
+
+#ifdef PBN_STAMPS
+int pbn_debug_set_qnet_stamps(unsigned long long* d_buf) {
+  g_qstamps = d_buf;
+  return 0;
+}
+#endif
 
 int pbn_qnet_heads(const pbn_net* net, int64_t n_envs, const float* d_y, const float* d_w1, const float* d_b1,
                    const float* d_w2, const float* d_b2, const float* d_w3, const float* d_b3, const float* d_wh1,

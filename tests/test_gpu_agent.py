@@ -440,6 +440,7 @@ def test_qnet_from_state_rejects_bad_arguments():
     ok = [h, 1, 0, None, 0, 64, st, tg, *ptrs, 3, 29, 0.01, 0.0, None, fm, None, None]
     assert L.pbn_qnet_flipmask_from_state(*ok) == 0
     for idx, val in [(8, None),                       # T with attractors
+                     (8, ptrs[0] + 4),                # T misaligned (16-byte loads)
                      (9, ptrs[1] + 4),                # b0 misaligned
                      (6, None),                       # state
                      (20, 0),                         # n_branches
