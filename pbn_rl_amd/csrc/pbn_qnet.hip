@@ -258,66 +258,91 @@ __device__ __forceinline__ float pad_if(uint32_t vm, int bit, float x, uint32_t 
   return __builtin_bit_cast(float, (__builtin_bit_cast(uint32_t, x) & mk) | (pad & ~mk));
 }
 
-template <int T16, bool SCR>
-__device__ __forceinline__ int dueling_argmax(const f32x4 (&o)[T16], int lane, int A, uint32_t vm, float v,
-                                              float* scr) {
-  f32x4 op[T16];   // -0.0 past A
+template <int T16, int NB, bool SCR>
+__device__ __forceinline__ void dueling_argmax(const f32x4 (&o)[NB][T16], int lane, int A, uint32_t vm, float v,
+                                               float* scr, int (&act)[NB]) {
+  // NB heads at once, head b innermost in every loop: their dependent chains (the sums, the
+  // walks) interleave instead of running one after the other
+  f32x4 op[NB][T16];   // -0.0 past A
 #pragma unroll
-  for (int m = 0; m < T16; ++m)
+  for (int b = 0; b < NB; ++b)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) op[m][i] = pad_if(vm, 4 * m + i, o[m][i], 0x80000000u);
-  float row[T16][4][4];   // [m][g][i]
+    for (int m = 0; m < T16; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) op[b][m][i] = pad_if(vm, 4 * m + i, o[b][m][i], 0x80000000u);
+  float row[NB][T16][4][4];   // [b][m][g][i]
   if constexpr (SCR) {
-    float* mine = scr + (lane & 15) * 16 * T16;
+    // [b][16 envs][kScrPitch]: rows 16 T16 + 4 floats apart, so the 16 rows of a 16-byte access
+    // start on 16 distinct 4-bank groups (a 16 T16-float pitch put them on one or two: 8-way conflicts)
+    constexpr int P = 16 * T16 + 4;
+    float* mine = scr + (lane & 15) * P;
 #pragma unroll
-    for (int m = 0; m < T16; ++m) *reinterpret_cast<f32x4*>(mine + 16 * m + 4 * (lane >> 4)) = op[m];
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int m = 0; m < T16; ++m)
+        *reinterpret_cast<f32x4*>(mine + b * 16 * P + 16 * m + 4 * (lane >> 4)) = op[b][m];
     __builtin_amdgcn_wave_barrier();   // one wave's LDS operations execute in order
 #pragma unroll
-    for (int m = 0; m < T16; ++m)
+    for (int b = 0; b < NB; ++b)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 q = *reinterpret_cast<const f32x4*>(mine + 16 * m + 4 * g);
+      for (int m = 0; m < T16; ++m)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) row[m][g][i] = q[i];
-      }
-    __builtin_amdgcn_wave_barrier();   // (the next head's writes follow these reads)
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 q = *reinterpret_cast<const f32x4*>(mine + b * 16 * P + 16 * m + 4 * g);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) row[b][m][g][i] = q[i];
+        }
+    __builtin_amdgcn_wave_barrier();   // (the next heads' writes follow these reads)
   } else {
 #pragma unroll
-    for (int m = 0; m < T16; ++m)
+    for (int b = 0; b < NB; ++b)
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
+      for (int m = 0; m < T16; ++m)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) row[m][g][i] = __shfl(op[m][i], (lane & 15) + 16 * g);
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) row[b][m][g][i] = __shfl(op[b][m][i], (lane & 15) + 16 * g);
   }
-  float sum = 0.f;
+  float sum[NB], mean[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) sum[b] = 0.f;
 #pragma unroll
   for (int m = 0; m < T16; ++m)
 #pragma unroll
-    for (int f = 0; f < 16; ++f) sum += row[m][f >> 2][f & 3];
-  const float mean = sum / (float)A;
+    for (int f = 0; f < 16; ++f)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) sum[b] += row[b][m][f >> 2][f & 3];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) mean[b] = sum[b] / (float)A;
   const int g = lane >> 4;
-  float best = 0.f;
-  int bi = 0;
+  float best[NB];
+  int bi[NB];
 #pragma unroll
   for (int m = 0; m < T16; ++m)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float qa = pad_if(vm, 4 * m + i, (v + o[m][i]) - mean, 0xFF800000u);   // -inf past A
-      // (bitwise & and |: the short-circuit forms compile to exec-mask branches)
-      const bool take = (m == 0 && i == 0) || ((!isnan(best)) & (isnan(qa) | (qa > best)));
-      best = take ? qa : best;
-      bi = take ? 16 * m + 4 * g + i : bi;
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const float qa = pad_if(vm, 4 * m + i, (v + o[b][m][i]) - mean[b], 0xFF800000u);   // -inf past A
+        // (bitwise & and |: the short-circuit forms compile to exec-mask branches)
+        const bool take = (m == 0 && i == 0) || ((!isnan(best[b])) & (isnan(qa) | (qa > best[b])));
+        best[b] = take ? qa : best[b];
+        bi[b] = take ? 16 * m + 4 * g + i : bi[b];
+      }
+#pragma unroll
+  for (int x = 16; x <= 32; x <<= 1)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const float ob = __shfl_xor(best[b], x);
+      const int oi = __shfl_xor(bi[b], x);
+      const bool nm = isnan(best[b]), no = isnan(ob);
+      const bool take = (nm & no) ? oi < bi[b]
+                                  : (no ? true : (nm ? false : ((ob > best[b]) | ((ob == best[b]) & (oi < bi[b])))));
+      best[b] = take ? ob : best[b];
+      bi[b] = take ? oi : bi[b];
     }
 #pragma unroll
-  for (int x = 16; x <= 32; x <<= 1) {
-    const float ob = __shfl_xor(best, x);
-    const int oi = __shfl_xor(bi, x);
-    const bool nm = isnan(best), no = isnan(ob);
-    const bool take = (nm & no) ? oi < bi : (no ? true : (nm ? false : ((ob > best) | ((ob == best) & (oi < bi)))));
-    best = take ? ob : best;
-    bi = take ? oi : bi;
-  }
-  return bi;
+  for (int b = 0; b < NB; ++b) act[b] = bi[b];
 }
 
 template <int AT, bool FLIP, bool BIL>   // AT: the second head layers' outputs in 32-row units, A <= 32 AT
@@ -326,7 +351,11 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
   using Plan = StagePlan<AT>;
   __shared__ __attribute__((aligned(16))) float wbuf[2 * kBufFloats];
   // FLIP: per-wave scratch rows of the dueling epilogue (AT <= 2: 16 KB or 32 KB per block)
-  constexpr int kScr = (FLIP && AT <= 2) ? kWaves * 16 * 16 * T16 : 1;
+  // branch heads of stage S9 wait for the first head stage and are dueled with its heads
+  constexpr int kPend = Plan::kS9Heads > 1 ? Plan::kS9Heads - 1 : 0;
+  constexpr int kNB = kPend + Plan::kHPS;   // heads dueled together at most
+  constexpr int kScrWave = kNB * 16 * (16 * T16 + 4);   // one wave's scratch rows (dueling_argmax)
+  constexpr int kScr = (FLIP && AT <= 2) ? kWaves * kScrWave : 1;
   __shared__ __attribute__((aligned(16))) float escr[kScr];
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4;
@@ -586,82 +615,130 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
     explore = (uint64_t)r0.x < eps_u;
   }
   // head k from its stage buffer: the Linear(32, 64) piece at h1, the Linear(64, A) pieces at h2
-  // and h2 + 32 AT rows; then its output (FLIP: the value or the branch's action)
+  // and h2 + 32 AT rows, into o (raw outputs)
   f32x4 x3[kD3 / 16];
-  auto head = [&](int k, const float* h1, const float* h2) __attribute__((always_inline)) {
+  auto head = [&](int k, const float* h1, const float* h2, f32x4 (&o)[T16]) __attribute__((always_inline)) {
     f32x4 z[kDH / 16];
 #pragma unroll
     for (int m = 0; m < kDH / 16; ++m) z[m] = bias_tile(bsh1 + kDH * k, m, g, kDH);
     mfma_chunk<kDH / 16>(z, h1, lane, x3[0], x3[1]);
 #pragma unroll
     for (int m = 0; m < kDH / 16; ++m) z[m] = leaky(z[m], a.slope);
-    f32x4 o[T16];
 #pragma unroll
     for (int m = 0; m < T16; ++m) o[m] = bias_tile(bsh2 + 32 * AT * k, m, g, 32 * AT);
     mfma_chunk<T16>(o, h2, lane, z[0], z[1]);
     mfma_chunk<T16>(o, h2 + 32 * AT * kPitch, lane, z[2], z[3]);
-    if constexpr (FLIP) {
-      if (k == 0) {
-        v = __shfl(o[0][0], lane & 15);   // value head output 0: register 0 of lane group 0
-      } else {
-        const int b = k - 1;   // branch
-        int act;
-        if (explore) {   // branch b: EXPLORE word b + 1 across calls 0 and 1, onto [0, N]
-          const uint32_t rw = b == 0 ? r0.y : b == 1 ? r0.z : b == 2 ? r0.w : b == 3 ? r1.x
-                            : b == 4 ? r1.y : b == 5 ? r1.z : r1.w;
-          act = (int)__umulhi(rw, (uint32_t)(a.n_nodes + 1));
-        } else {
-          uint32_t vmk = vm;
-          asm volatile("" : "+v"(vmk));   // (per head: hoisted, its selects were SGPR pairs that spilled)
-          act = dueling_argmax<T16, (AT <= 2)>(o, lane, A, vmk, v,
-                                               (AT <= 2) ? escr + (threadIdx.x >> 6) * 16 * 16 * T16 : nullptr);
-        }
-        if (act > 0 && act <= a.n_nodes) {   // a > 0 flips node a - 1, once however often
+  };
+  // !FLIP: head k's raw outputs to heads[k][e][a]
+  auto store_head = [&](int k, const f32x4 (&o)[T16]) __attribute__((always_inline)) {
+    if (!live) return;
+    float* out = a.heads + ((size_t)k * a.n + e) * A;
 #pragma unroll
-          for (int w = 0; w < 4; ++w)
-            if (w == ((act - 1) >> 5)) mk[w] |= 1u << ((act - 1) & 31);
-        }
-        if (a.actions && live && g == 0) a.actions[e * (H - 1) + b] = act;
-      }
-    } else if (live) {
-      float* out = a.heads + ((size_t)k * a.n + e) * A;
+    for (int m = 0; m < T16; ++m) {
 #pragma unroll
-      for (int m = 0; m < T16; ++m) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int act = 16 * m + 4 * g + i;
-          if (act < A) out[act] = o[m][i];
-        }
+      for (int i = 0; i < 4; ++i) {
+        const int act = 16 * m + 4 * g + i;
+        if (act < A) out[act] = o[m][i];
       }
     }
   };
+  // FLIP: the actions of branch heads kk[b] (those >= H skipped) into the flip mask: epsilon-greedy,
+  // EXPLORE word b + 1 across calls 0 and 1 onto [0, N] for an exploring env, else the dueling argmax
+  auto act_heads = [&](auto nb_c, const f32x4 (&o)[decltype(nb_c)::value][T16], const int (&kk)[decltype(nb_c)::value])
+      __attribute__((always_inline)) {
+    constexpr int NB = decltype(nb_c)::value;
+    uint32_t vmk = vm;
+    asm volatile("" : "+v"(vmk));   // (hoisted, its selects were SGPR pairs that spilled)
+    int act[NB];
+    dueling_argmax<T16, NB, (AT <= 2)>(o, lane, A, vmk, v, (AT <= 2) ? escr + (threadIdx.x >> 6) * kScrWave : nullptr,
+                                       act);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      if (kk[b] >= H) continue;
+      const int br = kk[b] - 1;   // branch
+      const uint32_t rw = br == 0 ? r0.y : br == 1 ? r0.z : br == 2 ? r0.w : br == 3 ? r1.x
+                        : br == 4 ? r1.y : br == 5 ? r1.z : r1.w;
+      const int ac = explore ? (int)__umulhi(rw, (uint32_t)(a.n_nodes + 1)) : act[b];
+      if (ac > 0 && ac <= a.n_nodes) {   // a > 0 flips node a - 1, once however often
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+          if (w == ((ac - 1) >> 5)) mk[w] |= 1u << ((ac - 1) & 31);
+      }
+      if (a.actions && live && g == 0) a.actions[e * (H - 1) + br] = ac;
+    }
+  };
+  f32x4 pend[kPend > 0 ? kPend : 1][T16];   // FLIP: stage S9's branch heads, dueled later
 
-  // ---- Linear(64, 32) (stage 9, with head 0 when it fits)
+  // ---- Linear(64, 32) (stage S9, with the heads that fit beside it)
 #pragma unroll
   for (int m = 0; m < kD3 / 16; ++m) x3[m] = bias_tile(bs3, m, g, kD3);
-  auto stage9 = [&](const float* buf) __attribute__((always_inline)) {
+  auto stage9 = [&](const float* buf, bool last) __attribute__((always_inline)) {
     mfma_chunk<kD3 / 16>(x3, buf, lane, x2[0], x2[1]);
     mfma_chunk<kD3 / 16>(x3, buf + 32 * kPitch, lane, x2[2], x2[3]);
 #pragma unroll
     for (int m = 0; m < kD3 / 16; ++m) x3[m] = leaky(x3[m], a.slope);
 #pragma unroll
-    for (int j = 0; j < Plan::kS9Heads; ++j)
-      if (j < H) head(j, buf + (64 + j * Plan::kHeadRows) * kPitch, buf + (128 + j * Plan::kHeadRows) * kPitch);
-  };
-  // the heads of one head stage (those past H, in the last stage's unused slots, are skipped)
-  auto heads = [&](int k0, const float* buf) __attribute__((always_inline)) {
+    for (int j = 0; j < Plan::kS9Heads; ++j) {
+      if (j >= H) continue;
+      f32x4 o[T16];
+      head(j, buf + (64 + j * Plan::kHeadRows) * kPitch, buf + (128 + j * Plan::kHeadRows) * kPitch, o);
+      if constexpr (!FLIP) {
+        store_head(j, o);
+      } else if (j == 0) {
+        v = __shfl(o[0][0], lane & 15);   // value head output 0: register 0 of lane group 0
+      } else {
 #pragma unroll
-    for (int j = 0; j < Plan::kHPS; ++j)
-      if (k0 + j < H) head(k0 + j, buf + j * Plan::kHeadRows * kPitch, buf + (64 + j * Plan::kHeadRows) * kPitch);
+        for (int m = 0; m < T16; ++m) pend[j - 1][m] = o[m];
+      }
+    }
+    if constexpr (FLIP && kPend > 0) {
+      if (last) {   // no head stage follows
+        int kk[kPend];
+#pragma unroll
+        for (int b = 0; b < kPend; ++b) kk[b] = 1 + b;
+        act_heads(std::integral_constant<int, kPend>{}, pend, kk);
+      }
+    }
+  };
+  // the heads of one head stage (those past H, in the last stage's unused slots, are skipped);
+  // FLIP: dueled together, with stage S9's pending heads in the first head stage
+  auto heads = [&](int k0, const float* buf, bool first) __attribute__((always_inline)) {
+    f32x4 oc[Plan::kHPS][T16];
+#pragma unroll
+    for (int j = 0; j < Plan::kHPS; ++j) {
+      if (k0 + j < H) head(k0 + j, buf + j * Plan::kHeadRows * kPitch, buf + (64 + j * Plan::kHeadRows) * kPitch, oc[j]);
+      if constexpr (!FLIP) {
+        if (k0 + j < H) store_head(k0 + j, oc[j]);
+      }
+    }
+    if constexpr (FLIP) {
+      if (kPend > 0 && first) {
+        f32x4 ob[kNB][T16];
+        int kk[kNB];
+#pragma unroll
+        for (int b = 0; b < kNB; ++b) {
+#pragma unroll
+          for (int m = 0; m < T16; ++m) ob[b][m] = b < kPend ? pend[b < kPend ? b : 0][m] : oc[b < kPend ? 0 : b - kPend][m];
+          kk[b] = b < kPend ? 1 + b : k0 + b - kPend;
+        }
+        act_heads(std::integral_constant<int, kNB>{}, ob, kk);
+      } else {
+        int kk[Plan::kHPS];
+#pragma unroll
+        for (int j = 0; j < Plan::kHPS; ++j) kk[j] = k0 + j;
+        act_heads(std::integral_constant<int, Plan::kHPS>{}, oc, kk);
+      }
+    }
   };
   if (n_stages > Plan::kFirstHeadStage)
-    PBN_STAGE(Plan::kS9Stage, kHead, Plan::kS9Heads, Plan::kHeadPasses, { stage9(buf); });
+    PBN_STAGE(Plan::kS9Stage, kHead, Plan::kS9Heads, Plan::kHeadPasses, { stage9(buf, false); });
   else
-    PBN_STAGE(Plan::kS9Stage, kHead, 0, 0, { stage9(buf); });
+    PBN_STAGE(Plan::kS9Stage, kHead, 0, 0, { stage9(buf, true); });
   for (int s = Plan::kFirstHeadStage; s < n_stages; ++s) {
     const int k0 = Plan::kS9Heads + (s - Plan::kFirstHeadStage) * Plan::kHPS;
-    if (s + 1 < n_stages) PBN_STAGE(s, kHead, k0 + Plan::kHPS, Plan::kHeadPasses, { heads(k0, buf); });
-    else PBN_STAGE(s, kHead, 0, 0, { heads(k0, buf); });
+    const bool first = s == Plan::kFirstHeadStage;
+    if (s + 1 < n_stages) PBN_STAGE(s, kHead, k0 + Plan::kHPS, Plan::kHeadPasses, { heads(k0, buf, first); });
+    else PBN_STAGE(s, kHead, 0, 0, { heads(k0, buf, first); });
   }
   if constexpr (FLIP) {
     if (live && g == 0) {
