@@ -339,8 +339,10 @@ int pbn_qnet_flipmask(const pbn_net* net, uint64_t seed, uint64_t step, const ui
  * d_target, d_T, d_b0 = the layer's bias [256], out_dim 256) followed by those of the function
  * it extends.  d_T here is pbn_bilinear_targets' table with every 256-output row stored as 16 x 16
  * transposed (ABI 5): float [n_attr][n_nodes][16][16], element [a][i][j][q] = T[a][i][16 q + j]
- * (a lane's 16 MFMA operands of one node are contiguous); d_T and d_b0 16-byte aligned.  Each block sorts its envs by target, so a wave's 16 envs share one or two
- * targets' tables, and the layer runs on the MFMAs (k = node, 0/1 state bits as the B operand);
+ * (a lane's 16 MFMA operands of one node are contiguous); d_T and d_b0 16-byte aligned.  The
+ * envs are sorted by target within domains of 1,024 (each block takes its 128-env slice of its
+ * domain's order), so a wave's 16 envs mostly share one target's table, and the layer runs on the
+ * MFMAs (k = node, 0/1 state bits as the B operand);
  * its sums are exact f32 but grouped differently from pbn_bilinear_targets' sequential adds:
  * compare with a tolerance.  This is config 5's acting frame in one launch before pbn_step.
  */

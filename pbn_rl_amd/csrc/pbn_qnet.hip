@@ -365,7 +365,8 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
   const int n_stages = Plan::kFirstHeadStage + (H - Plan::kS9Heads + Plan::kHPS - 1) / Plan::kHPS;
   PBN_QSTAMP(0);
   // this lane's env: the wave's 16 envs in order (y input), or (BIL) the wave's 16 of the block's
-  // envs stably sorted by target, so that a wave's envs share one or two targets' tables
+  // slice of its sort domain's envs stably sorted by target, so that a wave's envs share one target's
+  // table (sometimes two)
   int64_t e;
   bool live;
   int key = 0;   // BIL: target id, n_attr = none, 255 = past the end
@@ -374,44 +375,65 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
     live = e0 < a.n;   // (a wave past the end still stages weights and meets the barriers)
     e = live ? e0 + (lane & 15) : 0;
   } else {
-    __shared__ uint8_t skey[kWaves * kEnvs];
-    __shared__ uint8_t sperm[kWaves * kEnvs];
-    __shared__ uint16_t wcnt[2][256];   // keys per sorting wave (waves 0, 1 hold one key per lane)
-    __shared__ uint16_t kbase[256];     // keys below, block-wide (exclusive prefix)
-    static_assert(kWaves * kEnvs == 128, "the block's keys are the lanes of waves 0 and 1");
-    const int64_t eb = (int64_t)blockIdx.x * kWaves * kEnvs;
+    // Sort domain: the kDom envs of kDom / 128 consecutive blocks.  Every block of a domain sorts
+    // the domain's keys (stable counting sort) and takes its own 128-env slice of the order: a
+    // target's run is then ~kDom / A envs long (73 at Bittner-28's 14 targets), so most waves hold
+    // one target (1.2 bilinear passes per wave on average, against 2.75 when each block sorted its
+    // own 128).  The sort's LDS is the second weight buffer's, first written by stage 1's loads.
+    constexpr int kDom = 1024, kChunks = kDom / 64, kSlices = kDom / (kWaves * kEnvs);
+    static_assert(kWaves * 64 * 2 == kDom, "two keys per thread");
+    static_assert(kDom + 2 * kDom + 2 * kChunks * 256 + 2 * 256 <= 4 * kBufFloats, "sort LDS");
+    uint8_t* const skey = reinterpret_cast<uint8_t*>(wbuf + kBufFloats);   // [kDom]
+    uint16_t* const sperm = reinterpret_cast<uint16_t*>(skey + kDom);        // [kDom]
+    uint16_t* const wcnt = sperm + kDom;     // [kChunks][256]: keys per 64-key chunk, then their prefix
+    uint16_t* const kbase = wcnt + kChunks * 256;   // [256]: key totals, then keys below
+    const int64_t d0 = (int64_t)(blockIdx.x / kSlices) * kDom;
+    const int slice = (int)(blockIdx.x % kSlices);
     const int tt = threadIdx.x;
     const int wv = tt >> 6;
-    if (tt < 256) reinterpret_cast<uint32_t*>(&wcnt[0][0])[tt] = 0u;
-    int k = 255, rank = 0;
-    if (tt < kWaves * kEnvs) {
-      const bool lv = eb + tt < a.n;
-      const uint32_t tg = lv ? (uint32_t)a.target[eb + tt] : 255u;
-      k = lv ? (int)(tg < (uint32_t)a.n_attr ? tg : (uint32_t)a.n_attr) : 255;
-      skey[tt] = (uint8_t)k;
+    for (int i = tt; i < kChunks * 128; i += 64 * kWaves) reinterpret_cast<uint32_t*>(wcnt)[i] = 0u;
+    int kq[2], rank[2] = {0, 0};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {   // keys tt and 512 + tt: chunks wv and kWaves + wv
+      const int i = h * 64 * kWaves + tt;
+      const bool lv = d0 + i < a.n;
+      const uint32_t tg = lv ? (uint32_t)a.target[d0 + i] : 255u;
+      kq[h] = lv ? (int)(tg < (uint32_t)a.n_attr ? tg : (uint32_t)a.n_attr) : 255;
+      skey[i] = (uint8_t)kq[h];
     }
     __syncthreads();
-    // stable counting sort in three barriers: each of waves 0, 1 ranks its lanes among equal keys
-    // (one ballot per distinct key of the wave) and counts them; wave 0 scans the counts; every
-    // key's position = keys below + equal keys in wave 0 (for wave 1) + equal keys on lower lanes
-    if (wv < 2) {
+    // rank among equal keys of the chunk (one ballot per distinct key) and the chunk's counts
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = kq[h], c = h * kWaves + wv;
       uint64_t rem = __ballot(1);
       while (rem) {
         const int l = __builtin_ctzll(rem);
         const int kk = __builtin_amdgcn_readlane(k, l);
         const uint64_t m = __ballot(k == kk);
-        if (k == kk) rank = __builtin_popcountll(m & ((1ull << lane) - 1ull));
-        if (lane == l) wcnt[wv][kk] = (uint16_t)__builtin_popcountll(m);
+        if (k == kk) rank[h] = __builtin_popcountll(m & ((1ull << lane) - 1ull));
+        if (lane == l) wcnt[c * 256 + kk] = (uint16_t)__builtin_popcountll(m);
         rem &= ~m;
       }
     }
     __syncthreads();
+    if (tt < 256) {   // per key: exclusive prefix over the chunks, in place; the key's total
+      int run = 0;
+#pragma unroll
+      for (int c = 0; c < kChunks; ++c) {
+        const int v = wcnt[c * 256 + tt];
+        wcnt[c * 256 + tt] = (uint16_t)run;
+        run += v;
+      }
+      kbase[tt] = (uint16_t)run;
+    }
+    __syncthreads();
     if (wv == 0) {   // exclusive prefix over the 256 keys: four per lane, then across lanes
-      int c[4], tot = 0;
+      int c4[4], tot = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        c[j] = tot;
-        tot += (int)wcnt[0][4 * lane + j] + (int)wcnt[1][4 * lane + j];
+        c4[j] = tot;
+        tot += (int)kbase[4 * lane + j];
       }
       int inc = tot;
 #pragma unroll
@@ -420,16 +442,20 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
         inc += lane >= d ? y : 0;
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) kbase[4 * lane + j] = (uint16_t)(inc - tot + c[j]);
+      for (int j = 0; j < 4; ++j) kbase[4 * lane + j] = (uint16_t)(inc - tot + c4[j]);
     }
     __syncthreads();
-    if (tt < kWaves * kEnvs) sperm[(int)kbase[k] + (wv == 1 ? (int)wcnt[0][k] : 0) + rank] = (uint8_t)tt;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = kq[h], c = h * kWaves + wv;
+      sperm[(int)kbase[k] + (int)wcnt[c * 256 + k] + rank[h]] = (uint16_t)(h * 64 * kWaves + tt);
+    }
     __syncthreads();
     PBN_QSTAMP(1);
-    const int li = sperm[(threadIdx.x >> 6) * kEnvs + (lane & 15)];
+    const int li = sperm[slice * kWaves * kEnvs + (threadIdx.x >> 6) * kEnvs + (lane & 15)];
     key = skey[li];
     live = key != 255;
-    e = live ? eb + li : 0;
+    e = live ? d0 + li : 0;
   }
 
   const int t = threadIdx.x;
