@@ -72,7 +72,9 @@ struct QnetArgs {
 
 // Diagnostic phase clocks (tools/qnet_stamps.py): lane 0 of every wave stores s_memtime at
 // 0 entry, 1 after the block's target sort, 2 after the bilinear layer, 3 stage 0 in LDS, and for
-// stage s at 4 + 3 s (its MFMA body starts), 5 + 3 s (body done), 6 + 3 s (past its barrier)
+// stage s at 4 + 3 s (its MFMA body starts), 5 + 3 s (body done), 6 + 3 s (past its barrier);
+// inside the sort 57 keys stored, 58 past the barrier, 59 ranked, 60 past the barrier, 61 chunk
+// prefixes, 62 key prefix
 constexpr int kQStampRow = 64;
 #ifdef PBN_STAMPS
 #define PBN_QSTAMP(i)                                                                                       \
@@ -385,7 +387,7 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
     static_assert(kDom + 2 * kDom + 2 * kChunks * 256 + 2 * 256 <= 4 * kBufFloats, "sort LDS");
     uint8_t* const skey = reinterpret_cast<uint8_t*>(wbuf + kBufFloats);   // [kDom]
     uint16_t* const sperm = reinterpret_cast<uint16_t*>(skey + kDom);        // [kDom]
-    uint16_t* const wcnt = sperm + kDom;     // [kChunks][256]: keys per 64-key chunk, then their prefix
+    uint16_t* const wcnt = sperm + kDom;     // [256][kChunks]: keys per 64-key chunk, then their prefix
     uint16_t* const kbase = wcnt + kChunks * 256;   // [256]: key totals, then keys below
     const int64_t d0 = (int64_t)(blockIdx.x / kSlices) * kDom;
     const int slice = (int)(blockIdx.x % kSlices);
@@ -401,33 +403,49 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
       kq[h] = lv ? (int)(tg < (uint32_t)a.n_attr ? tg : (uint32_t)a.n_attr) : 255;
       skey[i] = (uint8_t)kq[h];
     }
+    PBN_QSTAMP(57);
     __syncthreads();
-    // rank among equal keys of the chunk (one ballot per distinct key) and the chunk's counts
+    PBN_QSTAMP(58);
+    // rank among equal keys of the chunk and the chunk's counts: the lanes with an equal key are the
+    // AND over the 8 key bits of ballot(bit) or its complement (8 ballots per key, where one ballot
+    // per distinct key took a serial scalar loop: 4,500 cycles at 15 keys)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int k = kq[h], c = h * kWaves + wv;
-      uint64_t rem = __ballot(1);
-      while (rem) {
-        const int l = __builtin_ctzll(rem);
-        const int kk = __builtin_amdgcn_readlane(k, l);
-        const uint64_t m = __ballot(k == kk);
-        if (k == kk) rank[h] = __builtin_popcountll(m & ((1ull << lane) - 1ull));
-        if (lane == l) wcnt[c * 256 + kk] = (uint16_t)__builtin_popcountll(m);
-        rem &= ~m;
-      }
-    }
-    __syncthreads();
-    if (tt < 256) {   // per key: exclusive prefix over the chunks, in place; the key's total
-      int run = 0;
+      uint64_t eq = ~0ull;
 #pragma unroll
-      for (int c = 0; c < kChunks; ++c) {
-        const int v = wcnt[c * 256 + tt];
-        wcnt[c * 256 + tt] = (uint16_t)run;
-        run += v;
+      for (int b = 0; b < 8; ++b) {
+        const bool bit = (k >> b) & 1;
+        const uint64_t bl = __ballot(bit);
+        eq &= bit ? bl : ~bl;
       }
+      rank[h] = __builtin_popcountll(eq & ((1ull << lane) - 1ull));
+      if ((eq & ~((2ull << lane) - 1ull)) == 0ull)   // the last lane of its key
+        wcnt[k * kChunks + c] = (uint16_t)__builtin_popcountll(eq);
+    }
+    PBN_QSTAMP(59);
+    __syncthreads();
+    PBN_QSTAMP(60);
+    if (tt < 256) {   // per key: exclusive prefix over the chunks, in place (its 16 counts are two
+                      // 16-byte words); the key's total
+      static_assert(kChunks == 16, "two uint4 of uint16 counts per key");
+      uint4* const row = reinterpret_cast<uint4*>(wcnt + tt * kChunks);
+      const uint4 q0 = row[0], q1 = row[1];
+      const uint32_t in[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+      uint32_t outw[8];
+      uint32_t run = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t lo = in[j] & 0xFFFFu, hi = in[j] >> 16;
+        outw[j] = run | ((run + lo) << 16);
+        run += lo + hi;
+      }
+      row[0] = make_uint4(outw[0], outw[1], outw[2], outw[3]);
+      row[1] = make_uint4(outw[4], outw[5], outw[6], outw[7]);
       kbase[tt] = (uint16_t)run;
     }
     __syncthreads();
+    PBN_QSTAMP(61);
     if (wv == 0) {   // exclusive prefix over the 256 keys: four per lane, then across lanes
       int c4[4], tot = 0;
 #pragma unroll
@@ -445,10 +463,11 @@ __global__ void __launch_bounds__(64 * kWaves) qnet_tail_kernel(QnetArgs a) {
       for (int j = 0; j < 4; ++j) kbase[4 * lane + j] = (uint16_t)(inc - tot + c4[j]);
     }
     __syncthreads();
+    PBN_QSTAMP(62);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int k = kq[h], c = h * kWaves + wv;
-      sperm[(int)kbase[k] + (int)wcnt[c * 256 + k] + rank[h]] = (uint16_t)(h * 64 * kWaves + tt);
+      sperm[(int)kbase[k] + (int)wcnt[k * kChunks + c] + rank[h]] = (uint16_t)(h * 64 * kWaves + tt);
     }
     __syncthreads();
     PBN_QSTAMP(1);

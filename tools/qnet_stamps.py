@@ -57,7 +57,14 @@ def main():
     torch.cuda.synchronize()
     L.pbn_debug_set_qnet_stamps(None)
     s = buf.view(waves, ROW).cpu().numpy().astype(np.int64)
-    used = [i for i in range(ROW) if np.all(s[:, i] > 0)]
+    sub = [57, 58, 59, 60, 61, 62]   # the sort's inner clocks (pbn_qnet.hip PBN_QSTAMP 57-62)
+    sort_detail = {}
+    if all(np.all(s[:, i] > 0) for i in sub):
+        names = ["keys loaded", "barrier", "ballot ranks", "barrier", "chunk prefixes + barrier",
+                 "key prefix + barrier", "permutation + barrier"]
+        pts = [0] + sub + [1]
+        sort_detail = {names[j]: int(np.median(s[:, pts[j + 1]] - s[:, pts[j]])) for j in range(len(pts) - 1)}
+    used = [i for i in range(ROW) if np.all(s[:, i] > 0) and i not in sub]
     n_stages = (max(used) - 3) // 3
     med = lambda x: int(np.median(x))
     span = s[:, max(used)] - s[:, 0]
@@ -75,6 +82,7 @@ def main():
            "store+barrier": sum(v["cycles"] for k, v in out["phases"].items() if k.endswith("barrier")),
            "fetch issue": sum(v["cycles"] for k, v in out["phases"].items() if k.endswith("issue"))}
     out["totals"] = tot
+    out["sort_detail"] = sort_detail
     print(json.dumps(out, indent=1))
 
 
