@@ -12,7 +12,7 @@
 #   8m               pbn28 x 8,388,608 envs, 200 steps
 #   pbn70            config 3: pbn70 x 1,048,576 envs, 200 steps
 #   bdq              config 5: the BDQ frame at 32,768 envs (+ kernel trace)
-#   bdq-learn        BDQ training frames at 32,768 envs
+#   bdq-learn        BDQ training frames at 32,768 envs (+ kernel trace)
 #   stamps           the pipelined kernel's per-role segment clocks at iteration 10 (diagnostic build
 #                    pbn_rl_amd/libpbn_env_stamps.so: tools/stamps.py --build), 20- and 100-step launches
 #   qstamps          config 5's Q-network launch per-phase clocks (stamps build; tools/qnet_stamps.py)
@@ -66,7 +66,12 @@ for step in "$@"; do
       timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats --output-format csv \
         -d "$out/bdq_pmc_write" -o run -- python bench.py --workload bdq --no-cpu-baseline > /dev/null 2> "$out/bdq_pmc_write.err" || fail bdqpmc-write
       echo "bdqpmc done" ;;
-    bdq-learn) bench bench_bdq_learn --workload bdq-learn ;;
+    bdq-learn)
+      bench bench_bdq_learn --workload bdq-learn
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/bdq_learn_trace" -o run -- \
+        python bench.py --workload bdq-learn > "$out/bdq_learn_trace.json" 2> "$out/bdq_learn_trace.err" || fail bdq-learn-trace
+      # (every dispatch's row: tens of MB; the stats stay)
+      find "$out/bdq_learn_trace" -name '*kernel_trace.csv' -delete ;;
     stamps)
       for T in 20 100; do
         timeout -k 10 120 python tools/stamps.py --pipe --rollout $T > "$out/stamps_T$T.json" 2> "$out/stamps_T$T.err" \
