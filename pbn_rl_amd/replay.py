@@ -169,9 +169,15 @@ class BDQLearner:
                  batch_size: int = 256, learning_rate: float = 1e-4, gamma: float = 0.999,
                  target_update: int = 10_000, learning_starts: int = 288, updates_per_frame: int = 1,
                  epsilon_start: float = 1.0, epsilon_final: float = 0.0, epsilon_decay: int = 10_000, seed: int = 0,
-                 graphable: bool = False):
+                 graphable: bool = False, blas: Optional[str] = "cublas"):
         if not env.keep_final_state:
             raise ValueError("BDQLearner needs the env's final_state (keep_final_state=True)")
+        if blas:
+            # the update's GEMMs are small (batch 256-512, widths 28-256): rocBLAS ("cublas" in
+            # torch's naming on ROCm) runs the weight-gradient products (K = batch) 2.5-8x faster
+            # than hipBLASLt's picks (tools/learn_profile.py, profiles/r04_z*); this sets the
+            # process-wide preference, None leaves it alone
+            torch.backends.cuda.preferred_blas_library(blas)
         self.env = env
         self.agent = BatchedBDQ(env, qnet)
         self.q = self.agent.q.train()

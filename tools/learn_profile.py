@@ -30,6 +30,8 @@ def main():
     from pbn_rl_amd.vector_env import VectorPBNEnv
 
     dev = torch.device("cuda", 0)
+    if os.environ.get("PBN_BLAS"):   # "cublas" = rocBLAS on ROCm, "cublaslt" = hipBLASLt (torch's default)
+        torch.backends.cuda.preferred_blas_library(os.environ["PBN_BLAS"])
     spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.01, prob_bits=16, horizon=20)
     env = VectorPBNEnv(spec, args.envs, seed=0, device=dev, keep_final_state=True)
     env.reset()
@@ -39,7 +41,7 @@ def main():
     for _ in range(10):
         learner.frame()
     torch.cuda.synchronize()
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
         for _ in range(args.frames):
             learner.frame()
         torch.cuda.synchronize()
@@ -53,8 +55,17 @@ def main():
         rows.append({"op": e.key, "calls_per_frame": e.count / args.frames,
                      "device_us_per_frame": dev_us / args.frames})
     rows.sort(key=lambda r: -r["device_us_per_frame"])
-    print(json.dumps({"frames": args.frames, "envs": args.envs,
-                      "device_us_per_frame": sum(r["device_us_per_frame"] for r in rows), "ops": rows[:60]},
+    gemms = []   # the matrix products by operand shapes
+    for e in prof.key_averages(group_by_input_shape=True):
+        if e.key not in ("aten::mm", "aten::addmm", "aten::bmm", "aten::baddbmm"):
+            continue
+        dev_us = getattr(e, "device_time_total", None) or getattr(e, "cuda_time_total", 0)
+        gemms.append({"op": e.key, "shapes": str(e.input_shapes), "calls_per_frame": e.count / args.frames,
+                      "device_us_per_frame": dev_us / args.frames})
+    gemms.sort(key=lambda r: -r["device_us_per_frame"])
+    print(json.dumps({"frames": args.frames, "envs": args.envs, "blas": str(torch.backends.cuda.preferred_blas_library()),
+                      "device_us_per_frame": sum(r["device_us_per_frame"] for r in rows), "ops": rows[:60],
+                      "gemms": gemms},
                      indent=1))
 
 
