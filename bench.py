@@ -332,6 +332,9 @@ def settle_stats(updates, elapsed_s: float, env_steps: int) -> dict:
     synchronous updates applied per second and their distribution."""
     u = torch.cat([x.reshape(-1) for x in updates]).to(torch.int64)
     total = int(u.sum().item())
+    # the updates the kernel runs per step: a 32-env group (one bit-sliced word) runs to its
+    # slowest env, so its step takes the group's maximum (plus at most one dropped speculation)
+    groups = torch.cat([x.reshape(x.shape[0], -1, 32).amax(-1).reshape(-1) for x in updates]).to(torch.float64)
     hist = torch.bincount(u).cpu().tolist()
     n = u.numel()
     cum, q = 0, {}
@@ -341,6 +344,7 @@ def settle_stats(updates, elapsed_s: float, env_steps: int) -> dict:
             if p not in q and cum >= p * n:
                 q[p] = length
     return {"updates_per_s": total / elapsed_s, "mean_updates_per_env_step": total / n,
+            "mean_group_updates_per_step": float(groups.mean().item()),
             "updates_quantiles": {"p50": q.get(0.5), "p90": q.get(0.9), "p99": q.get(0.99), "max": len(hist) - 1},
             "settle_length_histogram": {str(k): c for k, c in enumerate(hist) if c},
             "env_steps_sampled": n, "env_steps_timed": env_steps,
@@ -528,7 +532,7 @@ def pmc_profile(args, plan):
     launch (tools/pmc_summary.py)."""
     if len(set(plan)) != 1:
         return None, None
-    tail = "_nofinal" if args.no_final_state else ""
+    tail = ("_nofinal" if args.no_final_state else "") + (f"_settle{args.settle}" if args.settle >= 2 else "")
     path = os.path.join(ROOT, "profiles", f"pmc_{args.network}_{args.envs}_{args.mode}_T{plan[0]}{tail}.json")
     if not os.path.exists(path):
         return None, None
@@ -814,7 +818,8 @@ def main():
         elif agent is not None:
             roofline = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                         "traffic": None, "kernel": kernel, "launch_ms": frame_ms,
-                        "note": "training frame (~150 launches): no single dominant kernel is priced"}
+                        "note": "training frame (~170 launches, profiles/r04_u_bdq_learn_trace_kernel_stats.csv): no "
+                                "single dominant kernel is priced"}
         elif rollout_mode:
             per_step = survey_bytes_per_env_step(spec.n)
             bytes_run = env.n_alloc * args.steps * per_step
@@ -901,6 +906,17 @@ def main():
         elif rollout_mode:
             out["config"]["step_law"] = "one synchronous update per env step (SURVEY.md 8(d)'s unit of work)"
         if settle_other is not None:
+            # what one synchronous update costs against one step of the
+            # one-update law (this line's own clock): per group update (the kernel's unit) and per
+            # update an env needs (the group's other envs ride along until its slowest settles)
+            g = settle_other.get("mean_group_updates_per_step")
+            if g:
+                per_group = settle_other["ms_per_step"] / g
+                per_env = settle_other["ms_per_step"] / settle_other["mean_updates_per_env_step"]
+                settle_other["update_cost_vs_one_update_step"] = {
+                    "per_group_update": per_group / (dev_ms / args.steps),
+                    "per_env_update": per_env / (dev_ms / args.steps),
+                    "note": "ms per step / updates per step, over the headline's ms per step"}
             out["settle_law"] = settle_other
         if with_gather is not None:
             out["value_with_gather"] = with_gather["learner"]["value"]

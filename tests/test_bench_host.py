@@ -107,3 +107,16 @@ def test_qnet_tail_flops_count_the_layers_after_the_bilinear():
     macs = 32768 + 8192 + 2048 + 4 * 2048 + 64 + 3 * 64 * 29
     assert bench.qnet_tail_flops_per_env(28, 3) == 2 * macs
     assert bench.qnet_flops_per_env(28, 3) - bench.qnet_tail_flops_per_env(28, 3) == 2 * 28 * 28 * 256
+
+
+def test_settle_stats_group_updates_are_the_group_maximum():
+    """A 32-env group runs to its slowest env: mean_group_updates_per_step is the mean over
+    (step, group) of the group's largest settle length, never below the per-env mean."""
+    import torch
+    u = torch.ones(3, 64, dtype=torch.int16)
+    u[0, 5] = 40          # step 0, group 0
+    u[2, 63] = 7          # step 2, group 1
+    s = bench.settle_stats([u], 1.0, 192)
+    assert s["mean_group_updates_per_step"] == pytest.approx((40 + 1 + 1 + 1 + 1 + 7) / 6)
+    assert s["mean_updates_per_env_step"] == pytest.approx((192 - 2 + 40 + 7) / 192)
+    assert s["updates_quantiles"]["max"] == 40
