@@ -360,6 +360,40 @@ int pbn_qnet_flipmask_from_state(const pbn_net* net, uint64_t seed, uint64_t ste
                                  float epsilon, const float* d_epsilon, uint32_t* d_flipmask, int32_t* d_actions,
                                  void* stream);
 
+/*
+ * One replay batch for the learner's update (pbn_rl_amd/replay.py DeviceReplay), in one launch:
+ * rows d_idx[0..batch) (int64, < capacity) of the ring -- d_state / d_next_state uint32 [W][capacity],
+ * d_target uint8 [capacity], d_action int32 [capacity][n_branches], d_reward float [capacity],
+ * d_done uint8 [capacity] -- into
+ *   d_x       float [2][2 batch][N]: plane 0 = the states (rows 0..batch-1) and next states
+ *             (rows batch..2 batch-1) as 0/1, plane 1 = the first state of each row's target
+ *             attractor (zeros without one), i.e. pbn_obs_unpack of both, concatenated by rows
+ *   d_actions int64 [batch][n_branches], d_rewards float [batch], d_masks float [batch] (= done)
+ */
+int pbn_replay_batch(const pbn_net* net, int64_t batch, const int64_t* d_idx, int64_t capacity,
+                     const uint32_t* d_state, const uint32_t* d_next_state, const uint8_t* d_target,
+                     const int32_t* d_action, int32_t n_branches, const float* d_reward, const uint8_t* d_done,
+                     float* d_x, int64_t* d_actions, float* d_rewards, float* d_masks, void* stream);
+
+/*
+ * The learner's TD loss on raw head outputs (bdq_model/__init__.py:111-126; pbn_rl_amd/replay.py
+ * bdq_update), and its gradient, in one launch:
+ *   d_online  in   float [K+1][2B][A]: the online network's raw head outputs (head 0 = value,
+ *                  output 0) for the batch's states (rows 0..B-1) and next states (rows B..2B-1)
+ *   d_target  in   float [K+1][B][A]: the target network's raw head outputs for the next states
+ *   d_actions in   int64 [B][K], d_rewards float [B], d_masks float [B]
+ *   d_loss    out  float [1]: mean over (b, k) of (r_b + q_T(b, k, a*) gamma m_b - q(b, k, a_bk))^2,
+ *                  q = (v + adv_a) - mean(adv) (the dueling), a* = argmax_a q(B + b, k, a) (first
+ *                  maximum, NaN maximal)
+ *   d_grad    out  float [K+1][2B][A]: d loss / d d_online (0 for rows B.. and the value head's
+ *                  outputs past 0)
+ * batch = B, n_branches = K, n_actions = A.  fp32; the dueling means are sequential sums, so the
+ * values equal PyTorch's to rounding.
+ */
+int pbn_bdq_td_loss(const float* d_online, const float* d_target, const int64_t* d_actions, const float* d_rewards,
+                    const float* d_masks, int32_t batch, int32_t n_branches, int32_t n_actions, float gamma,
+                    float* d_loss, float* d_grad, void* stream);
+
 const char* pbn_last_error(void);
 int pbn_abi_version(void);
 

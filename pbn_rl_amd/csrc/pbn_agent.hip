@@ -360,6 +360,152 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 }  // namespace
 
+// ---- a replay batch in one pass (pbn_replay_batch): rows idx of the ring unpacked into the
+// update's network input x = (2, 2B, N) (plane 0: the states in rows 0..B-1, the next states in
+// rows B..2B-1; plane 1: the target attractor's first state for both), plus the actions as int64,
+// the rewards and the done masks as float.  Replaces three index_selects, two obs unpacks, one
+// concatenation and the five gathers and casts of the scalars.
+__global__ void __launch_bounds__(kObsThreads) replay_batch_kernel(
+    const int64_t* __restrict__ idx, int B, int64_t cap, const uint32_t* __restrict__ st,
+    const uint32_t* __restrict__ nst, const uint8_t* __restrict__ tgt, const int32_t* __restrict__ act, int K,
+    const float* __restrict__ rew, const uint8_t* __restrict__ done, const int32_t* __restrict__ att_start,
+    const uint32_t* __restrict__ att_states, int n_attr, int N, int W, float* __restrict__ x,
+    int64_t* __restrict__ act_out, float* __restrict__ rew_out, float* __restrict__ mask_out) {
+  const int64_t rows = 2 * (int64_t)B;
+  const int64_t total = rows * N;
+  for (int64_t f = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; f < total; f += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = f / N;
+    const int i = (int)(f - r * N);
+    const int b = (int)(r < B ? r : r - B);
+    const int64_t j = idx[b];
+    const uint32_t sw = (r < B ? st : nst)[(size_t)(i >> 5) * cap + j];
+    const uint32_t tg = tgt[j];
+    const uint32_t tw = tg < (uint32_t)n_attr ? att_states[(size_t)att_start[tg] * W + (i >> 5)] : 0u;
+    x[f] = (float)((sw >> (i & 31)) & 1u);
+    x[total + f] = (float)((tw >> (i & 31)) & 1u);
+    if (i == 0 && r < B) {
+      for (int k = 0; k < K; ++k) act_out[(size_t)b * K + k] = (int64_t)act[(size_t)j * K + k];
+      rew_out[b] = rew[j];
+      mask_out[b] = (float)done[j];
+    }
+  }
+}
+
+// ---- the learner's TD loss (bdq_model/__init__.py:111-126, bdq_update in pbn_rl_amd/replay.py)
+// on raw head outputs: one launch where PyTorch runs both duelings, the online argmax, the two
+// gathers, the target, the MSE and their backward (~25 launches at the update's batch).
+// Per (row b, branch k), with heads [K+1][rows][A] (head 0 = value, output 0):
+//   q(h, r, a)  = (v + adv_a) - mean(adv)            the dueling of row r (torch's expression)
+//   current     = q(online, b, a_bk)
+//   a*          = argmax_a q(online, B + b, a)      (first maximum, NaN maximal: torch.argmax)
+//   expected    = r_b + (q(target, b, a*) * gamma) * m_b
+//   loss        = sum (expected - current)^2 / (B K)
+//   d loss / d online[k+1][b][j] = g (j == a_bk) - g / A,  d / d online[0][b][0] = sum_k g,
+//   g = 2 (current - expected) / (B K); every other gradient entry (the rows B.. and the unused
+//   value-head outputs) is 0.
+// One block: the update's B K pairs are a few hundred, and the loss is reduced in a fixed order.
+constexpr int kTdThreads = 1024;
+
+__device__ __forceinline__ float td_mean(const float* __restrict__ adv, int A) {
+  float s = 0.f;
+  for (int j = 0; j < A; ++j) s += adv[j];
+  return s / (float)A;
+}
+
+__global__ void __launch_bounds__(kTdThreads) td_loss_kernel(const float* __restrict__ on, const float* __restrict__ tg,
+                                                             const int64_t* __restrict__ actions,
+                                                             const float* __restrict__ rewards,
+                                                             const float* __restrict__ masks, int B, int K, int A,
+                                                             float gamma, float* __restrict__ loss,
+                                                             float* __restrict__ grad) {
+  __shared__ float red[kTdThreads];
+  __shared__ float gsum[kTdThreads];   // g per pair, for the value head's sum over k
+  const int t = threadIdx.x;
+  const int64_t rows = 2 * (int64_t)B;
+  const int64_t total = (int64_t)(K + 1) * rows * A;
+  for (int64_t i = t; i < total; i += kTdThreads) grad[i] = 0.f;
+  __syncthreads();
+  const float inv_bk = 1.f / (float)(B * K);
+  float acc = 0.f;
+  for (int p = t; p < B * K; p += kTdThreads) {
+    const int b = p / K, k = p - b * K;
+    const float* adv = on + ((size_t)(k + 1) * rows + b) * A;
+    const float v = on[(size_t)b * A];
+    const int a = (int)actions[p];
+    const float current = (v + adv[a]) - td_mean(adv, A);
+    const float* adv2 = on + ((size_t)(k + 1) * rows + B + b) * A;
+    const float v2 = on[(size_t)(B + b) * A];
+    const float m2 = td_mean(adv2, A);
+    float best = (v2 + adv2[0]) - m2;
+    int am = 0;
+    for (int j = 1; j < A; ++j) {
+      const float qj = (v2 + adv2[j]) - m2;
+      const bool take = !isnan(best) && (isnan(qj) || qj > best);
+      best = take ? qj : best;
+      am = take ? j : am;
+    }
+    const float* tadv = tg + ((size_t)(k + 1) * B + b) * A;
+    const float tnext = (tg[(size_t)b * A] + tadv[am]) - td_mean(tadv, A);
+    const float expected = rewards[b] + (tnext * gamma) * masks[b];
+    const float d = expected - current;
+    acc += d * d;
+    const float g = 2.f * (current - expected) * inv_bk;
+    float* gr = grad + ((size_t)(k + 1) * rows + b) * A;
+    const float gA = g / (float)A;
+    for (int j = 0; j < A; ++j) gr[j] = (j == a ? g : 0.f) - gA;
+    if (p < kTdThreads) gsum[p] = g;
+  }
+  red[t] = acc;
+  __syncthreads();
+  for (int w = kTdThreads / 2; w > 0; w >>= 1) {
+    if (t < w) red[t] += red[t + w];
+    __syncthreads();
+  }
+  if (t == 0) loss[0] = red[0] * inv_bk;
+  // the value head: sum over the branches of each row's g (rows whose pairs all fit in the first
+  // kTdThreads pairs; larger batches sum from a second pass below)
+  if (B * K <= kTdThreads) {
+    for (int b = t; b < B; b += kTdThreads) {
+      float s = 0.f;
+      for (int k = 0; k < K; ++k) s += gsum[b * K + k];
+      grad[(size_t)b * A] = s;
+    }
+  }
+}
+
+// the value head's gradient when B K > kTdThreads: every row's g recomputed from the written
+// advantage gradients (g = grad[k+1][b][a] + g / A is not exact, so it is recomputed in full)
+__global__ void td_value_grad_kernel(const float* __restrict__ on, const float* __restrict__ tg,
+                                     const int64_t* __restrict__ actions, const float* __restrict__ rewards,
+                                     const float* __restrict__ masks, int B, int K, int A, float gamma,
+                                     float* __restrict__ grad) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int64_t rows = 2 * (int64_t)B;
+  const float inv_bk = 1.f / (float)(B * K);
+  float s = 0.f;
+  for (int k = 0; k < K; ++k) {
+    const float* adv = on + ((size_t)(k + 1) * rows + b) * A;
+    const float current = (on[(size_t)b * A] + adv[(int)actions[b * K + k]]) - td_mean(adv, A);
+    const float* adv2 = on + ((size_t)(k + 1) * rows + B + b) * A;
+    const float v2 = on[(size_t)(B + b) * A];
+    const float m2 = td_mean(adv2, A);
+    float best = (v2 + adv2[0]) - m2;
+    int am = 0;
+    for (int j = 1; j < A; ++j) {
+      const float qj = (v2 + adv2[j]) - m2;
+      const bool take = !isnan(best) && (isnan(qj) || qj > best);
+      best = take ? qj : best;
+      am = take ? j : am;
+    }
+    const float* tadv = tg + ((size_t)(k + 1) * B + b) * A;
+    const float tnext = (tg[(size_t)b * A] + tadv[am]) - td_mean(tadv, A);
+    const float expected = rewards[b] + (tnext * gamma) * masks[b];
+    s += 2.f * (current - expected) * inv_bk;
+  }
+  grad[(size_t)b * A] = s;
+}
+
 extern "C" {
 
 int pbn_obs_unpack(const pbn_net* net, int64_t n_envs, const uint32_t* d_state, const uint8_t* d_target,
@@ -506,6 +652,47 @@ int pbn_heads_to_flipmask(const pbn_net* net, uint64_t seed, uint64_t step, cons
   if (d_epsilon && ((uintptr_t)d_epsilon & 3u) != 0) return pbn::set_error(PBN_EINVAL, "d_epsilon misaligned");
   return q_to_flipmask_impl(net, seed, step, d_step, env_offset, n_envs, n_branches, n_actions, d_heads, epsilon,
                             d_epsilon, d_flipmask, d_actions, stream, 1);
+}
+
+int pbn_replay_batch(const pbn_net* net, int64_t batch, const int64_t* d_idx, int64_t capacity,
+                     const uint32_t* d_state, const uint32_t* d_next_state, const uint8_t* d_target,
+                     const int32_t* d_action, int32_t n_branches, const float* d_reward, const uint8_t* d_done,
+                     float* d_x, int64_t* d_actions, float* d_rewards, float* d_masks, void* stream) {
+  pbn::NetView v;
+  int rc = pbn::net_view(net, &v);
+  if (rc) return rc;
+  if ((rc = pbn::check_device(net))) return rc;
+  if (batch < 1 || capacity < 1 || n_branches < 1) return pbn::set_error(PBN_EINVAL, "batch, capacity, n_branches >= 1");
+  if (2 * batch * v.n_nodes >= ((int64_t)1 << 31)) return pbn::set_error(PBN_EINVAL, "batch too large");
+  if (!d_idx || !d_state || !d_next_state || !d_target || !d_action || !d_reward || !d_done || !d_x || !d_actions ||
+      !d_rewards || !d_masks)
+    return pbn::set_error(PBN_EINVAL, "null buffer");
+  const int64_t total = 2 * batch * v.n_nodes;
+  const unsigned blocks = (unsigned)std::min<int64_t>((total + kObsThreads - 1) / kObsThreads, 4096);
+  hipLaunchKernelGGL(replay_batch_kernel, dim3(blocks), dim3(kObsThreads), 0, (hipStream_t)stream, d_idx, (int)batch,
+                     capacity, d_state, d_next_state, d_target, d_action, n_branches, d_reward, d_done, v.att_start,
+                     v.att_states, v.n_attr, v.n_nodes, v.W, d_x, d_actions, d_rewards, d_masks);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return pbn::set_error(PBN_EDEVICE, hipGetErrorString(e));
+  return PBN_OK;
+}
+
+int pbn_bdq_td_loss(const float* d_online, const float* d_target, const int64_t* d_actions, const float* d_rewards,
+                    const float* d_masks, int32_t batch, int32_t n_branches, int32_t n_actions, float gamma,
+                    float* d_loss, float* d_grad, void* stream) {
+  if (batch < 1 || n_branches < 1 || n_actions < 1) return pbn::set_error(PBN_EINVAL, "batch, n_branches, n_actions >= 1");
+  if ((int64_t)batch * n_branches > (1 << 24)) return pbn::set_error(PBN_EINVAL, "batch * n_branches too large");
+  if (!d_online || !d_target || !d_actions || !d_rewards || !d_masks || !d_loss || !d_grad)
+    return pbn::set_error(PBN_EINVAL, "null buffer");
+  hipLaunchKernelGGL(td_loss_kernel, dim3(1), dim3(kTdThreads), 0, (hipStream_t)stream, d_online, d_target, d_actions,
+                     d_rewards, d_masks, batch, n_branches, n_actions, gamma, d_loss, d_grad);
+  if (hipGetLastError() != hipSuccess) return pbn::set_error(PBN_EDEVICE, "td_loss_kernel launch failed");
+  if (batch * n_branches > kTdThreads) {
+    hipLaunchKernelGGL(td_value_grad_kernel, dim3((batch + 255) / 256), dim3(256), 0, (hipStream_t)stream, d_online,
+                       d_target, d_actions, d_rewards, d_masks, batch, n_branches, n_actions, gamma, d_grad);
+    if (hipGetLastError() != hipSuccess) return pbn::set_error(PBN_EDEVICE, "td_value_grad_kernel launch failed");
+  }
+  return PBN_OK;
 }
 
 }  // extern "C"

@@ -104,29 +104,31 @@ class DeviceReplay:
         return torch.minimum(idx, size_t - 1)
 
     def gather(self, idx: torch.Tensor, net_handle, stream=None) -> Dict[str, torch.Tensor]:
-        """Rows ``idx`` (B a multiple of 32) as network inputs: obs / next_obs fp32 (2, B, N)
-        (state or next state, and the target attractor's first state), actions (B, K, 1) int64,
+        """Rows ``idx`` (B a multiple of 32) as network inputs, in one launch (``pbn_replay_batch``):
+        x fp32 (2, 2B, N) = obs and next_obs concatenated by rows (obs / next_obs are its halves:
+        state or next state, and the target attractor's first state), actions (B, K, 1) int64,
         rewards (B, 1), masks (B, 1)."""
         B = idx.shape[0]
         if B % 32:
             raise ValueError("batch size must be a multiple of 32")
-        st = self.state.index_select(1, idx).contiguous()
-        nst = self.next_state.index_select(1, idx).contiguous()
-        tg = self.target.index_select(0, idx).contiguous()
         N = net_handle.spec.n
-        obs = torch.empty(2, B, N, dtype=torch.float32, device=self.device)
-        next_obs = torch.empty_like(obs)
+        K = self.action.shape[1]
+        dev = self.device
+        x = torch.empty(2, 2 * B, N, dtype=torch.float32, device=dev)
+        actions = torch.empty(B, K, dtype=torch.int64, device=dev)
+        rewards = torch.empty(B, dtype=torch.float32, device=dev)
+        masks = torch.empty(B, dtype=torch.float32, device=dev)
+        idx = idx.to(torch.int64).contiguous()
         L = _lib.load()
-        s = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
-        with torch.cuda.device(self.device):
-            _lib.check(L.pbn_obs_unpack(net_handle.handle, B, st.data_ptr(), tg.data_ptr(), obs.data_ptr(), s),
-                       "pbn_obs_unpack")
-            _lib.check(L.pbn_obs_unpack(net_handle.handle, B, nst.data_ptr(), tg.data_ptr(), next_obs.data_ptr(), s),
-                       "pbn_obs_unpack")
-        return {"obs": obs, "next_obs": next_obs,
-                "actions": self.action.index_select(0, idx).long().unsqueeze(-1),
-                "rewards": self.reward.index_select(0, idx).reshape(-1, 1),
-                "masks": self.done.index_select(0, idx).float().reshape(-1, 1)}
+        s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+        with torch.cuda.device(dev):
+            _lib.check(L.pbn_replay_batch(net_handle.handle, B, idx.data_ptr(), self.capacity, self.state.data_ptr(),
+                                          self.next_state.data_ptr(), self.target.data_ptr(), self.action.data_ptr(),
+                                          K, self.reward.data_ptr(), self.done.data_ptr(), x.data_ptr(),
+                                          actions.data_ptr(), rewards.data_ptr(), masks.data_ptr(), s),
+                       "pbn_replay_batch")
+        return {"x": x, "obs": x[:, :B], "next_obs": x[:, B:], "actions": actions.unsqueeze(-1),
+                "rewards": rewards.reshape(-1, 1), "masks": masks.reshape(-1, 1)}
 
 
 @torch.no_grad()
@@ -136,19 +138,55 @@ def soft_update(target: torch.nn.Module, online: torch.nn.Module) -> None:
         t.div_(2).add_(o / 2)
 
 
+class _TDLoss(torch.autograd.Function):
+    """pbn_bdq_td_loss: the TD loss of bdq_update on raw head outputs and its gradient in one HIP
+    launch (forward computes both; backward scales the stored gradient)."""
+
+    @staticmethod
+    def forward(ctx, online, target_heads, actions, rewards, masks, gamma):
+        H, rows, A = online.shape
+        B = rows // 2
+        loss = torch.empty(1, dtype=torch.float32, device=online.device)
+        grad = torch.empty_like(online)
+        L = _lib.load()
+        with torch.cuda.device(online.device):
+            _lib.check(L.pbn_bdq_td_loss(online.data_ptr(), target_heads.data_ptr(), actions.data_ptr(),
+                                         rewards.data_ptr(), masks.data_ptr(), B, H - 1, A, float(gamma),
+                                         loss.data_ptr(), grad.data_ptr(),
+                                         torch.cuda.current_stream(online.device).cuda_stream), "pbn_bdq_td_loss")
+        ctx.save_for_backward(grad)
+        return loss[0]
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        (grad,) = ctx.saved_tensors
+        return grad * grad_out, None, None, None, None, None
+
+
 def bdq_update(q: torch.nn.Module, target: torch.nn.Module, opt: torch.optim.Optimizer, batch: Dict[str, torch.Tensor],
                gamma: float = 0.999, grad_clamp: float = 1.0) -> torch.Tensor:
-    """One update_policy step (bdq_model/__init__.py:111-131) on a gathered batch; returns the loss."""
+    """One update_policy step (bdq_model/__init__.py:111-131) on a gathered batch; returns the loss.
+    On the GPU the duelings, the double-DQN target, the MSE and their backward run as one HIP
+    launch on the raw head outputs (``pbn_bdq_td_loss``); elsewhere (CPU tensors) as PyTorch
+    expressions."""
     # q(obs) and q(next_obs) as one forward over 2B rows (half the launches; only the first
     # half carries gradient)
     B = batch["obs"].shape[1]
-    q_all = q(torch.cat([batch["obs"], batch["next_obs"]], 1))          # (2B, K, A)
-    current = q_all[:B].gather(2, batch["actions"]).squeeze(-1)         # (B, K)
-    with torch.no_grad():
-        argmax = torch.argmax(q_all[B:].detach(), dim=2)
-        max_next = target(batch["next_obs"]).gather(2, argmax.unsqueeze(2)).squeeze(-1)
-    expected = batch["rewards"] + max_next * gamma * batch["masks"]
-    loss = F.mse_loss(expected, current)
+    x = batch["x"] if "x" in batch else torch.cat([batch["obs"], batch["next_obs"]], 1)
+    if x.is_cuda and isinstance(q, BranchingQNetwork) and isinstance(target, BranchingQNetwork):
+        heads = q.forward_heads(q.model[0](x))                          # (K+1, 2B, A), raw
+        with torch.no_grad():
+            t_heads = target.forward_heads(target.model[0](batch["next_obs"])).contiguous()   # (K+1, B, A)
+        loss = _TDLoss.apply(heads.contiguous(), t_heads, batch["actions"].reshape(B, -1).contiguous(),
+                             batch["rewards"].reshape(B).contiguous(), batch["masks"].reshape(B).contiguous(), gamma)
+    else:
+        q_all = q(x)                                                    # (2B, K, A)
+        current = q_all[:B].gather(2, batch["actions"]).squeeze(-1)     # (B, K)
+        with torch.no_grad():
+            argmax = torch.argmax(q_all[B:].detach(), dim=2)
+            max_next = target(batch["next_obs"]).gather(2, argmax.unsqueeze(2)).squeeze(-1)
+        expected = batch["rewards"] + max_next * gamma * batch["masks"]
+        loss = F.mse_loss(expected, current)
     opt.zero_grad()
     loss.backward()
     grads = [p.grad for p in q.parameters() if p.grad is not None]
