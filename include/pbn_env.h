@@ -387,12 +387,14 @@ int pbn_replay_batch(const pbn_net* net, int64_t batch, const int64_t* d_idx, in
  *                  maximum, NaN maximal)
  *   d_grad    out  float [K+1][2B][A]: d loss / d d_online (0 for rows B.. and the value head's
  *                  outputs past 0)
- * batch = B, n_branches = K, n_actions = A.  fp32; the dueling means are sequential sums, so the
- * values equal PyTorch's to rounding.
+ *   d_scratch      float [ceil(B / 8)]: per-block partial sums of the loss
+ * batch = B, n_branches = K (1..7), n_actions = A (1..128).  fp32; the dueling means are
+ * sequential sums, so the values equal PyTorch's to rounding.  Two launches (the pass over the
+ * rows, then the partial sums added in order).
  */
 int pbn_bdq_td_loss(const float* d_online, const float* d_target, const int64_t* d_actions, const float* d_rewards,
                     const float* d_masks, int32_t batch, int32_t n_branches, int32_t n_actions, float gamma,
-                    float* d_loss, float* d_grad, void* stream);
+                    float* d_loss, float* d_grad, float* d_scratch, void* stream);
 
 const char* pbn_last_error(void);
 int pbn_abi_version(void);

@@ -125,7 +125,7 @@ def load() -> ctypes.CDLL:
     L.pbn_replay_batch.argtypes = [vp, i64, vp, i64, vp, vp, vp, vp, ctypes.c_int32, vp, vp, vp, vp, vp, vp, vp]
     L.pbn_replay_batch.restype = ctypes.c_int
     L.pbn_bdq_td_loss.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_float,
-                                  vp, vp, vp]
+                                  vp, vp, vp, vp]
     L.pbn_bdq_td_loss.restype = ctypes.c_int
     L.pbn_abi_version.argtypes = []
     L.pbn_abi_version.restype = ctypes.c_int

@@ -392,7 +392,7 @@ __global__ void __launch_bounds__(kObsThreads) replay_batch_kernel(
 }
 
 // ---- the learner's TD loss (bdq_model/__init__.py:111-126, bdq_update in pbn_rl_amd/replay.py)
-// on raw head outputs: one launch where PyTorch runs both duelings, the online argmax, the two
+// on raw head outputs: one pass where PyTorch runs both duelings, the online argmax, the two
 // gathers, the target, the MSE and their backward (~25 launches at the update's batch).
 // Per (row b, branch k), with heads [K+1][rows][A] (head 0 = value, output 0):
 //   q(h, r, a)  = (v + adv_a) - mean(adv)            the dueling of row r (torch's expression)
@@ -403,8 +403,12 @@ __global__ void __launch_bounds__(kObsThreads) replay_batch_kernel(
 //   d loss / d online[k+1][b][j] = g (j == a_bk) - g / A,  d / d online[0][b][0] = sum_k g,
 //   g = 2 (current - expected) / (B K); every other gradient entry (the rows B.. and the unused
 //   value-head outputs) is 0.
-// One block: the update's B K pairs are a few hundred, and the loss is reduced in a fixed order.
-constexpr int kTdThreads = 1024;
+// A block takes kTdRows rows: their head rows (online states, online next states, target) come
+// into LDS with coalesced loads, one thread per (row, branch) pair does the arithmetic from LDS,
+// and the block writes its gradient rows and one partial sum; a second one-block launch adds the
+// partial sums in block order (fixed order: the loss is reproducible).
+constexpr int kTdRows = 8;
+constexpr int kTdThreads = 256;
 
 __device__ __forceinline__ float td_mean(const float* __restrict__ adv, int A) {
   float s = 0.f;
@@ -416,25 +420,37 @@ __global__ void __launch_bounds__(kTdThreads) td_loss_kernel(const float* __rest
                                                              const int64_t* __restrict__ actions,
                                                              const float* __restrict__ rewards,
                                                              const float* __restrict__ masks, int B, int K, int A,
-                                                             float gamma, float* __restrict__ loss,
+                                                             float gamma, float* __restrict__ partial,
                                                              float* __restrict__ grad) {
-  __shared__ float red[kTdThreads];
-  __shared__ float gsum[kTdThreads];   // g per pair, for the value head's sum over k
-  const int t = threadIdx.x;
+  extern __shared__ float sm[];
+  const int H = K + 1;
+  const int R = kTdRows;
+  const int b0 = blockIdx.x * R;
+  const int nr = min(R, B - b0);
   const int64_t rows = 2 * (int64_t)B;
-  const int64_t total = (int64_t)(K + 1) * rows * A;
-  for (int64_t i = t; i < total; i += kTdThreads) grad[i] = 0.f;
+  float* so = sm;                              // [H][2][R][A]: online rows b0.. and B + b0..
+  float* st = so + (size_t)H * 2 * R * A;      // [H][R][A]: target rows b0..
+  float* sg = st + (size_t)H * R * A;          // [R][K]: g per pair
+  float* sd = sg + R * K;                      // [R][K]: (expected - current)^2 per pair
+  const int t = threadIdx.x;
+  const int per = nr * A;                      // floats of one head's block of rows
+  for (int h = 0; h < H; ++h) {
+    for (int i = t; i < per; i += kTdThreads) {
+      so[((size_t)h * 2 + 0) * R * A + i] = on[((size_t)h * rows + b0) * A + i];
+      so[((size_t)h * 2 + 1) * R * A + i] = on[((size_t)h * rows + B + b0) * A + i];
+      st[(size_t)h * R * A + i] = tg[((size_t)h * B + b0) * A + i];
+    }
+  }
   __syncthreads();
   const float inv_bk = 1.f / (float)(B * K);
-  float acc = 0.f;
-  for (int p = t; p < B * K; p += kTdThreads) {
-    const int b = p / K, k = p - b * K;
-    const float* adv = on + ((size_t)(k + 1) * rows + b) * A;
-    const float v = on[(size_t)b * A];
-    const int a = (int)actions[p];
+  if (t < nr * K) {
+    const int r = t / K, k = t - r * K, b = b0 + r;
+    const float* adv = so + ((size_t)(k + 1) * 2 + 0) * R * A + (size_t)r * A;
+    const float v = so[(size_t)r * A];
+    const int a = (int)actions[(size_t)b * K + k];
     const float current = (v + adv[a]) - td_mean(adv, A);
-    const float* adv2 = on + ((size_t)(k + 1) * rows + B + b) * A;
-    const float v2 = on[(size_t)(B + b) * A];
+    const float* adv2 = so + ((size_t)(k + 1) * 2 + 1) * R * A + (size_t)r * A;
+    const float v2 = so[(size_t)R * A + (size_t)r * A];
     const float m2 = td_mean(adv2, A);
     float best = (v2 + adv2[0]) - m2;
     int am = 0;
@@ -444,66 +460,46 @@ __global__ void __launch_bounds__(kTdThreads) td_loss_kernel(const float* __rest
       best = take ? qj : best;
       am = take ? j : am;
     }
-    const float* tadv = tg + ((size_t)(k + 1) * B + b) * A;
-    const float tnext = (tg[(size_t)b * A] + tadv[am]) - td_mean(tadv, A);
+    const float* tadv = st + (size_t)(k + 1) * R * A + (size_t)r * A;
+    const float tnext = (st[(size_t)r * A] + tadv[am]) - td_mean(tadv, A);
     const float expected = rewards[b] + (tnext * gamma) * masks[b];
     const float d = expected - current;
-    acc += d * d;
-    const float g = 2.f * (current - expected) * inv_bk;
-    float* gr = grad + ((size_t)(k + 1) * rows + b) * A;
-    const float gA = g / (float)A;
-    for (int j = 0; j < A; ++j) gr[j] = (j == a ? g : 0.f) - gA;
-    if (p < kTdThreads) gsum[p] = g;
+    sd[t] = d * d;
+    sg[t] = 2.f * (current - expected) * inv_bk;
   }
-  red[t] = acc;
   __syncthreads();
-  for (int w = kTdThreads / 2; w > 0; w >>= 1) {
-    if (t < w) red[t] += red[t + w];
-    __syncthreads();
-  }
-  if (t == 0) loss[0] = red[0] * inv_bk;
-  // the value head: sum over the branches of each row's g (rows whose pairs all fit in the first
-  // kTdThreads pairs; larger batches sum from a second pass below)
-  if (B * K <= kTdThreads) {
-    for (int b = t; b < B; b += kTdThreads) {
-      float s = 0.f;
-      for (int k = 0; k < K; ++k) s += gsum[b * K + k];
-      grad[(size_t)b * A] = s;
+  // gradient rows of this block, row-major and coalesced: head h, first-half row b0 + r, then the
+  // second half's rows (zeros)
+  for (int h = 0; h < H; ++h) {
+    for (int i = t; i < per; i += kTdThreads) {
+      const int r = i / A, j = i - r * A;
+      float gv;
+      if (h == 0) {
+        float s = 0.f;
+        for (int k = 0; k < K; ++k) s += sg[r * K + k];
+        gv = j == 0 ? s : 0.f;
+      } else {
+        const float g = sg[r * K + h - 1];
+        gv = (j == (int)actions[(size_t)(b0 + r) * K + h - 1] ? g : 0.f) - g / (float)A;
+      }
+      grad[((size_t)h * rows + b0) * A + i] = gv;
+      grad[((size_t)h * rows + B + b0) * A + i] = 0.f;
     }
+  }
+  if (t == 0) {
+    float s = 0.f;
+    for (int p = 0; p < nr * K; ++p) s += sd[p];
+    partial[blockIdx.x] = s;
   }
 }
 
-// the value head's gradient when B K > kTdThreads: every row's g recomputed from the written
-// advantage gradients (g = grad[k+1][b][a] + g / A is not exact, so it is recomputed in full)
-__global__ void td_value_grad_kernel(const float* __restrict__ on, const float* __restrict__ tg,
-                                     const int64_t* __restrict__ actions, const float* __restrict__ rewards,
-                                     const float* __restrict__ masks, int B, int K, int A, float gamma,
-                                     float* __restrict__ grad) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  const int64_t rows = 2 * (int64_t)B;
-  const float inv_bk = 1.f / (float)(B * K);
-  float s = 0.f;
-  for (int k = 0; k < K; ++k) {
-    const float* adv = on + ((size_t)(k + 1) * rows + b) * A;
-    const float current = (on[(size_t)b * A] + adv[(int)actions[b * K + k]]) - td_mean(adv, A);
-    const float* adv2 = on + ((size_t)(k + 1) * rows + B + b) * A;
-    const float v2 = on[(size_t)(B + b) * A];
-    const float m2 = td_mean(adv2, A);
-    float best = (v2 + adv2[0]) - m2;
-    int am = 0;
-    for (int j = 1; j < A; ++j) {
-      const float qj = (v2 + adv2[j]) - m2;
-      const bool take = !isnan(best) && (isnan(qj) || qj > best);
-      best = take ? qj : best;
-      am = take ? j : am;
-    }
-    const float* tadv = tg + ((size_t)(k + 1) * B + b) * A;
-    const float tnext = (tg[(size_t)b * A] + tadv[am]) - td_mean(tadv, A);
-    const float expected = rewards[b] + (tnext * gamma) * masks[b];
-    s += 2.f * (current - expected) * inv_bk;
+// the loss: the blocks' partial sums added in block order
+__global__ void td_loss_sum_kernel(const float* __restrict__ partial, int n, float inv_bk, float* __restrict__ loss) {
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int i = 0; i < n; ++i) s += partial[i];
+    loss[0] = s * inv_bk;
   }
-  grad[(size_t)b * A] = s;
 }
 
 extern "C" {
@@ -679,19 +675,23 @@ int pbn_replay_batch(const pbn_net* net, int64_t batch, const int64_t* d_idx, in
 
 int pbn_bdq_td_loss(const float* d_online, const float* d_target, const int64_t* d_actions, const float* d_rewards,
                     const float* d_masks, int32_t batch, int32_t n_branches, int32_t n_actions, float gamma,
-                    float* d_loss, float* d_grad, void* stream) {
-  if (batch < 1 || n_branches < 1 || n_actions < 1) return pbn::set_error(PBN_EINVAL, "batch, n_branches, n_actions >= 1");
-  if ((int64_t)batch * n_branches > (1 << 24)) return pbn::set_error(PBN_EINVAL, "batch * n_branches too large");
-  if (!d_online || !d_target || !d_actions || !d_rewards || !d_masks || !d_loss || !d_grad)
+                    float* d_loss, float* d_grad, float* d_scratch, void* stream) {
+  if (batch < 1 || n_branches < 1 || n_branches > 7 || n_actions < 1 || n_actions > 128)
+    return pbn::set_error(PBN_EINVAL, "batch >= 1, n_branches 1..7, n_actions 1..128");
+  if (!d_online || !d_target || !d_actions || !d_rewards || !d_masks || !d_loss || !d_grad || !d_scratch)
     return pbn::set_error(PBN_EINVAL, "null buffer");
-  hipLaunchKernelGGL(td_loss_kernel, dim3(1), dim3(kTdThreads), 0, (hipStream_t)stream, d_online, d_target, d_actions,
-                     d_rewards, d_masks, batch, n_branches, n_actions, gamma, d_loss, d_grad);
+  const int blocks = (batch + kTdRows - 1) / kTdRows;
+  const int H = n_branches + 1;
+  const size_t lds = ((size_t)H * 3 * kTdRows * n_actions + 2 * kTdRows * n_branches) * sizeof(float);
+  if (lds > 64 * 1024 &&   // (up to 98 KB at 8 heads of 128 actions)
+      hipFuncSetAttribute((const void*)td_loss_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return pbn::set_error(PBN_EDEVICE, "hipFuncSetAttribute failed");
+  hipLaunchKernelGGL(td_loss_kernel, dim3(blocks), dim3(kTdThreads), lds, (hipStream_t)stream, d_online, d_target,
+                     d_actions, d_rewards, d_masks, batch, n_branches, n_actions, gamma, d_scratch, d_grad);
   if (hipGetLastError() != hipSuccess) return pbn::set_error(PBN_EDEVICE, "td_loss_kernel launch failed");
-  if (batch * n_branches > kTdThreads) {
-    hipLaunchKernelGGL(td_value_grad_kernel, dim3((batch + 255) / 256), dim3(256), 0, (hipStream_t)stream, d_online,
-                       d_target, d_actions, d_rewards, d_masks, batch, n_branches, n_actions, gamma, d_grad);
-    if (hipGetLastError() != hipSuccess) return pbn::set_error(PBN_EDEVICE, "td_value_grad_kernel launch failed");
-  }
+  hipLaunchKernelGGL(td_loss_sum_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, d_scratch, blocks,
+                     1.f / (float)(batch * n_branches), d_loss);
+  if (hipGetLastError() != hipSuccess) return pbn::set_error(PBN_EDEVICE, "td_loss_sum_kernel launch failed");
   return PBN_OK;
 }
 

@@ -148,11 +148,12 @@ class _TDLoss(torch.autograd.Function):
         B = rows // 2
         loss = torch.empty(1, dtype=torch.float32, device=online.device)
         grad = torch.empty_like(online)
+        scratch = torch.empty((B + 7) // 8, dtype=torch.float32, device=online.device)
         L = _lib.load()
         with torch.cuda.device(online.device):
             _lib.check(L.pbn_bdq_td_loss(online.data_ptr(), target_heads.data_ptr(), actions.data_ptr(),
                                          rewards.data_ptr(), masks.data_ptr(), B, H - 1, A, float(gamma),
-                                         loss.data_ptr(), grad.data_ptr(),
+                                         loss.data_ptr(), grad.data_ptr(), scratch.data_ptr(),
                                          torch.cuda.current_stream(online.device).cuda_stream), "pbn_bdq_td_loss")
         ctx.save_for_backward(grad)
         return loss[0]

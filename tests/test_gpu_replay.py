@@ -87,13 +87,13 @@ def test_learner_many_frames():
     assert learner.replay.size == 12 * 4096
 
 
-@pytest.mark.parametrize("B,K", [(256, 3), (512, 3), (32, 1)])
+@pytest.mark.parametrize("B,K", [(256, 3), (512, 3), (32, 1), (40, 7)])
 def test_fused_td_loss_matches_pytorch(B, K):
     """pbn_bdq_td_loss (bdq_update's GPU path: both duelings, the double-DQN target, the MSE and
     the backward in one launch) against the same update written in PyTorch, on the same nets and
     batch: the loss to rtol 1e-5 and every parameter gradient to rtol 1e-4 / atol 1e-7 (the
     dueling means and the value head's sum over branches are summed in a different order).
-    B = 512 at K = 3 runs the second (value-head) launch."""
+    B = 32 at K = 1 is one block of the row pass."""
     import copy
 
     import torch.nn.functional as F
