@@ -179,7 +179,10 @@ class ShardedRollout:
         gathers of this shape and form) or, with async_op, (records, work): the records are
         readable on the current stream after ``work.wait()``.
         """
-        if dst is not None and not copy_own and (not dist.is_initialized() or self.world == 1):
+        if (dst is None or not copy_own) and not dist.is_initialized():
+            # one process without a process group: its records are the whole batch
+            return ([rec], None) if async_op else [rec]
+        if dst is not None and not copy_own and self.world == 1:
             # the learner's own shard: already where the kernel wrote it (all_gather still runs
             # at world 1, so the collective path is exercised on a one-GPU box)
             return ([rec], None) if async_op else [rec]
