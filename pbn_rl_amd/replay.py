@@ -165,11 +165,12 @@ class _TDLoss(torch.autograd.Function):
 
 
 def bdq_update(q: torch.nn.Module, target: torch.nn.Module, opt: torch.optim.Optimizer, batch: Dict[str, torch.Tensor],
-               gamma: float = 0.999, grad_clamp: float = 1.0) -> torch.Tensor:
+               gamma: float = 0.999, grad_clamp: float = 1.0, target_weights=None) -> torch.Tensor:
     """One update_policy step (bdq_model/__init__.py:111-131) on a gathered batch; returns the loss.
     On the GPU the duelings, the double-DQN target, the MSE and their backward run as one HIP
     launch on the raw head outputs (``pbn_bdq_td_loss``); elsewhere (CPU tensors) as PyTorch
-    expressions."""
+    expressions.  ``target_weights``: the target network's ``head_weights()`` computed beforehand
+    (it changes only at soft updates)."""
     # q(obs) and q(next_obs) as one forward over 2B rows (half the launches; only the first
     # half carries gradient)
     B = batch["obs"].shape[1]
@@ -177,7 +178,8 @@ def bdq_update(q: torch.nn.Module, target: torch.nn.Module, opt: torch.optim.Opt
     if x.is_cuda and isinstance(q, BranchingQNetwork) and isinstance(target, BranchingQNetwork):
         heads = q.forward_heads(q.model[0](x))                          # (K+1, 2B, A), raw
         with torch.no_grad():
-            t_heads = target.forward_heads(target.model[0](batch["next_obs"])).contiguous()   # (K+1, B, A)
+            t_heads = target.forward_heads(target.model[0](batch["next_obs"]),
+                                           weights=target_weights).contiguous()   # (K+1, B, A)
         loss = _TDLoss.apply(heads.contiguous(), t_heads, batch["actions"].reshape(B, -1).contiguous(),
                              batch["rewards"].reshape(B).contiguous(), batch["masks"].reshape(B).contiguous(), gamma)
     else:
@@ -239,6 +241,22 @@ class BDQLearner:
         self.last_loss: Optional[torch.Tensor] = None
         self.graphable = graphable
         self._graph: Optional[torch.cuda.CUDAGraph] = None
+        self._tw = None   # _target_weights()
+
+    def _target_weights(self):
+        """The target network's stacked head weights (BranchingQNetwork.head_weights), held in
+        fixed tensors: the target changes only at soft updates, which refresh them in place (a
+        captured frame reads these very tensors)."""
+        if self._tw is None:
+            with torch.no_grad():
+                self._tw = tuple(w.detach().clone() for w in self.target.head_weights())
+        return self._tw
+
+    def _refresh_target_weights(self) -> None:
+        if self._tw is not None:
+            with torch.no_grad():
+                for dst, w in zip(self._tw, self.target.head_weights()):
+                    dst.copy_(w)
 
     def frame(self):
         if self._graph is not None:
@@ -258,10 +276,12 @@ class BDQLearner:
             for _ in range(self.updates_per_frame):
                 idx = self.replay.sample_indices(self.batch_size, self.gen)
                 batch = self.replay.gather(idx, env.net)
-                self.last_loss = bdq_update(self.q, self.target, self.opt, batch, self.gamma)
+                self.last_loss = bdq_update(self.q, self.target, self.opt, batch, self.gamma,
+                                            target_weights=self._target_weights())
                 self.updates += 1
                 if self.updates % self.target_update == 0:
                     soft_update(self.target, self.q)
+                    self._refresh_target_weights()
         return reward, done
 
     # ---- graph-captured frames -------------------------------------------------------------
@@ -319,7 +339,8 @@ class BDQLearner:
         for _ in range(self.updates_per_frame):
             idx = self.replay.sample_indices(self.batch_size, self.gen, size_t=self._size_t)
             batch = self.replay.gather(idx, env.net)
-            loss = bdq_update(self.q, self.target, self.opt, batch, self.gamma)
+            loss = bdq_update(self.q, self.target, self.opt, batch, self.gamma,
+                              target_weights=self._target_weights())
         return env.reward[: env.num_envs], done_all[: env.num_envs], loss
 
     def _replay_frame(self):
@@ -333,6 +354,7 @@ class BDQLearner:
         self.updates += self.updates_per_frame
         if self.updates % self.target_update == 0:
             soft_update(self.target, self.q)
+            self._refresh_target_weights()
         reward, done, self.last_loss = self._g_out
         return reward, done
 
