@@ -361,6 +361,20 @@ int pbn_qnet_flipmask_from_state(const pbn_net* net, uint64_t seed, uint64_t ste
                                  void* stream);
 
 /*
+ * n transitions into the learner's replay ring (pbn_rl_amd/replay.py DeviceReplay), in one launch:
+ * env e's state / next_state (uint32 [words][n]), target (uint8 [n]), action (int32 [n][n_branches]),
+ * reward (float [n]) and done (uint8 [n], nonzero = done) go to slot (*d_pos + e) mod capacity of
+ * the ring arrays (state / next_state uint32 [words][capacity], target uint8 [capacity], action
+ * int32 [capacity][n_branches], reward float [capacity], done uint8 [capacity] as 0/1).  d_pos
+ * (int64, device memory) is read, not advanced.  capacity >= n.
+ */
+int pbn_replay_store(int64_t n, const int64_t* d_pos, int64_t capacity, int32_t words, int32_t n_branches,
+                     const uint32_t* d_state, const uint32_t* d_next_state, const uint8_t* d_target,
+                     const int32_t* d_action, const float* d_reward, const uint8_t* d_done, uint32_t* d_ring_state,
+                     uint32_t* d_ring_next_state, uint8_t* d_ring_target, int32_t* d_ring_action,
+                     float* d_ring_reward, uint8_t* d_ring_done, void* stream);
+
+/*
  * One replay batch for the learner's update (pbn_rl_amd/replay.py DeviceReplay), in one launch:
  * rows d_idx[0..batch) (int64, < capacity) of the ring -- d_state / d_next_state uint32 [W][capacity],
  * d_target uint8 [capacity], d_action int32 [capacity][n_branches], d_reward float [capacity],

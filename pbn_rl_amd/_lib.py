@@ -28,7 +28,7 @@ EXPORTS = ["pbn_net_create", "pbn_net_destroy", "pbn_net_words", "pbn_reset", "p
            "pbn_rollout", "pbn_rollout_ex", "pbn_state_histogram", "pbn_obs_unpack", "pbn_bilinear_targets", "pbn_q_to_flipmask",
            "pbn_q_to_flipmask_dev",
            "pbn_heads_to_flipmask", "pbn_qnet_heads", "pbn_qnet_flipmask", "pbn_qnet_heads_from_state",
-           "pbn_qnet_flipmask_from_state", "pbn_replay_batch", "pbn_bdq_td_loss", "pbn_last_error", "pbn_abi_version"]
+           "pbn_qnet_flipmask_from_state", "pbn_replay_store", "pbn_replay_batch", "pbn_bdq_td_loss", "pbn_last_error", "pbn_abi_version"]
 SOURCES = ["pbn_env.hip", "pbn_settle.hip", "pbn_agent.hip", "pbn_qnet.hip"]
 
 _lib: Optional[ctypes.CDLL] = None
@@ -122,6 +122,8 @@ def load() -> ctypes.CDLL:
     L.pbn_qnet_flipmask_from_state.restype = ctypes.c_int
     L.pbn_last_error.argtypes = []
     L.pbn_last_error.restype = ctypes.c_char_p
+    L.pbn_replay_store.argtypes = [i64, vp, i64, ctypes.c_int32, ctypes.c_int32] + [vp] * 12 + [vp]
+    L.pbn_replay_store.restype = ctypes.c_int
     L.pbn_replay_batch.argtypes = [vp, i64, vp, i64, vp, vp, vp, vp, ctypes.c_int32, vp, vp, vp, vp, vp, vp, vp]
     L.pbn_replay_batch.restype = ctypes.c_int
     L.pbn_bdq_td_loss.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_float,

@@ -360,6 +360,29 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 }  // namespace
 
+// ---- n transitions into the replay ring in one pass (pbn_replay_store): env e goes to slot
+// (pos + e) mod capacity, pos read from device memory (graph replays advance it on the stream).
+// Replaces the ring's six index_copy_ launches and the slot arithmetic.
+__global__ void __launch_bounds__(kObsThreads) replay_store_kernel(
+    int64_t n, const int64_t* __restrict__ pos, int64_t cap, int W, int K, const uint32_t* __restrict__ st,
+    const uint32_t* __restrict__ nst, const uint8_t* __restrict__ tgt, const int32_t* __restrict__ act,
+    const float* __restrict__ rew, const uint8_t* __restrict__ done, uint32_t* __restrict__ r_st,
+    uint32_t* __restrict__ r_nst, uint8_t* __restrict__ r_tgt, int32_t* __restrict__ r_act,
+    float* __restrict__ r_rew, uint8_t* __restrict__ r_done) {
+  const int64_t p0 = *pos;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j = (p0 + e) % cap;
+    for (int w = 0; w < W; ++w) {
+      r_st[(size_t)w * cap + j] = st[(size_t)w * n + e];
+      r_nst[(size_t)w * cap + j] = nst[(size_t)w * n + e];
+    }
+    r_tgt[j] = tgt[e];
+    for (int k = 0; k < K; ++k) r_act[(size_t)j * K + k] = act[(size_t)e * K + k];
+    r_rew[j] = rew[e];
+    r_done[j] = done[e] ? 1 : 0;
+  }
+}
+
 // ---- a replay batch in one pass (pbn_replay_batch): rows idx of the ring unpacked into the
 // update's network input x = (2, 2B, N) (plane 0: the states in rows 0..B-1, the next states in
 // rows B..2B-1; plane 1: the target attractor's first state for both), plus the actions as int64,
@@ -648,6 +671,25 @@ int pbn_heads_to_flipmask(const pbn_net* net, uint64_t seed, uint64_t step, cons
   if (d_epsilon && ((uintptr_t)d_epsilon & 3u) != 0) return pbn::set_error(PBN_EINVAL, "d_epsilon misaligned");
   return q_to_flipmask_impl(net, seed, step, d_step, env_offset, n_envs, n_branches, n_actions, d_heads, epsilon,
                             d_epsilon, d_flipmask, d_actions, stream, 1);
+}
+
+int pbn_replay_store(int64_t n, const int64_t* d_pos, int64_t capacity, int32_t words, int32_t n_branches,
+                     const uint32_t* d_state, const uint32_t* d_next_state, const uint8_t* d_target,
+                     const int32_t* d_action, const float* d_reward, const uint8_t* d_done, uint32_t* d_ring_state,
+                     uint32_t* d_ring_next_state, uint8_t* d_ring_target, int32_t* d_ring_action,
+                     float* d_ring_reward, uint8_t* d_ring_done, void* stream) {
+  if (n < 1 || capacity < n || words < 1 || words > 4 || n_branches < 1)
+    return pbn::set_error(PBN_EINVAL, "n >= 1, capacity >= n, words 1..4, n_branches >= 1");
+  if (!d_pos || !d_state || !d_next_state || !d_target || !d_action || !d_reward || !d_done || !d_ring_state ||
+      !d_ring_next_state || !d_ring_target || !d_ring_action || !d_ring_reward || !d_ring_done)
+    return pbn::set_error(PBN_EINVAL, "null buffer");
+  const unsigned blocks = (unsigned)std::min<int64_t>((n + kObsThreads - 1) / kObsThreads, 4096);
+  hipLaunchKernelGGL(replay_store_kernel, dim3(blocks), dim3(kObsThreads), 0, (hipStream_t)stream, n, d_pos, capacity,
+                     words, n_branches, d_state, d_next_state, d_target, d_action, d_reward, d_done, d_ring_state,
+                     d_ring_next_state, d_ring_target, d_ring_action, d_ring_reward, d_ring_done);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return pbn::set_error(PBN_EDEVICE, hipGetErrorString(e));
+  return PBN_OK;
 }
 
 int pbn_replay_batch(const pbn_net* net, int64_t batch, const int64_t* d_idx, int64_t capacity,

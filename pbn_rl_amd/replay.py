@@ -80,6 +80,23 @@ class DeviceReplay:
         n = target.shape[0]
         if n > self.capacity:
             raise ValueError("more transitions than the ring holds")
+        if (self.device.type == "cuda" and state.dtype == torch.int32 and next_state.dtype == torch.int32
+                and target.dtype == torch.uint8 and action.dtype == torch.int32 and reward.dtype == torch.float32
+                and done.dtype in (torch.bool, torch.uint8)):
+            # the six field copies in one launch (pbn_replay_store)
+            st, nst, act = state.contiguous(), next_state.contiguous(), action.contiguous()
+            L = _lib.load()
+            with torch.cuda.device(self.device):
+                _lib.check(L.pbn_replay_store(n, pos_t.data_ptr(), self.capacity, self.words, self.action.shape[1],
+                                              st.data_ptr(), nst.data_ptr(), target.contiguous().data_ptr(),
+                                              act.data_ptr(), reward.contiguous().data_ptr(),
+                                              done.contiguous().data_ptr(), self.state.data_ptr(),
+                                              self.next_state.data_ptr(), self.target.data_ptr(),
+                                              self.action.data_ptr(), self.reward.data_ptr(), self.done.data_ptr(),
+                                              torch.cuda.current_stream(self.device).cuda_stream), "pbn_replay_store")
+            pos_t.add_(n).remainder_(self.capacity)
+            size_t.add_(n).clamp_(max=self.capacity)
+            return
         idx = (torch.arange(n, device=self.device, dtype=torch.int64) + pos_t) % self.capacity
         self.state.index_copy_(1, idx, state)
         self.next_state.index_copy_(1, idx, next_state)

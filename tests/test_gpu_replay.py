@@ -133,3 +133,35 @@ def test_fused_td_loss_matches_pytorch(B, K):
             assert a is None and b is None
             continue
         assert torch.allclose(a, b, rtol=1e-4, atol=1e-7), (a - b).abs().max().item()
+
+
+def test_replay_store_kernel_matches_index_copy():
+    """store_at's one-launch ring write (pbn_replay_store) equals the six index_copy_ of the
+    same transitions, across the ring's wrap-around, and advances the device position and size."""
+    dev = torch.device("cuda")
+    cap, n, W, K = 100, 64, 2, 3
+    g = torch.Generator(device="cuda").manual_seed(1)
+    a = DeviceReplay(cap, W, K, dev)
+    for step in range(3):   # 64, 128 -> wraps at 100
+        st = torch.randint(-2 ** 31, 2 ** 31 - 1, (W, n), device=dev, generator=g, dtype=torch.int64).to(torch.int32)
+        nst = torch.randint(-2 ** 31, 2 ** 31 - 1, (W, n), device=dev, generator=g, dtype=torch.int64).to(torch.int32)
+        tg = torch.randint(0, 200, (n,), device=dev, generator=g).to(torch.uint8)
+        act = torch.randint(0, 29, (n, K), device=dev, generator=g).to(torch.int32)
+        rew = torch.randn(n, device=dev, generator=g)
+        done = torch.randint(0, 2, (n,), device=dev, generator=g).bool()
+        pos_t = torch.full((1,), a.pos, dtype=torch.int64, device=dev)
+        size_t = torch.full((1,), a.size, dtype=torch.int64, device=dev)
+        want = {k: getattr(a, k).clone() for k in ("state", "next_state", "target", "action", "reward", "done")}
+        idx = (torch.arange(n, device=dev) + a.pos) % cap
+        want["state"].index_copy_(1, idx, st)
+        want["next_state"].index_copy_(1, idx, nst)
+        want["target"].index_copy_(0, idx, tg)
+        want["action"].index_copy_(0, idx, act)
+        want["reward"].index_copy_(0, idx, rew)
+        want["done"].index_copy_(0, idx, done.to(torch.uint8))
+        a.store_at(pos_t, size_t, st, tg, act, rew, nst, done)
+        for k, v in want.items():
+            assert torch.equal(getattr(a, k), v), (step, k)
+        a.pos = (a.pos + n) % cap
+        a.size = min(a.size + n, cap)
+        assert int(pos_t.item()) == a.pos and int(size_t.item()) == a.size
