@@ -34,9 +34,15 @@ def main():
     ap.add_argument("--no-final", action="store_true", help="the run did not store s' (bench.py --no-final-state)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--command", default=None, help="the profiled command, recorded in the summary")
+    ap.add_argument("--kernel", default="pbn_",
+                    help="kernel-name substring to average (a bench line with a settle_law object runs "
+                         "pbn_rollout_pipe and pbn_rollout_settle in one process)")
+    ap.add_argument("--suffix", default="", help="file-name suffix (e.g. _settle64)")
     args = ap.parse_args()
-    f, n, name = mean_counter(os.path.join(args.run_dir, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
-    w, _, _ = mean_counter(os.path.join(args.run_dir, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    f, n, name = mean_counter(os.path.join(args.run_dir, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE",
+                              args.kernel)
+    w, _, _ = mean_counter(os.path.join(args.run_dir, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE",
+                           args.kernel)
     W, T = args.words, args.steps_per_launch
     if args.mode == "rollout":
         alg = args.envs * (2 * (4 * W + 2) + T * ((8 if args.no_final else 12) * W + 5))
@@ -54,7 +60,7 @@ def main():
         for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_ACTIVE_INST_VALU", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES",
                   "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "GRBM_GUI_ACTIVE"):
             try:
-                out[c + "_per_launch"] = mean_counter(sq, c)[0]
+                out[c + "_per_launch"] = mean_counter(sq, c, args.kernel)[0]
             except ZeroDivisionError:   # counter not in this pass
                 pass
         out["valu_insts_per_launch"] = out["SQ_INSTS_VALU_per_launch"]
@@ -66,7 +72,7 @@ def main():
                 "active_valu": out["SQ_ACTIVE_INST_VALU_per_launch"] / wc,
                 "wait_any (s_waitcnt / barrier)": out["SQ_WAIT_ANY_per_launch"] / wc,
                 "wait_inst_any (issue stall)": out["SQ_WAIT_INST_ANY_per_launch"] / wc}
-    tail = "_nofinal" if args.no_final else ""
+    tail = ("_nofinal" if args.no_final else "") + args.suffix
     path = args.out or os.path.join("profiles",
                                     f"pmc_{args.network}_{args.envs}_{args.mode}_T{args.steps_per_launch}{tail}.json")
     with open(path, "w") as fo:
