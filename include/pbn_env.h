@@ -63,7 +63,7 @@
 extern "C" {
 #endif
 
-#define PBN_ABI_VERSION 5
+#define PBN_ABI_VERSION 6
 
 #define PBN_MAX_NODES 128
 #define PBN_MAX_ARITY 4
@@ -409,6 +409,41 @@ int pbn_replay_batch(const pbn_net* net, int64_t batch, const int64_t* d_idx, in
 int pbn_bdq_td_loss(const float* d_online, const float* d_target, const int64_t* d_actions, const float* d_rewards,
                     const float* d_masks, int32_t batch, int32_t n_branches, int32_t n_actions, float gamma,
                     float* d_loss, float* d_grad, float* d_scratch, void* stream);
+
+/*
+ * The whole update_policy step (bdq_model/__init__.py:100-139) on a flat parameter buffer, for the
+ * reference's network BranchingQNetwork((N, N), N + 1, K) (bdq_model/network.py:24-63: bilinear
+ * N x N -> 256, trunk 256-128-64-32, K + 1 heads 32-64-(N+1), LeakyReLU).  Replaces the sampled
+ * batch's np.stack and upload (:102-109), both forwards, the target, the MSE, the backward, the
+ * per-tensor gradient clamp (:129-130) and optimizer.step() (:131): three launches.
+ *
+ * pbn_bdq_layout: offsets[0..11] (floats, 16-float aligned) of the segments bilinear weight
+ *   (256, N, N), bilinear bias (256), the trunk's three weight (out, in) / bias pairs, the heads'
+ *   first layers (K+1, 64, 32) and biases (K+1, 64), second layers (K+1, N+1, 64) and biases
+ *   (K+1, N+1) -- head 0 is the value head, whose rows / biases past output 0 are zero padding;
+ *   offsets[12] = the total.  Parameters, Adam's moments and d_grad share this layout.
+ * pbn_bdq_learn_workspace: bytes of the update's workspace at batch B (a multiple of 16).
+ * pbn_bdq_pack: d_Tq float [n_attr][N][256], the bilinear layer contracted with each attractor's
+ *   first state, T[t][i][o] = sum_j x_t[j] W[o][i][j], stored [t][i][j][q] = T[t][i][16 q + j]
+ *   (the table pbn_qnet_*_from_state read).  Needed once per parameter version not written by
+ *   pbn_bdq_learn (initial weights, a loaded checkpoint, the target network after a soft update).
+ * pbn_bdq_learn: rows d_idx [B] of the replay ring (the layout of pbn_replay_store);
+ *   d_params / d_Tq the online network (updated in place: Adam step, and the table of the new
+ *   weights), d_target_params / d_target_Tq the target network (read); d_adam_m / d_adam_v the
+ *   moments, d_adam_step float [1] Adam's step count (incremented on the device); the loss to
+ *   d_loss float [1]; when d_grad is not null, the clamped gradient there.  Same arithmetic as
+ *   pbn_rl_amd/replay.py bdq_update + torch.optim.Adam in fp32, to summation order.
+ */
+int pbn_bdq_layout(int32_t n_nodes, int32_t n_branches, int64_t* offsets);
+int pbn_bdq_learn_workspace(int32_t n_nodes, int32_t n_branches, int64_t batch, int64_t* bytes);
+int pbn_bdq_pack(const pbn_net* net, int32_t n_branches, const float* d_params, float* d_Tq, void* stream);
+int pbn_bdq_learn(const pbn_net* net, int64_t batch, const int64_t* d_idx, int64_t capacity, const uint32_t* d_state,
+                  const uint32_t* d_next_state, const uint8_t* d_target, const int32_t* d_action, int32_t n_branches,
+                  const float* d_reward, const uint8_t* d_done, float* d_params, float* d_Tq,
+                  const float* d_target_params, const float* d_target_Tq, float* d_adam_m, float* d_adam_v,
+                  float* d_adam_step, float lr, float beta1, float beta2, float eps, float gamma, float grad_clamp,
+                  float slope, void* d_workspace, int64_t workspace_bytes, float* d_loss, float* d_grad,
+                  void* stream);
 
 const char* pbn_last_error(void);
 int pbn_abi_version(void);

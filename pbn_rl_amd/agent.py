@@ -167,6 +167,8 @@ class BatchedBDQ:
         self._act = isinstance(act, nn.LeakyReLU)
         self._slope = float(act.negative_slope) if self._act else 0.0
         self._pack, self._pack_key = None, None
+        # set by a learner that keeps the weight-derived operands itself (FusedBDQUpdate.acting_pack)
+        self.pack_provider = None
         self._y = torch.empty(n, self.q.model[0].output_dim if self.fast else 1, dtype=torch.float32,
                               device=env.device)
         self.fused_tail = bool(fused_tail) and self._tail_fusable()
@@ -254,6 +256,8 @@ class BatchedBDQ:
         reused, so a frame runs no assembly kernels; a captured frame keeps the pack of its
         capture (re-capture after changing the weights).  In train mode (the learner) they are
         recomputed every call."""
+        if self.pack_provider is not None:
+            return self.pack_provider()
         key = None
         if not self.q.training:
             key = tuple((p.data_ptr(), p._version) for p in self.q.parameters())
@@ -273,7 +277,9 @@ class BatchedBDQ:
         fast forward); returns the head weights of the same pack."""
         env = self.env
         bil = self.q.model[0]
-        T, bias, hw, _ = self._packed()
+        T, bias, hw, Tq = self._packed()
+        if T is None and Tq is not None:   # (a provider's pack holds only the fused layout)
+            T = Tq.transpose(2, 3).reshape(Tq.shape[0], Tq.shape[1], -1).contiguous()
         L = _lib.load()
         with torch.cuda.device(env.device):
             _lib.check(L.pbn_bilinear_targets(env.net.handle, env.n_alloc, env.state.data_ptr(),

@@ -1,0 +1,769 @@
+// pbn_learn.hip -- the BDQ learner's update_policy step (bdq_model/__init__.py:100-139) as three
+// HIP launches over one flat parameter buffer (SURVEY.md 8(f) #3, config 5's training frame).
+//
+// The reference's update is a PyTorch program: np.stack of 256 sampled transitions, two forwards
+// of the online network and one of the target network, the double-DQN target, the MSE, autograd,
+// a per-tensor gradient clamp and Adam (:100-131).  On the GPU that is ~100 kernels of a few
+// microseconds each, and the frame waits on their launch latency, not on arithmetic (the whole
+// update is ~0.3 GFLOP).  Here it is three launches:
+//
+//   learn_fwd    3 B/16 blocks.  Block = 16 transitions of one of three row sets (online network
+//                on s, online on s', target network on s').  The bilinear layer is a sum of
+//                target-table rows (T[t][i][:] = sum_j target_t[j] W[:, i, j], the table the acting
+//                kernel reads) over the state's set bits; the trunk and the heads run on
+//                v_mfma_f32_16x16x4_f32 with the 16 transitions as the MFMA's columns and the
+//                activations in LDS.  Stores the raw head outputs of all three sets and, for the
+//                online s rows, every layer's activation (the backward's operands).
+//   learn_bwd    B/16 blocks.  The TD error of bdq_update per (transition, branch): both duelings,
+//                the online argmax over s', the target network's value there, the MSE's partial
+//                sum, and the gradient at the head outputs; then the backward through the heads
+//                and the trunk (transposed MFMA tiles, LeakyReLU derivative from the stored
+//                activation), storing every layer's delta.
+//   learn_apply  one wave per 16 x 16 gradient tile (K = the batch: dW = delta . act^T), the
+//                bilinear layer's weight gradient from the packed state and target bits
+//                (dW[o][i][j] = sum_r g[o][r] s_i[r] t_j[r]); each wave clamps its tile to
+//                [-c, c] (:129-130), takes the Adam step on it, and, for the bilinear layer,
+//                recomputes the target-table rows of the weights it just wrote.  Block 0 adds
+//                the MSE's partial sums in block order (the loss is reproducible).
+//
+// Parameters, Adam's moments and the gradient share one layout (pbn_bdq_layout): the module's
+// nn.Parameters are views into it (pbn_rl_amd/replay.py FusedBDQUpdate), so the acting kernel,
+// the checkpoint and the PyTorch forward all see the same weights.  Row sets and activations
+// are [feature][batch] in the workspace: both MFMA operands of a gradient tile are float4 loads
+// along the batch.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "../../include/pbn_env.h"
+#include "net_view.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kRows = 16;              // transitions per tile: the MFMA's 16 columns
+constexpr int kWaves = 8;              // waves per forward / backward block
+constexpr int kThreads = 64 * kWaves;
+constexpr int kApplyWaves = 4;
+constexpr int kD0 = 256, kD1 = 128, kD2 = 64, kD3 = 32, kDH = 64;   // bdq_model/network.py:29-36,46
+constexpr int kMaxNT = 8;              // 16-column tiles of the bilinear layer's j (N <= 127)
+
+enum Seg { BIL_W, BIL_B, L2_W, L2_B, L3_W, L3_B, L4_W, L4_B, H1_W, H1_B, H2_W, H2_B, TOTAL };
+
+__host__ __device__ inline int64_t al16(int64_t x) { return (x + 15) & ~int64_t(15); }
+
+void make_layout(int N, int H, int64_t* off) {
+  const int64_t A = N + 1;
+  const int64_t sz[TOTAL] = {256LL * N * N, kD0, (int64_t)kD1 * kD0, kD1, (int64_t)kD2 * kD1, kD2,
+                             (int64_t)kD3 * kD2, kD3, (int64_t)H * kDH * kD3, (int64_t)H * kDH, H * A * kDH, H * A};
+  int64_t o = 0;
+  for (int s = 0; s < TOTAL; ++s) {
+    off[s] = o;
+    o += al16(sz[s]);
+  }
+  off[TOTAL] = o;
+}
+
+struct LearnArgs {
+  // the replay ring and the sampled rows
+  const int64_t* idx;
+  int B;
+  int64_t cap;
+  const uint32_t* st;
+  const uint32_t* nst;
+  const uint8_t* tgt;
+  const int32_t* act;
+  const float* rew;
+  const uint8_t* done;
+  // the network's attractor table (first state of attractor t: the target half of the input)
+  const int32_t* att_start;
+  const uint32_t* att_states;
+  int n_attr, N, W, K, H, A, Apad;
+  // parameters (online, updated in place; target, read), their target tables, Adam's state
+  float* P;
+  float* Tq;
+  const float* PT;
+  const float* TqT;
+  float* m;
+  float* v;
+  float* step;
+  int64_t off[TOTAL + 1];
+  float lr, b1, b2, eps, gamma, clampv, slope;
+  // workspace: [feature][B] planes
+  float* heads;   // [3][H][Apad][B]
+  float* y1;      // [256][B]  online s rows, after the activation
+  float* h2;      // [128][B]
+  float* h3;      // [64][B]
+  float* h4;      // [32][B]
+  float* hh;      // [64 H][B]
+  float* dheads;  // [H][Apad][B]
+  float* dhh;     // [64 H][B]
+  float* dh4;     // [32][B]
+  float* dh3;     // [64][B]
+  float* dh2;     // [128][B]
+  float* g1;      // [256][B]
+  uint32_t* srow; // [W][B] state words of the sampled rows
+  uint32_t* trow; // [W][B] their target attractors' first-state words
+  float* partial; // [B / 16]
+  float* loss;
+  float* grad;    // optional: the clamped gradient, parameter layout
+};
+
+__device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float leaky(float x, float slope) { return x > 0.f ? x : x * slope; }
+
+__device__ __forceinline__ int64_t row_index(const LearnArgs& a, int b) {
+  const int64_t j = a.idx[b];
+  return j < 0 ? 0 : (j >= a.cap ? a.cap - 1 : j);   // (sample_indices keeps 0 <= j < size)
+}
+
+// ---- forward tiles.  Activations in LDS are blocked [K/16][16 rows][16]: the float4 at
+// (kb, r, 4g) holds features 16 kb + 4g .. +3 of row r, the B operand of four k-steps of lane
+// (g = lane >> 4, r = lane & 15).  D[o][r] = sum_k W[o][k] X[k][r] for the 16 outputs o0..o0+15:
+// lane l supplies A[o0 + (l & 15)][k] = one float4 of weight row o0 + (l & 15); its accumulator
+// holds D[o0 + 4g + v][r], v = 0..3.
+template <int K>
+__device__ __forceinline__ f32x4 fwd_tile(const float* __restrict__ W, int ldw, int o0, int o_valid,
+                                          const float* __restrict__ Xs, int lane) {
+  const int g = lane >> 4, rr = lane & 15;
+  const int o = o0 + rr;
+  const bool ov = o < o_valid;
+  const float* wrow = W + (size_t)(ov ? o : 0) * ldw + 4 * g;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kb = 0; kb < K / 16; ++kb) {
+    float4 w = *reinterpret_cast<const float4*>(wrow + kb * 16);
+    if (!ov) w = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 x = *reinterpret_cast<const float4*>(Xs + (kb * 16 + rr) * 16 + 4 * g);
+    acc = mfma(w.x, x.x, acc);
+    acc = mfma(w.y, x.y, acc);
+    acc = mfma(w.z, x.z, acc);
+    acc = mfma(w.w, x.w, acc);
+  }
+  return acc;
+}
+
+// bias + LeakyReLU, into the blocked LDS plane (tile o0) and, when `out` is set, the [O][B] plane
+__device__ __forceinline__ void fwd_store(f32x4 acc, const float* __restrict__ bias, int o0, float slope,
+                                          float* __restrict__ Ys, float* __restrict__ out, int B, int b0, int lane) {
+  const int g = lane >> 4, rr = lane & 15;
+  float4 y;
+  float* yp = &y.x;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int o = o0 + 4 * g + v;
+    yp[v] = leaky(acc[v] + bias[o], slope);
+    if (out) out[(size_t)o * B + b0 + rr] = yp[v];
+  }
+  *reinterpret_cast<float4*>(Ys + ((o0 >> 4) * 16 + rr) * 16 + 4 * g) = y;
+}
+
+__global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* Y1 = lds;                    // [256/16][16][16]
+  float* X2 = Y1 + kD0 * kRows;       // [128/16][16][16]
+  float* X3 = X2 + kD1 * kRows;
+  float* X4 = X3 + kD2 * kRows;
+  float* XH = X4 + kD3 * kRows;       // [64 H / 16][16][16]
+  uint32_t* sw = reinterpret_cast<uint32_t*>(XH + kDH * a.H * kRows);   // [4][16]
+  int* stg = reinterpret_cast<int*>(sw + 4 * kRows);                  // [16]
+  const int tiles = a.B / kRows;
+  const int set = blockIdx.x / tiles;
+  const int b0 = (blockIdx.x - set * tiles) * kRows;
+  const float* P = set == 2 ? a.PT : a.P;
+  const float* Tq = set == 2 ? a.TqT : a.Tq;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int B = a.B;
+  float* keep = nullptr;   // the online s rows keep their activations for the backward
+  if (tid < kRows) {
+    const int64_t j = row_index(a, b0 + tid);
+    const int tg = a.tgt[j];
+    stg[tid] = tg;
+    for (int w = 0; w < a.W; ++w) {
+      const uint32_t s = (set == 0 ? a.st : a.nst)[(size_t)w * a.cap + j];
+      sw[w * kRows + tid] = s;
+      if (set == 0) {
+        a.srow[(size_t)w * B + b0 + tid] = s;
+        a.trow[(size_t)w * B + b0 + tid] = tg < a.n_attr ? a.att_states[(size_t)a.att_start[tg] * a.W + w] : 0u;
+      }
+    }
+  }
+  __syncthreads();
+  // bilinear layer: y[o] = bias[o] + sum over the set bits i of T[t][i][o] (t = the row's target;
+  // a row without a target has an all-zero second input: bias only).  Wave w takes rows 2w, 2w+1;
+  // lane p reads Tq positions 4p..4p+3 ([t][i][j][q] = T[t][i][16 q + j]: o = 16 q + j).
+  {
+    const float* bias = P + a.off[BIL_B];
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      const int r = 2 * wave + rr;
+      const int t = stg[r];
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (t < a.n_attr) {
+        const float* T = Tq + (size_t)t * a.N * 256 + 4 * lane;
+        for (int i0 = 0; i0 < a.N; i0 += 4) {
+          float4 x[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) x[u] = i0 + u < a.N ? *reinterpret_cast<const float4*>(T + (size_t)(i0 + u) * 256)
+                                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int i = i0 + u;
+            const bool on = i < a.N && ((sw[(i >> 5) * kRows + r] >> (i & 31)) & 1u);
+            acc.x += on ? x[u].x : 0.f;
+            acc.y += on ? x[u].y : 0.f;
+            acc.z += on ? x[u].z : 0.f;
+            acc.w += on ? x[u].w : 0.f;
+          }
+        }
+      }
+      const float* ap = &acc.x;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int o = 16 * (4 * (lane & 3) + c) + (lane >> 2);
+        const float y = leaky(ap[c] + bias[o], a.slope);
+        Y1[((o >> 4) * 16 + r) * 16 + (o & 15)] = y;
+        if (set == 0) a.y1[(size_t)o * B + b0 + r] = y;
+      }
+    }
+  }
+  __syncthreads();
+  if (set == 0) keep = a.h2;
+  {   // 256 -> 128: one output tile per wave
+    const f32x4 acc = fwd_tile<kD0>(P + a.off[L2_W], kD0, 16 * wave, kD1, Y1, lane);
+    fwd_store(acc, P + a.off[L2_B], 16 * wave, a.slope, X2, keep, B, b0, lane);
+  }
+  __syncthreads();
+  if (wave < kD2 / 16) {   // 128 -> 64
+    const f32x4 acc = fwd_tile<kD1>(P + a.off[L3_W], kD1, 16 * wave, kD2, X2, lane);
+    fwd_store(acc, P + a.off[L3_B], 16 * wave, a.slope, X3, set == 0 ? a.h3 : nullptr, B, b0, lane);
+  }
+  __syncthreads();
+  if (wave < kD3 / 16) {   // 64 -> 32
+    const f32x4 acc = fwd_tile<kD2>(P + a.off[L4_W], kD2, 16 * wave, kD3, X3, lane);
+    fwd_store(acc, P + a.off[L4_B], 16 * wave, a.slope, X4, set == 0 ? a.h4 : nullptr, B, b0, lane);
+  }
+  __syncthreads();
+  for (int tt = wave; tt < a.H * kDH / 16; tt += kWaves) {   // the H first head layers: 32 -> 64 H
+    const f32x4 acc = fwd_tile<kD3>(P + a.off[H1_W], kD3, 16 * tt, a.H * kDH, X4, lane);
+    fwd_store(acc, P + a.off[H1_B], 16 * tt, a.slope, XH, set == 0 ? a.hh : nullptr, B, b0, lane);
+  }
+  __syncthreads();
+  // second head layers: head h, outputs 16 at .. (A of them, no activation) -> heads[set][h][a][b]
+  const int at16 = a.Apad / 16;
+  for (int tt = wave; tt < a.H * at16; tt += kWaves) {
+    const int h = tt / at16, o0 = 16 * (tt - h * at16);
+    const f32x4 acc = fwd_tile<kDH>(P + a.off[H2_W] + (size_t)h * a.A * kDH, kDH, o0, a.A, XH + h * kDH * kRows, lane);
+    const int g = lane >> 4, rr = lane & 15;
+    const float* b2 = P + a.off[H2_B] + (size_t)h * a.A;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int o = o0 + 4 * g + v;
+      if (o < a.A) a.heads[(((size_t)set * a.H + h) * a.Apad + o) * B + b0 + rr] = acc[v] + b2[o];
+    }
+  }
+}
+
+// ---- backward tiles: dX[k][r] = sum_o W[o][k] dY[o][r] for the 16 inputs k0..k0+15 (A operand
+// lane l: W[o][k0 + (l & 15)] for the k-step's o = 16 ob + 4g + v; B operand: the blocked dY
+// plane, as the forward's X).  Its accumulator holds dX[k0 + 4g + v][r].
+__device__ __forceinline__ f32x4 bwd_tile(const float* __restrict__ W, int ldw, int k0, int n_ob, int o_valid,
+                                          const float* __restrict__ dYs, int lane) {
+  const int g = lane >> 4, rr = lane & 15;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int ob = 0; ob < n_ob; ++ob) {
+    float w[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int o = 16 * ob + 4 * g + v;
+      w[v] = o < o_valid ? W[(size_t)o * ldw + k0 + rr] : 0.f;
+    }
+    const float4 y = *reinterpret_cast<const float4*>(dYs + (ob * 16 + rr) * 16 + 4 * g);
+    acc = mfma(w[0], y.x, acc);
+    acc = mfma(w[1], y.y, acc);
+    acc = mfma(w[2], y.z, acc);
+    acc = mfma(w[3], y.w, acc);
+  }
+  return acc;
+}
+
+// times LeakyReLU' (from the stored activation: y > 0 exactly when its input was), into the
+// blocked LDS plane (rows kk0..) when Ys is set and the [K][B] plane
+__device__ __forceinline__ void bwd_store(f32x4 acc, const float* __restrict__ act, int kk0, float slope,
+                                          float* __restrict__ Ys, float* __restrict__ out, int B, int b0, int lane) {
+  const int g = lane >> 4, rr = lane & 15;
+  float4 d;
+  float* dp = &d.x;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int k = kk0 + 4 * g + v;
+    const float y = act[(size_t)k * B + b0 + rr];
+    dp[v] = y > 0.f ? acc[v] : acc[v] * slope;
+    out[(size_t)k * B + b0 + rr] = dp[v];
+  }
+  if (Ys) *reinterpret_cast<float4*>(Ys + ((kk0 >> 4) * 16 + rr) * 16 + 4 * g) = d;
+}
+
+__global__ void __launch_bounds__(kThreads) learn_bwd_kernel(LearnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int H = a.H, A = a.A, Ap = a.Apad, K = a.K, B = a.B;
+  float* DH = lds;                        // per head [Apad/16][16][16]
+  float* DHH = DH + H * Ap * kRows;       // [64 H / 16][16][16]
+  float* DH4 = DHH + H * kDH * kRows;
+  float* DH3 = DH4 + kD3 * kRows;
+  float* DH2 = DH3 + kD2 * kRows;
+  float* sg = DH2 + kD1 * kRows;          // [16][K]
+  float* sd = sg + kRows * K;             // [16][K]
+  int* sact = reinterpret_cast<int*>(sd + kRows * K);   // [16][K]
+  const int tile = blockIdx.x, b0 = tile * kRows;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // the TD error per (row, branch): bdq_update / update_policy (:111-126) on the raw heads
+  if (tid < kRows * K) {
+    const int r = tid & 15, k = tid >> 4, b = b0 + r;
+    const int64_t j = row_index(a, b);
+    int ak = a.act[(size_t)j * K + k];
+    ak = ak < 0 ? 0 : (ak >= A ? A - 1 : ak);
+    const float* hs = a.heads + (size_t)b;
+    const size_t ps = (size_t)Ap * B;                // one head's plane
+    auto head = [&](int set, int h) { return hs + ((size_t)set * H + h) * ps; };
+    const float* adv = head(0, k + 1);
+    float s = 0.f;
+    for (int o = 0; o < A; ++o) s += adv[(size_t)o * B];
+    const float current = (head(0, 0)[0] + adv[(size_t)ak * B]) - s / (float)A;
+    const float* adv2 = head(1, k + 1);
+    const float v2 = head(1, 0)[0];
+    float s2 = 0.f;
+    for (int o = 0; o < A; ++o) s2 += adv2[(size_t)o * B];
+    const float m2 = s2 / (float)A;
+    float best = (v2 + adv2[0]) - m2;
+    int am = 0;
+    for (int o = 1; o < A; ++o) {   // torch.argmax: first maximum, NaN is the maximum
+      const float qo = (v2 + adv2[(size_t)o * B]) - m2;
+      const bool take = !isnan(best) && (isnan(qo) || qo > best);
+      best = take ? qo : best;
+      am = take ? o : am;
+    }
+    const float* tadv = head(2, k + 1);
+    float s3 = 0.f;
+    for (int o = 0; o < A; ++o) s3 += tadv[(size_t)o * B];
+    const float tnext = (head(2, 0)[0] + tadv[(size_t)am * B]) - s3 / (float)A;
+    const float expected = a.rew[j] + (tnext * a.gamma) * (float)a.done[j];
+    const float d = expected - current;
+    sd[r * K + k] = d * d;
+    sg[r * K + k] = 2.f * (current - expected) / (float)(B * K);
+    sact[r * K + k] = ak;
+  }
+  __syncthreads();
+  // the gradient at the head outputs: d/d adv[k][o] = g ([o == a_k] - 1/A), d/d v = sum_k g
+  for (int e = tid; e < H * Ap * kRows; e += kThreads) {
+    const int oi = e & 15, r = (e >> 4) & 15, hb = e >> 8;   // hb = h * Apad/16 + o/16
+    const int h = hb / (Ap / 16), o = 16 * (hb - h * (Ap / 16)) + oi;
+    float val = 0.f;
+    if (o < A) {
+      if (h == 0) {
+        if (o == 0)
+          for (int k = 0; k < K; ++k) val += sg[r * K + k];
+      } else {
+        const float gk = sg[r * K + h - 1];
+        val = (o == sact[r * K + h - 1] ? gk : 0.f) - gk / (float)A;
+      }
+    }
+    DH[e] = val;
+    a.dheads[((size_t)h * Ap + o) * B + b0 + r] = val;
+  }
+  if (tid == 0) {
+    float s = 0.f;
+    for (int p = 0; p < kRows * K; ++p) s += sd[p];
+    a.partial[tile] = s;
+    if (tile == 0) a.step[0] += 1.f;   // Adam's step count, read by learn_apply
+  }
+  __syncthreads();
+  for (int tt = wave; tt < H * (kDH / 16); tt += kWaves) {   // second head layers: Apad -> 64 per head
+    const int h = tt / (kDH / 16), c0 = 16 * (tt - h * (kDH / 16));
+    const f32x4 acc = bwd_tile(a.P + a.off[H2_W] + (size_t)h * A * kDH, kDH, c0, Ap / 16, A, DH + h * Ap * kRows, lane);
+    bwd_store(acc, a.hh, h * kDH + c0, a.slope, DHH, a.dhh, B, b0, lane);
+  }
+  __syncthreads();
+  if (wave < kD3 / 16) {   // first head layers: 64 H -> 32
+    const f32x4 acc = bwd_tile(a.P + a.off[H1_W], kD3, 16 * wave, H * kDH / 16, H * kDH, DHH, lane);
+    bwd_store(acc, a.h4, 16 * wave, a.slope, DH4, a.dh4, B, b0, lane);
+  }
+  __syncthreads();
+  if (wave < kD2 / 16) {   // 32 -> 64
+    const f32x4 acc = bwd_tile(a.P + a.off[L4_W], kD2, 16 * wave, kD3 / 16, kD3, DH4, lane);
+    bwd_store(acc, a.h3, 16 * wave, a.slope, DH3, a.dh3, B, b0, lane);
+  }
+  __syncthreads();
+  if (wave < kD1 / 16) {   // 64 -> 128
+    const f32x4 acc = bwd_tile(a.P + a.off[L3_W], kD1, 16 * wave, kD2 / 16, kD2, DH3, lane);
+    bwd_store(acc, a.h2, 16 * wave, a.slope, DH2, a.dh2, B, b0, lane);
+  }
+  __syncthreads();
+  for (int tt = wave; tt < kD0 / 16; tt += kWaves) {   // 128 -> 256: the bilinear layer's output gradient
+    const f32x4 acc = bwd_tile(a.P + a.off[L2_W], kD0, 16 * tt, kD1 / 16, kD1, DH2, lane);
+    bwd_store(acc, a.y1, 16 * tt, a.slope, nullptr, a.g1, B, b0, lane);
+  }
+}
+
+// ---- Adam (torch.optim.Adam, fused, defaults but lr: bdq_model/__init__.py:34) on one element,
+// after clamping its gradient to [-c, c] (torch.clamp: NaN stays NaN)
+__device__ __forceinline__ void adam(const LearnArgs& a, int64_t i, float g, float bc1, float bc2s) {
+  g = isnan(g) ? g : fminf(fmaxf(g, -a.clampv), a.clampv);
+  if (a.grad) a.grad[i] = g;
+  const float m = a.b1 * a.m[i] + (1.f - a.b1) * g;
+  const float v = a.b2 * a.v[i] + (1.f - a.b2) * g * g;
+  a.m[i] = m;
+  a.v[i] = v;
+  const float denom = sqrtf(v) / bc2s + a.eps;
+  a.P[i] -= (a.lr / bc1) * m / denom;
+}
+
+// T[t][i][o] = sum_j target_t[j] W[o][i][j] in j order (pbn_bdq_pack computes the same sums)
+__device__ __forceinline__ float table_entry(const LearnArgs& a, int t, const float* __restrict__ wrow, int stride) {
+  const uint32_t* ts = a.att_states + (size_t)a.att_start[t] * a.W;
+  float s = 0.f;
+  for (int j = 0; j < a.N; ++j) {
+    const bool on = (ts[j >> 5] >> (j & 31)) & 1u;
+    s += on ? wrow[j * stride] : 0.f;
+  }
+  return s;
+}
+
+struct Dense {
+  const float* dY;
+  const float* X;
+  int64_t w_off, b_off;
+  int ldw, o_valid, k_tiles;
+};
+
+template <int NT>
+__global__ void __launch_bounds__(64 * kApplyWaves) learn_apply_kernel(LearnArgs a) {
+  __shared__ float wsc[kApplyWaves][16][kMaxNT * 16 + 1];   // a bilinear tile's new weights, per wave
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, rr = lane & 15;
+  const int B = a.B;
+  if (blockIdx.x == 0 && tid == 0) {
+    float s = 0.f;
+    for (int p = 0; p < B / kRows; ++p) s += a.partial[p];
+    a.loss[0] = s / (float)(B * a.K);
+  }
+  const float stepc = a.step[0];
+  const float bc1 = 1.f - powf(a.b1, stepc);
+  const float bc2s = sqrtf(1.f - powf(a.b2, stepc));
+  int task = blockIdx.x * kApplyWaves + wave;
+  const int n_bil = 16 * a.N;
+  if (task < n_bil) {
+    // bilinear weight tile: outputs o0..o0+15 of input i, all j: D[o][j] = sum_r g1[o][r] s_i[r] t_j[r]
+    const int ot = task / a.N, i = task - ot * a.N, o0 = 16 * ot;
+    const uint32_t* si = a.srow + (size_t)(i >> 5) * B;
+    const float* grow = a.g1 + (size_t)(o0 + rr) * B;
+    f32x4 acc[NT];
+#pragma unroll
+    for (int jt = 0; jt < NT; ++jt) acc[jt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float bsum = 0.f;
+    for (int r0 = 0; r0 < B; r0 += 16) {
+      float4 y = *reinterpret_cast<const float4*>(grow + r0 + 4 * g);
+      bsum += (y.x + y.y) + (y.z + y.w);
+      const uint4 sv = *reinterpret_cast<const uint4*>(si + r0 + 4 * g);
+      const uint32_t sh = i & 31;
+      y.x = (sv.x >> sh) & 1u ? y.x : 0.f;
+      y.y = (sv.y >> sh) & 1u ? y.y : 0.f;
+      y.z = (sv.z >> sh) & 1u ? y.z : 0.f;
+      y.w = (sv.w >> sh) & 1u ? y.w : 0.f;
+#pragma unroll
+      for (int jt = 0; jt < NT; ++jt) {
+        const int jj = 16 * jt + rr;
+        const uint4 tv = *reinterpret_cast<const uint4*>(a.trow + (size_t)(jj >> 5) * B + r0 + 4 * g);
+        const uint32_t tsh = jj & 31;
+        acc[jt] = mfma(y.x, (float)((tv.x >> tsh) & 1u), acc[jt]);
+        acc[jt] = mfma(y.y, (float)((tv.y >> tsh) & 1u), acc[jt]);
+        acc[jt] = mfma(y.z, (float)((tv.z >> tsh) & 1u), acc[jt]);
+        acc[jt] = mfma(y.w, (float)((tv.w >> tsh) & 1u), acc[jt]);
+      }
+    }
+    const int64_t NN = (int64_t)a.N * a.N;
+#pragma unroll
+    for (int jt = 0; jt < NT; ++jt) {
+      const int jj = 16 * jt + rr;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int o = o0 + 4 * g + v;
+        float nw = 0.f;
+        if (jj < a.N) {
+          const int64_t pi = a.off[BIL_W] + o * NN + (int64_t)i * a.N + jj;
+          adam(a, pi, acc[jt][v], bc1, bc2s);
+          nw = a.P[pi];
+        }
+        wsc[wave][4 * g + v][jj] = nw;
+      }
+    }
+    if (i == 0) {   // the bilinear bias: sum over the batch of g1 (lane groups added in a fixed order)
+      bsum += __shfl_xor(bsum, 16);
+      bsum += __shfl_xor(bsum, 32);
+      if (g == 0) adam(a, a.off[BIL_B] + o0 + rr, bsum, bc1, bc2s);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // the target-table rows of input i for these 16 outputs, from the weights just written
+    for (int t = g; t < a.n_attr; t += 4) {
+      const float s = table_entry(a, t, &wsc[wave][rr][0], 1);
+      a.Tq[((size_t)t * a.N + i) * 256 + rr * 16 + ot] = s;
+    }
+    return;
+  }
+  task -= n_bil;
+  // dense layers: (layer, output tile, input tile) -> dW[o][k] = sum_r dY[o][r] X[k][r]
+  const int H = a.H, at16 = a.Apad / 16;
+  Dense L;
+  int ot, kt;
+  const int n0 = (kD1 / 16) * (kD0 / 16), n1 = (kD2 / 16) * (kD1 / 16), n2 = (kD3 / 16) * (kD2 / 16),
+            n3 = (H * kDH / 16) * (kD3 / 16), n4 = H * at16 * (kDH / 16);
+  if (task < n0) {
+    L = Dense{a.dh2, a.y1, a.off[L2_W], a.off[L2_B], kD0, kD1, kD0 / 16};
+  } else if ((task -= n0) < n1) {
+    L = Dense{a.dh3, a.h2, a.off[L3_W], a.off[L3_B], kD1, kD2, kD1 / 16};
+  } else if ((task -= n1) < n2) {
+    L = Dense{a.dh4, a.h3, a.off[L4_W], a.off[L4_B], kD2, kD3, kD2 / 16};
+  } else if ((task -= n2) < n3) {
+    L = Dense{a.dhh, a.h4, a.off[H1_W], a.off[H1_B], kD3, H * kDH, kD3 / 16};
+  } else if ((task -= n3) < n4) {
+    const int per = at16 * (kDH / 16);
+    const int h = task / per;
+    task -= h * per;
+    // head h's second layer: rows are its A outputs (the value head has one real output)
+    L = Dense{a.dheads + (size_t)h * a.Apad * B, a.hh + (size_t)h * kDH * B, a.off[H2_W] + (int64_t)h * a.A * kDH,
+              a.off[H2_B] + (int64_t)h * a.A, kDH, h == 0 ? 1 : a.A, kDH / 16};
+  } else {
+    return;
+  }
+  ot = task / L.k_tiles;
+  kt = task - ot * L.k_tiles;
+  const int o0 = 16 * ot, k0 = 16 * kt;
+  const float* yrow = L.dY + (size_t)(o0 + rr) * B;
+  const float* xrow = L.X + (size_t)(k0 + rr) * B;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+  for (int r0 = 0; r0 < B; r0 += 16) {
+    const float4 y = *reinterpret_cast<const float4*>(yrow + r0 + 4 * g);
+    const float4 x = *reinterpret_cast<const float4*>(xrow + r0 + 4 * g);
+    bsum += (y.x + y.y) + (y.z + y.w);
+    acc = mfma(y.x, x.x, acc);
+    acc = mfma(y.y, x.y, acc);
+    acc = mfma(y.z, x.z, acc);
+    acc = mfma(y.w, x.w, acc);
+  }
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int o = o0 + 4 * g + v;
+    if (o < L.o_valid) adam(a, L.w_off + (int64_t)o * L.ldw + k0 + rr, acc[v], bc1, bc2s);
+  }
+  if (kt == 0) {
+    bsum += __shfl_xor(bsum, 16);
+    bsum += __shfl_xor(bsum, 32);
+    if (g == 0 && o0 + rr < L.o_valid) adam(a, L.b_off + o0 + rr, bsum, bc1, bc2s);
+  }
+}
+
+// the target table of the bilinear layer, [t][i][j][q] = T[t][i][16 q + j] (the layout the
+// acting kernel reads); block (t, i), thread o
+__global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ P, int64_t w_off, int N, int W,
+                                                   const int32_t* __restrict__ att_start,
+                                                   const uint32_t* __restrict__ att_states, float* __restrict__ Tq) {
+  const int t = blockIdx.x / N, i = blockIdx.x - t * N, o = threadIdx.x;
+  const uint32_t* ts = att_states + (size_t)att_start[t] * W;
+  const float* wrow = P + w_off + (int64_t)o * N * N + (int64_t)i * N;
+  float s = 0.f;
+  for (int j = 0; j < N; ++j) {
+    const bool on = (ts[j >> 5] >> (j & 31)) & 1u;
+    s += on ? wrow[j] : 0.f;
+  }
+  Tq[((size_t)t * N + i) * 256 + (o & 15) * 16 + (o >> 4)] = s;
+}
+
+struct Work {
+  int64_t heads, y1, h2, h3, h4, hh, dheads, dhh, dh4, dh3, dh2, g1, srow, trow, partial, total;   // float offsets
+};
+
+Work make_work(int N, int H, int64_t B) {
+  const int A = N + 1, Ap = 16 * ((A + 15) / 16), W = (N + 31) / 32;
+  Work w;
+  int64_t o = 0;
+  auto take = [&](int64_t n) { const int64_t at = o; o += al16(n); return at; };
+  w.heads = take(3LL * H * Ap * B);
+  w.y1 = take(kD0 * B);
+  w.h2 = take(kD1 * B);
+  w.h3 = take(kD2 * B);
+  w.h4 = take(kD3 * B);
+  w.hh = take((int64_t)H * kDH * B);
+  w.dheads = take((int64_t)H * Ap * B);
+  w.dhh = take((int64_t)H * kDH * B);
+  w.dh4 = take(kD3 * B);
+  w.dh3 = take(kD2 * B);
+  w.dh2 = take(kD1 * B);
+  w.g1 = take(kD0 * B);
+  w.srow = take((int64_t)W * B);
+  w.trow = take((int64_t)W * B);
+  w.partial = take(B / kRows);
+  w.total = o;
+  return w;
+}
+
+int check_shape(int N, int n_branches) {
+  if (N < 1 || N > 127) return pbn::set_error(PBN_EINVAL, "fused BDQ update: 1 <= n_nodes <= 127");
+  if (n_branches < 1 || n_branches > 7) return pbn::set_error(PBN_EINVAL, "fused BDQ update: n_branches 1..7");
+  return PBN_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pbn_bdq_layout(int32_t n_nodes, int32_t n_branches, int64_t* offsets) {
+  int rc = check_shape(n_nodes, n_branches);
+  if (rc) return rc;
+  if (!offsets) return pbn::set_error(PBN_EINVAL, "null offsets");
+  make_layout(n_nodes, n_branches + 1, offsets);
+  return PBN_OK;
+}
+
+int pbn_bdq_learn_workspace(int32_t n_nodes, int32_t n_branches, int64_t batch, int64_t* bytes) {
+  int rc = check_shape(n_nodes, n_branches);
+  if (rc) return rc;
+  if (!bytes) return pbn::set_error(PBN_EINVAL, "null bytes");
+  if (batch < kRows || batch % kRows || batch > (1 << 20))
+    return pbn::set_error(PBN_EINVAL, "fused BDQ update: batch a multiple of 16, 16..2^20");
+  *bytes = make_work(n_nodes, n_branches + 1, batch).total * (int64_t)sizeof(float);
+  return PBN_OK;
+}
+
+int pbn_bdq_pack(const pbn_net* net, int32_t n_branches, const float* d_params, float* d_Tq, void* stream) {
+  pbn::NetView v;
+  int rc = pbn::net_view(net, &v);
+  if (rc) return rc;
+  if ((rc = pbn::check_device(net))) return rc;
+  if ((rc = check_shape(v.n_nodes, n_branches))) return rc;
+  if (v.n_attr == 0) return PBN_OK;
+  if (!d_params || !d_Tq) return pbn::set_error(PBN_EINVAL, "null buffer");
+  int64_t off[TOTAL + 1];
+  make_layout(v.n_nodes, n_branches + 1, off);
+  hipLaunchKernelGGL(pack_kernel, dim3(v.n_attr * v.n_nodes), dim3(256), 0, (hipStream_t)stream, d_params, off[BIL_W],
+                     v.n_nodes, v.W, v.att_start, v.att_states, d_Tq);
+  if (hipGetLastError() != hipSuccess) return pbn::set_error(PBN_EDEVICE, "pack_kernel launch failed");
+  return PBN_OK;
+}
+
+int pbn_bdq_learn(const pbn_net* net, int64_t batch, const int64_t* d_idx, int64_t capacity, const uint32_t* d_state,
+                  const uint32_t* d_next_state, const uint8_t* d_target, const int32_t* d_action, int32_t n_branches,
+                  const float* d_reward, const uint8_t* d_done, float* d_params, float* d_Tq,
+                  const float* d_target_params, const float* d_target_Tq, float* d_adam_m, float* d_adam_v,
+                  float* d_adam_step, float lr, float beta1, float beta2, float eps, float gamma, float grad_clamp,
+                  float slope, void* d_workspace, int64_t workspace_bytes, float* d_loss, float* d_grad,
+                  void* stream) {
+  pbn::NetView nv;
+  int rc = pbn::net_view(net, &nv);
+  if (rc) return rc;
+  if ((rc = pbn::check_device(net))) return rc;
+  const int N = nv.n_nodes;
+  if ((rc = check_shape(N, n_branches))) return rc;
+  int64_t need = 0;
+  if ((rc = pbn_bdq_learn_workspace(N, n_branches, batch, &need))) return rc;
+  if (capacity < 1) return pbn::set_error(PBN_EINVAL, "capacity >= 1");
+  if (workspace_bytes < need) return pbn::set_error(PBN_EINVAL, "workspace too small (pbn_bdq_learn_workspace)");
+  if (!d_idx || !d_state || !d_next_state || !d_target || !d_action || !d_reward || !d_done || !d_params ||
+      !d_target_params || !d_adam_m || !d_adam_v || !d_adam_step || !d_workspace || !d_loss)
+    return pbn::set_error(PBN_EINVAL, "null buffer");
+  if (nv.n_attr > 0 && (!d_Tq || !d_target_Tq)) return pbn::set_error(PBN_EINVAL, "null target table");
+  for (const void* p : {(const void*)d_params, (const void*)d_target_params, (const void*)d_adam_m,
+                        (const void*)d_adam_v, (const void*)d_workspace, (const void*)d_Tq, (const void*)d_target_Tq})
+    if ((uintptr_t)p & 15u) return pbn::set_error(PBN_EINVAL, "parameter, table and workspace buffers: 16-byte aligned");
+  const int H = n_branches + 1, A = N + 1;
+  LearnArgs a;
+  a.idx = d_idx;
+  a.B = (int)batch;
+  a.cap = capacity;
+  a.st = d_state;
+  a.nst = d_next_state;
+  a.tgt = d_target;
+  a.act = d_action;
+  a.rew = d_reward;
+  a.done = d_done;
+  a.att_start = nv.att_start;
+  a.att_states = nv.att_states;
+  a.n_attr = nv.n_attr;
+  a.N = N;
+  a.W = nv.W;
+  a.K = n_branches;
+  a.H = H;
+  a.A = A;
+  a.Apad = 16 * ((A + 15) / 16);
+  a.P = d_params;
+  a.Tq = d_Tq;
+  a.PT = d_target_params;
+  a.TqT = d_target_Tq;
+  a.m = d_adam_m;
+  a.v = d_adam_v;
+  a.step = d_adam_step;
+  make_layout(N, H, a.off);
+  a.lr = lr;
+  a.b1 = beta1;
+  a.b2 = beta2;
+  a.eps = eps;
+  a.gamma = gamma;
+  a.clampv = grad_clamp;
+  a.slope = slope;
+  const Work w = make_work(N, H, batch);
+  float* ws = static_cast<float*>(d_workspace);
+  a.heads = ws + w.heads;
+  a.y1 = ws + w.y1;
+  a.h2 = ws + w.h2;
+  a.h3 = ws + w.h3;
+  a.h4 = ws + w.h4;
+  a.hh = ws + w.hh;
+  a.dheads = ws + w.dheads;
+  a.dhh = ws + w.dhh;
+  a.dh4 = ws + w.dh4;
+  a.dh3 = ws + w.dh3;
+  a.dh2 = ws + w.dh2;
+  a.g1 = ws + w.g1;
+  a.srow = reinterpret_cast<uint32_t*>(ws + w.srow);
+  a.trow = reinterpret_cast<uint32_t*>(ws + w.trow);
+  a.partial = ws + w.partial;
+  a.loss = d_loss;
+  a.grad = d_grad;
+  const hipStream_t s = (hipStream_t)stream;
+  const int tiles = (int)(batch / kRows);
+  const size_t lds_f = ((size_t)(kD0 + kD1 + kD2 + kD3 + kDH * H) * kRows + 2 * 4 * kRows) * sizeof(float);
+  hipLaunchKernelGGL(learn_fwd_kernel, dim3(3 * tiles), dim3(kThreads), lds_f, s, a);
+  if (hipGetLastError() != hipSuccess) return pbn::set_error(PBN_EDEVICE, "learn_fwd_kernel launch failed");
+  const size_t lds_b = ((size_t)(H * a.Apad + H * kDH + kD3 + kD2 + kD1) * kRows + 3 * kRows * n_branches) * sizeof(float);
+  if (lds_b > 64 * 1024 && hipFuncSetAttribute((const void*)learn_bwd_kernel,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_b) != hipSuccess)
+    return pbn::set_error(PBN_EDEVICE, "hipFuncSetAttribute failed");
+  hipLaunchKernelGGL(learn_bwd_kernel, dim3(tiles), dim3(kThreads), lds_b, s, a);
+  if (hipGetLastError() != hipSuccess) return pbn::set_error(PBN_EDEVICE, "learn_bwd_kernel launch failed");
+  const int ntasks = 16 * N + (kD1 / 16) * (kD0 / 16) + (kD2 / 16) * (kD1 / 16) + (kD3 / 16) * (kD2 / 16) +
+                     (H * kDH / 16) * (kD3 / 16) + H * (a.Apad / 16) * (kDH / 16);
+  const dim3 grid((ntasks + kApplyWaves - 1) / kApplyWaves), blk(64 * kApplyWaves);
+  switch ((N + 15) / 16) {
+    case 1: hipLaunchKernelGGL(learn_apply_kernel<1>, grid, blk, 0, s, a); break;
+    case 2: hipLaunchKernelGGL(learn_apply_kernel<2>, grid, blk, 0, s, a); break;
+    case 3: hipLaunchKernelGGL(learn_apply_kernel<3>, grid, blk, 0, s, a); break;
+    case 4: hipLaunchKernelGGL(learn_apply_kernel<4>, grid, blk, 0, s, a); break;
+    case 5: hipLaunchKernelGGL(learn_apply_kernel<5>, grid, blk, 0, s, a); break;
+    case 6: hipLaunchKernelGGL(learn_apply_kernel<6>, grid, blk, 0, s, a); break;
+    case 7: hipLaunchKernelGGL(learn_apply_kernel<7>, grid, blk, 0, s, a); break;
+    default: hipLaunchKernelGGL(learn_apply_kernel<8>, grid, blk, 0, s, a); break;
+  }
+  if (hipGetLastError() != hipSuccess) return pbn::set_error(PBN_EDEVICE, "learn_apply_kernel launch failed");
+  return PBN_OK;
+}
+
+}  // extern "C"

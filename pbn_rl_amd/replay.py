@@ -25,7 +25,8 @@ MSE loss, gradients clamped to [-1, 1] (:129-130), one Adam step, and every
 """
 from __future__ import annotations
 
-from typing import Dict, Optional
+import ctypes
+from typing import Dict, List, Optional
 
 import torch
 import torch.nn.functional as F
@@ -34,7 +35,7 @@ from . import _lib
 from .agent import BatchedBDQ, BranchingQNetwork
 from .vector_env import VectorPBNEnv
 
-__all__ = ["DeviceReplay", "bdq_update", "soft_update", "BDQLearner"]
+__all__ = ["DeviceReplay", "bdq_update", "soft_update", "BDQLearner", "FusedBDQUpdate", "bdq_layout"]
 
 
 class DeviceReplay:
@@ -216,18 +217,157 @@ def bdq_update(q: torch.nn.Module, target: torch.nn.Module, opt: torch.optim.Opt
     return loss.detach()
 
 
+def bdq_layout(n_nodes: int, n_branches: int) -> List[int]:
+    """pbn_bdq_layout: the float offsets of the flat parameter buffer's 12 segments, then its size."""
+    L = _lib.load()
+    off = (ctypes.c_int64 * 13)()
+    _lib.check(L.pbn_bdq_layout(n_nodes, n_branches, off), "pbn_bdq_layout")
+    return list(off)
+
+
+def _bdq_segments(q: BranchingQNetwork):
+    """(parameter, segment, offset within the segment) in pbn_bdq_layout order."""
+    m, A = q.model, q.ac_dim
+    out = [(m[0].bilinear.weight, 0, 0), (m[0].bilinear.bias, 1, 0), (m[2].weight, 2, 0), (m[2].bias, 3, 0),
+           (m[4].weight, 4, 0), (m[4].bias, 5, 0), (m[6].weight, 6, 0), (m[6].bias, 7, 0)]
+    for h, hd in enumerate([q.value_head] + list(q.adv_heads)):
+        out += [(hd[0].weight, 8, h * 64 * 32), (hd[0].bias, 9, h * 64), (hd[2].weight, 10, h * A * 64),
+                (hd[2].bias, 11, h * A)]
+    return out
+
+
+class FusedBDQUpdate:
+    """update_policy (bdq_model/__init__.py:100-139) as three HIP launches (``pbn_bdq_learn``,
+    csrc/pbn_learn.hip) instead of ~100 PyTorch kernels: the online and target networks' forwards,
+    the double-DQN TD loss, the backward, the gradient clamp and the Adam step.
+
+    The networks' parameters move into one flat fp32 buffer each (``pbn_bdq_layout``); their
+    nn.Parameters become views of it, so ``state_dict``, the PyTorch forward and the acting kernel
+    see the same weights.  The online network's bilinear target table (``Tq``, the acting kernel's
+    operand) is rewritten by every update; ``pack()`` recomputes the tables after weights change
+    any other way (a loaded checkpoint), ``soft_update()`` moves the target network halfway
+    (bdq_model/__init__.py:137-139) and repacks its table.  Adam (torch.optim.Adam's arithmetic,
+    betas (0.9, 0.999), eps 1e-8) keeps its moments in buffers of the same layout and its step
+    count on the device (graph-capturable)."""
+
+    def __init__(self, q: BranchingQNetwork, target: BranchingQNetwork, net, branches: int, *, batch_size: int,
+                 learning_rate: float = 1e-4, gamma: float = 0.999, grad_clamp: float = 1.0,
+                 betas=(0.9, 0.999), eps: float = 1e-8, keep_grad: bool = False):
+        spec = net.spec
+        N = spec.n
+        dev = next(q.parameters()).device
+        if dev.type != "cuda":
+            raise ValueError("FusedBDQUpdate runs on the GPU")
+        for m in (q, target):
+            if (not isinstance(m, BranchingQNetwork) or m.n != branches or m.ac_dim != N + 1
+                    or m.model[0].input1_dim != N or m.model[0].input2_dim != N):
+                raise ValueError("FusedBDQUpdate needs BranchingQNetwork((N, N), N + 1, branches) for both networks")
+        self.net, self.N, self.K, self.B = net, N, int(branches), int(batch_size)
+        self.lr, self.gamma, self.grad_clamp = float(learning_rate), float(gamma), float(grad_clamp)
+        self.betas, self.eps = (float(betas[0]), float(betas[1])), float(eps)
+        self.slope = float(q.model[1].negative_slope)
+        self.off = bdq_layout(N, self.K)
+        self.q_flat = self._flatten(q, dev)
+        self.t_flat = self._flatten(target, dev)
+        self.q, self.target = q, target
+        self.m = torch.zeros_like(self.q_flat)
+        self.v = torch.zeros_like(self.q_flat)
+        self.step = torch.zeros(1, dtype=torch.float32, device=dev)
+        n_attr = len(spec.attractors)
+        self.q_table = torch.zeros(n_attr, N, 16, 16, dtype=torch.float32, device=dev)
+        self.t_table = torch.zeros_like(self.q_table)
+        L = _lib.load()
+        nbytes = ctypes.c_int64()
+        _lib.check(L.pbn_bdq_learn_workspace(N, self.K, self.B, ctypes.byref(nbytes)), "pbn_bdq_learn_workspace")
+        self.work = torch.empty((nbytes.value + 3) // 4, dtype=torch.float32, device=dev)
+        self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros_like(self.q_flat) if keep_grad else None
+        H, A = self.K + 1, N + 1
+        o = self.off
+        self._acting = (None, self.q_flat[o[1]:o[1] + 256],
+                        (self.q_flat[o[8]:o[8] + H * 64 * 32].view(H * 64, 32), self.q_flat[o[9]:o[9] + H * 64],
+                         self.q_flat[o[10]:o[10] + H * A * 64].view(H, A, 64),
+                         self.q_flat[o[11]:o[11] + H * A].view(H, 1, A)),
+                        self.q_table)
+        self.pack()
+
+    def _flatten(self, q: BranchingQNetwork, dev) -> torch.Tensor:
+        flat = torch.zeros(self.off[12], dtype=torch.float32, device=dev)
+        with torch.no_grad():
+            for p, seg, extra in _bdq_segments(q):
+                at = self.off[seg] + extra
+                view = flat[at:at + p.numel()].view(p.shape)
+                view.copy_(p.detach())
+                p.data = view
+        return flat
+
+    def _stream(self):
+        return torch.cuda.current_stream(self.q_flat.device).cuda_stream
+
+    def pack(self, which: str = "both") -> None:
+        """Recompute the bilinear target tables (pbn_bdq_pack) of the online and/or target network."""
+        L = _lib.load()
+        with torch.cuda.device(self.q_flat.device):
+            for name, flat, table in (("online", self.q_flat, self.q_table), ("target", self.t_flat, self.t_table)):
+                if which in ("both", name):
+                    _lib.check(L.pbn_bdq_pack(self.net.handle, self.K, flat.data_ptr(), table.data_ptr(),
+                                              self._stream()), "pbn_bdq_pack")
+
+    def soft_update(self) -> None:
+        """target <- target / 2 + online / 2 (soft_update's arithmetic, one pass over the buffer)."""
+        with torch.no_grad():
+            self.t_flat.div_(2).add_(self.q_flat / 2)
+        self.pack("target")
+
+    def acting_pack(self):
+        """BatchedBDQ's weight-derived operands as views of the flat buffer (no assembly kernels)."""
+        return self._acting
+
+    def update(self, replay: "DeviceReplay", idx: torch.Tensor) -> torch.Tensor:
+        """One update on ring rows ``idx`` (int64, ``batch_size`` of them); returns the loss buffer
+        (overwritten by the next update)."""
+        if idx.shape != (self.B,) or idx.dtype != torch.int64:
+            raise ValueError(f"idx must be {self.B} int64 ring indices")
+        L = _lib.load()
+        b1, b2 = self.betas
+        with torch.cuda.device(self.q_flat.device):
+            _lib.check(L.pbn_bdq_learn(self.net.handle, self.B, idx.contiguous().data_ptr(), replay.capacity,
+                                       replay.state.data_ptr(), replay.next_state.data_ptr(), replay.target.data_ptr(),
+                                       replay.action.data_ptr(), self.K, replay.reward.data_ptr(),
+                                       replay.done.data_ptr(), self.q_flat.data_ptr(), self.q_table.data_ptr(),
+                                       self.t_flat.data_ptr(), self.t_table.data_ptr(), self.m.data_ptr(),
+                                       self.v.data_ptr(), self.step.data_ptr(), self.lr, b1, b2, self.eps, self.gamma,
+                                       self.grad_clamp, self.slope, self.work.data_ptr(), self.work.numel() * 4,
+                                       self.loss.data_ptr(), self.grad.data_ptr() if self.grad is not None else None,
+                                       self._stream()), "pbn_bdq_learn")
+        return self.loss[0]
+
+    def grads(self) -> List[torch.Tensor]:
+        """The last update's clamped gradient (keep_grad=True) as views shaped like q.parameters()."""
+        if self.grad is None:
+            raise ValueError("construct with keep_grad=True")
+        g = {id(p): self.grad[self.off[seg] + extra:self.off[seg] + extra + p.numel()].view(p.shape)
+             for p, seg, extra in _bdq_segments(self.q)}
+        return [g[id(p)] for p in self.q.parameters()]
+
+
 class BDQLearner:
     """BranchingDQN.learn (bdq_model/__init__.py:150-238) over a VectorPBNEnv: every frame acts
     for all envs (BatchedBDQ), appends their transitions to the device replay, and, once
     ``learning_starts`` transitions are stored, takes ``updates_per_frame`` update_policy steps.
     Exploration decays linearly from ``epsilon_start`` to ``epsilon_final`` over
-    ``epsilon_decay`` frames after ``learning_starts`` (decrement_epsilon, :141-148)."""
+    ``epsilon_decay`` frames after ``learning_starts`` (decrement_epsilon, :141-148).
+
+    ``fused`` (default: whenever the network is the reference's BranchingQNetwork on the GPU and
+    the batch is a multiple of 16) runs each update as FusedBDQUpdate's three HIP launches; the
+    Adam state is then FusedBDQUpdate's and ``opt`` is None.  ``fused=False`` keeps the PyTorch
+    update (bdq_update + torch.optim.Adam)."""
 
     def __init__(self, env: VectorPBNEnv, qnet: Optional[BranchingQNetwork] = None, *, capacity: int = 10 ** 4,
                  batch_size: int = 256, learning_rate: float = 1e-4, gamma: float = 0.999,
                  target_update: int = 10_000, learning_starts: int = 288, updates_per_frame: int = 1,
                  epsilon_start: float = 1.0, epsilon_final: float = 0.0, epsilon_decay: int = 10_000, seed: int = 0,
-                 graphable: bool = False, blas: Optional[str] = "cublas"):
+                 graphable: bool = False, blas: Optional[str] = "cublas", fused: Optional[bool] = None):
         if not env.keep_final_state:
             raise ValueError("BDQLearner needs the env's final_state (keep_final_state=True)")
         if blas:
@@ -241,9 +381,20 @@ class BDQLearner:
         self.q = self.agent.q.train()
         self.target = BranchingQNetwork((env.n_nodes, env.n_nodes), env.n_nodes + 1, self.agent.branches).to(env.device)
         self.target.load_state_dict(self.q.state_dict())
-        # one fused multi-tensor kernel per step instead of a handful per parameter tensor
-        # capturable keeps Adam's step counts on the device (needed to replay it in a hipGraph)
-        self.opt = torch.optim.Adam(self.q.parameters(), lr=learning_rate, fused=True, capturable=graphable)
+        can_fuse = (env.device.type == "cuda" and self.agent.fused_tail and batch_size % 16 == 0
+                    and env.n_nodes <= 127 and isinstance(self.q, BranchingQNetwork))
+        if fused and not can_fuse:
+            raise ValueError("fused update: the reference BranchingQNetwork on a GPU env, batch a multiple of 16")
+        self.fused: Optional[FusedBDQUpdate] = None
+        self.opt = None
+        if fused if fused is not None else can_fuse:
+            self.fused = FusedBDQUpdate(self.q, self.target, env.net, self.agent.branches, batch_size=batch_size,
+                                        learning_rate=learning_rate, gamma=gamma)
+            self.agent.pack_provider = self.fused.acting_pack
+        else:
+            # one fused multi-tensor kernel per step instead of a handful per parameter tensor
+            # capturable keeps Adam's step counts on the device (needed to replay it in a hipGraph)
+            self.opt = torch.optim.Adam(self.q.parameters(), lr=learning_rate, fused=True, capturable=graphable)
         self.replay = DeviceReplay(max(capacity, env.n_alloc), env.words, self.agent.branches, env.device)
         self.batch_size, self.gamma, self.target_update = batch_size, gamma, target_update
         self.learning_starts = max(learning_starts, batch_size)
@@ -292,14 +443,24 @@ class BDQLearner:
             self.epsilon = max(self.epsilon_final, self.epsilon - self.epsilon_step)
             for _ in range(self.updates_per_frame):
                 idx = self.replay.sample_indices(self.batch_size, self.gen)
-                batch = self.replay.gather(idx, env.net)
-                self.last_loss = bdq_update(self.q, self.target, self.opt, batch, self.gamma,
-                                            target_weights=self._target_weights())
+                self.last_loss = self._update(idx)
                 self.updates += 1
                 if self.updates % self.target_update == 0:
-                    soft_update(self.target, self.q)
-                    self._refresh_target_weights()
+                    self._soft_update()
         return reward, done
+
+    def _update(self, idx: torch.Tensor) -> torch.Tensor:
+        if self.fused is not None:
+            return self.fused.update(self.replay, idx)
+        batch = self.replay.gather(idx, self.env.net)
+        return bdq_update(self.q, self.target, self.opt, batch, self.gamma, target_weights=self._target_weights())
+
+    def _soft_update(self) -> None:
+        if self.fused is not None:
+            self.fused.soft_update()
+        else:
+            soft_update(self.target, self.q)
+            self._refresh_target_weights()
 
     # ---- graph-captured frames -------------------------------------------------------------
     def capture(self, min_updates: int = 3) -> None:
@@ -332,7 +493,8 @@ class BDQLearner:
         self._size_t = torch.full((1,), self.replay.size, dtype=torch.int64, device=dev)
         g = torch.cuda.CUDAGraph()
         g.register_generator_state(self.gen)
-        self.opt.zero_grad(set_to_none=True)
+        if self.opt is not None:
+            self.opt.zero_grad(set_to_none=True)
         with torch.cuda.graph(g):
             self._g_out = self._graph_body()
         self._graph = g
@@ -355,9 +517,7 @@ class BDQLearner:
         loss = None
         for _ in range(self.updates_per_frame):
             idx = self.replay.sample_indices(self.batch_size, self.gen, size_t=self._size_t)
-            batch = self.replay.gather(idx, env.net)
-            loss = bdq_update(self.q, self.target, self.opt, batch, self.gamma,
-                              target_weights=self._target_weights())
+            loss = self._update(idx)
         return env.reward[: env.num_envs], done_all[: env.num_envs], loss
 
     def _replay_frame(self):
@@ -370,8 +530,7 @@ class BDQLearner:
         self.frames += 1
         self.updates += self.updates_per_frame
         if self.updates % self.target_update == 0:
-            soft_update(self.target, self.q)
-            self._refresh_target_weights()
+            self._soft_update()
         reward, done, self.last_loss = self._g_out
         return reward, done
 
