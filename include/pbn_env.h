@@ -366,13 +366,31 @@ int pbn_qnet_flipmask_from_state(const pbn_net* net, uint64_t seed, uint64_t ste
  * reward (float [n]) and done (uint8 [n], nonzero = done) go to slot (*d_pos + e) mod capacity of
  * the ring arrays (state / next_state uint32 [words][capacity], target uint8 [capacity], action
  * int32 [capacity][n_branches], reward float [capacity], done uint8 [capacity] as 0/1).  d_pos
- * (int64, device memory) is read, not advanced.  capacity >= n.
+ * (int64, device memory) is read, not advanced.  capacity >= n.  With done_mask != 0, d_done is the
+ * env's flags and done = (flags & done_mask) != 0 (PBN_FLAG_TERMINATED | PBN_FLAG_TRUNCATED: the
+ * frame's done); d_done_out (optional, uint8 [n]) receives the same 0/1.
  */
 int pbn_replay_store(int64_t n, const int64_t* d_pos, int64_t capacity, int32_t words, int32_t n_branches,
                      const uint32_t* d_state, const uint32_t* d_next_state, const uint8_t* d_target,
-                     const int32_t* d_action, const float* d_reward, const uint8_t* d_done, uint32_t* d_ring_state,
-                     uint32_t* d_ring_next_state, uint8_t* d_ring_target, int32_t* d_ring_action,
-                     float* d_ring_reward, uint8_t* d_ring_done, void* stream);
+                     const int32_t* d_action, const float* d_reward, const uint8_t* d_done, uint32_t done_mask,
+                     uint8_t* d_done_out, uint32_t* d_ring_state, uint32_t* d_ring_next_state, uint8_t* d_ring_target,
+                     int32_t* d_ring_action, float* d_ring_reward, uint8_t* d_ring_done, void* stream);
+
+/*
+ * A captured learning frame's counters and the update's rows, one single-block launch (no
+ * reference counterpart: the reference keeps these on the host).  All int64 / double / float
+ * one-element device tensors; each optional one is skipped when null:
+ *   n_store > 0   *d_pos = (*d_pos + n_store) mod capacity, *d_size = min(*d_size + n_store, capacity)
+ *   d_step        += 1 (the env step index of the next frame)
+ *   d_eps64       = max(eps_final, *d_eps64 - eps_step) (decrement_epsilon, bdq_model/__init__.py:141-148);
+ *                   d_eps32 its fp32 copy
+ *   n_idx > 0     d_idx int64 [n_idx]: rows uniform over [0, *d_size) with replacement (row b of draw
+ *                 c = *d_counter: mulhi64 of the REPLAY Philox pair of (seed, b, c) and the size);
+ *                 *d_counter then advances by 1
+ */
+int pbn_replay_advance(int64_t n_store, int64_t capacity, int64_t* d_pos, int64_t* d_size, int64_t* d_step,
+                       double* d_eps64, float* d_eps32, double eps_final, double eps_step, int64_t n_idx,
+                       uint64_t seed, int64_t* d_counter, int64_t* d_idx, void* stream);
 
 /*
  * One replay batch for the learner's update (pbn_rl_amd/replay.py DeviceReplay), in one launch:

@@ -51,6 +51,23 @@ def explore_words(seed: int, step: int, env_offset: int, n: int, calls: int = 1)
     return out
 
 
+REPLAY = 7
+
+
+def replay_rows(seed: int, draw: int, n: int, size: int) -> np.ndarray:
+    """The fused learner's replay rows (pbn_replay_advance): row b of draw c is
+    floor((x << 32 | y) * size / 2^64) for the REPLAY-stream Philox words (x, y) of (seed, id = b,
+    step = c) -- uniform with replacement, as DeviceReplay.sample_indices (the reference draws
+    without replacement, random.sample at bdq_model/memory.py:62)."""
+    b = np.arange(n, dtype=np.uint64)
+    c0 = b & np.uint64(0xFFFFFFFF)
+    c1 = np.full(n, draw & 0xFFFFFFFF, dtype=np.uint64)
+    c2 = np.full(n, REPLAY << 28, dtype=np.uint64)
+    c3 = ((b >> np.uint64(32)) & np.uint64(0xFFFF)) | np.uint64(((draw >> 32) & 0xFFFF) << 16)
+    x, y, _, _ = philox_vec(c0, c1, c2, c3, seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+    return np.array([((int(xi) << 32 | int(yi)) * size) >> 64 for xi, yi in zip(x, y)], dtype=np.int64)
+
+
 def obs_unpack(spec, state: np.ndarray, target: np.ndarray) -> np.ndarray:
     """state (W, n) uint32, target (n,) uint8 -> (2, n, N) float32."""
     N = spec.n

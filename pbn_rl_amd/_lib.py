@@ -28,7 +28,7 @@ EXPORTS = ["pbn_net_create", "pbn_net_destroy", "pbn_net_words", "pbn_reset", "p
            "pbn_rollout", "pbn_rollout_ex", "pbn_state_histogram", "pbn_obs_unpack", "pbn_bilinear_targets", "pbn_q_to_flipmask",
            "pbn_q_to_flipmask_dev",
            "pbn_heads_to_flipmask", "pbn_qnet_heads", "pbn_qnet_flipmask", "pbn_qnet_heads_from_state",
-           "pbn_qnet_flipmask_from_state", "pbn_replay_store", "pbn_replay_batch", "pbn_bdq_td_loss", "pbn_bdq_layout", "pbn_bdq_learn_workspace",
+           "pbn_qnet_flipmask_from_state", "pbn_replay_store", "pbn_replay_advance", "pbn_replay_batch", "pbn_bdq_td_loss", "pbn_bdq_layout", "pbn_bdq_learn_workspace",
            "pbn_bdq_pack", "pbn_bdq_learn", "pbn_last_error", "pbn_abi_version"]
 SOURCES = ["pbn_env.hip", "pbn_settle.hip", "pbn_agent.hip", "pbn_qnet.hip", "pbn_learn.hip"]
 
@@ -123,7 +123,8 @@ def load() -> ctypes.CDLL:
     L.pbn_qnet_flipmask_from_state.restype = ctypes.c_int
     L.pbn_last_error.argtypes = []
     L.pbn_last_error.restype = ctypes.c_char_p
-    L.pbn_replay_store.argtypes = [i64, vp, i64, ctypes.c_int32, ctypes.c_int32] + [vp] * 12 + [vp]
+    L.pbn_replay_store.argtypes = ([i64, vp, i64, ctypes.c_int32, ctypes.c_int32] + [vp] * 6 + [u32, vp] + [vp] * 6 +
+                                   [vp])
     L.pbn_replay_store.restype = ctypes.c_int
     L.pbn_replay_batch.argtypes = [vp, i64, vp, i64, vp, vp, vp, vp, ctypes.c_int32, vp, vp, vp, vp, vp, vp, vp]
     L.pbn_replay_batch.restype = ctypes.c_int
@@ -131,15 +132,19 @@ def load() -> ctypes.CDLL:
                                   vp, vp, vp, vp]
     L.pbn_bdq_td_loss.restype = ctypes.c_int
     i32, f32 = ctypes.c_int32, ctypes.c_float
-    L.pbn_bdq_layout.argtypes = [i32, i32, vp]
-    L.pbn_bdq_layout.restype = ctypes.c_int
-    L.pbn_bdq_learn_workspace.argtypes = [i32, i32, i64, vp]
-    L.pbn_bdq_learn_workspace.restype = ctypes.c_int
-    L.pbn_bdq_pack.argtypes = [vp, i32, vp, vp, vp]
-    L.pbn_bdq_pack.restype = ctypes.c_int
-    L.pbn_bdq_learn.argtypes = ([vp, i64, vp, i64, vp, vp, vp, vp, i32, vp, vp] + [vp] * 7 + [f32] * 7 +
-                                [vp, i64, vp, vp, vp])
-    L.pbn_bdq_learn.restype = ctypes.c_int
+    if hasattr(L, "pbn_bdq_learn"):   # (diagnostic builds of older revisions predate the fused update)
+        L.pbn_replay_advance.argtypes = [i64, i64, vp, vp, vp, vp, vp, ctypes.c_double, ctypes.c_double, i64, u64,
+                                         vp, vp, vp]
+        L.pbn_replay_advance.restype = ctypes.c_int
+        L.pbn_bdq_layout.argtypes = [i32, i32, vp]
+        L.pbn_bdq_layout.restype = ctypes.c_int
+        L.pbn_bdq_learn_workspace.argtypes = [i32, i32, i64, vp]
+        L.pbn_bdq_learn_workspace.restype = ctypes.c_int
+        L.pbn_bdq_pack.argtypes = [vp, i32, vp, vp, vp]
+        L.pbn_bdq_pack.restype = ctypes.c_int
+        L.pbn_bdq_learn.argtypes = ([vp, i64, vp, i64, vp, vp, vp, vp, i32, vp, vp] + [vp] * 7 + [f32] * 7 +
+                                    [vp, i64, vp, vp, vp])
+        L.pbn_bdq_learn.restype = ctypes.c_int
     L.pbn_abi_version.argtypes = []
     L.pbn_abi_version.restype = ctypes.c_int
     _lib = L

@@ -15,6 +15,7 @@ struct NetView {
   int n_states;
   const int32_t* att_start;     // device [n_attr + 1]
   const uint32_t* att_states;   // device [n_states * W]
+  const uint32_t* att_first;    // device [n_attr * W]: attractor t's first state (the BDQ target input)
 };
 
 // 0 on success, else a PBN_E* code with pbn_last_error() set

@@ -366,8 +366,8 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 __global__ void __launch_bounds__(kObsThreads) replay_store_kernel(
     int64_t n, const int64_t* __restrict__ pos, int64_t cap, int W, int K, const uint32_t* __restrict__ st,
     const uint32_t* __restrict__ nst, const uint8_t* __restrict__ tgt, const int32_t* __restrict__ act,
-    const float* __restrict__ rew, const uint8_t* __restrict__ done, uint32_t* __restrict__ r_st,
-    uint32_t* __restrict__ r_nst, uint8_t* __restrict__ r_tgt, int32_t* __restrict__ r_act,
+    const float* __restrict__ rew, const uint8_t* __restrict__ done, uint32_t done_mask, uint8_t* __restrict__ done_out,
+    uint32_t* __restrict__ r_st, uint32_t* __restrict__ r_nst, uint8_t* __restrict__ r_tgt, int32_t* __restrict__ r_act,
     float* __restrict__ r_rew, uint8_t* __restrict__ r_done) {
   const int64_t p0 = *pos;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
@@ -379,7 +379,52 @@ __global__ void __launch_bounds__(kObsThreads) replay_store_kernel(
     r_tgt[j] = tgt[e];
     for (int k = 0; k < K; ++k) r_act[(size_t)j * K + k] = act[(size_t)e * K + k];
     r_rew[j] = rew[e];
-    r_done[j] = done[e] ? 1 : 0;
+    const uint8_t d = done_mask ? ((done[e] & done_mask) ? 1 : 0) : (done[e] ? 1 : 0);
+    r_done[j] = d;
+    if (done_out) done_out[e] = d;
+  }
+}
+
+// ---- the learning frame's counters and the update's rows, one single-block launch
+// (pbn_replay_advance): the env step index, the ring position and fill level after n_store
+// transitions, epsilon's linear decay (decrement_epsilon, bdq_model/__init__.py:141-148, in fp64
+// and its fp32 copy), then n_idx ring rows uniform over the new fill level: row b of draw c
+// (*counter) is mulhi64(x << 32 | y, size) of Philox word pair (x, y) = REPLAY(seed, id = b,
+// step = c) -- with replacement, as sample_indices; *counter then advances.  Replaces ~14
+// one-element PyTorch launches of a captured frame.
+__global__ void __launch_bounds__(256) replay_advance_kernel(int64_t n_store, int64_t cap, int64_t* __restrict__ pos,
+                                                             int64_t* __restrict__ size, int64_t* __restrict__ step,
+                                                             double* __restrict__ eps64, float* __restrict__ eps32,
+                                                             double eps_final, double eps_step, int64_t n_idx,
+                                                             uint64_t seed, int64_t* __restrict__ counter,
+                                                             int64_t* __restrict__ idx) {
+  __shared__ int64_t s_size;
+  if (threadIdx.x == 0) {
+    int64_t sz = *size;
+    if (n_store > 0) {
+      *pos = (*pos + n_store) % cap;
+      sz = sz + n_store < cap ? sz + n_store : cap;
+      *size = sz;
+    }
+    if (step) *step += 1;
+    if (eps64) {
+      const double e = *eps64 - eps_step;
+      const double v = isnan(e) ? e : (e > eps_final ? e : eps_final);   // torch.maximum(final, e)
+      *eps64 = v;
+      if (eps32) *eps32 = (float)v;
+    }
+    s_size = sz;
+  }
+  __syncthreads();
+  if (n_idx > 0) {
+    const uint64_t sz = (uint64_t)(s_size > 0 ? s_size : 1);
+    const uint64_t c = (uint64_t)*counter;
+    for (int64_t b = threadIdx.x; b < n_idx; b += blockDim.x) {
+      const pbn::Word4 r = pbn::draw(seed, (uint64_t)b, c, pbn::kStreamReplay, 0);
+      idx[b] = (int64_t)__umul64hi(((uint64_t)r.x << 32) | r.y, sz);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *counter = (int64_t)(c + 1);
   }
 }
 
@@ -675,9 +720,9 @@ int pbn_heads_to_flipmask(const pbn_net* net, uint64_t seed, uint64_t step, cons
 
 int pbn_replay_store(int64_t n, const int64_t* d_pos, int64_t capacity, int32_t words, int32_t n_branches,
                      const uint32_t* d_state, const uint32_t* d_next_state, const uint8_t* d_target,
-                     const int32_t* d_action, const float* d_reward, const uint8_t* d_done, uint32_t* d_ring_state,
-                     uint32_t* d_ring_next_state, uint8_t* d_ring_target, int32_t* d_ring_action,
-                     float* d_ring_reward, uint8_t* d_ring_done, void* stream) {
+                     const int32_t* d_action, const float* d_reward, const uint8_t* d_done, uint32_t done_mask,
+                     uint8_t* d_done_out, uint32_t* d_ring_state, uint32_t* d_ring_next_state, uint8_t* d_ring_target,
+                     int32_t* d_ring_action, float* d_ring_reward, uint8_t* d_ring_done, void* stream) {
   if (n < 1 || capacity < n || words < 1 || words > 4 || n_branches < 1)
     return pbn::set_error(PBN_EINVAL, "n >= 1, capacity >= n, words 1..4, n_branches >= 1");
   if (!d_pos || !d_state || !d_next_state || !d_target || !d_action || !d_reward || !d_done || !d_ring_state ||
@@ -685,8 +730,22 @@ int pbn_replay_store(int64_t n, const int64_t* d_pos, int64_t capacity, int32_t 
     return pbn::set_error(PBN_EINVAL, "null buffer");
   const unsigned blocks = (unsigned)std::min<int64_t>((n + kObsThreads - 1) / kObsThreads, 4096);
   hipLaunchKernelGGL(replay_store_kernel, dim3(blocks), dim3(kObsThreads), 0, (hipStream_t)stream, n, d_pos, capacity,
-                     words, n_branches, d_state, d_next_state, d_target, d_action, d_reward, d_done, d_ring_state,
-                     d_ring_next_state, d_ring_target, d_ring_action, d_ring_reward, d_ring_done);
+                     words, n_branches, d_state, d_next_state, d_target, d_action, d_reward, d_done, done_mask,
+                     d_done_out, d_ring_state, d_ring_next_state, d_ring_target, d_ring_action, d_ring_reward,
+                     d_ring_done);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return pbn::set_error(PBN_EDEVICE, hipGetErrorString(e));
+  return PBN_OK;
+}
+
+int pbn_replay_advance(int64_t n_store, int64_t capacity, int64_t* d_pos, int64_t* d_size, int64_t* d_step,
+                       double* d_eps64, float* d_eps32, double eps_final, double eps_step, int64_t n_idx,
+                       uint64_t seed, int64_t* d_counter, int64_t* d_idx, void* stream) {
+  if (n_store < 0 || capacity < 1 || n_idx < 0) return pbn::set_error(PBN_EINVAL, "n_store >= 0, capacity >= 1, n_idx >= 0");
+  if (!d_size || (n_store > 0 && !d_pos) || (n_idx > 0 && (!d_counter || !d_idx)))
+    return pbn::set_error(PBN_EINVAL, "null buffer");
+  hipLaunchKernelGGL(replay_advance_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, n_store, capacity, d_pos,
+                     d_size, d_step, d_eps64, d_eps32, eps_final, eps_step, n_idx, seed, d_counter, d_idx);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return pbn::set_error(PBN_EDEVICE, hipGetErrorString(e));
   return PBN_OK;

@@ -158,6 +158,7 @@ struct pbn_net {
   uint32_t* d_tab = nullptr;
   int32_t* d_att_start = nullptr;
   uint32_t* d_att_states = nullptr;
+  uint32_t* d_att_first = nullptr;        // [n_attr][W]: each attractor's first state
 };
 
 namespace pbn {
@@ -173,6 +174,7 @@ int net_view(const pbn_net* net, NetView* v) {
   v->n_states = net->n_states;
   v->att_start = net->d_att_start;
   v->att_states = net->d_att_states;
+  v->att_first = net->d_att_first;
   return PBN_OK;
 }
 
@@ -195,6 +197,7 @@ void free_net(pbn_net* net) {
   (void)hipFree(net->d_tab);
   (void)hipFree(net->d_att_start);
   (void)hipFree(net->d_att_states);
+  (void)hipFree(net->d_att_first);
   delete net;
 }
 
@@ -613,6 +616,9 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     if (!strcmp(env, "lean")) net->force_roll = 2;
     if (!strcmp(env, "pipe")) net->force_roll = 3;
   }
+  std::vector<uint32_t> att_first((size_t)A * W);
+  for (int t = 0; t < A; ++t)
+    for (int w = 0; w < W; ++w) att_first[(size_t)t * W + w] = d->attractor_states[(size_t)d->attractor_start[t] * W + w];
   int rc;
   if (hipGetDevice(&net->device) != hipSuccess) {
     free_net(net);
@@ -625,7 +631,8 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
       (rc = upload(&net->d_nrec, nrec.data(), nrec.size())) ||
       (rc = upload(&net->d_tab, tab.data(), tab.size())) ||
       (rc = upload(&net->d_att_start, A ? d->attractor_start : nullptr, (size_t)A + 1)) ||
-      (rc = upload(&net->d_att_states, S ? d->attractor_states : nullptr, (size_t)S * W))) {
+      (rc = upload(&net->d_att_states, S ? d->attractor_states : nullptr, (size_t)S * W)) ||
+      (rc = upload(&net->d_att_first, A ? att_first.data() : nullptr, (size_t)A * W))) {
     free_net(net);
     return rc;
   }

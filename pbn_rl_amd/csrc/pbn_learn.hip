@@ -80,8 +80,7 @@ struct LearnArgs {
   const float* rew;
   const uint8_t* done;
   // the network's attractor table (first state of attractor t: the target half of the input)
-  const int32_t* att_start;
-  const uint32_t* att_states;
+  const uint32_t* att_first;   // [n_attr][W]
   int n_attr, N, W, K, H, A, Apad;
   // parameters (online, updated in place; target, read), their target tables, Adam's state
   float* P;
@@ -94,7 +93,7 @@ struct LearnArgs {
   int64_t off[TOTAL + 1];
   float lr, b1, b2, eps, gamma, clampv, slope;
   // workspace: [feature][B] planes
-  float* heads;   // [3][H][Apad][B]
+  float* heads;   // [3][H][B][Apad]: a row's outputs contiguous (the TD pass reads them by rows)
   float* y1;      // [256][B]  online s rows, after the activation
   float* h2;      // [128][B]
   float* h3;      // [64][B]
@@ -111,7 +110,22 @@ struct LearnArgs {
   float* partial; // [B / 16]
   float* loss;
   float* grad;    // optional: the clamped gradient, parameter layout
+  unsigned long long* stamps;   // diagnostic builds (PBN_STAMPS): [kernel][block][wave][32] s_memtime
 };
+
+// Diagnostic phase clocks (tools/learn_stamps.py): lane 0 of every wave of the first 1,024 blocks
+// stores s_memtime at numbered points of each kernel (below), and s_memrealtime at entry (31)
+constexpr int kLStampRow = 32;
+#ifdef PBN_STAMPS
+#define PBN_LSTAMP(k, i)                                                                                      \
+  do {                                                                                                      \
+    if (a.stamps && (threadIdx.x & 63) == 0 && blockIdx.x < 1024)                                           \
+      a.stamps[(((size_t)(k) * 1024 + blockIdx.x) * 8 + (threadIdx.x >> 6)) * kLStampRow + (i)] =           \
+          (i) == 31 ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();                      \
+  } while (0)
+#else
+#define PBN_LSTAMP(k, i) do {} while (0)
+#endif
 
 __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -129,18 +143,29 @@ __device__ __forceinline__ int64_t row_index(const LearnArgs& a, int b) {
 // (g = lane >> 4, r = lane & 15).  D[o][r] = sum_k W[o][k] X[k][r] for the 16 outputs o0..o0+15:
 // lane l supplies A[o0 + (l & 15)][k] = one float4 of weight row o0 + (l & 15); its accumulator
 // holds D[o0 + 4g + v][r], v = 0..3.
+// The weight fragments come in registers, loaded by wfrag before the layer's inputs are ready
+// (every layer's fragments are requested at kernel entry: one L2 round trip, not one per layer).
 template <int K>
-__device__ __forceinline__ f32x4 fwd_tile(const float* __restrict__ W, int ldw, int o0, int o_valid,
-                                          const float* __restrict__ Xs, int lane) {
+__device__ __forceinline__ void wfrag(float4 (&w)[K / 16], const float* __restrict__ W, int ldw, int o0, int o_valid,
+                                      int lane) {
   const int g = lane >> 4, rr = lane & 15;
   const int o = o0 + rr;
   const bool ov = o < o_valid;
   const float* wrow = W + (size_t)(ov ? o : 0) * ldw + 4 * g;
+#pragma unroll
+  for (int kb = 0; kb < K / 16; ++kb) {
+    w[kb] = *reinterpret_cast<const float4*>(wrow + kb * 16);
+    if (!ov) w[kb] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+template <int K>
+__device__ __forceinline__ f32x4 fwd_tile(const float4 (&wf)[K / 16], const float* __restrict__ Xs, int lane) {
+  const int g = lane >> 4, rr = lane & 15;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int kb = 0; kb < K / 16; ++kb) {
-    float4 w = *reinterpret_cast<const float4*>(wrow + kb * 16);
-    if (!ov) w = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 w = wf[kb];
     const float4 x = *reinterpret_cast<const float4*>(Xs + (kb * 16 + rr) * 16 + 4 * g);
     acc = mfma(w.x, x.x, acc);
     acc = mfma(w.y, x.y, acc);
@@ -179,52 +204,74 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
   const int b0 = (blockIdx.x - set * tiles) * kRows;
   const float* P = set == 2 ? a.PT : a.P;
   const float* Tq = set == 2 ? a.TqT : a.Tq;
+  PBN_LSTAMP(0, 31);
+  PBN_LSTAMP(0, 0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int B = a.B;
   float* keep = nullptr;   // the online s rows keep their activations for the backward
-  if (tid < kRows) {
+  if (tid < kRows) {   // the rows' targets and state words (the backward keeps them for learn_apply)
     const int64_t j = row_index(a, b0 + tid);
-    const int tg = a.tgt[j];
-    stg[tid] = tg;
-    for (int w = 0; w < a.W; ++w) {
-      const uint32_t s = (set == 0 ? a.st : a.nst)[(size_t)w * a.cap + j];
-      sw[w * kRows + tid] = s;
-      if (set == 0) {
-        a.srow[(size_t)w * B + b0 + tid] = s;
-        a.trow[(size_t)w * B + b0 + tid] = tg < a.n_attr ? a.att_states[(size_t)a.att_start[tg] * a.W + w] : 0u;
-      }
-    }
+    stg[tid] = a.tgt[j];
+    for (int w = 0; w < a.W; ++w) sw[w * kRows + tid] = (set == 0 ? a.st : a.nst)[(size_t)w * a.cap + j];
   }
   __syncthreads();
+  PBN_LSTAMP(0, 1);
+  // every layer's weight fragments of this wave, requested now (they arrive during the bilinear
+  // layer): its trunk tiles, its first two first-head-layer tiles and its first second-layer tile
+  // (more heads or outputs than that load theirs in the layer's loop)
+  const int at16 = a.Apad / 16;
+  float4 w2[kD0 / 16], w3[kD1 / 16], w4[kD2 / 16], wh1[2][kD3 / 16], wh2[kDH / 16];
+  wfrag<kD0>(w2, P + a.off[L2_W], kD0, 16 * wave, kD1, lane);
+  wfrag<kD1>(w3, P + a.off[L3_W], kD1, 16 * (wave & 3), kD2, lane);
+  wfrag<kD2>(w4, P + a.off[L4_W], kD2, 16 * (wave & 1), kD3, lane);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) wfrag<kD3>(wh1[u], P + a.off[H1_W], kD3, 16 * (wave + kWaves * u), a.H * kDH, lane);
+  {
+    const int tt = wave < a.H * at16 ? wave : 0, h = tt / at16;
+    wfrag<kDH>(wh2, P + a.off[H2_W] + (size_t)h * a.A * kDH, kDH, 16 * (tt - h * at16), a.A, lane);
+  }
   // bilinear layer: y[o] = bias[o] + sum over the set bits i of T[t][i][o] (t = the row's target;
   // a row without a target has an all-zero second input: bias only).  Wave w takes rows 2w, 2w+1;
-  // lane p reads Tq positions 4p..4p+3 ([t][i][j][q] = T[t][i][16 q + j]: o = 16 q + j).
+  // lane p reads Tq positions 4p..4p+3 ([t][i][j][q] = T[t][i][16 q + j]: o = 16 q + j), eight
+  // table rows of both rows per round trip.
   {
     const float* bias = P + a.off[BIL_B];
+    const int r0 = 2 * wave;
+    const int t0 = stg[r0], t1 = stg[r0 + 1];
+    const bool h0 = t0 < a.n_attr, h1 = t1 < a.n_attr;
+    float4 acc[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+    if (h0 || h1) {
+      const float* T0 = Tq + (size_t)(h0 ? t0 : 0) * a.N * 256 + 4 * lane;
+      const float* T1 = Tq + (size_t)(h1 ? t1 : 0) * a.N * 256 + 4 * lane;
+      for (int i0 = 0; i0 < a.N; i0 += 8) {
+        float4 x0[8], x1[8];
 #pragma unroll
-    for (int rr = 0; rr < 2; ++rr) {
-      const int r = 2 * wave + rr;
-      const int t = stg[r];
-      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (t < a.n_attr) {
-        const float* T = Tq + (size_t)t * a.N * 256 + 4 * lane;
-        for (int i0 = 0; i0 < a.N; i0 += 4) {
-          float4 x[4];
+        for (int u = 0; u < 8; ++u) {
+          const size_t ii = (size_t)min(i0 + u, a.N - 1) * 256;
+          x0[u] = *reinterpret_cast<const float4*>(T0 + ii);
+          x1[u] = *reinterpret_cast<const float4*>(T1 + ii);
+        }
 #pragma unroll
-          for (int u = 0; u < 4; ++u) x[u] = i0 + u < a.N ? *reinterpret_cast<const float4*>(T + (size_t)(i0 + u) * 256)
-                                                          : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int i = i0 + u;
-            const bool on = i < a.N && ((sw[(i >> 5) * kRows + r] >> (i & 31)) & 1u);
-            acc.x += on ? x[u].x : 0.f;
-            acc.y += on ? x[u].y : 0.f;
-            acc.z += on ? x[u].z : 0.f;
-            acc.w += on ? x[u].w : 0.f;
-          }
+        for (int u = 0; u < 8; ++u) {
+          const int i = i0 + u;
+          const uint32_t wi = sw[(min(i, a.N - 1) >> 5) * kRows + r0], wj = sw[(min(i, a.N - 1) >> 5) * kRows + r0 + 1];
+          const bool on0 = h0 && i < a.N && ((wi >> (i & 31)) & 1u);
+          const bool on1 = h1 && i < a.N && ((wj >> (i & 31)) & 1u);
+          acc[0].x += on0 ? x0[u].x : 0.f;
+          acc[0].y += on0 ? x0[u].y : 0.f;
+          acc[0].z += on0 ? x0[u].z : 0.f;
+          acc[0].w += on0 ? x0[u].w : 0.f;
+          acc[1].x += on1 ? x1[u].x : 0.f;
+          acc[1].y += on1 ? x1[u].y : 0.f;
+          acc[1].z += on1 ? x1[u].z : 0.f;
+          acc[1].w += on1 ? x1[u].w : 0.f;
         }
       }
-      const float* ap = &acc.x;
+    }
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      const int r = r0 + rr;
+      const float* ap = &acc[rr].x;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int o = 16 * (4 * (lane & 3) + c) + (lane >> 2);
@@ -234,66 +281,74 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
       }
     }
   }
+  PBN_LSTAMP(0, 2);
   __syncthreads();
+  PBN_LSTAMP(0, 3);
   if (set == 0) keep = a.h2;
   {   // 256 -> 128: one output tile per wave
-    const f32x4 acc = fwd_tile<kD0>(P + a.off[L2_W], kD0, 16 * wave, kD1, Y1, lane);
+    const f32x4 acc = fwd_tile<kD0>(w2, Y1, lane);
     fwd_store(acc, P + a.off[L2_B], 16 * wave, a.slope, X2, keep, B, b0, lane);
   }
+  PBN_LSTAMP(0, 4);
   __syncthreads();
+  PBN_LSTAMP(0, 5);
   if (wave < kD2 / 16) {   // 128 -> 64
-    const f32x4 acc = fwd_tile<kD1>(P + a.off[L3_W], kD1, 16 * wave, kD2, X2, lane);
+    const f32x4 acc = fwd_tile<kD1>(w3, X2, lane);
     fwd_store(acc, P + a.off[L3_B], 16 * wave, a.slope, X3, set == 0 ? a.h3 : nullptr, B, b0, lane);
   }
   __syncthreads();
+  PBN_LSTAMP(0, 6);
   if (wave < kD3 / 16) {   // 64 -> 32
-    const f32x4 acc = fwd_tile<kD2>(P + a.off[L4_W], kD2, 16 * wave, kD3, X3, lane);
+    const f32x4 acc = fwd_tile<kD2>(w4, X3, lane);
     fwd_store(acc, P + a.off[L4_B], 16 * wave, a.slope, X4, set == 0 ? a.h4 : nullptr, B, b0, lane);
   }
   __syncthreads();
-  for (int tt = wave; tt < a.H * kDH / 16; tt += kWaves) {   // the H first head layers: 32 -> 64 H
-    const f32x4 acc = fwd_tile<kD3>(P + a.off[H1_W], kD3, 16 * tt, a.H * kDH, X4, lane);
-    fwd_store(acc, P + a.off[H1_B], 16 * tt, a.slope, XH, set == 0 ? a.hh : nullptr, B, b0, lane);
+  PBN_LSTAMP(0, 7);
+  {   // the H first head layers: 32 -> 64 H
+    const int n1 = a.H * kDH / 16;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int tt = wave + kWaves * u;
+      if (tt < n1) {
+        const f32x4 acc = fwd_tile<kD3>(wh1[u], X4, lane);
+        fwd_store(acc, P + a.off[H1_B], 16 * tt, a.slope, XH, set == 0 ? a.hh : nullptr, B, b0, lane);
+      }
+    }
+    for (int tt = wave + 2 * kWaves; tt < n1; tt += kWaves) {
+      float4 wl[kD3 / 16];
+      wfrag<kD3>(wl, P + a.off[H1_W], kD3, 16 * tt, a.H * kDH, lane);
+      const f32x4 acc = fwd_tile<kD3>(wl, X4, lane);
+      fwd_store(acc, P + a.off[H1_B], 16 * tt, a.slope, XH, set == 0 ? a.hh : nullptr, B, b0, lane);
+    }
   }
   __syncthreads();
-  // second head layers: head h, outputs 16 at .. (A of them, no activation) -> heads[set][h][a][b]
-  const int at16 = a.Apad / 16;
-  for (int tt = wave; tt < a.H * at16; tt += kWaves) {
+  PBN_LSTAMP(0, 8);
+  // second head layers: head h, outputs 16 at .. (A of them, no activation) -> heads[set][h][b][a]
+  auto head_out = [&](const float4 (&wl)[kDH / 16], int tt) {
     const int h = tt / at16, o0 = 16 * (tt - h * at16);
-    const f32x4 acc = fwd_tile<kDH>(P + a.off[H2_W] + (size_t)h * a.A * kDH, kDH, o0, a.A, XH + h * kDH * kRows, lane);
+    const f32x4 acc = fwd_tile<kDH>(wl, XH + h * kDH * kRows, lane);
     const int g = lane >> 4, rr = lane & 15;
     const float* b2 = P + a.off[H2_B] + (size_t)h * a.A;
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int o = o0 + 4 * g + v;
-      if (o < a.A) a.heads[(((size_t)set * a.H + h) * a.Apad + o) * B + b0 + rr] = acc[v] + b2[o];
+      if (o < a.A) a.heads[(((size_t)set * a.H + h) * B + b0 + rr) * a.Apad + o] = acc[v] + b2[o];
     }
+  };
+  if (wave < a.H * at16) head_out(wh2, wave);
+  for (int tt = wave + kWaves; tt < a.H * at16; tt += kWaves) {
+    const int h = tt / at16;
+    float4 wl[kDH / 16];
+    wfrag<kDH>(wl, P + a.off[H2_W] + (size_t)h * a.A * kDH, kDH, 16 * (tt - h * at16), a.A, lane);
+    head_out(wl, tt);
   }
+  PBN_LSTAMP(0, 9);
 }
 
 // ---- backward tiles: dX[k][r] = sum_o W[o][k] dY[o][r] for the 16 inputs k0..k0+15 (A operand
 // lane l: W[o][k0 + (l & 15)] for the k-step's o = 16 ob + 4g + v; B operand: the blocked dY
-// plane, as the forward's X).  Its accumulator holds dX[k0 + 4g + v][r].
-__device__ __forceinline__ f32x4 bwd_tile(const float* __restrict__ W, int ldw, int k0, int n_ob, int o_valid,
-                                          const float* __restrict__ dYs, int lane) {
-  const int g = lane >> 4, rr = lane & 15;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int ob = 0; ob < n_ob; ++ob) {
-    float w[4];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int o = 16 * ob + 4 * g + v;
-      w[v] = o < o_valid ? W[(size_t)o * ldw + k0 + rr] : 0.f;
-    }
-    const float4 y = *reinterpret_cast<const float4*>(dYs + (ob * 16 + rr) * 16 + 4 * g);
-    acc = mfma(w[0], y.x, acc);
-    acc = mfma(w[1], y.y, acc);
-    acc = mfma(w[2], y.z, acc);
-    acc = mfma(w[3], y.w, acc);
-  }
-  return acc;
-}
-
+// plane, as the forward's X).  The accumulator holds dX[k0 + 4g + v][r].  Fragments (bwd_frag)
+// are loaded ahead of the layer that uses them (bwd_mma).
 // times LeakyReLU' (from the stored activation: y > 0 exactly when its input was), into the
 // blocked LDS plane (rows kk0..) when Ys is set and the [K][B] plane
 __device__ __forceinline__ void bwd_store(f32x4 acc, const float* __restrict__ act, int kk0, float slope,
@@ -311,6 +366,45 @@ __device__ __forceinline__ void bwd_store(f32x4 acc, const float* __restrict__ a
   if (Ys) *reinterpret_cast<float4*>(Ys + ((kk0 >> 4) * 16 + rr) * 16 + 4 * g) = d;
 }
 
+// a layer's weight fragments for bwd_mma, NOB output blocks from ob0 (0 past n_ob or o_valid)
+template <int NOB>
+__device__ __forceinline__ void bwd_frag(float (&w)[NOB][4], const float* __restrict__ W, int ldw, int k0, int ob0,
+                                         int n_ob, int o_valid, int lane) {
+  const int g = lane >> 4, rr = lane & 15;
+#pragma unroll
+  for (int u = 0; u < NOB; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int o = 16 * (ob0 + u) + 4 * g + v;
+      w[u][v] = (ob0 + u < n_ob && o < o_valid) ? W[(size_t)o * ldw + k0 + rr] : 0.f;
+    }
+}
+
+template <int NOB>
+__device__ __forceinline__ f32x4 bwd_mma(f32x4 acc, const float (&w)[NOB][4], int ob0, int n_ob,
+                                         const float* __restrict__ dYs, int lane) {
+  const int g = lane >> 4, rr = lane & 15;
+#pragma unroll
+  for (int u = 0; u < NOB; ++u) {
+    if (ob0 + u < n_ob) {
+      const float4 y = *reinterpret_cast<const float4*>(dYs + ((ob0 + u) * 16 + rr) * 16 + 4 * g);
+      acc = mfma(w[u][0], y.x, acc);
+      acc = mfma(w[u][1], y.y, acc);
+      acc = mfma(w[u][2], y.z, acc);
+      acc = mfma(w[u][3], y.w, acc);
+    }
+  }
+  return acc;
+}
+
+constexpr int kMaxK = 7;
+
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m);
+  return x;
+}
+
 __global__ void __launch_bounds__(kThreads) learn_bwd_kernel(LearnArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int H = a.H, A = a.A, Ap = a.Apad, K = a.K, B = a.B;
@@ -319,97 +413,226 @@ __global__ void __launch_bounds__(kThreads) learn_bwd_kernel(LearnArgs a) {
   float* DH4 = DHH + H * kDH * kRows;
   float* DH3 = DH4 + kD3 * kRows;
   float* DH2 = DH3 + kD2 * kRows;
-  float* sg = DH2 + kD1 * kRows;          // [16][K]
-  float* sd = sg + kRows * K;             // [16][K]
-  int* sact = reinterpret_cast<int*>(sd + kRows * K);   // [16][K]
+  float* part = DH2 + kD1 * kRows;        // [8 waves][64 lanes][4]: the split first-head-layer tiles
+  float* sdw = part + kWaves * 64 * 4;    // [8]: each wave's squared TD errors
   const int tile = blockIdx.x, b0 = tile * kRows;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // the TD error per (row, branch): bdq_update / update_policy (:111-126) on the raw heads
-  if (tid < kRows * K) {
-    const int r = tid & 15, k = tid >> 4, b = b0 + r;
-    const int64_t j = row_index(a, b);
-    int ak = a.act[(size_t)j * K + k];
-    ak = ak < 0 ? 0 : (ak >= A ? A - 1 : ak);
-    const float* hs = a.heads + (size_t)b;
-    const size_t ps = (size_t)Ap * B;                // one head's plane
-    auto head = [&](int set, int h) { return hs + ((size_t)set * H + h) * ps; };
-    const float* adv = head(0, k + 1);
-    float s = 0.f;
-    for (int o = 0; o < A; ++o) s += adv[(size_t)o * B];
-    const float current = (head(0, 0)[0] + adv[(size_t)ak * B]) - s / (float)A;
-    const float* adv2 = head(1, k + 1);
-    const float v2 = head(1, 0)[0];
-    float s2 = 0.f;
-    for (int o = 0; o < A; ++o) s2 += adv2[(size_t)o * B];
-    const float m2 = s2 / (float)A;
-    float best = (v2 + adv2[0]) - m2;
-    int am = 0;
-    for (int o = 1; o < A; ++o) {   // torch.argmax: first maximum, NaN is the maximum
-      const float qo = (v2 + adv2[(size_t)o * B]) - m2;
-      const bool take = !isnan(best) && (isnan(qo) || qo > best);
-      best = take ? qo : best;
-      am = take ? o : am;
-    }
-    const float* tadv = head(2, k + 1);
-    float s3 = 0.f;
-    for (int o = 0; o < A; ++o) s3 += tadv[(size_t)o * B];
-    const float tnext = (head(2, 0)[0] + tadv[(size_t)am * B]) - s3 / (float)A;
-    const float expected = a.rew[j] + (tnext * a.gamma) * (float)a.done[j];
-    const float d = expected - current;
-    sd[r * K + k] = d * d;
-    sg[r * K + k] = 2.f * (current - expected) / (float)(B * K);
-    sact[r * K + k] = ak;
+  const int g = lane >> 4, rr = lane & 15;
+  const float* P = a.P;
+  PBN_LSTAMP(1, 31);
+  PBN_LSTAMP(1, 0);
+  // weight fragments of the first four backward layers, requested before the TD pass so they
+  // arrive during it: second head layers (tiles wave, wave + 8 of H x 4), the first head layers
+  // split four ways per output tile (wave & 1 = tile, wave >> 1 = quarter of the 4 H blocks),
+  // 32 -> 64 (waves < 4) and 64 -> 128
+  const int at16 = Ap / 16;
+  float wh2[2][2][4], wh1[8][4], w4[2][4], w3[4][4];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int tt = min(wave + kWaves * u, H * (kDH / 16) - 1), h = tt >> 2;
+    bwd_frag<2>(wh2[u], P + a.off[H2_W] + (size_t)h * A * kDH, kDH, 16 * (tt & 3), 0, at16, A, lane);
   }
-  __syncthreads();
-  // the gradient at the head outputs: d/d adv[k][o] = g ([o == a_k] - 1/A), d/d v = sum_k g
-  for (int e = tid; e < H * Ap * kRows; e += kThreads) {
-    const int oi = e & 15, r = (e >> 4) & 15, hb = e >> 8;   // hb = h * Apad/16 + o/16
-    const int h = hb / (Ap / 16), o = 16 * (hb - h * (Ap / 16)) + oi;
-    float val = 0.f;
-    if (o < A) {
-      if (h == 0) {
-        if (o == 0)
-          for (int k = 0; k < K; ++k) val += sg[r * K + k];
-      } else {
-        const float gk = sg[r * K + h - 1];
-        val = (o == sact[r * K + h - 1] ? gk : 0.f) - gk / (float)A;
+  const int q1 = wave >> 1;   // quarter of the first head layers' 4 H output blocks: [q H, q H + H)
+  bwd_frag<8>(wh1, P + a.off[H1_W], kD3, 16 * (wave & 1), q1 * H, q1 * H + H, H * kDH, lane);
+  bwd_frag<2>(w4, P + a.off[L4_W], kD2, 16 * (wave & 3), 0, kD3 / 16, kD3, lane);
+  bwd_frag<4>(w3, P + a.off[L3_W], kD1, 16 * wave, 0, kD2 / 16, kD2, lane);
+  PBN_LSTAMP(1, 1);
+
+  // the TD error per (row, branch): bdq_update / update_policy (:111-126) on the raw heads.  Wave
+  // w takes rows 2w and 2w + 1, every branch; lane = head output (o = lane, lane + 64): the three
+  // duelings' means and the online argmax over s' are wave reductions, and every load of the
+  // pass is in flight at once.
+  {
+    float x[2][3][kMaxK][2], vv[2][3];
+    int64_t jr[2];
+    int ak[2][kMaxK];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int b = b0 + 2 * wave + q;
+      jr[q] = row_index(a, b);
+#pragma unroll
+      for (int set = 0; set < 3; ++set) {
+        const float* hrow = a.heads + ((size_t)set * H * B + b) * Ap;   // head h at + h B Ap
+        vv[q][set] = hrow[0];
+#pragma unroll
+        for (int k = 0; k < kMaxK; ++k)
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const int o = lane + 64 * c;
+            x[q][set][k][c] = (k < K && o < A) ? hrow[(size_t)(k + 1) * B * Ap + o] : 0.f;
+          }
       }
     }
-    DH[e] = val;
-    a.dheads[((size_t)h * Ap + o) * B + b0 + r] = val;
+    float rw[2], dn[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int64_t j = jr[q];
+#pragma unroll
+      for (int k = 0; k < kMaxK; ++k) {
+        const int v = k < K ? a.act[(size_t)j * K + k] : 0;
+        ak[q][k] = v < 0 ? 0 : (v >= A ? A - 1 : v);
+      }
+      rw[q] = a.rew[j];
+      dn[q] = (float)a.done[j];
+      if (lane < a.W) {   // the row's state and target words for learn_apply's bilinear tiles
+        const int b = b0 + 2 * wave + q;
+        a.srow[(size_t)lane * B + b] = a.st[(size_t)lane * a.cap + j];
+        const int tg = a.tgt[j];
+        a.trow[(size_t)lane * B + b] = tg < a.n_attr ? a.att_first[(size_t)tg * a.W + lane] : 0u;
+      }
+    }
+    float sq = 0.f;
+    PBN_LSTAMP(1, 2);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int r = 2 * wave + q;
+      float gk[kMaxK];
+#pragma unroll
+      for (int k = 0; k < kMaxK; ++k) {
+        gk[k] = 0.f;
+        if (k < K) {
+          const float m0 = wave_sum(x[q][0][k][0] + x[q][0][k][1]) / (float)A;
+          const float m1 = wave_sum(x[q][1][k][0] + x[q][1][k][1]) / (float)A;
+          const float m2 = wave_sum(x[q][2][k][0] + x[q][2][k][1]) / (float)A;
+          // argmax_o q(s', o): torch.argmax's first maximum, NaN the maximum
+          float best = -INFINITY;
+          int bi = 0x7fffffff;
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const int o = lane + 64 * c;
+            if (o < A) {
+              const float qv = (vv[q][1] + x[q][1][k][c]) - m1;
+              const bool take = bi == 0x7fffffff || (!isnan(best) && (isnan(qv) || qv > best));
+              best = take ? qv : best;
+              bi = take ? o : bi;
+            }
+          }
+#pragma unroll
+          for (int m = 32; m >= 1; m >>= 1) {
+            const float ob = __shfl_xor(best, m);
+            const int oi = __shfl_xor(bi, m);
+            const bool bn = isnan(best), on = isnan(ob);
+            const bool take = oi != 0x7fffffff &&
+                              (bi == 0x7fffffff || (on && (!bn || oi < bi)) ||
+                               (!bn && !on && (ob > best || (ob == best && oi < bi))));
+            best = take ? ob : best;
+            bi = take ? oi : bi;
+          }
+          const int a0 = ak[q][k];
+          const float c0 = __shfl(x[q][0][k][0], a0 & 63), c1 = __shfl(x[q][0][k][1], a0 & 63);
+          const float t0 = __shfl(x[q][2][k][0], bi & 63), t1 = __shfl(x[q][2][k][1], bi & 63);
+          const float current = (vv[q][0] + (a0 < 64 ? c0 : c1)) - m0;
+          const float tnext = (vv[q][2] + (bi < 64 ? t0 : t1)) - m2;
+          const float expected = rw[q] + (tnext * a.gamma) * dn[q];
+          const float d = expected - current;
+          sq += d * d;
+          gk[k] = 2.f * (current - expected) / (float)(B * K);
+        }
+      }
+      // this row's gradient at the head outputs: d/d adv[k][o] = g_k ([o == a_k] - 1/A),
+      // d/d v = sum_k g_k (0 for the value head's other outputs and the padding)
+      float gsum = 0.f;
+#pragma unroll
+      for (int k = 0; k < kMaxK; ++k) gsum += k < K ? gk[k] : 0.f;
+      for (int e = lane; e < H * Ap; e += 64) {
+        const int h = e / Ap, o = e - h * Ap;
+        float val = 0.f;
+        if (o < A) {
+          if (h == 0) {
+            val = o == 0 ? gsum : 0.f;
+          } else {
+            float gh = 0.f;
+            int ah = 0;
+#pragma unroll
+            for (int k = 0; k < kMaxK; ++k)
+              if (k == h - 1) {
+                gh = gk[k];
+                ah = ak[q][k];
+              }
+            val = (o == ah ? gh : 0.f) - gh / (float)A;
+          }
+        }
+        DH[((h * at16 + (o >> 4)) * 16 + r) * 16 + (o & 15)] = val;
+        a.dheads[((size_t)h * Ap + o) * B + b0 + r] = val;
+      }
+    }
+    if (lane == 0) sdw[wave] = sq;
   }
+  PBN_LSTAMP(1, 3);
+  __syncthreads();
+  PBN_LSTAMP(1, 4);
   if (tid == 0) {
-    float s = 0.f;
-    for (int p = 0; p < kRows * K; ++p) s += sd[p];
-    a.partial[tile] = s;
+    float sacc = 0.f;
+    for (int w = 0; w < kWaves; ++w) sacc += sdw[w];
+    a.partial[tile] = sacc;
     if (tile == 0) a.step[0] += 1.f;   // Adam's step count, read by learn_apply
   }
-  __syncthreads();
-  for (int tt = wave; tt < H * (kDH / 16); tt += kWaves) {   // second head layers: Apad -> 64 per head
-    const int h = tt / (kDH / 16), c0 = 16 * (tt - h * (kDH / 16));
-    const f32x4 acc = bwd_tile(a.P + a.off[H2_W] + (size_t)h * A * kDH, kDH, c0, Ap / 16, A, DH + h * Ap * kRows, lane);
+  // the last layer's fragments (256 inputs: tiles wave, wave + 8), requested now for the end
+  float w2[2][8][4];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) bwd_frag<8>(w2[u], P + a.off[L2_W], kD0, 16 * (wave + kWaves * u), 0, kD1 / 16, kD1, lane);
+  // second head layers: Apad -> 64 per head
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int tt = wave + kWaves * u;
+    if (tt < H * (kDH / 16)) {
+      const int h = tt >> 2, c0 = 16 * (tt & 3);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      acc = bwd_mma<2>(acc, wh2[u], 0, at16, DH + h * Ap * kRows, lane);
+      for (int ob0 = 2; ob0 < at16; ob0 += 2) {   // (A > 32)
+        float wl[2][4];
+        bwd_frag<2>(wl, P + a.off[H2_W] + (size_t)h * A * kDH, kDH, c0, ob0, at16, A, lane);
+        acc = bwd_mma<2>(acc, wl, ob0, at16, DH + h * Ap * kRows, lane);
+      }
+      bwd_store(acc, a.hh, h * kDH + c0, a.slope, DHH, a.dhh, B, b0, lane);
+    }
+  }
+  for (int tt = wave + 2 * kWaves; tt < H * (kDH / 16); tt += kWaves) {   // (H > 4)
+    const int h = tt >> 2, c0 = 16 * (tt & 3);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int ob0 = 0; ob0 < at16; ob0 += 2) {
+      float wl[2][4];
+      bwd_frag<2>(wl, P + a.off[H2_W] + (size_t)h * A * kDH, kDH, c0, ob0, at16, A, lane);
+      acc = bwd_mma<2>(acc, wl, ob0, at16, DH + h * Ap * kRows, lane);
+    }
     bwd_store(acc, a.hh, h * kDH + c0, a.slope, DHH, a.dhh, B, b0, lane);
   }
+  PBN_LSTAMP(1, 5);
   __syncthreads();
-  if (wave < kD3 / 16) {   // first head layers: 64 H -> 32
-    const f32x4 acc = bwd_tile(a.P + a.off[H1_W], kD3, 16 * wave, H * kDH / 16, H * kDH, DHH, lane);
+  PBN_LSTAMP(1, 6);
+  {   // first head layers: 64 H -> 32, each output tile split over four waves (H blocks each)
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    acc = bwd_mma<8>(acc, wh1, q1 * H, q1 * H + H, DHH, lane);
+    *reinterpret_cast<f32x4*>(part + (wave * 64 + lane) * 4) = acc;
+  }
+  __syncthreads();
+  if (wave < kD3 / 16) {   // the four quarters added in order
+    f32x4 acc = *reinterpret_cast<const f32x4*>(part + (wave * 64 + lane) * 4);
+#pragma unroll
+    for (int qq = 1; qq < 4; ++qq) acc += *reinterpret_cast<const f32x4*>(part + ((wave + 2 * qq) * 64 + lane) * 4);
     bwd_store(acc, a.h4, 16 * wave, a.slope, DH4, a.dh4, B, b0, lane);
   }
   __syncthreads();
+  PBN_LSTAMP(1, 7);
   if (wave < kD2 / 16) {   // 32 -> 64
-    const f32x4 acc = bwd_tile(a.P + a.off[L4_W], kD2, 16 * wave, kD3 / 16, kD3, DH4, lane);
+    const f32x4 acc = bwd_mma<2>(f32x4{0.f, 0.f, 0.f, 0.f}, w4, 0, kD3 / 16, DH4, lane);
     bwd_store(acc, a.h3, 16 * wave, a.slope, DH3, a.dh3, B, b0, lane);
   }
   __syncthreads();
-  if (wave < kD1 / 16) {   // 64 -> 128
-    const f32x4 acc = bwd_tile(a.P + a.off[L3_W], kD1, 16 * wave, kD2 / 16, kD2, DH3, lane);
+  {   // 64 -> 128
+    const f32x4 acc = bwd_mma<4>(f32x4{0.f, 0.f, 0.f, 0.f}, w3, 0, kD2 / 16, DH3, lane);
     bwd_store(acc, a.h2, 16 * wave, a.slope, DH2, a.dh2, B, b0, lane);
   }
   __syncthreads();
-  for (int tt = wave; tt < kD0 / 16; tt += kWaves) {   // 128 -> 256: the bilinear layer's output gradient
-    const f32x4 acc = bwd_tile(a.P + a.off[L2_W], kD0, 16 * tt, kD1 / 16, kD1, DH2, lane);
-    bwd_store(acc, a.y1, 16 * tt, a.slope, nullptr, a.g1, B, b0, lane);
+  PBN_LSTAMP(1, 8);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {   // 128 -> 256: the bilinear layer's output gradient
+    const f32x4 acc = bwd_mma<8>(f32x4{0.f, 0.f, 0.f, 0.f}, w2[u], 0, kD1 / 16, DH2, lane);
+    bwd_store(acc, a.y1, 16 * (wave + kWaves * u), a.slope, nullptr, a.g1, B, b0, lane);
   }
+  PBN_LSTAMP(1, 9);
+  (void)g;
+  (void)rr;
 }
 
 // ---- Adam (torch.optim.Adam, fused, defaults but lr: bdq_model/__init__.py:34) on one element,
@@ -426,12 +649,16 @@ __device__ __forceinline__ void adam(const LearnArgs& a, int64_t i, float g, flo
 }
 
 // T[t][i][o] = sum_j target_t[j] W[o][i][j] in j order (pbn_bdq_pack computes the same sums)
-__device__ __forceinline__ float table_entry(const LearnArgs& a, int t, const float* __restrict__ wrow, int stride) {
-  const uint32_t* ts = a.att_states + (size_t)a.att_start[t] * a.W;
+__device__ __forceinline__ float table_entry(const LearnArgs& a, int t, const float* __restrict__ wrow) {
+  const uint32_t* ts = a.att_first + (size_t)t * a.W;
+  uint32_t tw[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) tw[w] = w < a.W ? ts[w] : 0u;
   float s = 0.f;
   for (int j = 0; j < a.N; ++j) {
-    const bool on = (ts[j >> 5] >> (j & 31)) & 1u;
-    s += on ? wrow[j * stride] : 0.f;
+    const uint32_t word = (j >> 5) == 0 ? tw[0] : (j >> 5) == 1 ? tw[1] : (j >> 5) == 2 ? tw[2] : tw[3];
+    const bool on = (word >> (j & 31)) & 1u;
+    s += on ? wrow[j] : 0.f;
   }
   return s;
 }
@@ -449,10 +676,14 @@ __global__ void __launch_bounds__(64 * kApplyWaves) learn_apply_kernel(LearnArgs
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, rr = lane & 15;
   const int B = a.B;
-  if (blockIdx.x == 0 && tid == 0) {
+  PBN_LSTAMP(2, 31);
+  PBN_LSTAMP(2, 0);
+  if (blockIdx.x == 0 && wave == 0) {   // the loss: the backward blocks' partial sums, a fixed-order reduction
     float s = 0.f;
-    for (int p = 0; p < B / kRows; ++p) s += a.partial[p];
-    a.loss[0] = s / (float)(B * a.K);
+    for (int p = lane; p < B / kRows; p += 64) s += a.partial[p];
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
+    if (lane == 0) a.loss[0] = s / (float)(B * a.K);
   }
   const float stepc = a.step[0];
   const float bc1 = 1.f - powf(a.b1, stepc);
@@ -468,26 +699,41 @@ __global__ void __launch_bounds__(64 * kApplyWaves) learn_apply_kernel(LearnArgs
 #pragma unroll
     for (int jt = 0; jt < NT; ++jt) acc[jt] = f32x4{0.f, 0.f, 0.f, 0.f};
     float bsum = 0.f;
-    for (int r0 = 0; r0 < B; r0 += 16) {
-      float4 y = *reinterpret_cast<const float4*>(grow + r0 + 4 * g);
-      bsum += (y.x + y.y) + (y.z + y.w);
-      const uint4 sv = *reinterpret_cast<const uint4*>(si + r0 + 4 * g);
-      const uint32_t sh = i & 31;
-      y.x = (sv.x >> sh) & 1u ? y.x : 0.f;
-      y.y = (sv.y >> sh) & 1u ? y.y : 0.f;
-      y.z = (sv.z >> sh) & 1u ? y.z : 0.f;
-      y.w = (sv.w >> sh) & 1u ? y.w : 0.f;
+    constexpr int RC = NT <= 2 ? 8 : 4;   // 16-row steps per round of loads
+    const uint32_t sh = i & 31;
+    for (int r0 = 0; r0 < B; r0 += 16 * RC) {
+      float4 y[RC];
+      uint4 sv[RC], tv[RC][NT];
 #pragma unroll
-      for (int jt = 0; jt < NT; ++jt) {
-        const int jj = 16 * jt + rr;
-        const uint4 tv = *reinterpret_cast<const uint4*>(a.trow + (size_t)(jj >> 5) * B + r0 + 4 * g);
-        const uint32_t tsh = jj & 31;
-        acc[jt] = mfma(y.x, (float)((tv.x >> tsh) & 1u), acc[jt]);
-        acc[jt] = mfma(y.y, (float)((tv.y >> tsh) & 1u), acc[jt]);
-        acc[jt] = mfma(y.z, (float)((tv.z >> tsh) & 1u), acc[jt]);
-        acc[jt] = mfma(y.w, (float)((tv.w >> tsh) & 1u), acc[jt]);
+      for (int u = 0; u < RC; ++u) {
+        const int rb = min(r0 + 16 * u, B - 16) + 4 * g;
+        y[u] = *reinterpret_cast<const float4*>(grow + rb);
+        sv[u] = *reinterpret_cast<const uint4*>(si + rb);
+#pragma unroll
+        for (int jt = 0; jt < NT; ++jt)
+          tv[u][jt] = *reinterpret_cast<const uint4*>(a.trow + (size_t)((16 * jt + rr) >> 5) * B + rb);
+      }
+#pragma unroll
+      for (int u = 0; u < RC; ++u) {
+        if (r0 + 16 * u < B) {
+          float4 yy = y[u];
+          bsum += (yy.x + yy.y) + (yy.z + yy.w);
+          yy.x = (sv[u].x >> sh) & 1u ? yy.x : 0.f;
+          yy.y = (sv[u].y >> sh) & 1u ? yy.y : 0.f;
+          yy.z = (sv[u].z >> sh) & 1u ? yy.z : 0.f;
+          yy.w = (sv[u].w >> sh) & 1u ? yy.w : 0.f;
+#pragma unroll
+          for (int jt = 0; jt < NT; ++jt) {
+            const uint32_t tsh = (16 * jt + rr) & 31;
+            acc[jt] = mfma(yy.x, (float)((tv[u][jt].x >> tsh) & 1u), acc[jt]);
+            acc[jt] = mfma(yy.y, (float)((tv[u][jt].y >> tsh) & 1u), acc[jt]);
+            acc[jt] = mfma(yy.z, (float)((tv[u][jt].z >> tsh) & 1u), acc[jt]);
+            acc[jt] = mfma(yy.w, (float)((tv[u][jt].w >> tsh) & 1u), acc[jt]);
+          }
+        }
       }
     }
+    PBN_LSTAMP(2, 1);
     const int64_t NN = (int64_t)a.N * a.N;
 #pragma unroll
     for (int jt = 0; jt < NT; ++jt) {
@@ -509,14 +755,16 @@ __global__ void __launch_bounds__(64 * kApplyWaves) learn_apply_kernel(LearnArgs
       bsum += __shfl_xor(bsum, 32);
       if (g == 0) adam(a, a.off[BIL_B] + o0 + rr, bsum, bc1, bc2s);
     }
+    PBN_LSTAMP(2, 2);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // the target-table rows of input i for these 16 outputs, from the weights just written
     for (int t = g; t < a.n_attr; t += 4) {
-      const float s = table_entry(a, t, &wsc[wave][rr][0], 1);
+      const float s = table_entry(a, t, &wsc[wave][rr][0]);
       a.Tq[((size_t)t * a.N + i) * 256 + rr * 16 + ot] = s;
     }
+    PBN_LSTAMP(2, 3);
     return;
   }
   task -= n_bil;
@@ -551,15 +799,26 @@ __global__ void __launch_bounds__(64 * kApplyWaves) learn_apply_kernel(LearnArgs
   const float* xrow = L.X + (size_t)(k0 + rr) * B;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f;
-  for (int r0 = 0; r0 < B; r0 += 16) {
-    const float4 y = *reinterpret_cast<const float4*>(yrow + r0 + 4 * g);
-    const float4 x = *reinterpret_cast<const float4*>(xrow + r0 + 4 * g);
-    bsum += (y.x + y.y) + (y.z + y.w);
-    acc = mfma(y.x, x.x, acc);
-    acc = mfma(y.y, x.y, acc);
-    acc = mfma(y.z, x.z, acc);
-    acc = mfma(y.w, x.w, acc);
+  for (int r0 = 0; r0 < B; r0 += 128) {   // eight 16-row steps per round of loads
+    float4 y[8], x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int rb = min(r0 + 16 * u, B - 16) + 4 * g;
+      y[u] = *reinterpret_cast<const float4*>(yrow + rb);
+      x[u] = *reinterpret_cast<const float4*>(xrow + rb);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (r0 + 16 * u < B) {
+        bsum += (y[u].x + y[u].y) + (y[u].z + y[u].w);
+        acc = mfma(y[u].x, x[u].x, acc);
+        acc = mfma(y[u].y, x[u].y, acc);
+        acc = mfma(y[u].z, x[u].z, acc);
+        acc = mfma(y[u].w, x[u].w, acc);
+      }
+    }
   }
+  PBN_LSTAMP(2, 4);
 #pragma unroll
   for (int v = 0; v < 4; ++v) {
     const int o = o0 + 4 * g + v;
@@ -570,15 +829,15 @@ __global__ void __launch_bounds__(64 * kApplyWaves) learn_apply_kernel(LearnArgs
     bsum += __shfl_xor(bsum, 32);
     if (g == 0 && o0 + rr < L.o_valid) adam(a, L.b_off + o0 + rr, bsum, bc1, bc2s);
   }
+  PBN_LSTAMP(2, 5);
 }
 
 // the target table of the bilinear layer, [t][i][j][q] = T[t][i][16 q + j] (the layout the
 // acting kernel reads); block (t, i), thread o
 __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ P, int64_t w_off, int N, int W,
-                                                   const int32_t* __restrict__ att_start,
-                                                   const uint32_t* __restrict__ att_states, float* __restrict__ Tq) {
+                                                   const uint32_t* __restrict__ att_first, float* __restrict__ Tq) {
   const int t = blockIdx.x / N, i = blockIdx.x - t * N, o = threadIdx.x;
-  const uint32_t* ts = att_states + (size_t)att_start[t] * W;
+  const uint32_t* ts = att_first + (size_t)t * W;
   const float* wrow = P + w_off + (int64_t)o * N * N + (int64_t)i * N;
   float s = 0.f;
   for (int j = 0; j < N; ++j) {
@@ -616,6 +875,10 @@ Work make_work(int N, int H, int64_t B) {
   return w;
 }
 
+#ifdef PBN_STAMPS
+unsigned long long* g_lstamps = nullptr;   // pbn_debug_set_learn_stamps
+#endif
+
 int check_shape(int N, int n_branches) {
   if (N < 1 || N > 127) return pbn::set_error(PBN_EINVAL, "fused BDQ update: 1 <= n_nodes <= 127");
   if (n_branches < 1 || n_branches > 7) return pbn::set_error(PBN_EINVAL, "fused BDQ update: n_branches 1..7");
@@ -625,6 +888,15 @@ int check_shape(int N, int n_branches) {
 }  // namespace
 
 extern "C" {
+
+#ifdef PBN_STAMPS
+// diagnostic builds: the learner kernels' phase clocks go to d_buf (uint64 [3][1024][8][32]), or
+// nowhere when null
+int pbn_debug_set_learn_stamps(unsigned long long* d_buf) {
+  g_lstamps = d_buf;
+  return PBN_OK;
+}
+#endif
 
 int pbn_bdq_layout(int32_t n_nodes, int32_t n_branches, int64_t* offsets) {
   int rc = check_shape(n_nodes, n_branches);
@@ -655,7 +927,7 @@ int pbn_bdq_pack(const pbn_net* net, int32_t n_branches, const float* d_params, 
   int64_t off[TOTAL + 1];
   make_layout(v.n_nodes, n_branches + 1, off);
   hipLaunchKernelGGL(pack_kernel, dim3(v.n_attr * v.n_nodes), dim3(256), 0, (hipStream_t)stream, d_params, off[BIL_W],
-                     v.n_nodes, v.W, v.att_start, v.att_states, d_Tq);
+                     v.n_nodes, v.W, v.att_first, d_Tq);
   if (hipGetLastError() != hipSuccess) return pbn::set_error(PBN_EDEVICE, "pack_kernel launch failed");
   return PBN_OK;
 }
@@ -695,8 +967,7 @@ int pbn_bdq_learn(const pbn_net* net, int64_t batch, const int64_t* d_idx, int64
   a.act = d_action;
   a.rew = d_reward;
   a.done = d_done;
-  a.att_start = nv.att_start;
-  a.att_states = nv.att_states;
+  a.att_first = nv.att_first;
   a.n_attr = nv.n_attr;
   a.N = N;
   a.W = nv.W;
@@ -738,12 +1009,16 @@ int pbn_bdq_learn(const pbn_net* net, int64_t batch, const int64_t* d_idx, int64
   a.partial = ws + w.partial;
   a.loss = d_loss;
   a.grad = d_grad;
+  a.stamps = nullptr;
+#ifdef PBN_STAMPS
+  a.stamps = g_lstamps;
+#endif
   const hipStream_t s = (hipStream_t)stream;
   const int tiles = (int)(batch / kRows);
   const size_t lds_f = ((size_t)(kD0 + kD1 + kD2 + kD3 + kDH * H) * kRows + 2 * 4 * kRows) * sizeof(float);
   hipLaunchKernelGGL(learn_fwd_kernel, dim3(3 * tiles), dim3(kThreads), lds_f, s, a);
   if (hipGetLastError() != hipSuccess) return pbn::set_error(PBN_EDEVICE, "learn_fwd_kernel launch failed");
-  const size_t lds_b = ((size_t)(H * a.Apad + H * kDH + kD3 + kD2 + kD1) * kRows + 3 * kRows * n_branches) * sizeof(float);
+  const size_t lds_b = ((size_t)(H * a.Apad + H * kDH + kD3 + kD2 + kD1) * kRows + kWaves * 64 * 4 + kWaves) * sizeof(float);
   if (lds_b > 64 * 1024 && hipFuncSetAttribute((const void*)learn_bwd_kernel,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_b) != hipSuccess)
     return pbn::set_error(PBN_EDEVICE, "hipFuncSetAttribute failed");

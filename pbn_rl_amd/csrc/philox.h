@@ -17,10 +17,11 @@ namespace pbn {
 
 // EXPLORE = 4: epsilon-greedy draws of pbn_q_to_flipmask (per env; word 0 = explore test,
 // word k + 1 = branch k's random action, by multiply-high); SETTLE_SEL = 5 (per group) and
-// SETTLE_ENV = 6 (per env): updates k >= 1 of a step under the settle law (settle_updates)
+// SETTLE_ENV = 6 (per env): updates k >= 1 of a step under the settle law (settle_updates);
+// REPLAY = 7: the learner's replay rows (pbn_replay_advance: id = row of the batch, step = draw)
 enum : uint32_t {
   kStreamSel = 0, kStreamEnv = 1, kStreamPert = 2, kStreamReset = 3, kStreamExplore = 4,
-  kStreamSettleSel = 5, kStreamSettleEnv = 6
+  kStreamSettleSel = 5, kStreamSettleEnv = 6, kStreamReplay = 7
 };
 
 struct Word4 {

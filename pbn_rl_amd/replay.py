@@ -74,10 +74,12 @@ class DeviceReplay:
         self.size = min(self.size + n, self.capacity)
 
     def store_at(self, pos_t: torch.Tensor, size_t: torch.Tensor, state, target, action, reward, next_state,
-                 done) -> None:
+                 done, *, done_mask: int = 0, done_out: Optional[torch.Tensor] = None, advance: bool = True) -> None:
         """``store`` with the ring position and fill level held in one-element int64 device
-        tensors (advanced here, on the stream) instead of host ints: graph-capturable.  The
-        caller mirrors them in ``pos`` / ``size``."""
+        tensors (advanced here, on the stream, unless ``advance`` is False) instead of host ints:
+        graph-capturable.  The caller mirrors them in ``pos`` / ``size``.  ``done_mask`` != 0:
+        ``done`` is the env's flags and a transition is done when ``flags & done_mask``;
+        ``done_out`` (uint8 [n]) then receives those 0/1 values too."""
         n = target.shape[0]
         if n > self.capacity:
             raise ValueError("more transitions than the ring holds")
@@ -86,18 +88,26 @@ class DeviceReplay:
                 and done.dtype in (torch.bool, torch.uint8)):
             # the six field copies in one launch (pbn_replay_store)
             st, nst, act = state.contiguous(), next_state.contiguous(), action.contiguous()
+            if done_out is not None and (done_out.dtype != torch.uint8 or done_out.numel() < n):
+                raise ValueError("done_out must be uint8 with n elements")
             L = _lib.load()
             with torch.cuda.device(self.device):
                 _lib.check(L.pbn_replay_store(n, pos_t.data_ptr(), self.capacity, self.words, self.action.shape[1],
                                               st.data_ptr(), nst.data_ptr(), target.contiguous().data_ptr(),
                                               act.data_ptr(), reward.contiguous().data_ptr(),
-                                              done.contiguous().data_ptr(), self.state.data_ptr(),
-                                              self.next_state.data_ptr(), self.target.data_ptr(),
+                                              done.contiguous().data_ptr(), int(done_mask),
+                                              done_out.data_ptr() if done_out is not None else None,
+                                              self.state.data_ptr(), self.next_state.data_ptr(), self.target.data_ptr(),
                                               self.action.data_ptr(), self.reward.data_ptr(), self.done.data_ptr(),
                                               torch.cuda.current_stream(self.device).cuda_stream), "pbn_replay_store")
-            pos_t.add_(n).remainder_(self.capacity)
-            size_t.add_(n).clamp_(max=self.capacity)
+            if advance:
+                pos_t.add_(n).remainder_(self.capacity)
+                size_t.add_(n).clamp_(max=self.capacity)
             return
+        if done_mask:
+            done = (done & done_mask) != 0
+            if done_out is not None:
+                done_out[:n].copy_(done)
         idx = (torch.arange(n, device=self.device, dtype=torch.int64) + pos_t) % self.capacity
         self.state.index_copy_(1, idx, state)
         self.next_state.index_copy_(1, idx, next_state)
@@ -105,8 +115,9 @@ class DeviceReplay:
         self.action.index_copy_(0, idx, action.to(torch.int32))
         self.reward.index_copy_(0, idx, reward.to(torch.float32))
         self.done.index_copy_(0, idx, done.to(torch.uint8))
-        pos_t.add_(n).remainder_(self.capacity)
-        size_t.add_(n).clamp_(max=self.capacity)
+        if advance:
+            pos_t.add_(n).remainder_(self.capacity)
+            size_t.add_(n).clamp_(max=self.capacity)
 
     def sample_indices(self, batch: int, generator: Optional[torch.Generator] = None,
                        size_t: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -120,6 +131,17 @@ class DeviceReplay:
         u = torch.rand(batch, dtype=torch.float64, device=self.device, generator=generator)
         idx = (u * size_t).long()
         return torch.minimum(idx, size_t - 1)
+
+    def sample_rows(self, idx_out: torch.Tensor, seed: int, counter_t: torch.Tensor, size_t: torch.Tensor) -> torch.Tensor:
+        """Fill ``idx_out`` (int64) with rows uniform over [0, size) with replacement, from the
+        Philox REPLAY stream of (seed, row, *counter_t) (pbn_replay_advance; counter_t advances):
+        one launch, graph-capturable, and the same rows eager or captured."""
+        L = _lib.load()
+        with torch.cuda.device(self.device):
+            _lib.check(L.pbn_replay_advance(0, self.capacity, None, size_t.data_ptr(), None, None, None, 0.0, 0.0,
+                                            idx_out.numel(), seed, counter_t.data_ptr(), idx_out.data_ptr(),
+                                            torch.cuda.current_stream(self.device).cuda_stream), "pbn_replay_advance")
+        return idx_out
 
     def gather(self, idx: torch.Tensor, net_handle, stream=None) -> Dict[str, torch.Tensor]:
         """Rows ``idx`` (B a multiple of 32) as network inputs, in one launch (``pbn_replay_batch``):
@@ -406,6 +428,12 @@ class BDQLearner:
         self.updates = 0
         self.gen = torch.Generator(device=env.device)
         self.gen.manual_seed(seed)
+        self.seed = int(seed)
+        if self.fused is not None:
+            # the fused learner draws its rows from the REPLAY Philox stream (pbn_replay_advance):
+            # all updates_per_frame batches of a frame in one draw, eager or captured
+            self._draw_t = torch.zeros(1, dtype=torch.int64, device=env.device)
+            self._idx = torch.empty(updates_per_frame * batch_size, dtype=torch.int64, device=env.device)
         self.last_loss: Optional[torch.Tensor] = None
         self.graphable = graphable
         self._graph: Optional[torch.cuda.CUDAGraph] = None
@@ -441,9 +469,14 @@ class BDQLearner:
         self.frames += 1
         if self.replay.size >= self.learning_starts:
             self.epsilon = max(self.epsilon_final, self.epsilon - self.epsilon_step)
-            for _ in range(self.updates_per_frame):
-                idx = self.replay.sample_indices(self.batch_size, self.gen)
-                self.last_loss = self._update(idx)
+            if self.fused is not None:
+                size_t = torch.full((1,), self.replay.size, dtype=torch.int64, device=env.device)
+                self.replay.sample_rows(self._idx, self.seed, self._draw_t, size_t)
+            for u in range(self.updates_per_frame):
+                if self.fused is not None:
+                    self.last_loss = self.fused.update(self.replay, self._idx[u * self.batch_size:(u + 1) * self.batch_size])
+                else:
+                    self.last_loss = self._update(self.replay.sample_indices(self.batch_size, self.gen))
                 self.updates += 1
                 if self.updates % self.target_update == 0:
                     self._soft_update()
@@ -491,6 +524,7 @@ class BDQLearner:
         self._eps32 = self._eps64.float()
         self._pos_t = torch.full((1,), self.replay.pos, dtype=torch.int64, device=dev)
         self._size_t = torch.full((1,), self.replay.size, dtype=torch.int64, device=dev)
+        self._done_buf = torch.zeros(env.n_alloc, dtype=torch.uint8, device=dev)
         g = torch.cuda.CUDAGraph()
         g.register_generator_state(self.gen)
         if self.opt is not None:
@@ -507,18 +541,29 @@ class BDQLearner:
         target = env.target.clone()
         self.agent.act_q(step_t=self._step_t, epsilon_t=self._eps32)
         env.step_flipmask_dev(self._step_t)
-        self._step_t.add_(1)
-        done_all = (env.flags & (_lib.FLAG_TERMINATED | _lib.FLAG_TRUNCATED)) != 0
+        # the ring store derives done from the flags; then one launch advances the step index,
+        # the ring position and fill level and epsilon, and (fused) draws the frame's batches
         self.replay.store_at(self._pos_t, self._size_t, state, target, self.agent.actions, env.reward,
-                             env.final_state, done_all)
-        final = torch.full_like(self._eps64, self.epsilon_final)
-        self._eps64.copy_(torch.maximum(final, self._eps64 - self.epsilon_step))
-        self._eps32.copy_(self._eps64)
+                             env.final_state, env.flags, done_mask=_lib.FLAG_TERMINATED | _lib.FLAG_TRUNCATED,
+                             done_out=self._done_buf, advance=False)
+        fused = self.fused is not None
+        L = _lib.load()
+        with torch.cuda.device(env.device):
+            _lib.check(L.pbn_replay_advance(env.n_alloc, self.replay.capacity, self._pos_t.data_ptr(),
+                                            self._size_t.data_ptr(), self._step_t.data_ptr(), self._eps64.data_ptr(),
+                                            self._eps32.data_ptr(), float(self.epsilon_final), float(self.epsilon_step),
+                                            self._idx.numel() if fused else 0, self.seed,
+                                            self._draw_t.data_ptr() if fused else None,
+                                            self._idx.data_ptr() if fused else None,
+                                            torch.cuda.current_stream(env.device).cuda_stream), "pbn_replay_advance")
         loss = None
-        for _ in range(self.updates_per_frame):
-            idx = self.replay.sample_indices(self.batch_size, self.gen, size_t=self._size_t)
-            loss = self._update(idx)
-        return env.reward[: env.num_envs], done_all[: env.num_envs], loss
+        B = self.batch_size
+        for u in range(self.updates_per_frame):
+            if fused:
+                loss = self.fused.update(self.replay, self._idx[u * B:(u + 1) * B])
+            else:
+                loss = self._update(self.replay.sample_indices(B, self.gen, size_t=self._size_t))
+        return env.reward[: env.num_envs], self._done_buf[: env.num_envs].view(torch.bool), loss
 
     def _replay_frame(self):
         env, rp = self.env, self.replay

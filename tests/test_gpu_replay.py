@@ -165,3 +165,52 @@ def test_replay_store_kernel_matches_index_copy():
         a.pos = (a.pos + n) % cap
         a.size = min(a.size + n, cap)
         assert int(pos_t.item()) == a.pos and int(size_t.item()) == a.size
+
+
+def test_replay_advance_counters_and_rows():
+    """pbn_replay_advance (a captured frame's counters and the fused learner's rows): position,
+    fill level, step index and epsilon as the host arithmetic of BDQLearner.frame, and the rows
+    bit-exact against oracle.agent_oracle.replay_rows."""
+    from pbn_rl_amd import _lib
+    dev = torch.device("cuda")
+    i64 = lambda v: torch.tensor([v], dtype=torch.int64, device=dev)  # noqa: E731
+    pos, size, step, draw = i64(990), i64(500), i64(7), i64(5)
+    eps64 = torch.tensor([0.3], dtype=torch.float64, device=dev)
+    eps32 = torch.empty(1, dtype=torch.float32, device=dev)
+    idx = torch.empty(300, dtype=torch.int64, device=dev)
+    L = _lib.load()
+    for k in range(3):
+        _lib.check(L.pbn_replay_advance(40, 1000, pos.data_ptr(), size.data_ptr(), step.data_ptr(), eps64.data_ptr(),
+                                        eps32.data_ptr(), 0.2, 0.05, 300, 123, draw.data_ptr(), idx.data_ptr(),
+                                        torch.cuda.current_stream().cuda_stream), "pbn_replay_advance")
+        torch.cuda.synchronize()
+        want_size = min(500 + 40 * (k + 1), 1000)
+        assert int(pos) == (990 + 40 * (k + 1)) % 1000 and int(size) == want_size and int(step) == 8 + k
+        e = 0.3
+        for _ in range(k + 1):
+            e = max(0.2, e - 0.05)
+        assert float(eps64) == e and float(eps32) == float(np.float32(e))
+        assert int(draw) == 6 + k
+        assert np.array_equal(idx.cpu().numpy(), agent_oracle.replay_rows(123, 5 + k, 300, want_size))
+
+
+def test_replay_store_done_from_flags():
+    """store_at with done_mask: the ring's done (and done_out) = flags & mask != 0."""
+    dev = torch.device("cuda")
+    n = 96
+    a = DeviceReplay(128, 1, 3, dev)
+    g = torch.Generator(device=dev).manual_seed(2)
+    st = torch.randint(0, 2 ** 31, (1, n), device=dev, generator=g, dtype=torch.int32)
+    tg = torch.randint(0, 14, (n,), device=dev, generator=g).to(torch.uint8)
+    act = torch.randint(0, 29, (n, 3), device=dev, generator=g, dtype=torch.int32)
+    rew = torch.randn(n, device=dev, generator=g)
+    flags = torch.randint(0, 64, (n,), device=dev, generator=g).to(torch.uint8)
+    out = torch.full((n,), 7, dtype=torch.uint8, device=dev)
+    pos_t = torch.tensor([100], dtype=torch.int64, device=dev)
+    size_t = torch.tensor([0], dtype=torch.int64, device=dev)
+    a.store_at(pos_t, size_t, st, tg, act, rew, st, flags, done_mask=3, done_out=out, advance=False)
+    torch.cuda.synchronize()
+    want = ((flags & 3) != 0).to(torch.uint8)
+    slots = (torch.arange(n, device=dev) + 100) % 128
+    assert torch.equal(a.done[slots], want) and torch.equal(out, want)
+    assert int(pos_t) == 100 and int(size_t) == 0

@@ -43,3 +43,14 @@ def test_layout_and_workspace_reject_bad_shapes():
     assert L.pbn_bdq_learn_workspace(28, 3, 512, ctypes.byref(b)) == 0 and b.value > small
     for bad in (0, 8, 250):
         assert L.pbn_bdq_learn_workspace(28, 3, bad, ctypes.byref(b)) != 0
+
+
+def test_replay_rows_restatement():
+    """agent_oracle.replay_rows (the numpy checker of pbn_replay_advance's rows) against the scalar
+    Philox restatement pyoracle.draw, REPLAY stream 7."""
+    from oracle import agent_oracle, pyoracle
+    rows = agent_oracle.replay_rows(123, 5, 50, 540)
+    for b in range(50):
+        x, y, _, _ = pyoracle.draw(123, b, 5, 7, 0)
+        assert rows[b] == ((x << 32 | y) * 540) >> 64
+    assert rows.min() >= 0 and rows.max() < 540
