@@ -317,7 +317,7 @@ def workload_text(args, chunk: int, rollout_mode: bool) -> str:
     if args.workload == "bdq-learn":
         return (f"BDQ training frames: {args.network} x {args.envs} envs per GPU, per step the config-5 frame "
                 f"(eps={args.epsilon}), the envs' transitions into the device replay, one update_policy step "
-                f"(batch 256, Adam, double-DQN target), "
+                f"(batch 256, Adam, double-DQN target; the fused update pbn_bdq_learn, three launches), "
                 f"{'one captured hipGraph per frame' if args.learn_graph else 'eager launches'}, {common}")
     stored = "obs/actions/rewards/flags" + ("" if args.no_final_state else "/s'")
     return (f"{args.network} x {args.envs} envs per GPU, in-kernel random interventions (3 uniform actions/env/step), "
@@ -818,7 +818,8 @@ def main():
         elif agent is not None:
             roofline = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                         "traffic": None, "kernel": kernel, "launch_ms": frame_ms,
-                        "note": "training frame (~170 launches, profiles/r04_u_bdq_learn_trace_kernel_stats.csv): no "
+                        "note": "training frame (11 launches: Q-network, step, ring store, counters + rows, "
+                                "the fused update's forward / backward / apply; profiles/r04_l*_bdq_learn_trace*): no "
                                 "single dominant kernel is priced"}
         elif rollout_mode:
             per_step = survey_bytes_per_env_step(spec.n)

@@ -368,13 +368,18 @@ int pbn_qnet_flipmask_from_state(const pbn_net* net, uint64_t seed, uint64_t ste
  * int32 [capacity][n_branches], reward float [capacity], done uint8 [capacity] as 0/1).  d_pos
  * (int64, device memory) is read, not advanced.  capacity >= n.  With done_mask != 0, d_done is the
  * env's flags and done = (flags & done_mask) != 0 (PBN_FLAG_TERMINATED | PBN_FLAG_TRUNCATED: the
- * frame's done); d_done_out (optional, uint8 [n]) receives the same 0/1.
+ * frame's done); d_done_out (optional, uint8 [n]) receives the same 0/1.  The optional pairs
+ * d_state_dst / d_state_src (uint32 [words][n]) and d_target_dst / d_target_src (uint8 [n]) are
+ * element copies done in the same pass after each element of d_state / d_target is read (a
+ * destination may be d_state / d_target itself): a captured frame's copy of the stepped state back
+ * into the env and its carried pre-step target, without launches of their own.
  */
 int pbn_replay_store(int64_t n, const int64_t* d_pos, int64_t capacity, int32_t words, int32_t n_branches,
                      const uint32_t* d_state, const uint32_t* d_next_state, const uint8_t* d_target,
                      const int32_t* d_action, const float* d_reward, const uint8_t* d_done, uint32_t done_mask,
                      uint8_t* d_done_out, uint32_t* d_ring_state, uint32_t* d_ring_next_state, uint8_t* d_ring_target,
-                     int32_t* d_ring_action, float* d_ring_reward, uint8_t* d_ring_done, void* stream);
+                     int32_t* d_ring_action, float* d_ring_reward, uint8_t* d_ring_done, uint32_t* d_state_dst,
+                     const uint32_t* d_state_src, uint8_t* d_target_dst, const uint8_t* d_target_src, void* stream);
 
 /*
  * A captured learning frame's counters and the update's rows, one single-block launch (no

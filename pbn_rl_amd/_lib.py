@@ -124,7 +124,7 @@ def load() -> ctypes.CDLL:
     L.pbn_last_error.argtypes = []
     L.pbn_last_error.restype = ctypes.c_char_p
     L.pbn_replay_store.argtypes = ([i64, vp, i64, ctypes.c_int32, ctypes.c_int32] + [vp] * 6 + [u32, vp] + [vp] * 6 +
-                                   [vp])
+                                   [vp] * 4 + [vp])
     L.pbn_replay_store.restype = ctypes.c_int
     L.pbn_replay_batch.argtypes = [vp, i64, vp, i64, vp, vp, vp, vp, ctypes.c_int32, vp, vp, vp, vp, vp, vp, vp]
     L.pbn_replay_batch.restype = ctypes.c_int

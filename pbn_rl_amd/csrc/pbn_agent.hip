@@ -364,19 +364,25 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 // (pos + e) mod capacity, pos read from device memory (graph replays advance it on the stream).
 // Replaces the ring's six index_copy_ launches and the slot arithmetic.
 __global__ void __launch_bounds__(kObsThreads) replay_store_kernel(
-    int64_t n, const int64_t* __restrict__ pos, int64_t cap, int W, int K, const uint32_t* __restrict__ st,
-    const uint32_t* __restrict__ nst, const uint8_t* __restrict__ tgt, const int32_t* __restrict__ act,
+    int64_t n, const int64_t* __restrict__ pos, int64_t cap, int W, int K, const uint32_t* st,
+    const uint32_t* __restrict__ nst, const uint8_t* tgt, const int32_t* __restrict__ act,
     const float* __restrict__ rew, const uint8_t* __restrict__ done, uint32_t done_mask, uint8_t* __restrict__ done_out,
     uint32_t* __restrict__ r_st, uint32_t* __restrict__ r_nst, uint8_t* __restrict__ r_tgt, int32_t* __restrict__ r_act,
-    float* __restrict__ r_rew, uint8_t* __restrict__ r_done) {
+    float* __restrict__ r_rew, uint8_t* __restrict__ r_done, uint32_t* st_dst, const uint32_t* __restrict__ st_src,
+    uint8_t* tgt_dst, const uint8_t* __restrict__ tgt_src) {
   const int64_t p0 = *pos;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t j = (p0 + e) % cap;
     for (int w = 0; w < W; ++w) {
-      r_st[(size_t)w * cap + j] = st[(size_t)w * n + e];
+      const uint32_t sv = st[(size_t)w * n + e];
+      r_st[(size_t)w * cap + j] = sv;
       r_nst[(size_t)w * cap + j] = nst[(size_t)w * n + e];
+      // (st_dst may be st: each element is read above before this thread overwrites it)
+      if (st_dst) st_dst[(size_t)w * n + e] = st_src[(size_t)w * n + e];
     }
-    r_tgt[j] = tgt[e];
+    const uint8_t tv = tgt[e];
+    r_tgt[j] = tv;
+    if (tgt_dst) tgt_dst[e] = tgt_src[e];
     for (int k = 0; k < K; ++k) r_act[(size_t)j * K + k] = act[(size_t)e * K + k];
     r_rew[j] = rew[e];
     const uint8_t d = done_mask ? ((done[e] & done_mask) ? 1 : 0) : (done[e] ? 1 : 0);
@@ -722,7 +728,10 @@ int pbn_replay_store(int64_t n, const int64_t* d_pos, int64_t capacity, int32_t 
                      const uint32_t* d_state, const uint32_t* d_next_state, const uint8_t* d_target,
                      const int32_t* d_action, const float* d_reward, const uint8_t* d_done, uint32_t done_mask,
                      uint8_t* d_done_out, uint32_t* d_ring_state, uint32_t* d_ring_next_state, uint8_t* d_ring_target,
-                     int32_t* d_ring_action, float* d_ring_reward, uint8_t* d_ring_done, void* stream) {
+                     int32_t* d_ring_action, float* d_ring_reward, uint8_t* d_ring_done, uint32_t* d_state_dst,
+                     const uint32_t* d_state_src, uint8_t* d_target_dst, const uint8_t* d_target_src, void* stream) {
+  if ((d_state_dst != nullptr) != (d_state_src != nullptr) || (d_target_dst != nullptr) != (d_target_src != nullptr))
+    return pbn::set_error(PBN_EINVAL, "state_dst / state_src and target_dst / target_src come in pairs");
   if (n < 1 || capacity < n || words < 1 || words > 4 || n_branches < 1)
     return pbn::set_error(PBN_EINVAL, "n >= 1, capacity >= n, words 1..4, n_branches >= 1");
   if (!d_pos || !d_state || !d_next_state || !d_target || !d_action || !d_reward || !d_done || !d_ring_state ||
@@ -732,7 +741,7 @@ int pbn_replay_store(int64_t n, const int64_t* d_pos, int64_t capacity, int32_t 
   hipLaunchKernelGGL(replay_store_kernel, dim3(blocks), dim3(kObsThreads), 0, (hipStream_t)stream, n, d_pos, capacity,
                      words, n_branches, d_state, d_next_state, d_target, d_action, d_reward, d_done, done_mask,
                      d_done_out, d_ring_state, d_ring_next_state, d_ring_target, d_ring_action, d_ring_reward,
-                     d_ring_done);
+                     d_ring_done, d_state_dst, d_state_src, d_target_dst, d_target_src);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return pbn::set_error(PBN_EDEVICE, hipGetErrorString(e));
   return PBN_OK;

@@ -199,6 +199,8 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
   float* XH = X4 + kD3 * kRows;       // [64 H / 16][16][16]
   uint32_t* sw = reinterpret_cast<uint32_t*>(XH + kDH * a.H * kRows);   // [4][16]
   int* stg = reinterpret_cast<int*>(sw + 4 * kRows);                  // [16]
+  int* scnt = stg + kRows;                                            // [16]: set bits per row
+  uint8_t* slist = reinterpret_cast<uint8_t*>(scnt + kRows);          // [16][128]: their indices, ascending
   const int tiles = a.B / kRows;
   const int set = blockIdx.x / tiles;
   const int b0 = (blockIdx.x - set * tiles) * kRows;
@@ -209,10 +211,20 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int B = a.B;
   float* keep = nullptr;   // the online s rows keep their activations for the backward
-  if (tid < kRows) {   // the rows' targets and state words (the backward keeps them for learn_apply)
+  if (tid < kRows) {   // the rows' targets, state words and the list of their set bits
     const int64_t j = row_index(a, b0 + tid);
     stg[tid] = a.tgt[j];
-    for (int w = 0; w < a.W; ++w) sw[w * kRows + tid] = (set == 0 ? a.st : a.nst)[(size_t)w * a.cap + j];
+    int c = 0;
+    for (int w = 0; w < a.W; ++w) {
+      uint32_t x = (set == 0 ? a.st : a.nst)[(size_t)w * a.cap + j];
+      if (w == a.W - 1 && (a.N & 31)) x &= (1u << (a.N & 31)) - 1u;
+      sw[w * kRows + tid] = x;
+      while (x) {
+        slist[tid * 128 + c++] = (uint8_t)(32 * w + __builtin_ctz(x));
+        x &= x - 1u;
+      }
+    }
+    scnt[tid] = c;
   }
   __syncthreads();
   PBN_LSTAMP(0, 1);
@@ -232,31 +244,31 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
   }
   // bilinear layer: y[o] = bias[o] + sum over the set bits i of T[t][i][o] (t = the row's target;
   // a row without a target has an all-zero second input: bias only).  Wave w takes rows 2w, 2w+1;
-  // lane p reads Tq positions 4p..4p+3 ([t][i][j][q] = T[t][i][16 q + j]: o = 16 q + j), eight
-  // table rows of both rows per round trip.
+  // lane p reads Tq positions 4p..4p+3 ([t][i][j][q] = T[t][i][16 q + j]: o = 16 q + j): only the
+  // table rows of set bits, eight of each row per round trip.
   {
     const float* bias = P + a.off[BIL_B];
     const int r0 = 2 * wave;
     const int t0 = stg[r0], t1 = stg[r0 + 1];
-    const bool h0 = t0 < a.n_attr, h1 = t1 < a.n_attr;
+    const int c0 = t0 < a.n_attr ? scnt[r0] : 0, c1 = t1 < a.n_attr ? scnt[r0 + 1] : 0;
     float4 acc[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
-    if (h0 || h1) {
-      const float* T0 = Tq + (size_t)(h0 ? t0 : 0) * a.N * 256 + 4 * lane;
-      const float* T1 = Tq + (size_t)(h1 ? t1 : 0) * a.N * 256 + 4 * lane;
-      for (int i0 = 0; i0 < a.N; i0 += 8) {
+    const int cm = max(c0, c1);
+    if (cm > 0) {
+      const float* T0 = Tq + (size_t)(c0 ? t0 : 0) * a.N * 256 + 4 * lane;
+      const float* T1 = Tq + (size_t)(c1 ? t1 : 0) * a.N * 256 + 4 * lane;
+      const uint8_t* l0 = slist + r0 * 128;
+      const uint8_t* l1 = l0 + 128;
+      for (int p0 = 0; p0 < cm; p0 += 8) {
         float4 x0[8], x1[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const size_t ii = (size_t)min(i0 + u, a.N - 1) * 256;
-          x0[u] = *reinterpret_cast<const float4*>(T0 + ii);
-          x1[u] = *reinterpret_cast<const float4*>(T1 + ii);
+          const int p = p0 + u;
+          x0[u] = *reinterpret_cast<const float4*>(T0 + (size_t)(p < c0 ? l0[p] : 0) * 256);
+          x1[u] = *reinterpret_cast<const float4*>(T1 + (size_t)(p < c1 ? l1[p] : 0) * 256);
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const int i = i0 + u;
-          const uint32_t wi = sw[(min(i, a.N - 1) >> 5) * kRows + r0], wj = sw[(min(i, a.N - 1) >> 5) * kRows + r0 + 1];
-          const bool on0 = h0 && i < a.N && ((wi >> (i & 31)) & 1u);
-          const bool on1 = h1 && i < a.N && ((wj >> (i & 31)) & 1u);
+          const bool on0 = p0 + u < c0, on1 = p0 + u < c1;
           acc[0].x += on0 ? x0[u].x : 0.f;
           acc[0].y += on0 ? x0[u].y : 0.f;
           acc[0].z += on0 ? x0[u].z : 0.f;
@@ -351,15 +363,24 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
 // are loaded ahead of the layer that uses them (bwd_mma).
 // times LeakyReLU' (from the stored activation: y > 0 exactly when its input was), into the
 // blocked LDS plane (rows kk0..) when Ys is set and the [K][B] plane
-__device__ __forceinline__ void bwd_store(f32x4 acc, const float* __restrict__ act, int kk0, float slope,
-                                          float* __restrict__ Ys, float* __restrict__ out, int B, int b0, int lane) {
+// the stored activations a backward tile's derivative needs (loaded ahead, like the weights)
+__device__ __forceinline__ f32x4 act_frag(const float* __restrict__ act, int kk0, int B, int b0, int lane) {
+  const int g = lane >> 4, rr = lane & 15;
+  f32x4 y;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) y[v] = act[(size_t)(kk0 + 4 * g + v) * B + b0 + rr];
+  return y;
+}
+
+__device__ __forceinline__ void bwd_store(f32x4 acc, f32x4 yv, int kk0, float slope, float* __restrict__ Ys,
+                                          float* __restrict__ out, int B, int b0, int lane) {
   const int g = lane >> 4, rr = lane & 15;
   float4 d;
   float* dp = &d.x;
 #pragma unroll
   for (int v = 0; v < 4; ++v) {
     const int k = kk0 + 4 * g + v;
-    const float y = act[(size_t)k * B + b0 + rr];
+    const float y = yv[v];
     dp[v] = y > 0.f ? acc[v] : acc[v] * slope;
     out[(size_t)k * B + b0 + rr] = dp[v];
   }
@@ -397,8 +418,6 @@ __device__ __forceinline__ f32x4 bwd_mma(f32x4 acc, const float (&w)[NOB][4], in
   return acc;
 }
 
-constexpr int kMaxK = 7;
-
 __device__ __forceinline__ float wave_sum(float x) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m);
@@ -414,7 +433,10 @@ __global__ void __launch_bounds__(kThreads) learn_bwd_kernel(LearnArgs a) {
   float* DH3 = DH4 + kD3 * kRows;
   float* DH2 = DH3 + kD2 * kRows;
   float* part = DH2 + kD1 * kRows;        // [8 waves][64 lanes][4]: the split first-head-layer tiles
-  float* sdw = part + kWaves * 64 * 4;    // [8]: each wave's squared TD errors
+  const int planes = (H * Ap + H * kDH + kD3 + kD2 + kD1) * kRows + kWaves * 64 * 4;
+  float* sg = lds + max(planes, 3 * H * kRows * (Ap + 4));   // [16][K] (past the TD pass's staged heads)
+  float* sd = sg + kRows * K;                          // [16][K]
+  int* sact = reinterpret_cast<int*>(sd + kRows * K);  // [16][K]
   const int tile = blockIdx.x, b0 = tile * kRows;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, rr = lane & 15;
@@ -436,137 +458,134 @@ __global__ void __launch_bounds__(kThreads) learn_bwd_kernel(LearnArgs a) {
   bwd_frag<8>(wh1, P + a.off[H1_W], kD3, 16 * (wave & 1), q1 * H, q1 * H + H, H * kDH, lane);
   bwd_frag<2>(w4, P + a.off[L4_W], kD2, 16 * (wave & 3), 0, kD3 / 16, kD3, lane);
   bwd_frag<4>(w3, P + a.off[L3_W], kD1, 16 * wave, 0, kD2 / 16, kD2, lane);
+  // and the stored activations of the same tiles (the LeakyReLU derivative)
+  f32x4 yh2[2], y4 = act_frag(a.h4, 16 * (wave & 1), B, b0, lane), y3 = act_frag(a.h3, 16 * (wave & 3), B, b0, lane),
+        y2 = act_frag(a.h2, 16 * wave, B, b0, lane), y1v[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int tt = min(wave + kWaves * u, H * (kDH / 16) - 1);
+    yh2[u] = act_frag(a.hh, (tt >> 2) * kDH + 16 * (tt & 3), B, b0, lane);
+    y1v[u] = act_frag(a.y1, 16 * (wave + kWaves * u), B, b0, lane);
+  }
   PBN_LSTAMP(1, 1);
 
-  // the TD error per (row, branch): bdq_update / update_policy (:111-126) on the raw heads.  Wave
-  // w takes rows 2w and 2w + 1, every branch; lane = head output (o = lane, lane + 64): the three
-  // duelings' means and the online argmax over s' are wave reductions, and every load of the
-  // pass is in flight at once.
+  // the TD error per (row, branch): bdq_update / update_policy (:111-126) on the raw heads.  The
+  // block's head rows of the three sets come into LDS (coalesced; the staging area is the delta
+  // planes', written only after this pass), then thread (row r, branch k) runs the duelings and
+  // the online argmax over s' as sequential sums (the order of pbn_bdq_td_loss).
+  // [set][h][16][Apad + 4]: the row pitch Apad + 4 puts the 16 rows' lanes on distinct banks
+  float* SH = lds;
+  const int pitch = Ap + 4;
   {
-    float x[2][3][kMaxK][2], vv[2][3];
-    int64_t jr[2];
-    int ak[2][kMaxK];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int b = b0 + 2 * wave + q;
-      jr[q] = row_index(a, b);
-#pragma unroll
-      for (int set = 0; set < 3; ++set) {
-        const float* hrow = a.heads + ((size_t)set * H * B + b) * Ap;   // head h at + h B Ap
-        vv[q][set] = hrow[0];
-#pragma unroll
-        for (int k = 0; k < kMaxK; ++k)
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            const int o = lane + 64 * c;
-            x[q][set][k][c] = (k < K && o < A) ? hrow[(size_t)(k + 1) * B * Ap + o] : 0.f;
-          }
-      }
+    const int per4 = kRows * Ap / 4;   // float4s of one (set, head) block of rows
+    for (int e = tid; e < 3 * H * per4; e += kThreads) {
+      const int sh = e / per4, f = e - sh * per4;   // sh = set * H + h
+      const int r = f / (Ap / 4), c = f - r * (Ap / 4);
+      *reinterpret_cast<float4*>(SH + ((size_t)sh * kRows + r) * pitch + 4 * c) =
+          reinterpret_cast<const float4*>(a.heads + ((size_t)sh * B + b0) * Ap)[f];
     }
-    float rw[2], dn[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int64_t j = jr[q];
-#pragma unroll
-      for (int k = 0; k < kMaxK; ++k) {
-        const int v = k < K ? a.act[(size_t)j * K + k] : 0;
-        ak[q][k] = v < 0 ? 0 : (v >= A ? A - 1 : v);
-      }
-      rw[q] = a.rew[j];
-      dn[q] = (float)a.done[j];
-      if (lane < a.W) {   // the row's state and target words for learn_apply's bilinear tiles
-        const int b = b0 + 2 * wave + q;
-        a.srow[(size_t)lane * B + b] = a.st[(size_t)lane * a.cap + j];
-        const int tg = a.tgt[j];
-        a.trow[(size_t)lane * B + b] = tg < a.n_attr ? a.att_first[(size_t)tg * a.W + lane] : 0u;
-      }
+  }
+  int64_t jrow = 0;
+  int ak = 0;
+  float rwj = 0.f, dnj = 0.f;
+  if (tid < kRows * K) {
+    jrow = row_index(a, b0 + (tid & 15));
+    ak = a.act[(size_t)jrow * K + (tid >> 4)];
+    ak = ak < 0 ? 0 : (ak >= A ? A - 1 : ak);
+    rwj = a.rew[jrow];
+    dnj = (float)a.done[jrow];
+  }
+  if (tid >= 64 * (kWaves - 1) && tid - 64 * (kWaves - 1) < kRows) {   // wave 7: the rows' words for learn_apply
+    const int r = tid - 64 * (kWaves - 1), b = b0 + r;
+    const int64_t j = row_index(a, b);
+    const int tg = a.tgt[j];
+    for (int w = 0; w < a.W; ++w) {
+      a.srow[(size_t)w * B + b] = a.st[(size_t)w * a.cap + j];
+      a.trow[(size_t)w * B + b] = tg < a.n_attr ? a.att_first[(size_t)tg * a.W + w] : 0u;
     }
-    float sq = 0.f;
-    PBN_LSTAMP(1, 2);
+  }
+  __syncthreads();
+  PBN_LSTAMP(1, 2);
+  if (tid < kRows * K) {
+    const int r = tid & 15, k = tid >> 4;
+    auto hrow = [&](int set, int h) { return SH + ((size_t)(set * H + h) * kRows + r) * pitch; };
+    const float* adv0 = hrow(0, k + 1);
+    const float* adv1 = hrow(1, k + 1);
+    const float* adv2 = hrow(2, k + 1);
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+    for (int o0 = 0; o0 < A; o0 += 8) {   // eight LDS reads of each row in flight, added in order
+      float x0[8], x1[8], x2[8];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int r = 2 * wave + q;
-      float gk[kMaxK];
+      for (int u = 0; u < 8; ++u) {
+        const int o = min(o0 + u, A - 1);
+        x0[u] = adv0[o];
+        x1[u] = adv1[o];
+        x2[u] = adv2[o];
+      }
 #pragma unroll
-      for (int k = 0; k < kMaxK; ++k) {
-        gk[k] = 0.f;
-        if (k < K) {
-          const float m0 = wave_sum(x[q][0][k][0] + x[q][0][k][1]) / (float)A;
-          const float m1 = wave_sum(x[q][1][k][0] + x[q][1][k][1]) / (float)A;
-          const float m2 = wave_sum(x[q][2][k][0] + x[q][2][k][1]) / (float)A;
-          // argmax_o q(s', o): torch.argmax's first maximum, NaN the maximum
-          float best = -INFINITY;
-          int bi = 0x7fffffff;
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            const int o = lane + 64 * c;
-            if (o < A) {
-              const float qv = (vv[q][1] + x[q][1][k][c]) - m1;
-              const bool take = bi == 0x7fffffff || (!isnan(best) && (isnan(qv) || qv > best));
-              best = take ? qv : best;
-              bi = take ? o : bi;
-            }
-          }
-#pragma unroll
-          for (int m = 32; m >= 1; m >>= 1) {
-            const float ob = __shfl_xor(best, m);
-            const int oi = __shfl_xor(bi, m);
-            const bool bn = isnan(best), on = isnan(ob);
-            const bool take = oi != 0x7fffffff &&
-                              (bi == 0x7fffffff || (on && (!bn || oi < bi)) ||
-                               (!bn && !on && (ob > best || (ob == best && oi < bi))));
-            best = take ? ob : best;
-            bi = take ? oi : bi;
-          }
-          const int a0 = ak[q][k];
-          const float c0 = __shfl(x[q][0][k][0], a0 & 63), c1 = __shfl(x[q][0][k][1], a0 & 63);
-          const float t0 = __shfl(x[q][2][k][0], bi & 63), t1 = __shfl(x[q][2][k][1], bi & 63);
-          const float current = (vv[q][0] + (a0 < 64 ? c0 : c1)) - m0;
-          const float tnext = (vv[q][2] + (bi < 64 ? t0 : t1)) - m2;
-          const float expected = rw[q] + (tnext * a.gamma) * dn[q];
-          const float d = expected - current;
-          sq += d * d;
-          gk[k] = 2.f * (current - expected) / (float)(B * K);
+      for (int u = 0; u < 8; ++u) {
+        if (o0 + u < A) {
+          s0 += x0[u];
+          s1 += x1[u];
+          s2 += x2[u];
         }
       }
-      // this row's gradient at the head outputs: d/d adv[k][o] = g_k ([o == a_k] - 1/A),
-      // d/d v = sum_k g_k (0 for the value head's other outputs and the padding)
-      float gsum = 0.f;
+    }
+    const float m0 = s0 / (float)A, m1 = s1 / (float)A, m2 = s2 / (float)A;
+    const float v1 = hrow(1, 0)[0];
+    float best = (v1 + adv1[0]) - m1;
+    int am = 0;
+    for (int o0 = 1; o0 < A; o0 += 8) {   // torch.argmax: first maximum, NaN is the maximum
+      float x1[8];
 #pragma unroll
-      for (int k = 0; k < kMaxK; ++k) gsum += k < K ? gk[k] : 0.f;
-      for (int e = lane; e < H * Ap; e += 64) {
-        const int h = e / Ap, o = e - h * Ap;
-        float val = 0.f;
-        if (o < A) {
-          if (h == 0) {
-            val = o == 0 ? gsum : 0.f;
-          } else {
-            float gh = 0.f;
-            int ah = 0;
+      for (int u = 0; u < 8; ++u) x1[u] = adv1[min(o0 + u, A - 1)];
 #pragma unroll
-            for (int k = 0; k < kMaxK; ++k)
-              if (k == h - 1) {
-                gh = gk[k];
-                ah = ak[q][k];
-              }
-            val = (o == ah ? gh : 0.f) - gh / (float)A;
-          }
-        }
-        DH[((h * at16 + (o >> 4)) * 16 + r) * 16 + (o & 15)] = val;
-        a.dheads[((size_t)h * Ap + o) * B + b0 + r] = val;
+      for (int u = 0; u < 8; ++u) {
+        const float qo = (v1 + x1[u]) - m1;
+        const bool take = o0 + u < A && !isnan(best) && (isnan(qo) || qo > best);
+        best = take ? qo : best;
+        am = take ? o0 + u : am;
       }
     }
-    if (lane == 0) sdw[wave] = sq;
+    const float current = (hrow(0, 0)[0] + adv0[ak]) - m0;
+    const float tnext = (hrow(2, 0)[0] + adv2[am]) - m2;
+    const float expected = rwj + (tnext * a.gamma) * dnj;
+    const float d = expected - current;
+    sd[r * K + k] = d * d;
+    sg[r * K + k] = 2.f * (current - expected) / (float)(B * K);
+    sact[r * K + k] = ak;
   }
   PBN_LSTAMP(1, 3);
   __syncthreads();
   PBN_LSTAMP(1, 4);
-  if (tid == 0) {
-    float sacc = 0.f;
-    for (int w = 0; w < kWaves; ++w) sacc += sdw[w];
-    a.partial[tile] = sacc;
-    if (tile == 0) a.step[0] += 1.f;   // Adam's step count, read by learn_apply
+  // the gradient at the head outputs: d/d adv[k][o] = g_k ([o == a_k] - 1/A), d/d v = sum_k g_k
+  // (0 for the value head's other outputs and the padding)
+  for (int e = tid; e < H * Ap * kRows; e += kThreads) {
+    const int oi = e & 15, r = (e >> 4) & 15, hb = e >> 8;   // hb = h * Apad/16 + o/16
+    const int h = hb / at16, o = 16 * (hb - h * at16) + oi;
+    float val = 0.f;
+    if (o < A) {
+      if (h == 0) {
+        if (o == 0)
+          for (int k = 0; k < K; ++k) val += sg[r * K + k];
+      } else {
+        const float gk = sg[r * K + h - 1];
+        val = (o == sact[r * K + h - 1] ? gk : 0.f) - gk / (float)A;
+      }
+    }
+    DH[e] = val;
+    a.dheads[((size_t)h * Ap + o) * B + b0 + r] = val;
   }
+  if (wave == 0) {   // the block's squared TD errors, a fixed-order reduction
+    float sacc = 0.f;
+    for (int p = lane; p < kRows * K; p += 64) sacc += sd[p];
+    sacc = wave_sum(sacc);
+    if (lane == 0) {
+      a.partial[tile] = sacc;
+      if (tile == 0) a.step[0] += 1.f;   // Adam's step count, read by learn_apply
+    }
+  }
+  __syncthreads();
   // the last layer's fragments (256 inputs: tiles wave, wave + 8), requested now for the end
   float w2[2][8][4];
 #pragma unroll
@@ -584,7 +603,7 @@ __global__ void __launch_bounds__(kThreads) learn_bwd_kernel(LearnArgs a) {
         bwd_frag<2>(wl, P + a.off[H2_W] + (size_t)h * A * kDH, kDH, c0, ob0, at16, A, lane);
         acc = bwd_mma<2>(acc, wl, ob0, at16, DH + h * Ap * kRows, lane);
       }
-      bwd_store(acc, a.hh, h * kDH + c0, a.slope, DHH, a.dhh, B, b0, lane);
+      bwd_store(acc, yh2[u], h * kDH + c0, a.slope, DHH, a.dhh, B, b0, lane);
     }
   }
   for (int tt = wave + 2 * kWaves; tt < H * (kDH / 16); tt += kWaves) {   // (H > 4)
@@ -595,7 +614,7 @@ __global__ void __launch_bounds__(kThreads) learn_bwd_kernel(LearnArgs a) {
       bwd_frag<2>(wl, P + a.off[H2_W] + (size_t)h * A * kDH, kDH, c0, ob0, at16, A, lane);
       acc = bwd_mma<2>(acc, wl, ob0, at16, DH + h * Ap * kRows, lane);
     }
-    bwd_store(acc, a.hh, h * kDH + c0, a.slope, DHH, a.dhh, B, b0, lane);
+    bwd_store(acc, act_frag(a.hh, h * kDH + c0, B, b0, lane), h * kDH + c0, a.slope, DHH, a.dhh, B, b0, lane);
   }
   PBN_LSTAMP(1, 5);
   __syncthreads();
@@ -610,25 +629,25 @@ __global__ void __launch_bounds__(kThreads) learn_bwd_kernel(LearnArgs a) {
     f32x4 acc = *reinterpret_cast<const f32x4*>(part + (wave * 64 + lane) * 4);
 #pragma unroll
     for (int qq = 1; qq < 4; ++qq) acc += *reinterpret_cast<const f32x4*>(part + ((wave + 2 * qq) * 64 + lane) * 4);
-    bwd_store(acc, a.h4, 16 * wave, a.slope, DH4, a.dh4, B, b0, lane);
+    bwd_store(acc, y4, 16 * wave, a.slope, DH4, a.dh4, B, b0, lane);
   }
   __syncthreads();
   PBN_LSTAMP(1, 7);
   if (wave < kD2 / 16) {   // 32 -> 64
     const f32x4 acc = bwd_mma<2>(f32x4{0.f, 0.f, 0.f, 0.f}, w4, 0, kD3 / 16, DH4, lane);
-    bwd_store(acc, a.h3, 16 * wave, a.slope, DH3, a.dh3, B, b0, lane);
+    bwd_store(acc, y3, 16 * wave, a.slope, DH3, a.dh3, B, b0, lane);
   }
   __syncthreads();
   {   // 64 -> 128
     const f32x4 acc = bwd_mma<4>(f32x4{0.f, 0.f, 0.f, 0.f}, w3, 0, kD2 / 16, DH3, lane);
-    bwd_store(acc, a.h2, 16 * wave, a.slope, DH2, a.dh2, B, b0, lane);
+    bwd_store(acc, y2, 16 * wave, a.slope, DH2, a.dh2, B, b0, lane);
   }
   __syncthreads();
   PBN_LSTAMP(1, 8);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {   // 128 -> 256: the bilinear layer's output gradient
     const f32x4 acc = bwd_mma<8>(f32x4{0.f, 0.f, 0.f, 0.f}, w2[u], 0, kD1 / 16, DH2, lane);
-    bwd_store(acc, a.y1, 16 * (wave + kWaves * u), a.slope, nullptr, a.g1, B, b0, lane);
+    bwd_store(acc, y1v[u], 16 * (wave + kWaves * u), a.slope, nullptr, a.g1, B, b0, lane);
   }
   PBN_LSTAMP(1, 9);
   (void)g;
@@ -648,19 +667,28 @@ __device__ __forceinline__ void adam(const LearnArgs& a, int64_t i, float g, flo
   a.P[i] -= (a.lr / bc1) * m / denom;
 }
 
-// T[t][i][o] = sum_j target_t[j] W[o][i][j] in j order (pbn_bdq_pack computes the same sums)
-__device__ __forceinline__ float table_entry(const LearnArgs& a, int t, const float* __restrict__ wrow) {
-  const uint32_t* ts = a.att_first + (size_t)t * a.W;
-  uint32_t tw[4];
-#pragma unroll
-  for (int w = 0; w < 4; ++w) tw[w] = w < a.W ? ts[w] : 0u;
+// T[t][i][o] = sum_j target_t[j] W[o][i][j] in j order (pbn_bdq_pack computes the same sums), from
+// the target's first-state words tw and the weight row in LDS (eight reads in flight)
+__device__ __forceinline__ float table_entry(const uint32_t (&tw)[4], int N, const float* __restrict__ wrow) {
   float s = 0.f;
-  for (int j = 0; j < a.N; ++j) {
-    const uint32_t word = (j >> 5) == 0 ? tw[0] : (j >> 5) == 1 ? tw[1] : (j >> 5) == 2 ? tw[2] : tw[3];
-    const bool on = (word >> (j & 31)) & 1u;
-    s += on ? wrow[j] : 0.f;
+  for (int j0 = 0; j0 < N; j0 += 8) {
+    float x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = wrow[min(j0 + u, N - 1)];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = j0 + u;
+      const uint32_t word = (j >> 5) == 0 ? tw[0] : (j >> 5) == 1 ? tw[1] : (j >> 5) == 2 ? tw[2] : tw[3];
+      const bool on = j < N && ((word >> (j & 31)) & 1u);
+      s += on ? x[u] : 0.f;
+    }
   }
   return s;
+}
+
+__device__ __forceinline__ void target_words(const LearnArgs& a, int t, uint32_t (&tw)[4]) {
+#pragma unroll
+  for (int w = 0; w < 4; ++w) tw[w] = (t < a.n_attr && w < a.W) ? a.att_first[(size_t)t * a.W + w] : 0u;
 }
 
 struct Dense {
@@ -693,6 +721,9 @@ __global__ void __launch_bounds__(64 * kApplyWaves) learn_apply_kernel(LearnArgs
   if (task < n_bil) {
     // bilinear weight tile: outputs o0..o0+15 of input i, all j: D[o][j] = sum_r g1[o][r] s_i[r] t_j[r]
     const int ot = task / a.N, i = task - ot * a.N, o0 = 16 * ot;
+    uint32_t tpre[4][4];   // the first four target rows' words of this lane (t = g + 4u), requested now
+#pragma unroll
+    for (int u = 0; u < 4; ++u) target_words(a, g + 4 * u, tpre[u]);
     const uint32_t* si = a.srow + (size_t)(i >> 5) * B;
     const float* grow = a.g1 + (size_t)(o0 + rr) * B;
     f32x4 acc[NT];
@@ -760,9 +791,15 @@ __global__ void __launch_bounds__(64 * kApplyWaves) learn_apply_kernel(LearnArgs
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // the target-table rows of input i for these 16 outputs, from the weights just written
-    for (int t = g; t < a.n_attr; t += 4) {
-      const float s = table_entry(a, t, &wsc[wave][rr][0]);
-      a.Tq[((size_t)t * a.N + i) * 256 + rr * 16 + ot] = s;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = g + 4 * u;
+      if (t < a.n_attr) a.Tq[((size_t)t * a.N + i) * 256 + rr * 16 + ot] = table_entry(tpre[u], a.N, &wsc[wave][rr][0]);
+    }
+    for (int t = g + 16; t < a.n_attr; t += 4) {
+      uint32_t tw[4];
+      target_words(a, t, tw);
+      a.Tq[((size_t)t * a.N + i) * 256 + rr * 16 + ot] = table_entry(tw, a.N, &wsc[wave][rr][0]);
     }
     PBN_LSTAMP(2, 3);
     return;
@@ -879,6 +916,14 @@ Work make_work(int N, int H, int64_t B) {
 unsigned long long* g_lstamps = nullptr;   // pbn_debug_set_learn_stamps
 #endif
 
+// learn_bwd's LDS: the delta planes and the split tiles, or the TD pass's staged head rows (the
+// same space), then the per-(row, branch) TD values
+size_t learn_bwd_lds(int H, int Apad, int K) {
+  const size_t planes = (size_t)(H * Apad + H * kDH + kD3 + kD2 + kD1) * kRows + kWaves * 64 * 4;
+  const size_t staged = (size_t)3 * H * kRows * (Apad + 4);
+  return (std::max(planes, staged) + 3 * kRows * K) * sizeof(float);
+}
+
 int check_shape(int N, int n_branches) {
   if (N < 1 || N > 127) return pbn::set_error(PBN_EINVAL, "fused BDQ update: 1 <= n_nodes <= 127");
   if (n_branches < 1 || n_branches > 7) return pbn::set_error(PBN_EINVAL, "fused BDQ update: n_branches 1..7");
@@ -912,6 +957,8 @@ int pbn_bdq_learn_workspace(int32_t n_nodes, int32_t n_branches, int64_t batch, 
   if (!bytes) return pbn::set_error(PBN_EINVAL, "null bytes");
   if (batch < kRows || batch % kRows || batch > (1 << 20))
     return pbn::set_error(PBN_EINVAL, "fused BDQ update: batch a multiple of 16, 16..2^20");
+  if (learn_bwd_lds(n_branches + 1, 16 * ((n_nodes + 16) / 16), n_branches) > 160 * 1024)
+    return pbn::set_error(PBN_EINVAL, "fused BDQ update: (n_branches + 1) x (n_nodes + 1) too large for one block's LDS");
   *bytes = make_work(n_nodes, n_branches + 1, batch).total * (int64_t)sizeof(float);
   return PBN_OK;
 }
@@ -1015,10 +1062,11 @@ int pbn_bdq_learn(const pbn_net* net, int64_t batch, const int64_t* d_idx, int64
 #endif
   const hipStream_t s = (hipStream_t)stream;
   const int tiles = (int)(batch / kRows);
-  const size_t lds_f = ((size_t)(kD0 + kD1 + kD2 + kD3 + kDH * H) * kRows + 2 * 4 * kRows) * sizeof(float);
+  const size_t lds_f = ((size_t)(kD0 + kD1 + kD2 + kD3 + kDH * H) * kRows + 4 * kRows + 2 * kRows) * sizeof(float) +
+                       kRows * 128;
   hipLaunchKernelGGL(learn_fwd_kernel, dim3(3 * tiles), dim3(kThreads), lds_f, s, a);
   if (hipGetLastError() != hipSuccess) return pbn::set_error(PBN_EDEVICE, "learn_fwd_kernel launch failed");
-  const size_t lds_b = ((size_t)(H * a.Apad + H * kDH + kD3 + kD2 + kD1) * kRows + kWaves * 64 * 4 + kWaves) * sizeof(float);
+  const size_t lds_b = learn_bwd_lds(H, a.Apad, n_branches);
   if (lds_b > 64 * 1024 && hipFuncSetAttribute((const void*)learn_bwd_kernel,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_b) != hipSuccess)
     return pbn::set_error(PBN_EDEVICE, "hipFuncSetAttribute failed");

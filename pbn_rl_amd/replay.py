@@ -35,7 +35,8 @@ from . import _lib
 from .agent import BatchedBDQ, BranchingQNetwork
 from .vector_env import VectorPBNEnv
 
-__all__ = ["DeviceReplay", "bdq_update", "soft_update", "BDQLearner", "FusedBDQUpdate", "bdq_layout"]
+__all__ = ["DeviceReplay", "bdq_update", "soft_update", "BDQLearner", "FusedBDQUpdate", "bdq_layout",
+           "fused_update_supported"]
 
 
 class DeviceReplay:
@@ -74,12 +75,15 @@ class DeviceReplay:
         self.size = min(self.size + n, self.capacity)
 
     def store_at(self, pos_t: torch.Tensor, size_t: torch.Tensor, state, target, action, reward, next_state,
-                 done, *, done_mask: int = 0, done_out: Optional[torch.Tensor] = None, advance: bool = True) -> None:
+                 done, *, done_mask: int = 0, done_out: Optional[torch.Tensor] = None, advance: bool = True,
+                 state_copy=None, target_copy=None) -> None:
         """``store`` with the ring position and fill level held in one-element int64 device
         tensors (advanced here, on the stream, unless ``advance`` is False) instead of host ints:
         graph-capturable.  The caller mirrors them in ``pos`` / ``size``.  ``done_mask`` != 0:
         ``done`` is the env's flags and a transition is done when ``flags & done_mask``;
-        ``done_out`` (uint8 [n]) then receives those 0/1 values too."""
+        ``done_out`` (uint8 [n]) then receives those 0/1 values too.  ``state_copy`` / ``target_copy``:
+        optional (dst, src) pairs copied element by element in the same pass, after the element of
+        ``state`` / ``target`` is read (dst may be ``state`` / ``target`` itself; GPU path only)."""
         n = target.shape[0]
         if n > self.capacity:
             raise ValueError("more transitions than the ring holds")
@@ -99,11 +103,15 @@ class DeviceReplay:
                                               done_out.data_ptr() if done_out is not None else None,
                                               self.state.data_ptr(), self.next_state.data_ptr(), self.target.data_ptr(),
                                               self.action.data_ptr(), self.reward.data_ptr(), self.done.data_ptr(),
+                                              *(t.data_ptr() if t is not None else None
+                                                for t in (state_copy or (None, None)) + (target_copy or (None, None))),
                                               torch.cuda.current_stream(self.device).cuda_stream), "pbn_replay_store")
             if advance:
                 pos_t.add_(n).remainder_(self.capacity)
                 size_t.add_(n).clamp_(max=self.capacity)
             return
+        if state_copy is not None or target_copy is not None:
+            raise ValueError("state_copy / target_copy need the GPU path (int32 / uint8 / float32 fields)")
         if done_mask:
             done = (done & done_mask) != 0
             if done_out is not None:
@@ -245,6 +253,14 @@ def bdq_layout(n_nodes: int, n_branches: int) -> List[int]:
     off = (ctypes.c_int64 * 13)()
     _lib.check(L.pbn_bdq_layout(n_nodes, n_branches, off), "pbn_bdq_layout")
     return list(off)
+
+
+def fused_update_supported(n_nodes: int, n_branches: int, batch_size: int) -> bool:
+    """Whether pbn_bdq_learn runs this shape (its workspace query accepts it): batch a multiple of
+    16, n_nodes <= 127, n_branches 1..7, and the backward's LDS within one block."""
+    L = _lib.load()
+    nbytes = ctypes.c_int64()
+    return L.pbn_bdq_learn_workspace(n_nodes, n_branches, batch_size, ctypes.byref(nbytes)) == 0
 
 
 def _bdq_segments(q: BranchingQNetwork):
@@ -403,8 +419,8 @@ class BDQLearner:
         self.q = self.agent.q.train()
         self.target = BranchingQNetwork((env.n_nodes, env.n_nodes), env.n_nodes + 1, self.agent.branches).to(env.device)
         self.target.load_state_dict(self.q.state_dict())
-        can_fuse = (env.device.type == "cuda" and self.agent.fused_tail and batch_size % 16 == 0
-                    and env.n_nodes <= 127 and isinstance(self.q, BranchingQNetwork))
+        can_fuse = (env.device.type == "cuda" and self.agent.fused_tail and isinstance(self.q, BranchingQNetwork)
+                    and fused_update_supported(env.n_nodes, self.agent.branches, batch_size))
         if fused and not can_fuse:
             raise ValueError("fused update: the reference BranchingQNetwork on a GPU env, batch a multiple of 16")
         self.fused: Optional[FusedBDQUpdate] = None
@@ -525,6 +541,7 @@ class BDQLearner:
         self._pos_t = torch.full((1,), self.replay.pos, dtype=torch.int64, device=dev)
         self._size_t = torch.full((1,), self.replay.size, dtype=torch.int64, device=dev)
         self._done_buf = torch.zeros(env.n_alloc, dtype=torch.uint8, device=dev)
+        self._tgt_prev = env.target.clone()   # the pre-step targets, carried by the ring store
         g = torch.cuda.CUDAGraph()
         g.register_generator_state(self.gen)
         if self.opt is not None:
@@ -537,15 +554,16 @@ class BDQLearner:
 
     def _graph_body(self):
         env = self.env
-        state = env.state.clone()
-        target = env.target.clone()
         self.agent.act_q(step_t=self._step_t, epsilon_t=self._eps32)
-        env.step_flipmask_dev(self._step_t)
-        # the ring store derives done from the flags; then one launch advances the step index,
+        env.step_flipmask_dev(self._step_t, copy_back=False)
+        # the ring store reads the pre-step state (still in env.state) and target (carried in
+        # _tgt_prev), derives done from the flags, and in the same pass moves the stepped state into
+        # env.state and the new targets into _tgt_prev; then one launch advances the step index,
         # the ring position and fill level and epsilon, and (fused) draws the frame's batches
-        self.replay.store_at(self._pos_t, self._size_t, state, target, self.agent.actions, env.reward,
+        self.replay.store_at(self._pos_t, self._size_t, env.state, self._tgt_prev, self.agent.actions, env.reward,
                              env.final_state, env.flags, done_mask=_lib.FLAG_TERMINATED | _lib.FLAG_TRUNCATED,
-                             done_out=self._done_buf, advance=False)
+                             done_out=self._done_buf, advance=False, state_copy=(env.state, env._state_next),
+                             target_copy=(self._tgt_prev, env.target))
         fused = self.fused is not None
         L = _lib.load()
         with torch.cuda.device(env.device):

@@ -183,12 +183,14 @@ class VectorPBNEnv:
         fm = control_to_flipmask(self.state[:, : self.num_envs], values, control_nodes, self.n_nodes)
         return self.step_flipmask(fm)
 
-    def step_flipmask_dev(self, step_t: torch.Tensor):
+    def step_flipmask_dev(self, step_t: torch.Tensor, copy_back: bool = True):
         """``step_flipmask(use_current=True)`` through ``pbn_step_dev``: the step index is read
         from the int64 device tensor ``step_t`` when the kernel runs, and the new state is
         copied back into ``self.state`` (no buffer swap), so the call can be captured in a
         hipGraph and replayed.  Neither ``step_t`` nor ``step_index`` is advanced here: the
-        caller advances ``step_t`` on the stream and mirrors it in ``step_index``."""
+        caller advances ``step_t`` on the stream and mirrors it in ``step_index``.  ``copy_back=False``
+        leaves the new state in ``_state_next`` for the caller to move (BDQLearner's captured frame
+        does it inside its ring store) and returns it instead of ``state``."""
         if step_t.dtype != torch.int64 or step_t.device != self.device or step_t.numel() != 1:
             raise ValueError("step_t must be a one-element int64 tensor on the env's device")
         L = _lib.load()
@@ -199,8 +201,10 @@ class VectorPBNEnv:
                                       mode, self.state.data_ptr(), self.flipmask.data_ptr(), self.target.data_ptr(),
                                       self.t.data_ptr(), self._state_next.data_ptr(), fs, self.reward.data_ptr(),
                                       self.flags.data_ptr(), self._stream()), "pbn_step_dev")
-        self.state.copy_(self._state_next)
         k = self.num_envs
+        if not copy_back:
+            return self._state_next[:, :k], self.reward[:k], self.flags[:k]
+        self.state.copy_(self._state_next)
         return self.state[:, :k], self.reward[:k], self.flags[:k]
 
     def rollout_buffers(self, n_steps: int, keep_obs: bool = False, keep_final: bool = True,

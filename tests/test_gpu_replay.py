@@ -214,3 +214,27 @@ def test_replay_store_done_from_flags():
     slots = (torch.arange(n, device=dev) + 100) % 128
     assert torch.equal(a.done[slots], want) and torch.equal(out, want)
     assert int(pos_t) == 100 and int(size_t) == 0
+
+
+def test_replay_store_in_pass_copies():
+    """store_at's state_copy / target_copy: the ring gets the values read before the same pass
+    overwrites them in place (the captured learner's copy-back of the stepped state)."""
+    dev = torch.device("cuda")
+    n = 64
+    a = DeviceReplay(64, 2, 3, dev)
+    g = torch.Generator(device=dev).manual_seed(4)
+    st = torch.randint(0, 2 ** 31, (2, n), device=dev, generator=g, dtype=torch.int32)
+    nxt = torch.randint(0, 2 ** 31, (2, n), device=dev, generator=g, dtype=torch.int32)
+    tg = torch.randint(0, 14, (n,), device=dev, generator=g).to(torch.uint8)
+    tg_new = torch.randint(0, 14, (n,), device=dev, generator=g).to(torch.uint8)
+    st0, tg0 = st.clone(), tg.clone()
+    act = torch.zeros(n, 3, dtype=torch.int32, device=dev)
+    rew = torch.zeros(n, device=dev)
+    done = torch.zeros(n, dtype=torch.uint8, device=dev)
+    pos_t = torch.tensor([0], dtype=torch.int64, device=dev)
+    size_t = torch.tensor([0], dtype=torch.int64, device=dev)
+    a.store_at(pos_t, size_t, st, tg, act, rew, nxt, done, state_copy=(st, nxt), target_copy=(tg, tg_new))
+    torch.cuda.synchronize()
+    assert torch.equal(a.state, st0) and torch.equal(a.target, tg0) and torch.equal(a.next_state, nxt)
+    assert torch.equal(st, nxt) and torch.equal(tg, tg_new)
+    assert int(pos_t) == 0 and int(size_t) == 64

@@ -54,3 +54,11 @@ def test_replay_rows_restatement():
         x, y, _, _ = pyoracle.draw(123, b, 5, 7, 0)
         assert rows[b] == ((x << 32 | y) * 540) >> 64
     assert rows.min() >= 0 and rows.max() < 540
+
+
+def test_fused_support_query():
+    from pbn_rl_amd.replay import fused_update_supported
+    assert fused_update_supported(28, 3, 256) and fused_update_supported(70, 3, 64)
+    assert not fused_update_supported(28, 3, 100)        # batch not a multiple of 16
+    assert not fused_update_supported(127, 7, 256)       # the backward's staged heads exceed one block's LDS
+    assert fused_update_supported(127, 3, 256)
