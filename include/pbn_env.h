@@ -22,7 +22,11 @@
  *                                                                 pbn_heads_to_flipmask / pbn_q_to_flipmask,
  *                                                                 or pbn_qnet_flipmask (both in one)
  *   update_policy's np.stack of sampled Transitions
- *        bdq_model/__init__.py:100-109                         -> pbn_obs_unpack
+ *        bdq_model/__init__.py:100-109                         -> pbn_obs_unpack, pbn_replay_batch
+ *   update_policy (forwards, TD loss, backward, clamp, Adam)
+ *        bdq_model/__init__.py:100-139                         -> pbn_bdq_learn (+ pbn_bdq_layout,
+ *                                                                 pbn_bdq_pack, pbn_replay_store,
+ *                                                                 pbn_replay_advance)
  *   a frame loop captured once and replayed (no reference counterpart)
  *                                                              -> pbn_step_dev, pbn_q_to_flipmask_dev
  *

@@ -3,7 +3,9 @@
   python tools/learn_profile.py [--envs 32768] [--frames 20]
 
 torch.profiler over eager frames after warm-up: per PyTorch operator its calls per frame and device
-time per frame, so the frame's ~170 kernels can be attributed to the update's operations.
+time per frame, so the PyTorch update's ~170 kernels can be attributed to its operations.  Profiles
+the PyTorch update (fused=False); the default learner's fused update is three HIP launches
+(tools/learn_stamps.py times their phases).
 """
 import argparse
 import json
@@ -37,7 +39,7 @@ def main():
     env.reset()
     torch.manual_seed(0)
     learner = BDQLearner(env, BranchingQNetwork((spec.n, spec.n), spec.n + 1, 3), capacity=4 * args.envs,
-                         learning_starts=256, epsilon_start=0.0, epsilon_final=0.0)
+                         learning_starts=256, epsilon_start=0.0, epsilon_final=0.0, fused=False)
     for _ in range(10):
         learner.frame()
     torch.cuda.synchronize()
