@@ -233,15 +233,20 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
   // (more heads or outputs than that load theirs in the layer's loop)
   const int at16 = a.Apad / 16;
   float4 w2[kD0 / 16], w3[kD1 / 16], w4[kD2 / 16], wh1[2][kD3 / 16], wh2[kDH / 16];
-  wfrag<kD0>(w2, P + a.off[L2_W], kD0, 16 * wave, kD1, lane);
-  wfrag<kD1>(w3, P + a.off[L3_W], kD1, 16 * (wave & 3), kD2, lane);
-  wfrag<kD2>(w4, P + a.off[L4_W], kD2, 16 * (wave & 1), kD3, lane);
+  auto fetch_weights = [&]() {
+    wfrag<kD0>(w2, P + a.off[L2_W], kD0, 16 * wave, kD1, lane);
+    wfrag<kD1>(w3, P + a.off[L3_W], kD1, 16 * (wave & 3), kD2, lane);
+    wfrag<kD2>(w4, P + a.off[L4_W], kD2, 16 * (wave & 1), kD3, lane);
 #pragma unroll
-  for (int u = 0; u < 2; ++u) wfrag<kD3>(wh1[u], P + a.off[H1_W], kD3, 16 * (wave + kWaves * u), a.H * kDH, lane);
-  {
-    const int tt = wave < a.H * at16 ? wave : 0, h = tt / at16;
-    wfrag<kDH>(wh2, P + a.off[H2_W] + (size_t)h * a.A * kDH, kDH, 16 * (tt - h * at16), a.A, lane);
-  }
+    for (int u = 0; u < 2; ++u) wfrag<kD3>(wh1[u], P + a.off[H1_W], kD3, 16 * (wave + kWaves * u), a.H * kDH, lane);
+    {
+      const int tt = wave < a.H * at16 ? wave : 0, h = tt / at16;
+      wfrag<kDH>(wh2, P + a.off[H2_W] + (size_t)h * a.A * kDH, kDH, 16 * (tt - h * at16), a.A, lane);
+    }
+  };
+#ifndef PBN_DIAG_LATE_WFRAG
+  fetch_weights();
+#endif
   // bilinear layer: y[o] = bias[o] + sum over the set bits i of T[t][i][o] (t = the row's target;
   // a row without a target has an all-zero second input: bias only).  Wave w takes rows 2w, 2w+1;
   // lane p reads Tq positions 4p..4p+3 ([t][i][j][q] = T[t][i][16 q + j]: o = 16 q + j): only the
@@ -294,6 +299,9 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
     }
   }
   PBN_LSTAMP(0, 2);
+#ifdef PBN_DIAG_LATE_WFRAG   // (diagnostic: the weights requested after the bilinear layer's table reads)
+  fetch_weights();
+#endif
   __syncthreads();
   PBN_LSTAMP(0, 3);
   if (set == 0) keep = a.h2;

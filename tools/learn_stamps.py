@@ -30,8 +30,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=32768)
     ap.add_argument("--frames", type=int, default=4)
+    ap.add_argument("--lib", default=STAMP_LIB, help="a stamps build (default: tools/stamps.py --build's)")
     args = ap.parse_args()
-    os.environ["PBN_LIB"] = STAMP_LIB
+    os.environ["PBN_LIB"] = args.lib
     import numpy as np
     import torch
 
