@@ -498,6 +498,16 @@ class BDQLearner:
                     self._soft_update()
         return reward, done
 
+    def refresh_weights(self) -> None:
+        """Call after changing ``q`` / ``target`` weights outside frame() (e.g. loading a reference
+        checkpoint, bdq_model/__init__.py:244, with load_state_dict): repacks the fused update's
+        bilinear target tables, or the PyTorch path's cached target head weights.  A captured
+        frame reads the same buffers, so it needs no re-capture."""
+        if self.fused is not None:
+            self.fused.pack()
+        else:
+            self._refresh_target_weights()
+
     def _update(self, idx: torch.Tensor) -> torch.Tensor:
         if self.fused is not None:
             return self.fused.update(self.replay, idx)

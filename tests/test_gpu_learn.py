@@ -139,23 +139,25 @@ def test_fused_layout_views():
     assert torch.equal(bias, q.model[0].bilinear.bias)
 
 
-def _learner(n, seed, fused):
+def _learner(n, seed, fused, updates_per_frame=1):
     spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.01)
     env = VectorPBNEnv(spec, n, seed=seed)
     torch.manual_seed(4)
     lr = BDQLearner(env, BranchingQNetwork((28, 28), 29, 3), capacity=8 * n, learning_starts=2 * n,
                     batch_size=256, target_update=4, epsilon_start=1.0, epsilon_final=1.0, seed=11,
-                    graphable=True, fused=fused)
+                    graphable=True, fused=fused, updates_per_frame=updates_per_frame)
     env.reset()
     return env, lr
 
 
-def test_captured_fused_learner_is_bit_exact():
+@pytest.mark.parametrize("upf", [1, 2])
+def test_captured_fused_learner_is_bit_exact(upf):
     """epsilon = 1 and the fused update (no atomics, fixed reduction orders): a captured learner's
-    weights, Adam state and losses equal the eager one's bit for bit, soft updates included."""
+    weights, Adam state and losses equal the eager one's bit for bit, soft updates included, with
+    one or two updates per frame (both batches of a frame from one draw)."""
     n = 1024
-    env_e, eager = _learner(n, 21, True)
-    env_g, graph = _learner(n, 21, True)
+    env_e, eager = _learner(n, 21, True, upf)
+    env_g, graph = _learner(n, 21, True, upf)
     assert eager.fused is not None and eager.opt is None
     graph.capture()
     for _ in range(graph.frames):
@@ -193,3 +195,28 @@ def test_fused_learner_acts_with_its_tables():
     torch.cuda.synchronize()
     same = (lr.agent.actions == ref.actions).float().mean().item()
     assert same > 0.999, same   # (argmax ties broken by fp rounding may differ)
+
+
+def test_fused_learner_loads_a_checkpoint():
+    """A reference-style checkpoint (the networks' state_dict, bdq_model/__init__.py:244) loads into
+    the fused learner's view parameters; refresh_weights() repacks the tables the acting frame and
+    the update read, equal to pbn_bdq_pack of the loaded weights."""
+    env, lr = _learner(256, 3, True)
+    src = BranchingQNetwork((28, 28), 29, 3).cuda()
+    with torch.no_grad():
+        for p in src.parameters():
+            p.mul_(-1.5)
+    lr.q.load_state_dict(src.state_dict())
+    lr.target.load_state_dict(src.state_dict())
+    lr.refresh_weights()
+    torch.cuda.synchronize()
+    for (k, a), b in zip(lr.q.named_parameters(), src.parameters()):
+        assert torch.equal(a, b), k
+    targets = torch.tensor([list(a[0]) for a in env.spec.attractors], dtype=torch.float32, device="cuda")
+    T = src.model[0].target_table(targets)
+    for table in (lr.fused.q_table, lr.fused.t_table):
+        assert torch.allclose(table.transpose(2, 3).reshape(T.shape), T, rtol=1e-5, atol=1e-6)
+    for _ in range(3):
+        lr.frame()
+    torch.cuda.synchronize()
+    assert torch.isfinite(lr.last_loss)
