@@ -235,8 +235,8 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
   float4 w2[kD0 / 16], w3[kD1 / 16], w4[kD2 / 16], wh1[2][kD3 / 16], wh2[kDH / 16];
   auto fetch_weights = [&]() {
     wfrag<kD0>(w2, P + a.off[L2_W], kD0, 16 * wave, kD1, lane);
-    wfrag<kD1>(w3, P + a.off[L3_W], kD1, 16 * (wave & 3), kD2, lane);
-    wfrag<kD2>(w4, P + a.off[L4_W], kD2, 16 * (wave & 1), kD3, lane);
+    if (wave < kD2 / 16) wfrag<kD1>(w3, P + a.off[L3_W], kD1, 16 * wave, kD2, lane);   // (only these waves
+    if (wave < kD3 / 16) wfrag<kD2>(w4, P + a.off[L4_W], kD2, 16 * wave, kD3, lane);   // compute the layers)
 #pragma unroll
     for (int u = 0; u < 2; ++u) wfrag<kD3>(wh1[u], P + a.off[H1_W], kD3, 16 * (wave + kWaves * u), a.H * kDH, lane);
     {
