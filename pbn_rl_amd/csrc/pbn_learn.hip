@@ -664,15 +664,27 @@ __global__ void __launch_bounds__(kThreads) learn_bwd_kernel(LearnArgs a) {
 
 // ---- Adam (torch.optim.Adam, fused, defaults but lr: bdq_model/__init__.py:34) on one element,
 // after clamping its gradient to [-c, c] (torch.clamp: NaN stays NaN)
-__device__ __forceinline__ void adam(const LearnArgs& a, int64_t i, float g, float bc1, float bc2s) {
+// The element's parameter and moments are loaded ahead (adam_load, at the task's start: the
+// round trip overlaps the gradient loop), adam_apply writes the step and returns the new value.
+struct AdamIn {
+  float p, m, v;
+};
+
+__device__ __forceinline__ AdamIn adam_load(const LearnArgs& a, int64_t i, bool ok) {
+  return ok ? AdamIn{a.P[i], a.m[i], a.v[i]} : AdamIn{0.f, 0.f, 0.f};
+}
+
+__device__ __forceinline__ float adam_apply(const LearnArgs& a, int64_t i, AdamIn in, float g, float bc1, float bc2s) {
   g = isnan(g) ? g : fminf(fmaxf(g, -a.clampv), a.clampv);
   if (a.grad) a.grad[i] = g;
-  const float m = a.b1 * a.m[i] + (1.f - a.b1) * g;
-  const float v = a.b2 * a.v[i] + (1.f - a.b2) * g * g;
+  const float m = a.b1 * in.m + (1.f - a.b1) * g;
+  const float v = a.b2 * in.v + (1.f - a.b2) * g * g;
   a.m[i] = m;
   a.v[i] = v;
   const float denom = sqrtf(v) / bc2s + a.eps;
-  a.P[i] -= (a.lr / bc1) * m / denom;
+  const float p = in.p - (a.lr / bc1) * m / denom;
+  a.P[i] = p;
+  return p;
 }
 
 // T[t][i][o] = sum_j target_t[j] W[o][i][j] in j order (pbn_bdq_pack computes the same sums), from
@@ -732,6 +744,16 @@ __global__ void __launch_bounds__(64 * kApplyWaves) learn_apply_kernel(LearnArgs
     uint32_t tpre[4][4];   // the first four target rows' words of this lane (t = g + 4u), requested now
 #pragma unroll
     for (int u = 0; u < 4; ++u) target_words(a, g + 4 * u, tpre[u]);
+    const int64_t NN = (int64_t)a.N * a.N;
+    AdamIn pre[NT][4];
+#pragma unroll
+    for (int jt = 0; jt < NT; ++jt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int jj = 16 * jt + rr;
+        pre[jt][v] = adam_load(a, a.off[BIL_W] + (o0 + 4 * g + v) * NN + (int64_t)i * a.N + jj, jj < a.N);
+      }
+    const AdamIn preb = adam_load(a, a.off[BIL_B] + o0 + rr, i == 0 && g == 0);
     const uint32_t* si = a.srow + (size_t)(i >> 5) * B;
     const float* grow = a.g1 + (size_t)(o0 + rr) * B;
     f32x4 acc[NT];
@@ -773,7 +795,6 @@ __global__ void __launch_bounds__(64 * kApplyWaves) learn_apply_kernel(LearnArgs
       }
     }
     PBN_LSTAMP(2, 1);
-    const int64_t NN = (int64_t)a.N * a.N;
 #pragma unroll
     for (int jt = 0; jt < NT; ++jt) {
       const int jj = 16 * jt + rr;
@@ -781,18 +802,14 @@ __global__ void __launch_bounds__(64 * kApplyWaves) learn_apply_kernel(LearnArgs
       for (int v = 0; v < 4; ++v) {
         const int o = o0 + 4 * g + v;
         float nw = 0.f;
-        if (jj < a.N) {
-          const int64_t pi = a.off[BIL_W] + o * NN + (int64_t)i * a.N + jj;
-          adam(a, pi, acc[jt][v], bc1, bc2s);
-          nw = a.P[pi];
-        }
+        if (jj < a.N) nw = adam_apply(a, a.off[BIL_W] + o * NN + (int64_t)i * a.N + jj, pre[jt][v], acc[jt][v], bc1, bc2s);
         wsc[wave][4 * g + v][jj] = nw;
       }
     }
     if (i == 0) {   // the bilinear bias: sum over the batch of g1 (lane groups added in a fixed order)
       bsum += __shfl_xor(bsum, 16);
       bsum += __shfl_xor(bsum, 32);
-      if (g == 0) adam(a, a.off[BIL_B] + o0 + rr, bsum, bc1, bc2s);
+      if (g == 0) adam_apply(a, a.off[BIL_B] + o0 + rr, preb, bsum, bc1, bc2s);
     }
     PBN_LSTAMP(2, 2);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -840,6 +857,13 @@ __global__ void __launch_bounds__(64 * kApplyWaves) learn_apply_kernel(LearnArgs
   ot = task / L.k_tiles;
   kt = task - ot * L.k_tiles;
   const int o0 = 16 * ot, k0 = 16 * kt;
+  AdamIn pre[4];
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int o = o0 + 4 * g + v;
+    pre[v] = adam_load(a, L.w_off + (int64_t)o * L.ldw + k0 + rr, o < L.o_valid);
+  }
+  const AdamIn preb = adam_load(a, L.b_off + o0 + rr, kt == 0 && g == 0 && o0 + rr < L.o_valid);
   const float* yrow = L.dY + (size_t)(o0 + rr) * B;
   const float* xrow = L.X + (size_t)(k0 + rr) * B;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -867,12 +891,12 @@ __global__ void __launch_bounds__(64 * kApplyWaves) learn_apply_kernel(LearnArgs
 #pragma unroll
   for (int v = 0; v < 4; ++v) {
     const int o = o0 + 4 * g + v;
-    if (o < L.o_valid) adam(a, L.w_off + (int64_t)o * L.ldw + k0 + rr, acc[v], bc1, bc2s);
+    if (o < L.o_valid) adam_apply(a, L.w_off + (int64_t)o * L.ldw + k0 + rr, pre[v], acc[v], bc1, bc2s);
   }
   if (kt == 0) {
     bsum += __shfl_xor(bsum, 16);
     bsum += __shfl_xor(bsum, 32);
-    if (g == 0 && o0 + rr < L.o_valid) adam(a, L.b_off + o0 + rr, bsum, bc1, bc2s);
+    if (g == 0 && o0 + rr < L.o_valid) adam_apply(a, L.b_off + o0 + rr, preb, bsum, bc1, bc2s);
   }
   PBN_LSTAMP(2, 5);
 }
