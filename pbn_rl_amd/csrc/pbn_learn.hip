@@ -133,6 +133,15 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
 
 __device__ __forceinline__ float leaky(float x, float slope) { return x > 0.f ? x : x * slope; }
 
+// A block barrier that orders LDS only: the waves of learn_fwd / learn_bwd exchange nothing
+// through global memory, so a barrier need not wait for their global stores (on CDNA they count
+// in vmcnt with the loads) or for the weight fragments requested ahead.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 __device__ __forceinline__ int64_t row_index(const LearnArgs& a, int b) {
   const int64_t j = a.idx[b];
   return j < 0 ? 0 : (j >= a.cap ? a.cap - 1 : j);   // (sample_indices keeps 0 <= j < size)
@@ -211,6 +220,24 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int B = a.B;
   float* keep = nullptr;   // the online s rows keep their activations for the backward
+  // every layer's weight fragments of this wave, requested at entry (they arrive during the row
+  // and bilinear phases: no barrier waits for them)
+  const int at16 = a.Apad / 16;
+  float4 w2[kD0 / 16], w3[kD1 / 16], w4[kD2 / 16], wh1[2][kD3 / 16], wh2[kDH / 16];
+  auto fetch_weights = [&]() {
+    wfrag<kD0>(w2, P + a.off[L2_W], kD0, 16 * wave, kD1, lane);
+    if (wave < kD2 / 16) wfrag<kD1>(w3, P + a.off[L3_W], kD1, 16 * wave, kD2, lane);   // (only these waves
+    if (wave < kD3 / 16) wfrag<kD2>(w4, P + a.off[L4_W], kD2, 16 * wave, kD3, lane);   // compute the layers)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) wfrag<kD3>(wh1[u], P + a.off[H1_W], kD3, 16 * (wave + kWaves * u), a.H * kDH, lane);
+    {
+      const int tt = wave < a.H * at16 ? wave : 0, h = tt / at16;
+      wfrag<kDH>(wh2, P + a.off[H2_W] + (size_t)h * a.A * kDH, kDH, 16 * (tt - h * at16), a.A, lane);
+    }
+  };
+#ifndef PBN_DIAG_LATE_WFRAG
+  if (wave != 0) fetch_weights();   // (wave 0 loads the rows first: the load counter is in order)
+#endif
   if (tid < kRows) {   // the rows' targets, state words and the list of their set bits
     const int64_t j = row_index(a, b0 + tid);
     stg[tid] = a.tgt[j];
@@ -226,27 +253,11 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
     }
     scnt[tid] = c;
   }
-  __syncthreads();
-  PBN_LSTAMP(0, 1);
-  // every layer's weight fragments of this wave, requested now (they arrive during the bilinear
-  // layer): its trunk tiles, its first two first-head-layer tiles and its first second-layer tile
-  // (more heads or outputs than that load theirs in the layer's loop)
-  const int at16 = a.Apad / 16;
-  float4 w2[kD0 / 16], w3[kD1 / 16], w4[kD2 / 16], wh1[2][kD3 / 16], wh2[kDH / 16];
-  auto fetch_weights = [&]() {
-    wfrag<kD0>(w2, P + a.off[L2_W], kD0, 16 * wave, kD1, lane);
-    if (wave < kD2 / 16) wfrag<kD1>(w3, P + a.off[L3_W], kD1, 16 * wave, kD2, lane);   // (only these waves
-    if (wave < kD3 / 16) wfrag<kD2>(w4, P + a.off[L4_W], kD2, 16 * wave, kD3, lane);   // compute the layers)
-#pragma unroll
-    for (int u = 0; u < 2; ++u) wfrag<kD3>(wh1[u], P + a.off[H1_W], kD3, 16 * (wave + kWaves * u), a.H * kDH, lane);
-    {
-      const int tt = wave < a.H * at16 ? wave : 0, h = tt / at16;
-      wfrag<kDH>(wh2, P + a.off[H2_W] + (size_t)h * a.A * kDH, kDH, 16 * (tt - h * at16), a.A, lane);
-    }
-  };
 #ifndef PBN_DIAG_LATE_WFRAG
-  fetch_weights();
+  if (wave == 0) fetch_weights();
 #endif
+  lds_barrier();
+  PBN_LSTAMP(0, 1);
   // bilinear layer: y[o] = bias[o] + sum over the set bits i of T[t][i][o] (t = the row's target;
   // a row without a target has an all-zero second input: bias only).  Wave w takes rows 2w, 2w+1;
   // lane p reads Tq positions 4p..4p+3 ([t][i][j][q] = T[t][i][16 q + j]: o = 16 q + j): only the
@@ -302,7 +313,7 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
 #ifdef PBN_DIAG_LATE_WFRAG   // (diagnostic: the weights requested after the bilinear layer's table reads)
   fetch_weights();
 #endif
-  __syncthreads();
+  lds_barrier();
   PBN_LSTAMP(0, 3);
   if (set == 0) keep = a.h2;
   {   // 256 -> 128: one output tile per wave
@@ -310,19 +321,19 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
     fwd_store(acc, P + a.off[L2_B], 16 * wave, a.slope, X2, keep, B, b0, lane);
   }
   PBN_LSTAMP(0, 4);
-  __syncthreads();
+  lds_barrier();
   PBN_LSTAMP(0, 5);
   if (wave < kD2 / 16) {   // 128 -> 64
     const f32x4 acc = fwd_tile<kD1>(w3, X2, lane);
     fwd_store(acc, P + a.off[L3_B], 16 * wave, a.slope, X3, set == 0 ? a.h3 : nullptr, B, b0, lane);
   }
-  __syncthreads();
+  lds_barrier();
   PBN_LSTAMP(0, 6);
   if (wave < kD3 / 16) {   // 64 -> 32
     const f32x4 acc = fwd_tile<kD2>(w4, X3, lane);
     fwd_store(acc, P + a.off[L4_B], 16 * wave, a.slope, X4, set == 0 ? a.h4 : nullptr, B, b0, lane);
   }
-  __syncthreads();
+  lds_barrier();
   PBN_LSTAMP(0, 7);
   {   // the H first head layers: 32 -> 64 H
     const int n1 = a.H * kDH / 16;
@@ -341,7 +352,7 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
       fwd_store(acc, P + a.off[H1_B], 16 * tt, a.slope, XH, set == 0 ? a.hh : nullptr, B, b0, lane);
     }
   }
-  __syncthreads();
+  lds_barrier();
   PBN_LSTAMP(0, 8);
   // second head layers: head h, outputs 16 at .. (A of them, no activation) -> heads[set][h][b][a]
   auto head_out = [&](const float4 (&wl)[kDH / 16], int tt) {
@@ -512,7 +523,7 @@ __global__ void __launch_bounds__(kThreads) learn_bwd_kernel(LearnArgs a) {
       a.trow[(size_t)w * B + b] = tg < a.n_attr ? a.att_first[(size_t)tg * a.W + w] : 0u;
     }
   }
-  __syncthreads();
+  lds_barrier();
   PBN_LSTAMP(1, 2);
   if (tid < kRows * K) {
     const int r = tid & 15, k = tid >> 4;
@@ -564,7 +575,7 @@ __global__ void __launch_bounds__(kThreads) learn_bwd_kernel(LearnArgs a) {
     sact[r * K + k] = ak;
   }
   PBN_LSTAMP(1, 3);
-  __syncthreads();
+  lds_barrier();
   PBN_LSTAMP(1, 4);
   // the gradient at the head outputs: d/d adv[k][o] = g_k ([o == a_k] - 1/A), d/d v = sum_k g_k
   // (0 for the value head's other outputs and the padding)
@@ -593,7 +604,7 @@ __global__ void __launch_bounds__(kThreads) learn_bwd_kernel(LearnArgs a) {
       if (tile == 0) a.step[0] += 1.f;   // Adam's step count, read by learn_apply
     }
   }
-  __syncthreads();
+  lds_barrier();
   // the last layer's fragments (256 inputs: tiles wave, wave + 8), requested now for the end
   float w2[2][8][4];
 #pragma unroll
@@ -625,32 +636,32 @@ __global__ void __launch_bounds__(kThreads) learn_bwd_kernel(LearnArgs a) {
     bwd_store(acc, act_frag(a.hh, h * kDH + c0, B, b0, lane), h * kDH + c0, a.slope, DHH, a.dhh, B, b0, lane);
   }
   PBN_LSTAMP(1, 5);
-  __syncthreads();
+  lds_barrier();
   PBN_LSTAMP(1, 6);
   {   // first head layers: 64 H -> 32, each output tile split over four waves (H blocks each)
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     acc = bwd_mma<8>(acc, wh1, q1 * H, q1 * H + H, DHH, lane);
     *reinterpret_cast<f32x4*>(part + (wave * 64 + lane) * 4) = acc;
   }
-  __syncthreads();
+  lds_barrier();
   if (wave < kD3 / 16) {   // the four quarters added in order
     f32x4 acc = *reinterpret_cast<const f32x4*>(part + (wave * 64 + lane) * 4);
 #pragma unroll
     for (int qq = 1; qq < 4; ++qq) acc += *reinterpret_cast<const f32x4*>(part + ((wave + 2 * qq) * 64 + lane) * 4);
     bwd_store(acc, y4, 16 * wave, a.slope, DH4, a.dh4, B, b0, lane);
   }
-  __syncthreads();
+  lds_barrier();
   PBN_LSTAMP(1, 7);
   if (wave < kD2 / 16) {   // 32 -> 64
     const f32x4 acc = bwd_mma<2>(f32x4{0.f, 0.f, 0.f, 0.f}, w4, 0, kD3 / 16, DH4, lane);
     bwd_store(acc, y3, 16 * wave, a.slope, DH3, a.dh3, B, b0, lane);
   }
-  __syncthreads();
+  lds_barrier();
   {   // 64 -> 128
     const f32x4 acc = bwd_mma<4>(f32x4{0.f, 0.f, 0.f, 0.f}, w3, 0, kD2 / 16, DH3, lane);
     bwd_store(acc, y2, 16 * wave, a.slope, DH2, a.dh2, B, b0, lane);
   }
-  __syncthreads();
+  lds_barrier();
   PBN_LSTAMP(1, 8);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {   // 128 -> 256: the bilinear layer's output gradient
