@@ -16,6 +16,7 @@
 #   stamps           the pipelined kernel's per-role segment clocks at iteration 10 (diagnostic build
 #                    pbn_rl_amd/libpbn_env_stamps.so: tools/stamps.py --build), 20- and 100-step launches
 #   qstamps          config 5's Q-network launch per-phase clocks (stamps build; tools/qnet_stamps.py)
+#   lstamps          the fused learner update's per-phase clocks (stamps build; tools/learn_stamps.py)
 #   settle           the driver's command (with its settle_law and hand-off fields) and config 2 under the
 #                    settle law alone (--settle 64, 200 steps) + its kernel trace
 #   bdqpmc           the BDQ frame under two PMC passes: L2 hits / misses / requests, HBM fetch + write
@@ -81,6 +82,10 @@ for step in "$@"; do
     qstamps)
       timeout -k 10 180 python tools/qnet_stamps.py > "$out/qstamps.json" 2> "$out/qstamps.err" || fail qstamps
       echo "qstamps done" ;;
+    lstamps)
+      timeout -k 10 180 python tools/learn_stamps.py > "$out/learn_stamps.json" 2> "$out/learn_stamps.err" \
+        || fail lstamps
+      echo "lstamps done" ;;
     settle)
       bench bench_driver --gpus 1 --steps 20 --warmup 5
       bench bench_settle64 --settle 64 --steps 200 --warmup 20 --no-cpu-baseline --no-gather
