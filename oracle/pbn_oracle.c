@@ -187,49 +187,60 @@ int oracle_reset(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t e
   return 0;
 }
 
-/* the rule update of every node of env bit b of its group from state s1, digit words D[i][d] */
-static void rule_update(const pbn_net_desc* d, const uint32_t* s1, uint32_t D[][16], int b, uint32_t* sp) {
-  const int N = d->n_nodes, W = words_of(N), B = d->prob_bits;
+/* the rule update of every node from state s1 and the nodes' B-bit selection uniforms U[i]
+ * (function j = min{j : U[i] < c_ij}) */
+static void rule_update(const pbn_net_desc* d, const uint32_t* s1, const uint32_t* U, uint32_t* sp) {
+  const int N = d->n_nodes, W = words_of(N);
   uint8_t gv[PBN_MAX_GATES];
   eval_gates(d, s1, gv);
   for (int w = 0; w < W; ++w) sp[w] = 0;
   for (int i = 0; i < N; ++i) {
-    int f0 = d->node_func_start[i], nf = d->node_func_start[i + 1] - f0, x;
-    if (nf == 1) {
-      x = eval_func(d, f0, s1, gv);
-    } else {
-      uint32_t u = 0;
-      for (int dd = 0; dd < B; ++dd) u |= ((D[i][dd] >> b) & 1u) << (B - 1 - dd);
-      int j = 0;
-      while (j < nf - 1 && !(u < d->func_threshold[f0 + j])) ++j;
-      x = eval_func(d, f0 + j, s1, gv);
-    }
-    if (x) sp[i >> 5] |= 1u << (i & 31);
+    int f0 = d->node_func_start[i], nf = d->node_func_start[i + 1] - f0, j = 0;
+    while (j < nf - 1 && !(U[i] < d->func_threshold[f0 + j])) ++j;
+    if (eval_func(d, f0 + j, s1, gv)) sp[i >> 5] |= 1u << (i & 31);
   }
 }
 
-/* selection digit words of group G for update `sub` of a step: sub 0 = the SEL stream (the
- * one-update law), sub k >= 1 = SETTLE_SEL with idx (k-1) << 9 | 4i + c */
-static void group_digits(const pbn_net_desc* d, uint64_t seed, uint64_t G, uint64_t step, int sub,
-                         uint32_t D[][16]) {
+/* one-update law: selection digit words of group G (SEL call 4i + c, word d & 3 = digit plane
+ * 4c + d, digit 0 the MSB), and env bit b's uniforms U[i] from them */
+static void group_digits(const pbn_net_desc* d, uint64_t seed, uint64_t G, uint64_t step, uint32_t D[][16]) {
   const int N = d->n_nodes, B = d->prob_bits;
   for (int i = 0; i < N; ++i) {
     int nf = d->node_func_start[i + 1] - d->node_func_start[i];
     if (nf < 2) continue;
-    for (int c = 0; c < B / 4; ++c) {
-      if (sub == 0) draw(seed, G, step, STREAM_SEL, (uint32_t)(4 * i + c), &D[i][4 * c]);
-      else draw(seed, G, step, STREAM_SETTLE_SEL, ((uint32_t)(sub - 1) << 9) | (uint32_t)(4 * i + c), &D[i][4 * c]);
-    }
+    for (int c = 0; c < B / 4; ++c) draw(seed, G, step, STREAM_SEL, (uint32_t)(4 * i + c), &D[i][4 * c]);
   }
 }
 
-/* settle law (settle_max >= 2): updates k = 1 .. settle_max-1 of env e (group bit b) from sp
- * until sp is a state of some attractor.  Update k: perturbation gaps j = 0, 1, ... from
- * SETTLE_ENV call ((k-1) << 8 | j >> 2), word j & 3; unperturbed, the rule update with the
- * group's SETTLE_SEL digits of update k (Dk[k-1], drawn on demand).  Returns 1 if still
- * outside every attractor after the last update; *nupd counts the updates applied. */
-static int settle(const pbn_net_desc* d, uint64_t seed, uint64_t G, uint64_t e, uint64_t step, int b,
-                  uint32_t (*Dk)[PBN_MAX_NODES][16], int* have, uint32_t* sp, int* perturbed, int* nupd) {
+static void group_uniforms(const pbn_net_desc* d, uint32_t D[][16], int b, uint32_t* U) {
+  const int N = d->n_nodes, B = d->prob_bits;
+  for (int i = 0; i < N; ++i) {
+    int nf = d->node_func_start[i + 1] - d->node_func_start[i];
+    U[i] = 0;
+    if (nf < 2) continue;
+    for (int dd = 0; dd < B; ++dd) U[i] |= ((D[i][dd] >> b) & 1u) << (B - 1 - dd);
+  }
+}
+
+/* settle law: env e's uniforms of update k of its step, keyed per env (DESIGN.md "Step law"):
+ * node i's is the top B bits of 16-bit field i & 1 of word (i >> 1) & 3 of SETTLE_SEL call
+ * (k << 8 | i >> 3) */
+static void env_uniforms(const pbn_net_desc* d, uint64_t seed, uint64_t e, uint64_t step, int k, uint32_t* U) {
+  const int N = d->n_nodes, B = d->prob_bits;
+  uint32_t P[4];
+  for (int i = 0; i < N; ++i) {
+    if ((i & 7) == 0) draw(seed, e, step, STREAM_SETTLE_SEL, ((uint32_t)k << 8) | (uint32_t)(i >> 3), P);
+    U[i] = ((P[(i >> 1) & 3] >> (16 * (i & 1))) & 0xFFFFu) >> (16 - B);
+  }
+}
+
+/* settle law (settle_max >= 2): updates k = 1 .. settle_max-1 of env e from sp until sp is a
+ * state of some attractor.  Update k: perturbation gaps j = 0, 1, ... from SETTLE_ENV call
+ * ((k-1) << 8 | j >> 2), word j & 3; unperturbed, the rule update with env e's SETTLE_SEL
+ * uniforms of update k.  Returns 1 if still outside every attractor after the last update;
+ * *nupd counts the updates applied. */
+static int settle(const pbn_net_desc* d, uint64_t seed, uint64_t e, uint64_t step, uint32_t* sp, int* perturbed,
+                  int* nupd) {
   const int N = d->n_nodes, W = words_of(N);
   for (int k = 1; k < d->settle_max; ++k) {
     if (attractor_of(d, sp, W) >= 0) return 0;
@@ -247,12 +258,9 @@ static int settle(const pbn_net_desc* d, uint64_t seed, uint64_t G, uint64_t e, 
       for (int w = 0; w < W; ++w) sp[w] ^= gam[w];
       *perturbed = 1;
     } else {
-      if (!have[k - 1]) {
-        group_digits(d, seed, G, step, k, Dk[k - 1]);
-        have[k - 1] = 1;
-      }
-      uint32_t x[4];
-      rule_update(d, sp, Dk[k - 1], b, x);
+      uint32_t U[PBN_MAX_NODES], x[4];
+      env_uniforms(d, seed, e, step, k, U);
+      rule_update(d, sp, U, x);
       for (int w = 0; w < W; ++w) sp[w] = x[w];
     }
     ++*nupd;
@@ -276,13 +284,11 @@ int oracle_step_ex(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t
 #endif
   for (int64_t g = 0; g < n_groups; ++g) {
     const uint64_t G = (env_offset >> 5) + (uint64_t)g;
-    /* selection digit words of this group: D[i][d], digit d = 0 is the MSB of u */
+    /* one-update law: the selection digit words of this group: D[i][d], digit d = 0 is the MSB
+     * of u; the settle law keys every update's selection per env (env_uniforms) */
+    const int settle_law = d->settle_max >= 2;
     uint32_t D[PBN_MAX_NODES][16];
-    group_digits(d, seed, G, step, 0, D);
-    /* settle law: the group's digit words of updates 1.., drawn when an env first needs them */
-    const int n_sub = d->settle_max > 1 ? d->settle_max - 1 : 0;
-    uint32_t (*Dk)[PBN_MAX_NODES][16] = n_sub ? malloc((size_t)n_sub * sizeof *Dk) : NULL;
-    int* have = n_sub ? calloc((size_t)n_sub, sizeof(int)) : NULL;
+    if (!settle_law) group_digits(d, seed, G, step, D);
     for (int b = 0; b < 32; ++b) {
       const int64_t li = g * 32 + b;
       const uint64_t e = env_offset + (uint64_t)li;
@@ -341,10 +347,13 @@ int oracle_step_ex(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t
       if (perturbed) {
         for (int w = 0; w < W; ++w) sp[w] = s1[w] ^ gam[w];
       } else {
-        rule_update(d, s1, D, b, sp);
+        uint32_t U[PBN_MAX_NODES];
+        if (settle_law) env_uniforms(d, seed, e, step, 0, U);
+        else group_uniforms(d, D, b, U);
+        rule_update(d, s1, U, sp);
       }
       int nupd = 1;
-      int unsettled = n_sub ? settle(d, seed, G, e, step, b, Dk, have, sp, &perturbed, &nupd) : 0;
+      int unsettled = settle_law ? settle(d, seed, e, step, sp, &perturbed, &nupd) : 0;
       if (updates) updates[li] = (uint16_t)nupd;
       /* 5. reward / termination */
       int a = attractor_of(d, sp, W);
@@ -378,8 +387,6 @@ int oracle_step_ex(const pbn_net_desc* d, uint64_t seed, uint64_t step, uint64_t
       }
       flags[li] = fl;
     }
-    free(Dk);
-    free(have);
   }
   return 0;
 }

@@ -102,18 +102,28 @@ class PyPBN:
         state, tgt = self.reset_from_words(seed, e, step, R[1], R[0])
         return state, tgt, 0
 
-    def rule_update(self, seed: int, G: int, b: int, step: int, s1: List[int], ctr) -> List[int]:
-        """Every node's rule update of env bit b of group G from s1; ctr(i, c) = (stream, idx) of
-        node i's selection call c."""
-        B = self.spec.prob_bits
+    def group_uniform(self, seed: int, G: int, b: int, step: int, i: int) -> int:
+        """One-update law: node i's B-bit uniform for env bit b of group G, from the group's
+        digit planes (SEL call 4i + c, word d & 3 = digit 4c + d, digit 0 the MSB)."""
+        B, u = self.spec.prob_bits, 0
+        for d in range(B):
+            word = draw(seed, G, step, SEL, 4 * i + (d >> 2))[d & 3]
+            u |= ((word >> b) & 1) << (B - 1 - d)
+        return u
+
+    def env_uniform(self, seed: int, e: int, step: int, k: int, i: int) -> int:
+        """Settle law: node i's B-bit uniform for update k of env e's step, keyed per env: the
+        top B bits of 16-bit field i & 1 of word (i >> 1) & 3 of SETTLE_SEL call (k << 8 | i >> 3)."""
+        word = draw(seed, e, step, SETTLE_SEL, (k << 8) | (i >> 3))[(i >> 1) & 3]
+        return ((word >> (16 * (i & 1))) & 0xFFFF) >> (16 - self.spec.prob_bits)
+
+    def rule_update(self, s1: List[int], uniform) -> List[int]:
+        """Every node's rule update from s1; uniform(i) = node i's B-bit selection uniform."""
         sp = []
         for i, fl in enumerate(self.net.nodes):
             j = 0
             if len(fl) > 1:
-                u = 0
-                for d in range(B):
-                    word = draw(seed, G, step, *ctr(i, d >> 2))[d & 3]
-                    u |= ((word >> b) & 1) << (B - 1 - d)
+                u = uniform(i)
                 while j < len(fl) - 1 and not (u < self.thr[i][j]):
                     j += 1
             sp.append(fl[j](s1))
@@ -156,12 +166,15 @@ class PyPBN:
                 break
             gamma[pos] = 1
         perturbed = any(gamma)
+        settle_law = self.spec.settle >= 2
         if perturbed:
             sp = [s1[i] ^ gamma[i] for i in range(n)]
+        elif settle_law:
+            sp = self.rule_update(s1, lambda i: self.env_uniform(seed, e, step, 0, i))
         else:
-            sp = self.rule_update(seed, G, b, step, s1, lambda i, c: (SEL, 4 * i + c))
-        # settle law (spec.settle >= 2): update k = 1.. from SETTLE_ENV gaps and SETTLE_SEL
-        # digits until sp is an attractor state, at most spec.settle updates in all
+            sp = self.rule_update(s1, lambda i: self.group_uniform(seed, G, b, step, i))
+        # settle law (spec.settle >= 2): update k = 1.. from SETTLE_ENV gaps and the env's
+        # SETTLE_SEL uniforms until sp is an attractor state, at most spec.settle updates in all
         unsettled = False
         for k in range(1, self.spec.settle):
             if tuple(sp) in self.att_of:
@@ -179,7 +192,7 @@ class PyPBN:
                 sp = [sp[i] ^ gk[i] for i in range(n)]
                 perturbed = True
             else:
-                sp = self.rule_update(seed, G, b, step, sp, lambda i, c, k=k: (SETTLE_SEL, ((k - 1) << 9) | (4 * i + c)))
+                sp = self.rule_update(sp, lambda i, k=k: self.env_uniform(seed, e, step, k, i))
         else:
             unsettled = self.spec.settle >= 2 and tuple(sp) not in self.att_of
         a = self.att_of.get(tuple(sp), -1)

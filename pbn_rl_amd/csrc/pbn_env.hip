@@ -137,6 +137,7 @@ struct pbn_net {
   float inv_log2q = 0.f;
   uint4* d_fcompact = nullptr;
   uint4* d_nrec = nullptr;
+  uint32_t* d_sthr = nullptr;   // settle law: thresholds scaled to 16 bits [lq][32W] (StepArgs::sthr)
   int n_funcs = 0;
   size_t lds_wave = 0;
   StepFn wave1 = nullptr;       // single step (pbn_step)
@@ -149,7 +150,7 @@ struct pbn_net {
   StepFn pipe = nullptr;        // rollout, three waves per group pair (every other network)
   size_t lds_pipe = 0;
   int n_gates = 0, n_glayers = 0, gate_off = 0, glayer_off = 0;   // lowered wide functions
-  int max_nf = 0, lq = 1, slot_words = 0;
+  int max_nf = 0, lq = 1, slot_words = 0, slot_words_settle = 0;
   uint32_t n1_magic = 0, am1_magic = 0;   // ceil(2^32 / (N + 1)), ceil(2^32 / (A - 1))
   uint64_t x_mult = 0;
   int att_single = 0;                     // every attractor is a single state
@@ -194,6 +195,7 @@ void free_net(pbn_net* net) {
   if (!net) return;
   (void)hipFree(net->d_fcompact);
   (void)hipFree(net->d_nrec);
+  (void)hipFree(net->d_sthr);
   (void)hipFree(net->d_tab);
   (void)hipFree(net->d_att_start);
   (void)hipFree(net->d_att_states);
@@ -604,7 +606,12 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   net->settle_max = d->settle_max;
   net->pipe_settle = net->max_nf <= kNodeRecs ? reinterpret_cast<StepFn>(pbn::settle_pipe_kernel(W, d->prob_bits))
                                               : nullptr;
-  net->lds_settle = net->lds_pipe + 8 * 4;   // + the per-half update plan [parity][half]{t, k}
+  // pbn_rollout_settle: S planes [64W] | 2 slots {flip, perturbation, reset-state planes [3W][64],
+  // selection planes [lq][64W], env masks [4]} | C [parity][t, k][64] | ended-step results
+  // [parity][2 + W][64]
+  net->slot_words_settle = 192 * W + net->lq * 64 * W + 4;
+  net->lds_settle = ((size_t)net->tab_words + 64 * (size_t)W + 2 * (size_t)net->slot_words_settle + 256 +
+                     2 * (size_t)(2 + W) * 64) * 4;
   net->pipe = pick_pipe(W, d->prob_bits, net->max_nf > kNodeRecs);
   net->reset = pick_reset(W);
   // multiply-high divisors (exact for the operand ranges used: see actions_from_draw, autoreset)
@@ -615,6 +622,14 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   if (const char* env = getenv("PBN_ROLL")) {
     if (!strcmp(env, "lean")) net->force_roll = 2;
     if (!strcmp(env, "pipe")) net->force_roll = 3;
+  }
+  // the settle law's per-env selection thresholds (settle_lt_word): node i, threshold q <
+  // nf_i - 1 as c << (16 - B), 65536 (always) past a node's last function and past the network
+  std::vector<uint32_t> sthr((size_t)net->lq * 32 * W, 65536u);
+  for (int i = 0; i < N; ++i) {
+    const int f0 = d->node_func_start[i], nf = d->node_func_start[i + 1] - f0;
+    for (int q = 0; q < nf - 1 && q < net->lq; ++q)
+      sthr[(size_t)q * 32 * W + i] = d->func_threshold[f0 + q] << (16 - d->prob_bits);
   }
   std::vector<uint32_t> att_first((size_t)A * W);
   for (int t = 0; t < A; ++t)
@@ -629,6 +644,7 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     net->n_cus = 256;
   if ((rc = upload(&net->d_fcompact, fcomp.data(), fcomp.size())) ||
       (rc = upload(&net->d_nrec, nrec.data(), nrec.size())) ||
+      (rc = upload(&net->d_sthr, sthr.data(), sthr.size())) ||
       (rc = upload(&net->d_tab, tab.data(), tab.size())) ||
       (rc = upload(&net->d_att_start, A ? d->attractor_start : nullptr, (size_t)A + 1)) ||
       (rc = upload(&net->d_att_states, S ? d->attractor_states : nullptr, (size_t)S * W)) ||
@@ -728,6 +744,7 @@ static void fill_args(const pbn_net* net, StepArgs* p, uint64_t seed, uint64_t s
   a.inv_log2q = net->inv_log2q;
   a.fcompact = net->d_fcompact;
   a.nrec = net->d_nrec;
+  a.sthr = net->d_sthr;
   a.n1_magic = net->n1_magic;
   a.att_single = net->att_single;
   a.am1_magic = net->am1_magic;
@@ -852,6 +869,7 @@ int pbn_rollout_ex(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offs
     const int64_t pblocks = (a.n_groups + 1) / 2;
 #endif
     if (settle) {
+      a.slot_words = net->slot_words_settle;
       hipLaunchKernelGGL(net->pipe_settle, dim3((unsigned)pblocks), dim3(192), net->lds_settle,
                          (hipStream_t)stream, a);
       HIP_OK(hipGetLastError());

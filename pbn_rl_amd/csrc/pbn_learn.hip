@@ -1107,6 +1107,9 @@ int pbn_bdq_learn(const pbn_net* net, int64_t batch, const int64_t* d_idx, int64
   const int tiles = (int)(batch / kRows);
   const size_t lds_f = ((size_t)(kD0 + kD1 + kD2 + kD3 + kDH * H) * kRows + 4 * kRows + 2 * kRows) * sizeof(float) +
                        kRows * 128;
+  if (lds_f > 64 * 1024 && hipFuncSetAttribute((const void*)learn_fwd_kernel,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_f) != hipSuccess)
+    return pbn::set_error(PBN_EDEVICE, "hipFuncSetAttribute failed");
   hipLaunchKernelGGL(learn_fwd_kernel, dim3(3 * tiles), dim3(kThreads), lds_f, s, a);
   if (hipGetLastError() != hipSuccess) return pbn::set_error(PBN_EDEVICE, "learn_fwd_kernel launch failed");
   const size_t lds_b = learn_bwd_lds(H, a.Apad, n_branches);

@@ -95,6 +95,8 @@ struct StepArgs {
   int settle_max;      // step law: >= 2 = the settle law (wave kernel variants 3, 4,
                        // pbn_rollout_settle)
   uint16_t* updates;   // rollouts: [n_steps][n] synchronous updates applied per env-step (nullable)
+  const uint32_t* sthr;  // settle law: thresholds scaled to 16 bits, [lq][32W] (65536 past a node's
+                         // last function): the per-env selection compares (settle_lt_word)
 };
 
 // In-kernel phase clocks (cdna_hip_programming.md section 7, "In-kernel stamps"):
@@ -569,6 +571,45 @@ __device__ __forceinline__ void eval_gate_levels(const StepArgs& a, const uint32
   }
 }
 
+// The settle law's per-env selection (oracle/pbn_oracle.c env_uniforms): the 16 words of env
+// ge's SETTLE_SEL calls 4r .. 4r+3 for update k; node 32r + b's 16-bit field is b & 1 of
+// U[b >> 1].  Calls past the network's last node are not made (U = 0).
+__device__ __forceinline__ void settle_sel_words(uint32_t ge_lo, uint32_t ge_hi, uint32_t st_lo, uint32_t k, int r,
+                                                 int N, uint32_t k0, uint32_t k1, uint32_t (&U)[16]) {
+  const uint32_t c2 = (pbn::kStreamSettleSel << 28) | (k << 8) | (uint32_t)(4 * r);
+  if (32 * r + 24 < N) {   // every call (a word of more than 24 nodes): in one block, interleaved
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const Word4 P = pbn::philox(ge_lo, st_lo, c2 | (uint32_t)c, ge_hi, k0, k1);
+      U[4 * c + 0] = P.x; U[4 * c + 1] = P.y; U[4 * c + 2] = P.z; U[4 * c + 3] = P.w;
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      Word4 P = {0u, 0u, 0u, 0u};
+      if (32 * r + 8 * c < N) P = pbn::philox(ge_lo, st_lo, c2 | (uint32_t)c, ge_hi, k0, k1);
+      U[4 * c + 0] = P.x; U[4 * c + 1] = P.y; U[4 * c + 2] = P.z; U[4 * c + 3] = P.w;
+    }
+  }
+}
+
+// env-major selection word of one threshold: bit b = (field of node 32r + b < C[b]), C = the
+// thresholds scaled to 16 bits (c << (16 - B); 65536 past a node's last function: sthr), most
+// significant node first.  Per node one subtract (the field selected by SDWA) whose sign is the
+// compare (both operands <= 2^16) and one v_alignbit_b32 that shifts it in: (lt:d) >> 31.  C is
+// read through the constant address space, so the 32 thresholds of a row are scalar loads.
+using ConstU32 = const __attribute__((address_space(4))) uint32_t;
+__device__ __forceinline__ uint32_t settle_lt_word(const uint32_t (&U)[16], const uint32_t* C_) {
+  ConstU32* C = (ConstU32*)C_;
+  uint32_t lt = 0;
+#pragma unroll
+  for (int b = 31; b >= 0; --b) {
+    const uint32_t u = (b & 1) ? (U[b >> 1] >> 16) : (U[b >> 1] & 0xFFFFu);
+    lt = __builtin_amdgcn_alignbit(lt, u - C[b], 31);
+  }
+  return lt;
+}
+
 // node l32 + 32r on lane l32: the rule update of every env of the group from the bit-sliced
 // planes S, the selection digit planes dig (perturbed envs are replaced by the caller)
 template <int W, int B>
@@ -618,20 +659,61 @@ __device__ __forceinline__ void node_update(const StepArgs& a, const uint4 (&rec
   }
 }
 
+// settle law: node l32 + 32r's rule update on lane l32 (lower lanes) from the planes S, with env
+// l32's per-env selection uniforms of update k (settle_sel_words; every lane computes its env's
+// words, the upper half repeating the lower's: the settle variants are off the hot path).  The
+// chain runs from the widest node's last function down (uniform q); threshold q's plane of every
+// node is compared env-major and transposed once per q, so that only one word's uniforms are live.
+template <int W, int B>
+__device__ __forceinline__ void node_update_settle(const StepArgs& a, const uint4 (&rec_)[W][kNodeRecs],
+                                                   const uint4* __restrict__ selq, const uint32_t* __restrict__ S,
+                                                   uint32_t ge_lo, uint32_t ge_hi, uint32_t st_lo, uint32_t k,
+                                                   int lane, uint32_t (&X)[W]) {
+  const int N = a.n_nodes;
+  const bool lo = lane < 32;
+  const int l32 = lane & 31;
+  const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+  const int mnf = a.max_nf;
+#pragma unroll
+  for (int r = 0; r < W; ++r) {
+    X[r] = 0;
+    const int i = l32 + 32 * r;
+    const int ii = lo && i < N ? i : 0;   // other lanes evaluate node 0 and discard it
+    uint32_t U[16];
+    settle_sel_words(ge_lo, ge_hi, st_lo, k, r, N, k0, k1, U);
+    const int nf = (int)rec_[r][0].w;
+    const int f0 = (int)rec_[r][1].w;
+    uint32_t x = 0;
+    for (int q = mnf - 1; q >= 0; --q) {
+      uint32_t pl = 0;
+      if (q < mnf - 1) pl = lane_transpose32(settle_lt_word(U, a.sthr + (size_t)(q * W + r) * 32), lane);
+      if (q < nf) {
+        uint32_t fq;
+        if (q < kNodeRecs) {
+          const uint4 rc = q == 0 ? rec_[r][0] : (q == 1 ? rec_[r][1] : (q == 2 ? rec_[r][2] : rec_[r][3]));
+          fq = eval_sel(rc.x, selq[(2 * q) * 32 * W + ii], selq[(2 * q + 1) * 32 * W + ii], S);
+        } else {
+          const uint4 rc = a.fcompact[CK(f0 + q, a.n_funcs, 9)];
+          fq = eval_compact(rc.x, rc.y, S);
+        }
+        x = (q == nf - 1) ? fq : bfi(pl, fq, x);
+      }
+    }
+    if (lo && i < N) X[r] = x;
+  }
+}
+
 // The settle law (settle_max >= 2, include/pbn_env.h "Step law"): updates k = 1 ..
 // settle_max - 1 of the envs (lower lanes) whose state sp is outside every attractor, until all
 // of the wave's envs are in one.  Update k: perturbation gaps j = 0, 1, ... from SETTLE_ENV call
-// ((k-1) << 8 | j >> 2), word j & 3 (per env); unperturbed envs take the rule update with the
-// group's SETTLE_SEL digit planes of update k (call idx (k-1) << 9 | 4i + c).  Every lane
-// computes the digit calls of its node (the upper half repeats the lower's: settle updates are
-// off the one-update hot path).  Returns true on lanes whose env is still outside after the
-// last update (PBN_FLAG_UNSETTLED).
+// ((k-1) << 8 | j >> 2), word j & 3 (per env); unperturbed envs take the rule update with their
+// own SETTLE_SEL uniforms of update k (node_update_settle).  Returns true on lanes whose env is
+// still outside after the last update (PBN_FLAG_UNSETTLED).
 template <int W, int B>
 __device__ __forceinline__ bool settle_updates(const StepArgs& a, const uint32_t* __restrict__ L, uint32_t* S,
                                             const uint4 (&rec_)[W][kNodeRecs], int lane, uint32_t ge_lo,
-                                            uint32_t ge_hi, uint32_t G_lo, uint32_t G_hi, uint32_t st_lo,
-                                            uint32_t (&sp)[W], int& att, bool& pert, uint32_t& nupd) {
-  constexpr int CPN = B / 4;
+                                            uint32_t ge_hi, uint32_t st_lo, uint32_t (&sp)[W], int& att, bool& pert,
+                                            uint32_t& nupd) {
   const bool lo = lane < 32;
   const int l32 = lane & 31;
   const int N = a.n_nodes;
@@ -642,16 +724,6 @@ __device__ __forceinline__ bool settle_updates(const StepArgs& a, const uint32_t
   for (int k = 1; k < a.settle_max; ++k) {
     if (__ballot(open) == 0) return false;
     const uint32_t sub = (uint32_t)(k - 1);
-    uint32_t dig[W][16];
-#pragma unroll
-    for (int r = 0; r < W; ++r) {
-#pragma unroll
-      for (int c = 0; c < CPN; ++c) {
-        const Word4 d = pbn::philox(G_lo, st_lo, (pbn::kStreamSettleSel << 28) | (sub << 9) |
-                                                     (uint32_t)(4 * (l32 + 32 * r) + c), G_hi, k0, k1);
-        dig[r][4 * c + 0] = d.x; dig[r][4 * c + 1] = d.y; dig[r][4 * c + 2] = d.z; dig[r][4 * c + 3] = d.w;
-      }
-    }
     uint32_t gam[W];
     bool pk = false;
 #pragma unroll
@@ -680,7 +752,7 @@ __device__ __forceinline__ bool settle_updates(const StepArgs& a, const uint32_t
     __builtin_amdgcn_wave_barrier();
     if (a.n_glayers > 0) eval_gate_levels(a, L, S, lane);
     uint32_t X[W], x[W];
-    node_update<W, B>(a, rec_, selq, S, dig, lo, l32, X);
+    node_update_settle<W, B>(a, rec_, selq, S, ge_lo, ge_hi, st_lo, (uint32_t)k, lane, X);
 #pragma unroll
     for (int w = 0; w < W; ++w) x[w] = lane_transpose32(X[w], lane);
     if (open) {
@@ -704,7 +776,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   constexpr bool LEAN = VARIANT == 2 || VARIANT == 4;
   constexpr bool SINGLE = VARIANT == 1 || VARIANT == 3;
   constexpr bool SETTLE = VARIANT >= 3;
-  constexpr int CPN = B / 4;               // selection calls per node
+  constexpr int CPN = SETTLE ? 0 : B / 4;  // group selection calls per node (the settle law's are per env)
   constexpr int H = (CPN + 1) / 2;         // of which the lower half computes H
   constexpr int NLO = 1 + W * H;           // lower list: ENV, SEL(c < H)
   constexpr int NUP = W * (CPN - H);       // upper list: SEL(c >= H)
@@ -801,9 +873,10 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
     if (it == 0) {
       lc0 = ge_lo; lc2 = pbn::kStreamEnv << 28; lc3 = ge_hi;
     } else {
+      constexpr int HD = H > 0 ? H : 1;   // (the settle variants have no group selection calls)
       const int idx = it - 1;
-      const int r = (idx / H) < W ? idx / H : W - 1;
-      const int c = idx % H;
+      const int r = (idx / HD) < W ? idx / HD : W - 1;
+      const int c = idx % HD;
       lc0 = G_lo; lc2 = (pbn::kStreamSel << 28) | (uint32_t)(4 * (l32 + 32 * r) + c); lc3 = G_hi;
     }
     if (it < W * (CPN - H)) {
@@ -917,7 +990,8 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   // replaced after the back-transpose)
   PBN_STAMP(4);
   uint32_t X[W];
-  node_update<W, B>(a, rec_, selq, S, dig, lo, l32, X);
+  if constexpr (SETTLE) node_update_settle<W, B>(a, rec_, selq, S, ge_lo, ge_hi, st_lo, 0u, lane, X);
+  else node_update<W, B>(a, rec_, selq, S, dig, lo, l32, X);
 
   // ---- 5. back to per-env words, reward, termination, autoreset, stores
   PBN_STAMP(5);
@@ -933,7 +1007,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   bool unsettled = false;
   uint32_t nupd = 1;   // synchronous updates applied this step
   if constexpr (SETTLE) {   // the whole wave (cross-lane transposes)
-    unsettled = settle_updates<W, B>(a, L, S, rec_, lane, ge_lo, ge_hi, G_lo, G_hi, st_lo, sp, att, pert, nupd);
+    unsettled = settle_updates<W, B>(a, L, S, rec_, lane, ge_lo, ge_hi, st_lo, sp, att, pert, nupd);
   }
   if (lo) {
   if constexpr (!SINGLE) {
@@ -1747,61 +1821,50 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
 
 // ------------------------------- settle-law rollout, three waves per pair of 32-env groups
 // pbn_rollout under the settle law (settle_max = K >= 2, include/pbn_env.h "Step law"): the
-// intervention, then synchronous updates until every env of the group is in an attractor or K
-// updates have run.  Same roles as pbn_rollout_pipe, but one iteration is one UPDATE (t, k) of a
-// step t (k = 0 the one-update law's draws; k >= 1 the SETTLE_ENV / SETTLE_SEL draws), and each
-// of the block's two groups (halves) runs its own sequence of updates:
-//   wave 1 (env draws): k = 0: ENV (+ PERT) call -> flip mask, autoreset draw, gaps;
-//                       k >= 1: the SETTLE_ENV gaps of update k (per env);
-//   wave 2 (selection): SEL (k = 0) or SETTLE_SEL (k >= 1) digit planes -> (u < c_j) masks;
-//   wave 0 (state):     the update of the envs still outside every attractor (all at k = 0),
-//                       the group's decision (continue or end the step), the step's epilogue.
-// Iteration i: the RNG waves produce update R(i) into slot i & 1 while the state wave applies
-// R(i-1).  Whether a group needs (t, k+1) or (t+1, 0) after R(i-1) is only known at the end of
-// iteration i, so R(i) is speculated as (t, k+1) (k + 1 < K) and re-issued as the state wave's
-// decision C when the speculation was wrong: one idle iteration of that group per step that ends
-// before the cap.  C is published in LDS per half and iteration parity; every wave derives the
-// same R, validity and loop exit from it, so all waves pass the same number of block barriers.
+// intervention, then synchronous updates until the env's state is in an attractor or K updates
+// have run.  The roles of pbn_rollout_pipe, but one iteration is one UPDATE (t, k) of a step t,
+// and every env runs its own sequence of updates: the settle law keys each update's selection per
+// env (SETTLE_SEL call (k << 8 | i >> 3) of env e; DESIGN.md "Step law"), so an env that settles
+// starts its next step while the other envs of its 32-env word are still updating.
+//   wave 1 (env draws, lane = env): the epilogue of the step that ended in the previous iteration
+//     (reward, flags, final state, update count, the autoreset decision, next obs), then the
+//     update's draws: k = 0 the ENV call (actions, the step's autoreset draws, gaps 0-2), k >= 1
+//     the SETTLE_ENV call (gaps); flip, perturbation and reset masks transposed to bit planes;
+//   wave 2 (selection, lane = env): the env's SETTLE_SEL words of its update, compared with the
+//     thresholds env-major (one compare and one add-with-carry per node and threshold), then
+//     transposed to the (u < c_j) bit planes of every node;
+//   wave 0 (state): keeps the 32 envs of a word bit-sliced across updates (lane = node): applies
+//     the update to the envs whose update is valid (a proc mask), back-transposes once per update
+//     for the attractor lookup and decides, per env, to continue or to end the step.
+// Iteration i: the RNG waves produce each env's update R(i) into slot i & 1 while the state wave
+// applies R(i-1) (EnvPlan).  The state wave publishes each env's decision C (next update) in LDS,
+// plus the ended step's attractor id, flags, length and final state for the env wave's epilogue.
 // Results are bit-identical to pbn_step_wave's settle variants and to oracle/pbn_oracle.c.
-// The per-half update plan of pbn_rollout_settle, wave-uniform (SGPRs), identical in every wave.
-// P = R(i-1), the update produced in the previous iteration (t = ~0: none); C = C(i-2), the
-// state wave's decision after the update it applied in iteration i-1 (the next update each group
-// needs); R = R(i), the update the RNG waves produce in iteration i.  R(i-1) is valid (the state
-// wave applies it in iteration i) iff it equals C; R(i) continues a valid R(i-1) speculatively
-// ((t, k+1), or (t+1, 0) at the cap), else re-issues C.
-struct SettlePlan {
-  uint32_t Pt0 = ~0u, Pk0 = 0, Pt1 = ~0u, Pk1 = 0;
-  uint32_t Ct0 = 0, Ck0 = 0, Ct1 = 0, Ck1 = 0;
-  uint32_t Rt0 = 0, Rk0 = 0, Rt1 = 0, Rk1 = 0;
-  bool v0 = false, v1 = false;
-  // false once both groups have finished all steps (the loop's exit, the same in every wave).
-  // A step takes at most K updates and one dropped speculation, so n_steps (K + 1) + 1
-  // iterations always suffice: the bound is a guard that every wave reaches, never the exit.
-  __device__ __forceinline__ bool next(const uint32_t* ctl, uint32_t it, uint32_t K, uint32_t n_steps) {
-    const uint32_t* cin = ctl + ((it + 1) & 1) * 4;   // written in iteration i-1
-    Ct0 = __builtin_amdgcn_readfirstlane(cin[0]);
-    Ck0 = __builtin_amdgcn_readfirstlane(cin[1]);
-    Ct1 = __builtin_amdgcn_readfirstlane(cin[2]);
-    Ck1 = __builtin_amdgcn_readfirstlane(cin[3]);
-    if (Ct0 >= n_steps && Ct1 >= n_steps) return false;
-    if ((uint64_t)it > (uint64_t)n_steps * (K + 1) + 1) return false;
-    v0 = Pt0 == Ct0 && Pk0 == Ck0;
-    v1 = Pt1 == Ct1 && Pk1 == Ck1;
-    Rt0 = v0 ? (Pk0 + 1 < K ? Pt0 : Pt0 + 1) : Ct0;
-    Rk0 = v0 ? (Pk0 + 1 < K ? Pk0 + 1 : 0u) : Ck0;
-    Rt1 = v1 ? (Pk1 + 1 < K ? Pt1 : Pt1 + 1) : Ct1;
-    Rk1 = v1 ? (Pk1 + 1 < K ? Pk1 + 1 : 0u) : Ck1;
-    return true;
+constexpr uint32_t kNoUpd = 0xFFFFFFFFu;
+
+// The per-env update plan of pbn_rollout_settle, in that env's lane of every wave (VGPRs; the
+// same values in all three waves).  P = R(i-1), the update the RNG waves produced in the previous
+// iteration (kNoUpd: none); C = the next update the env needs, the state wave's decision in
+// iteration i-1; R = R(i), the update produced in iteration i.  R(i-1) is applied in iteration i
+// iff it equals C.  A valid R(i-1) continues speculatively as (t, k+1) while k+1 < K (dropped if
+// the state wave finds the env settled: one idle iteration per step that ends before the cap);
+// otherwise C is re-issued.  A step's first update is therefore always produced once its previous
+// step's end is known, i.e. with that end's autoreset decision.
+struct EnvPlan {
+  uint32_t Pt = kNoUpd, Pk = 0, Rt = 0, Rk = 0;
+  bool v = false;
+  __device__ __forceinline__ void next(uint32_t Ct, uint32_t Ck, uint32_t K) {
+    v = Pt == Ct && Pk == Ck;
+    const bool cont = v && Pk + 1 < K;
+    Rt = cont ? Pt : (v ? kNoUpd : Ct);
+    Rk = cont ? Pk + 1 : Ck;
   }
-  __device__ __forceinline__ void done() {
-    Pt0 = Rt0; Pk0 = Rk0; Pt1 = Rt1; Pk1 = Rk1;
-  }
+  __device__ __forceinline__ void done() { Pt = Rt; Pk = Rk; }
 };
 
 template <int W, int B>
 __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(4, 8)))
 pbn_rollout_settle(StepArgs a) {
-  constexpr int CPN = B / 4;              // selection calls per node
   extern __shared__ uint32_t smem[];
   const int lane = threadIdx.x & 63;
   const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1814,31 +1877,43 @@ pbn_rollout_settle(StepArgs a) {
   const int64_t n = a.n_envs;
   const int64_t le = g * 32 + l32;
   const uint64_t ge = a.env_offset + (uint64_t)le;
-  const uint64_t G = ge >> 5;
   const size_t plane = (size_t)W * n;
   const uint32_t n_steps = (uint32_t)a.n_steps;
   const uint32_t K = (uint32_t)a.settle_max;
+  const int lq = a.lq;
+  // iterations that always suffice (a step takes at most K updates and one dropped speculation):
+  // a guard every wave reaches, never the exit
+  const uint64_t max_it = (uint64_t)n_steps * (K + 1) + 1;
   uint32_t* L = smem;
   const float* rtab = reinterpret_cast<const float*>(L + a.cdf_len);
   const uint32_t* htab = L + a.cdf_len + 4 * (N + 1);
   const uint4* selq = reinterpret_cast<const uint4*>(L + a.sel_off);
   const uint4* recL = reinterpret_cast<const uint4*>(L + a.nrec_off);
   uint32_t* Sg = smem + a.tab_words + half * 32 * W;
+  // slot (per iteration parity): flip planes [W][64] | perturbation planes [W][64] | reset-state
+  // planes [W][64] | selection planes [lq][2][32W] | {perturbed, reset} env masks per half [4]
   uint32_t* slots = smem + a.tab_words + 2 * 32 * W;
-  uint32_t* cm = slots + 2 * (size_t)a.slot_words;                      // W == 1: threshold digit masks
-  uint32_t* ctl = cm + (W == 1 ? (kNodeRecs - 1) * B * 32 : 0);         // [parity][half]{t, k}
+  constexpr int kGP = 64 * W, kRP = 128 * W, kLT = 192 * W;
+  const int kMK = kLT + lq * 64 * W;
+  uint32_t* ctl = slots + 2 * (size_t)a.slot_words;   // [parity][t, k][64]: C per env
+  uint32_t* einfo = ctl + 256;                        // [parity][2 + W][64]: the ended step's results
+  if (threadIdx.x < 64) {   // C before iteration 0: (0, 0); envs of groups past the end: finished
+    ctl[128 + threadIdx.x] = valid ? 0u : n_steps;
+    ctl[192 + threadIdx.x] = 0u;
+  }
   uint32_t st[W];
   uint32_t tt0 = 0, tg0 = 0;
 #pragma unroll
   for (int w = 0; w < W; ++w) st[w] = 0;
-  if (role == 0 && valid) {
+  if (role != 2 && valid) {
 #pragma unroll
     for (int w = 0; w < W; ++w) st[w] = a.state[CK((size_t)w * n + le, plane, 1)];
-    tt0 = a.t[CK(le, n, 2)];
-    tg0 = a.target[CK(le, n, 3)];
+    if (role == 1) {
+      tt0 = a.t[CK(le, n, 2)];
+      tg0 = a.target[CK(le, n, 3)];
+    }
   }
   copy_image(L, a);
-  if (threadIdx.x < 4) ctl[4 + threadIdx.x] = 0u;   // C before iteration 0: (t, k) = (0, 0) for both halves
 #pragma unroll
   for (int w = 0; w < W; ++w) st[w] &= valid_word_mask(N, w);
   uint32_t u_k0 = (uint32_t)a.seed, u_k1 = (uint32_t)(a.seed >> 32);
@@ -1847,50 +1922,86 @@ pbn_rollout_settle(StepArgs a) {
                                                        ((a.mode & PBN_MODE_AUTORESET) ? 8u : 0u) |
                                                        (a.updates ? 32u : 0u));
   __syncthreads();
-  if constexpr (W == 1) {   // threshold digit masks [q][d][32], as pbn_rollout_pipe
-    const int p = (int)threadIdx.x % ((kNodeRecs - 1) * 32), h = (int)threadIdx.x / ((kNodeRecs - 1) * 32);
-    const int i = p & 31, q = p >> 5;
-    uint32_t c = 0;
-    if (i < N && q < (int)recL[i].w - 1) c = recL[q * 32 + i].z;
-#pragma unroll
-    for (int dd = 0; dd < B / 2; ++dd) {
-      const int d = h * (B / 2) + dd;
-      cm[(q * B + d) * 32 + i] = ((c >> (B - 1 - d)) & 1u) ? ~0u : 0u;
-    }
-    __syncthreads();
-  }
   __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the initial state loads (see pbn_rollout_pipe)
-
   const int mnf = __builtin_amdgcn_readfirstlane(a.max_nf);
-  // one loop per role (each role's loop-carried values occupy registers in that loop only);
-  // every role derives the same update plan from the LDS words, so all leave at the same iteration
+  const uint32_t ge_lo = (uint32_t)ge;
+
+  // one loop per role; every role derives the same plans and loop exit from the same C values
   if (role == 1) {
-    SettlePlan p;
-    for (uint32_t it = 0; p.next(ctl, it, K, n_steps); ++it) {
+    // ---- env draws and step epilogues, env `lane`
+    uint32_t rs[W];        // the autoreset state drawn at the current step's first update
+    uint32_t rtv = 0, pcv = 0, t_prev = 0;
+    bool proc_prev = false;
+#pragma unroll
+    for (int w = 0; w < W; ++w) rs[w] = 0;
+    if (valid && (u_fl & 1u)) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) LANE_STV(a.obs, (size_t)w * n + (size_t)le, (size_t)n_steps * plane, 7, st[w]);
+    }
+    EnvPlan p;
+    for (uint32_t it = 0;; ++it) {
       asm volatile("" : "+s"(u_k0), "+s"(u_k1));
-      const uint32_t Rt0 = p.Rt0, Rk0 = p.Rk0, Rt1 = p.Rt1, Rk1 = p.Rk1;
-      // ---- env draws of update R(i), env `lane`
-      const uint32_t t = half ? Rt1 : Rt0, k = half ? Rk1 : Rk0;
+      const uint32_t* cin = ctl + ((it + 1) & 1) * 128;
+      const uint32_t Ct = cin[lane], Ck = cin[64 + lane];
+      // -- the epilogue of the step the state wave ended in iteration i-1 (step t_prev)
+      bool rst = false;
+      if (proc_prev && Ck == 0) {
+        const uint32_t* ei = einfo + ((it + 1) & 1) * (2 + W) * 64;
+        const uint32_t e0 = ei[lane], nupd = ei[64 + lane];
+        uint32_t cur[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) cur[w] = ei[(2 + w) * 64 + lane];
+        const size_t t = t_prev;
+        if (u_fl & 2u) {
+#pragma unroll
+          for (int w = 0; w < W; ++w) LANE_STV(a.final_state, (t * plane + (size_t)w * n) + (size_t)le, (size_t)n_steps * plane, 10, cur[w]);
+        }
+        if (u_fl & 32u) LANE_STV(a.updates, (t * n) + (size_t)le, (size_t)n_steps * n, 23, (uint16_t)min(nupd, 0xFFFFu));
+        const int att = (int)(e0 & 0xFFFFu) - 1;
+        const bool in_attr = att >= 0;
+        const bool term = in_attr && (uint32_t)att == tg0;
+        const bool wrong = in_attr && !term;
+        int tt = (int)tt0 + 1;
+        tt = tt > 255 ? 255 : tt;
+        const bool trunc = a.horizon > 0 && tt >= a.horizon;
+        rst = (u_fl & 8u) && (term || trunc);
+        const uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) |
+                            (((e0 >> 16) & 1u) << 3) | ((uint32_t)rst << 4) | (((e0 >> 17) & 1u) << 5);
+        const float4 r4 = reinterpret_cast<const float4*>(rtab)[pcv];
+        LANE_STV(a.reward, (t * n) + (size_t)le, (size_t)n_steps * n, 11, term ? r4.z : (wrong ? r4.y : r4.x));
+        LANE_STV(a.flags, (t * n) + (size_t)le, (size_t)n_steps * n, 15, (uint8_t)fl);
+        tg0 = rst ? rtv : tg0;
+        tt0 = rst ? 0u : (uint32_t)tt;
+#pragma unroll
+        for (int w = 0; w < W; ++w) st[w] = rst ? rs[w] : cur[w];
+        if ((u_fl & 1u) && t + 1 < n_steps) {
+#pragma unroll
+          for (int w = 0; w < W; ++w) LANE_STV(a.obs, ((t + 1) * plane + (size_t)w * n) + (size_t)le, (size_t)n_steps * plane, 7, st[w]);
+        }
+      }
+      if (__ballot(Ct < n_steps) == 0 || (uint64_t)it > max_it) break;
+      p.next(Ct, Ck, K);
+      const uint32_t t = p.Rt, k = p.Rk;
       uint32_t* slot = slots + (size_t)(it & 1) * a.slot_words;
-      const uint64_t step = a.step + (uint64_t)t;
-      const uint32_t st_lo = (uint32_t)step;
-      const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
-      const uint32_t ge_lo = (uint32_t)ge;
+      uint32_t m[W], gam[W];
+#pragma unroll
+      for (int w = 0; w < W; ++w) { m[w] = 0; gam[w] = 0; }
+      bool pk = false;
       if (valid && t < n_steps) {
-        uint32_t gam[W];
-#pragma unroll
-        for (int w = 0; w < W; ++w) gam[w] = 0;
-        if (k == 0) {
-          // the one-update law's draws of step t (pbn_rollout_pipe's general env loop)
-          const Word4 E = pbn::philox(ge_lo, st_lo, pbn::kStreamEnv << 28, ge_hi, u_k0, u_k1);
-          uint32_t m[W], rsv[W];
-#pragma unroll
-          for (int w = 0; w < W; ++w) { m[w] = 0; rsv[w] = 0; }
+        const uint64_t step = a.step + (uint64_t)t;
+        const uint32_t st_lo = (uint32_t)step;
+        const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
+        const bool first = k == 0;
+        // one call per update: ENV at k = 0, SETTLE_ENV call (k-1) << 8 at k >= 1
+        const uint32_t c2 = first ? (pbn::kStreamEnv << 28) : ((pbn::kStreamSettleEnv << 28) | ((k - 1) << 8));
+        const Word4 E = pbn::philox(ge_lo, st_lo, c2, ge_hi, u_k0, u_k1);
+        uint32_t u2 = E.z;
+        if (first) {
+          // the step's draws from X = ENV words 3:2: actions, the autoreset draws, gap 2's uniform
           uint32_t xhi = E.w, xlo = E.z;
           const uint32_t n1 = (uint32_t)(N + 1);
           const uint32_t c_act = ext64(xhi, xlo, n1 * n1 * n1);
           uint64_t xr = ((((uint64_t)E.w) << 32) | E.z) * a.x_mult;
-          uint32_t rtv;
           if (a.n_attr >= 1) {
             const int32_t* att_first = reinterpret_cast<const int32_t*>(L + a.att_off);
             const uint32_t* att_words = L + a.att_off + a.n_attr + 1;
@@ -1911,114 +2022,107 @@ pbn_rollout_settle(StepArgs a) {
               xr *= size;
             }
 #pragma unroll
-            for (int w = 0; w < W; ++w) rsv[w] = att_words[(size_t)(st0 + idx) * W + w];
+            for (int w = 0; w < W; ++w) rs[w] = att_words[(size_t)(st0 + idx) * W + w];
           } else {
             const Word4 rr = pbn::philox(ge_lo, st_lo, (pbn::kStreamReset << 28) | 1u, ge_hi, u_k0, u_k1);
             const uint32_t rw4[4] = {rr.x, rr.y, rr.z, rr.w};
 #pragma unroll
-            for (int w = 0; w < W; ++w) rsv[w] = rw4[w] & valid_word_mask(N, w);
+            for (int w = 0; w < W; ++w) rs[w] = rw4[w] & valid_word_mask(N, w);
             rtv = PBN_NO_TARGET;
           }
-          const uint32_t u2 = (uint32_t)(xr >> 32);
+          u2 = (uint32_t)(xr >> 32);
           if (u_fl & 4u) {
             actions_from_draw<W>(c_act, N, a.n1_magic, m);
 #pragma unroll
-            for (int w = 0; w < W; ++w) LANE_STV(a.flipmask, (t * plane + (size_t)w * n) + (size_t)le, (size_t)n_steps * plane, 8, m[w]);
+            for (int w = 0; w < W; ++w) LANE_STV(a.flipmask, ((size_t)t * plane + (size_t)w * n) + (size_t)le, (size_t)n_steps * plane, 8, m[w]);
           } else {
 #pragma unroll
             for (int w = 0; w < W; ++w)
-              m[w] = a.flipmask[CK((t * plane + (size_t)w * n) + (size_t)le, (size_t)n_steps * plane, 6)] & valid_word_mask(N, w);
+              m[w] = a.flipmask[CK(((size_t)t * plane + (size_t)w * n) + (size_t)le, (size_t)n_steps * plane, 6)] & valid_word_mask(N, w);
           }
-          uint32_t pcv = 0;
+          pcv = 0;
 #pragma unroll
           for (int w = 0; w < W; ++w) pcv += __builtin_popcount(m[w]);
-          const int g0 = gap_any(a.gap_exact, L, a, E.x), g1 = gap_any(a.gap_exact, L, a, E.y),
-                    g2 = gap_any(a.gap_exact, L, a, u2);
-          const int p0 = g0 - 1, p1 = p0 + g1, p2 = p1 + g2;
-          set_bit<W>(gam, p0, N);
-          set_bit<W>(gam, p1, N);
-          set_bit<W>(gam, p2, N);
-          if (p2 < N - 1) {   // rare: a fourth flip (gap k >= 3: PERT call (k-3)>>2, word (k-3)&3)
-            Word4 P = E;
-            int pos = p2;
-            for (int kk = 3; pos < N - 1; ++kk) {
-              if (((kk - 3) & 3) == 0)
-                P = pbn::philox(ge_lo, st_lo, (pbn::kStreamPert << 28) | (uint32_t)((kk - 3) >> 2), ge_hi, u_k0, u_k1);
-              const int j4 = (kk - 3) & 3;
-              const uint32_t u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
-              pos += gap_any(a.gap_exact, L, a, u);
-              set_bit<W>(gam, pos, N);
-            }
-          }
-          bool pert = false;
-#pragma unroll
-          for (int w = 0; w < W; ++w) {
-            pert = pert || gam[w] != 0;
-            slot[w * 64 + lane] = m[w];
-            slot[(2 * W + w) * 64 + lane] = rsv[w];
-          }
-          slot[3 * W * 64 + lane] = rtv | (pcv << 8) | ((uint32_t)pert << 16);
-        } else {
-          // update k >= 1: perturbation gaps j = 0, 1, ... from SETTLE_ENV call ((k-1) << 8 | j >> 2), word j & 3
-          const uint32_t sub = k - 1;
-          Word4 P = {0, 0, 0, 0};
-          int pos = -1;
-          for (int j = 0; pos < N - 1; ++j) {
-            if ((j & 3) == 0)
-              P = pbn::philox(ge_lo, st_lo, (pbn::kStreamSettleEnv << 28) | (sub << 8) | (uint32_t)(j >> 2), ge_hi,
-                              u_k0, u_k1);
-            const int j4 = j & 3;
+        }
+        // gaps 0, 1 = words 0, 1; gap 2 = u2 (k = 0) or word 2 (k >= 1); then, rarely, more
+        const int g0 = gap_any(a.gap_exact, L, a, E.x), g1 = gap_any(a.gap_exact, L, a, E.y),
+                  g2 = gap_any(a.gap_exact, L, a, u2);
+        const int p0 = g0 - 1, p1 = p0 + g1, p2 = p1 + g2;
+        set_bit<W>(gam, p0, N);
+        set_bit<W>(gam, p1, N);
+        set_bit<W>(gam, p2, N);
+        if (p2 < N - 1) {   // k = 0: gap j >= 3 is PERT call (j-3) >> 2, word (j-3) & 3;
+                            // k >= 1: gap 3 is word 3, gap j >= 4 SETTLE_ENV call (k-1) << 8 | j >> 2
+          Word4 P = E;
+          int pos = p2;
+          for (int j = 3; pos < N - 1; ++j) {
+            const int jj = first ? j - 3 : j;
+            if ((jj & 3) == 0)
+              P = pbn::philox(ge_lo, st_lo,
+                              first ? ((pbn::kStreamPert << 28) | (uint32_t)(jj >> 2))
+                                    : ((pbn::kStreamSettleEnv << 28) | ((k - 1) << 8) | (uint32_t)(jj >> 2)),
+                              ge_hi, u_k0, u_k1);
+            const int j4 = jj & 3;
             const uint32_t u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
             pos += gap_any(a.gap_exact, L, a, u);
             set_bit<W>(gam, pos, N);
           }
-          bool pert = false;
-#pragma unroll
-          for (int w = 0; w < W; ++w) pert = pert || gam[w] != 0;
-          slot[3 * W * 64 + lane] = (uint32_t)pert << 16;
         }
 #pragma unroll
-        for (int w = 0; w < W; ++w) slot[(W + w) * 64 + lane] = gam[w];
+        for (int w = 0; w < W; ++w) pk = pk || gam[w] != 0;
       }
+      // -- the state wave's bit planes: flip and perturbation masks, the reset states
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        slot[w * 64 + lane] = lane_transpose32(m[w], lane);
+        slot[kGP + w * 64 + lane] = lane_transpose32(gam[w], lane);
+      }
+      const uint64_t pb = __ballot(pk), rb = __ballot(rst);
+      if (rb) {
+#pragma unroll
+        for (int w = 0; w < W; ++w) slot[kRP + w * 64 + lane] = lane_transpose32(rst ? st[w] : 0u, lane);
+      }
+      if (lane == 0) {
+        slot[kMK + 0] = (uint32_t)pb;
+        slot[kMK + 1] = (uint32_t)(pb >> 32);
+        slot[kMK + 2] = (uint32_t)rb;
+        slot[kMK + 3] = (uint32_t)(rb >> 32);
+      }
+      proc_prev = p.v && p.Pt < n_steps;   // what the state wave applies in this iteration
+      t_prev = p.Pt;
       lds_barrier();
       p.done();
     }
+    if (valid) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) a.state_out[CK((size_t)w * n + le, plane, 16)] = st[w];
+      a.t[CK(le, n, 17)] = (uint8_t)tt0;
+      a.target[CK(le, n, 18)] = (uint8_t)tg0;
+    }
   } else if (role == 2) {
-    SettlePlan p;
-    for (uint32_t it = 0; p.next(ctl, it, K, n_steps); ++it) {
-      asm volatile("" : "+s"(u_k0), "+s"(u_k1));
-      const uint32_t Rt0 = p.Rt0, Rk0 = p.Rk0, Rt1 = p.Rt1, Rk1 = p.Rk1;
-      // ---- selection masks of update R(i): node l32 + 32r of group g
-      const uint32_t t = half ? Rt1 : Rt0, k = half ? Rk1 : Rk0;
-      uint32_t* lt_out = slots + (size_t)(it & 1) * a.slot_words + (3 * W + 1) * 64 + half * 32 * W;
+    // ---- selection planes of each env's update R(i), env `lane`
+    EnvPlan p;
+    for (uint32_t it = 0;; ++it) {
+      const uint32_t* cin = ctl + ((it + 1) & 1) * 128;
+      const uint32_t Ct = cin[lane], Ck = cin[64 + lane];
+      if (__ballot(Ct < n_steps) == 0 || (uint64_t)it > max_it) break;
+      p.next(Ct, Ck, K);
+      const uint32_t t = p.Rt, k = p.Rk;   // (no update: the words are computed and discarded)
+      uint32_t* lt_out = slots + (size_t)(it & 1) * a.slot_words + kLT + half * 32 * W;
       const uint64_t step = a.step + (uint64_t)t;
       const uint32_t st_lo = (uint32_t)step;
-      const uint32_t G_hi = (uint32_t)((G >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
-      const uint32_t G_lo = (uint32_t)G;
-      // SEL (k = 0) or SETTLE_SEL idx (k-1) << 9 | 4i + c (k >= 1)
-      const uint32_t base = k == 0 ? (pbn::kStreamSel << 28) : ((pbn::kStreamSettleSel << 28) | ((k - 1) << 9));
-      if (valid && t < n_steps) {
+      const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
+      const uint32_t* th = a.sthr;
+      asm volatile("" : "+s"(th));   // the thresholds are read per iteration (hoisted: 32 SGPRs each)
 #pragma unroll
-        for (int r = 0; r < W; ++r) {
-          const int i = l32 + 32 * r;
-          const int ic = i < N ? i : 0;
-          const uint4 r0 = recL[ic];
-          if (i < N && (int)r0.w > 1) {
-            uint32_t dig[16];
+      for (int r = 0; r < W; ++r) {
+        uint32_t U[16];
+        settle_sel_words(ge_lo, ge_hi, st_lo, k, r, N, u_k0, u_k1, U);
 #pragma unroll
-            for (int c = 0; c < CPN; ++c) {
-              const Word4 o = pbn::philox(G_lo, st_lo, base | (uint32_t)(4 * i + c), G_hi, u_k0, u_k1);
-              dig[4 * c + 0] = o.x; dig[4 * c + 1] = o.y; dig[4 * c + 2] = o.z; dig[4 * c + 3] = o.w;
-            }
-            const int nf = (int)r0.w;
-#pragma unroll
-            for (int q = 0; q < kNodeRecs - 1; ++q)
-              if (q < nf - 1) {
-                if constexpr (W == 1)
-                  lt_out[q * 64 * W + i] = less_than_cm<B>(dig, cm + (size_t)q * B * 32 + i, 32);
-                else
-                  lt_out[q * 64 * W + i] = less_than(dig, recL[q * 32 * W + ic].z, B);
-              }
+        for (int q = 0; q < kNodeRecs - 1; ++q) {
+          if (q < lq) {
+            const uint32_t lt = settle_lt_word(U, th + (size_t)(q * W + r) * 32);
+            lt_out[q * 64 * W + 32 * r + l32] = lane_transpose32(lt, lane);
           }
         }
       }
@@ -2026,52 +2130,29 @@ pbn_rollout_settle(StepArgs a) {
       p.done();
     }
   } else {
-    // per-env state of the step in progress
-    uint32_t cur[W], rs[W];
-    uint32_t rt = 0, pc = 0, nupd = 0;
-    bool open = false, pacc = false;
-    int att = -1;
+    // ---- state: the envs of each word bit-sliced (lane = node l32 + 32w of group `half`)
+    uint32_t planes[W];
 #pragma unroll
-    for (int w = 0; w < W; ++w) { cur[w] = 0; rs[w] = 0; }
-    SettlePlan p;
-    for (uint32_t it = 0; p.next(ctl, it, K, n_steps); ++it) {
-      const uint32_t Pt0 = p.Pt0, Pk0 = p.Pk0, Pt1 = p.Pt1, Pk1 = p.Pk1;
-      const uint32_t Ct0 = p.Ct0, Ck0 = p.Ck0, Ct1 = p.Ct1, Ck1 = p.Ck1;
-      const bool v0 = p.v0, v1 = p.v1;
-      // ---- state: apply R(i-1) (slot (i-1) & 1) to the groups for which it is valid
-      const bool proc0 = v0 && Pt0 < n_steps, proc1 = v1 && Pt1 < n_steps;
-      const bool proc = half ? proc1 : proc0;
-      const uint32_t t = half ? Pt1 : Pt0, k = half ? Pk1 : Pk0;
+    for (int w = 0; w < W; ++w) planes[w] = lane_transpose32(st[w], lane);
+    uint32_t Ct = valid ? 0u : n_steps, Ck = 0;
+    bool pacc = false;
+    EnvPlan p;
+    for (uint32_t it = 0;; ++it) {
+      if (__ballot(Ct < n_steps) == 0 || (uint64_t)it > max_it) break;
+      p.next(Ct, Ck, K);
+      const bool proc = p.v && p.Pt < n_steps;
+      const uint32_t t = p.Pt, k = p.Pk;
       const uint32_t* slot = slots + (size_t)((it + 1) & 1) * a.slot_words;
-      const uint32_t* lt_in = slot + (3 * W + 1) * 64 + half * 32 * W;
-      uint32_t s1[W], gam[W];
-      const uint32_t info = slot[3 * W * 64 + lane];
-      const bool pk = (info >> 16) & 1u;
-      if (k == 0) {
-        if (proc && valid && (u_fl & 1u)) {
+      const uint32_t* lt_in = slot + kLT + half * 32 * W;
+      const uint32_t PKh = slot[kMK + half], RMh = slot[kMK + 2 + half];
+      const uint64_t prb = __ballot(proc);
+      const uint32_t PRh = half ? (uint32_t)(prb >> 32) : (uint32_t)prb;
+      uint32_t s1[W];
 #pragma unroll
-          for (int w = 0; w < W; ++w) LANE_STV(a.obs, (t * plane + (size_t)w * n) + (size_t)le, (size_t)n_steps * plane, 7, st[w]);
-        }
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-          s1[w] = st[w] ^ slot[w * 64 + lane];
-          if (proc) rs[w] = slot[(2 * W + w) * 64 + lane];
-        }
-        if (proc) {
-          rt = info & 0xFFu;
-          pc = (info >> 8) & 0xFFu;
-          open = valid;
-          pacc = false;
-          nupd = 0;
-        }
-      } else {
-#pragma unroll
-        for (int w = 0; w < W; ++w) s1[w] = cur[w];
+      for (int w = 0; w < W; ++w) {
+        s1[w] = pbn::bfi3(RMh, slot[kRP + w * 64 + lane], planes[w]) ^ slot[w * 64 + lane];
+        Sg[32 * w + l32] = s1[w];
       }
-#pragma unroll
-      for (int w = 0; w < W; ++w) gam[w] = slot[(W + w) * 64 + lane];
-#pragma unroll
-      for (int w = 0; w < W; ++w) Sg[32 * w + l32] = lane_transpose32(s1[w], lane);
       __builtin_amdgcn_wave_barrier();
       uint32_t X[W];
 #pragma unroll
@@ -2088,60 +2169,35 @@ pbn_rollout_settle(StepArgs a) {
           default: X[r] = chain_padded<4, (W <= 2)>(rc, sel, 32 * W, Sg, lti, 64 * W); break;
         }
       }
-      uint32_t sp[W];
+      uint32_t cur[W];
 #pragma unroll
-      for (int w = 0; w < W; ++w) sp[w] = lane_transpose32(X[w], lane);
-      if (proc && open) {
-#pragma unroll
-        for (int w = 0; w < W; ++w) cur[w] = pk ? (s1[w] ^ gam[w]) : sp[w];
-        pacc = pacc || pk;
-        ++nupd;
-        att = attractor_lookup<W>(a, htab, cur);
-        open = att < 0;
+      for (int w = 0; w < W; ++w) {
+        // perturbed envs: s1 ^ gamma; envs without a valid update keep their state
+        const uint32_t xp = pbn::bfi3(PKh, s1[w] ^ slot[kGP + w * 64 + lane], X[w]);
+        planes[w] = pbn::bfi3(PRh, xp, planes[w]);
+        cur[w] = lane_transpose32(planes[w], lane);
       }
-      // the group's decision: the step ends when no env of the group is open or the cap is reached
-      const uint64_t ob = __ballot(proc && open);
-      const bool end0 = proc0 && ((uint32_t)ob == 0u || Pk0 + 1 >= K);
-      const bool end1 = proc1 && ((uint32_t)(ob >> 32) == 0u || Pk1 + 1 >= K);
-      if (lane == 0) {
-        uint32_t* cout = ctl + (it & 1) * 4;
-        cout[0] = proc0 ? (end0 ? Pt0 + 1 : Pt0) : Ct0;
-        cout[1] = proc0 ? (end0 ? 0u : Pk0 + 1) : Ck0;
-        cout[2] = proc1 ? (end1 ? Pt1 + 1 : Pt1) : Ct1;
-        cout[3] = proc1 ? (end1 ? 0u : Pk1 + 1) : Ck1;
+      const int att = attractor_lookup<W>(a, htab, cur);
+      const bool open = att < 0;
+      const bool pkl = (PKh >> l32) & 1u;
+      const bool end = proc && (!open || k + 1 >= K);
+      if (proc) {
+        pacc = (k != 0 && pacc) || pkl;
+        Ct = end ? t + 1 : t;
+        Ck = end ? 0u : k + 1;
       }
-      if ((half ? end1 : end0) && valid) {
-        // epilogue of step t
-        if (u_fl & 2u) {
+      uint32_t* cout = ctl + (it & 1) * 128;
+      cout[lane] = Ct;
+      cout[64 + lane] = Ck;
+      if (end) {
+        uint32_t* eo = einfo + (it & 1) * (2 + W) * 64;
+        eo[lane] = (uint32_t)(att + 1) | ((uint32_t)pacc << 16) | ((uint32_t)open << 17);
+        eo[64 + lane] = k + 1;
 #pragma unroll
-          for (int w = 0; w < W; ++w) LANE_STV(a.final_state, (t * plane + (size_t)w * n) + (size_t)le, (size_t)n_steps * plane, 10, cur[w]);
-        }
-        if (u_fl & 32u) LANE_STV(a.updates, ((size_t)t * n) + (size_t)le, (size_t)n_steps * n, 23, (uint16_t)min(nupd, 0xFFFFu));
-        const float4 r4 = reinterpret_cast<const float4*>(rtab)[pc];
-        const bool in_attr = att >= 0;
-        const bool term = in_attr && (uint32_t)att == tg0;
-        const bool wrong = in_attr && !term;
-        int tt = (int)tt0 + 1;
-        tt = tt > 255 ? 255 : tt;
-        const bool trunc = a.horizon > 0 && tt >= a.horizon;
-        const bool reset = (u_fl & 8u) && (term || trunc);
-        const uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) |
-                            ((uint32_t)pacc << 3) | ((uint32_t)reset << 4) | ((uint32_t)open << 5);
-        LANE_STV(a.reward, ((size_t)t * n) + (size_t)le, (size_t)n_steps * n, 11, term ? r4.z : (wrong ? r4.y : r4.x));
-        LANE_STV(a.flags, ((size_t)t * n) + (size_t)le, (size_t)n_steps * n, 15, (uint8_t)fl);
-        tg0 = reset ? rt : tg0;
-        tt0 = reset ? 0u : (uint32_t)tt;
-#pragma unroll
-        for (int w = 0; w < W; ++w) st[w] = reset ? rs[w] : cur[w];
+        for (int w = 0; w < W; ++w) eo[(2 + w) * 64 + lane] = cur[w];
       }
       lds_barrier();
       p.done();
-    }
-    if (valid) {
-#pragma unroll
-      for (int w = 0; w < W; ++w) a.state_out[CK((size_t)w * n + le, plane, 16)] = st[w];
-      a.t[CK(le, n, 17)] = (uint8_t)tt0;
-      a.target[CK(le, n, 18)] = (uint8_t)tg0;
     }
   }
 }

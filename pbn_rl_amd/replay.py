@@ -308,6 +308,8 @@ class FusedBDQUpdate:
         self.q_flat = self._flatten(q, dev)
         self.t_flat = self._flatten(target, dev)
         self.q, self.target = q, target
+        self._qp, self._tp = list(q.parameters()), list(target.parameters())
+        self._qv = self._tv = None
         self.m = torch.zeros_like(self.q_flat)
         self.v = torch.zeros_like(self.q_flat)
         self.step = torch.zeros(1, dtype=torch.float32, device=dev)
@@ -342,6 +344,17 @@ class FusedBDQUpdate:
     def _stream(self):
         return torch.cuda.current_stream(self.q_flat.device).cuda_stream
 
+    @staticmethod
+    def _versions(params) -> tuple:
+        return tuple(p._version for p in params)
+
+    @staticmethod
+    def _bump(params) -> None:
+        """Mark parameters the HIP kernels rewrote in place (their version counters are how
+        PyTorch, and BatchedBDQ's eval-mode pack cache, see an in-place change)."""
+        for p in params:
+            torch.autograd.graph.increment_version(p)
+
     def pack(self, which: str = "both") -> None:
         """Recompute the bilinear target tables (pbn_bdq_pack) of the online and/or target network."""
         L = _lib.load()
@@ -350,11 +363,30 @@ class FusedBDQUpdate:
                 if which in ("both", name):
                     _lib.check(L.pbn_bdq_pack(self.net.handle, self.K, flat.data_ptr(), table.data_ptr(),
                                               self._stream()), "pbn_bdq_pack")
+        if which in ("both", "online"):
+            self._qv = self._versions(self._qp)
+        if which in ("both", "target"):
+            self._tv = self._versions(self._tp)
+
+    def sync(self) -> None:
+        """Repack the table of a network whose parameters changed since its last pack (e.g. a
+        load_state_dict: the copy bumps the parameters' versions); a no-op otherwise."""
+        if self._versions(self._qp) != self._qv:
+            self.pack("online")
+        if self._versions(self._tp) != self._tv:
+            self.pack("target")
+
+    def mark_updated(self) -> None:
+        """After a pbn_bdq_learn launch (eager, or a replayed graph holding one): the online
+        parameters changed in place."""
+        self._bump(self._qp)
+        self._qv = self._versions(self._qp)
 
     def soft_update(self) -> None:
         """target <- target / 2 + online / 2 (soft_update's arithmetic, one pass over the buffer)."""
         with torch.no_grad():
             self.t_flat.div_(2).add_(self.q_flat / 2)
+        self._bump(self._tp)
         self.pack("target")
 
     def acting_pack(self):
@@ -366,6 +398,7 @@ class FusedBDQUpdate:
         (overwritten by the next update)."""
         if idx.shape != (self.B,) or idx.dtype != torch.int64:
             raise ValueError(f"idx must be {self.B} int64 ring indices")
+        self.sync()
         L = _lib.load()
         b1, b2 = self.betas
         with torch.cuda.device(self.q_flat.device):
@@ -378,6 +411,8 @@ class FusedBDQUpdate:
                                        self.grad_clamp, self.slope, self.work.data_ptr(), self.work.numel() * 4,
                                        self.loss.data_ptr(), self.grad.data_ptr() if self.grad is not None else None,
                                        self._stream()), "pbn_bdq_learn")
+        if not torch.cuda.is_current_stream_capturing():
+            self.mark_updated()   # (a captured update is marked by each replay: BDQLearner._replay_frame)
         return self.loss[0]
 
     def grads(self) -> List[torch.Tensor]:
@@ -408,12 +443,6 @@ class BDQLearner:
                  graphable: bool = False, blas: Optional[str] = "cublas", fused: Optional[bool] = None):
         if not env.keep_final_state:
             raise ValueError("BDQLearner needs the env's final_state (keep_final_state=True)")
-        if blas:
-            # the update's GEMMs are small (batch 256-512, widths 28-256): rocBLAS ("cublas" in
-            # torch's naming on ROCm) runs the weight-gradient products (K = batch) 2.5-8x faster
-            # than hipBLASLt's picks (tools/learn_profile.py, profiles/r04_z*); this sets the
-            # process-wide preference, None leaves it alone
-            torch.backends.cuda.preferred_blas_library(blas)
         self.env = env
         self.agent = BatchedBDQ(env, qnet)
         self.q = self.agent.q.train()
@@ -430,6 +459,13 @@ class BDQLearner:
                                         learning_rate=learning_rate, gamma=gamma)
             self.agent.pack_provider = self.fused.acting_pack
         else:
+            if blas:
+                # the PyTorch update's GEMMs are small (batch 256-512, widths 28-256): rocBLAS
+                # ("cublas" in torch's naming on ROCm) runs the weight-gradient products (K = batch)
+                # 2.5-8x faster than hipBLASLt's picks (tools/learn_profile.py, profiles/r04_z*).
+                # This sets the process-wide preference, so only this path sets it (the fused
+                # update runs no GEMM); blas=None leaves it alone
+                torch.backends.cuda.preferred_blas_library(blas)
             # one fused multi-tensor kernel per step instead of a handful per parameter tensor
             # capturable keeps Adam's step counts on the device (needed to replay it in a hipGraph)
             self.opt = torch.optim.Adam(self.q.parameters(), lr=learning_rate, fused=True, capturable=graphable)
@@ -454,14 +490,20 @@ class BDQLearner:
         self.graphable = graphable
         self._graph: Optional[torch.cuda.CUDAGraph] = None
         self._tw = None   # _target_weights()
+        self._tw_key = None
 
     def _target_weights(self):
         """The target network's stacked head weights (BranchingQNetwork.head_weights), held in
-        fixed tensors: the target changes only at soft updates, which refresh them in place (a
-        captured frame reads these very tensors)."""
+        fixed tensors (a captured frame reads these very tensors).  They are refreshed in place
+        whenever the target's parameters changed since (soft updates, a load_state_dict: any
+        in-place write bumps the parameters' versions)."""
+        key = tuple(p._version for p in self.target.parameters())
         if self._tw is None:
             with torch.no_grad():
                 self._tw = tuple(w.detach().clone() for w in self.target.head_weights())
+        elif key != self._tw_key:
+            self._refresh_target_weights()
+        self._tw_key = key
         return self._tw
 
     def _refresh_target_weights(self) -> None:
@@ -469,6 +511,7 @@ class BDQLearner:
             with torch.no_grad():
                 for dst, w in zip(self._tw, self.target.head_weights()):
                     dst.copy_(w)
+            self._tw_key = tuple(p._version for p in self.target.parameters())
 
     def frame(self):
         if self._graph is not None:
@@ -595,7 +638,17 @@ class BDQLearner:
 
     def _replay_frame(self):
         env, rp = self.env, self.replay
+        if self.fused is not None:
+            self.fused.sync()            # weights loaded between replays: repack the tables
+        else:
+            self._target_weights()       # (refreshes the captured head-weight copies if stale)
         self._graph.replay()
+        # the replayed update rewrote the online parameters in place (version counters: what
+        # PyTorch and BatchedBDQ's eval-mode pack cache read)
+        if self.fused is not None:
+            self.fused.mark_updated()
+        else:
+            FusedBDQUpdate._bump(self.q.parameters())
         env.step_index += 1
         rp.pos = (rp.pos + env.n_alloc) % rp.capacity
         rp.size = min(rp.size + env.n_alloc, rp.capacity)

@@ -79,22 +79,26 @@ def test_act_dev_matches_act():
         assert torch.equal(env.flipmask, fm) and torch.equal(agent.actions, acts), eps
 
 
-def _learner(n, seed):
+def _learner(n, seed, fused):
     spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.01)
     env = VectorPBNEnv(spec, n, seed=seed)
     torch.manual_seed(4)
     lr = BDQLearner(env, BranchingQNetwork((28, 28), 29, 3), capacity=8 * n, learning_starts=2 * n,
                     batch_size=256, target_update=4, epsilon_start=1.0, epsilon_final=1.0, seed=11,
-                    graphable=True)
+                    graphable=True, fused=fused)
     env.reset()
     return env, lr
 
 
-def test_captured_learner_matches_eager():
-    """epsilon = 1: actions do not depend on Q, so env and ring must agree exactly."""
+@pytest.mark.parametrize("fused", [True, False])
+def test_captured_learner_matches_eager(fused):
+    """epsilon = 1: actions do not depend on Q, so env and ring must agree exactly.  Both update
+    paths: the fused HIP update (pbn_bdq_learn) and the PyTorch one (bdq_update + Adam), each
+    with its own captured body."""
     n = 1024
-    env_e, eager = _learner(n, 21)
-    env_g, graph = _learner(n, 21)
+    env_e, eager = _learner(n, 21, fused)
+    env_g, graph = _learner(n, 21, fused)
+    assert (graph.fused is not None) == fused and (eager.fused is not None) == fused
     graph.capture()
     assert graph.updates == 3 and graph.frames == 4
     for _ in range(graph.frames):
@@ -123,11 +127,13 @@ def test_captured_learner_matches_eager():
     assert abs(float(eager.last_loss) - float(graph.last_loss)) <= 1e-3 * max(1.0, abs(float(eager.last_loss)))
 
 
-def test_captured_learner_epsilon_schedule():
+@pytest.mark.parametrize("fused", [True, False])
+def test_captured_learner_epsilon_schedule(fused):
     spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"))
     env = VectorPBNEnv(spec, 512, seed=2)
     lr = BDQLearner(env, capacity=4096, learning_starts=1024, batch_size=128, epsilon_start=1.0,
-                    epsilon_final=0.5, epsilon_decay=6, target_update=2, updates_per_frame=2, graphable=True)
+                    epsilon_final=0.5, epsilon_decay=6, target_update=2, updates_per_frame=2, graphable=True,
+                    fused=fused)
     env.reset()
     lr.capture(min_updates=2)
     for _ in range(8):
@@ -136,3 +142,35 @@ def test_captured_learner_epsilon_schedule():
     assert lr.epsilon == 0.5
     assert float(lr._eps64.item()) == lr.epsilon and lr.replay.size == 4096
     assert torch.isfinite(lr.last_loss)
+
+
+@pytest.mark.parametrize("fused,captured", [(True, False), (True, True), (False, True)])
+def test_eval_agent_sees_learner_updates(fused, captured):
+    """the fused update (and a replayed captured update) rewrites the parameters in
+    place, and an eval-mode BatchedBDQ caches its weight pack by parameter version, so the learner
+    bumps the versions.  An evaluation agent built on learner.q (evaluated in eval mode between
+    training frames) answers after training as a fresh agent does, not with its first pack."""
+    env, lr = _learner(512, 5, fused)
+    ev_env = VectorPBNEnv(env.spec, 256, seed=9)
+    ev_env.reset()
+    if captured:
+        lr.capture()
+    ev = BatchedBDQ(ev_env, lr.q)
+
+    def evaluate(agent):
+        lr.q.eval()
+        try:
+            out = agent.q_values().clone()
+        finally:
+            lr.q.train()
+        return out
+
+    first = evaluate(ev)
+    for _ in range(6):
+        lr.frame()
+    torch.cuda.synchronize()
+    after = evaluate(ev)
+    fresh = evaluate(BatchedBDQ(ev_env, lr.q))
+    torch.cuda.synchronize()
+    assert not torch.equal(first, after), "the eval agent served its stale pack"
+    assert torch.allclose(after, fresh, rtol=1e-5, atol=1e-6)

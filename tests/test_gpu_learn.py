@@ -220,3 +220,50 @@ def test_fused_learner_loads_a_checkpoint():
         lr.frame()
     torch.cuda.synchronize()
     assert torch.isfinite(lr.last_loss)
+
+
+def test_fused_update_matches_reference_update_policy():
+    """pbn_bdq_learn held to the reference's own update_policy (bdq_model/__init__.py:100-139):
+    tests/golden/bdq_update.npz, two calls of that method's source on the reference network
+    (tools/gen_update_golden.py; the CPU form is held to it in tests/test_update_golden.py).  The
+    fixture's batches go into a DeviceReplay ring (rows 0..255 in order, targets as attractor ids).
+    Loss rtol 1e-5; clamped gradients rtol 1e-3 / atol 1e-6; parameters after Adam: atol 1e-5
+    where the reference gradient exceeds 1e-4 (one Adam step is ~lr there), else within two steps
+    (2 lr: a gradient near 0 may take the other sign); the soft-updated target likewise."""
+    from tests.test_update_golden import load_fixture
+    d, names = load_fixture()
+    N, K, B = 7, 3, 256
+    lr, gamma = float(d["lr"]), float(d["gamma"])
+    spec = EnvSpec(load_network("pbn7"), load_attractors("pbn7"))
+    env = VectorPBNEnv(spec, 64)
+    dev = torch.device("cuda")
+    q, tgt = BranchingQNetwork((N, N), N + 1, K).to(dev), BranchingQNetwork((N, N), N + 1, K).to(dev)
+    q.load_state_dict({n: torch.from_numpy(d["q0." + n]) for n in names})
+    tgt.load_state_dict({n: torch.from_numpy(d["t0." + n]) for n in names})
+    fused = FusedBDQUpdate(q, tgt, env.net, K, batch_size=B, learning_rate=lr, gamma=gamma, keep_grad=True)
+    bits = (1 << np.arange(N, dtype=np.uint32))
+    to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    idx = torch.arange(B, dtype=torch.int64, device=dev)
+    for call in (1, 2):
+        p = f"b{call}."
+        R = DeviceReplay(B, 1, K, dev)
+        st = (d[p + "states"].astype(np.uint32) * bits).sum(1).astype(np.uint32)[None]
+        nst = (d[p + "next_states"].astype(np.uint32) * bits).sum(1).astype(np.uint32)[None]
+        R.store(to(st.view(np.int32)), to(d[p + "target_ids"]), to(d[p + "actions"].astype(np.int32)),
+                to(d[p + "rewards"]), to(nst.view(np.int32)), to(d[p + "done"]))
+        loss = float(fused.update(R, idx))
+        torch.cuda.synchronize()
+        want = float(d["losses"][call - 1])
+        assert abs(loss - want) <= 1e-5 * abs(want), (call, loss, want)
+        for n, g, w in zip(names, fused.grads(), q.parameters()):
+            g_ref = torch.from_numpy(d[f"g{call}.{n}"]).to(dev)
+            assert torch.allclose(g, g_ref, rtol=1e-3, atol=1e-6), (call, n, (g - g_ref).abs().max().item())
+            w_ref = torch.from_numpy(d[f"q{call}.{n}"]).to(dev)
+            err = (w.detach() - w_ref).abs()
+            big = g_ref.abs() > 1e-4
+            assert err[big].max().item() <= 1e-5 if big.any() else True, (call, n, err[big].max().item())
+            assert err.max().item() <= 2.1 * lr * call, (call, n, err.max().item())
+    fused.soft_update()
+    for n, w in zip(names, tgt.parameters()):
+        w_ref = torch.from_numpy(d["t2." + n]).to(dev)
+        assert (w.detach() - w_ref).abs().max().item() <= 2.1 * lr, n

@@ -20,13 +20,14 @@ def u32(x):
     return x.cpu().numpy().view(np.uint32)
 
 
-def test_learner_transitions_match_oracle():
+@pytest.mark.parametrize("fused", [True, False])
+def test_learner_transitions_match_oracle(fused):
     spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.02)
     n, seed = 1024, 17
     env = VectorPBNEnv(spec, n, seed=seed)
     torch.manual_seed(0)
     learner = BDQLearner(env, BranchingQNetwork((28, 28), 29, 3), capacity=4 * n, learning_starts=2 * n,
-                         epsilon_start=0.5, seed=3)
+                         epsilon_start=0.5, seed=3, fused=fused)
     env.reset()
     st, tg, t = oracle.reset(spec, seed, 0, 0, n)
     for k in range(3):
@@ -72,11 +73,13 @@ def test_gather_unpacks_like_the_oracle():
     assert np.array_equal(b["next_obs"].cpu().numpy(), agent_oracle.obs_unpack(spec, nst[:, i], tg[i]))
 
 
-def test_learner_many_frames():
+@pytest.mark.parametrize("fused", [True, False])
+def test_learner_many_frames(fused):
     spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"))
     env = VectorPBNEnv(spec, 4096, seed=1)
     torch.manual_seed(1)
-    learner = BDQLearner(env, capacity=1 << 16, learning_starts=4096, updates_per_frame=2, target_update=5)
+    learner = BDQLearner(env, capacity=1 << 16, learning_starts=4096, updates_per_frame=2, target_update=5,
+                         fused=fused)
     env.reset()
     w0 = learner.q.model[0].bilinear.weight.detach().clone()
     for _ in range(12):

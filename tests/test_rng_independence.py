@@ -5,7 +5,9 @@ Every stream draws Philox4x32-7 at counter (lo32 id, lo32 step, stream << 28 | i
 hi16 id | hi16 step << 16) under one fixed key (DESIGN.md "RNG").  Neighbouring counters are
 where a marginal round count would fail, so these tests draw the words the kernels actually
 use for pairs of neighbours -- env e vs e + 1, step k vs k + 1, call idx vs idx + 1, the SEL vs
-the ENV stream at the same id and step, SETTLE_SEL vs SEL -- and check each pair:
+the ENV stream at the same id and step, SETTLE_SEL vs SEL, the settle law's per-env selection
+calls (update k vs k + 1, call c vs c + 1, and the two 16-bit node fields of one word) -- and
+check each pair:
   * joint chi-square of the top 4 bits (256 cells, 2^16 pairs: 256 expected per cell);
   * every one of the 32 x 32 single-bit XOR relations between the two words (a linear
     dependence between bit i of one and bit j of the other shows as a biased XOR): each must
@@ -34,17 +36,18 @@ def words(ident, step, stream, idx):
     return philox_vec(c0, c1, c2, c3, SEED & 0xFFFFFFFF, SEED >> 32)
 
 
-def check_pair(a: np.ndarray, b: np.ndarray, what: str):
+def check_pair(a: np.ndarray, b: np.ndarray, what: str, bits: int = 32):
     n = a.size
     # joint top-4-bit chi-square
-    cells = ((a >> np.uint32(28)).astype(np.int64) << 4) | (b >> np.uint32(28)).astype(np.int64)
+    top = np.uint32(bits - 4)
+    cells = ((a >> top).astype(np.int64) << 4) | (b >> top).astype(np.int64)
     counts = np.bincount(cells, minlength=256)
     expect = n / 256
     chi2 = ((counts - expect) ** 2 / expect).sum()
     assert chi2 < 255 + 6 * np.sqrt(2 * 255) + 10, (what, chi2)
     # single-bit XOR relations, all 32 x 32 bit pairs
-    abits = ((a[:, None] >> np.arange(32, dtype=np.uint32)) & 1).astype(np.uint8)
-    bbits = ((b[:, None] >> np.arange(32, dtype=np.uint32)) & 1).astype(np.uint8)
+    abits = ((a[:, None] >> np.arange(bits, dtype=np.uint32)) & 1).astype(np.uint8)
+    bbits = ((b[:, None] >> np.arange(bits, dtype=np.uint32)) & 1).astype(np.uint8)
     ones_a = abits.sum(axis=0).astype(np.int64)
     ones_b = bbits.sum(axis=0).astype(np.int64)
     both = abits.T.astype(np.int32) @ bbits.astype(np.int32)               # (32, 32): count a_i = b_j = 1
@@ -56,7 +59,7 @@ def check_pair(a: np.ndarray, b: np.ndarray, what: str):
     assert abs(r) < 6.0 / np.sqrt(n), (what, r)
 
 
-@pytest.mark.parametrize("stream", [ENV, PERT, RESET, EXPLORE, SETTLE_ENV])
+@pytest.mark.parametrize("stream", [ENV, PERT, RESET, EXPLORE, SETTLE_SEL, SETTLE_ENV])
 def test_neighbouring_envs(stream):
     e = np.arange(N_PAIRS, dtype=np.uint64) * np.uint64(2)    # pairs (e, e + 1)
     step = np.full(N_PAIRS, 17, dtype=np.uint64)
@@ -105,6 +108,19 @@ def test_sel_vs_env_and_settle_streams():
     for k in range(4):
         check_pair(S[k], E[k], f"SEL vs ENV word {k}")
         check_pair(S[k], T[k], f"SEL vs SETTLE_SEL word {k}")
+
+
+def test_settle_selection_calls():
+    """The settle law's per-env selection draws (SETTLE_SEL idx = k << 8 | call, node i = 16-bit
+    field i & 1 of word (i >> 1) & 3 of call i >> 3): update k vs k + 1 and call c vs c + 1 of
+    one env, and the two node fields of one word."""
+    e = np.arange(N_PAIRS, dtype=np.uint64)
+    step = np.full(N_PAIRS, 9, dtype=np.uint64)
+    A = words(e, step, SETTLE_SEL, (3 << 8) | 1)
+    check_pair(A[2], words(e, step, SETTLE_SEL, (4 << 8) | 1)[2], "SETTLE_SEL update k vs k+1")
+    check_pair(A[0], words(e, step, SETTLE_SEL, (3 << 8) | 2)[0], "SETTLE_SEL call c vs c+1")
+    for k in range(4):
+        check_pair(A[k] & np.uint32(0xFFFF), A[k] >> np.uint32(16), f"SETTLE_SEL word {k}: node 2j vs 2j+1", bits=16)
 
 
 def test_words_within_one_call():

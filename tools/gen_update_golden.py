@@ -1,0 +1,129 @@
+"""Generate tests/golden/bdq_update.npz: two steps of the reference's own ``update_policy``
+(bdq_model/__init__.py:100-139), the learner row's pin.
+
+  python tools/gen_update_golden.py       (build container only: reads /root/reference)
+
+The reference package cannot be imported (its __init__ imports the absent gym), so:
+  * ``BranchingQNetwork`` is loaded from its own file, bdq_model/network.py, by path (as
+    tools/gen_bdq_golden.py does);
+  * ``BranchingDQN.update_policy`` is taken from bdq_model/__init__.py with ``ast`` (the method's
+    source text, unchanged) and executed as a plain function on a stand-in ``self`` that carries
+    what the method reads: ``q``, ``target`` (reference networks), ``config.device``, ``gamma``,
+    ``target_net_update_freq``, ``update_counter`` and ``wandb.log`` (records the loss);
+  * ``memory.sample(batch_size)`` returns a fixed list of Transition tuples (the stand-in for
+    ExperienceReplay.sample's random.sample; the rows are the fixture's batch, in order).
+Network: pbn7's shape, BranchingQNetwork((7, 7), 8, 3) (the fused learner's smallest case; its
+parameters fit a small fixture), seeded init, the target a perturbed copy.  Batch: 256 rows:
+random 0/1 states and next states, targets = first states of pbn7's attractors (the replay stores
+the attractor id), three actions in [0, 7], random rewards, done in {0, 1}; a second batch for
+the second call.  Adam(lr=1e-3), gamma 0.9, target_net_update_freq 2: call 1 is an update, call 2
+an update followed by the soft update (target <- target / 2 + q / 2).
+
+Stored: the batches (uint8 / int / float32), the parameters before (q0.*, t0.*), the clamped
+gradients and parameters after each call (g1.*, q1.*, g2.*, q2.*), the target after call 2
+(t2.*), the losses.
+"""
+import ast
+import importlib.util
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, ROOT)
+
+from pbn_rl_amd.attractors import load_attractors  # noqa: E402
+
+REF = "/root/reference"
+OUT = os.path.join(ROOT, "tests", "golden", "bdq_update.npz")
+N, K, B = 7, 3, 256
+LR, GAMMA = 1e-3, 0.9
+
+
+def ref_network_module():
+    spec = importlib.util.spec_from_file_location("ref_bdq_network", os.path.join(REF, "bdq_model", "network.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def ref_update_policy():
+    """BranchingDQN.update_policy's source from the reference file, compiled as a function."""
+    path = os.path.join(REF, "bdq_model", "__init__.py")
+    tree = ast.parse(open(path).read(), filename=path)
+    cls = next(n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == "BranchingDQN")
+    fn = next(n for n in cls.body if isinstance(n, ast.FunctionDef) and n.name == "update_policy")
+    mod = ast.Module(body=[fn], type_ignores=[])
+    ns = {"torch": torch, "np": np, "F": F}
+    exec(compile(mod, path, "exec"), ns)
+    return ns["update_policy"], (fn.lineno, fn.end_lineno)
+
+
+def batch(rng, att_first):
+    states = rng.integers(0, 2, size=(B, N), dtype=np.uint8)
+    next_states = rng.integers(0, 2, size=(B, N), dtype=np.uint8)
+    tid = rng.integers(0, len(att_first), size=B).astype(np.uint8)
+    targets = att_first[tid]
+    actions = rng.integers(0, N + 1, size=(B, K)).astype(np.int64)
+    rewards = rng.standard_normal(B).astype(np.float32)
+    done = (rng.random(B) < 0.5).astype(np.uint8)
+    return dict(states=states, next_states=next_states, target_ids=tid, targets=targets, actions=actions,
+                rewards=rewards, done=done)
+
+
+def transitions(b):
+    """Transition tuples as bdq_model/__init__.py:192-199 stores them: numpy state / target /
+    next state, the action tensor, a float reward, a bool done."""
+    return [(b["states"][r].astype(np.int64), b["targets"][r].astype(np.int64), torch.tensor(b["actions"][r]),
+             float(b["rewards"][r]), b["next_states"][r].astype(np.int64), bool(b["done"][r])) for r in range(B)]
+
+
+def main():
+    net_mod = ref_network_module()
+    update_policy, lines = ref_update_policy()
+    att = load_attractors("pbn7")
+    att_first = np.array([list(a[0]) for a in att], dtype=np.uint8)
+    rng = np.random.default_rng(20261018)
+    torch.manual_seed(5)
+    q = net_mod.BranchingQNetwork((N, N), N + 1, K)
+    target = net_mod.BranchingQNetwork((N, N), N + 1, K)
+    with torch.no_grad():
+        for pt, pq in zip(target.parameters(), q.parameters()):
+            pt.copy_(pq + 0.05 * torch.randn_like(pq))
+    names = [n for n, _ in q.named_parameters()]
+    out = {"lines": np.array(lines), "lr": np.float32(LR), "gamma": np.float32(GAMMA)}
+    for n, p in q.named_parameters():
+        out["q0." + n] = p.detach().numpy().copy()
+    for n, p in target.named_parameters():
+        out["t0." + n] = p.detach().numpy().copy()
+
+    losses = []
+    this = types.SimpleNamespace(
+        q=q, target=target, config=types.SimpleNamespace(device="cpu"), gamma=GAMMA, target_net_update_freq=2,
+        update_counter=0, wandb=types.SimpleNamespace(log=lambda d: losses.append(float(d["loss"]))))
+    adam = torch.optim.Adam(q.parameters(), lr=LR)
+    for call in (1, 2):
+        b = batch(rng, att_first)
+        for k, v in b.items():
+            out[f"b{call}.{k}"] = v
+        rows = transitions(b)
+        memory = types.SimpleNamespace(sample=lambda n, rows=rows: list(rows[:n]))
+        update_policy(this, adam, memory, B)
+        for n, p in q.named_parameters():
+            out[f"g{call}.{n}"] = p.grad.detach().numpy().copy()
+            out[f"q{call}." + n] = p.detach().numpy().copy()
+    assert this.update_counter == 0, "call 2 ran the soft update"
+    for n, p in target.named_parameters():
+        out["t2." + n] = p.detach().numpy().copy()
+    out["losses"] = np.array(losses, dtype=np.float32)
+    out["names"] = np.array(names)
+    np.savez_compressed(OUT, **out)
+    print("wrote", OUT, "update_policy lines", lines, "losses", losses, "bytes", os.path.getsize(OUT))
+
+
+if __name__ == "__main__":
+    main()
