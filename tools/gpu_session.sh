@@ -20,6 +20,8 @@
 #   settle           the driver's command (with its settle_law and hand-off fields) and config 2 under the
 #                    settle law alone (--settle 64, 200 steps) + its kernel trace
 #   bdqpmc           the BDQ frame under two PMC passes: L2 hits / misses / requests, HBM fetch + write
+#   handoff          the world-1 hand-off pass alone (tools/handoff_trace.py, plans 20 and 10,10) and its
+#                    rocprofv3 kernel + memory-copy trace, attributed per rep
 #   ubench           tools/ubench_valu_issue (VALU issue rates by instruction and waves per SIMD)
 #   nofinal          the driver's command and 2,000 steps without s' (--no-final-state)
 #   abenv            every pbn_rl_amd/libpbn_env_diag_*.so, then this tree: tests/test_gpu_parity.py,
@@ -92,6 +94,16 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/settle_trace" -o run -- \
         python bench.py --settle 64 --steps 200 --warmup 20 --no-cpu-baseline --no-gather \
         > "$out/settle_trace.json" 2> "$out/settle_trace.err" || fail settle-trace ;;
+    handoff)
+      for plan in 20 10,10; do
+        timeout -k 10 180 python tools/handoff_trace.py --plan $plan > "$out/handoff_${plan/,/_}.json" 2> "$out/handoff.err" \
+          || fail "handoff $plan"
+        cat "$out/handoff_${plan/,/_}.json"
+      done
+      timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$out/handoff_trace" -o run -- \
+        python tools/handoff_trace.py --plan 20 > "$out/handoff_trace.json" 2> "$out/handoff_trace.err" || fail handoff-trace
+      python tools/handoff_trace.py --summarize "$out/handoff_trace" > "$out/handoff_summary.json" || fail handoff-summary
+      echo "handoff done" ;;
     ubench)
       timeout -k 10 300 tools/ubench_valu_issue > "$out/ubench_valu_issue.jsonl" 2> "$out/ubench.err" || fail ubench
       echo "ubench done" ;;

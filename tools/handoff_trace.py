@@ -1,0 +1,102 @@
+"""The world-1 hand-off pass of bench.py (gather_pass, ShardedRollout.gather with copy_own) alone,
+for a kernel-and-copy trace:
+
+  rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d DIR -o run -- \\
+      python tools/handoff_trace.py [--steps 20] [--plan 20] [--reps 20]
+
+Each rep: the rollout launches of the plan into the ring's record slots, each followed by the
+hand-off of its records (at world 1: the learner's own shard copied into its receive slot on a
+side stream), then a device sync.  Prints one JSON line with the per-rep device time of the
+pass (HIP events around each rep, after two untimed reps), and with --summarize DIR attributes
+the trace: per rep, the rollout kernels, the copy (kernel or DMA), and the gaps between them.
+"""
+import argparse
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, ROOT)
+
+
+def run(args):
+    import torch
+
+    from pbn_rl_amd.attractors import load_attractors
+    from pbn_rl_amd.distributed import ShardedRollout
+    from pbn_rl_amd.network import load_network
+    from pbn_rl_amd.spec import EnvSpec
+    from pbn_rl_amd.vector_env import VectorPBNEnv
+
+    spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.01, horizon=20)
+    env = VectorPBNEnv(spec, args.envs, seed=0, keep_final_state=True)
+    env.reset()
+    plan = [int(x) for x in args.plan.split(",")]
+    ro = ShardedRollout(env.n_alloc, lambda off, cnt: env)
+    stream = torch.cuda.current_stream()
+
+    def rep():
+        for k in plan:
+            ro.gather(ro.rollout(k), dst=0, async_op=True, copy_own=True)
+        for works in ro._pending.values():
+            for w in works:
+                if w is not None:
+                    w.wait()
+
+    for _ in range(2):
+        rep()
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(args.reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(2_000_000)   # the host enqueues the rep while this spins
+        e0.record(stream)
+        rep()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        times.append(e0.elapsed_time(e1) * 1e3)
+    times.sort()
+    wire = sum(env.n_alloc * k * (12 * env.words + 5) for k in plan)
+    print(json.dumps({"what": "world-1 hand-off pass", "plan": plan, "envs": env.n_alloc, "reps": args.reps,
+                      "us_median": times[len(times) // 2], "us_min": times[0], "wire_bytes": wire}))
+
+
+def summarize(d):
+    """Attribute the trace: the dispatches and copies between consecutive spin-gate kernels."""
+    import csv
+    kf = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    mf = glob.glob(os.path.join(d, "**", "*memory_copy_trace.csv"), recursive=True)
+    ev = []
+    for f in kf:
+        for r in csv.DictReader(open(f)):
+            ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "K:" + r["Kernel_Name"][:60]))
+    for f in mf:
+        for r in csv.DictReader(open(f)):
+            ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                       "C:" + r.get("Direction", r.get("Operation", "copy"))))
+    ev.sort()
+    gates = [i for i, e in enumerate(ev) if "sleep" in e[2].lower() or "spin" in e[2].lower()]
+    reps = []
+    for a, b in zip(gates, gates[1:] + [len(ev)]):
+        seg = ev[a + 1:b]
+        if not seg:
+            continue
+        t0 = ev[a][1]
+        items = [{"what": w, "start_us": (s - t0) / 1e3, "dur_us": (e - s) / 1e3} for s, e, w in seg]
+        reps.append({"span_us": (max(e for _, e, _ in seg) - t0) / 1e3, "items": items})
+    out = {"reps": len(reps), "median_rep": sorted(reps, key=lambda r: r["span_us"])[len(reps) // 2] if reps else None}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    p = argparse.ArgumentParser()
+    p.add_argument("--envs", type=int, default=65536)
+    p.add_argument("--plan", default="20")
+    p.add_argument("--reps", type=int, default=20)
+    p.add_argument("--summarize", default=None)
+    a = p.parse_args()
+    if a.summarize:
+        summarize(a.summarize)
+    else:
+        run(a)
