@@ -863,11 +863,7 @@ int pbn_rollout_ex(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offs
   bool pipe = (settle ? net->lds_settle : net->lds_pipe) <= 64 * 1024 && !net->n_gates && (!settle || net->pipe_settle);
   if (net->force_roll) pipe = net->force_roll == 3 && !net->n_gates && (!settle || net->pipe_settle);
   if (pipe) {   // one block of three waves per pair of groups
-#ifdef PBN_DIAG_ONE_GROUP
-    const int64_t pblocks = settle ? (a.n_groups + 1) / 2 : a.n_groups;
-#else
     const int64_t pblocks = (a.n_groups + 1) / 2;
-#endif
     if (settle) {
       a.slot_words = net->slot_words_settle;
       hipLaunchKernelGGL(net->pipe_settle, dim3((unsigned)pblocks), dim3(192), net->lds_settle,

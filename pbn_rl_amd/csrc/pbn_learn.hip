@@ -235,9 +235,7 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
       wfrag<kDH>(wh2, P + a.off[H2_W] + (size_t)h * a.A * kDH, kDH, 16 * (tt - h * at16), a.A, lane);
     }
   };
-#ifndef PBN_DIAG_LATE_WFRAG
   if (wave != 0) fetch_weights();   // (wave 0 loads the rows first: the load counter is in order)
-#endif
   if (tid < kRows) {   // the rows' targets, state words and the list of their set bits
     const int64_t j = row_index(a, b0 + tid);
     stg[tid] = a.tgt[j];
@@ -253,9 +251,7 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
     }
     scnt[tid] = c;
   }
-#ifndef PBN_DIAG_LATE_WFRAG
   if (wave == 0) fetch_weights();
-#endif
   lds_barrier();
   PBN_LSTAMP(0, 1);
   // bilinear layer: y[o] = bias[o] + sum over the set bits i of T[t][i][o] (t = the row's target;
@@ -310,9 +306,6 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
     }
   }
   PBN_LSTAMP(0, 2);
-#ifdef PBN_DIAG_LATE_WFRAG   // (diagnostic: the weights requested after the bilinear layer's table reads)
-  fetch_weights();
-#endif
   lds_barrier();
   PBN_LSTAMP(0, 3);
   if (set == 0) keep = a.h2;

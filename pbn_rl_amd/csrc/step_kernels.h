@@ -1192,12 +1192,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
 #endif
   const int half = lane >> 5;
   const int l32 = lane & 31;
-#ifdef PBN_DIAG_ONE_GROUP
-  // diagnostic build (tools/ab_build.sh): one group per block, the upper half of every wave idle
-  const int64_t g = half ? a.n_groups : (int64_t)blockIdx.x;
-#else
   const int64_t g = (int64_t)blockIdx.x * 2 + half;
-#endif
   const bool valid = g < a.n_groups;
   const int N = a.n_nodes;
   const int64_t n = a.n_envs;
