@@ -450,8 +450,8 @@ def gather_pass(env, plan, world, local, dev, stream, dst, copy_own=False):
     assert ro.offset == env.env_offset and ro.count == env.n_alloc
 
     def run():
-        for k in plan:
-            ro.gather(ro.rollout(k), dst=dst, async_op=True, copy_own=copy_own)
+        for j, k in enumerate(plan):
+            ro.gather(ro.rollout(k), dst=dst, async_op=True, copy_own=copy_own, last=j == len(plan) - 1)
         for works in ro._pending.values():   # the last hand-offs, before the end event
             for w in works:
                 if w is not None:
@@ -749,9 +749,11 @@ def main():
     with_gather = None
     if rollout_mode and not args.no_gather:
         with_gather = {}
-        # the hand-off of launch k overlaps launch k + 1: a one-launch plan (the driver's 20 steps) is
-        # split in two so that there is something to overlap
-        gplan = plan if len(plan) >= 2 else launch_plan(args.steps, max(1, (args.steps + 1) // 2))
+        # the hand-off of launch k overlaps launch k + 1 (a side stream); the last one follows its
+        # launch on the launch stream.  A one-launch plan (the driver's 20 steps) stays one launch:
+        # split in two it paid a second launch's floor for the overlap (68.6 against 59.2 us,
+        # profiles/r05_a_handoff_*.json)
+        gplan = plan
         own = world == 1
         for key, dst, what in (("learner", 0, "point-to-point sends of every shard to rank 0" +
                                               (" (world 1: the learner's own shard copied into its receive slot "

@@ -29,6 +29,8 @@
  *                                                                 pbn_replay_advance)
  *   a frame loop captured once and replayed (no reference counterpart)
  *                                                              -> pbn_step_dev, pbn_q_to_flipmask_dev
+ *   the hand-off of a rollout's transitions to the learner (north_star's per-rollout gather;
+ *   at world 1 the learner's own shard into its receive slot)  -> pbn_copy_async
  *
  * The Python facade (pbn_rl_amd.env.PBNEnv / pbn_rl_amd.vector_env.VectorPBNEnv)
  * keeps that gym surface and calls these entry points through ctypes;
@@ -67,7 +69,7 @@
 extern "C" {
 #endif
 
-#define PBN_ABI_VERSION 6
+#define PBN_ABI_VERSION 7
 
 #define PBN_MAX_NODES 128
 #define PBN_MAX_ARITY 4
@@ -471,6 +473,15 @@ int pbn_bdq_learn(const pbn_net* net, int64_t batch, const int64_t* d_idx, int64
                   float* d_adam_step, float lr, float beta1, float beta2, float eps, float gamma, float grad_clamp,
                   float slope, void* d_workspace, int64_t workspace_bytes, float* d_loss, float* d_grad,
                   void* stream);
+
+/*
+ * pbn_copy_async (ABI 7): d_dst[0 .. bytes) <- d_src[0 .. bytes), device to device on `stream`:
+ * one kernel of 16-byte non-temporal loads and stores (the world-1 hand-off of a rollout's
+ * transition records, pbn_rl_amd/distributed.py; hipMemcpyAsync's blit ran 22 MB at 3.9 TB/s,
+ * profiles/r05_a_handoff_summary.json).  Both pointers and `bytes` 16-byte aligned; the ranges
+ * must not overlap.
+ */
+int pbn_copy_async(void* d_dst, const void* d_src, int64_t bytes, void* stream);
 
 const char* pbn_last_error(void);
 int pbn_abi_version(void);

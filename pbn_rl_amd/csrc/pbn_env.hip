@@ -296,6 +296,45 @@ int pbn_state_histogram(const uint32_t* d_states, int64_t n_rows, int64_t n_cols
 }
 int pbn_abi_version(void) { return PBN_ABI_VERSION; }
 
+// pbn_copy_async: a grid-stride copy in 16-byte non-temporal vectors (the records are read once and
+// go to the learner: neither side should displace the rollout's table image from L2), four
+// independent vectors in flight per thread
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(256) pbn_copy_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ src,
+                                                       int64_t n16) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(src + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(v[u], dst + i + u * stride);
+  }
+  for (; i < n16; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+
+int pbn_copy_async(void* d_dst, const void* d_src, int64_t bytes, void* stream) {
+  if (bytes < 0) return fail(PBN_EINVAL, "bytes < 0");
+  if (bytes == 0) return PBN_OK;
+  if (!d_dst || !d_src) return fail(PBN_EINVAL, "null buffer");
+  if ((bytes & 15) || ((uintptr_t)d_dst & 15u) || ((uintptr_t)d_src & 15u))
+    return fail(PBN_EINVAL, "pointers and bytes must be 16-byte aligned");
+  const char* d = static_cast<const char*>(d_dst);
+  const char* s = static_cast<const char*>(d_src);
+  if (d < s + bytes && s < d + bytes) return fail(PBN_EINVAL, "overlapping ranges");
+  const int64_t n16 = bytes / 16;
+  int dev = 0, n_cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n_cus, hipDeviceAttributeMultiprocessorCount, dev);
+  // enough blocks to fill every CU several times over, each thread moving 4 vectors per trip
+  const int64_t want = (n16 + 4 * 256 - 1) / (4 * 256);
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)n_cus * 8));
+  hipLaunchKernelGGL(pbn_copy_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, static_cast<u32x4*>(d_dst),
+                     static_cast<const u32x4*>(d_src), n16);
+  HIP_OK(hipGetLastError());
+  return PBN_OK;
+}
+
 int pbn_net_words(const pbn_net* net) { return net ? net->W : PBN_EINVAL; }
 
 int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {

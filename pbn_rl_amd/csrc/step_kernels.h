@@ -1836,6 +1836,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
 // plus the ended step's attractor id, flags, length and final state for the env wave's epilogue.
 // Results are bit-identical to pbn_step_wave's settle variants and to oracle/pbn_oracle.c.
 constexpr uint32_t kNoUpd = 0xFFFFFFFFu;
+constexpr uint32_t kSettleStampIt = 300;   // stamps build: the iteration the settle kernel clocks
 
 // The per-env update plan of pbn_rollout_settle, in that env's lane of every wave (VGPRs; the
 // same values in all three waves).  P = R(i-1), the update the RNG waves produced in the previous
@@ -1936,6 +1937,7 @@ pbn_rollout_settle(StepArgs a) {
     EnvPlan p;
     for (uint32_t it = 0;; ++it) {
       asm volatile("" : "+s"(u_k0), "+s"(u_k1));
+      PBN_PSTAMP(it - kSettleStampIt + 10, 0);
       const uint32_t* cin = ctl + ((it + 1) & 1) * 128;
       const uint32_t Ct = cin[lane], Ck = cin[64 + lane];
       // -- the epilogue of the step the state wave ended in iteration i-1 (step t_prev)
@@ -1974,6 +1976,7 @@ pbn_rollout_settle(StepArgs a) {
           for (int w = 0; w < W; ++w) LANE_STV(a.obs, ((t + 1) * plane + (size_t)w * n) + (size_t)le, (size_t)n_steps * plane, 7, st[w]);
         }
       }
+      PBN_PSTAMP_AT(it - kSettleStampIt + 10, 16);
       if (__ballot(Ct < n_steps) == 0 || (uint64_t)it > max_it) break;
       p.next(Ct, Ck, K);
       const uint32_t t = p.Rt, k = p.Rk;
@@ -2066,6 +2069,7 @@ pbn_rollout_settle(StepArgs a) {
 #pragma unroll
         for (int w = 0; w < W; ++w) pk = pk || gam[w] != 0;
       }
+      PBN_PSTAMP_AT(it - kSettleStampIt + 10, 17);
       // -- the state wave's bit planes: flip and perturbation masks, the reset states
 #pragma unroll
       for (int w = 0; w < W; ++w) {
@@ -2085,7 +2089,9 @@ pbn_rollout_settle(StepArgs a) {
       }
       proc_prev = p.v && p.Pt < n_steps;   // what the state wave applies in this iteration
       t_prev = p.Pt;
+      PBN_PSTAMP(it - kSettleStampIt + 10, 1);
       lds_barrier();
+      PBN_PSTAMP(it - kSettleStampIt + 10, 2);
       p.done();
     }
     if (valid) {
@@ -2098,6 +2104,7 @@ pbn_rollout_settle(StepArgs a) {
     // ---- selection planes of each env's update R(i), env `lane`
     EnvPlan p;
     for (uint32_t it = 0;; ++it) {
+      PBN_PSTAMP(it - kSettleStampIt + 10, 0);
       const uint32_t* cin = ctl + ((it + 1) & 1) * 128;
       const uint32_t Ct = cin[lane], Ck = cin[64 + lane];
       if (__ballot(Ct < n_steps) == 0 || (uint64_t)it > max_it) break;
@@ -2113,6 +2120,7 @@ pbn_rollout_settle(StepArgs a) {
       for (int r = 0; r < W; ++r) {
         uint32_t U[16];
         settle_sel_words(ge_lo, ge_hi, st_lo, k, r, N, u_k0, u_k1, U);
+        PBN_PSTAMP_AT(it - kSettleStampIt + 10, 18);
 #pragma unroll
         for (int q = 0; q < kNodeRecs - 1; ++q) {
           if (q < lq) {
@@ -2121,7 +2129,9 @@ pbn_rollout_settle(StepArgs a) {
           }
         }
       }
+      PBN_PSTAMP(it - kSettleStampIt + 10, 1);
       lds_barrier();
+      PBN_PSTAMP(it - kSettleStampIt + 10, 2);
       p.done();
     }
   } else {
@@ -2133,6 +2143,7 @@ pbn_rollout_settle(StepArgs a) {
     bool pacc = false;
     EnvPlan p;
     for (uint32_t it = 0;; ++it) {
+      PBN_PSTAMP(it - kSettleStampIt + 10, 0);
       if (__ballot(Ct < n_steps) == 0 || (uint64_t)it > max_it) break;
       p.next(Ct, Ck, K);
       const bool proc = p.v && p.Pt < n_steps;
@@ -2148,6 +2159,7 @@ pbn_rollout_settle(StepArgs a) {
         s1[w] = pbn::bfi3(RMh, slot[kRP + w * 64 + lane], planes[w]) ^ slot[w * 64 + lane];
         Sg[32 * w + l32] = s1[w];
       }
+      PBN_PSTAMP_AT(it - kSettleStampIt + 10, 15);
       __builtin_amdgcn_wave_barrier();
       uint32_t X[W];
 #pragma unroll
@@ -2164,6 +2176,7 @@ pbn_rollout_settle(StepArgs a) {
           default: X[r] = chain_padded<4, (W <= 2)>(rc, sel, 32 * W, Sg, lti, 64 * W); break;
         }
       }
+      PBN_PSTAMP_AT(it - kSettleStampIt + 10, 3);
       uint32_t cur[W];
 #pragma unroll
       for (int w = 0; w < W; ++w) {
@@ -2172,6 +2185,7 @@ pbn_rollout_settle(StepArgs a) {
         planes[w] = pbn::bfi3(PRh, xp, planes[w]);
         cur[w] = lane_transpose32(planes[w], lane);
       }
+      PBN_PSTAMP_AT(it - kSettleStampIt + 10, 12);
       const int att = attractor_lookup<W>(a, htab, cur);
       const bool open = att < 0;
       const bool pkl = (PKh >> l32) & 1u;
@@ -2191,7 +2205,9 @@ pbn_rollout_settle(StepArgs a) {
 #pragma unroll
         for (int w = 0; w < W; ++w) eo[(2 + w) * 64 + lane] = cur[w];
       }
+      PBN_PSTAMP(it - kSettleStampIt + 10, 1);
       lds_barrier();
+      PBN_PSTAMP(it - kSettleStampIt + 10, 2);
       p.done();
     }
   }

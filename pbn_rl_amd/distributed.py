@@ -168,7 +168,7 @@ class ShardedRollout:
         return rec
 
     def gather(self, rec: TransitionRecords, dst: Optional[int] = None, async_op: bool = False,
-               copy_own: bool = False):
+               copy_own: bool = False, last: bool = False):
         """Hand the records of one rollout to the learner.
 
         dst = None: ``all_gather_into_tensor``; every rank receives every rank's records
@@ -178,6 +178,10 @@ class ShardedRollout:
         empty list).  Returns the list of per-rank records (valid until ``buffers`` further
         gathers of this shape and form) or, with async_op, (records, work): the records are
         readable on the current stream after ``work.wait()``.
+
+        ``last``: nothing follows this hand-off to overlap with, so the own-shard copy is issued on
+        the current stream (no cross-stream wait: the side stream's wait on the rollout's event
+        cost ~11 us of idle device time per hand-off, profiles/r05_a_handoff_summary.json).
         """
         if (dst is None or not copy_own) and not dist.is_initialized():
             # one process without a process group: its records are the whole batch
@@ -209,7 +213,7 @@ class ShardedRollout:
                                   dist.get_global_rank(self.group, r) if self.group is not None else r, self.group)
                        for r in range(self.world) if r != dst]
                 if copy_own:
-                    works.append(self._copy_async(out[dst * nbytes:(dst + 1) * nbytes], rec.flat))
+                    works.append(self._copy_async(out[dst * nbytes:(dst + 1) * nbytes], rec.flat, same_stream=last))
                 parts = [rec if (r == dst and not copy_own) else
                          TransitionRecords(rec.steps, rec.words, rec.n, flat=out[r * nbytes:(r + 1) * nbytes])
                          for r in range(self.world)]
@@ -227,16 +231,24 @@ class ShardedRollout:
         _wait(work)
         return parts
 
-    def _copy_async(self, out: torch.Tensor, src: torch.Tensor):
-        """out <- src on a side stream ordered after the current stream's work so far; the
-        returned work's wait() orders the current stream after the copy (as a collective's)."""
+    def _copy_async(self, out: torch.Tensor, src: torch.Tensor, same_stream: bool = False):
+        """out <- src (pbn_copy_async: 16-byte non-temporal vectors) on a side stream ordered after
+        the current stream's work so far, so that it overlaps the next rollout; the returned
+        work's wait() orders the current stream after the copy (as a collective's).  With
+        ``same_stream`` the copy simply follows on the current stream (nothing to wait for)."""
+        if not src.is_cuda:   # (gloo on the CPU: a plain copy)
+            out.copy_(src)
+            return None
         cur = torch.cuda.current_stream(src.device)
+        if same_stream:
+            _device_copy(out, src, cur)
+            return None
         side = getattr(self, "_side", None)
         if side is None:
             side = self._side = torch.cuda.Stream(device=src.device)
         side.wait_stream(cur)
         with torch.cuda.stream(side):
-            out.copy_(src, non_blocking=True)
+            _device_copy(out, src, side)
             done = torch.cuda.Event()
             done.record(side)
         return _StreamWork(done, src.device)
@@ -251,7 +263,7 @@ class ShardedRollout:
         prev = None
         for k in range(n_rollouts):
             rec = self.rollout(steps, random_actions=random_actions)
-            parts, work = self.gather(rec, dst=dst, async_op=True, copy_own=copy_own)
+            parts, work = self.gather(rec, dst=dst, async_op=True, copy_own=copy_own, last=k == n_rollouts - 1)
             if self.buffers < 2:
                 _finish((k, parts, work), consume)
                 continue
@@ -267,12 +279,20 @@ class ShardedRollout:
         return {name: torch.cat([p[name] for p in parts], dim=-1) for name, _, _ in _FIELDS}
 
 
+def _device_copy(out: torch.Tensor, src: torch.Tensor, stream) -> None:
+    """out <- src, both contiguous uint8 device buffers: libpbn_env's pbn_copy_async on ``stream``
+    (the record buffers are 16-byte multiples: (12W + 5) B x T x n, n a multiple of 32)."""
+    from . import _lib
+    _lib.check(_lib.load().pbn_copy_async(out.data_ptr(), src.data_ptr(), out.numel(), stream.cuda_stream),
+               "pbn_copy_async")
+
+
 class _Works:
     """The works of one hand-off, waited together, at most once (a second wait on a finished
     gloo receive blocks)."""
 
     def __init__(self, works):
-        self.works = list(works or [])
+        self.works = [w for w in (works or []) if w is not None]
 
     def wait(self):
         works, self.works = self.works, []

@@ -39,11 +39,16 @@ def _worker(rank, world, port, n_total, steps, result_path, form="all"):
     spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.05)
     ro = ShardedRollout(n_total, lambda off, cnt: OracleVectorEnv(spec, off, cnt, seed=11),
                         buffers=1 if form == "run1" else 2)
-    if form in ("run", "run1"):
-        # three rollouts, each hand-off to rank 0 overlapped with the next rollout
+    if form in ("run", "run1", "run_own"):
+        # three rollouts, each hand-off to rank 0 overlapped with the next rollout ("run_own": rank 0
+        # also copies its own shard into its receive slot, bench.py's value_with_gather form)
         got = {}
-        ro.run(3, steps, dst=0, consume=lambda k, parts: got.__setitem__(
-            k, {n: v.clone() for n, v in ShardedRollout.to_global(parts).items()}))
+
+        def consume(k, parts):
+            if form == "run_own":
+                assert all(p.flat.data_ptr() != ro._ring[steps][k % 2].flat.data_ptr() for p in parts)
+            got[k] = {n: v.clone() for n, v in ShardedRollout.to_global(parts).items()}
+        ro.run(3, steps, dst=0, consume=consume, copy_own=form == "run_own")
         if rank == 0:
             torch.save(got, result_path)
         else:
@@ -94,7 +99,7 @@ def test_record_wire_format():
         TransitionRecords(1, 1, 48)
 
 
-@pytest.mark.parametrize("form", ["run", "run1"])
+@pytest.mark.parametrize("form", ["run", "run1", "run_own"])
 def test_two_rank_overlapped_run_equals_single_run(tmp_path, form):
     """ShardedRollout.run: three rollouts with the hand-off of rollout k to rank 0 in flight
     while rollout k + 1 runs (two record slots; "run1": one slot, each rollout consumed before

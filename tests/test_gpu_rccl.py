@@ -100,3 +100,53 @@ def test_rccl_config4_shard_at_size(rccl_world1):
         for name in ("obs", "flipmask", "final_state", "flags"):
             assert torch.equal(seen[k][name], want[name]), (k, name)
         assert np.array_equal(seen[k]["reward"].numpy().view(np.uint32), want["reward"].numpy().view(np.uint32))
+
+
+def test_world1_own_shard_handoff_copies_records():
+    """bench.py's value_with_gather hand-off at world 1 (no process group): the learner's own shard
+    copied into its receive slot by pbn_copy_async, on the side stream (overlapping the next
+    rollout) or, for the last hand-off of a run, on the launch stream.  Three overlapped rollouts;
+    every received slot equals the records the kernel wrote, and the oracle."""
+    from pbn_rl_amd.distributed import ShardedRollout
+    spec = _spec()
+    n, steps = 4096, 5
+    ro = ShardedRollout(n, _factory(spec, 3))
+    seen = []
+
+    def consume(k, parts):
+        assert len(parts) == 1 and parts[0].flat.data_ptr() != ro._ring[steps][k % 2].flat.data_ptr()
+        seen.append({f: v.cpu().clone() for f, v in ShardedRollout.to_global(parts).items()})
+        seen[-1]["_src"] = ro._ring[steps][k % 2].flat.cpu().clone()
+        seen[-1]["_dst"] = parts[0].flat.cpu().clone()
+
+    ro.run(3, steps, dst=0, consume=consume, copy_own=True)
+    torch.cuda.synchronize()
+    assert len(seen) == 3
+    for k in range(3):
+        assert torch.equal(seen[k]["_src"], seen[k]["_dst"]), k
+    from tests.oracle_env import OracleVectorEnv
+    ref = OracleVectorEnv(spec, 0, n, seed=3)
+    for k in range(3):
+        want = ref.rollout(steps)
+        for name in ("obs", "flipmask", "final_state", "flags"):
+            assert torch.equal(seen[k][name], want[name]), (k, name)
+
+
+def test_copy_async_entry_point():
+    """pbn_copy_async: ragged sizes (every 16-byte multiple up to a few vectors past the grid's
+    stride loop), offsets into a buffer, and its argument checks."""
+    import ctypes
+    from pbn_rl_amd import _lib
+    L = _lib.load()
+    src = torch.randint(0, 256, (1 << 22,), dtype=torch.uint8, device="cuda")
+    for nbytes in (16, 4096 + 48, (1 << 22) - 16 * 7):
+        dst = torch.zeros(1 << 22, dtype=torch.uint8, device="cuda")
+        _lib.check(L.pbn_copy_async(dst.data_ptr() + 16, src.data_ptr(), nbytes, None), "copy")
+        torch.cuda.synchronize()
+        assert torch.equal(dst[16:16 + nbytes], src[:nbytes]) and not dst[:16].any()
+        assert not dst[16 + nbytes:].any()
+    assert L.pbn_copy_async(src.data_ptr(), src.data_ptr() + 8, 16, None) != 0      # misaligned
+    assert L.pbn_copy_async(src.data_ptr() + 16, src.data_ptr(), 64, None) != 0     # overlapping
+    assert L.pbn_copy_async(None, src.data_ptr(), 16, None) != 0
+    assert L.pbn_copy_async(src.data_ptr(), src.data_ptr(), 0, None) == 0
+    del ctypes

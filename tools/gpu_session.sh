@@ -15,6 +15,7 @@
 #   bdq-learn        BDQ training frames at 32,768 envs (+ kernel trace)
 #   stamps           the pipelined kernel's per-role segment clocks at iteration 10 (diagnostic build
 #                    pbn_rl_amd/libpbn_env_stamps.so: tools/stamps.py --build), 20- and 100-step launches
+#   sstamps          the settle kernel's per-role segment clocks (stamps build; tools/stamps.py --settle 64)
 #   qstamps          config 5's Q-network launch per-phase clocks (stamps build; tools/qnet_stamps.py)
 #   lstamps          the fused learner update's per-phase clocks (stamps build; tools/learn_stamps.py)
 #   settle           the driver's command (with its settle_law and hand-off fields) and config 2 under the
@@ -81,6 +82,12 @@ for step in "$@"; do
           || fail "stamps T$T"
       done
       echo "stamps done" ;;
+    sstamps)
+      for T in 20 100; do
+        timeout -k 10 120 python tools/stamps.py --settle 64 --rollout $T > "$out/settle_stamps_T$T.json" \
+          2> "$out/settle_stamps_T$T.err" || fail "sstamps T$T"
+      done
+      echo "sstamps done" ;;
     qstamps)
       timeout -k 10 180 python tools/qnet_stamps.py > "$out/qstamps.json" 2> "$out/qstamps.err" || fail qstamps
       echo "qstamps done" ;;

@@ -50,6 +50,31 @@ def segments(full, it):
     return out
 
 
+SETTLE_ROLES = {
+    "state": [("slot reads, reset / flip planes, S store", 0, 15), ("gathers + mux chains", 15, 3),
+              ("perturb / proc select + back-transpose", 3, 12), ("hash, decision, C / end-info writes", 12, 1),
+              ("barrier wait", 1, 2)],
+    "env draws": [("epilogues of the steps ended last iteration", 4, 16), ("ENV / SETTLE_ENV call, step draws, gaps", 16, 17),
+                  ("flip / perturbation / reset planes, slot writes", 17, 5), ("barrier wait", 5, 6)],
+    "selection": [("SETTLE_SEL Philox calls (4 per env)", 8, 18), ("env-major compares, transposes, slot writes", 18, 9),
+                  ("barrier wait", 9, 10)],
+}
+
+
+def settle_segments(full, it):
+    """pbn_rollout_settle's per-role segments of iteration kSettleStampIt (step_kernels.h)."""
+    import numpy as np
+    med = lambda x: int(np.median(x))
+    c = lambda i: full[:, i]
+    out = {"iteration_median": med(it)}
+    for role, segs in SETTLE_ROLES.items():
+        ok = np.all([(c(a) > 0) & (c(b) > 0) for _, a, b in segs], axis=0)
+        rows = {name: {"cycles": med(c(b)[ok] - c(a)[ok]), "share": round(med(c(b)[ok] - c(a)[ok]) / max(med(it), 1), 3)}
+                for name, a, b in segs}
+        out[role] = {"segments": rows, "blocks": int(ok.sum())}
+    return out
+
+
 def placement(full, it):
     """Where the pipelined kernel's waves ran (HW_ID/XCC_ID words the stamps build stores at
     kernel start: role 0 in column 14, roles 1, 2 in columns 7, 11): the role mix per SIMD and the
@@ -114,6 +139,9 @@ def main():
     ap.add_argument("--pipe", action="store_true", help="pipelined rollout kernel: per-role clocks of iteration 10")
     ap.add_argument("--plane", action="store_true", help="plane-resident rollout kernel (4 roles; implies --pipe)")
     ap.add_argument("--lib", default=STAMP_LIB, help="a stamps build (default: the one --build makes)")
+    ap.add_argument("--settle", type=int, default=0,
+                    help="the settle law with this cap (pbn_rollout_settle; implies --pipe): per-role segments of "
+                         "iteration kSettleStampIt")
     ap.add_argument("--rollout", type=int, default=0,
                     help="stamp a pbn_rollout launch of this many steps (phases of its last step)")
     args = ap.parse_args()
@@ -135,7 +163,9 @@ def main():
 
     L = _lib.load()
     L.pbn_debug_set_stamps.argtypes = [ctypes.c_void_p]
-    spec = EnvSpec(load_network(args.network), load_attractors(args.network))
+    if args.settle:
+        args.pipe = True
+    spec = EnvSpec(load_network(args.network), load_attractors(args.network), settle=args.settle)
     env = VectorPBNEnv(spec, args.envs, seed=1, keep_final_state=False)
     env.reset()
     waves = env.n_alloc // 32
@@ -165,6 +195,14 @@ def main():
                          "barrier_wait_median": int(np.median(wait))}
         full = buf.view(-1, ROW)[:waves].cpu().numpy().astype(np.int64)
         st0 = full[:, 0]
+        if args.settle:
+            ok = (t[:, :, 2] > 0).all(axis=1)
+            it = t[ok][:, :, 2].max(axis=1) - t[ok][:, :, 0].min(axis=1)
+            rep["settle_max"] = args.settle
+            rep["iteration_median"] = int(np.median(it))
+            rep["critical_path"] = settle_segments(full[ok], it)
+            print(json.dumps(rep, indent=1))
+            return
         if args.plane:
             it = t[:, :, 2].max(axis=1) - t[:, :, 0].min(axis=1)
             rep["iteration_median"] = int(np.median(it))
