@@ -1821,19 +1821,19 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
 // and every env runs its own sequence of updates: the settle law keys each update's selection per
 // env (SETTLE_SEL call (k << 8 | i >> 3) of env e; DESIGN.md "Step law"), so an env that settles
 // starts its next step while the other envs of its 32-env word are still updating.
-//   wave 1 (env draws, lane = env): the epilogue of the step that ended in the previous iteration
-//     (reward, flags, final state, update count, the autoreset decision, next obs), then the
-//     update's draws: k = 0 the ENV call (actions, the step's autoreset draws, gaps 0-2), k >= 1
-//     the SETTLE_ENV call (gaps); flip, perturbation and reset masks transposed to bit planes;
+//   wave 1 (env draws, lane = env): the update's draws: k = 0 the ENV call (actions, the step's
+//     autoreset draws, gaps 0-2), k >= 1 the SETTLE_ENV call (gaps), one call per lane with a
+//     per-lane counter; flip mask, perturbation mask (and at k = 0 the reset state, target and
+//     action count) to the slot, env-major;
 //   wave 2 (selection, lane = env): the env's SETTLE_SEL words of its update, compared with the
-//     thresholds env-major (one compare and one add-with-carry per node and threshold), then
-//     transposed to the (u < c_j) bit planes of every node;
-//   wave 0 (state): keeps the 32 envs of a word bit-sliced across updates (lane = node): applies
-//     the update to the envs whose update is valid (a proc mask), back-transposes once per update
-//     for the attractor lookup and decides, per env, to continue or to end the step.
+//     thresholds env-major (a subtract and a v_alignbit per node and threshold), transposed to
+//     the (u < c_j) bit planes of every node;
+//   wave 0 (state): the update of every env whose update is valid (s1 = s ^ m, bit-slice, node
+//     chains, back-transpose, perturbed envs s1 ^ gamma), the attractor lookup, the per-env
+//     decision to continue or end the step, and the step's epilogue (reward, flags, s', update
+//     count, autoreset, next obs) in the iteration that ends it.
 // Iteration i: the RNG waves produce each env's update R(i) into slot i & 1 while the state wave
-// applies R(i-1) (EnvPlan).  The state wave publishes each env's decision C (next update) in LDS,
-// plus the ended step's attractor id, flags, length and final state for the env wave's epilogue.
+// applies R(i-1) (EnvPlan); the state wave publishes each env's decision C (next update) in LDS.
 // Results are bit-identical to pbn_step_wave's settle variants and to oracle/pbn_oracle.c.
 constexpr uint32_t kNoUpd = 0xFFFFFFFFu;
 constexpr uint32_t kSettleStampIt = 300;   // stamps build: the iteration the settle kernel clocks
@@ -1842,18 +1842,17 @@ constexpr uint32_t kSettleStampIt = 300;   // stamps build: the iteration the se
 // same values in all three waves).  P = R(i-1), the update the RNG waves produced in the previous
 // iteration (kNoUpd: none); C = the next update the env needs, the state wave's decision in
 // iteration i-1; R = R(i), the update produced in iteration i.  R(i-1) is applied in iteration i
-// iff it equals C.  A valid R(i-1) continues speculatively as (t, k+1) while k+1 < K (dropped if
-// the state wave finds the env settled: one idle iteration per step that ends before the cap);
-// otherwise C is re-issued.  A step's first update is therefore always produced once its previous
-// step's end is known, i.e. with that end's autoreset decision.
+// iff it equals C.  A valid R(i-1) = (t, k) continues speculatively as (t, k+1), or (t+1, 0) at
+// the cap; when the state wave finds the env settled the speculation is dropped and C re-issued
+// (one idle iteration per step that ends before the cap).
 struct EnvPlan {
   uint32_t Pt = kNoUpd, Pk = 0, Rt = 0, Rk = 0;
   bool v = false;
   __device__ __forceinline__ void next(uint32_t Ct, uint32_t Ck, uint32_t K) {
     v = Pt == Ct && Pk == Ck;
-    const bool cont = v && Pk + 1 < K;
-    Rt = cont ? Pt : (v ? kNoUpd : Ct);
-    Rk = cont ? Pk + 1 : Ck;
+    const bool cap = Pk + 1 >= K;
+    Rt = v ? (cap ? Pt + 1 : Pt) : Ct;
+    Rk = v ? (cap ? 0u : Pk + 1) : Ck;
   }
   __device__ __forceinline__ void done() { Pt = Rt; Pk = Rk; }
 };
@@ -1886,13 +1885,11 @@ pbn_rollout_settle(StepArgs a) {
   const uint4* selq = reinterpret_cast<const uint4*>(L + a.sel_off);
   const uint4* recL = reinterpret_cast<const uint4*>(L + a.nrec_off);
   uint32_t* Sg = smem + a.tab_words + half * 32 * W;
-  // slot (per iteration parity): flip planes [W][64] | perturbation planes [W][64] | reset-state
-  // planes [W][64] | selection planes [lq][2][32W] | {perturbed, reset} env masks per half [4]
+  // slot (per iteration parity), env-major [.][64]: flip mask [W] | perturbation mask [W] | k = 0:
+  // reset state [W] | k = 0: {reset target, action count} | selection planes [lq][2][32W]
   uint32_t* slots = smem + a.tab_words + 2 * 32 * W;
-  constexpr int kGP = 64 * W, kRP = 128 * W, kLT = 192 * W;
-  const int kMK = kLT + lq * 64 * W;
+  constexpr int kGP = 64 * W, kRS = 128 * W, kIN = 192 * W, kLT = 192 * W + 64;
   uint32_t* ctl = slots + 2 * (size_t)a.slot_words;   // [parity][t, k][64]: C per env
-  uint32_t* einfo = ctl + 256;                        // [parity][2 + W][64]: the ended step's results
   if (threadIdx.x < 64) {   // C before iteration 0: (0, 0); envs of groups past the end: finished
     ctl[128 + threadIdx.x] = valid ? 0u : n_steps;
     ctl[192 + threadIdx.x] = 0u;
@@ -1901,13 +1898,11 @@ pbn_rollout_settle(StepArgs a) {
   uint32_t tt0 = 0, tg0 = 0;
 #pragma unroll
   for (int w = 0; w < W; ++w) st[w] = 0;
-  if (role != 2 && valid) {
+  if (role == 0 && valid) {
 #pragma unroll
     for (int w = 0; w < W; ++w) st[w] = a.state[CK((size_t)w * n + le, plane, 1)];
-    if (role == 1) {
-      tt0 = a.t[CK(le, n, 2)];
-      tg0 = a.target[CK(le, n, 3)];
-    }
+    tt0 = a.t[CK(le, n, 2)];
+    tg0 = a.target[CK(le, n, 3)];
   }
   copy_image(L, a);
 #pragma unroll
@@ -1924,67 +1919,21 @@ pbn_rollout_settle(StepArgs a) {
 
   // one loop per role; every role derives the same plans and loop exit from the same C values
   if (role == 1) {
-    // ---- env draws and step epilogues, env `lane`
-    uint32_t rs[W];        // the autoreset state drawn at the current step's first update
-    uint32_t rtv = 0, pcv = 0, t_prev = 0;
-    bool proc_prev = false;
-#pragma unroll
-    for (int w = 0; w < W; ++w) rs[w] = 0;
-    if (valid && (u_fl & 1u)) {
-#pragma unroll
-      for (int w = 0; w < W; ++w) LANE_STV(a.obs, (size_t)w * n + (size_t)le, (size_t)n_steps * plane, 7, st[w]);
-    }
+    // ---- the draws of each env's update R(i), env `lane`
     EnvPlan p;
     for (uint32_t it = 0;; ++it) {
       asm volatile("" : "+s"(u_k0), "+s"(u_k1));
       PBN_PSTAMP(it - kSettleStampIt + 10, 0);
       const uint32_t* cin = ctl + ((it + 1) & 1) * 128;
       const uint32_t Ct = cin[lane], Ck = cin[64 + lane];
-      // -- the epilogue of the step the state wave ended in iteration i-1 (step t_prev)
-      bool rst = false;
-      if (proc_prev && Ck == 0) {
-        const uint32_t* ei = einfo + ((it + 1) & 1) * (2 + W) * 64;
-        const uint32_t e0 = ei[lane], nupd = ei[64 + lane];
-        uint32_t cur[W];
-#pragma unroll
-        for (int w = 0; w < W; ++w) cur[w] = ei[(2 + w) * 64 + lane];
-        const size_t t = t_prev;
-        if (u_fl & 2u) {
-#pragma unroll
-          for (int w = 0; w < W; ++w) LANE_STV(a.final_state, (t * plane + (size_t)w * n) + (size_t)le, (size_t)n_steps * plane, 10, cur[w]);
-        }
-        if (u_fl & 32u) LANE_STV(a.updates, (t * n) + (size_t)le, (size_t)n_steps * n, 23, (uint16_t)min(nupd, 0xFFFFu));
-        const int att = (int)(e0 & 0xFFFFu) - 1;
-        const bool in_attr = att >= 0;
-        const bool term = in_attr && (uint32_t)att == tg0;
-        const bool wrong = in_attr && !term;
-        int tt = (int)tt0 + 1;
-        tt = tt > 255 ? 255 : tt;
-        const bool trunc = a.horizon > 0 && tt >= a.horizon;
-        rst = (u_fl & 8u) && (term || trunc);
-        const uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) |
-                            (((e0 >> 16) & 1u) << 3) | ((uint32_t)rst << 4) | (((e0 >> 17) & 1u) << 5);
-        const float4 r4 = reinterpret_cast<const float4*>(rtab)[pcv];
-        LANE_STV(a.reward, (t * n) + (size_t)le, (size_t)n_steps * n, 11, term ? r4.z : (wrong ? r4.y : r4.x));
-        LANE_STV(a.flags, (t * n) + (size_t)le, (size_t)n_steps * n, 15, (uint8_t)fl);
-        tg0 = rst ? rtv : tg0;
-        tt0 = rst ? 0u : (uint32_t)tt;
-#pragma unroll
-        for (int w = 0; w < W; ++w) st[w] = rst ? rs[w] : cur[w];
-        if ((u_fl & 1u) && t + 1 < n_steps) {
-#pragma unroll
-          for (int w = 0; w < W; ++w) LANE_STV(a.obs, ((t + 1) * plane + (size_t)w * n) + (size_t)le, (size_t)n_steps * plane, 7, st[w]);
-        }
-      }
-      PBN_PSTAMP_AT(it - kSettleStampIt + 10, 16);
       if (__ballot(Ct < n_steps) == 0 || (uint64_t)it > max_it) break;
       p.next(Ct, Ck, K);
       const uint32_t t = p.Rt, k = p.Rk;
       uint32_t* slot = slots + (size_t)(it & 1) * a.slot_words;
+      PBN_PSTAMP_AT(it - kSettleStampIt + 10, 16);
       uint32_t m[W], gam[W];
 #pragma unroll
       for (int w = 0; w < W; ++w) { m[w] = 0; gam[w] = 0; }
-      bool pk = false;
       if (valid && t < n_steps) {
         const uint64_t step = a.step + (uint64_t)t;
         const uint32_t st_lo = (uint32_t)step;
@@ -2000,6 +1949,7 @@ pbn_rollout_settle(StepArgs a) {
           const uint32_t n1 = (uint32_t)(N + 1);
           const uint32_t c_act = ext64(xhi, xlo, n1 * n1 * n1);
           uint64_t xr = ((((uint64_t)E.w) << 32) | E.z) * a.x_mult;
+          uint32_t rs[W], rtv;
           if (a.n_attr >= 1) {
             const int32_t* att_first = reinterpret_cast<const int32_t*>(L + a.att_off);
             const uint32_t* att_words = L + a.att_off + a.n_attr + 1;
@@ -2038,9 +1988,13 @@ pbn_rollout_settle(StepArgs a) {
             for (int w = 0; w < W; ++w)
               m[w] = a.flipmask[CK(((size_t)t * plane + (size_t)w * n) + (size_t)le, (size_t)n_steps * plane, 6)] & valid_word_mask(N, w);
           }
-          pcv = 0;
+          uint32_t pcv = 0;
 #pragma unroll
-          for (int w = 0; w < W; ++w) pcv += __builtin_popcount(m[w]);
+          for (int w = 0; w < W; ++w) {
+            pcv += __builtin_popcount(m[w]);
+            slot[kRS + w * 64 + lane] = rs[w];
+          }
+          slot[kIN + lane] = rtv | (pcv << 8);
         }
         // gaps 0, 1 = words 0, 1; gap 2 = u2 (k = 0) or word 2 (k >= 1); then, rarely, more
         const int g0 = gap_any(a.gap_exact, L, a, E.x), g1 = gap_any(a.gap_exact, L, a, E.y),
@@ -2066,39 +2020,17 @@ pbn_rollout_settle(StepArgs a) {
             set_bit<W>(gam, pos, N);
           }
         }
-#pragma unroll
-        for (int w = 0; w < W; ++w) pk = pk || gam[w] != 0;
       }
       PBN_PSTAMP_AT(it - kSettleStampIt + 10, 17);
-      // -- the state wave's bit planes: flip and perturbation masks, the reset states
 #pragma unroll
       for (int w = 0; w < W; ++w) {
-        slot[w * 64 + lane] = lane_transpose32(m[w], lane);
-        slot[kGP + w * 64 + lane] = lane_transpose32(gam[w], lane);
+        slot[w * 64 + lane] = m[w];
+        slot[kGP + w * 64 + lane] = gam[w];
       }
-      const uint64_t pb = __ballot(pk), rb = __ballot(rst);
-      if (rb) {
-#pragma unroll
-        for (int w = 0; w < W; ++w) slot[kRP + w * 64 + lane] = lane_transpose32(rst ? st[w] : 0u, lane);
-      }
-      if (lane == 0) {
-        slot[kMK + 0] = (uint32_t)pb;
-        slot[kMK + 1] = (uint32_t)(pb >> 32);
-        slot[kMK + 2] = (uint32_t)rb;
-        slot[kMK + 3] = (uint32_t)(rb >> 32);
-      }
-      proc_prev = p.v && p.Pt < n_steps;   // what the state wave applies in this iteration
-      t_prev = p.Pt;
       PBN_PSTAMP(it - kSettleStampIt + 10, 1);
       lds_barrier();
       PBN_PSTAMP(it - kSettleStampIt + 10, 2);
       p.done();
-    }
-    if (valid) {
-#pragma unroll
-      for (int w = 0; w < W; ++w) a.state_out[CK((size_t)w * n + le, plane, 16)] = st[w];
-      a.t[CK(le, n, 17)] = (uint8_t)tt0;
-      a.target[CK(le, n, 18)] = (uint8_t)tg0;
     }
   } else if (role == 2) {
     // ---- selection planes of each env's update R(i), env `lane`
@@ -2135,12 +2067,17 @@ pbn_rollout_settle(StepArgs a) {
       p.done();
     }
   } else {
-    // ---- state: the envs of each word bit-sliced (lane = node l32 + 32w of group `half`)
-    uint32_t planes[W];
-#pragma unroll
-    for (int w = 0; w < W; ++w) planes[w] = lane_transpose32(st[w], lane);
+    // ---- state of env `lane` (env-major), bit-sliced per update for the node chains
+    uint32_t rs[W];           // the autoreset state drawn at the current step's first update
+    uint32_t rtv = 0, pcv = 0;
     uint32_t Ct = valid ? 0u : n_steps, Ck = 0;
     bool pacc = false;
+#pragma unroll
+    for (int w = 0; w < W; ++w) rs[w] = 0;
+    if (valid && (u_fl & 1u)) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) LANE_STV(a.obs, (size_t)w * n + (size_t)le, (size_t)n_steps * plane, 7, st[w]);
+    }
     EnvPlan p;
     for (uint32_t it = 0;; ++it) {
       PBN_PSTAMP(it - kSettleStampIt + 10, 0);
@@ -2150,15 +2087,24 @@ pbn_rollout_settle(StepArgs a) {
       const uint32_t t = p.Pt, k = p.Pk;
       const uint32_t* slot = slots + (size_t)((it + 1) & 1) * a.slot_words;
       const uint32_t* lt_in = slot + kLT + half * 32 * W;
-      const uint32_t PKh = slot[kMK + half], RMh = slot[kMK + 2 + half];
-      const uint64_t prb = __ballot(proc);
-      const uint32_t PRh = half ? (uint32_t)(prb >> 32) : (uint32_t)prb;
-      uint32_t s1[W];
+      uint32_t s1[W], gam[W];
+      bool pk = false;
 #pragma unroll
       for (int w = 0; w < W; ++w) {
-        s1[w] = pbn::bfi3(RMh, slot[kRP + w * 64 + lane], planes[w]) ^ slot[w * 64 + lane];
-        Sg[32 * w + l32] = s1[w];
+        s1[w] = st[w] ^ slot[w * 64 + lane];   // (the flip mask is 0 past an update's first)
+        gam[w] = slot[kGP + w * 64 + lane];
+        pk = pk || gam[w] != 0;
       }
+      if (proc && k == 0) {   // the step's reset draw and action count
+#pragma unroll
+        for (int w = 0; w < W; ++w) rs[w] = slot[kRS + w * 64 + lane];
+        const uint32_t info = slot[kIN + lane];
+        rtv = info & 0xFFu;
+        pcv = (info >> 8) & 0xFFu;
+        pacc = false;
+      }
+#pragma unroll
+      for (int w = 0; w < W; ++w) Sg[32 * w + l32] = lane_transpose32(s1[w], lane);
       PBN_PSTAMP_AT(it - kSettleStampIt + 10, 15);
       __builtin_amdgcn_wave_barrier();
       uint32_t X[W];
@@ -2180,35 +2126,62 @@ pbn_rollout_settle(StepArgs a) {
       uint32_t cur[W];
 #pragma unroll
       for (int w = 0; w < W; ++w) {
-        // perturbed envs: s1 ^ gamma; envs without a valid update keep their state
-        const uint32_t xp = pbn::bfi3(PKh, s1[w] ^ slot[kGP + w * 64 + lane], X[w]);
-        planes[w] = pbn::bfi3(PRh, xp, planes[w]);
-        cur[w] = lane_transpose32(planes[w], lane);
+        const uint32_t x = lane_transpose32(X[w], lane);
+        cur[w] = proc ? (pk ? s1[w] ^ gam[w] : x) : st[w];
       }
       PBN_PSTAMP_AT(it - kSettleStampIt + 10, 12);
       const int att = attractor_lookup<W>(a, htab, cur);
       const bool open = att < 0;
-      const bool pkl = (PKh >> l32) & 1u;
       const bool end = proc && (!open || k + 1 >= K);
       if (proc) {
-        pacc = (k != 0 && pacc) || pkl;
+        pacc = pacc || pk;
         Ct = end ? t + 1 : t;
         Ck = end ? 0u : k + 1;
       }
       uint32_t* cout = ctl + (it & 1) * 128;
       cout[lane] = Ct;
       cout[64 + lane] = Ck;
-      if (end) {
-        uint32_t* eo = einfo + (it & 1) * (2 + W) * 64;
-        eo[lane] = (uint32_t)(att + 1) | ((uint32_t)pacc << 16) | ((uint32_t)open << 17);
-        eo[64 + lane] = k + 1;
 #pragma unroll
-        for (int w = 0; w < W; ++w) eo[(2 + w) * 64 + lane] = cur[w];
+      for (int w = 0; w < W; ++w) st[w] = cur[w];
+      if (end) {
+        // the epilogue of step t
+        const size_t tz = t;
+        if (u_fl & 2u) {
+#pragma unroll
+          for (int w = 0; w < W; ++w) LANE_STV(a.final_state, (tz * plane + (size_t)w * n) + (size_t)le, (size_t)n_steps * plane, 10, cur[w]);
+        }
+        if (u_fl & 32u) LANE_STV(a.updates, (tz * n) + (size_t)le, (size_t)n_steps * n, 23, (uint16_t)min(k + 1, 0xFFFFu));
+        const bool in_attr = att >= 0;
+        const bool term = in_attr && (uint32_t)att == tg0;
+        const bool wrong = in_attr && !term;
+        int tt = (int)tt0 + 1;
+        tt = tt > 255 ? 255 : tt;
+        const bool trunc = a.horizon > 0 && tt >= a.horizon;
+        const bool rst = (u_fl & 8u) && (term || trunc);
+        const uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) |
+                            ((uint32_t)pacc << 3) | ((uint32_t)rst << 4) | ((uint32_t)open << 5);
+        const float4 r4 = reinterpret_cast<const float4*>(rtab)[pcv];
+        LANE_STV(a.reward, (tz * n) + (size_t)le, (size_t)n_steps * n, 11, term ? r4.z : (wrong ? r4.y : r4.x));
+        LANE_STV(a.flags, (tz * n) + (size_t)le, (size_t)n_steps * n, 15, (uint8_t)fl);
+        tg0 = rst ? rtv : tg0;
+        tt0 = rst ? 0u : (uint32_t)tt;
+#pragma unroll
+        for (int w = 0; w < W; ++w) st[w] = rst ? rs[w] : cur[w];
+        if ((u_fl & 1u) && tz + 1 < n_steps) {
+#pragma unroll
+          for (int w = 0; w < W; ++w) LANE_STV(a.obs, ((tz + 1) * plane + (size_t)w * n) + (size_t)le, (size_t)n_steps * plane, 7, st[w]);
+        }
       }
       PBN_PSTAMP(it - kSettleStampIt + 10, 1);
       lds_barrier();
       PBN_PSTAMP(it - kSettleStampIt + 10, 2);
       p.done();
+    }
+    if (valid) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) a.state_out[CK((size_t)w * n + le, plane, 16)] = st[w];
+      a.t[CK(le, n, 17)] = (uint8_t)tt0;
+      a.target[CK(le, n, 18)] = (uint8_t)tg0;
     }
   }
 }
