@@ -1889,11 +1889,9 @@ pbn_rollout_settle(StepArgs a) {
   // reset state [W] | k = 0: {reset target, action count} | selection planes [lq][2][32W]
   uint32_t* slots = smem + a.tab_words + 2 * 32 * W;
   constexpr int kGP = 64 * W, kRS = 128 * W, kIN = 192 * W, kLT = 192 * W + 64;
-  uint32_t* ctl = slots + 2 * (size_t)a.slot_words;   // [parity][t, k][64]: C per env
-  if (threadIdx.x < 64) {   // C before iteration 0: (0, 0); envs of groups past the end: finished
-    ctl[128 + threadIdx.x] = valid ? 0u : n_steps;
-    ctl[192 + threadIdx.x] = 0u;
-  }
+  uint2* ctl = reinterpret_cast<uint2*>(slots + 2 * (size_t)a.slot_words);   // [parity][64]{t, k}: C per env
+  if (threadIdx.x < 64) ctl[64 + threadIdx.x] = make_uint2(valid ? 0u : n_steps, 0u);   // C before iteration 0:
+                                                         // (0, 0); envs of groups past the end: finished
   uint32_t st[W];
   uint32_t tt0 = 0, tg0 = 0;
 #pragma unroll
@@ -1918,16 +1916,115 @@ pbn_rollout_settle(StepArgs a) {
   const uint32_t ge_lo = (uint32_t)ge;
 
   // one loop per role; every role derives the same plans and loop exit from the same C values
-  if (role == 1) {
-    // ---- the draws of each env's update R(i), env `lane`
+  // (the env draws' fast path: random actions, the gap bucket table, two or more single-state
+  // attractors and N <= 31 for single-word states -- every kaban network -- branch-free)
+  const bool env_fast = __builtin_amdgcn_readfirstlane((u_fl & 4u) && a.gap_exact == 2 && a.n_attr >= 2 &&
+                                                       a.att_single && (W > 1 || N <= 31) ? 1 : 0) != 0;
+  if (role == 1 && env_fast) {
+    // ---- the draws of each env's update R(i), env `lane`: one Philox call (ENV at k = 0,
+    // SETTLE_ENV at k >= 1); the step's draws are computed on every lane and kept where k = 0
+    const uint2* lut = reinterpret_cast<const uint2*>(L + a.gap_lut_off);
+    const uint32_t* att_words = L + a.att_off + a.n_attr + 1;
+    const uint32_t A = (uint32_t)a.n_attr, n1 = (uint32_t)(N + 1);
     EnvPlan p;
     for (uint32_t it = 0;; ++it) {
       asm volatile("" : "+s"(u_k0), "+s"(u_k1));
       PBN_PSTAMP(it - kSettleStampIt + 10, 0);
-      const uint32_t* cin = ctl + ((it + 1) & 1) * 128;
-      const uint32_t Ct = cin[lane], Ck = cin[64 + lane];
-      if (__ballot(Ct < n_steps) == 0 || (uint64_t)it > max_it) break;
-      p.next(Ct, Ck, K);
+      const uint2 C = ctl[((it + 1) & 1) * 64 + lane];
+      if (__ballot(C.x < n_steps) == 0 || (uint64_t)it > max_it) break;
+      p.next(C.x, C.y, K);
+      const uint32_t t = p.Rt, k = p.Rk;
+      uint32_t* slot = slots + (size_t)(it & 1) * a.slot_words;
+      PBN_PSTAMP_AT(it - kSettleStampIt + 10, 16);
+      const bool live = valid && t < n_steps, first = k == 0;
+      const uint64_t step = a.step + (uint64_t)t;
+      const uint32_t st_lo = (uint32_t)step;
+      const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
+      const uint32_t c2 = first ? (pbn::kStreamEnv << 28) : ((pbn::kStreamSettleEnv << 28) | ((k - 1) << 8));
+      const Word4 E = pbn::philox(ge_lo, st_lo, c2, ge_hi, u_k0, u_k1);
+      // the step's draws from X = ENV words 3:2 (used where k = 0): actions, the autoreset pair,
+      // gap 2's uniform (X * x_mult, off the draws' chain)
+      uint32_t xhi = E.w, xlo = E.z;
+      const uint32_t c_act = ext64(xhi, xlo, n1 * n1 * n1);
+      const uint32_t c = ext64(xhi, xlo, A * (A - 1));
+      const uint32_t as = a.am1_magic ? __umulhi(c, a.am1_magic) : c;   // c / (A - 1)
+      const uint32_t u2 = first ? (uint32_t)((((((uint64_t)E.w) << 32) | E.z) * a.x_mult) >> 32) : E.z;
+      uint32_t rs[W];
+#pragma unroll
+      for (int w = 0; w < W; ++w) rs[w] = att_words[(size_t)as * W + w];
+      const uint2 e0 = lut[min(E.x >> a.gap_shift, (uint32_t)a.gap_nb)];
+      const uint2 e1 = lut[min(E.y >> a.gap_shift, (uint32_t)a.gap_nb)];
+      const uint2 e2 = lut[min(u2 >> a.gap_shift, (uint32_t)a.gap_nb)];
+      uint32_t rt = c - as * (A - 1);
+      rt += (rt >= as) ? 1u : 0u;
+      uint32_t m[W], gam[W];
+#pragma unroll
+      for (int w = 0; w < W; ++w) { m[w] = 0; gam[w] = 0; }
+      if constexpr (W == 1) m[0] = actions_mask31(c_act, n1, a.n1_magic, valid_word_mask(N, 0));   // N <= 31
+      else actions_from_draw<W>(c_act, N, a.n1_magic, m);
+      uint32_t pcv = 0;
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        m[w] = live && first ? m[w] : 0u;
+        pcv += __builtin_popcount(m[w]);
+      }
+      const int g0 = (int)e0.y + (E.x >= e0.x ? 1 : 0);   // gap_lut
+      const int g1 = (int)e1.y + (E.y >= e1.x ? 1 : 0);
+      const int g2 = (int)e2.y + (u2 >= e2.x ? 1 : 0);
+      const int p0 = g0 - 1, p1 = p0 + g1, p2 = p1 + g2;
+      if constexpr (W == 1) {
+        // N <= 31: a position past the network lands on a bit >= N (bit 31 at most), cleared by
+        // the word mask once
+        gam[0] = ((1u << min((uint32_t)p0, 31u)) | (1u << min((uint32_t)p1, 31u)) |
+                  (1u << min((uint32_t)p2, 31u))) & valid_word_mask(N, 0);
+      } else {
+        set_bit<W>(gam, p0, N);
+        set_bit<W>(gam, p1, N);
+        set_bit<W>(gam, p2, N);
+      }
+      if (live && p2 < N - 1) {   // rare: more gaps (k = 0: PERT call (j-3) >> 2, word (j-3) & 3;
+                                  // k >= 1: gap 3 is word 3, gap j >= 4 SETTLE_ENV call (k-1) << 8 | j >> 2)
+        Word4 P = E;
+        int pos = p2;
+        for (int j = 3; pos < N - 1; ++j) {
+          const int jj = first ? j - 3 : j;
+          if ((jj & 3) == 0)
+            P = pbn::philox(ge_lo, st_lo,
+                            first ? ((pbn::kStreamPert << 28) | (uint32_t)(jj >> 2))
+                                  : ((pbn::kStreamSettleEnv << 28) | ((k - 1) << 8) | (uint32_t)(jj >> 2)),
+                            ge_hi, u_k0, u_k1);
+          const int j4 = jj & 3;
+          const uint32_t u = j4 == 0 ? P.x : (j4 == 1 ? P.y : (j4 == 2 ? P.z : P.w));
+          pos += gap_lut(lut, a.gap_shift, a.gap_nb, u);
+          set_bit<W>(gam, pos, N);
+        }
+      }
+      if (live && first) {
+#pragma unroll
+        for (int w = 0; w < W; ++w) LANE_STV(a.flipmask, ((size_t)t * plane + (size_t)w * n) + (size_t)le, (size_t)n_steps * plane, 8, m[w]);
+      }
+      PBN_PSTAMP_AT(it - kSettleStampIt + 10, 17);
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        slot[w * 64 + lane] = m[w];
+        slot[kGP + w * 64 + lane] = live ? gam[w] : 0u;
+        slot[kRS + w * 64 + lane] = rs[w];
+      }
+      slot[kIN + lane] = rt | (pcv << 8);
+      PBN_PSTAMP(it - kSettleStampIt + 10, 1);
+      lds_barrier();
+      PBN_PSTAMP(it - kSettleStampIt + 10, 2);
+      p.done();
+    }
+  } else if (role == 1) {
+    // ---- the draws of each env's update R(i), env `lane` (general networks and modes)
+    EnvPlan p;
+    for (uint32_t it = 0;; ++it) {
+      asm volatile("" : "+s"(u_k0), "+s"(u_k1));
+      PBN_PSTAMP(it - kSettleStampIt + 10, 0);
+      const uint2 C = ctl[((it + 1) & 1) * 64 + lane];
+      if (__ballot(C.x < n_steps) == 0 || (uint64_t)it > max_it) break;
+      p.next(C.x, C.y, K);
       const uint32_t t = p.Rt, k = p.Rk;
       uint32_t* slot = slots + (size_t)(it & 1) * a.slot_words;
       PBN_PSTAMP_AT(it - kSettleStampIt + 10, 16);
@@ -1997,8 +2094,17 @@ pbn_rollout_settle(StepArgs a) {
           slot[kIN + lane] = rtv | (pcv << 8);
         }
         // gaps 0, 1 = words 0, 1; gap 2 = u2 (k = 0) or word 2 (k >= 1); then, rarely, more
-        const int g0 = gap_any(a.gap_exact, L, a, E.x), g1 = gap_any(a.gap_exact, L, a, E.y),
-                  g2 = gap_any(a.gap_exact, L, a, u2);
+        int g0, g1, g2;
+        if (a.gap_exact == 2) {   // the bucket table (every kaban network): three reads side by side
+          const uint2* lut = reinterpret_cast<const uint2*>(L + a.gap_lut_off);
+          g0 = gap_lut(lut, a.gap_shift, a.gap_nb, E.x);
+          g1 = gap_lut(lut, a.gap_shift, a.gap_nb, E.y);
+          g2 = gap_lut(lut, a.gap_shift, a.gap_nb, u2);
+        } else {
+          g0 = gap_any(a.gap_exact, L, a, E.x);
+          g1 = gap_any(a.gap_exact, L, a, E.y);
+          g2 = gap_any(a.gap_exact, L, a, u2);
+        }
         const int p0 = g0 - 1, p1 = p0 + g1, p2 = p1 + g2;
         set_bit<W>(gam, p0, N);
         set_bit<W>(gam, p1, N);
@@ -2037,10 +2143,9 @@ pbn_rollout_settle(StepArgs a) {
     EnvPlan p;
     for (uint32_t it = 0;; ++it) {
       PBN_PSTAMP(it - kSettleStampIt + 10, 0);
-      const uint32_t* cin = ctl + ((it + 1) & 1) * 128;
-      const uint32_t Ct = cin[lane], Ck = cin[64 + lane];
-      if (__ballot(Ct < n_steps) == 0 || (uint64_t)it > max_it) break;
-      p.next(Ct, Ck, K);
+      const uint2 C = ctl[((it + 1) & 1) * 64 + lane];
+      if (__ballot(C.x < n_steps) == 0 || (uint64_t)it > max_it) break;
+      p.next(C.x, C.y, K);
       const uint32_t t = p.Rt, k = p.Rk;   // (no update: the words are computed and discarded)
       uint32_t* lt_out = slots + (size_t)(it & 1) * a.slot_words + kLT + half * 32 * W;
       const uint64_t step = a.step + (uint64_t)t;
@@ -2138,9 +2243,7 @@ pbn_rollout_settle(StepArgs a) {
         Ct = end ? t + 1 : t;
         Ck = end ? 0u : k + 1;
       }
-      uint32_t* cout = ctl + (it & 1) * 128;
-      cout[lane] = Ct;
-      cout[64 + lane] = Ck;
+      ctl[(it & 1) * 64 + lane] = make_uint2(Ct, Ck);
 #pragma unroll
       for (int w = 0; w < W; ++w) st[w] = cur[w];
       if (end) {
