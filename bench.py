@@ -327,14 +327,14 @@ def workload_text(args, chunk: int, rollout_mode: bool) -> str:
                if rollout_mode else "pbn_step per step"))
 
 
-def settle_stats(updates, elapsed_s: float, env_steps: int) -> dict:
+def settle_stats(updates, elapsed_s: float, env_steps: int, cap: int = 0) -> dict:
     """Settle lengths (pbn_rollout_ex's d_updates) of every env-step of a timed run: the
-    synchronous updates applied per second and their distribution."""
+    synchronous updates applied per second, their distribution, and the kernel's update slots.
+    pbn_rollout_settle runs every env's own sequence of updates (per-env plans; DESIGN.md "Step
+    law"): an env spends its updates plus one dropped speculation per step that settles before
+    the cap, and a launch lasts as long as its busiest env (the launch tail)."""
     u = torch.cat([x.reshape(-1) for x in updates]).to(torch.int64)
     total = int(u.sum().item())
-    # the updates the kernel runs per step: a 32-env group (one bit-sliced word) runs to its
-    # slowest env, so its step takes the group's maximum (plus at most one dropped speculation)
-    groups = torch.cat([x.reshape(x.shape[0], -1, 32).amax(-1).reshape(-1) for x in updates]).to(torch.float64)
     hist = torch.bincount(u).cpu().tolist()
     n = u.numel()
     cum, q = 0, {}
@@ -343,14 +343,27 @@ def settle_stats(updates, elapsed_s: float, env_steps: int) -> dict:
         for p in (0.5, 0.9, 0.99):
             if p not in q and cum >= p * n:
                 q[p] = length
+    # iterations per env and launch: updates + the dropped speculation of steps ending before the cap
+    slots = []
+    for x in updates:   # [T][n] per launch
+        x = x.to(torch.int64)
+        per_env = (x + (x < cap).to(torch.int64) if cap else x).sum(0).to(torch.float64)
+        slots.append((per_env.mean().item(), per_env.max().item(), x.shape[0]))
+    T = sum(t for _, _, t in slots)
+    mean_it = sum(m for m, _, _ in slots) / T
+    launch_it = sum(mx for _, mx, _ in slots) / T
     return {"updates_per_s": total / elapsed_s, "mean_updates_per_env_step": total / n,
-            "mean_group_updates_per_step": float(groups.mean().item()),
+            "mean_env_iterations_per_step": mean_it,
+            "launch_iterations_per_step": launch_it,
+            "launch_tail": launch_it / mean_it,
             "updates_quantiles": {"p50": q.get(0.5), "p90": q.get(0.9), "p99": q.get(0.99), "max": len(hist) - 1},
             "settle_length_histogram": {str(k): c for k, c in enumerate(hist) if c},
             "env_steps_sampled": n, "env_steps_timed": env_steps,
             "note": "updates = synchronous updates applied per env-step (1 + the settle updates), read from "
-                    "pbn_rollout_ex's d_updates of every timed launch; a 32-env group runs until its last env "
-                    "settles, so the kernel's update slots are at least the sum of these"}
+                    "pbn_rollout_ex's d_updates of every timed launch.  pbn_rollout_settle gives every env its "
+                    "own sequence of updates: mean_env_iterations_per_step = an env's updates + one dropped "
+                    "speculation per step that settles before the cap; launch_iterations_per_step = the "
+                    "busiest env's (a launch lasts as long as its busiest env: launch_tail = their ratio)"}
 
 
 def launch_plan(steps: int, chunk: int):
@@ -505,23 +518,37 @@ def settle_line(args, dev, stream, world, local, plan, K):
         ms, _ = timed(run, stream, dev, world, local)
     elapsed = ms * 1e-3
     total = world * args.envs * args.steps
-    stats = settle_stats([b["updates"] for b in bufs], elapsed, total)
+    stats = settle_stats([b["updates"] for b in bufs], elapsed, total, cap=K)
     if world > 1:   # every rank's updates
         t = torch.tensor([stats["updates_per_s"]], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t)
         stats["updates_per_s"] = float(t.item())
     per_step = survey_bytes_per_env_step(spec.n)
     achieved = env.n_alloc * world * args.steps * per_step / elapsed / 1e9
+    hbm = {"achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+           "bytes_per_env_step": per_step,
+           "note": "the same per-env-step I/O as the headline; a settle step applies mean_updates_per_env_step "
+                   "updates on chip for it"}
+    roofline = {"bound": "valu", "achieved": None, "peak": VALU_WAVE_INSTS_PER_S, "unit": "wave-instructions/s",
+                "frac": None, "hbm": hbm,
+                "note": "the settle kernel is bound by VALU issue and latency (its three waves share one SIMD at "
+                        "65,536 envs), so it is priced on SQ_INSTS_VALU of the same launch shape over this run's "
+                        "time against the chip's issue rate (256 CU x 4 SIMD x 2.4 GHz / 2 cycles per wave64 "
+                        "VALU instruction); none committed for this shape: null"}
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.network}_{args.envs}_rollout_T{plan[0]}_settle{K}.json")
+    if len(set(plan)) == 1 and os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            pmc = json.load(f)
+        if pmc.get("valu_insts_per_launch"):
+            v = pmc["valu_insts_per_launch"] * len(plan) / elapsed
+            roofline.update(achieved=v, frac=v / VALU_WAVE_INSTS_PER_S, insts_per_launch=pmc["valu_insts_per_launch"],
+                            source={"file": os.path.relpath(pmc_path, ROOT), "command": pmc.get("command")})
+            roofline["note"] = roofline["note"].rsplit(";", 1)[0]
     line = {"value": total / elapsed, "unit": "env-steps/s", "ms_per_step": ms / args.steps, "settle_max": K,
             "step_law": f"settle: the intervention, then synchronous updates until every state is an attractor "
                         f"state, at most {K} updates (PBNEnv's default; include/pbn_env.h 'Step law')",
             "kernel": "pbn_rollout_settle (%s)" % ", ".join(f"{k} steps" for k in plan),
-            "launch_ms": ms / len(plan),
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "bytes_per_env_step": per_step,
-                         "note": "the same per-env-step I/O as the headline; a settle step applies "
-                                 "mean_updates_per_env_step updates on chip for it"},
-            **stats}
+            "launch_ms": ms / len(plan), "roofline": roofline, **stats}
     env.close()
     return line, spec
 
@@ -909,17 +936,17 @@ def main():
         elif rollout_mode:
             out["config"]["step_law"] = "one synchronous update per env step (SURVEY.md 8(d)'s unit of work)"
         if settle_other is not None:
-            # what one synchronous update costs against one step of the
-            # one-update law (this line's own clock): per group update (the kernel's unit) and per
-            # update an env needs (the group's other envs ride along until its slowest settles)
-            g = settle_other.get("mean_group_updates_per_step")
+            # what one synchronous update costs against one step of the one-update law (this line's
+            # own clock): per kernel iteration (the launch's busiest env's iterations) and per update
+            # an env needs
+            g = settle_other.get("launch_iterations_per_step")
             if g:
-                per_group = settle_other["ms_per_step"] / g
+                per_it = settle_other["ms_per_step"] / g
                 per_env = settle_other["ms_per_step"] / settle_other["mean_updates_per_env_step"]
                 settle_other["update_cost_vs_one_update_step"] = {
-                    "per_group_update": per_group / (dev_ms / args.steps),
+                    "per_kernel_iteration": per_it / (dev_ms / args.steps),
                     "per_env_update": per_env / (dev_ms / args.steps),
-                    "note": "ms per step / updates per step, over the headline's ms per step"}
+                    "note": "ms per step / (launch iterations, updates) per step, over the headline's ms per step"}
             out["settle_law"] = settle_other
         if with_gather is not None:
             out["value_with_gather"] = with_gather["learner"]["value"]

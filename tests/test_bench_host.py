@@ -109,14 +109,19 @@ def test_qnet_tail_flops_count_the_layers_after_the_bilinear():
     assert bench.qnet_flops_per_env(28, 3) - bench.qnet_tail_flops_per_env(28, 3) == 2 * 28 * 28 * 256
 
 
-def test_settle_stats_group_updates_are_the_group_maximum():
-    """A 32-env group runs to its slowest env: mean_group_updates_per_step is the mean over
-    (step, group) of the group's largest settle length, never below the per-env mean."""
+def test_settle_stats_iterations_and_launch_tail():
+    """pbn_rollout_settle's per-env plans: an env spends its updates plus one dropped speculation
+    per step that settles before the cap; a launch lasts as long as its busiest env."""
     import torch
     u = torch.ones(3, 64, dtype=torch.int16)
-    u[0, 5] = 40          # step 0, group 0
-    u[2, 63] = 7          # step 2, group 1
-    s = bench.settle_stats([u], 1.0, 192)
-    assert s["mean_group_updates_per_step"] == pytest.approx((40 + 1 + 1 + 1 + 1 + 7) / 6)
-    assert s["mean_updates_per_env_step"] == pytest.approx((192 - 2 + 40 + 7) / 192)
-    assert s["updates_quantiles"]["max"] == 40
+    u[0, 5] = 40          # step 0, env 5: 40 updates, below the cap
+    u[2, 63] = 64         # step 2, env 63: capped (no dropped speculation)
+    s = bench.settle_stats([u], 1.0, 192, cap=64)
+    assert s["mean_updates_per_env_step"] == pytest.approx((192 - 2 + 40 + 64) / 192)
+    per_env = [6.0] * 64
+    per_env[5] = 41 + 2 + 2
+    per_env[63] = 2 + 2 + 64
+    assert s["mean_env_iterations_per_step"] == pytest.approx(sum(per_env) / 64 / 3)
+    assert s["launch_iterations_per_step"] == pytest.approx(68 / 3)
+    assert s["launch_tail"] == pytest.approx(68 / (sum(per_env) / 64))
+    assert s["updates_quantiles"]["max"] == 64

@@ -5,8 +5,8 @@ for a kernel-and-copy trace:
       python tools/handoff_trace.py [--steps 20] [--plan 20] [--reps 20]
 
 Each rep: the rollout launches of the plan into the ring's record slots, each followed by the
-hand-off of its records (at world 1: the learner's own shard copied into its receive slot on a
-side stream), then a device sync.  Prints one JSON line with the per-rep device time of the
+hand-off of its records (at world 1: the learner's own shard copied into its receive slot by
+pbn_copy_async, on a side stream, the last one on the launch stream), then a device sync.  Prints one JSON line with the per-rep device time of the
 pass (HIP events around each rep, after two untimed reps), and with --summarize DIR attributes
 the trace: per rep, the rollout kernels, the copy (kernel or DMA), and the gaps between them.
 """
@@ -37,8 +37,8 @@ def run(args):
     stream = torch.cuda.current_stream()
 
     def rep():
-        for k in plan:
-            ro.gather(ro.rollout(k), dst=0, async_op=True, copy_own=True)
+        for j, k in enumerate(plan):
+            ro.gather(ro.rollout(k), dst=0, async_op=True, copy_own=True, last=j == len(plan) - 1)
         for works in ro._pending.values():
             for w in works:
                 if w is not None:
