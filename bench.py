@@ -307,6 +307,70 @@ def cpu_baseline_bdq(spec, qnet, seconds: float, threads: int):
                       f"flip masks + oracle/pbn_oracle.c step, {n} envs x {frames} frames ({el:.1f} s)"}
 
 
+def cpu_baseline_bdq_learn(spec, qnet, n: int, seconds: float, threads: int, batch: int = 256,
+                          lr: float = 1e-4, gamma: float = 0.999):
+    """The BDQ training frame on the host cores for ~`seconds`, at the GPU line's shape: the acting
+    frame of cpu_baseline_bdq over the same n envs, their transitions into a host ring, and one
+    update_policy step per frame (batch 256, Adam; bdq_update's PyTorch form on CPU tensors, which
+    tests/test_update_golden.py pins to the reference's update_policy)."""
+    import copy
+
+    import numpy as np
+
+    from oracle import agent_oracle, oracle
+    from pbn_rl_amd.replay import bdq_update
+
+    torch.set_num_threads(threads)
+    q_cpu = copy.deepcopy(qnet).to("cpu").train()
+    target = copy.deepcopy(q_cpu)
+    opt = torch.optim.Adam(q_cpu.parameters(), lr=lr)
+    N, K = spec.n, q_cpu.n
+    cap = 4 * n
+    ring = {"obs": np.zeros((2, cap, N), np.float32), "next_obs": np.zeros((2, cap, N), np.float32),
+            "actions": np.zeros((cap, K), np.int64), "rewards": np.zeros(cap, np.float32),
+            "masks": np.zeros(cap, np.float32)}
+    rng = np.random.default_rng(0)
+    st, tg, t = oracle.reset(spec, 1, 0, 0, n)
+    frames, updates, pos, size, t0 = 0, 0, 0, 0, time.perf_counter()
+    while True:
+        obs = agent_oracle.obs_unpack(spec, st, tg)
+        with torch.no_grad():
+            q = q_cpu(torch.from_numpy(obs)).numpy()
+        flip, actions = agent_oracle.q_to_flipmask(spec, q, 1, frames + 1, 0, 0.0)
+        out = oracle.step(spec, 1, frames + 1, 0, st, flip, tg, t, 1, want_final=True, n_threads=threads)
+        rows = (pos + np.arange(n)) % cap
+        ring["obs"][:, rows] = obs
+        ring["next_obs"][:, rows] = agent_oracle.obs_unpack(spec, out["final_state"], tg)
+        ring["actions"][rows] = actions
+        ring["rewards"][rows] = out["reward"]
+        ring["masks"][rows] = ((out["flags"] & 3) != 0).astype(np.float32)
+        pos, size = (pos + n) % cap, min(size + n, cap)
+        st, tg, t = out["state_out"], out["target"], out["t"]
+        idx = rng.integers(0, size, batch)
+        b = {"obs": torch.from_numpy(ring["obs"][:, idx]), "next_obs": torch.from_numpy(ring["next_obs"][:, idx]),
+             "actions": torch.from_numpy(ring["actions"][idx]).unsqueeze(-1),
+             "rewards": torch.from_numpy(ring["rewards"][idx]).reshape(-1, 1),
+             "masks": torch.from_numpy(ring["masks"][idx]).reshape(-1, 1)}
+        bdq_update(q_cpu, target, opt, b, gamma)
+        frames += 1
+        updates += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": n * frames / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"BDQ training frame on CPU: numpy obs + torch CPU BranchingQNetwork ({threads} threads) + "
+                      f"greedy flip masks + oracle/pbn_oracle.c step + host ring store + one update_policy step "
+                      f"(bdq_update on CPU tensors, batch {batch}, Adam), {n} envs x {frames} frames ({el:.1f} s)"}
+
+
+def update_flops(n: int, batch: int, branches: int = 3) -> int:
+    """FLOPs of one update_policy step (bdq_model/__init__.py:111-131) in the reference's
+    arithmetic: forwards of the online network over 2B rows (states, next states) and of the
+    target over B rows, and the backward over the B rows that carry gradient (weight and input
+    gradients: two forwards' worth), 5B row-forwards of qnet_flops_per_env."""
+    return 5 * batch * qnet_flops_per_env(n, branches)
+
+
 def workload_text(args, chunk: int, rollout_mode: bool) -> str:
     common = (f"horizon {args.horizon}, p={args.perturbation}, prob_bits={args.prob_bits}")
     if args.workload == "bdq":
@@ -797,7 +861,7 @@ def main():
                                 "records": "s, a, s' (final_state), r, flags of every env-step"}
 
     tail_ms = None
-    if args.workload == "bdq" and agent.fused_tail:
+    if args.workload in ("bdq", "bdq-learn") and agent.fused_tail:
         # the frame's long launch timed alone: 50 back to back, replayed from one hipGraph (eager,
         # the host's ctypes calls would set the pace)
         with torch.cuda.stream(stream):
@@ -809,6 +873,20 @@ def main():
             tg.replay()
             tail_ms, _ = timed(tg.replay, stream, dev, world, local)
             tail_ms /= 50
+    learn_ms = None
+    if args.workload == "bdq-learn" and learner.fused is not None:
+        # the fused update (pbn_bdq_learn's three launches) timed alone: 50 back to back on the
+        # frame's batch rows, replayed from one hipGraph (after the timed frames: they train on)
+        with torch.cuda.stream(stream):
+            rows = learner._idx[:learner.batch_size]
+            lg = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(lg, stream=stream):
+                for _ in range(50):
+                    learner.fused.update(learner.replay, rows)
+            lg.replay()
+            learn_ms, _ = timed(lg.replay, stream, dev, world, local)
+            learn_ms /= 50
+            learner.fused.mark_updated()
 
     if rank == 0:
         W = spec.words
@@ -820,7 +898,7 @@ def main():
                 kernel += " + replay store + update_policy (batch 256)"
                 kernel += ", one hipGraph replay per frame" if args.learn_graph else ", eager"
         frame_ms = dev_ms / args.steps
-        if args.workload == "bdq":
+        if args.workload in ("bdq", "bdq-learn"):
             # dominant launch: pbn_qnet_flipmask_from_state, MFMA-bound.  Algorithmic FLOPs = the
             # bilinear layer as the target-contracted product (N x 256 MACs per env) + the layers
             # after it (qnet_tail_flops_per_env), fp32 MFMA peak
@@ -840,16 +918,23 @@ def main():
                                     "layer contracted with the target (N x 256 MACs) + the Linear layers after it "
                                     "(trunk 256-128-64-32, K+1 heads 32-64-A)",
                             "model_flops_utilisation": mfu}
+                if args.workload == "bdq-learn":
+                    roofline["note"] += ("; the training frame's longest launch, as in the acting line (the frame: "
+                                         "Q-network, step, ring store, row draw, the fused update's three launches)")
+                    if learn_ms is not None:
+                        uf = update_flops(spec.n, learner.batch_size, agent.branches)
+                        ut = uf / (learn_ms * 1e-3) / 1e12
+                        roofline["update"] = {
+                            "bound": "mfma", "achieved": ut, "peak": FP32_MATRIX_TFLOPS, "unit": "TFLOP/s",
+                            "frac": ut / FP32_MATRIX_TFLOPS, "kernel": "pbn_bdq_learn (forward, backward, apply)",
+                            "update_ms": learn_ms, "flops_per_update": uf,
+                            "note": "update_policy's FLOPs in the reference's arithmetic (5B row-forwards: online "
+                                    "over states and next states, target over next states, backward over B rows, "
+                                    "bench.py update_flops) over the fused update's time, 50 replayed back to back"}
             else:
                 roofline = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                             "traffic": None, "kernel": "frame (PyTorch tail)", "launch_ms": frame_ms,
                             "model_flops_utilisation": mfu}
-        elif agent is not None:
-            roofline = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-                        "traffic": None, "kernel": kernel, "launch_ms": frame_ms,
-                        "note": "training frame (11 launches: Q-network, step, ring store, counters + rows, "
-                                "the fused update's forward / backward / apply; profiles/r04_l*_bdq_learn_trace*): no "
-                                "single dominant kernel is priced"}
         elif rollout_mode:
             per_step = survey_bytes_per_env_step(spec.n)
             bytes_run = env.n_alloc * args.steps * per_step
@@ -954,7 +1039,9 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             host = host_info()
             threads = host["usable"]
-            if agent is not None:
+            if args.workload == "bdq-learn":
+                out["cpu_baseline"] = cpu_baseline_bdq_learn(spec, agent.q, args.envs, args.cpu_seconds, threads)
+            elif agent is not None:
                 out["cpu_baseline"] = cpu_baseline_bdq(spec, agent.q, args.cpu_seconds, threads)
             else:
                 out["cpu_baseline"] = cpu_baseline(spec, args.envs, args.cpu_seconds, threads)

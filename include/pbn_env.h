@@ -116,7 +116,11 @@ extern "C" {
  * flags carry PBN_FLAG_UNSETTLED when the K-th update still left it outside every attractor.
  * That is the "intervene, then run to a (pseudo-)attractor" step that the reference's
  * recorded bb33 evaluation pins (data/results/pbn_33_3.pkl under model_tester.py:587-658;
- * DESIGN.md "Parity status").  Updates k >= 1 draw from the SETTLE_SEL / SETTLE_ENV streams.
+ * DESIGN.md "Parity status").  Update 0 draws its actions, autoreset and perturbation from the
+ * one-update law's ENV / PERT calls, updates k >= 1 their perturbation from SETTLE_ENV; every
+ * update's rule selection (k >= 0) is keyed per env (ABI 7): node i's uniform is the top
+ * prob_bits bits of 16-bit field i & 1 of word (i >> 1) & 3 of SETTLE_SEL call (k << 8 | i >> 3)
+ * of (env, step) -- so every env runs its own sequence of updates (DESIGN.md "Step law").
  */
 typedef struct pbn_net_desc {
   int32_t n_nodes;
@@ -212,8 +216,9 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
  *              env-step, 1 under the one-update law, 1..settle_max under the settle law (the
  *              settle length; the env-step carries PBN_FLAG_UNSETTLED when it reached settle_max
  *              outside every attractor).
- * Under the settle law the pipelined kernel runs one update per iteration for each 32-env group
- * and continues a group's step while any of its envs is outside every attractor.
+ * Under the settle law the pipelined kernel runs one update per iteration for every env on its
+ * own plan (the selection keyed per env): an env starts its next step as soon as its current
+ * step ends, whatever the other envs of its 32-env word do.
  *   the frame loop bdq_model/__init__.py:172-213 on the env constructed at train_BDQ.py:50 /
  *   model_tester.py:409-413, whose step runs to an attractor (model_tester.py:616-626)
  */

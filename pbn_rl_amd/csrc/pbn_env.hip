@@ -138,6 +138,8 @@ struct pbn_net {
   uint4* d_fcompact = nullptr;
   uint4* d_nrec = nullptr;
   uint32_t* d_sthr = nullptr;   // settle law: thresholds scaled to 16 bits [lq][32W] (StepArgs::sthr)
+  uint32_t* d_sthr_pk = nullptr;   // the same, packed biased node pairs [lq][W][16] (StepArgs::sthr_pk)
+  int settle_pk = 0;
   int n_funcs = 0;
   size_t lds_wave = 0;
   StepFn wave1 = nullptr;       // single step (pbn_step)
@@ -196,6 +198,7 @@ void free_net(pbn_net* net) {
   (void)hipFree(net->d_fcompact);
   (void)hipFree(net->d_nrec);
   (void)hipFree(net->d_sthr);
+  (void)hipFree(net->d_sthr_pk);
   (void)hipFree(net->d_tab);
   (void)hipFree(net->d_att_start);
   (void)hipFree(net->d_att_states);
@@ -634,9 +637,12 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   }
   net->lds_wave = ((size_t)net->tab_words + (size_t)kWavesPerBlock * net->wave_words) * 4;
   net->slot_words = (3 * W + 1) * 64 + net->lq * 64 * W;
-  // + the selection wave's threshold digit masks [kNodeRecs - 1][B][32] (W == 1)
+  // + the selection wave's threshold digit masks (W == 1): [32][sel_mask_stride(B)], lane-major
+  // (or [kNodeRecs - 1][B][32] node-major without PBN_SEL_MASK_B128)
+  const size_t cm_words = PBN_SEL_MASK_B128 ? 32 * (size_t)sel_mask_stride(d->prob_bits)
+                                            : (size_t)(kNodeRecs - 1) * d->prob_bits * 32;
   net->lds_pipe = ((size_t)net->tab_words + 64 * (size_t)W + 2 * (size_t)net->slot_words +
-                   (W == 1 ? (size_t)(kNodeRecs - 1) * d->prob_bits * 32 : 0)) * 4;
+                   (W == 1 ? cm_words : 0)) * 4;
   // compact records for the wave kernel: {inputs as bytes, 4-input truth table, threshold, 0}
   net->wave1 = pick_wave<1>(W, d->prob_bits);
   net->wave_lean = pick_wave<2>(W, d->prob_bits);
@@ -668,6 +674,21 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
     for (int q = 0; q < nf - 1 && q < net->lq; ++q)
       sthr[(size_t)q * 32 * W + i] = d->func_threshold[f0 + q] << (16 - d->prob_bits);
   }
+  // packed biased node pairs for settle_lt_word_pk, exact when no compared threshold is 65536
+  std::vector<uint32_t> sthr_pk((size_t)net->lq * W * 16);
+  net->settle_pk = 1;
+  for (int q = 0; q < net->lq; ++q)
+    for (int i = 0; i < 32 * W; i += 2) {
+      uint32_t c[2];
+      for (int h = 0; h < 2; ++h) {
+        const int ii = i + h;
+        const bool real = ii < N && q < d->node_func_start[ii + 1] - d->node_func_start[ii] - 1;
+        const uint32_t v = sthr[(size_t)q * 32 * W + ii];
+        if (real && v > 65535u) net->settle_pk = 0;
+        c[h] = std::min(v, 65535u) ^ 0x8000u;
+      }
+      sthr_pk[((size_t)q * W + i / 32) * 16 + (i % 32) / 2] = c[0] | (c[1] << 16);
+    }
   std::vector<uint32_t> att_first((size_t)A * W);
   for (int t = 0; t < A; ++t)
     for (int w = 0; w < W; ++w) att_first[(size_t)t * W + w] = d->attractor_states[(size_t)d->attractor_start[t] * W + w];
@@ -682,6 +703,7 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   if ((rc = upload(&net->d_fcompact, fcomp.data(), fcomp.size())) ||
       (rc = upload(&net->d_nrec, nrec.data(), nrec.size())) ||
       (rc = upload(&net->d_sthr, sthr.data(), sthr.size())) ||
+      (rc = upload(&net->d_sthr_pk, sthr_pk.data(), sthr_pk.size())) ||
       (rc = upload(&net->d_tab, tab.data(), tab.size())) ||
       (rc = upload(&net->d_att_start, A ? d->attractor_start : nullptr, (size_t)A + 1)) ||
       (rc = upload(&net->d_att_states, S ? d->attractor_states : nullptr, (size_t)S * W)) ||
@@ -782,6 +804,8 @@ static void fill_args(const pbn_net* net, StepArgs* p, uint64_t seed, uint64_t s
   a.fcompact = net->d_fcompact;
   a.nrec = net->d_nrec;
   a.sthr = net->d_sthr;
+  a.sthr_pk = net->d_sthr_pk;
+  a.settle_pk = net->settle_pk;
   a.n1_magic = net->n1_magic;
   a.att_single = net->att_single;
   a.am1_magic = net->am1_magic;

@@ -16,7 +16,8 @@
 namespace pbn {
 
 // EXPLORE = 4: epsilon-greedy draws of pbn_q_to_flipmask (per env; word 0 = explore test,
-// word k + 1 = branch k's random action, by multiply-high); SETTLE_SEL = 5 (per group) and
+// word k + 1 = branch k's random action, by multiply-high); SETTLE_SEL = 5 (per env: node i's
+// selection uniform of update k is 16-bit field i & 7 of call (k << 8) | (i >> 3)) and
 // SETTLE_ENV = 6 (per env): updates k >= 1 of a step under the settle law (settle_updates);
 // REPLAY = 7: the learner's replay rows (pbn_replay_advance: id = row of the batch, step = draw)
 enum : uint32_t {

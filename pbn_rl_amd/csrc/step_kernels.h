@@ -97,6 +97,9 @@ struct StepArgs {
   uint16_t* updates;   // rollouts: [n_steps][n] synchronous updates applied per env-step (nullable)
   const uint32_t* sthr;  // settle law: thresholds scaled to 16 bits, [lq][32W] (65536 past a node's
                          // last function): the per-env selection compares (settle_lt_word)
+  const uint32_t* sthr_pk;  // the same, node pairs packed biased for settle_lt_word_pk: [lq][W][16]
+                            // {(C[2j+1] ^ 0x8000) << 16 | (C[2j] ^ 0x8000)}, C clamped to 65535
+  int settle_pk;            // 1: every threshold a compare uses is below 65536 (sthr_pk is exact)
 };
 
 // In-kernel phase clocks (cdna_hip_programming.md section 7, "In-kernel stamps"):
@@ -146,11 +149,42 @@ struct StepArgs {
     __builtin_amdgcn_sched_barrier(0);                                                        \
     if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)(gridDim.x + blockIdx.x) * 32 + (idx_)] = t_; \
   } while (0)
+#elif defined(PBN_ISA_MARKS)
+// assembly listings only (tools/isa_budget.py compiles one instance with -S): each stamp site
+// becomes a comment line in the listing, fenced so that no instruction crosses it; no code
+#define PBN_ISA_MARK(txt)                                                                     \
+  do {                                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    asm volatile(";@mark " txt);                                                              \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+  } while (0)
+#define PBN_STAMP(k) do {} while (0)
+#define PBN_PSTAMP(k, slot_) PBN_ISA_MARK("P" #slot_)
+#define PBN_PSTAMP_AT(k, idx_) PBN_ISA_MARK("A" #idx_)
+#define PBN_RSTAMP(idx_) PBN_ISA_MARK("R" #idx_)
+// names the side of a runtime uniform branch it opens (tools/isa_budget.py --arms picks the live ones)
+#define PBN_ISA_ARM(name_)                                                                    \
+  do {                                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    asm volatile(";@arm " name_);                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+  } while (0)
+// names the loop body it opens (role and compile-time variant) in the listing
+#define PBN_ISA_LOOP(name_, v_)                                                               \
+  do {                                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    asm volatile(";@loop " name_ " %0" ::"i"(v_));                                            \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+  } while (0)
 #else
 #define PBN_STAMP(k) do {} while (0)
 #define PBN_PSTAMP(k, slot_) do {} while (0)
 #define PBN_PSTAMP_AT(k, idx_) do {} while (0)
 #define PBN_RSTAMP(idx_) do {} while (0)
+#endif
+#ifndef PBN_ISA_LOOP
+#define PBN_ISA_LOOP(name_, v_) do {} while (0)
+#define PBN_ISA_ARM(name_) do {} while (0)
 #endif
 
 // Bounds-checked global indexing for the diagnostic library (-DPBN_CHECKS): an
@@ -315,6 +349,33 @@ __device__ __forceinline__ uint32_t less_than(const uint32_t (&dig)[16], uint32_
 
 // less_than with the threshold's digit masks read from LDS: cmq[d * stride] = ~0 if bit
 // (B-1-d) of the threshold is set, else 0 (built once per block; saves a v_bfe per digit)
+// pbn_rollout_pipe's threshold digit masks, lane-major: node i's masks of threshold q, digit d at
+// cm[i * S + q * B + d], S = sel_mask_stride(B) words: four masks are one 16-byte ds_read_b128,
+// and S = 4 x odd puts the 16 lanes of each read quarter on distinct 4-bank groups (conflict
+// free; the node-major layout before it read two masks per ds_read2_b32, at twice the LDS-array
+// cycles per mask)
+#ifndef PBN_SEL_MASK_B128
+#define PBN_SEL_MASK_B128 1
+#endif
+__host__ __device__ constexpr int sel_mask_stride(int B) {
+  return PBN_SEL_MASK_B128 ? 4 * (((3 * B + 3) / 4) | 1) : 0;
+}
+template <int B>
+__device__ __forceinline__ uint32_t less_than_cm4(const uint32_t (&dig)[16], const uint32_t* __restrict__ cmq) {
+  const uint4* c4 = reinterpret_cast<const uint4*>(cmq);
+  uint4 m[B / 4];
+#pragma unroll
+  for (int j = 0; j < B / 4; ++j) m[j] = c4[j];
+  uint32_t lt = 0;
+#pragma unroll
+  for (int d = B - 1; d >= 0; --d) {
+    const uint4 v = m[d >> 2];
+    const uint32_t c = (d & 3) == 0 ? v.x : ((d & 3) == 1 ? v.y : ((d & 3) == 2 ? v.z : v.w));
+    lt = __builtin_amdgcn_bitop3_b32(dig[d], lt, c, 0x8E);
+  }
+  return lt;
+}
+
 template <int B>
 __device__ __forceinline__ uint32_t less_than_cm(const uint32_t (&dig)[16], const uint32_t* __restrict__ cmq,
                                                  int stride) {
@@ -403,9 +464,19 @@ __device__ __forceinline__ uint32_t perm_sel(int lane) {
 
 // lane k holds row k of a 32x32 bit matrix (per 32-lane half); afterwards lane c holds column c.
 // 11 VALU (J = 16: swizzle + perm; 8: DPP + perm; 4: swizzle + alignbit + bitop3; 2, 1: DPP +
-// alignbit + bitop3) where five transpose_step spend 20.
+// alignbit + bitop3) where five transpose_step spend 20.  PL16: the J = 16 stage without the LDS
+// crossbar, v_permlane16_swap (rows 0 <-> 1 and 2 <-> 3 of the wave: lane ^ 16) feeding the same
+// v_perm_b32 with the operands in fixed order: 12 VALU, one LDS round trip fewer on the chain.
+template <bool PL16 = false>
 __device__ __forceinline__ uint32_t lane_transpose32(uint32_t a, int lane) {
-  a = __builtin_amdgcn_perm(swizzle_xor<16>(a), a, perm_sel<16>(lane));
+  if constexpr (PL16) {
+    // r[0]: rows (a0, a0, a2, a2), r[1]: rows (a1, a1, a3, a3) -- own value and partner's in
+    // both; low lanes keep r[0]'s low half and take r[1]'s, high lanes the other way round
+    const auto r = __builtin_amdgcn_permlane16_swap(a, a, false, false);
+    a = __builtin_amdgcn_perm(r[1], r[0], (lane & 16) ? 0x07060302u : 0x05040100u);
+  } else {
+    a = __builtin_amdgcn_perm(swizzle_xor<16>(a), a, perm_sel<16>(lane));
+  }
   a = __builtin_amdgcn_perm(xor_lane<8>(a, lane), a, perm_sel<8>(lane));
   {
     const uint32_t y = swizzle_xor<4>(a);
@@ -536,19 +607,21 @@ __device__ __forceinline__ int attractor_lookup(const StepArgs& a, const uint32_
                                                 const uint32_t (&sp)[W]) {
   int att = -1;
   if (a.hash_bits > 0) {
+    PBN_ISA_ARM("hash");
     const uint32_t hmask = (1u << a.hash_bits) - 1u;
     uint32_t h = 0;
 #pragma unroll
     for (int w = 0; w < W; ++w) h += sp[w] * a.hash_mult[w];
     h >>= (32 - a.hash_bits);
-#pragma unroll
-    for (int pr = 0; pr < 4; ++pr) {
-      const int id = hash_probe<W>(htab, (h + pr) & hmask, sp);
-      if (pr < a.hash_probes && id >= 0) att = id;
-    }
-    for (int pr = 4; pr < a.hash_probes; ++pr) {
-      const int id = hash_probe<W>(htab, (h + pr) & hmask, sp);
-      if (id >= 0) att = id;
+    // the first probe always (h < 2^bits needs no mask); the table is usually collision free
+    // (hash_probes = 1: every bundled network), so the others sit behind a uniform branch
+    att = hash_probe<W>(htab, h, sp);
+    if (a.hash_probes > 1) {
+      PBN_ISA_ARM("hash_more_probes");
+      for (int pr = 1; pr < a.hash_probes; ++pr) {
+        const int id = hash_probe<W>(htab, (h + pr) & hmask, sp);
+        if (id >= 0) att = id;
+      }
     }
   }
   return att;
@@ -578,12 +651,14 @@ __device__ __forceinline__ void settle_sel_words(uint32_t ge_lo, uint32_t ge_hi,
                                                  int N, uint32_t k0, uint32_t k1, uint32_t (&U)[16]) {
   const uint32_t c2 = (pbn::kStreamSettleSel << 28) | (k << 8) | (uint32_t)(4 * r);
   if (32 * r + 24 < N) {   // every call (a word of more than 24 nodes): in one block, interleaved
+    PBN_ISA_ARM("sel_all_calls");
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const Word4 P = pbn::philox(ge_lo, st_lo, c2 | (uint32_t)c, ge_hi, k0, k1);
       U[4 * c + 0] = P.x; U[4 * c + 1] = P.y; U[4 * c + 2] = P.z; U[4 * c + 3] = P.w;
     }
   } else {
+    PBN_ISA_ARM("sel_some_calls");
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       Word4 P = {0u, 0u, 0u, 0u};
@@ -609,6 +684,32 @@ __device__ __forceinline__ uint32_t settle_lt_word(const uint32_t (&U)[16], cons
   }
   return lt;
 }
+
+// settle_lt_word two nodes per instruction: U biased (^ 0x80008000) makes each 16-bit field a
+// signed value whose order is the unsigned one, so the saturating v_pk_sub_i16 of the packed biased
+// thresholds has the sign of (u < C) in bits 15 and 31 of each node pair's difference.  v_perm_b32
+// gathers the sign bytes of two pairs (four nodes) into one word, and four-node word m lands at bit
+// offset m of every byte: bit 8c + m of the result = node 4m + c (pk_lane_node, the inverse, is
+// applied at the planes' LDS write).  39 VALU per 32 nodes where settle_lt_word spends 64.
+typedef short s16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t settle_lt_word_pk(const uint32_t (&Ub)[16], const uint32_t* Cpk_) {
+  ConstU32* Cpk = (ConstU32*)Cpk_;
+  uint32_t d[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j)
+    d[j] = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(__builtin_bit_cast(s16x2_t, Ub[j]),
+                                                                     __builtin_bit_cast(s16x2_t, Cpk[j])));
+  uint32_t lt = 0;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    // bytes: node 4m (d[2m] bit 15), 4m+1 (d[2m] bit 31), 4m+2 (d[2m+1] bit 15), 4m+3 (d[2m+1] bit 31)
+    const uint32_t e = __builtin_amdgcn_perm(d[2 * m + 1], d[2 * m], 0x07050301u);
+    lt = pbn::bfi3(0x80808080u >> (7 - m), e >> (7 - m), lt);
+  }
+  return lt;
+}
+// the node whose plane lane l32 holds after transposing a settle_lt_word_pk word
+__device__ __forceinline__ int pk_lane_node(int l32) { return 4 * (l32 & 7) + (l32 >> 3); }
 
 // node l32 + 32r on lane l32: the rule update of every env of the group from the bit-sliced
 // planes S, the selection digit planes dig (perturbed envs are replaced by the caller)
@@ -1259,7 +1360,9 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
 #pragma unroll
       for (int dd = 0; dd < B / 2; ++dd) {
         const int d = h * (B / 2) + dd;
-        cm[(q * B + d) * 32 + i] = ((c >> (B - 1 - d)) & 1u) ? ~0u : 0u;
+        const uint32_t v = ((c >> (B - 1 - d)) & 1u) ? ~0u : 0u;
+        if constexpr (PBN_SEL_MASK_B128) cm[i * sel_mask_stride(B) + q * B + d] = v;
+        else cm[(q * B + d) * 32 + i] = v;
       }
     }
     __syncthreads();
@@ -1290,6 +1393,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
     auto env_step = [&](int k, const Word4& E, Word4& E_next) {
       asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
       asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
+      PBN_ISA_LOOP("env_fast", W);
       PBN_PSTAMP(k, 0);
       if (k < n_steps) {
         uint32_t* slot = slots + (size_t)(k & 1) * a.slot_words;
@@ -1502,7 +1606,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
     // SEL calls computed in the same block as this step's compares
     auto sel_fast = [&](auto nq_c) {
       constexpr int NQ = decltype(nq_c)::value;   // thresholds per node: max_nf - 1
-      const uint32_t* cmi = cm + l32;
+      const uint32_t* cmi = cm + (PBN_SEL_MASK_B128 ? l32 * sel_mask_stride(B) : l32);
       uint32_t* lt_base = slots + (3 * W + 1) * 64 + half * 32 * W + l32;
       auto sel_calls = [&](int k, uint32_t (&d)[16]) {
         const uint64_t step = a.step + (uint64_t)k;
@@ -1517,6 +1621,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
       // one step: this step's compares from `cur`, the next step's calls into `nxt`
       auto sel_step = [&](int k, const uint32_t (&cur)[16], uint32_t (&nxt)[16]) {
         asm volatile("" : "+s"(u_k0), "+s"(u_k1));
+        PBN_ISA_LOOP("sel_fast", NQ);
         PBN_PSTAMP(k, 0);
         if (k < n_steps) {
           sel_calls(k + 1, nxt);   // (one unused set per launch)
@@ -1527,7 +1632,9 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
           PBN_PSTAMP_AT(k, 18);
           uint32_t* lt_out = lt_base + (size_t)(k & 1) * a.slot_words;
 #pragma unroll
-          for (int q = 0; q < NQ; ++q) lt_out[q * 64] = less_than_cm<B>(cur, cmi + (size_t)q * B * 32, 32);
+          for (int q = 0; q < NQ; ++q)
+            lt_out[q * 64] = PBN_SEL_MASK_B128 ? less_than_cm4<B>(cur, cmi + q * B)
+                                               : less_than_cm<B>(cur, cmi + (size_t)q * B * 32, 32);
           // keeps the next calls in this block (LLVM would sink them to the loop latch)
 #pragma unroll
           for (int d = 0; d < 16; ++d) asm volatile("" : "+v"(nxt[d]));
@@ -1581,7 +1688,9 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
               for (int q = 0; q < kNodeRecs - 1; ++q)
                 if (q < nf - 1) {
                   if constexpr (W == 1)
-                    lt_out[q * 64 * W + i] = less_than_cm<B>(dig, cm + (size_t)q * B * 32 + i, 32);
+                    lt_out[q * 64 * W + i] = PBN_SEL_MASK_B128
+                                                 ? less_than_cm<B>(dig, cm + i * sel_mask_stride(B) + q * B, 1)
+                                                 : less_than_cm<B>(dig, cm + (size_t)q * B * 32 + i, 32);
                   else
                     lt_out[q * 64 * W + i] = less_than(dig, recL[q * 32 * W + ic].z, B);
                 }
@@ -1667,6 +1776,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
           // s_waitcnt vmcnt(0) waited on the step's streaming stores in the middle of the chain
 #pragma unroll
           for (int q = 0; q < K; ++q) asm volatile("" : "+v"(ins[q]));
+          PBN_ISA_LOOP("state_fast", K);
           PBN_PSTAMP(k, 0);
           if (k >= 1) {
             const int t = k - 1;
@@ -1836,7 +1946,12 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
 // applies R(i-1) (EnvPlan); the state wave publishes each env's decision C (next update) in LDS.
 // Results are bit-identical to pbn_step_wave's settle variants and to oracle/pbn_oracle.c.
 constexpr uint32_t kNoUpd = 0xFFFFFFFFu;
-constexpr uint32_t kSettleStampIt = 300;   // stamps build: the iteration the settle kernel clocks
+constexpr uint32_t kSettleStampIt = 300;
+// the settle kernel's transposes take the J = 16 stage through v_permlane16_swap (lane_transpose32)
+#ifndef PBN_SETTLE_PL16
+#define PBN_SETTLE_PL16 1
+#endif
+constexpr bool kSettlePL16 = PBN_SETTLE_PL16 != 0;   // stamps build: the iteration the settle kernel clocks
 
 // The per-env update plan of pbn_rollout_settle, in that env's lane of every wave (VGPRs; the
 // same values in all three waves).  P = R(i-1), the update the RNG waves produced in the previous
@@ -1929,6 +2044,7 @@ pbn_rollout_settle(StepArgs a) {
     EnvPlan p;
     for (uint32_t it = 0;; ++it) {
       asm volatile("" : "+s"(u_k0), "+s"(u_k1));
+      PBN_ISA_LOOP("settle_env_fast", W);
       PBN_PSTAMP(it - kSettleStampIt + 10, 0);
       const uint2 C = ctl[((it + 1) & 1) * 64 + lane];
       if (__ballot(C.x < n_steps) == 0 || (uint64_t)it > max_it) break;
@@ -2139,9 +2255,17 @@ pbn_rollout_settle(StepArgs a) {
       p.done();
     }
   } else if (role == 2) {
-    // ---- selection planes of each env's update R(i), env `lane`
+    // ---- selection planes of each env's update R(i), env `lane`; one loop per threshold count
+    // NQ (= mnf - 1) and compare form PK, so that neither is a branch inside the loop (NQ = 0: every
+    // node has one function, no draws are needed)
+    const int pk_node = pk_lane_node(l32);
+    // (the key by value: captured by reference it left the env role's laundered copy in VGPRs)
+    auto sel_loop = [&, s_k0 = u_k0, s_k1 = u_k1](auto nq_c, auto pk_c) __attribute__((always_inline)) {
+    constexpr int NQ = decltype(nq_c)::value;
+    constexpr bool PK = decltype(pk_c)::value;
     EnvPlan p;
     for (uint32_t it = 0;; ++it) {
+      PBN_ISA_LOOP("settle_sel", 2 * NQ + (PK ? 1 : 0));
       PBN_PSTAMP(it - kSettleStampIt + 10, 0);
       const uint2 C = ctl[((it + 1) & 1) * 64 + lane];
       if (__ballot(C.x < n_steps) == 0 || (uint64_t)it > max_it) break;
@@ -2152,17 +2276,28 @@ pbn_rollout_settle(StepArgs a) {
       const uint32_t st_lo = (uint32_t)step;
       const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
       const uint32_t* th = a.sthr;
-      asm volatile("" : "+s"(th));   // the thresholds are read per iteration (hoisted: 32 SGPRs each)
+      const uint32_t* thp = a.sthr_pk;
+      asm volatile("" : "+s"(th), "+s"(thp));   // the thresholds are read per iteration (hoisted: SGPR spills)
 #pragma unroll
       for (int r = 0; r < W; ++r) {
-        uint32_t U[16];
-        settle_sel_words(ge_lo, ge_hi, st_lo, k, r, N, u_k0, u_k1, U);
-        PBN_PSTAMP_AT(it - kSettleStampIt + 10, 18);
+        if constexpr (NQ > 0) {
+          uint32_t U[16];
+          settle_sel_words(ge_lo, ge_hi, st_lo, k, r, N, s_k0, s_k1, U);
+          PBN_PSTAMP_AT(it - kSettleStampIt + 10, 18);
+          if constexpr (PK) {
 #pragma unroll
-        for (int q = 0; q < kNodeRecs - 1; ++q) {
-          if (q < lq) {
-            const uint32_t lt = settle_lt_word(U, th + (size_t)(q * W + r) * 32);
-            lt_out[q * 64 * W + 32 * r + l32] = lane_transpose32(lt, lane);
+            for (int j = 0; j < 16; ++j) U[j] ^= 0x80008000u;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+              const uint32_t lt = settle_lt_word_pk(U, thp + (size_t)(q * W + r) * 16);
+              lt_out[q * 64 * W + 32 * r + pk_node] = lane_transpose32<kSettlePL16>(lt, lane);
+            }
+          } else {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+              const uint32_t lt = settle_lt_word(U, th + (size_t)(q * W + r) * 32);
+              lt_out[q * 64 * W + 32 * r + l32] = lane_transpose32<kSettlePL16>(lt, lane);
+            }
           }
         }
       }
@@ -2170,6 +2305,16 @@ pbn_rollout_settle(StepArgs a) {
       lds_barrier();
       PBN_PSTAMP(it - kSettleStampIt + 10, 2);
       p.done();
+    }
+    };
+    const bool pk = __builtin_amdgcn_readfirstlane(a.settle_pk) != 0;
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    switch (min(mnf - 1, kNodeRecs - 1)) {   // (lq >= 1 in the slot layout; one function per node needs no draws)
+      case 0: sel_loop(std::integral_constant<int, 0>{}, F_{}); break;
+      case 1: pk ? sel_loop(std::integral_constant<int, 1>{}, T_{}) : sel_loop(std::integral_constant<int, 1>{}, F_{}); break;
+      case 2: pk ? sel_loop(std::integral_constant<int, 2>{}, T_{}) : sel_loop(std::integral_constant<int, 2>{}, F_{}); break;
+      default: pk ? sel_loop(std::integral_constant<int, 3>{}, T_{}) : sel_loop(std::integral_constant<int, 3>{}, F_{}); break;
     }
   } else {
     // ---- state of env `lane` (env-major), bit-sliced per update for the node chains
@@ -2183,8 +2328,26 @@ pbn_rollout_settle(StepArgs a) {
 #pragma unroll
       for (int w = 0; w < W; ++w) LANE_STV(a.obs, (size_t)w * n + (size_t)le, (size_t)n_steps * plane, 7, st[w]);
     }
+    // the epilogue's output bases, held in VGPRs (laundered each iteration): as SGPRs they came
+    // from the kernel arguments' 16-dword load tuples, which the allocator spilled and restored
+    // whole (16 v_readlane_b32 per tuple) to use two of them
+    uint32_t* o_final = a.final_state;
+    uint16_t* o_upd = a.updates;
+    float* o_rew = a.reward;
+    uint8_t* o_flags = a.flags;
+    uint32_t* o_obs = a.obs;
+    // one loop per function count KF (mnf, at most kNodeRecs): no switch inside the loop
+    auto state_loop = [&](auto kf_c) __attribute__((always_inline)) {
+    constexpr int KF = decltype(kf_c)::value;
+    // single-word states: the node records' input indices held in VGPRs, and each update's
+    // selection planes and selectors read before the transpose (as pbn_rollout_pipe's state_fast),
+    // so that their LDS latency is off the chain slot -> transpose -> gathers -> back-transpose
+    uint32_t ins[KF];
+#pragma unroll
+    for (int q = 0; q < KF; ++q) ins[q] = W == 1 ? recL[q * 32 + l32].x : 0u;
     EnvPlan p;
     for (uint32_t it = 0;; ++it) {
+      PBN_ISA_LOOP("settle_state", KF);
       PBN_PSTAMP(it - kSettleStampIt + 10, 0);
       if (__ballot(Ct < n_steps) == 0 || (uint64_t)it > max_it) break;
       p.next(Ct, Ck, K);
@@ -2208,30 +2371,49 @@ pbn_rollout_settle(StepArgs a) {
         pcv = (info >> 8) & 0xFFu;
         pacc = false;
       }
-#pragma unroll
-      for (int w = 0; w < W; ++w) Sg[32 * w + l32] = lane_transpose32(s1[w], lane);
-      PBN_PSTAMP_AT(it - kSettleStampIt + 10, 15);
-      __builtin_amdgcn_wave_barrier();
       uint32_t X[W];
+      if constexpr (W == 1) {
+        uint32_t ltv[KF];
+        uint4 sa[KF], sb[KF];
 #pragma unroll
-      for (int r = 0; r < W; ++r) {
-        int i = l32 + 32 * r;
-        asm volatile("" : "+v"(i));   // selector and record reads stay in the loop
-        const uint4* rc = recL + i;
-        const uint4* sel = selq + i;
-        const uint32_t* lti = lt_in + i;
-        switch (mnf) {
-          case 1: X[r] = chain_padded<1, (W <= 2)>(rc, sel, 32 * W, Sg, lti, 64 * W); break;
-          case 2: X[r] = chain_padded<2, (W <= 2)>(rc, sel, 32 * W, Sg, lti, 64 * W); break;
-          case 3: X[r] = chain_padded<3, (W <= 2)>(rc, sel, 32 * W, Sg, lti, 64 * W); break;
-          default: X[r] = chain_padded<4, (W <= 2)>(rc, sel, 32 * W, Sg, lti, 64 * W); break;
+        for (int q = 0; q < KF; ++q) {
+          ltv[q] = q < KF - 1 ? lt_in[q * 64 + l32] : 0u;
+          sa[q] = selq[(2 * q) * 32 + l32];
+          sb[q] = selq[(2 * q + 1) * 32 + l32];
+        }
+        Sg[l32] = lane_transpose32<kSettlePL16>(s1[0], lane);
+        PBN_PSTAMP_AT(it - kSettleStampIt + 10, 15);
+        __builtin_amdgcn_wave_barrier();
+        uint32_t x = 0;
+#pragma unroll
+        for (int q = KF - 1; q >= 0; --q) {
+          uint32_t xin[4];
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) xin[kk] = plane_in<true>(Sg, ins[q], kk);
+          const uint32_t fj = eval_sel_in(xin, sa[q], sb[q]);
+          x = (q == KF - 1) ? fj : bfi(ltv[q], fj, x);
+        }
+        X[0] = x;
+      } else {
+#pragma unroll
+        for (int w = 0; w < W; ++w) Sg[32 * w + l32] = lane_transpose32<kSettlePL16>(s1[w], lane);
+        PBN_PSTAMP_AT(it - kSettleStampIt + 10, 15);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int r = 0; r < W; ++r) {
+          int i = l32 + 32 * r;
+          asm volatile("" : "+v"(i));   // selector and record reads stay in the loop
+          const uint4* rc = recL + i;
+          const uint4* sel = selq + i;
+          const uint32_t* lti = lt_in + i;
+          X[r] = chain_padded<KF, (W <= 2)>(rc, sel, 32 * W, Sg, lti, 64 * W);
         }
       }
       PBN_PSTAMP_AT(it - kSettleStampIt + 10, 3);
       uint32_t cur[W];
 #pragma unroll
       for (int w = 0; w < W; ++w) {
-        const uint32_t x = lane_transpose32(X[w], lane);
+        const uint32_t x = lane_transpose32<kSettlePL16>(X[w], lane);
         cur[w] = proc ? (pk ? s1[w] ^ gam[w] : x) : st[w];
       }
       PBN_PSTAMP_AT(it - kSettleStampIt + 10, 12);
@@ -2246,14 +2428,18 @@ pbn_rollout_settle(StepArgs a) {
       ctl[(it & 1) * 64 + lane] = make_uint2(Ct, Ck);
 #pragma unroll
       for (int w = 0; w < W; ++w) st[w] = cur[w];
+      asm volatile("" : "+v"(o_final), "+v"(o_upd), "+v"(o_rew), "+v"(o_flags), "+v"(o_obs));
       if (end) {
-        // the epilogue of step t
+        // the epilogue of step t: one element index for every output (computed once, ahead of the
+        // stores' uniform branches; n < 2^31, so t * n + le is one v_mad_u64_u32)
         const size_t tz = t;
+        const size_t er = (uint64_t)t * (uint32_t)n + (uint64_t)(uint32_t)le;    // [t][n] outputs
+        const size_t ep = W == 1 ? er : tz * plane + (size_t)le;                   // [t][W][n] outputs
         if (u_fl & 2u) {
 #pragma unroll
-          for (int w = 0; w < W; ++w) LANE_STV(a.final_state, (tz * plane + (size_t)w * n) + (size_t)le, (size_t)n_steps * plane, 10, cur[w]);
+          for (int w = 0; w < W; ++w) LANE_STV(o_final, ep + (size_t)w * n, (size_t)n_steps * plane, 10, cur[w]);
         }
-        if (u_fl & 32u) LANE_STV(a.updates, (tz * n) + (size_t)le, (size_t)n_steps * n, 23, (uint16_t)min(k + 1, 0xFFFFu));
+        if (u_fl & 32u) LANE_STV(o_upd, er, (size_t)n_steps * n, 23, (uint16_t)min(k + 1, 0xFFFFu));
         const bool in_attr = att >= 0;
         const bool term = in_attr && (uint32_t)att == tg0;
         const bool wrong = in_attr && !term;
@@ -2264,21 +2450,28 @@ pbn_rollout_settle(StepArgs a) {
         const uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) |
                             ((uint32_t)pacc << 3) | ((uint32_t)rst << 4) | ((uint32_t)open << 5);
         const float4 r4 = reinterpret_cast<const float4*>(rtab)[pcv];
-        LANE_STV(a.reward, (tz * n) + (size_t)le, (size_t)n_steps * n, 11, term ? r4.z : (wrong ? r4.y : r4.x));
-        LANE_STV(a.flags, (tz * n) + (size_t)le, (size_t)n_steps * n, 15, (uint8_t)fl);
+        LANE_STV(o_rew, er, (size_t)n_steps * n, 11, term ? r4.z : (wrong ? r4.y : r4.x));
+        LANE_STV(o_flags, er, (size_t)n_steps * n, 15, (uint8_t)fl);
         tg0 = rst ? rtv : tg0;
         tt0 = rst ? 0u : (uint32_t)tt;
 #pragma unroll
         for (int w = 0; w < W; ++w) st[w] = rst ? rs[w] : cur[w];
         if ((u_fl & 1u) && tz + 1 < n_steps) {
 #pragma unroll
-          for (int w = 0; w < W; ++w) LANE_STV(a.obs, ((tz + 1) * plane + (size_t)w * n) + (size_t)le, (size_t)n_steps * plane, 7, st[w]);
+          for (int w = 0; w < W; ++w) LANE_STV(o_obs, ep + plane + (size_t)w * n, (size_t)n_steps * plane, 7, st[w]);
         }
       }
       PBN_PSTAMP(it - kSettleStampIt + 10, 1);
       lds_barrier();
       PBN_PSTAMP(it - kSettleStampIt + 10, 2);
       p.done();
+    }
+    };
+    switch (mnf) {
+      case 1: state_loop(std::integral_constant<int, 1>{}); break;
+      case 2: state_loop(std::integral_constant<int, 2>{}); break;
+      case 3: state_loop(std::integral_constant<int, 3>{}); break;
+      default: state_loop(std::integral_constant<int, 4>{}); break;
     }
     if (valid) {
 #pragma unroll

@@ -125,3 +125,27 @@ def test_settle_stats_iterations_and_launch_tail():
     assert s["launch_iterations_per_step"] == pytest.approx(68 / 3)
     assert s["launch_tail"] == pytest.approx(68 / (sum(per_env) / 64))
     assert s["updates_quantiles"]["max"] == 64
+
+
+def test_update_flops_are_five_row_forwards():
+    assert bench.update_flops(28, 256) == 5 * 256 * bench.qnet_flops_per_env(28)
+    assert bench.update_flops(7, 32, 2) == 5 * 32 * bench.qnet_flops_per_env(7, 2)
+
+
+def test_cpu_training_frame_baseline_runs_one_update_per_frame():
+    """bench.py --workload bdq-learn's cpu_baseline: acting frame + ring store + bdq_update on CPU."""
+    import torch
+
+    from pbn_rl_amd.attractors import load_attractors
+    from pbn_rl_amd.network import load_network
+    from pbn_rl_amd.spec import EnvSpec
+
+    spec = EnvSpec(load_network("pbn7"), load_attractors("pbn7"), perturbation=0.01, horizon=20)
+    torch.manual_seed(0)
+    q = BranchingQNetwork((spec.n, spec.n), spec.n + 1, 3)
+    before = [p.detach().clone() for p in q.parameters()]
+    cb = bench.cpu_baseline_bdq_learn(spec, q, 256, 0.05, 1)
+    assert cb["kind"] == "port" and cb["cores"] == 1 and cb["value"] > 0
+    assert "update_policy" in cb["sample"]
+    # the baseline trains a copy: the caller's network is untouched
+    assert all(torch.equal(a, b) for a, b in zip(before, q.parameters()))

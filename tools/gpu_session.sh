@@ -23,13 +23,17 @@
 #   bdqpmc           the BDQ frame under two PMC passes: L2 hits / misses / requests, HBM fetch + write
 #   handoff          the world-1 hand-off pass alone (tools/handoff_trace.py, plans 20 and 10,10) and its
 #                    rocprofv3 kernel + memory-copy trace, attributed per rep
+#   budget           the one-update kernel's instruction and LDS counters at 2,000 steps (65,536 envs)
+#                    and at 1M envs, two PMC passes each, for tools/isa_budget.py --pmc (issue model)
 #   ubench           tools/ubench_valu_issue (VALU issue rates by instruction and waves per SIMD)
 #   nofinal          the driver's command and 2,000 steps without s' (--no-final-state)
-#   abenv            every pbn_rl_amd/libpbn_env_diag_*.so, then this tree: tests/test_gpu_parity.py,
+#   abenv            every pbn_rl_amd/libpbn_env_diag_*.so but diag_s_*, then this tree: tests/test_gpu_parity.py,
 #                    the driver's command, 2,000 steps and 1M envs (env rollout variants)
 #   abbdq            every pbn_rl_amd/libpbn_env_diag_q*.so, then this tree: tests/test_gpu_agent.py
 #                    and the BDQ frame (frame and tail-launch times; Q-network tail variants)
 #   ab70             A/B: pbn70 x 1M and pbn28 x 1M, pbn_rl_amd/libpbn_env_diag_base.so, then this tree
+#   absettle         every pbn_rl_amd/libpbn_env_diag_s_*.so, then this tree: tests/test_gpu_settle.py,
+#                    the settle law at the driver's shape (20 steps) and at 200 steps (settle kernel variants)
 #   ab               A/B: the driver's command, 2,000 steps and the BDQ frame, first with
 #                    pbn_rl_amd/libpbn_env_diag_base.so (tools/ab_build.sh REV), then this tree
 set -o pipefail
@@ -111,6 +115,19 @@ for step in "$@"; do
         python tools/handoff_trace.py --plan 20 > "$out/handoff_trace.json" 2> "$out/handoff_trace.err" || fail handoff-trace
       python tools/handoff_trace.py --summarize "$out/handoff_trace" > "$out/handoff_summary.json" || fail handoff-summary
       echo "handoff done" ;;
+    budget)
+      for shape in "s2000:--steps 2000 --warmup 200" "1m:--envs 1048576 --steps 500 --warmup 100"; do
+        nm=${shape%%:*}; args=${shape#*:}
+        timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_WR \
+          SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --kernel-trace --stats --output-format csv \
+          -d "$out/budget_${nm}_a" -o run -- python bench.py --no-cpu-baseline --no-gather --settle-line 0 $args \
+          > "$out/budget_${nm}_a.json" 2> "$out/budget_${nm}_a.err" || fail "budget-$nm-a"
+        timeout -k 10 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS \
+          SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --kernel-trace --stats \
+          --output-format csv -d "$out/budget_${nm}_b" -o run -- python bench.py --no-cpu-baseline --no-gather \
+          --settle-line 0 $args > "$out/budget_${nm}_b.json" 2> "$out/budget_${nm}_b.err" || fail "budget-$nm-b"
+        echo "budget $nm done"
+      done ;;
     ubench)
       timeout -k 10 300 tools/ubench_valu_issue > "$out/ubench_valu_issue.jsonl" 2> "$out/ubench.err" || fail ubench
       echo "ubench done" ;;
@@ -144,14 +161,24 @@ for step in "$@"; do
       done
       unset PBN_LIB ;;
     abenv)
-      for lib in pbn_rl_amd/libpbn_env_diag_*.so tree; do
+      for lib in pbn_rl_amd/libpbn_env_diag_[!s]*.so tree; do
         side=$(basename "$lib" .so); side=${side#libpbn_env_diag_}
         if [ "$lib" = tree ]; then unset PBN_LIB; else export PBN_LIB=$PWD/$lib; fi
         timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread \
           > "$out/abenv_${side}_parity.log" 2>&1 || { tail -20 "$out/abenv_${side}_parity.log"; fail "abenv $side parity"; }
-        bench abenv_${side}_driver --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-gather
-        bench abenv_${side}_s2000 --steps 2000 --warmup 200 --no-cpu-baseline --no-gather
-        bench abenv_${side}_1m --envs 1048576 --steps 300 --warmup 50 --no-cpu-baseline --no-gather
+        bench abenv_${side}_driver --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-gather --settle-line 0
+        bench abenv_${side}_s2000 --steps 2000 --warmup 200 --no-cpu-baseline --no-gather --settle-line 0
+        bench abenv_${side}_1m --envs 1048576 --steps 300 --warmup 50 --no-cpu-baseline --no-gather --settle-line 0
+      done
+      unset PBN_LIB ;;
+    absettle)
+      for lib in pbn_rl_amd/libpbn_env_diag_s_*.so tree; do
+        side=$(basename "$lib" .so); side=${side#libpbn_env_diag_s_}
+        if [ "$lib" = tree ]; then unset PBN_LIB; else export PBN_LIB=$PWD/$lib; fi
+        timeout -k 10 300 python -u -m pytest tests/test_gpu_settle.py -m gpu -x -q --timeout 120 --timeout-method thread \
+          > "$out/absettle_${side}_settle.log" 2>&1 || { tail -20 "$out/absettle_${side}_settle.log"; fail "absettle $side"; }
+        bench absettle_${side}_d20 --gpus 1 --steps 20 --warmup 5 --settle 64 --no-cpu-baseline --no-gather
+        bench absettle_${side}_s200 --steps 200 --warmup 20 --settle 64 --no-cpu-baseline --no-gather
       done
       unset PBN_LIB ;;
     *) echo "unknown step $step"; exit 2 ;;

@@ -51,13 +51,13 @@ def segments(full, it):
 
 
 SETTLE_ROLES = {
-    "state": [("slot reads, reset / flip planes, S store", 0, 15), ("gathers + mux chains", 15, 3),
-              ("perturb / proc select + back-transpose", 3, 12), ("hash, decision, C / end-info writes", 12, 1),
-              ("barrier wait", 1, 2)],
-    "env draws": [("epilogues of the steps ended last iteration", 4, 16), ("ENV / SETTLE_ENV call, step draws, gaps", 16, 17),
-                  ("flip / perturbation / reset planes, slot writes", 17, 5), ("barrier wait", 5, 6)],
-    "selection": [("SETTLE_SEL Philox calls (4 per env)", 8, 18), ("env-major compares, transposes, slot writes", 18, 9),
-                  ("barrier wait", 9, 10)],
+    "state": [("plan, slot reads, transpose to bit planes + plane store", 0, 15), ("gathers + mux chains", 15, 3),
+              ("back-transpose, perturbed / idle select", 3, 12),
+              ("attractor lookup, decision C, epilogue at a step's end, stores", 12, 1), ("barrier wait", 1, 2)],
+    "env draws": [("decision C read, plan", 4, 16), ("ENV / SETTLE_ENV call, draws, gaps, flip-mask store", 16, 17),
+                  ("slot writes", 17, 5), ("barrier wait", 5, 6)],
+    "selection": [("decision C read, plan, SETTLE_SEL calls (4 per env)", 8, 18),
+                  ("env-major compares, transposes to planes, slot writes", 18, 9), ("barrier wait", 9, 10)],
 }
 
 
