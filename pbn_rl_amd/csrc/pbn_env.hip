@@ -654,7 +654,9 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   // pbn_rollout_settle: S planes [64W] | 2 slots {flip mask, perturbation mask, reset state [3W][64],
   // reset target and action count [64], selection planes [lq][64W]} | C [parity][64]{t, k}
   net->slot_words_settle = 192 * W + 64 + net->lq * 64 * W;
-  net->lds_settle = ((size_t)net->tab_words + 64 * (size_t)W + 2 * (size_t)net->slot_words_settle + 256) * 4;
+  // + ctl [2][64] uint4 + the packed thresholds [lq][W][16]
+  net->lds_settle = ((size_t)net->tab_words + 64 * (size_t)W + 2 * (size_t)net->slot_words_settle + 512 +
+                     (size_t)net->lq * W * 16) * 4;
   net->pipe = pick_pipe(W, d->prob_bits, net->max_nf > kNodeRecs);
   net->reset = pick_reset(W);
   // multiply-high divisors (exact for the operand ranges used: see actions_from_draw, autoreset)

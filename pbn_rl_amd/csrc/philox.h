@@ -41,16 +41,17 @@ __host__ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32
 constexpr int kPhiloxRounds = 7;
 
 // ctr = (c0, c1, c2, c3), key = (k0, k1); one round: two 32x32->64 products, two 3-input xors,
-// the Weyl key bump (SALU: the key is wave-uniform)
-template <int R = kPhiloxRounds>
+// the Weyl key bump (SALU: the key is wave-uniform).  XM (default 0) is xor-ed into output words
+// 0 and 2 for free, through the last round's keys (the settle law's packed compares bias them).
+template <int R = kPhiloxRounds, uint32_t XM = 0u>
 __host__ __device__ __forceinline__ Word4 philox(uint32_t c0, uint32_t c1, uint32_t c2,
                                                   uint32_t c3, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-    const uint32_t n0 = xor3((uint32_t)(p1 >> 32), c1, k0);
-    const uint32_t n2 = xor3((uint32_t)(p0 >> 32), c3, k1);
+    const uint32_t n0 = xor3((uint32_t)(p1 >> 32), c1, r == R - 1 ? (k0 ^ XM) : k0);
+    const uint32_t n2 = xor3((uint32_t)(p0 >> 32), c3, r == R - 1 ? (k1 ^ XM) : k1);
     c1 = (uint32_t)p1;
     c3 = (uint32_t)p0;
     c0 = n0;

@@ -464,19 +464,9 @@ __device__ __forceinline__ uint32_t perm_sel(int lane) {
 
 // lane k holds row k of a 32x32 bit matrix (per 32-lane half); afterwards lane c holds column c.
 // 11 VALU (J = 16: swizzle + perm; 8: DPP + perm; 4: swizzle + alignbit + bitop3; 2, 1: DPP +
-// alignbit + bitop3) where five transpose_step spend 20.  PL16: the J = 16 stage without the LDS
-// crossbar, v_permlane16_swap (rows 0 <-> 1 and 2 <-> 3 of the wave: lane ^ 16) feeding the same
-// v_perm_b32 with the operands in fixed order: 12 VALU, one LDS round trip fewer on the chain.
-template <bool PL16 = false>
+// alignbit + bitop3) where five transpose_step spend 20.
 __device__ __forceinline__ uint32_t lane_transpose32(uint32_t a, int lane) {
-  if constexpr (PL16) {
-    // r[0]: rows (a0, a0, a2, a2), r[1]: rows (a1, a1, a3, a3) -- own value and partner's in
-    // both; low lanes keep r[0]'s low half and take r[1]'s, high lanes the other way round
-    const auto r = __builtin_amdgcn_permlane16_swap(a, a, false, false);
-    a = __builtin_amdgcn_perm(r[1], r[0], (lane & 16) ? 0x07060302u : 0x05040100u);
-  } else {
-    a = __builtin_amdgcn_perm(swizzle_xor<16>(a), a, perm_sel<16>(lane));
-  }
+  a = __builtin_amdgcn_perm(swizzle_xor<16>(a), a, perm_sel<16>(lane));
   a = __builtin_amdgcn_perm(xor_lane<8>(a, lane), a, perm_sel<8>(lane));
   {
     const uint32_t y = swizzle_xor<4>(a);
@@ -647,6 +637,8 @@ __device__ __forceinline__ void eval_gate_levels(const StepArgs& a, const uint32
 // The settle law's per-env selection (oracle/pbn_oracle.c env_uniforms): the 16 words of env
 // ge's SETTLE_SEL calls 4r .. 4r+3 for update k; node 32r + b's 16-bit field is b & 1 of
 // U[b >> 1].  Calls past the network's last node are not made (U = 0).
+// XM: xor-ed into words 0 and 2 of every call (philox's last-round keys; settle_lt_word_pk's bias)
+template <uint32_t XM = 0u>
 __device__ __forceinline__ void settle_sel_words(uint32_t ge_lo, uint32_t ge_hi, uint32_t st_lo, uint32_t k, int r,
                                                  int N, uint32_t k0, uint32_t k1, uint32_t (&U)[16]) {
   const uint32_t c2 = (pbn::kStreamSettleSel << 28) | (k << 8) | (uint32_t)(4 * r);
@@ -654,7 +646,7 @@ __device__ __forceinline__ void settle_sel_words(uint32_t ge_lo, uint32_t ge_hi,
     PBN_ISA_ARM("sel_all_calls");
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const Word4 P = pbn::philox(ge_lo, st_lo, c2 | (uint32_t)c, ge_hi, k0, k1);
+      const Word4 P = pbn::philox<pbn::kPhiloxRounds, XM>(ge_lo, st_lo, c2 | (uint32_t)c, ge_hi, k0, k1);
       U[4 * c + 0] = P.x; U[4 * c + 1] = P.y; U[4 * c + 2] = P.z; U[4 * c + 3] = P.w;
     }
   } else {
@@ -662,7 +654,7 @@ __device__ __forceinline__ void settle_sel_words(uint32_t ge_lo, uint32_t ge_hi,
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       Word4 P = {0u, 0u, 0u, 0u};
-      if (32 * r + 8 * c < N) P = pbn::philox(ge_lo, st_lo, c2 | (uint32_t)c, ge_hi, k0, k1);
+      if (32 * r + 8 * c < N) P = pbn::philox<pbn::kPhiloxRounds, XM>(ge_lo, st_lo, c2 | (uint32_t)c, ge_hi, k0, k1);
       U[4 * c + 0] = P.x; U[4 * c + 1] = P.y; U[4 * c + 2] = P.z; U[4 * c + 3] = P.w;
     }
   }
@@ -687,10 +679,11 @@ __device__ __forceinline__ uint32_t settle_lt_word(const uint32_t (&U)[16], cons
 
 // settle_lt_word two nodes per instruction: U biased (^ 0x80008000) makes each 16-bit field a
 // signed value whose order is the unsigned one, so the saturating v_pk_sub_i16 of the packed biased
-// thresholds has the sign of (u < C) in bits 15 and 31 of each node pair's difference.  v_perm_b32
-// gathers the sign bytes of two pairs (four nodes) into one word, and four-node word m lands at bit
-// offset m of every byte: bit 8c + m of the result = node 4m + c (pk_lane_node, the inverse, is
-// applied at the planes' LDS write).  39 VALU per 32 nodes where settle_lt_word spends 64.
+// thresholds has the sign of (u < C) in bits 15 and 31 of each node pair's difference.  v_perm_b32's
+// sign-replicating selectors (8-11: byte 1, 3, 5, 7's bit 7 as 0x00 / 0xFF) turn two pairs (four
+// nodes) into four byte masks, and v_and_or_b32 drops four-node word m at bit offset m of every
+// byte: bit 8c + m of the result = node 4m + c (pk_lane_node, the inverse, is applied at the
+// planes' LDS write).  32 VALU per 32 nodes where settle_lt_word spends 64.
 typedef short s16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t settle_lt_word_pk(const uint32_t (&Ub)[16], const uint32_t* Cpk_) {
   ConstU32* Cpk = (ConstU32*)Cpk_;
@@ -702,9 +695,29 @@ __device__ __forceinline__ uint32_t settle_lt_word_pk(const uint32_t (&Ub)[16], 
   uint32_t lt = 0;
 #pragma unroll
   for (int m = 0; m < 8; ++m) {
-    // bytes: node 4m (d[2m] bit 15), 4m+1 (d[2m] bit 31), 4m+2 (d[2m+1] bit 15), 4m+3 (d[2m+1] bit 31)
-    const uint32_t e = __builtin_amdgcn_perm(d[2 * m + 1], d[2 * m], 0x07050301u);
-    lt = pbn::bfi3(0x80808080u >> (7 - m), e >> (7 - m), lt);
+    // byte masks: node 4m (d[2m] bit 15), 4m+1 (d[2m] bit 31), 4m+2 (d[2m+1] bit 15), 4m+3 (d[2m+1] bit 31)
+    const uint32_t e = __builtin_amdgcn_perm(d[2 * m + 1], d[2 * m], 0x0B0A0908u);
+    lt = (e & (0x01010101u << m)) | lt;
+  }
+  return lt;
+}
+// settle_lt_word_pk with the packed thresholds in registers (read from the kernel's LDS copy
+// ahead of the iteration's Philox calls: as scalar loads next to their use, two s_waitcnt on the
+// selection wave's chain)
+__device__ __forceinline__ uint32_t settle_lt_word_pk_v(const uint32_t (&Ub)[16], const uint4 (&Cv)[4]) {
+  uint32_t d[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint4 c4 = Cv[j >> 2];
+    const uint32_t c = (j & 3) == 0 ? c4.x : ((j & 3) == 1 ? c4.y : ((j & 3) == 2 ? c4.z : c4.w));
+    d[j] = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(__builtin_bit_cast(s16x2_t, Ub[j]),
+                                                                     __builtin_bit_cast(s16x2_t, c)));
+  }
+  uint32_t lt = 0;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const uint32_t e = __builtin_amdgcn_perm(d[2 * m + 1], d[2 * m], 0x0B0A0908u);
+    lt = (e & (0x01010101u << m)) | lt;
   }
   return lt;
 }
@@ -1946,12 +1959,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
 // applies R(i-1) (EnvPlan); the state wave publishes each env's decision C (next update) in LDS.
 // Results are bit-identical to pbn_step_wave's settle variants and to oracle/pbn_oracle.c.
 constexpr uint32_t kNoUpd = 0xFFFFFFFFu;
-constexpr uint32_t kSettleStampIt = 300;
-// the settle kernel's transposes take the J = 16 stage through v_permlane16_swap (lane_transpose32)
-#ifndef PBN_SETTLE_PL16
-#define PBN_SETTLE_PL16 1
-#endif
-constexpr bool kSettlePL16 = PBN_SETTLE_PL16 != 0;   // stamps build: the iteration the settle kernel clocks
+constexpr uint32_t kSettleStampIt = 300;   // stamps build: the iteration the settle kernel clocks
 
 // The per-env update plan of pbn_rollout_settle, in that env's lane of every wave (VGPRs; the
 // same values in all three waves).  P = R(i-1), the update the RNG waves produced in the previous
@@ -1979,6 +1987,10 @@ pbn_rollout_settle(StepArgs a) {
   const int lane = threadIdx.x & 63;
   const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (role == 0) __builtin_amdgcn_s_setprio(kStatePrio);
+  // the env-draw wave ahead of the selection wave (it was the iteration's pole at equal priority:
+  // +5 % at the driver's shape, profiles/r05_k_ab.json)
+  if (role == 1) __builtin_amdgcn_s_setprio(1);
+
   const int half = lane >> 5;
   const int l32 = lane & 31;
   const int64_t g = (int64_t)blockIdx.x * 2 + half;
@@ -2004,8 +2016,19 @@ pbn_rollout_settle(StepArgs a) {
   // reset state [W] | k = 0: {reset target, action count} | selection planes [lq][2][32W]
   uint32_t* slots = smem + a.tab_words + 2 * 32 * W;
   constexpr int kGP = 64 * W, kRS = 128 * W, kIN = 192 * W, kLT = 192 * W + 64;
-  uint2* ctl = reinterpret_cast<uint2*>(slots + 2 * (size_t)a.slot_words);   // [parity][64]{t, k}: C per env
-  if (threadIdx.x < 64) ctl[64 + threadIdx.x] = make_uint2(valid ? 0u : n_steps, 0u);   // C before iteration 0:
+  // [parity][64]{C.t, C.k, R.t, R.k}: per env the state wave's decision C and the plan R of the
+  // next iteration (EnvPlan, derived once by the state wave for all three)
+  uint4* ctl = reinterpret_cast<uint4*>(slots + 2 * (size_t)a.slot_words);
+  if (threadIdx.x < 64) {   // C = R = (0, 0) before iteration 0:
+    const uint32_t c0 = valid ? 0u : n_steps;
+    ctl[64 + threadIdx.x] = make_uint4(c0, 0u, c0, 0u);
+  }
+  // the packed thresholds (settle_pk), [lq][W][16] words after ctl: the selection wave reads them
+  // by broadcast LDS reads
+  uint32_t* thr_l = reinterpret_cast<uint32_t*>(ctl + 128);
+  if (a.settle_pk) {
+    for (int i = (int)threadIdx.x; i < lq * W * 16; i += (int)blockDim.x) thr_l[i] = a.sthr_pk[i];
+  }
                                                          // (0, 0); envs of groups past the end: finished
   uint32_t st[W];
   uint32_t tt0 = 0, tg0 = 0;
@@ -2041,15 +2064,15 @@ pbn_rollout_settle(StepArgs a) {
     const uint2* lut = reinterpret_cast<const uint2*>(L + a.gap_lut_off);
     const uint32_t* att_words = L + a.att_off + a.n_attr + 1;
     const uint32_t A = (uint32_t)a.n_attr, n1 = (uint32_t)(N + 1);
-    EnvPlan p;
     for (uint32_t it = 0;; ++it) {
       asm volatile("" : "+s"(u_k0), "+s"(u_k1));
       PBN_ISA_LOOP("settle_env_fast", W);
       PBN_PSTAMP(it - kSettleStampIt + 10, 0);
-      const uint2 C = ctl[((it + 1) & 1) * 64 + lane];
+      uint4 C = ctl[((it + 1) & 1) * 64 + lane];   // {C(i), R(i)}
+      // all four words from one read, ahead of the exit test (split, R came in a second round trip)
+      asm volatile("" : "+v"(C.x), "+v"(C.y), "+v"(C.z), "+v"(C.w));
       if (__ballot(C.x < n_steps) == 0 || (uint64_t)it > max_it) break;
-      p.next(C.x, C.y, K);
-      const uint32_t t = p.Rt, k = p.Rk;
+      const uint32_t t = C.z, k = C.w;
       uint32_t* slot = slots + (size_t)(it & 1) * a.slot_words;
       PBN_PSTAMP_AT(it - kSettleStampIt + 10, 16);
       const bool live = valid && t < n_steps, first = k == 0;
@@ -2130,18 +2153,17 @@ pbn_rollout_settle(StepArgs a) {
       PBN_PSTAMP(it - kSettleStampIt + 10, 1);
       lds_barrier();
       PBN_PSTAMP(it - kSettleStampIt + 10, 2);
-      p.done();
     }
   } else if (role == 1) {
     // ---- the draws of each env's update R(i), env `lane` (general networks and modes)
-    EnvPlan p;
     for (uint32_t it = 0;; ++it) {
       asm volatile("" : "+s"(u_k0), "+s"(u_k1));
       PBN_PSTAMP(it - kSettleStampIt + 10, 0);
-      const uint2 C = ctl[((it + 1) & 1) * 64 + lane];
+      uint4 C = ctl[((it + 1) & 1) * 64 + lane];   // {C(i), R(i)}
+      // all four words from one read, ahead of the exit test (split, R came in a second round trip)
+      asm volatile("" : "+v"(C.x), "+v"(C.y), "+v"(C.z), "+v"(C.w));
       if (__ballot(C.x < n_steps) == 0 || (uint64_t)it > max_it) break;
-      p.next(C.x, C.y, K);
-      const uint32_t t = p.Rt, k = p.Rk;
+      const uint32_t t = C.z, k = C.w;
       uint32_t* slot = slots + (size_t)(it & 1) * a.slot_words;
       PBN_PSTAMP_AT(it - kSettleStampIt + 10, 16);
       uint32_t m[W], gam[W];
@@ -2252,7 +2274,6 @@ pbn_rollout_settle(StepArgs a) {
       PBN_PSTAMP(it - kSettleStampIt + 10, 1);
       lds_barrier();
       PBN_PSTAMP(it - kSettleStampIt + 10, 2);
-      p.done();
     }
   } else if (role == 2) {
     // ---- selection planes of each env's update R(i), env `lane`; one loop per threshold count
@@ -2263,40 +2284,53 @@ pbn_rollout_settle(StepArgs a) {
     auto sel_loop = [&, s_k0 = u_k0, s_k1 = u_k1](auto nq_c, auto pk_c) __attribute__((always_inline)) {
     constexpr int NQ = decltype(nq_c)::value;
     constexpr bool PK = decltype(pk_c)::value;
-    EnvPlan p;
     for (uint32_t it = 0;; ++it) {
       PBN_ISA_LOOP("settle_sel", 2 * NQ + (PK ? 1 : 0));
       PBN_PSTAMP(it - kSettleStampIt + 10, 0);
-      const uint2 C = ctl[((it + 1) & 1) * 64 + lane];
+      uint4 C = ctl[((it + 1) & 1) * 64 + lane];   // {C(i), R(i)}
+      // all four words from one read, ahead of the exit test (split, R came in a second round trip)
+      asm volatile("" : "+v"(C.x), "+v"(C.y), "+v"(C.z), "+v"(C.w));
       if (__ballot(C.x < n_steps) == 0 || (uint64_t)it > max_it) break;
-      p.next(C.x, C.y, K);
-      const uint32_t t = p.Rt, k = p.Rk;   // (no update: the words are computed and discarded)
+      const uint32_t t = C.z, k = C.w;   // (no update: the words are computed and discarded)
+      // PK: this iteration's packed thresholds, requested now (used after the Philox calls)
+      uint4 thv[W][NQ > 0 ? NQ : 1][4];
+      if constexpr (PK) {
+#pragma unroll
+        for (int r = 0; r < W; ++r)
+#pragma unroll
+          for (int q = 0; q < NQ; ++q)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              thv[r][q][c] = reinterpret_cast<const uint4*>(thr_l + (size_t)(q * W + r) * 16)[c];
+            }
+      }
       uint32_t* lt_out = slots + (size_t)(it & 1) * a.slot_words + kLT + half * 32 * W;
       const uint64_t step = a.step + (uint64_t)t;
       const uint32_t st_lo = (uint32_t)step;
       const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
       const uint32_t* th = a.sthr;
-      const uint32_t* thp = a.sthr_pk;
-      asm volatile("" : "+s"(th), "+s"(thp));   // the thresholds are read per iteration (hoisted: SGPR spills)
+      asm volatile("" : "+s"(th));   // the thresholds are read per iteration (hoisted: SGPR spills)
 #pragma unroll
       for (int r = 0; r < W; ++r) {
         if constexpr (NQ > 0) {
           uint32_t U[16];
-          settle_sel_words(ge_lo, ge_hi, st_lo, k, r, N, s_k0, s_k1, U);
+          // PK: the compares' bias (^ 0x80008000) folded into words 0 and 2 of every call
+          settle_sel_words<PK ? 0x80008000u : 0u>(ge_lo, ge_hi, st_lo, k, r, N, s_k0, s_k1, U);
           PBN_PSTAMP_AT(it - kSettleStampIt + 10, 18);
           if constexpr (PK) {
 #pragma unroll
-            for (int j = 0; j < 16; ++j) U[j] ^= 0x80008000u;
+            for (int j = 0; j < 16; ++j)
+              if (j & 1) U[j] ^= 0x80008000u;   // words 1 and 3 (the low products) are not
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
-              const uint32_t lt = settle_lt_word_pk(U, thp + (size_t)(q * W + r) * 16);
-              lt_out[q * 64 * W + 32 * r + pk_node] = lane_transpose32<kSettlePL16>(lt, lane);
+              const uint32_t lt = settle_lt_word_pk_v(U, thv[r][q]);
+              lt_out[q * 64 * W + 32 * r + pk_node] = lane_transpose32(lt, lane);
             }
           } else {
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
               const uint32_t lt = settle_lt_word(U, th + (size_t)(q * W + r) * 32);
-              lt_out[q * 64 * W + 32 * r + l32] = lane_transpose32<kSettlePL16>(lt, lane);
+              lt_out[q * 64 * W + 32 * r + l32] = lane_transpose32(lt, lane);
             }
           }
         }
@@ -2304,7 +2338,6 @@ pbn_rollout_settle(StepArgs a) {
       PBN_PSTAMP(it - kSettleStampIt + 10, 1);
       lds_barrier();
       PBN_PSTAMP(it - kSettleStampIt + 10, 2);
-      p.done();
     }
     };
     const bool pk = __builtin_amdgcn_readfirstlane(a.settle_pk) != 0;
@@ -2346,11 +2379,11 @@ pbn_rollout_settle(StepArgs a) {
 #pragma unroll
     for (int q = 0; q < KF; ++q) ins[q] = W == 1 ? recL[q * 32 + l32].x : 0u;
     EnvPlan p;
+    p.next(Ct, Ck, K);   // iteration 0's plan (then each iteration's, at the end of the one before)
     for (uint32_t it = 0;; ++it) {
       PBN_ISA_LOOP("settle_state", KF);
       PBN_PSTAMP(it - kSettleStampIt + 10, 0);
       if (__ballot(Ct < n_steps) == 0 || (uint64_t)it > max_it) break;
-      p.next(Ct, Ck, K);
       const bool proc = p.v && p.Pt < n_steps;
       const uint32_t t = p.Pt, k = p.Pk;
       const uint32_t* slot = slots + (size_t)((it + 1) & 1) * a.slot_words;
@@ -2381,7 +2414,7 @@ pbn_rollout_settle(StepArgs a) {
           sa[q] = selq[(2 * q) * 32 + l32];
           sb[q] = selq[(2 * q + 1) * 32 + l32];
         }
-        Sg[l32] = lane_transpose32<kSettlePL16>(s1[0], lane);
+        Sg[l32] = lane_transpose32(s1[0], lane);
         PBN_PSTAMP_AT(it - kSettleStampIt + 10, 15);
         __builtin_amdgcn_wave_barrier();
         uint32_t x = 0;
@@ -2396,7 +2429,7 @@ pbn_rollout_settle(StepArgs a) {
         X[0] = x;
       } else {
 #pragma unroll
-        for (int w = 0; w < W; ++w) Sg[32 * w + l32] = lane_transpose32<kSettlePL16>(s1[w], lane);
+        for (int w = 0; w < W; ++w) Sg[32 * w + l32] = lane_transpose32(s1[w], lane);
         PBN_PSTAMP_AT(it - kSettleStampIt + 10, 15);
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -2413,7 +2446,7 @@ pbn_rollout_settle(StepArgs a) {
       uint32_t cur[W];
 #pragma unroll
       for (int w = 0; w < W; ++w) {
-        const uint32_t x = lane_transpose32<kSettlePL16>(X[w], lane);
+        const uint32_t x = lane_transpose32(X[w], lane);
         cur[w] = proc ? (pk ? s1[w] ^ gam[w] : x) : st[w];
       }
       PBN_PSTAMP_AT(it - kSettleStampIt + 10, 12);
@@ -2425,7 +2458,10 @@ pbn_rollout_settle(StepArgs a) {
         Ct = end ? t + 1 : t;
         Ck = end ? 0u : k + 1;
       }
-      ctl[(it & 1) * 64 + lane] = make_uint2(Ct, Ck);
+      // the next iteration's plan, published with the decision (the RNG waves read it)
+      p.done();
+      p.next(Ct, Ck, K);
+      ctl[(it & 1) * 64 + lane] = make_uint4(Ct, Ck, p.Rt, p.Rk);
 #pragma unroll
       for (int w = 0; w < W; ++w) st[w] = cur[w];
       asm volatile("" : "+v"(o_final), "+v"(o_upd), "+v"(o_rew), "+v"(o_flags), "+v"(o_obs));
@@ -2449,7 +2485,10 @@ pbn_rollout_settle(StepArgs a) {
         const bool rst = (u_fl & 8u) && (term || trunc);
         const uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) |
                             ((uint32_t)pacc << 3) | ((uint32_t)rst << 4) | ((uint32_t)open << 5);
-        const float4 r4 = reinterpret_cast<const float4*>(rtab)[pcv];
+        // the reward row as one 16-byte read (split by the compiler into reads under the term /
+        // wrong branches, it cost two round trips in the epilogue)
+        float4 r4 = reinterpret_cast<const float4*>(rtab)[pcv];
+        asm volatile("" : "+v"(r4.x), "+v"(r4.y), "+v"(r4.z));
         LANE_STV(o_rew, er, (size_t)n_steps * n, 11, term ? r4.z : (wrong ? r4.y : r4.x));
         LANE_STV(o_flags, er, (size_t)n_steps * n, 15, (uint8_t)fl);
         tg0 = rst ? rtv : tg0;
@@ -2464,7 +2503,6 @@ pbn_rollout_settle(StepArgs a) {
       PBN_PSTAMP(it - kSettleStampIt + 10, 1);
       lds_barrier();
       PBN_PSTAMP(it - kSettleStampIt + 10, 2);
-      p.done();
     }
     };
     switch (mnf) {

@@ -165,8 +165,10 @@ def take_uniform(blocks, i, t):
     """A uniform branch from block i to block t: by the PBN_ISA_ARM names first (taken into a
     live arm, or over dead arms only), else taken iff the code it skips (blocks i+1 .. t-1, a
     forward branch) enters an inner loop or holds a launch-anatomy stamp only."""
-    head = [s for s in blocks[t]["lines"] if is_insn(s) or "@arm" in s][:1]
-    if head and "@arm" in head[0]:
+    if blocks[t]["depth"] == 0:   # a loop exit: the walked iteration does not leave the loop
+        return False
+    head = [s for s in blocks[t]["lines"] if "@arm" in s][:1]   # (code sunk into an arm may precede its mark)
+    if head:
         return re.search(r"@arm (\w+)", head[0]).group(1) in ARMS
     if t > i:
         named = arms_in(blocks[i + 1:t])
