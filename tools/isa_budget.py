@@ -313,8 +313,8 @@ def main():
     ap.add_argument("--W", type=int, default=1)
     ap.add_argument("--B", type=int, default=16)
     ap.add_argument("--K", type=int, default=3, help="functions per node at most (pbn28: 3)")
-    ap.add_argument("--arms", default="sel_all_calls",
-                    help="comma-separated live PBN_ISA_ARM names (pbn28: sel_all_calls, N > 24)")
+    ap.add_argument("--arms", default="sel_all_calls,hash",
+                    help="comma-separated live PBN_ISA_ARM names (pbn28: sel_all_calls, N > 24; hash, an attractor table)")
     ap.add_argument("--pk", type=int, default=1, help="settle kernel: the packed two-node compares (settle_pk)")
     ap.add_argument("--listing", default=None, help="reuse this assembly listing")
     ap.add_argument("--json", default=None)
