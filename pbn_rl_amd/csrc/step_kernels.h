@@ -228,9 +228,14 @@ __device__ __forceinline__ T& lane_at(T* base, size_t uniform_elems, uint32_t la
 #else
 #define LANE_ST(base, ubase, le_, len, site, v) (LANE_AT(base, ubase, le_, len, site) = (v))
 #endif
-// LANE_ST with a per-lane element index (pbn_rollout_settle: the two halves of a wave may be
-// at different steps, so the step's base is not wave-uniform)
-#define LANE_STV(base, idx, len, site, v) __builtin_nontemporal_store((v), &(base)[CK((idx), (len), (site))])
+// LANE_ST with a per-lane element index (pbn_rollout_settle: every env is at its own step, so
+// the step's base is not wave-uniform).  Write-back stores, not streaming ones: the few lanes
+// that end a step in an iteration each write one element of a different output row, and a
+// non-temporal partial-line write went to HBM as a whole write each time (WRITE_SIZE 21x the
+// outputs' bytes, r05_t); through the L2 the lines fill up over the iterations before they are
+// written back
+// (r05_u: 495 -> 49 MB written per 20-step launch at config 2, +1 % on the settle line)
+#define LANE_STV(base, idx, len, site, v) ((base)[CK((idx), (len), (site))] = (v))
 __device__ __forceinline__ uint32_t valid_word_mask(int n, int w) {
   const int bits = n - 32 * w;
   return bits >= 32 ? 0xFFFFFFFFu : (bits <= 0 ? 0u : ((1u << bits) - 1u));

@@ -23,6 +23,8 @@
 #   bdqpmc           the BDQ frame under two PMC passes: L2 hits / misses / requests, HBM fetch + write
 #   handoff          the world-1 hand-off pass alone (tools/handoff_trace.py, plans 20 and 10,10) and its
 #                    rocprofv3 kernel + memory-copy trace, attributed per rep
+#   handoff100       the world-1 hand-off pass of four 100-step launches (the 2,000-step line's plan) and its
+#                    kernel + memory-copy trace
 #   budget           the one-update kernel's instruction and LDS counters at 2,000 steps (65,536 envs)
 #                    and at 1M envs, two PMC passes each, for tools/isa_budget.py --pmc (issue model)
 #   ubench           tools/ubench_valu_issue (VALU issue rates by instruction and waves per SIMD)
@@ -32,6 +34,8 @@
 #   abbdq            every pbn_rl_amd/libpbn_env_diag_q*.so, then this tree: tests/test_gpu_agent.py
 #                    and the BDQ frame (frame and tail-launch times; Q-network tail variants)
 #   ab70             A/B: pbn70 x 1M and pbn28 x 1M, pbn_rl_amd/libpbn_env_diag_base.so, then this tree
+#   ablearn          every pbn_rl_amd/libpbn_env_diag_l_*.so, then this tree: tests/test_gpu_learn.py and
+#                    the BDQ training frame (learner kernel variants)
 #   absettle         every pbn_rl_amd/libpbn_env_diag_s_*.so, then this tree: tests/test_gpu_settle.py,
 #                    the settle law at the driver's shape (20 steps) and at 200 steps (settle kernel variants)
 #   ab               A/B: the driver's command, 2,000 steps and the BDQ frame, first with
@@ -115,6 +119,15 @@ for step in "$@"; do
         python tools/handoff_trace.py --plan 20 > "$out/handoff_trace.json" 2> "$out/handoff_trace.err" || fail handoff-trace
       python tools/handoff_trace.py --summarize "$out/handoff_trace" > "$out/handoff_summary.json" || fail handoff-summary
       echo "handoff done" ;;
+    handoff100)
+      timeout -k 10 180 python tools/handoff_trace.py --plan 100,100,100,100 --reps 10 > "$out/handoff_100x4.json" \
+        2> "$out/handoff100.err" || fail "handoff100"
+      cat "$out/handoff_100x4.json"
+      timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$out/handoff100_trace" -o run -- \
+        python tools/handoff_trace.py --plan 100,100,100,100 --reps 10 > "$out/handoff100_trace.json" \
+        2> "$out/handoff100_trace.err" || fail handoff100-trace
+      python tools/handoff_trace.py --summarize "$out/handoff100_trace" > "$out/handoff100_summary.json" || fail handoff100-summary
+      echo "handoff100 done" ;;
     budget)
       for shape in "s2000:--steps 2000 --warmup 200" "1m:--envs 1048576 --steps 500 --warmup 100"; do
         nm=${shape%%:*}; args=${shape#*:}
@@ -171,6 +184,15 @@ for step in "$@"; do
         bench abenv_${side}_1m --envs 1048576 --steps 300 --warmup 50 --no-cpu-baseline --no-gather --settle-line 0
       done
       unset PBN_LIB ;;
+    ablearn)
+      for lib in pbn_rl_amd/libpbn_env_diag_l_*.so tree; do
+        side=$(basename "$lib" .so); side=${side#libpbn_env_diag_l_}
+        if [ "$lib" = tree ]; then unset PBN_LIB; else export PBN_LIB=$PWD/$lib; fi
+        timeout -k 10 300 python -u -m pytest tests/test_gpu_learn.py -m gpu -x -q --timeout 120 --timeout-method thread \
+          > "$out/ablearn_${side}_learn.log" 2>&1 || { tail -20 "$out/ablearn_${side}_learn.log"; fail "ablearn $side"; }
+        bench ablearn_${side}_frame --workload bdq-learn --no-cpu-baseline
+      done
+      unset PBN_LIB ;;
     absettle)
       for lib in pbn_rl_amd/libpbn_env_diag_s_*.so tree; do
         side=$(basename "$lib" .so); side=${side#libpbn_env_diag_s_}
@@ -179,6 +201,9 @@ for step in "$@"; do
           > "$out/absettle_${side}_settle.log" 2>&1 || { tail -20 "$out/absettle_${side}_settle.log"; fail "absettle $side"; }
         bench absettle_${side}_d20 --gpus 1 --steps 20 --warmup 5 --settle 64 --no-cpu-baseline --no-gather
         bench absettle_${side}_s200 --steps 200 --warmup 20 --settle 64 --no-cpu-baseline --no-gather
+        timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats --output-format csv \
+          -d "$out/absettle_${side}_write" -o run -- python bench.py --steps 20 --warmup 5 --settle 64 \
+          --no-cpu-baseline --no-gather > /dev/null 2> "$out/absettle_${side}_write.err" || fail "absettle $side write"
       done
       unset PBN_LIB ;;
     *) echo "unknown step $step"; exit 2 ;;
