@@ -519,7 +519,7 @@ def gather_pass(env, plan, world, local, dev, stream, dst, copy_own=False):
     (ShardedRollout: a ring of two record slots the kernel writes in place; the hand-off of
     launch k runs on the communicator's stream while launch k + 1 runs).  dst = 0: point to
     point to rank 0, which keeps its own shard in place, or with copy_own copies it into its
-    receive slot on a side stream (world 1: the whole hand-off); dst = None:
+    receive slot inside launch k + 1 (pbn_rollout_copy; world 1: the whole hand-off); dst = None:
     all_gather_into_tensor.  Device ms, max over ranks."""
     from pbn_rl_amd.distributed import ShardedRollout
 

@@ -69,7 +69,7 @@
 extern "C" {
 #endif
 
-#define PBN_ABI_VERSION 7
+#define PBN_ABI_VERSION 8
 
 #define PBN_MAX_NODES 128
 #define PBN_MAX_ARITY 4
@@ -226,6 +226,23 @@ int pbn_rollout_ex(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offs
                    int32_t n_steps, uint32_t mode, uint32_t* d_state, uint32_t* d_flipmask, uint8_t* d_target,
                    uint8_t* d_t, uint32_t* d_obs, uint32_t* d_final_state, float* d_reward, uint8_t* d_flags,
                    uint16_t* d_updates, void* stream);
+
+/*
+ * pbn_rollout_ex with a copy riding along (ABI 8): the launch also copies copy_bytes from
+ * d_copy_src to d_copy_dst (16-byte aligned, non-overlapping, neither one of this launch's
+ * buffers).  The copy is complete when the launch is, on the same stream.  The pipelined
+ * one-update kernel spreads it over its env-draw waves (each lane requests its vectors at an
+ * iteration's start and stores them before the iteration's barrier); every other kernel, or a
+ * copy of more than two vectors per env-draw lane and iteration, gets pbn_copy_async right after
+ * the launch.  The world-1 hand-off uses it to move rollout k's records into the learner's
+ * receive slot during rollout k + 1 (pbn_rl_amd/distributed.py ShardedRollout.gather): the
+ * receive half of the gather's point-to-point exchange, for the learner's own shard.
+ */
+int pbn_rollout_copy(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs,
+                     int32_t n_steps, uint32_t mode, uint32_t* d_state, uint32_t* d_flipmask, uint8_t* d_target,
+                     uint8_t* d_t, uint32_t* d_obs, uint32_t* d_final_state, float* d_reward, uint8_t* d_flags,
+                     uint16_t* d_updates, void* d_copy_dst, const void* d_copy_src, int64_t copy_bytes,
+                     void* stream);
 
 /*
  * State histogram, the accumulation step of the steady-state distribution

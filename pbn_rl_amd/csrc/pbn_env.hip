@@ -329,9 +329,13 @@ int pbn_copy_async(void* d_dst, const void* d_src, int64_t bytes, void* stream) 
   const int64_t n16 = bytes / 16;
   int dev = 0, n_cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n_cus, hipDeviceAttributeMultiprocessorCount, dev);
-  // enough blocks to fill every CU several times over, each thread moving 4 vectors per trip
+  // PBN_COPY_BLOCKS_PER_CU blocks per CU at most, each thread moving 4 vectors per trip
+#ifndef PBN_COPY_BLOCKS_PER_CU
+#define PBN_COPY_BLOCKS_PER_CU 8
+#endif
   const int64_t want = (n16 + 4 * 256 - 1) / (4 * 256);
-  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)n_cus * 8));
+  const unsigned blocks =
+      (unsigned)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)n_cus * PBN_COPY_BLOCKS_PER_CU));
   hipLaunchKernelGGL(pbn_copy_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, static_cast<u32x4*>(d_dst),
                      static_cast<const u32x4*>(d_src), n16);
   HIP_OK(hipGetLastError());
@@ -894,14 +898,27 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
                         d_obs, d_final_state, d_reward, d_flags, nullptr, stream);
 }
 
-int pbn_rollout_ex(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs,
-                   int32_t n_steps, uint32_t mode, uint32_t* d_state, uint32_t* d_flipmask, uint8_t* d_target,
-                   uint8_t* d_t, uint32_t* d_obs, uint32_t* d_final_state, float* d_reward, uint8_t* d_flags,
-                   uint16_t* d_updates, void* stream) {
+}  // extern "C"
+
+// pbn_rollout_ex, with (cp_bytes > 0) a copy riding along (pbn_rollout_copy): in the pipelined
+// one-update kernel's env-draw waves when it fits two vectors per lane and iteration, else as
+// pbn_copy_async right after the launch on the same stream
+static int rollout_impl(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs,
+                        int32_t n_steps, uint32_t mode, uint32_t* d_state, uint32_t* d_flipmask, uint8_t* d_target,
+                        uint8_t* d_t, uint32_t* d_obs, uint32_t* d_final_state, float* d_reward, uint8_t* d_flags,
+                        uint16_t* d_updates, void* cp_dst, const void* cp_src, int64_t cp_bytes, void* stream) {
   int rc = check_common(net, env_offset, n_envs);
   if (rc) return rc;
   if (n_steps < 0) return fail(PBN_EINVAL, "n_steps < 0");
-  if (n_envs == 0 || n_steps == 0) return PBN_OK;
+  bool copy_after = cp_bytes > 0;   // cleared when the copy rides along the launch
+  struct After {   // the standalone copy, if it is still owed when the launch has been issued
+    bool& owed;
+    void *dst, *stream;
+    const void* src;
+    int64_t bytes;
+    int finish(int r) { return (r == PBN_OK && owed) ? pbn_copy_async(dst, src, bytes, stream) : r; }
+  } after{copy_after, cp_dst, stream, cp_src, cp_bytes};
+  if (n_envs == 0 || n_steps == 0) return after.finish(PBN_OK);
   if (mode & ~(PBN_MODE_AUTORESET | PBN_MODE_RANDOM_ACTIONS)) return fail(PBN_EINVAL, "unknown mode bits");
   if (!d_state || !d_flipmask || !d_target || !d_t || !d_reward || !d_flags) return fail(PBN_EINVAL, "null buffer");
   if (net->lds_wave > 160 * 1024) return fail(PBN_EINVAL, "network too large for the rollout kernel's LDS");
@@ -932,21 +949,60 @@ int pbn_rollout_ex(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offs
       hipLaunchKernelGGL(net->pipe_settle, dim3((unsigned)pblocks), dim3(192), net->lds_settle,
                          (hipStream_t)stream, a);
       HIP_OK(hipGetLastError());
-      return PBN_OK;
+      return after.finish(PBN_OK);
     }
     // the one-update law applies exactly one synchronous update per env-step
     if (d_updates) HIP_OK(hipMemsetD16Async(d_updates, 1, (size_t)n_steps * (size_t)n_envs, (hipStream_t)stream));
     a.sel_prio = pblocks <= 4 * (int64_t)net->n_cus ? 1 : 0;
+    if (cp_bytes > 0) {   // the ride-along copy: cp_u vectors per env-draw lane and iteration
+      const int64_t n16 = cp_bytes / 16, per = (int64_t)(n_steps + 1) * pblocks * 64;
+      const int64_t u = (n16 + per - 1) / per;
+      if (u <= 2) {
+        a.cp_src = cp_src;
+        a.cp_dst = cp_dst;
+        a.cp_n16 = n16;
+        a.cp_u = (int)u;
+        copy_after = false;
+      }
+    }
     hipLaunchKernelGGL(net->pipe, dim3((unsigned)pblocks), dim3(192), net->lds_pipe,
                        (hipStream_t)stream, a);
     HIP_OK(hipGetLastError());
-    return PBN_OK;
+    return after.finish(PBN_OK);
   }
   const unsigned blocks = (unsigned)((a.n_groups + kWavesPerBlock - 1) / kWavesPerBlock);  // one wave per group
   hipLaunchKernelGGL(net->settle_max >= 2 ? net->wave_settle_lean : net->wave_lean, dim3(blocks),
                      dim3(64 * kWavesPerBlock), net->lds_wave, (hipStream_t)stream, a);
   HIP_OK(hipGetLastError());
-  return PBN_OK;
+  return after.finish(PBN_OK);
+}
+
+extern "C" {
+
+int pbn_rollout_ex(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs,
+                   int32_t n_steps, uint32_t mode, uint32_t* d_state, uint32_t* d_flipmask, uint8_t* d_target,
+                   uint8_t* d_t, uint32_t* d_obs, uint32_t* d_final_state, float* d_reward, uint8_t* d_flags,
+                   uint16_t* d_updates, void* stream) {
+  return rollout_impl(net, seed, step, env_offset, n_envs, n_steps, mode, d_state, d_flipmask, d_target, d_t, d_obs,
+                      d_final_state, d_reward, d_flags, d_updates, nullptr, nullptr, 0, stream);
+}
+
+int pbn_rollout_copy(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs,
+                     int32_t n_steps, uint32_t mode, uint32_t* d_state, uint32_t* d_flipmask, uint8_t* d_target,
+                     uint8_t* d_t, uint32_t* d_obs, uint32_t* d_final_state, float* d_reward, uint8_t* d_flags,
+                     uint16_t* d_updates, void* d_copy_dst, const void* d_copy_src, int64_t copy_bytes,
+                     void* stream) {
+  if (copy_bytes < 0) return fail(PBN_EINVAL, "copy_bytes < 0");
+  if (copy_bytes > 0) {
+    if (!d_copy_dst || !d_copy_src) return fail(PBN_EINVAL, "null copy buffer");
+    if ((copy_bytes & 15) || ((uintptr_t)d_copy_dst & 15u) || ((uintptr_t)d_copy_src & 15u))
+      return fail(PBN_EINVAL, "copy pointers and bytes must be 16-byte aligned");
+    const char* d = static_cast<const char*>(d_copy_dst);
+    const char* s = static_cast<const char*>(d_copy_src);
+    if (d < s + copy_bytes && s < d + copy_bytes) return fail(PBN_EINVAL, "overlapping copy ranges");
+  }
+  return rollout_impl(net, seed, step, env_offset, n_envs, n_steps, mode, d_state, d_flipmask, d_target, d_t, d_obs,
+                      d_final_state, d_reward, d_flags, d_updates, d_copy_dst, d_copy_src, copy_bytes, stream);
 }
 
 }  // extern "C"

@@ -100,7 +100,16 @@ struct StepArgs {
   const uint32_t* sthr_pk;  // the same, node pairs packed biased for settle_lt_word_pk: [lq][W][16]
                             // {(C[2j+1] ^ 0x8000) << 16 | (C[2j] ^ 0x8000)}, C clamped to 65535
   int settle_pk;            // 1: every threshold a compare uses is below 65536 (sthr_pk is exact)
+  // pbn_rollout_copy: cp_n16 16-byte vectors from cp_src to cp_dst ride along the launch, in the
+  // pipelined kernel's env-draw waves (vector (k L + lane id) + u (n_steps + 1) L at iteration k,
+  // u < cp_u, L = the grid's env-draw lanes); 0: none
+  const void* cp_src;
+  void* cp_dst;
+  int64_t cp_n16;
+  int cp_u;
 };
+
+typedef unsigned int pbn_u32x4 __attribute__((ext_vector_type(4)));
 
 // In-kernel phase clocks (cdna_hip_programming.md section 7, "In-kernel stamps"):
 // compiled only into the diagnostic library (-DPBN_STAMPS), never the product.
@@ -434,6 +443,41 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t a, int lane) {
     const auto r = __builtin_amdgcn_permlane16_swap(a, a, false, false);
     return pbn::bfi3(lane_bit_mask<16>(lane), r[0], r[1]);
   }
+}
+
+// the ride-along copy of pbn_rollout_copy, in the env-draw waves: iteration k's vectors are
+// stored before its barrier and iteration k + 1's requested right behind them (cp_next), so the
+// loads' latency hides under a whole iteration (a load at the iteration's start and its store at
+// the end left it exposed: +48 us on a 100-step launch of 65,536 envs, r05_u)
+struct RideCopy {
+  pbn_u32x4 v[2];
+  int64_t i0;
+};
+__device__ __forceinline__ void cp_load(const StepArgs& a, int k, int lane, RideCopy& c) {
+  const int64_t L = (int64_t)gridDim.x * 64;
+  c.i0 = (int64_t)k * L + (int64_t)blockIdx.x * 64 + lane;
+  const int64_t S = (int64_t)(a.n_steps + 1) * L;
+  const pbn_u32x4* src = static_cast<const pbn_u32x4*>(a.cp_src);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int64_t i = c.i0 + u * S;
+    if (u < a.cp_u && i < a.cp_n16) c.v[u] = __builtin_nontemporal_load(src + i);
+  }
+}
+__device__ __forceinline__ void cp_store(const StepArgs& a, const RideCopy& c) {
+  const int64_t L = (int64_t)gridDim.x * 64;
+  const int64_t S = (int64_t)(a.n_steps + 1) * L;
+  pbn_u32x4* dst = static_cast<pbn_u32x4*>(a.cp_dst);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int64_t i = c.i0 + u * S;
+    if (u < a.cp_u && i < a.cp_n16) __builtin_nontemporal_store(c.v[u], dst + i);
+  }
+}
+
+__device__ __forceinline__ void cp_next(const StepArgs& a, int k, int lane, RideCopy& c) {
+  cp_store(a, c);
+  if (k < a.n_steps) cp_load(a, k + 1, lane, c);
 }
 
 // one butterfly stage: lanes without bit J keep their M bits and take the partner's M bits
@@ -1407,6 +1451,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
       const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
       return pbn::philox((uint32_t)ge, (uint32_t)step, pbn::kStreamEnv << 28, ge_hi, u_k0, u_k1);
     };
+    RideCopy rc;   // (pbn_rollout_copy) the vectors of the next iteration's share, in flight
     // one step: this step's draws from E, the next step's ENV call into E_next
     auto env_step = [&](int k, const Word4& E, Word4& E_next) {
       asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
@@ -1496,17 +1541,21 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
           slot[3 * W * 64 + lane] = rt | (pc << 8) | ((uint32_t)pert << 16);
         }
       }
+      if (a.cp_n16) cp_next(a, k, lane, rc);
       PBN_PSTAMP(k, 1);
       lds_barrier();
       PBN_PSTAMP(k, 2);
     };
     // two steps per trip with the ENV words alternating between EA and EB: no copies between steps
     Word4 EA = env_call(0), EB = EA;
+    if (a.cp_n16) cp_load(a, 0, lane, rc);
     for (int k = 0; k <= n_steps; k += 2) {
       env_step(k, EA, EB);
       if (k + 1 <= n_steps) env_step(k + 1, EB, EA);
     }
   } else if (role == 1) {
+    RideCopy rc;
+    if (a.cp_n16) cp_load(a, 0, lane, rc);
     for (int k = 0; k <= n_steps; ++k) {
       asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
       asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
@@ -1614,6 +1663,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
           slot[3 * W * 64 + lane] = rt | (pc << 8) | ((uint32_t)pert << 16);
         }
       }
+      if (a.cp_n16) cp_next(a, k, lane, rc);
       PBN_PSTAMP(k, 1);
       lds_barrier();
     }

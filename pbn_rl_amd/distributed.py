@@ -161,8 +161,10 @@ class ShardedRollout:
         if pend[k] is not None:
             _wait(pend[k])
             pend[k] = None
+        ride = self._take_ride(rec)
+        kw = {"copy": (ride.dst, ride.src)} if ride is not None else {}
         self.env.rollout(steps, flipmasks=flipmasks, random_actions=random_actions, keep_obs=True,
-                         keep_final=True, out=rec.rollout_out())
+                         keep_final=True, out=rec.rollout_out(), **kw)
         self._issued[steps] = self._issued.get(steps, 0) + 1
         rec._slot = k
         return rec
@@ -213,7 +215,7 @@ class ShardedRollout:
                                   dist.get_global_rank(self.group, r) if self.group is not None else r, self.group)
                        for r in range(self.world) if r != dst]
                 if copy_own:
-                    works.append(self._copy_async(out[dst * nbytes:(dst + 1) * nbytes], rec.flat, same_stream=last))
+                    works.append(self._copy_own(out[dst * nbytes:(dst + 1) * nbytes], rec.flat, last))
                 parts = [rec if (r == dst and not copy_own) else
                          TransitionRecords(rec.steps, rec.words, rec.n, flat=out[r * nbytes:(r + 1) * nbytes])
                          for r in range(self.world)]
@@ -230,6 +232,44 @@ class ShardedRollout:
             return parts, work
         _wait(work)
         return parts
+
+    def _copy_own(self, out: torch.Tensor, src: torch.Tensor, last: bool):
+        """The learner's own shard into its receive slot.  On a GPU env whose ``rollout`` takes
+        ``copy=``, the copy rides along the next rollout launch (``pbn_rollout_copy``: no extra
+        kernel, no cross-stream wait); it is issued on the current stream instead if no rollout
+        takes it before the hand-off is waited on, or when nothing follows (``last``)."""
+        takes = getattr(self, "_env_takes_copy", None)
+        if takes is None:
+            takes = self._env_takes_copy = _takes_copy(self.env)
+        if src.is_cuda and takes:
+            self._flush_ride()
+            ride = _Ride(out, src)
+            if last:
+                ride.flush()
+            else:
+                self._ride = ride
+            return ride
+        return self._copy_async(out, src, same_stream=last)
+
+    def _take_ride(self, rec: "TransitionRecords"):
+        """The pending own-shard copy for the launch about to write ``rec`` (None: none, or one
+        that reads ``rec``'s own buffer, which is then issued first)."""
+        ride = getattr(self, "_ride", None)
+        if ride is None or ride.done:
+            self._ride = None
+            return None
+        self._ride = None
+        if ride.src.data_ptr() == rec.flat.data_ptr():
+            ride.flush()
+            return None
+        ride.done = True   # complete when the launch that carries it is, on the current stream
+        return ride
+
+    def _flush_ride(self) -> None:
+        ride = getattr(self, "_ride", None)
+        if ride is not None:
+            ride.flush()
+        self._ride = None
 
     def _copy_async(self, out: torch.Tensor, src: torch.Tensor, same_stream: bool = False):
         """out <- src (pbn_copy_async: 16-byte non-temporal vectors) on a side stream ordered after
@@ -277,6 +317,31 @@ class ShardedRollout:
     def to_global(parts: List[TransitionRecords]) -> Dict[str, torch.Tensor]:
         """Per-rank records -> per-field tensors over all envs in global order (env = last axis)."""
         return {name: torch.cat([p[name] for p in parts], dim=-1) for name, _, _ in _FIELDS}
+
+
+class _Ride:
+    """An own-shard copy waiting for the next rollout launch to carry it (a work object: wait()
+    issues it on the current stream if no launch has taken it yet)."""
+
+    def __init__(self, dst: torch.Tensor, src: torch.Tensor):
+        self.dst, self.src, self.done = dst, src, False
+
+    def flush(self) -> None:
+        if not self.done:
+            _device_copy(self.dst, self.src, torch.cuda.current_stream(self.src.device))
+            self.done = True
+
+    def wait(self) -> None:
+        self.flush()
+
+
+def _takes_copy(env) -> bool:
+    """Whether env.rollout accepts copy= (VectorPBNEnv: pbn_rollout_copy)."""
+    import inspect
+    try:
+        return "copy" in inspect.signature(env.rollout).parameters
+    except (TypeError, ValueError):
+        return False
 
 
 def _device_copy(out: torch.Tensor, src: torch.Tensor, stream) -> None:

@@ -225,13 +225,16 @@ class VectorPBNEnv:
 
     def rollout(self, n_steps: int, flipmasks: Optional[torch.Tensor] = None, random_actions: bool = True,
                 keep_obs: bool = False, keep_final: bool = True, out: Optional[dict] = None,
-                keep_updates: bool = False) -> dict:
+                keep_updates: bool = False, copy: Optional[tuple] = None) -> dict:
         """``n_steps`` env steps in one ``pbn_rollout_ex`` launch (state kept on chip).
 
         flipmasks: optional (n_steps, W, num_envs) interventions (else in-kernel random
         actions when ``random_actions``, else none).  Returns views of
         ``flipmask`` / ``reward`` / ``flags`` (+ ``obs`` / ``final_state`` / ``updates``) shaped
-        (n_steps, ...); pass ``out`` (a previous result) to reuse its buffers."""
+        (n_steps, ...); pass ``out`` (a previous result) to reuse its buffers.
+        ``copy = (dst, src)``: two contiguous device buffers of equal size (16-byte multiples, not
+        this launch's outputs); dst <- src rides along the launch (``pbn_rollout_copy``, done when
+        the launch is)."""
         L = _lib.load()
         n, k = self.n_alloc, self.num_envs
         if out is None or out["_n_steps"] != n_steps:
@@ -246,12 +249,24 @@ class VectorPBNEnv:
             out["flipmask"].zero_()
         ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
         with torch.cuda.device(self.device):
-            _lib.check(L.pbn_rollout_ex(self.net.handle, self.seed, self.step_index, self.env_offset, n, n_steps,
-                                        mode, self.state.data_ptr(), out["flipmask"].data_ptr(),
-                                        self.target.data_ptr(), self.t.data_ptr(), ptr(out["obs"]),
-                                        ptr(out["final_state"]), out["reward"].data_ptr(), out["flags"].data_ptr(),
-                                        ptr(out.get("updates")), self._stream()),
-                       "pbn_rollout_ex")
+            if copy is not None:
+                dst, src = copy
+                if dst.numel() * dst.element_size() != src.numel() * src.element_size():
+                    raise ValueError("copy: dst and src differ in size")
+                _lib.check(L.pbn_rollout_copy(self.net.handle, self.seed, self.step_index, self.env_offset, n,
+                                              n_steps, mode, self.state.data_ptr(), out["flipmask"].data_ptr(),
+                                              self.target.data_ptr(), self.t.data_ptr(), ptr(out["obs"]),
+                                              ptr(out["final_state"]), out["reward"].data_ptr(),
+                                              out["flags"].data_ptr(), ptr(out.get("updates")), dst.data_ptr(),
+                                              src.data_ptr(), src.numel() * src.element_size(), self._stream()),
+                           "pbn_rollout_copy")
+            else:
+                _lib.check(L.pbn_rollout_ex(self.net.handle, self.seed, self.step_index, self.env_offset, n,
+                                            n_steps, mode, self.state.data_ptr(), out["flipmask"].data_ptr(),
+                                            self.target.data_ptr(), self.t.data_ptr(), ptr(out["obs"]),
+                                            ptr(out["final_state"]), out["reward"].data_ptr(),
+                                            out["flags"].data_ptr(), ptr(out.get("updates")), self._stream()),
+                           "pbn_rollout_ex")
         self.step_index += n_steps
         return out
 

@@ -104,8 +104,8 @@ def test_rccl_config4_shard_at_size(rccl_world1):
 
 def test_world1_own_shard_handoff_copies_records():
     """bench.py's value_with_gather hand-off at world 1 (no process group): the learner's own shard
-    copied into its receive slot by pbn_copy_async, on the side stream (overlapping the next
-    rollout) or, for the last hand-off of a run, on the launch stream.  Three overlapped rollouts;
+    copied into its receive slot riding along the next rollout launch (pbn_rollout_copy) or, for
+    the last hand-off of a run, by pbn_copy_async on the launch stream.  Three overlapped rollouts;
     every received slot equals the records the kernel wrote, and the oracle."""
     from pbn_rl_amd.distributed import ShardedRollout
     spec = _spec()
@@ -150,3 +150,39 @@ def test_copy_async_entry_point():
     assert L.pbn_copy_async(None, src.data_ptr(), 16, None) != 0
     assert L.pbn_copy_async(src.data_ptr(), src.data_ptr(), 0, None) == 0
     del ctypes
+
+
+@pytest.mark.parametrize("settle", [0, 6])
+def test_rollout_copy_entry_point(settle):
+    """pbn_rollout_copy: the copy rides along the pipelined launch (sizes up to two vectors per
+    env-draw lane and iteration, ragged ends) or follows it (larger sizes, the settle kernel,
+    n_steps = 0); either way dst == src with the bytes around dst untouched, and the launch's
+    records equal a twin env's plain rollout."""
+    from pbn_rl_amd.attractors import load_attractors
+    from pbn_rl_amd.network import load_network
+    from pbn_rl_amd.spec import EnvSpec
+    from pbn_rl_amd.vector_env import VectorPBNEnv
+    spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.05, settle=settle)
+    n, steps = 8192, 5
+    cap = (steps + 1) * n * 16   # one vector per env-draw lane (64 envs) and iteration
+    envs = [VectorPBNEnv(spec, n, seed=11, device="cuda:0") for _ in range(2)]
+    for e in envs:
+        e.reset()
+    src = torch.randint(0, 256, (2 * cap + 4096,), dtype=torch.uint8, device="cuda")
+    for nbytes, t in ((16, steps), (4096 + 48, steps), (cap, steps), (cap + 16, steps), (2 * cap, steps),
+                      (2 * cap + 16, steps), (4096, 0)):
+        dst = torch.zeros(2 * cap + 4096 + 32, dtype=torch.uint8, device="cuda")
+        got = envs[0].rollout(t, keep_obs=True, copy=(dst[16:16 + nbytes], src[:nbytes]))
+        want = envs[1].rollout(t, keep_obs=True)
+        torch.cuda.synchronize()
+        assert torch.equal(dst[16:16 + nbytes], src[:nbytes]), nbytes
+        assert not dst[:16].any() and not dst[16 + nbytes:].any(), nbytes
+        for name, w in want.items():
+            if not isinstance(w, torch.Tensor):
+                continue
+            g = got[name]
+            if g.dtype == torch.float32:
+                g, w = g.view(torch.int32), w.view(torch.int32)
+            assert torch.equal(g, w), (nbytes, name)
+    with pytest.raises(ValueError):
+        envs[0].rollout(steps, copy=(dst[:32], src[:16]))

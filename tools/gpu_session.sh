@@ -34,6 +34,8 @@
 #   abbdq            every pbn_rl_amd/libpbn_env_diag_q*.so, then this tree: tests/test_gpu_agent.py
 #                    and the BDQ frame (frame and tail-launch times; Q-network tail variants)
 #   ab70             A/B: pbn70 x 1M and pbn28 x 1M, pbn_rl_amd/libpbn_env_diag_base.so, then this tree
+#   abgather         every pbn_rl_amd/libpbn_env_diag_g_*.so, then this tree: the driver's command and 2,000
+#                    steps with the hand-off passes (value_with_gather; hand-off variants)
 #   ablearn          every pbn_rl_amd/libpbn_env_diag_l_*.so, then this tree: tests/test_gpu_learn.py and
 #                    the BDQ training frame (learner kernel variants)
 #   absettle         every pbn_rl_amd/libpbn_env_diag_s_*.so, then this tree: tests/test_gpu_settle.py,
@@ -182,6 +184,15 @@ for step in "$@"; do
         bench abenv_${side}_driver --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-gather --settle-line 0
         bench abenv_${side}_s2000 --steps 2000 --warmup 200 --no-cpu-baseline --no-gather --settle-line 0
         bench abenv_${side}_1m --envs 1048576 --steps 300 --warmup 50 --no-cpu-baseline --no-gather --settle-line 0
+      done
+      unset PBN_LIB ;;
+    abgather)
+      for lib in pbn_rl_amd/libpbn_env_diag_g_*.so tree; do
+        side=$(basename "$lib" .so); side=${side#libpbn_env_diag_g_}
+        if [ "$lib" = tree ]; then unset PBN_LIB; else export PBN_LIB=$PWD/$lib; fi
+        bench abgather_${side}_driver --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --settle-line 0
+        bench abgather_${side}_s2000 --steps 2000 --warmup 200 --no-cpu-baseline --settle-line 0
+        python -c "import json; d=[json.loads(l) for l in open('$out/abgather_${side}_s2000.json') if l.startswith('{')][-1]; print('  with_gather / value', d['value_with_gather'] / d['value'])"
       done
       unset PBN_LIB ;;
     ablearn)
