@@ -514,7 +514,7 @@ def timed(fn, stream, dev, world, local, gate_cycles: int = None, system_fence: 
     return max_over_ranks(ev0.elapsed_time(ev1), world, dev), max_over_ranks(host_s, world, dev)
 
 
-def gather_pass(env, plan, world, local, dev, stream, dst, copy_own=False):
+def gather_pass(env, plan, world, local, dev, stream, dst, copy_own=False, clock_warm=0.0):
     """The timed steps again, the records of every rollout launch handed to the learner
     (ShardedRollout: a ring of two record slots the kernel writes in place; the hand-off of
     launch k runs on the communicator's stream while launch k + 1 runs).  dst = 0: point to
@@ -538,6 +538,12 @@ def gather_pass(env, plan, world, local, dev, stream, dst, copy_own=False):
         for _ in range(2):   # both record slots (and receive slots) allocated before timing
             run()
         torch.cuda.synchronize(dev)
+        # the same untimed clock ramp as the rollout-only run's (the passes before this one end
+        # on the host, and the GPU clock drops while it idles)
+        t_end = time.perf_counter() + clock_warm
+        while time.perf_counter() < t_end:
+            run()
+            torch.cuda.synchronize(dev)
         # the host enqueues every launch and hand-off of the plan while the gate spins (the
         # ring's Python bookkeeping costs more host time per launch than a bare rollout)
         ms, _ = timed(run, stream, dev, world, local, gate_cycles=GATE_CYCLES * (1 + len(plan)))
@@ -847,12 +853,14 @@ def main():
         gplan = plan
         own = world == 1
         for key, dst, what in (("learner", 0, "point-to-point sends of every shard to rank 0" +
-                                              (" (world 1: the learner's own shard copied into its receive slot "
-                                               "on a side stream, device to device)" if own else
+                                              (" (world 1: the learner's own shard copied into its receive slot, "
+                                               "device to device, by a fourth wave of the next rollout "
+                                               "launch)" if own else
                                                " (the learner keeps its own shard in place)")),
                                ("all_gather", None, "torch.distributed.all_gather_into_tensor (RCCL): every "
                                                     "rank receives every shard")):
-            gms, wire = gather_pass(env, gplan, world, local, dev, stream, dst, copy_own=own and dst == 0)
+            gms, wire = gather_pass(env, gplan, world, local, dev, stream, dst, copy_own=own and dst == 0,
+                                    clock_warm=args.clock_warm)
             with_gather[key] = {"value": total_env_steps / (gms * 1e-3), "ms_per_step": gms / args.steps,
                                 "collective": what + "; one hand-off per rollout launch, overlapped with the "
                                               "next launch (two record slots)",

@@ -900,9 +900,13 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
 
 }  // extern "C"
 
-// pbn_rollout_ex, with (cp_bytes > 0) a copy riding along (pbn_rollout_copy): in the pipelined
-// one-update kernel's env-draw waves when it fits two vectors per lane and iteration, else as
-// pbn_copy_async right after the launch on the same stream
+#ifndef PBN_RIDE_PACED   // pbn_rollout_copy's fourth wave: 1 paced by the block barriers, 0 one burst
+#define PBN_RIDE_PACED 1
+#endif
+
+// pbn_rollout_ex, with (cp_bytes > 0) a copy riding along (pbn_rollout_copy): a fourth wave per
+// block of the pipelined one-update kernel, else pbn_copy_async right after the launch on the
+// same stream
 static int rollout_impl(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs,
                         int32_t n_steps, uint32_t mode, uint32_t* d_state, uint32_t* d_flipmask, uint8_t* d_target,
                         uint8_t* d_t, uint32_t* d_obs, uint32_t* d_final_state, float* d_reward, uint8_t* d_flags,
@@ -954,18 +958,19 @@ static int rollout_impl(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env
     // the one-update law applies exactly one synchronous update per env-step
     if (d_updates) HIP_OK(hipMemsetD16Async(d_updates, 1, (size_t)n_steps * (size_t)n_envs, (hipStream_t)stream));
     a.sel_prio = pblocks <= 4 * (int64_t)net->n_cus ? 1 : 0;
-    if (cp_bytes > 0) {   // the ride-along copy: cp_u vectors per env-draw lane and iteration
-      const int64_t n16 = cp_bytes / 16, per = (int64_t)(n_steps + 1) * pblocks * 64;
-      const int64_t u = (n16 + per - 1) / per;
-      if (u <= 2) {
-        a.cp_src = cp_src;
-        a.cp_dst = cp_dst;
-        a.cp_n16 = n16;
-        a.cp_u = (int)u;
-        copy_after = false;
-      }
+    if (cp_bytes > 0) {   // the ride-along copy: a fourth wave per block
+      a.cp_src = cp_src;
+      a.cp_dst = cp_dst;
+      a.cp_n16 = cp_bytes / 16;
+      // paced at U vectors per lane and iteration when the grid's barriers cover the copy with
+      // U <= 4 (one hand-off of this launch's own records: 12 W + 5 bytes per env-step, 64 envs
+      // per block, U = 2 for single-word states), else one burst
+      const int64_t slots = (int64_t)(n_steps + 1) * pblocks * 64;
+      const int64_t u = (a.cp_n16 + slots - 1) / slots;
+      a.cp_u = PBN_RIDE_PACED ? (u <= 1 ? 1 : (u <= 2 ? 2 : (u <= 4 ? 4 : 0))) : 0;
+      copy_after = false;
     }
-    hipLaunchKernelGGL(net->pipe, dim3((unsigned)pblocks), dim3(192), net->lds_pipe,
+    hipLaunchKernelGGL(net->pipe, dim3((unsigned)pblocks), dim3(a.cp_n16 ? 256 : 192), net->lds_pipe,
                        (hipStream_t)stream, a);
     HIP_OK(hipGetLastError());
     return after.finish(PBN_OK);

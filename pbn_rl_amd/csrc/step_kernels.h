@@ -100,9 +100,10 @@ struct StepArgs {
   const uint32_t* sthr_pk;  // the same, node pairs packed biased for settle_lt_word_pk: [lq][W][16]
                             // {(C[2j+1] ^ 0x8000) << 16 | (C[2j] ^ 0x8000)}, C clamped to 65535
   int settle_pk;            // 1: every threshold a compare uses is below 65536 (sthr_pk is exact)
-  // pbn_rollout_copy: cp_n16 16-byte vectors from cp_src to cp_dst ride along the launch, in the
-  // pipelined kernel's env-draw waves (vector (k L + lane id) + u (n_steps + 1) L at iteration k,
-  // u < cp_u, L = the grid's env-draw lanes); 0: none
+  // pbn_rollout_copy: cp_n16 16-byte vectors from cp_src to cp_dst ride along the launch (the
+  // pipelined kernel's fourth wave, ride_copy_wave); 0: none.  cp_u: vectors per lane and step
+  // iteration (paced: the block's share in n_steps + 1 portions, one per block barrier); 0: the
+  // share in one burst
   const void* cp_src;
   void* cp_dst;
   int64_t cp_n16;
@@ -445,39 +446,85 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t a, int lane) {
   }
 }
 
-// the ride-along copy of pbn_rollout_copy, in the env-draw waves: iteration k's vectors are
-// stored before its barrier and iteration k + 1's requested right behind them (cp_next), so the
-// loads' latency hides under a whole iteration (a load at the iteration's start and its store at
-// the end left it exposed: +48 us on a 100-step launch of 65,536 envs, r05_u)
-struct RideCopy {
-  pbn_u32x4 v[2];
-  int64_t i0;
-};
-__device__ __forceinline__ void cp_load(const StepArgs& a, int k, int lane, RideCopy& c) {
-  const int64_t L = (int64_t)gridDim.x * 64;
-  c.i0 = (int64_t)k * L + (int64_t)blockIdx.x * 64 + lane;
-  const int64_t S = (int64_t)(a.n_steps + 1) * L;
+// the ride-along copy of pbn_rollout_copy: a fourth wave per block (launched only when there is a
+// copy) moves the block's contiguous share of the vectors and exits; s_barrier waits for the
+// surviving waves only, so the three step roles run as without it.
+//   burst (cp_u = 0): the share at once, kDepth 1-KB loads per lane in flight;
+//   paced (cp_u = U): the share in n_steps + 1 portions of U vectors per lane, portion k stored
+//   at iteration k's block barrier and requested A = 8 / U iterations ahead, so the copy's HBM
+//   traffic spreads over the launch instead of competing with its first iterations.
+// (The copy folded into the env-draw waves' step loop held every iteration to the loads'
+// latency: +48 us on a 100-step launch of 65,536 envs, r05_u, profiles/r05_u_ride_env_wave.patch.)
+__device__ __forceinline__ void ride_copy_burst(const StepArgs& a, int lane) {
+  constexpr int kDepth = 8;
+  const int64_t per = ((a.cp_n16 + (int64_t)gridDim.x - 1) / (int64_t)gridDim.x + 63) & ~(int64_t)63;
+  const int64_t i0 = (int64_t)blockIdx.x * per;
+  const int64_t i1 = min(i0 + per, a.cp_n16);
   const pbn_u32x4* src = static_cast<const pbn_u32x4*>(a.cp_src);
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int64_t i = c.i0 + u * S;
-    if (u < a.cp_u && i < a.cp_n16) c.v[u] = __builtin_nontemporal_load(src + i);
-  }
-}
-__device__ __forceinline__ void cp_store(const StepArgs& a, const RideCopy& c) {
-  const int64_t L = (int64_t)gridDim.x * 64;
-  const int64_t S = (int64_t)(a.n_steps + 1) * L;
   pbn_u32x4* dst = static_cast<pbn_u32x4*>(a.cp_dst);
+  for (int64_t base = i0 + lane; base < i1; base += kDepth * 64) {
+    pbn_u32x4 v[kDepth];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int64_t i = c.i0 + u * S;
-    if (u < a.cp_u && i < a.cp_n16) __builtin_nontemporal_store(c.v[u], dst + i);
+    for (int u = 0; u < kDepth; ++u)
+      if (base + u * 64 < i1) v[u] = __builtin_nontemporal_load(src + base + u * 64);
+#pragma unroll
+    for (int u = 0; u < kDepth; ++u)
+      if (base + u * 64 < i1) __builtin_nontemporal_store(v[u], dst + base + u * 64);
   }
 }
 
-__device__ __forceinline__ void cp_next(const StepArgs& a, int k, int lane, RideCopy& c) {
-  cp_store(a, c);
-  if (k < a.n_steps) cp_load(a, k + 1, lane, c);
+#ifndef PBN_RIDE_VECS
+#define PBN_RIDE_VECS 4
+#endif
+#ifndef PBN_RIDE_NTLOAD
+#define PBN_RIDE_NTLOAD 1
+#endif
+template <int U>
+__device__ __forceinline__ void ride_copy_paced(const StepArgs& a, int lane) {
+  constexpr int A = PBN_RIDE_VECS / U > 0 ? PBN_RIDE_VECS / U : 1;   // portions in flight: 4 vectors per lane
+  const int iters = a.n_steps + 1;
+  const int64_t per = (int64_t)iters * U * 64;   // the host sized U so that the grid covers cp_n16
+  const int64_t i0 = (int64_t)blockIdx.x * per + lane;
+  const int64_t i1 = a.cp_n16;
+  const pbn_u32x4* src = static_cast<const pbn_u32x4*>(a.cp_src);
+  pbn_u32x4* dst = static_cast<pbn_u32x4*>(a.cp_dst);
+  pbn_u32x4 v[A][U];
+  auto load = [&](int k, pbn_u32x4 (&r)[U]) {
+    if (k >= iters) return;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + ((int64_t)k * U + u) * 64;
+      if (i < i1) r[u] = PBN_RIDE_NTLOAD ? __builtin_nontemporal_load(src + i) : src[i];
+    }
+  };
+  auto store = [&](int k, const pbn_u32x4 (&r)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + ((int64_t)k * U + u) * 64;
+      if (i < i1) __builtin_nontemporal_store(r[u], dst + i);
+    }
+  };
+#pragma unroll
+  for (int j = 0; j < A; ++j) load(j, v[j]);
+  for (int k0 = 0; k0 < iters; k0 += A) {
+#pragma unroll
+    for (int j = 0; j < A; ++j) {
+      const int k = k0 + j;
+      if (k >= iters) return;
+      store(k, v[j]);
+      load(k + A, v[j]);
+      __builtin_amdgcn_s_barrier();   // the block's barrier of iteration k (no LDS to fence)
+    }
+  }
+}
+
+__device__ __forceinline__ void ride_copy_wave(const StepArgs& a, int lane) {
+  switch (a.cp_u) {
+    case 1: ride_copy_paced<1>(a, lane); break;
+    case 2: ride_copy_paced<2>(a, lane); break;
+    case 4: ride_copy_paced<4>(a, lane); break;
+    default: ride_copy_burst(a, lane); break;
+  }
 }
 
 // one butterfly stage: lanes without bit J keep their M bits and take the partner's M bits
@@ -1333,7 +1380,7 @@ __device__ __forceinline__ uint32_t chain_padded(const uint4* __restrict__ rec, 
 // where the compiler's choice is 181: 2 waves) and two words fit 4 waves as they are.
 #define PBN_PIPE_ATTR __attribute__((amdgpu_waves_per_eu(W == 1 ? 6 : (MANY ? (W == 3 ? 3 : 1) : 5), 8)))
 template <int W, int B, bool MANY>
-__global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a) {
+__global__ void __launch_bounds__(256) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a) {
   constexpr int CPN = B / 4;              // selection calls per node
   extern __shared__ uint32_t smem[];
   const int lane = threadIdx.x & 63;
@@ -1414,7 +1461,7 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
     // thread t: record (q, i) = p = t mod 96 and digits [h B/2, (h+1) B/2), h = t / 96 (192
     // threads = two per record: two LDS reads, then B/2 independent writes)
     static_assert((kNodeRecs - 1) * 32 * 2 == 192, "cm build assumes 192 threads");
-    {
+    if (role < 3) {
       const int p = (int)threadIdx.x % ((kNodeRecs - 1) * 32), h = (int)threadIdx.x / ((kNodeRecs - 1) * 32);
       const int i = p & 31, q = p >> 5;
       uint32_t c = 0;
@@ -1428,6 +1475,10 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
       }
     }
     __syncthreads();
+  }
+  if (role == 3) {   // (pbn_rollout_copy) past the block's last __syncthreads
+    ride_copy_wave(a, lane);
+    return;
   }
   // drain the initial state loads here: otherwise the loop-carried st / t / target copies at
   // the bottom of the loop wait on vmcnt(0), which also waits for every store of the step
@@ -1451,7 +1502,6 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
       const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
       return pbn::philox((uint32_t)ge, (uint32_t)step, pbn::kStreamEnv << 28, ge_hi, u_k0, u_k1);
     };
-    RideCopy rc;   // (pbn_rollout_copy) the vectors of the next iteration's share, in flight
     // one step: this step's draws from E, the next step's ENV call into E_next
     auto env_step = [&](int k, const Word4& E, Word4& E_next) {
       asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
@@ -1541,21 +1591,17 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
           slot[3 * W * 64 + lane] = rt | (pc << 8) | ((uint32_t)pert << 16);
         }
       }
-      if (a.cp_n16) cp_next(a, k, lane, rc);
       PBN_PSTAMP(k, 1);
       lds_barrier();
       PBN_PSTAMP(k, 2);
     };
     // two steps per trip with the ENV words alternating between EA and EB: no copies between steps
     Word4 EA = env_call(0), EB = EA;
-    if (a.cp_n16) cp_load(a, 0, lane, rc);
     for (int k = 0; k <= n_steps; k += 2) {
       env_step(k, EA, EB);
       if (k + 1 <= n_steps) env_step(k + 1, EB, EA);
     }
   } else if (role == 1) {
-    RideCopy rc;
-    if (a.cp_n16) cp_load(a, 0, lane, rc);
     for (int k = 0; k <= n_steps; ++k) {
       asm volatile("" : "+s"(u_k0), "+s"(u_k1), "+s"(u_gx), "+s"(u_na), "+s"(u_mnf));
       asm volatile("" : "+s"(u_hb), "+s"(u_hp), "+s"(u_hz), "+s"(u_fl));
@@ -1663,7 +1709,6 @@ __global__ void __launch_bounds__(192) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
           slot[3 * W * 64 + lane] = rt | (pc << 8) | ((uint32_t)pert << 16);
         }
       }
-      if (a.cp_n16) cp_next(a, k, lane, rc);
       PBN_PSTAMP(k, 1);
       lds_barrier();
     }

@@ -13,6 +13,7 @@ the trace: per rep, the rollout kernels, the copy (kernel or DMA), and the gaps 
 import argparse
 import glob
 import json
+import time
 import os
 import sys
 
@@ -44,22 +45,37 @@ def run(args):
                 if w is not None:
                     w.wait()
 
-    for _ in range(2):
-        rep()
-    torch.cuda.synchronize()
-    times = []
-    for _ in range(args.reps):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda._sleep(2_000_000)   # the host enqueues the rep while this spins
-        e0.record(stream)
-        rep()
-        e1.record(stream)
+    def bare():   # the same launches into the same record slots, no hand-off
+        for k in plan:
+            ro.rollout(k)
+
+    def clock(fn):
+        for _ in range(2):
+            fn()
         torch.cuda.synchronize()
-        times.append(e0.elapsed_time(e1) * 1e3)
-    times.sort()
+        t_end = time.perf_counter() + 0.3   # clock ramp, as bench.py's --clock-warm
+        while time.perf_counter() < t_end:
+            fn()
+            torch.cuda.synchronize()
+        times = []
+        for _ in range(args.reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda._sleep(2_000_000)   # the host enqueues the rep while this spins
+            e0.record(stream)
+            fn()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            times.append(e0.elapsed_time(e1) * 1e3)
+        times.sort()
+        return times
+
+    tb = clock(bare)
+    times = clock(rep)
     wire = sum(env.n_alloc * k * (12 * env.words + 5) for k in plan)
     print(json.dumps({"what": "world-1 hand-off pass", "plan": plan, "envs": env.n_alloc, "reps": args.reps,
-                      "us_median": times[len(times) // 2], "us_min": times[0], "wire_bytes": wire}))
+                      "us_median": times[len(times) // 2], "us_min": times[0], "wire_bytes": wire,
+                      "bare_us_median": tb[len(tb) // 2], "bare_us_min": tb[0],
+                      "with_handoff_over_bare": tb[len(tb) // 2] / times[len(times) // 2]}))
 
 
 def summarize(d):
@@ -80,12 +96,24 @@ def summarize(d):
     reps = []
     for a, b in zip(gates, gates[1:] + [len(ev)]):
         seg = ev[a + 1:b]
+        # the rep: the dispatches queued behind the gate run back to back; the first gap past
+        # 20 us ends it (what follows is the next phase's untimed warm-up)
+        for i in range(1, len(seg)):
+            if seg[i][0] - seg[i - 1][1] > 20_000:
+                seg = seg[:i]
+                break
         if not seg:
             continue
         t0 = ev[a][1]
         items = [{"what": w, "start_us": (s - t0) / 1e3, "dur_us": (e - s) / 1e3} for s, e, w in seg]
         reps.append({"span_us": (max(e for _, e, _ in seg) - t0) / 1e3, "items": items})
-    out = {"reps": len(reps), "median_rep": sorted(reps, key=lambda r: r["span_us"])[len(reps) // 2] if reps else None}
+    # the run times the bare launches first, then the hand-off pass (one more dispatch: the last
+    # hand-off's copy)
+    def median(rs):
+        return sorted(rs, key=lambda r: r["span_us"])[len(rs) // 2] if rs else None
+    most = max((len(r["items"]) for r in reps), default=0)
+    out = {"reps": len(reps), "median_rep": median([r for r in reps if len(r["items"]) == most]),
+           "median_bare_rep": median([r for r in reps if len(r["items"]) < most])}
     print(json.dumps(out, indent=1))
 
 
