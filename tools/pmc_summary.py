@@ -14,10 +14,14 @@ import os
 
 
 def mean_counter(path, counter, kernel="pbn_"):
+    """Mean of one counter over the dispatches of the kernel, leaving out the launches that carry
+    the hand-off's own-shard copy (pbn_rollout_copy: the pipelined kernel with a fourth wave)."""
     vals, name = [], None
     with open(path) as f:
         for r in csv.DictReader(f):
-            if r["Counter_Name"] == counter and kernel in r["Kernel_Name"] and "reset" not in r["Kernel_Name"]:
+            ride = "pbn_rollout_pipe" in r["Kernel_Name"] and r.get("Workgroup_Size") == "256"
+            if r["Counter_Name"] == counter and kernel in r["Kernel_Name"] and "reset" not in r["Kernel_Name"] \
+                    and not ride:
                 vals.append(float(r["Counter_Value"]))
                 name = r["Kernel_Name"]
     return sum(vals) / len(vals), len(vals), name
