@@ -107,7 +107,6 @@ def parse():
     if a.workload == "bdq-learn":
         a.learn_graph = not a.no_graph   # the learner captures its own one-frame graph
         a.no_graph = True
-        a.no_cpu_baseline = True   # the CPU baseline restates acting only
     a.steps = a.steps if a.steps is not None else (200 if bdq else 2000)
     a.warmup = a.warmup if a.warmup is not None else (20 if bdq else 200)
     a.envs = a.envs if a.envs is not None else (32768 if bdq else 65536)

@@ -53,7 +53,7 @@ def test_parse_defaults(monkeypatch):
     assert (a.steps, a.warmup, a.envs) == (200, 20, 32768)
     monkeypatch.setattr(sys, "argv", ["bench.py", "--workload", "bdq-learn"])
     a = bench.parse()
-    assert a.learn_graph and a.no_graph and a.no_cpu_baseline
+    assert a.learn_graph and a.no_graph and not a.no_cpu_baseline   # the training frame's own CPU baseline
 
 
 def test_multi_gpu_request_without_gpus_fails_loudly():
