@@ -329,13 +329,12 @@ int pbn_copy_async(void* d_dst, const void* d_src, int64_t bytes, void* stream) 
   const int64_t n16 = bytes / 16;
   int dev = 0, n_cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n_cus, hipDeviceAttributeMultiprocessorCount, dev);
-  // PBN_COPY_BLOCKS_PER_CU blocks per CU at most, each thread moving 4 vectors per trip
-#ifndef PBN_COPY_BLOCKS_PER_CU
-#define PBN_COPY_BLOCKS_PER_CU 8
-#endif
+  // 8 blocks per CU at most, each thread moving 4 vectors per trip (the last hand-off of a run, on
+  // the launch stream: the most blocks that still stream full 1-KB rows per wave)
+  constexpr int64_t kCopyBlocksPerCu = 8;
   const int64_t want = (n16 + 4 * 256 - 1) / (4 * 256);
   const unsigned blocks =
-      (unsigned)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)n_cus * PBN_COPY_BLOCKS_PER_CU));
+      (unsigned)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)n_cus * kCopyBlocksPerCu));
   hipLaunchKernelGGL(pbn_copy_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, static_cast<u32x4*>(d_dst),
                      static_cast<const u32x4*>(d_src), n16);
   HIP_OK(hipGetLastError());
@@ -642,9 +641,7 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   net->lds_wave = ((size_t)net->tab_words + (size_t)kWavesPerBlock * net->wave_words) * 4;
   net->slot_words = (3 * W + 1) * 64 + net->lq * 64 * W;
   // + the selection wave's threshold digit masks (W == 1): [32][sel_mask_stride(B)], lane-major
-  // (or [kNodeRecs - 1][B][32] node-major without PBN_SEL_MASK_B128)
-  const size_t cm_words = PBN_SEL_MASK_B128 ? 32 * (size_t)sel_mask_stride(d->prob_bits)
-                                            : (size_t)(kNodeRecs - 1) * d->prob_bits * 32;
+  const size_t cm_words = 32 * (size_t)sel_mask_stride(d->prob_bits);
   net->lds_pipe = ((size_t)net->tab_words + 64 * (size_t)W + 2 * (size_t)net->slot_words +
                    (W == 1 ? cm_words : 0)) * 4;
   // compact records for the wave kernel: {inputs as bytes, 4-input truth table, threshold, 0}
@@ -900,9 +897,6 @@ int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset,
 
 }  // extern "C"
 
-#ifndef PBN_RIDE_PACED   // pbn_rollout_copy's fourth wave: 1 paced by the block barriers, 0 one burst
-#define PBN_RIDE_PACED 1
-#endif
 
 // pbn_rollout_ex, with (cp_bytes > 0) a copy riding along (pbn_rollout_copy): a fourth wave per
 // block of the pipelined one-update kernel, else pbn_copy_async right after the launch on the
@@ -967,7 +961,7 @@ static int rollout_impl(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env
       // per block, U = 2 for single-word states), else one burst
       const int64_t slots = (int64_t)(n_steps + 1) * pblocks * 64;
       const int64_t u = (a.cp_n16 + slots - 1) / slots;
-      a.cp_u = PBN_RIDE_PACED ? (u <= 1 ? 1 : (u <= 2 ? 2 : (u <= 4 ? 4 : 0))) : 0;
+      a.cp_u = u <= 1 ? 1 : (u <= 2 ? 2 : (u <= 4 ? 4 : 0));
       copy_after = false;
     }
     hipLaunchKernelGGL(net->pipe, dim3((unsigned)pblocks), dim3(a.cp_n16 ? 256 : 192), net->lds_pipe,

@@ -369,11 +369,8 @@ __device__ __forceinline__ uint32_t less_than(const uint32_t (&dig)[16], uint32_
 // and S = 4 x odd puts the 16 lanes of each read quarter on distinct 4-bank groups (conflict
 // free; the node-major layout before it read two masks per ds_read2_b32, at twice the LDS-array
 // cycles per mask)
-#ifndef PBN_SEL_MASK_B128
-#define PBN_SEL_MASK_B128 1
-#endif
 __host__ __device__ constexpr int sel_mask_stride(int B) {
-  return PBN_SEL_MASK_B128 ? 4 * (((3 * B + 3) / 4) | 1) : 0;
+  return 4 * (((3 * B + 3) / 4) | 1);
 }
 template <int B>
 __device__ __forceinline__ uint32_t less_than_cm4(const uint32_t (&dig)[16], const uint32_t* __restrict__ cmq) {
@@ -451,8 +448,9 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t a, int lane) {
 // surviving waves only, so the three step roles run as without it.
 //   burst (cp_u = 0): the share at once, kDepth 1-KB loads per lane in flight;
 //   paced (cp_u = U): the share in n_steps + 1 portions of U vectors per lane, portion k stored
-//   at iteration k's block barrier and requested A = 8 / U iterations ahead, so the copy's HBM
-//   traffic spreads over the launch instead of competing with its first iterations.
+//   at iteration k's block barrier and requested A = 4 / U iterations ahead, so the copy's HBM
+//   traffic spreads over the launch instead of competing with its first iterations (the burst:
+//   0.65x of the bare launches' rate at 2,000 steps, paced 0.89x; r05_y, r05_za).
 // (The copy folded into the env-draw waves' step loop held every iteration to the loads'
 // latency: +48 us on a 100-step launch of 65,536 envs, r05_u, profiles/r05_u_ride_env_wave.patch.)
 __device__ __forceinline__ void ride_copy_burst(const StepArgs& a, int lane) {
@@ -473,15 +471,12 @@ __device__ __forceinline__ void ride_copy_burst(const StepArgs& a, int lane) {
   }
 }
 
-#ifndef PBN_RIDE_VECS
-#define PBN_RIDE_VECS 4
-#endif
-#ifndef PBN_RIDE_NTLOAD
-#define PBN_RIDE_NTLOAD 1
-#endif
+// vectors per lane in flight in the paced copy: 4 measured 0.89x of the bare launches at 2,000
+// steps, 2 0.69x, 8 0.81x, 16 (spills) 0.44x (profiles/r05_za_ab.json, r05_z)
+constexpr int kRideVecs = 4;
 template <int U>
 __device__ __forceinline__ void ride_copy_paced(const StepArgs& a, int lane) {
-  constexpr int A = PBN_RIDE_VECS / U > 0 ? PBN_RIDE_VECS / U : 1;   // portions in flight: 4 vectors per lane
+  constexpr int A = kRideVecs / U > 0 ? kRideVecs / U : 1;   // portions in flight
   const int iters = a.n_steps + 1;
   const int64_t per = (int64_t)iters * U * 64;   // the host sized U so that the grid covers cp_n16
   const int64_t i0 = (int64_t)blockIdx.x * per + lane;
@@ -494,7 +489,7 @@ __device__ __forceinline__ void ride_copy_paced(const StepArgs& a, int lane) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t i = i0 + ((int64_t)k * U + u) * 64;
-      if (i < i1) r[u] = PBN_RIDE_NTLOAD ? __builtin_nontemporal_load(src + i) : src[i];
+      if (i < i1) r[u] = __builtin_nontemporal_load(src + i);   // (plain loads: equal, r05_z)
     }
   };
   auto store = [&](int k, const pbn_u32x4 (&r)[U]) {
@@ -1470,8 +1465,7 @@ __global__ void __launch_bounds__(256) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
       for (int dd = 0; dd < B / 2; ++dd) {
         const int d = h * (B / 2) + dd;
         const uint32_t v = ((c >> (B - 1 - d)) & 1u) ? ~0u : 0u;
-        if constexpr (PBN_SEL_MASK_B128) cm[i * sel_mask_stride(B) + q * B + d] = v;
-        else cm[(q * B + d) * 32 + i] = v;
+        cm[i * sel_mask_stride(B) + q * B + d] = v;
       }
     }
     __syncthreads();
@@ -1719,7 +1713,7 @@ __global__ void __launch_bounds__(256) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
     // SEL calls computed in the same block as this step's compares
     auto sel_fast = [&](auto nq_c) {
       constexpr int NQ = decltype(nq_c)::value;   // thresholds per node: max_nf - 1
-      const uint32_t* cmi = cm + (PBN_SEL_MASK_B128 ? l32 * sel_mask_stride(B) : l32);
+      const uint32_t* cmi = cm + l32 * sel_mask_stride(B);
       uint32_t* lt_base = slots + (3 * W + 1) * 64 + half * 32 * W + l32;
       auto sel_calls = [&](int k, uint32_t (&d)[16]) {
         const uint64_t step = a.step + (uint64_t)k;
@@ -1746,8 +1740,7 @@ __global__ void __launch_bounds__(256) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
           uint32_t* lt_out = lt_base + (size_t)(k & 1) * a.slot_words;
 #pragma unroll
           for (int q = 0; q < NQ; ++q)
-            lt_out[q * 64] = PBN_SEL_MASK_B128 ? less_than_cm4<B>(cur, cmi + q * B)
-                                               : less_than_cm<B>(cur, cmi + (size_t)q * B * 32, 32);
+            lt_out[q * 64] = less_than_cm4<B>(cur, cmi + q * B);
           // keeps the next calls in this block (LLVM would sink them to the loop latch)
 #pragma unroll
           for (int d = 0; d < 16; ++d) asm volatile("" : "+v"(nxt[d]));
@@ -1801,9 +1794,7 @@ __global__ void __launch_bounds__(256) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
               for (int q = 0; q < kNodeRecs - 1; ++q)
                 if (q < nf - 1) {
                   if constexpr (W == 1)
-                    lt_out[q * 64 * W + i] = PBN_SEL_MASK_B128
-                                                 ? less_than_cm<B>(dig, cm + i * sel_mask_stride(B) + q * B, 1)
-                                                 : less_than_cm<B>(dig, cm + (size_t)q * B * 32 + i, 32);
+                    lt_out[q * 64 * W + i] = less_than_cm<B>(dig, cm + i * sel_mask_stride(B) + q * B, 1);
                   else
                     lt_out[q * 64 * W + i] = less_than(dig, recL[q * 32 * W + ic].z, B);
                 }
