@@ -448,7 +448,8 @@ def barrier(world: int, local: int) -> None:
 
 
 # cycles of the spin kernel queued ahead of the start event (~0.1 ms at the shader clock)
-GATE_CYCLES = 250_000
+GATE_CYCLES = 1_000_000   # ≈ 0.4 ms of spin: the host's enqueue behind it (≈ 0.15 ms for the driver's
+                          # one launch, events included) never reaches the start event late
 
 
 HIP_EVENT_DISABLE_SYSTEM_FENCE = 0x20000000   # hip_runtime_api.h
@@ -545,7 +546,7 @@ def gather_pass(env, plan, world, local, dev, stream, dst, copy_own=False, clock
             torch.cuda.synchronize(dev)
         # the host enqueues every launch and hand-off of the plan while the gate spins (the
         # ring's Python bookkeeping costs more host time per launch than a bare rollout)
-        ms, _ = timed(run, stream, dev, world, local, gate_cycles=GATE_CYCLES * (1 + len(plan)))
+        ms, _ = timed(run, stream, dev, world, local, gate_cycles=GATE_CYCLES * (1 + len(plan) // 4))
     wire = sum(env.n_alloc * k * (12 * env.words + 5) for k in plan)
     return ms, wire
 
@@ -826,6 +827,9 @@ def main():
         dev_ms, host_s = timed(run, stream, dev, world, local)
         # the same run between torch's default events (system-scope fence at each event)
         fenced_ms, _ = timed(run, stream, dev, world, local, system_fence=True)
+        # three more timings of the same K steps on the same clock, reported beside `value` (not
+        # in it): a one-launch run is a single sample, and these show whether it is typical
+        repeat_ms = [timed(run, stream, dev, world, local)[0] for _ in range(3)]
         # the floor of this timing method: the same gate + event pair around a one-element kernel
         tiny = torch.zeros(1, device=dev)
         floor_ms = min(timed(lambda: tiny.add_(1.0), stream, dev, world, local)[0] for _ in range(5))
@@ -1013,7 +1017,8 @@ def main():
                                                   "release device memory to system scope (host visibility)"},
                        "note": "event_floor_us: the same gate + event pair around a one-element kernel (dispatch "
                                "and event overhead, part of every timed region)",
-                       "host_ms_per_step": host_s * 1e3 / args.steps, "clock_warm_runs": warm_reps},
+                       "host_ms_per_step": host_s * 1e3 / args.steps, "clock_warm_runs": warm_reps,
+                       "repeats_ms_per_step": [r / args.steps for r in repeat_ms]},
         }
         if rollout_mode:
             kt = kernel_trace(args, plan)
