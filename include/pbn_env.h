@@ -231,10 +231,10 @@ int pbn_rollout_ex(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offs
  * pbn_rollout_ex with a copy riding along (ABI 8): the launch also copies copy_bytes from
  * d_copy_src to d_copy_dst (16-byte aligned, non-overlapping, neither one of this launch's
  * buffers).  The copy is complete when the launch is, on the same stream.  The pipelined
- * one-update kernel spreads it over its env-draw waves (each lane requests its vectors at an
- * iteration's start and stores them before the iteration's barrier); every other kernel, or a
- * copy of more than two vectors per env-draw lane and iteration, gets pbn_copy_async right after
- * the launch.  The world-1 hand-off uses it to move rollout k's records into the learner's
+ * one-update kernel runs with a fourth wave per block that moves the block's share of the copy,
+ * paced by the block's step barriers (up to four 16-byte vectors per lane and step, else in one
+ * burst), and exits; the settle kernel and the wave kernel get pbn_copy_async right after the
+ * launch, as does a launch of no steps.  The world-1 hand-off uses it to move rollout k's records into the learner's
  * receive slot during rollout k + 1 (pbn_rl_amd/distributed.py ShardedRollout.gather): the
  * receive half of the gather's point-to-point exchange, for the learner's own shard.
  */
