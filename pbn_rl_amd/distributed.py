@@ -165,6 +165,8 @@ class ShardedRollout:
         kw = {"copy": (ride.dst, ride.src)} if ride is not None else {}
         self.env.rollout(steps, flipmasks=flipmasks, random_actions=random_actions, keep_obs=True,
                          keep_final=True, out=rec.rollout_out(), **kw)
+        if ride is not None:   # complete when this launch is, on the current stream (a launch
+            ride.done = True   # that raised leaves it to the hand-off's wait())
         self._issued[steps] = self._issued.get(steps, 0) + 1
         rec._slot = k
         return rec
@@ -241,7 +243,7 @@ class ShardedRollout:
         takes = getattr(self, "_env_takes_copy", None)
         if takes is None:
             takes = self._env_takes_copy = _takes_copy(self.env)
-        if src.is_cuda and takes:
+        if takes:
             self._flush_ride()
             ride = _Ride(out, src)
             if last:
@@ -262,7 +264,6 @@ class ShardedRollout:
         if ride.src.data_ptr() == rec.flat.data_ptr():
             ride.flush()
             return None
-        ride.done = True   # complete when the launch that carries it is, on the current stream
         return ride
 
     def _flush_ride(self) -> None:
@@ -328,7 +329,10 @@ class _Ride:
 
     def flush(self) -> None:
         if not self.done:
-            _device_copy(self.dst, self.src, torch.cuda.current_stream(self.src.device))
+            if self.src.is_cuda:
+                _device_copy(self.dst, self.src, torch.cuda.current_stream(self.src.device))
+            else:
+                self.dst.copy_(self.src)
             self.done = True
 
     def wait(self) -> None:

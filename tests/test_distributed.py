@@ -139,3 +139,58 @@ def test_record_ring_keeps_previous_rollout():
     assert a.flat.data_ptr() != b.flat.data_ptr() and torch.equal(a["obs"], snap)
     c = ro.rollout(2)
     assert c.flat.data_ptr() == a.flat.data_ptr()
+
+
+def _spec():
+    from pbn_rl_amd.attractors import load_attractors
+    from pbn_rl_amd.network import load_network
+    from pbn_rl_amd.spec import EnvSpec
+    return EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.05)
+
+
+class _RideEnv:
+    """OracleVectorEnv with VectorPBNEnv's copy= contract (dst <- src once the launch is done),
+    logging the copies it carried."""
+
+    def __init__(self, inner):
+        self.inner, self.carried = inner, []
+        self.words = inner.words
+
+    @property
+    def state(self):
+        return self.inner.state
+
+    def rollout(self, n_steps, flipmasks=None, random_actions=True, keep_obs=True, keep_final=True, out=None,
+                copy=None):
+        res = self.inner.rollout(n_steps, flipmasks=flipmasks, random_actions=random_actions, keep_obs=keep_obs,
+                                 keep_final=keep_final, out=out)
+        if copy is not None:
+            dst, src = copy
+            dst.copy_(src)
+            self.carried.append(src.data_ptr())
+        return res
+
+
+@pytest.mark.parametrize("buffers", [1, 2, 3])
+def test_own_shard_copy_rides_along_the_next_rollout(buffers):
+    """World 1 without a process group, copy_own: rollout k's records reach the receive slot by
+    the copy riding along rollout k + 1 (when k + 1 writes another slot), or on the hand-off's
+    wait; the last hand-off is copied at once.  Every received slot equals a single run's records."""
+    from pbn_rl_amd.distributed import ShardedRollout
+    from tests.oracle_env import OracleVectorEnv
+    spec = _spec()
+    n, steps, k_total = 64, 3, 5
+    env = _RideEnv(OracleVectorEnv(spec, 0, n, seed=9))
+    ro = ShardedRollout(n, lambda off, cnt: env, buffers=buffers)
+    seen = []
+    ro.run(k_total, steps, dst=0, consume=lambda k, parts: seen.append(parts[0].flat.clone()), copy_own=True)
+    ref = OracleVectorEnv(spec, 0, n, seed=9)
+    from pbn_rl_amd.distributed import TransitionRecords
+    assert len(seen) == k_total
+    for k in range(k_total):
+        want = ref.rollout(steps)
+        got = TransitionRecords(steps, env.words, n, flat=seen[k])
+        for name in ("obs", "flipmask", "final_state", "flags"):
+            assert torch.equal(got[name], want[name]), (k, name)
+    # with two or more slots every hand-off but the last rode along the next launch
+    assert len(env.carried) == (k_total - 1 if buffers >= 2 else 0)

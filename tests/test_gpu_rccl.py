@@ -132,6 +132,35 @@ def test_world1_own_shard_handoff_copies_records():
             assert torch.equal(seen[k][name], want[name]), (k, name)
 
 
+@pytest.mark.parametrize("buffers", [1, 3])
+def test_world1_own_shard_handoff_ring_sizes(buffers):
+    """The ride-along own-shard copy with one record slot (the next rollout would overwrite the
+    copy's source: the copy is issued first, on the launch stream) and with three; the hand-off
+    waited on before the next rollout (a plain loop over gather + consume) as well as overlapped."""
+    from pbn_rl_amd.distributed import ShardedRollout
+    spec = _spec()
+    n, steps = 4096, 5
+    ro = ShardedRollout(n, _factory(spec, 5), buffers=buffers)
+    seen = []
+
+    def consume(k, parts):
+        seen.append(parts[0].flat.cpu().clone())
+
+    ro.run(4, steps, dst=0, consume=consume, copy_own=True)
+    rec = ro.rollout(steps)   # then one hand-off waited on at once, with no rollout after it
+    parts = ro.gather(rec, dst=0, copy_own=True)
+    seen.append(parts[0].flat.cpu().clone())
+    torch.cuda.synchronize()
+    from tests.oracle_env import OracleVectorEnv
+    ref = OracleVectorEnv(spec, 0, n, seed=5)
+    from pbn_rl_amd.distributed import TransitionRecords
+    for k in range(5):
+        want = ref.rollout(steps)
+        got = TransitionRecords(steps, 1, n, flat=seen[k])
+        for name in ("obs", "flipmask", "final_state", "flags"):
+            assert torch.equal(got[name], want[name]), (k, name)
+
+
 def test_copy_async_entry_point():
     """pbn_copy_async: ragged sizes (every 16-byte multiple up to a few vectors past the grid's
     stride loop), offsets into a buffer, and its argument checks."""
