@@ -253,6 +253,9 @@ class VectorPBNEnv:
                 dst, src = copy
                 if dst.numel() * dst.element_size() != src.numel() * src.element_size():
                     raise ValueError("copy: dst and src differ in size")
+                if not (dst.is_contiguous() and src.is_contiguous()) or dst.device != src.device or \
+                        src.device.type != "cuda":
+                    raise ValueError("copy: dst and src must be contiguous tensors on the env's GPU")
                 _lib.check(L.pbn_rollout_copy(self.net.handle, self.seed, self.step_index, self.env_offset, n,
                                               n_steps, mode, self.state.data_ptr(), out["flipmask"].data_ptr(),
                                               self.target.data_ptr(), self.t.data_ptr(), ptr(out["obs"]),

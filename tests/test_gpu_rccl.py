@@ -216,3 +216,5 @@ def test_rollout_copy_entry_point(settle):
             assert torch.equal(g, w), (nbytes, name)
     with pytest.raises(ValueError):
         envs[0].rollout(steps, copy=(dst[:32], src[:16]))
+    with pytest.raises(ValueError):   # a strided view: its bytes are not one range
+        envs[0].rollout(steps, copy=(dst[:64:2], src[:32]))
