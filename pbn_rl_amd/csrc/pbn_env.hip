@@ -962,6 +962,10 @@ static int rollout_impl(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env
       const int64_t slots = (int64_t)(n_steps + 1) * pblocks * 64;
       const int64_t u = (a.cp_n16 + slots - 1) / slots;
       a.cp_u = u <= 1 ? 1 : (u <= 2 ? 2 : (u <= 4 ? 4 : 0));
+      // a grid of more blocks than run at once: the burst, whose wave exits early, where the paced
+      // wave held a block slot for the whole launch (1M envs: 0.69 -> 0.74x of the bare launches'
+      // rate, pbn70 x 1M: 0.65 -> 0.73x; profiles/r05_zj_ab.json)
+      if (pblocks > 4 * (int64_t)net->n_cus) a.cp_u = 0;
       copy_after = false;
     }
     hipLaunchKernelGGL(net->pipe, dim3((unsigned)pblocks), dim3(a.cp_n16 ? 256 : 192), net->lds_pipe,
