@@ -23,9 +23,11 @@ that last read its slot.  With one slot there is nothing to overlap: each
 rollout is consumed before the next one overwrites the slot.
 
 ``gather(rec, dst, copy_own=True)`` also copies the learner's own shard into its
-receive slot (on a side stream, overlapped like the collective), so that every
-shard ends in a learner-owned buffer; at world 1 that copy is the whole
-hand-off (bench.py's ``value_with_gather``).
+receive slot, so that every shard ends in a learner-owned buffer; at world 1 that
+copy is the whole hand-off (bench.py's ``value_with_gather``).  On a GPU env it
+rides along the next rollout launch (``pbn_rollout_copy``: a fourth wave per block
+of the rollout kernel), overlapped like the collective; CPU tensors or envs without
+``copy=`` get a side-stream copy.
 
 Wire format (``TransitionRecords``): one flat byte buffer per shard and rollout,
 field-major so that ``pbn_rollout`` writes every field in place (no packing

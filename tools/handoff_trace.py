@@ -6,9 +6,11 @@ for a kernel-and-copy trace:
 
 Each rep: the rollout launches of the plan into the ring's record slots, each followed by the
 hand-off of its records (at world 1: the learner's own shard copied into its receive slot by
-pbn_copy_async, on a side stream, the last one on the launch stream), then a device sync.  Prints one JSON line with the per-rep device time of the
-pass (HIP events around each rep, after two untimed reps), and with --summarize DIR attributes
-the trace: per rep, the rollout kernels, the copy (kernel or DMA), and the gaps between them.
+the next launch's fourth wave, pbn_rollout_copy, the last one by pbn_copy_async on the launch
+stream), then a device sync.  The same launches without the hand-off are timed first (bare_*).
+Prints one JSON line with the per-rep device time of the pass (HIP events around each rep, after
+a 0.3 s clock warm-up), and with --summarize DIR attributes the trace: per rep, the rollout
+kernels, the copy (kernel or DMA), and the gaps between them.
 """
 import argparse
 import glob
