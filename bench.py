@@ -850,9 +850,9 @@ def main():
     if rollout_mode and not args.no_gather:
         with_gather = {}
         # the hand-off of launch k overlaps launch k + 1 (at world 1 the own-shard copy rides along
-        # launch k + 1); the last one follows its launch on the launch stream.  A one-launch plan (the driver's 20 steps) stays one launch:
-        # split in two it paid a second launch's floor for the overlap (68.6 against 59.2 us,
-        # profiles/r05_a_handoff_*.json)
+        # launch k + 1); the last one follows its launch on the launch stream.  A one-launch plan
+        # (the driver's 20 steps) stays one launch: split in two it paid a second launch's floor
+        # for the overlap (68.6 against 59.2 us, profiles/r05_a_handoff_*.json)
         gplan = plan
         own = world == 1
         for key, dst, what in (("learner", 0, "point-to-point sends of every shard to rank 0" +
