@@ -69,7 +69,7 @@
 extern "C" {
 #endif
 
-#define PBN_ABI_VERSION 8
+#define PBN_ABI_VERSION 9
 
 #define PBN_MAX_NODES 128
 #define PBN_MAX_ARITY 4
@@ -504,6 +504,19 @@ int pbn_bdq_learn(const pbn_net* net, int64_t batch, const int64_t* d_idx, int64
  * must not overlap.
  */
 int pbn_copy_async(void* d_dst, const void* d_src, int64_t bytes, void* stream);
+
+/*
+ * pbn_host_buffer (ABI 9): `bytes` of pinned host memory, coherent and mapped into the current
+ * device's address space (hipHostMalloc, mapped | coherent): *h_ptr is its host address, *d_ptr
+ * the address kernels use; pbn_host_buffer_free releases it.  The scalar gym facade (PBNEnv,
+ * one env per step, config 1) keeps its 32-env group there, so that a step is one
+ * pbn_step launch on those pointers and one pbn_stream_sync, with no copies
+ * (gym_PBN's env.step(), bdq_model/__init__.py:177).
+ */
+int pbn_host_buffer(int64_t bytes, void** h_ptr, void** d_ptr);
+int pbn_host_buffer_free(void* h_ptr);
+/* pbn_stream_sync (ABI 9): waits until the work issued on `stream` has completed. */
+int pbn_stream_sync(void* stream);
 
 const char* pbn_last_error(void);
 int pbn_abi_version(void);

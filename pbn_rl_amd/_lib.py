@@ -29,7 +29,8 @@ EXPORTS = ["pbn_net_create", "pbn_net_destroy", "pbn_net_words", "pbn_reset", "p
            "pbn_q_to_flipmask_dev",
            "pbn_heads_to_flipmask", "pbn_qnet_heads", "pbn_qnet_flipmask", "pbn_qnet_heads_from_state",
            "pbn_qnet_flipmask_from_state", "pbn_replay_store", "pbn_replay_advance", "pbn_replay_batch", "pbn_bdq_td_loss", "pbn_bdq_layout", "pbn_bdq_learn_workspace",
-           "pbn_bdq_pack", "pbn_bdq_learn", "pbn_copy_async", "pbn_rollout_copy", "pbn_last_error", "pbn_abi_version"]
+           "pbn_bdq_pack", "pbn_bdq_learn", "pbn_copy_async", "pbn_rollout_copy", "pbn_host_buffer", "pbn_host_buffer_free", "pbn_stream_sync",
+           "pbn_last_error", "pbn_abi_version"]
 SOURCES = ["pbn_env.hip", "pbn_settle.hip", "pbn_agent.hip", "pbn_qnet.hip", "pbn_learn.hip"]
 
 _lib: Optional[ctypes.CDLL] = None
@@ -150,6 +151,13 @@ def load() -> ctypes.CDLL:
     L.pbn_rollout_copy.argtypes = [vp, u64, u64, u64, i64, ctypes.c_int32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                    vp, vp, i64, vp]
     L.pbn_rollout_copy.restype = ctypes.c_int
+    if hasattr(L, "pbn_host_buffer"):   # (ABI 9)
+        L.pbn_host_buffer.argtypes = [i64, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+        L.pbn_host_buffer.restype = ctypes.c_int
+        L.pbn_host_buffer_free.argtypes = [vp]
+        L.pbn_host_buffer_free.restype = ctypes.c_int
+        L.pbn_stream_sync.argtypes = [vp]
+        L.pbn_stream_sync.restype = ctypes.c_int
     L.pbn_abi_version.argtypes = []
     L.pbn_abi_version.restype = ctypes.c_int
     _lib = L

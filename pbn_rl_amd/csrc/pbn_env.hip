@@ -299,6 +299,35 @@ int pbn_state_histogram(const uint32_t* d_states, int64_t n_rows, int64_t n_cols
 }
 int pbn_abi_version(void) { return PBN_ABI_VERSION; }
 
+int pbn_host_buffer(int64_t bytes, void** h_ptr, void** d_ptr) {
+  if (bytes <= 0 || !h_ptr || !d_ptr) return fail(PBN_EINVAL, "bytes <= 0 or null out pointer");
+  *h_ptr = nullptr;
+  *d_ptr = nullptr;
+  void* h = nullptr;
+  if (hipHostMalloc(&h, (size_t)bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess || !h)
+    return fail(PBN_ENOMEM, "hipHostMalloc failed");
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d) {
+    (void)hipHostFree(h);
+    return fail(PBN_EDEVICE, "hipHostGetDevicePointer failed");
+  }
+  memset(h, 0, (size_t)bytes);
+  *h_ptr = h;
+  *d_ptr = d;
+  return PBN_OK;
+}
+
+int pbn_host_buffer_free(void* h_ptr) {
+  if (!h_ptr) return PBN_OK;
+  HIP_OK(hipHostFree(h_ptr));
+  return PBN_OK;
+}
+
+int pbn_stream_sync(void* stream) {
+  HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+  return PBN_OK;
+}
+
 // pbn_copy_async: a grid-stride copy in 16-byte non-temporal vectors (the records are read once and
 // go to the learner: neither side should displace the rollout's table image from L2), four
 // independent vectors in flight per thread

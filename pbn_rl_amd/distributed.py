@@ -167,8 +167,8 @@ class ShardedRollout:
         kw = {"copy": (ride.dst, ride.src)} if ride is not None else {}
         self.env.rollout(steps, flipmasks=flipmasks, random_actions=random_actions, keep_obs=True,
                          keep_final=True, out=rec.rollout_out(), **kw)
-        if ride is not None:   # complete when this launch is, on the current stream (a launch
-            ride.done = True   # that raised leaves it to the hand-off's wait())
+        if ride is not None:   # complete when this launch is (a launch that raised leaves it to
+            ride.carried()     # the hand-off's wait())
         self._issued[steps] = self._issued.get(steps, 0) + 1
         rec._slot = k
         return rec
@@ -324,21 +324,39 @@ class ShardedRollout:
 
 class _Ride:
     """An own-shard copy waiting for the next rollout launch to carry it (a work object: wait()
-    issues it on the current stream if no launch has taken it yet)."""
+    issues it on the current stream if no launch has taken it yet, and otherwise orders the
+    current stream after the launch that carried it, as a collective's work does)."""
 
     def __init__(self, dst: torch.Tensor, src: torch.Tensor):
         self.dst, self.src, self.done = dst, src, False
+        self.event, self.stream = None, None
+
+    def carried(self) -> None:
+        """The rollout launch just issued on the current stream carries the copy (VectorPBNEnv
+        launches on the stream current at the call): its completion is an event on that stream."""
+        self.done = True
+        if self.src.is_cuda:
+            self.stream = torch.cuda.current_stream(self.src.device)
+            self.event = torch.cuda.Event()
+            self.event.record(self.stream)
 
     def flush(self) -> None:
         if not self.done:
             if self.src.is_cuda:
-                _device_copy(self.dst, self.src, torch.cuda.current_stream(self.src.device))
+                self.stream = torch.cuda.current_stream(self.src.device)
+                _device_copy(self.dst, self.src, self.stream)
+                self.event = torch.cuda.Event()
+                self.event.record(self.stream)
             else:
                 self.dst.copy_(self.src)
             self.done = True
 
     def wait(self) -> None:
         self.flush()
+        if self.event is not None:
+            cur = torch.cuda.current_stream(self.src.device)
+            if cur != self.stream:   # a consumer on another stream waits for the carrying launch
+                cur.wait_event(self.event)
 
 
 def _takes_copy(env) -> bool:

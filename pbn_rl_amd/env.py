@@ -27,9 +27,11 @@ Drop-in for the env the reference builds with
   env.env.env chain, close()                      train_pbn_BQN.py:90, train_BDQ.py:116
 
 One PBNEnv is one env (gym semantics: no autoreset; callers call reset()).  It
-runs on the GPU as a 32-env group of which env 0 is the visible one; every
-step is one pbn_step launch plus a tiny device->host copy.  Use VectorPBNEnv
-for batched rollouts.
+runs on the GPU as a 32-env group of which env 0 is the visible one.  Between
+steps the group lives in pinned host memory mapped into the device
+(pbn_host_buffer, _HostGroup): a step is one pbn_step launch on those pointers
+and one stream synchronisation, no copies and no torch tensors.  Use
+VectorPBNEnv for batched rollouts.
 """
 from __future__ import annotations
 
@@ -127,6 +129,45 @@ class _Graph:
         return stg
 
 
+class _HostGroup:
+    """The facade's 32-env group in pinned, device-mapped host memory (pbn_host_buffer, ABI 9):
+    two state buffers (ping-pong), the flip mask, reward, flags, target and step count, each as a
+    numpy view (host side) and a device address (the kernel's side)."""
+
+    _LAYOUT = (("state0", 4, 1), ("state1", 4, 1), ("flip", 4, 1), ("reward", 4, 0), ("flags", 1, 0),
+               ("target", 1, 0), ("t", 1, 0))
+
+    def __init__(self, words: int, n: int = 32):
+        import ctypes
+        L = _lib.load()
+        self.words, self.n = words, n
+        offs, off = {}, 0
+        for name, size, per_word in self._LAYOUT:
+            offs[name] = off
+            off += ((size * n * (words if per_word else 1)) + 15) & ~15
+        h, d = ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.check(L.pbn_host_buffer(off, ctypes.byref(h), ctypes.byref(d)), "pbn_host_buffer")
+        self._h, self._d, self.bytes = h.value, d.value, off
+        raw = np.ctypeslib.as_array((ctypes.c_uint8 * off).from_address(self._h))
+        dt = {"reward": np.float32, "flags": np.uint8, "target": np.uint8, "t": np.uint8}
+        self.view, self.dev = {}, {}
+        for name, size, per_word in self._LAYOUT:
+            o = offs[name]
+            nb = size * n * (words if per_word else 1)
+            v = raw[o:o + nb].view(dt.get(name, np.uint32))
+            self.view[name] = v.reshape(words, n) if per_word else v
+            self.dev[name] = self._d + o
+        self.cur = 0   # state{cur} holds the current state
+
+    def state(self) -> np.ndarray:
+        return self.view[f"state{self.cur}"]
+
+    def free(self) -> None:
+        if getattr(self, "_h", None):
+            _lib.load().pbn_host_buffer_free(self._h)
+            self._h = None
+
+
 class PBNEnv:
     metadata = {"render_modes": ["human", "PBN"]}
 
@@ -184,11 +225,6 @@ class PBNEnv:
         self.target_nodes: List[int] = []
         self.control_nodes = list(range(self.N))
         self._ep_lens: List[int] = []
-        W = self.spec.words
-        self._pin_flip = torch.zeros(W, 1, dtype=torch.int32).pin_memory()
-        self._pin_state = torch.zeros(W, 1, dtype=torch.int32).pin_memory()
-        self._pin_reward = torch.zeros(1, dtype=torch.float32).pin_memory()
-        self._pin_flags = torch.zeros(1, dtype=torch.uint8).pin_memory()
         # attractor growth (bdq_model/__init__.py:182-184): states revisited outside the known
         # attractors are verified as bottom SCCs (discovery.bottom_sccs) at episode ends
         self.grow_attractors = grow_attractors
@@ -198,6 +234,12 @@ class PBNEnv:
         # rework_probas (bdq_model/__init__.py:203): per (start, target) pair weights
         self._pair_len: Optional[np.ndarray] = None
         self._rng = np.random.default_rng(self._seed)
+        # the group in device-mapped host memory between steps (_HostGroup); ``_hg_live``: it, not
+        # the VectorPBNEnv's device tensors, holds the current state / target / step count
+        self._hg: Optional[_HostGroup] = None
+        self._hg_live = False
+        self._bit = np.arange(self.N)
+        self._bit_word, self._bit_pos = self._bit >> 5, (self._bit & 31).astype(np.uint32)
 
     # gymnasium wrapper chain compatibility (env.env.env, env.unwrapped)
     @property
@@ -209,23 +251,74 @@ class PBNEnv:
         return self
 
     # ---------------------------------------------------------------- core
+    def _unpack(self, words: np.ndarray) -> np.ndarray:
+        """bits of env 0's state words (node i = bit i & 31 of word i >> 5, Network.pack)"""
+        return ((words[self._bit_word] >> self._bit_pos) & 1).astype(np.int64)
+
     def _read_state(self) -> np.ndarray:
+        if self._hg_live:
+            return self._unpack(self._hg.state()[:, 0])
         w = self._venv.state[:, 0].cpu().numpy().view(np.uint32)
         return np.array(self.spec.network.unpack(list(w)), dtype=np.int64)
 
+    def _to_device(self) -> None:
+        """The host group's state / target / step count back into the VectorPBNEnv (before any
+        operation on its tensors)."""
+        if not self._hg_live:
+            return
+        hg, venv = self._hg, self._venv
+        n = hg.n
+        venv.state[:, :n].copy_(torch.from_numpy(hg.state().view(np.int32).copy()))
+        venv.target[:n].copy_(torch.from_numpy(hg.view["target"].copy()))
+        venv.t[:n].copy_(torch.from_numpy(hg.view["t"].copy()))
+        self._hg_live = False
+
+    def _to_host(self) -> None:
+        """The VectorPBNEnv's group into the host group (first step after reset / setState)."""
+        if self._hg is None:
+            self._hg = _HostGroup(self.spec.words, self._venv.n_alloc)
+        hg, venv = self._hg, self._venv
+        n = hg.n
+        hg.state()[:] = venv.state[:, :n].cpu().numpy().view(np.uint32)
+        hg.view["target"][:] = venv.target[:n].cpu().numpy()
+        hg.view["t"][:] = venv.t[:n].cpu().numpy()
+        hg.view["flip"][:] = 0
+        self._hg_live = True
+
     def _set_state(self, bits: Tuple[int, ...]) -> None:
-        words = torch.tensor(np.array(self.spec.network.pack(bits), dtype=np.uint32).view(np.int32)[:, None],
-                             device=self._venv.device)
-        self._venv.state[:, :1].copy_(words)
+        words = np.array(self.spec.network.pack(bits), dtype=np.uint32)
+        if self._hg_live:
+            self._hg.state()[:, 0] = words
+            return
+        self._venv.state[:, :1].copy_(torch.tensor(words.view(np.int32)[:, None], device=self._venv.device))
+
+    def _set_target_id(self, idx: int) -> None:
+        if self._hg_live:
+            self._hg.view["target"][0] = idx
+        else:
+            self._venv.target[:1].fill_(idx)
 
     def reset(self, seed: Optional[int] = None, options=None):
         if seed is not None:
             self._seed = int(seed)
-        self._venv.reset(seed=self._seed)
+        venv = self._venv
+        if self._hg is not None:   # pbn_reset straight into the host group (as VectorPBNEnv.reset)
+            hg = self._hg
+            venv.seed = self._seed & 0xFFFFFFFFFFFFFFFF
+            L = _lib.load()
+            stream = venv._stream()
+            _lib.check(L.pbn_reset(venv.net.handle, venv.seed, venv.step_index, venv.env_offset, venv.n_alloc,
+                                   hg.dev[f"state{hg.cur}"], hg.dev["target"], hg.dev["t"], stream), "pbn_reset")
+            _lib.check(L.pbn_stream_sync(stream), "pbn_stream_sync")
+            venv.step_index += 1
+            self._hg_live = True
+        else:
+            self._hg_live = False
+            venv.reset(seed=self._seed)
         if self._pair_len is not None and len(self.all_attractors) >= 2:
             self._reset_reweighted()
         state = self._read_state()
-        tgt = int(self._venv.target[0].item())
+        tgt = int(self._hg.view["target"][0]) if self._hg_live else int(venv.target[0].item())
         self.target_attractor_id = tgt if tgt != NO_TARGET else -1
         self.state_attractor_id = self.spec.attractor_id(state)
         self.target = list(self.all_attractors[tgt][0]) if tgt != NO_TARGET else None
@@ -255,21 +348,29 @@ class PBNEnv:
             if a > 0:
                 bits[a - 1] = 1
         venv = self._venv
-        self._pin_flip.numpy()[:, 0] = np.array(self.spec.network.pack(bits), dtype=np.uint32).view(np.int32)
-        venv.flipmask[:, :1].copy_(self._pin_flip, non_blocking=True)
-        venv.step_flipmask(use_current=True)
-        # one host synchronisation per step: the three results come back by async copies
-        self._pin_state.copy_(venv.state[:, :1], non_blocking=True)
-        self._pin_reward.copy_(venv.reward[:1], non_blocking=True)
-        self._pin_flags.copy_(venv.flags[:1], non_blocking=True)
-        torch.cuda.current_stream(venv.device).synchronize()
-        fl = int(self._pin_flags[0])
-        r = float(self._pin_reward[0])
-        obs = np.array(self.spec.network.unpack(list(self._pin_state.numpy()[:, 0].view(np.uint32))),
-                       dtype=np.int64)
+        if not self._hg_live:
+            self._to_host()
+        hg = self._hg
+        hg.view["flip"][:, 0] = np.array(self.spec.network.pack(bits), dtype=np.uint32)
+        # one launch on the mapped group, one synchronisation, no copies (pbn_step's arguments as
+        # VectorPBNEnv.step_flipmask passes them: same seed, step index and env range)
+        L = _lib.load()
+        nxt = 1 - hg.cur
+        stream = venv._stream()
+        _lib.check(L.pbn_step(venv.net.handle, venv.seed, venv.step_index, venv.env_offset, venv.n_alloc,
+                              _lib.MODE_AUTORESET if venv.autoreset else 0, hg.dev[f"state{hg.cur}"], hg.dev["flip"],
+                              hg.dev["target"], hg.dev["t"], hg.dev[f"state{nxt}"], None, hg.dev["reward"],
+                              hg.dev["flags"], stream), "pbn_step")
+        _lib.check(L.pbn_stream_sync(stream), "pbn_stream_sync")
+        venv.step_index += 1
+        hg.cur = nxt
+        words = hg.state()[:, 0]
+        fl = int(hg.view["flags"][0])
+        r = float(hg.view["reward"][0])
+        obs = self._unpack(words)
         self.n_steps += 1
         if self.grow_attractors and not fl & _lib.FLAG_IN_ATTRACTOR:
-            key = int.from_bytes(self._pin_state.numpy()[:, 0].view(np.uint32).tobytes(), "little")
+            key = int.from_bytes(words.tobytes(), "little")
             self._visits[key] = self._visits.get(key, 0) + 1
             if len(self._visits) > self.visit_cap:
                 self._prune_visits()
@@ -300,7 +401,7 @@ class PBNEnv:
                 raise ValueError("target is not a state of a known attractor")
         self.target_attractor_id = idx
         self.target = list(self.all_attractors[idx][0])
-        self._venv.target[:1].fill_(idx)
+        self._set_target_id(idx)
 
     def rework_probas(self, ep_len: Optional[int] = None) -> None:
         """Called by the learner after every episode (bdq_model/__init__.py:203;
@@ -347,7 +448,7 @@ class PBNEnv:
         A = len(self.all_attractors)
         s, t = divmod(k, A)
         self._set_state(self.all_attractors[s][0])
-        self._venv.target[:1].fill_(t)
+        self._set_target_id(t)
 
     def grow(self, min_visits: int = 2, max_states: int = 1 << 14) -> int:
         """Attractor growth (bdq_model/__init__.py:182-184 re-raises epsilon when
@@ -379,6 +480,7 @@ class PBNEnv:
         self.all_attractors.extend([list(a) for a in new])
         self.attracting_states = [s for a in self.all_attractors for s in a]
         self.spec = EnvSpec(self.spec.network, self.all_attractors, **self._spec_kwargs)
+        self._to_device()
         self._venv.set_spec(self.spec)
         return len(new)
 
@@ -392,6 +494,10 @@ class PBNEnv:
                 del self._visits[k]
 
     def close(self) -> None:
+        self._to_device()
+        if self._hg is not None:
+            self._hg.free()
+            self._hg = None
         self._venv.close()
 
 

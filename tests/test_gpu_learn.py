@@ -267,3 +267,51 @@ def test_fused_update_matches_reference_update_policy():
     for n, w in zip(names, tgt.parameters()):
         w_ref = torch.from_numpy(d["t2." + n]).to(dev)
         assert (w.detach() - w_ref).abs().max().item() <= 2.1 * lr, n
+
+
+def test_fused_update_matches_reference_update_policy_benched_shape():
+    """pbn_bdq_learn at the benched shape, BranchingQNetwork((28, 28), 29, 3) (config 5 and the
+    bdq-learn line), held to the reference's update_policy through the sampled fixture
+    tests/golden/bdq_update28.npz (tools/gen_update_golden.py --shape 28; formula initial weights,
+    per-tensor norms and 4,096 sampled entries).  The tolerances of the N = 7 test: loss rtol 1e-5,
+    clamped gradients rtol 1e-3 / atol 1e-6, parameters after Adam atol 1e-5 where the reference
+    gradient exceeds 1e-4, else within two Adam steps; the soft-updated target likewise."""
+    from tests.test_update_golden import load_fixture28, nets28_from, sampled_close
+    d, names = load_fixture28()
+    N, K, B = 28, 3, 256
+    lr, gamma = float(d["lr"]), float(d["gamma"])
+    spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"))
+    env = VectorPBNEnv(spec, 64)
+    dev = torch.device("cuda")
+    q, tgt = nets28_from(d, names)
+    q, tgt = q.to(dev), tgt.to(dev)
+    fused = FusedBDQUpdate(q, tgt, env.net, K, batch_size=B, learning_rate=lr, gamma=gamma, keep_grad=True)
+    bits = (1 << np.arange(N, dtype=np.uint32))
+    to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    idx = torch.arange(B, dtype=torch.int64, device=dev)
+    for call in (1, 2):
+        p = f"b{call}."
+        R = DeviceReplay(B, 1, K, dev)
+        st = (d[p + "states"].astype(np.uint32) * bits).sum(1).astype(np.uint32)[None]
+        nst = (d[p + "next_states"].astype(np.uint32) * bits).sum(1).astype(np.uint32)[None]
+        R.store(to(st.view(np.int32)), to(d[p + "target_ids"]), to(d[p + "actions"].astype(np.int32)),
+                to(d[p + "rewards"]), to(nst.view(np.int32)), to(d[p + "done"]))
+        loss = float(fused.update(R, idx))
+        torch.cuda.synchronize()
+        want = float(d["losses"][call - 1])
+        assert abs(loss - want) <= 1e-5 * abs(want), (call, loss, want)
+        for n, g, w in zip(names, fused.grads(), q.parameters()):
+            ok, err, _ = sampled_close(g, d, f"g{call}.{n}", n, 1e-3, 1e-6)
+            assert ok, (call, n, err)
+            sel = torch.from_numpy(d["idx." + n]).to(dev)
+            w_ref = torch.from_numpy(d[f"q{call}.{n}"]).to(dev)
+            g_ref = torch.from_numpy(d[f"g{call}.{n}"]).to(dev)
+            err = (w.detach().reshape(-1)[sel] - w_ref).abs()
+            big = g_ref.abs() > 1e-4
+            assert err[big].max().item() <= 1e-5 if big.any() else True, (call, n, err[big].max().item())
+            assert err.max().item() <= 2.1 * lr * call, (call, n, err.max().item())
+    fused.soft_update()
+    for n, w in zip(names, tgt.parameters()):
+        sel = torch.from_numpy(d["idx." + n]).to(dev)
+        w_ref = torch.from_numpy(d["t2." + n]).to(dev)
+        assert (w.detach().reshape(-1)[sel] - w_ref).abs().max().item() <= 2.1 * lr, n

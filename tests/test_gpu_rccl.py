@@ -161,6 +161,27 @@ def test_world1_own_shard_handoff_ring_sizes(buffers):
             assert torch.equal(got[name], want[name]), (k, name)
 
 
+def test_world1_ride_consumed_on_another_stream():
+    """The hand-off work of a ride-along copy orders a consumer on another stream after the
+    launch that carried the copy: gather, the next rollout (it carries the copy),
+    then work.wait() and the read on a second stream, with a long kernel queued on the launch
+    stream after the carrying launch so that an unordered read would see the slot before the copy."""
+    from pbn_rl_amd.distributed import ShardedRollout
+    spec = _spec()
+    n, steps = 4096, 5
+    ro = ShardedRollout(n, _factory(spec, 7))
+    rec = ro.rollout(steps)
+    want = rec.flat.clone()
+    parts, work = ro.gather(rec, dst=0, async_op=True, copy_own=True)
+    ro.rollout(steps)   # carries rollout 0's own-shard copy
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        work.wait()
+        got = parts[0].flat.clone()
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
+
+
 def test_copy_async_entry_point():
     """pbn_copy_async: ragged sizes (every 16-byte multiple up to a few vectors past the grid's
     stride loop), offsets into a buffer, and its argument checks."""

@@ -22,6 +22,15 @@ an update followed by the soft update (target <- target / 2 + q / 2).
 Stored: the batches (uint8 / int / float32), the parameters before (q0.*, t0.*), the clamped
 gradients and parameters after each call (g1.*, q1.*, g2.*, q2.*), the target after call 2
 (t2.*), the losses.
+
+  python tools/gen_update_golden.py --shape 28   -> tests/golden/bdq_update28.npz
+
+The benched shape: BranchingQNetwork((28, 28), 29, 3), Bittner-28's
+attractors as targets, the same batch law, two calls (the second with the soft update).  Its
+parameters would make a 9 MB fixture, so the initial weights come from a formula both sides
+compute (tests/test_update_golden.py formula_params: seeded normals scaled by 1/sqrt(fan-in), the
+target a perturbed copy), and per tensor the fixture keeps the L2 norm of every stored quantity
+and its values at a fixed-seed sample of 4,096 flat indices (idx.*).
 """
 import ast
 import importlib.util
@@ -41,6 +50,7 @@ from pbn_rl_amd.attractors import load_attractors  # noqa: E402
 REF = "/root/reference"
 OUT = os.path.join(ROOT, "tests", "golden", "bdq_update.npz")
 N, K, B = 7, 3, 256
+SAMPLE = 4096
 LR, GAMMA = 1e-3, 0.9
 
 
@@ -83,23 +93,45 @@ def transitions(b):
 
 
 def main():
+    global N, OUT
+    sampled = "--shape" in sys.argv and sys.argv[sys.argv.index("--shape") + 1] == "28"
     net_mod = ref_network_module()
     update_policy, lines = ref_update_policy()
-    att = load_attractors("pbn7")
+    if sampled:
+        N, OUT = 28, OUT.replace("bdq_update.npz", "bdq_update28.npz")
+    att = load_attractors("pbn28" if sampled else "pbn7")
     att_first = np.array([list(a[0]) for a in att], dtype=np.uint8)
     rng = np.random.default_rng(20261018)
     torch.manual_seed(5)
     q = net_mod.BranchingQNetwork((N, N), N + 1, K)
     target = net_mod.BranchingQNetwork((N, N), N + 1, K)
-    with torch.no_grad():
-        for pt, pq in zip(target.parameters(), q.parameters()):
-            pt.copy_(pq + 0.05 * torch.randn_like(pq))
     names = [n for n, _ in q.named_parameters()]
     out = {"lines": np.array(lines), "lr": np.float32(LR), "gamma": np.float32(GAMMA)}
-    for n, p in q.named_parameters():
-        out["q0." + n] = p.detach().numpy().copy()
-    for n, p in target.named_parameters():
-        out["t0." + n] = p.detach().numpy().copy()
+    if sampled:
+        from tests.test_update_golden import formula_params
+        init_q, init_t = formula_params([(n, tuple(p.shape)) for n, p in q.named_parameters()], seed=28)
+        q.load_state_dict({n: torch.from_numpy(v) for n, v in init_q.items()})
+        target.load_state_dict({n: torch.from_numpy(v) for n, v in init_t.items()})
+        out["init_seed"] = np.int64(28)
+        srng = np.random.default_rng(4096)
+        for n, p in q.named_parameters():
+            out["idx." + n] = np.sort(srng.choice(p.numel(), size=min(SAMPLE, p.numel()), replace=False)).astype(np.int64)
+    else:
+        with torch.no_grad():
+            for pt, pq in zip(target.parameters(), q.parameters()):
+                pt.copy_(pq + 0.05 * torch.randn_like(pq))
+        for n, p in q.named_parameters():
+            out["q0." + n] = p.detach().numpy().copy()
+        for n, p in target.named_parameters():
+            out["t0." + n] = p.detach().numpy().copy()
+
+    def keep(key, n, v):
+        """the whole tensor (N = 7), or its L2 norm and sampled entries (N = 28)"""
+        if not sampled:
+            out[key] = v
+            return
+        out[key + ".norm"] = np.float64(np.linalg.norm(v.astype(np.float64)))
+        out[key] = v.reshape(-1)[out["idx." + n]]
 
     losses = []
     this = types.SimpleNamespace(
@@ -114,11 +146,11 @@ def main():
         memory = types.SimpleNamespace(sample=lambda n, rows=rows: list(rows[:n]))
         update_policy(this, adam, memory, B)
         for n, p in q.named_parameters():
-            out[f"g{call}.{n}"] = p.grad.detach().numpy().copy()
-            out[f"q{call}." + n] = p.detach().numpy().copy()
+            keep(f"g{call}.{n}", n, p.grad.detach().numpy().copy())
+            keep(f"q{call}.{n}", n, p.detach().numpy().copy())
     assert this.update_counter == 0, "call 2 ran the soft update"
     for n, p in target.named_parameters():
-        out["t2." + n] = p.detach().numpy().copy()
+        keep(f"t2.{n}", n, p.detach().numpy().copy())
     out["losses"] = np.array(losses, dtype=np.float32)
     out["names"] = np.array(names)
     np.savez_compressed(OUT, **out)
