@@ -376,7 +376,10 @@ def workload_text(args, chunk: int, rollout_mode: bool) -> str:
         return (f"full BDQ rollout (config 5): {args.network} x {args.envs} envs per GPU, per step the "
                 f"BranchingQNetwork fp32 forward (random init, seed 0; bilinear layer by pbn_bilinear_targets from "
                 f"the packed state) -> epsilon-greedy (eps={args.epsilon}) pbn_heads_to_flipmask -> pbn_step, "
-                f"autoreset, {common}")
+                f"autoreset, {common}, "
+                + (f"step law: settle (at most {args.settle} updates per env step, the gym facade's default; "
+                   f"pbn_step's one-step launch of pbn_rollout_settle)" if args.settle >= 2 else
+                   "step law: one synchronous update per env step"))
     if args.workload == "bdq-learn":
         return (f"BDQ training frames: {args.network} x {args.envs} envs per GPU, per step the config-5 frame "
                 f"(eps={args.epsilon}), the envs' transitions into the device replay, one update_policy step "

@@ -47,7 +47,10 @@
  *   - a pbn_net is bound to the device that was current at create time and is
  *     not thread-safe: use one per GPU / process;
  *   - envs are processed in groups of 32 consecutive envs (bit-sliced layout):
- *     n_envs and env_offset must be multiples of 32.  Randomness depends only
+ *     n_envs and env_offset must be multiples of 32, except that pbn_reset and
+ *     pbn_step take any n_envs (ABI 9: the last group is partial; its missing
+ *     envs are neither read nor written, and the others' results do not depend on
+ *     them: the scalar gym facade steps n_envs = 1).  Randomness depends only
  *     on (seed, global env id = env_offset + local id, step), so sharding envs
  *     across GPUs gives bit-identical results.
  *

@@ -777,11 +777,14 @@ int pbn_net_destroy(pbn_net* net) {
   return PBN_OK;
 }
 
-static int check_common(pbn_net* net, uint64_t env_offset, int64_t n_envs) {
+// ragged: n_envs may be any count (pbn_step: the last 32-env group is partial); env_offset is
+// always a multiple of 32 (the groups' RNG keys)
+static int check_common(pbn_net* net, uint64_t env_offset, int64_t n_envs, bool ragged = false) {
   if (!net) return fail(PBN_EINVAL, "null net");
   if (n_envs < 0) return fail(PBN_EINVAL, "n_envs < 0");
-  if ((n_envs & 31) || (env_offset & 31))
-    return fail(PBN_EINVAL, "n_envs and env_offset must be multiples of 32");
+  if (ragged ? (env_offset & 31) != 0 : ((n_envs & 31) || (env_offset & 31)))
+    return fail(PBN_EINVAL, ragged ? "env_offset must be a multiple of 32"
+                                   : "n_envs and env_offset must be multiples of 32");
   int dev = -1;
   if (hipGetDevice(&dev) != hipSuccess || dev != net->device)
     return fail(PBN_EDEVICE, "current device differs from the net's device");
@@ -803,7 +806,7 @@ static void fill_args(const pbn_net* net, StepArgs* p, uint64_t seed, uint64_t s
   a.step = step;
   a.env_offset = env_offset;
   a.n_envs = n_envs;
-  a.n_groups = n_envs / 32;
+  a.n_groups = (n_envs + 31) / 32;
   a.n_steps = 1;
   a.n_nodes = net->n_nodes;
   a.n_attr = net->n_attr;
@@ -850,7 +853,7 @@ static void fill_args(const pbn_net* net, StepArgs* p, uint64_t seed, uint64_t s
 
 int pbn_reset(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs,
               uint32_t* d_state, uint8_t* d_target, uint8_t* d_t, void* stream) {
-  int rc = check_common(net, env_offset, n_envs);
+  int rc = check_common(net, env_offset, n_envs, true);
   if (rc) return rc;
   if (n_envs == 0) return PBN_OK;
   if (!d_state || !d_target || !d_t) return fail(PBN_EINVAL, "null buffer");
@@ -867,7 +870,7 @@ static int step_impl(pbn_net* net, uint64_t seed, uint64_t step, const uint64_t*
                      int64_t n_envs, uint32_t mode, const uint32_t* d_state, uint32_t* d_flipmask,
                      uint8_t* d_target, uint8_t* d_t, uint32_t* d_state_out, uint32_t* d_final_state,
                      float* d_reward, uint8_t* d_flags, void* stream) {
-  int rc = check_common(net, env_offset, n_envs);
+  int rc = check_common(net, env_offset, n_envs, true);
   if (rc) return rc;
   if (n_envs == 0) return PBN_OK;
   if (mode & ~(PBN_MODE_AUTORESET | PBN_MODE_RANDOM_ACTIONS)) return fail(PBN_EINVAL, "unknown mode bits");
@@ -891,6 +894,19 @@ static int step_impl(pbn_net* net, uint64_t seed, uint64_t step, const uint64_t*
   a.flags = d_flags;
   a.mode = (int)mode;
   if (net->lds_wave > 160 * 1024) return fail(PBN_EINVAL, "network too large for the step kernel's LDS");
+  // the settle law on whole groups: a one-step launch of the pipelined settle kernel
+  // (pbn_rollout_settle; its env-major outputs of one step are pbn_step's), where every env runs
+  // its own update sequence and an update is one pipeline iteration, against the wave kernel's
+  // variant 3, whose wave runs every update of its slowest env as a serial chain (VERDICT r05
+  // next 2).  Ragged env counts, gates, PBN_ROLL=lean: the wave kernel.
+  if (net->settle_max >= 2 && !(n_envs & 31) && net->pipe_settle && !net->n_gates &&
+      net->lds_settle <= 64 * 1024 && net->force_roll != 2) {
+    a.slot_words = net->slot_words_settle;
+    const int64_t pblocks = (a.n_groups + 1) / 2;
+    hipLaunchKernelGGL(net->pipe_settle, dim3((unsigned)pblocks), dim3(192), net->lds_settle, (hipStream_t)stream, a);
+    HIP_OK(hipGetLastError());
+    return PBN_OK;
+  }
   const unsigned blocks = (unsigned)((a.n_groups + kWavesPerBlock - 1) / kWavesPerBlock);  // one wave per group
   const StepFn fn = net->settle_max >= 2 ? net->wave_settle : net->wave1;
   hipLaunchKernelGGL(fn, dim3(blocks), dim3(64 * kWavesPerBlock), net->lds_wave, (hipStream_t)stream, a);

@@ -918,14 +918,14 @@ template <int W, int B>
 __device__ __forceinline__ bool settle_updates(const StepArgs& a, const uint32_t* __restrict__ L, uint32_t* S,
                                             const uint4 (&rec_)[W][kNodeRecs], int lane, uint32_t ge_lo,
                                             uint32_t ge_hi, uint32_t st_lo, uint32_t (&sp)[W], int& att, bool& pert,
-                                            uint32_t& nupd) {
+                                            uint32_t& nupd, bool live) {
   const bool lo = lane < 32;
   const int l32 = lane & 31;
   const int N = a.n_nodes;
   const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
   const uint4* selq = reinterpret_cast<const uint4*>(L + a.sel_off);
   const uint32_t* htab = L + a.cdf_len + 4 * (N + 1);
-  bool open = lo && att < 0;
+  bool open = live && att < 0;   // (envs past n_envs take part in the transposes only)
   for (int k = 1; k < a.settle_max; ++k) {
     if (__ballot(open) == 0) return false;
     const uint32_t sub = (uint32_t)(k - 1);
@@ -1009,13 +1009,16 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
   const bool random_actions = (a.mode & PBN_MODE_RANDOM_ACTIONS) != 0;
   const size_t plane = (size_t)W * n;   // words per step of a [steps][W][n] output
+  // env le exists (pbn_step takes any n_envs: the last group may be ragged; its other lanes
+  // compute, take part in the cross-lane work, and load or store nothing)
+  const bool live = lo && le < n;
 
   // ---- 0. issue the one-time global loads: env state, node records, tables
   uint32_t st[W];      // current observation s of env l32 (lower lanes), carried across steps
   uint32_t tt0 = 0, tg0 = 0;
 #pragma unroll
   for (int w = 0; w < W; ++w) st[w] = 0;
-  if (lo && g < a.n_groups) {   // (waves past the end only help copy the tables)
+  if (live) {   // (waves past the end only help copy the tables)
 #pragma unroll
     for (int w = 0; w < W; ++w) st[w] = a.state[CK((size_t)w * n + le, plane, 1)] & valid_word_mask(N, w);
     tt0 = a.t[CK(le, n, 2)];
@@ -1064,7 +1067,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   uint32_t m[W], s1[W];
 #pragma unroll
   for (int w = 0; w < W; ++w) { m[w] = 0; s1[w] = st[w]; }
-  if (lo && a.obs) {
+  if (live && a.obs) {
 #pragma unroll
     for (int w = 0; w < W; ++w) a.obs[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 7)] = st[w];
   }
@@ -1137,9 +1140,11 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
     u2 = xhi;
     if (random_actions) {
       actions_from_draw<W>(c_act, N, a.n1_magic, m);
+      if (live) {
 #pragma unroll
-      for (int w = 0; w < W; ++w) a.flipmask[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 8)] = m[w];
-    } else {
+        for (int w = 0; w < W; ++w) a.flipmask[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 8)] = m[w];
+      }
+    } else if (live) {
 #pragma unroll
       for (int w = 0; w < W; ++w)
         m[w] = a.flipmask[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 6)] & valid_word_mask(N, w);
@@ -1212,9 +1217,9 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   bool unsettled = false;
   uint32_t nupd = 1;   // synchronous updates applied this step
   if constexpr (SETTLE) {   // the whole wave (cross-lane transposes)
-    unsettled = settle_updates<W, B>(a, L, S, rec_, lane, ge_lo, ge_hi, st_lo, sp, att, pert, nupd);
+    unsettled = settle_updates<W, B>(a, L, S, rec_, lane, ge_lo, ge_hi, st_lo, sp, att, pert, nupd, live);
   }
-  if (lo) {
+  if (live) {
   if constexpr (!SINGLE) {
     if (a.updates) a.updates[CK(ks * n + le, n_steps * n, 23)] = (uint16_t)min(nupd, 0xFFFFu);
   }
@@ -1253,11 +1258,11 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   tt0 = (uint32_t)tt;
 #pragma unroll
   for (int w = 0; w < W; ++w) st[w] = sp[w];
-  }  // lo
+  }  // live
   PBN_STAMP(7);
   }  // steps
 
-  if (lo) {
+  if (live) {
 #pragma unroll
     for (int w = 0; w < W; ++w) a.state_out[CK((size_t)w * n + le, plane, 16)] = st[w];
     a.t[CK(le, n, 17)] = (uint8_t)tt0;
@@ -2097,6 +2102,8 @@ pbn_rollout_settle(StepArgs a) {
   // iterations that always suffice (a step takes at most K updates and one dropped speculation):
   // a guard every wave reaches, never the exit
   const uint64_t max_it = (uint64_t)n_steps * (K + 1) + 1;
+  // the first step's index: by value, or from device memory (pbn_step_dev's one-step launch)
+  const uint64_t step0 = a.step_ptr ? *a.step_ptr : a.step;
   uint32_t* L = smem;
   const float* rtab = reinterpret_cast<const float*>(L + a.cdf_len);
   const uint32_t* htab = L + a.cdf_len + 4 * (N + 1);
@@ -2167,7 +2174,7 @@ pbn_rollout_settle(StepArgs a) {
       uint32_t* slot = slots + (size_t)(it & 1) * a.slot_words;
       PBN_PSTAMP_AT(it - kSettleStampIt + 10, 16);
       const bool live = valid && t < n_steps, first = k == 0;
-      const uint64_t step = a.step + (uint64_t)t;
+      const uint64_t step = step0 + (uint64_t)t;
       const uint32_t st_lo = (uint32_t)step;
       const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
       const uint32_t c2 = first ? (pbn::kStreamEnv << 28) : ((pbn::kStreamSettleEnv << 28) | ((k - 1) << 8));
@@ -2261,7 +2268,7 @@ pbn_rollout_settle(StepArgs a) {
 #pragma unroll
       for (int w = 0; w < W; ++w) { m[w] = 0; gam[w] = 0; }
       if (valid && t < n_steps) {
-        const uint64_t step = a.step + (uint64_t)t;
+        const uint64_t step = step0 + (uint64_t)t;
         const uint32_t st_lo = (uint32_t)step;
         const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
         const bool first = k == 0;
@@ -2396,7 +2403,7 @@ pbn_rollout_settle(StepArgs a) {
             }
       }
       uint32_t* lt_out = slots + (size_t)(it & 1) * a.slot_words + kLT + half * 32 * W;
-      const uint64_t step = a.step + (uint64_t)t;
+      const uint64_t step = step0 + (uint64_t)t;
       const uint32_t st_lo = (uint32_t)step;
       const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | ((uint32_t)((step >> 32) & 0xFFFFu) << 16);
       const uint32_t* th = a.sthr;

@@ -27,11 +27,11 @@ Drop-in for the env the reference builds with
   env.env.env chain, close()                      train_pbn_BQN.py:90, train_BDQ.py:116
 
 One PBNEnv is one env (gym semantics: no autoreset; callers call reset()).  It
-runs on the GPU as a 32-env group of which env 0 is the visible one.  Between
-steps the group lives in pinned host memory mapped into the device
-(pbn_host_buffer, _HostGroup): a step is one pbn_step launch on those pointers
-and one stream synchronisation, no copies and no torch tensors.  Use
-VectorPBNEnv for batched rollouts.
+runs on the GPU as env 0 of a VectorPBNEnv group.  Between steps the env lives
+in pinned host memory mapped into the device (pbn_host_buffer, _HostGroup): a
+step is one pbn_step launch with n_envs = 1 on those pointers and one stream
+synchronisation, no copies and no torch tensors.  Use VectorPBNEnv for batched
+rollouts.
 """
 from __future__ import annotations
 
@@ -130,14 +130,16 @@ class _Graph:
 
 
 class _HostGroup:
-    """The facade's 32-env group in pinned, device-mapped host memory (pbn_host_buffer, ABI 9):
-    two state buffers (ping-pong), the flip mask, reward, flags, target and step count, each as a
-    numpy view (host side) and a device address (the kernel's side)."""
+    """The facade's env in pinned, device-mapped host memory (pbn_host_buffer, ABI 9): two state
+    buffers (ping-pong), the flip mask, reward, flags, target and step count, each as a numpy view
+    (host side) and a device address (the kernel's side).  pbn_reset / pbn_step run on it with
+    n_envs = n (1: the other 31 envs of the group are not computed into the step's cost, in
+    particular not into the settle law's wave-wide loop)."""
 
     _LAYOUT = (("state0", 4, 1), ("state1", 4, 1), ("flip", 4, 1), ("reward", 4, 0), ("flags", 1, 0),
                ("target", 1, 0), ("t", 1, 0))
 
-    def __init__(self, words: int, n: int = 32):
+    def __init__(self, words: int, n: int = 1):
         import ctypes
         L = _lib.load()
         self.words, self.n = words, n
@@ -275,8 +277,8 @@ class PBNEnv:
 
     def _to_host(self) -> None:
         """The VectorPBNEnv's group into the host group (first step after reset / setState)."""
-        if self._hg is None:
-            self._hg = _HostGroup(self.spec.words, self._venv.n_alloc)
+        if self._hg is None:   # env 0 alone: pbn_reset / pbn_step take n_envs = 1 (ABI 9)
+            self._hg = _HostGroup(self.spec.words, 1)
         hg, venv = self._hg, self._venv
         n = hg.n
         hg.state()[:] = venv.state[:, :n].cpu().numpy().view(np.uint32)
@@ -307,7 +309,7 @@ class PBNEnv:
             venv.seed = self._seed & 0xFFFFFFFFFFFFFFFF
             L = _lib.load()
             stream = venv._stream()
-            _lib.check(L.pbn_reset(venv.net.handle, venv.seed, venv.step_index, venv.env_offset, venv.n_alloc,
+            _lib.check(L.pbn_reset(venv.net.handle, venv.seed, venv.step_index, venv.env_offset, hg.n,
                                    hg.dev[f"state{hg.cur}"], hg.dev["target"], hg.dev["t"], stream), "pbn_reset")
             _lib.check(L.pbn_stream_sync(stream), "pbn_stream_sync")
             venv.step_index += 1
@@ -357,7 +359,7 @@ class PBNEnv:
         L = _lib.load()
         nxt = 1 - hg.cur
         stream = venv._stream()
-        _lib.check(L.pbn_step(venv.net.handle, venv.seed, venv.step_index, venv.env_offset, venv.n_alloc,
+        _lib.check(L.pbn_step(venv.net.handle, venv.seed, venv.step_index, venv.env_offset, hg.n,
                               _lib.MODE_AUTORESET if venv.autoreset else 0, hg.dev[f"state{hg.cur}"], hg.dev["flip"],
                               hg.dev["target"], hg.dev["t"], hg.dev[f"state{nxt}"], None, hg.dev["reward"],
                               hg.dev["flags"], stream), "pbn_step")

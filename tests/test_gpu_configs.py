@@ -11,7 +11,8 @@ once per frame (bdq_model/__init__.py:177).
             tests/test_gpu_rccl.py::test_rccl_config4_shard_at_size
   config 5  the BatchedBDQ frame at 32,768 envs (262,144 over 8 GPUs): six frames, the heads
             the frame consumed replayed through the oracle chain (dueling + epsilon-greedy +
-            flip masks + step), every output bit-exact
+            flip masks + step), every output bit-exact, under the one-update law and under the
+            facade's settle law (cap 64)
 """
 import numpy as np
 import pytest
@@ -74,9 +75,11 @@ def test_config3_pbn70_rollout_at_1m():
                               want["reward"].numpy().view(np.uint32)), lo
 
 
-@pytest.mark.parametrize("eps", [0.0, 0.1])
-def test_config5_bdq_frames_at_32768(eps):
-    spec = spec_for("pbn28", perturbation=0.01, horizon=20)
+@pytest.mark.parametrize("eps,settle", [(0.0, 0), (0.1, 0), (0.1, 64)])
+def test_config5_bdq_frames_at_32768(eps, settle):
+    """settle = 64: the gym facade's default law, the one train_BDQ.py:50 -> bdq_model/__init__.py:
+    172-220 runs (pbn_step's one-step launch of the pipelined settle kernel)."""
+    spec = spec_for("pbn28", perturbation=0.01, horizon=20, settle=settle)
     n, seed, frames = 32768, 0, 6
     torch.manual_seed(0)
     env = VectorPBNEnv(spec, n, seed=seed)

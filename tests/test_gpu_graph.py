@@ -21,9 +21,11 @@ def u32(x):
     return x.cpu().numpy().view(np.uint32)
 
 
-@pytest.mark.parametrize("name,p", [("pbn28", 0.02), ("pbn70", 0.01)])
-def test_step_dev_matches_step(name, p):
-    spec = EnvSpec(load_network(name), load_attractors(name), perturbation=p, horizon=6)
+@pytest.mark.parametrize("name,p,settle", [("pbn28", 0.02, 0), ("pbn70", 0.01, 0), ("pbn28", 0.02, 64)])
+def test_step_dev_matches_step(name, p, settle):
+    """settle = 64: pbn_step_dev's one-step launch of the pipelined settle kernel reads the step
+    index from device memory as the by-value form passes it."""
+    spec = EnvSpec(load_network(name), load_attractors(name), perturbation=p, horizon=6, settle=settle)
     n, seed = 2048, 5
     a, b = VectorPBNEnv(spec, n, seed=seed), VectorPBNEnv(spec, n, seed=seed)
     a.reset()
@@ -79,8 +81,8 @@ def test_act_dev_matches_act():
         assert torch.equal(env.flipmask, fm) and torch.equal(agent.actions, acts), eps
 
 
-def _learner(n, seed, fused):
-    spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.01)
+def _learner(n, seed, fused, settle=0):
+    spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.01, settle=settle)
     env = VectorPBNEnv(spec, n, seed=seed)
     torch.manual_seed(4)
     lr = BDQLearner(env, BranchingQNetwork((28, 28), 29, 3), capacity=8 * n, learning_starts=2 * n,
@@ -90,14 +92,14 @@ def _learner(n, seed, fused):
     return env, lr
 
 
-@pytest.mark.parametrize("fused", [True, False])
-def test_captured_learner_matches_eager(fused):
+@pytest.mark.parametrize("fused,settle", [(True, 0), (False, 0), (True, 64)])
+def test_captured_learner_matches_eager(fused, settle):
     """epsilon = 1: actions do not depend on Q, so env and ring must agree exactly.  Both update
     paths: the fused HIP update (pbn_bdq_learn) and the PyTorch one (bdq_update + Adam), each
-    with its own captured body."""
+    with its own captured body; and the captured frame under the facade's settle law."""
     n = 1024
-    env_e, eager = _learner(n, 21, fused)
-    env_g, graph = _learner(n, 21, fused)
+    env_e, eager = _learner(n, 21, fused, settle)
+    env_g, graph = _learner(n, 21, fused, settle)
     assert (graph.fused is not None) == fused and (eager.fused is not None) == fused
     graph.capture()
     assert graph.updates == 3 and graph.frames == 4

@@ -140,7 +140,7 @@ def test_abi_rejects_bad_arguments():
     rc = L.pbn_step(env.net.handle, 0, 0, 16, 64, 3, env.state.data_ptr(), env.flipmask.data_ptr(),
                     env.target.data_ptr(), env.t.data_ptr(), env._state_next.data_ptr(), None,
                     env.reward.data_ptr(), env.flags.data_ptr(), None)
-    assert rc == -22 and b"multiples of 32" in L.pbn_last_error()
+    assert rc == -22 and b"of 32" in L.pbn_last_error()
     rc = L.pbn_step(env.net.handle, 0, 0, 0, 64, 3, env.state.data_ptr(), env.flipmask.data_ptr(),
                     env.target.data_ptr(), env.t.data_ptr(), env.state.data_ptr(), None,
                     env.reward.data_ptr(), env.flags.data_ptr(), None)
@@ -300,3 +300,59 @@ def test_wide_random_network(monkeypatch):
     run_pair(spec, 1024, 5, mode=3, start_random=True)
     monkeypatch.setenv("PBN_ROLL", "lean")
     run_rollout_pair(spec, 1024, 6, 3)
+
+
+@pytest.mark.parametrize("name", ["pbn28", "pbn70"])
+@pytest.mark.parametrize("settle", [0, 6])
+def test_step_ragged_env_counts(name, settle):
+    """pbn_reset / pbn_step with n_envs not a multiple of 32 (ABI 9; the scalar facade steps
+    n_envs = 1): [W][n] buffers sized exactly, followed by canaries that must stay untouched;
+    every output of the n envs equals the oracle's for the same envs of a padded batch (the
+    missing envs of the last group change nothing: draws are keyed per env or per group)."""
+    spec = make_spec(name, perturbation=0.05, horizon=5, settle=settle)
+    env = VectorPBNEnv(spec, 32)
+    L, h, W, dev = _lib.load(), env.net.handle, spec.words, env.device
+    seed, off = 99, 64
+    for n in (1, 5, 33, 70):
+        pad = (n + 31) // 32 * 32
+        CAN = 64
+        def buf(count, dtype):
+            return torch.full((count + CAN,), 0x5A, dtype=dtype, device=dev)
+        st, tg, tt = buf(W * n, torch.int32), buf(n, torch.uint8), buf(n, torch.uint8)
+        _lib.check(L.pbn_reset(h, seed, 0, off, n, st.data_ptr(), tg.data_ptr(), tt.data_ptr(), None), "reset")
+        ost, otg, ott = oracle.reset(spec, seed, 0, off, pad)
+        torch.cuda.synchronize()
+        assert np.array_equal(u32(st[:W * n]).reshape(W, n), ost[:, :n])
+        assert np.array_equal(tg[:n].cpu().numpy(), otg[:n]) and np.array_equal(tt[:n].cpu().numpy(), ott[:n])
+        rng = np.random.default_rng(n)
+        for k, mode in enumerate((3, 1, 0)):
+            flip = (rng.integers(0, 2 ** 32, size=(W, pad), dtype=np.uint64).astype(np.uint32) & np.uint32(0x00410020))
+            if spec.n % 32:
+                flip[W - 1] &= np.uint32((1 << (spec.n % 32)) - 1)
+            fm = buf(W * n, torch.int32)
+            fm[:W * n] = torch.from_numpy(np.ascontiguousarray(flip[:, :n]).view(np.int32).reshape(-1)).to(dev)
+            out, fin = buf(W * n, torch.int32), buf(W * n, torch.int32)
+            rew, fl = buf(n, torch.float32), buf(n, torch.uint8)
+            _lib.check(L.pbn_step(h, seed, 1 + k, off, n, mode, st.data_ptr(), fm.data_ptr(), tg.data_ptr(),
+                                  tt.data_ptr(), out.data_ptr(), fin.data_ptr(), rew.data_ptr(), fl.data_ptr(), None),
+                       "pbn_step")
+            ref = oracle.step(spec, seed, 1 + k, off, np.pad(ost[:, :n], ((0, 0), (0, pad - n))), flip,
+                              np.pad(otg[:n], (0, pad - n)), np.pad(ott[:n], (0, pad - n)), mode)
+            torch.cuda.synchronize()
+            tag = (n, k)
+            assert np.array_equal(u32(out[:W * n]).reshape(W, n), ref["state_out"][:, :n]), tag
+            assert np.array_equal(u32(fin[:W * n]).reshape(W, n), ref["final_state"][:, :n]), tag
+            assert np.array_equal(fl[:n].cpu().numpy(), ref["flags"][:n]), tag
+            assert np.array_equal(rew[:n].cpu().numpy().view(np.uint32), ref["reward"][:n].view(np.uint32)), tag
+            assert np.array_equal(tg[:n].cpu().numpy(), ref["target"][:n]), tag
+            assert np.array_equal(tt[:n].cpu().numpy(), ref["t"][:n]), tag
+            if mode & 2:
+                assert np.array_equal(u32(fm[:W * n]).reshape(W, n), ref["flipmask"][:, :n]), tag
+            for b in (st, tg, tt, fm, out, fin, rew, fl):   # nothing past the n envs
+                tail = b[-CAN:]
+                assert torch.equal(tail, torch.full_like(tail, 0x5A)), tag
+            st, ost, otg, ott = out, ref["state_out"], ref["target"], ref["t"]
+    assert L.pbn_step(h, seed, 0, 16, 1, 0, st.data_ptr(), fm.data_ptr(), tg.data_ptr(), tt.data_ptr(),
+                      out.data_ptr(), None, rew.data_ptr(), fl.data_ptr(), None) == -22   # offset not a multiple of 32
+    assert L.pbn_rollout(h, seed, 0, 0, 33, 1, 0, st.data_ptr(), fm.data_ptr(), tg.data_ptr(), tt.data_ptr(), None,
+                         None, rew.data_ptr(), fl.data_ptr(), None) == -22   # rollouts keep whole groups

@@ -20,10 +20,12 @@ def u32(x):
     return x.cpu().numpy().view(np.uint32)
 
 
-@pytest.mark.parametrize("fused", [True, False])
-def test_learner_transitions_match_oracle(fused):
-    spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.02)
-    n, seed = 1024, 17
+@pytest.mark.parametrize("fused,settle,n", [(True, 0, 1024), (False, 0, 1024), (True, 64, 32768)])
+def test_learner_transitions_match_oracle(fused, settle, n):
+    """settle = 64 at 32,768 envs: BDQLearner's frames under the facade's default law (config 5's
+    per-GPU share), every stored transition against the oracle chain."""
+    spec = EnvSpec(load_network("pbn28"), load_attractors("pbn28"), perturbation=0.02, settle=settle)
+    seed = 17
     env = VectorPBNEnv(spec, n, seed=seed)
     torch.manual_seed(0)
     learner = BDQLearner(env, BranchingQNetwork((28, 28), 29, 3), capacity=4 * n, learning_starts=2 * n,

@@ -1,10 +1,11 @@
 """The settle law on the GPU (include/pbn_env.h "Step law"): kernels == oracle bit for bit, and
 the reference's bb33 evaluation replayed through the gym facade on the device.
 
-pbn_step runs the wave kernel's settle variant 3 when the descriptor's settle_max >= 2;
-pbn_rollout runs the pipelined settle kernel (pbn_rollout_settle: one update per iteration, a
-group's step continues while any env is outside every attractor) for networks without gates,
-and the wave kernel's variant 4 for networks with gates or under PBN_ROLL=lean.  Every output is
+pbn_rollout runs the pipelined settle kernel (pbn_rollout_settle: one update per iteration, every
+env its own update sequence, an env that settles starting its next step) for networks without
+gates, and the wave kernel's variant 4 for networks with gates or under PBN_ROLL=lean; pbn_step
+runs a one-step launch of the same pipelined kernel on whole groups (the wave kernel's variant 3
+for ragged env counts, gates, or PBN_ROLL=lean).  Every output is
 compared with oracle/pbn_oracle.c, including the PBN_FLAG_UNSETTLED bit of envs that hit the cap
 and the per-env-step update counts (pbn_rollout_ex's d_updates, the settle lengths).
 """
@@ -34,9 +35,13 @@ def settle_spec(name, settle, **kw):
     return EnvSpec(load_network(name), load_attractors(name), settle=settle, **kw)
 
 
+@pytest.mark.parametrize("variant", ["auto", "lean"])
 @pytest.mark.parametrize("name", ["pbn7", "pbn28", "pbn70", "bb33"])
-@pytest.mark.parametrize("settle", [2, 9])
-def test_settle_step_matches_oracle(name, settle):
+@pytest.mark.parametrize("settle", [2, 9, 64])
+def test_settle_step_matches_oracle(name, settle, variant, monkeypatch):
+    """pbn_step under the settle law: the one-step launch of the pipelined settle kernel (auto;
+    bb33 has gates and takes the wave kernel) and the wave kernel's variant 3 (lean)."""
+    monkeypatch.setenv("PBN_ROLL", variant)
     spec = settle_spec(name, settle, perturbation=0.02, horizon=6)
     run_pair(spec, 2048, 6, mode=3, env_offset=1024)
     run_pair(spec, 1024, 4, mode=0, start_random=True)
