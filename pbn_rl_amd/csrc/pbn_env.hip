@@ -685,8 +685,11 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   // reset target and action count [64], selection planes [lq][64W]} | C [parity][64]{t, k}
   net->slot_words_settle = 192 * W + 64 + net->lq * 64 * W;
   // + ctl [2][64] uint4 + the packed thresholds [lq][W][16]
+  // + the output rows [settle_stage_rows(W)][settle_row_words(W)], the stored-row counter [2] and
+  // the rows' output pointers (6 x 8 bytes)
   net->lds_settle = ((size_t)net->tab_words + 64 * (size_t)W + 2 * (size_t)net->slot_words_settle + 512 +
-                     (size_t)net->lq * W * 16) * 4;
+                     (((size_t)net->lq * W * 16 + 3) & ~(size_t)3) +
+                     (size_t)settle_stage_rows(W) * settle_row_words(W) + 2 + 12 + 2) * 4;
   net->pipe = pick_pipe(W, d->prob_bits, net->max_nf > kNodeRecs);
   net->reset = pick_reset(W);
   // multiply-high divisors (exact for the operand ranges used: see actions_from_draw, autoreset)

@@ -2055,6 +2055,26 @@ __global__ void __launch_bounds__(256) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
 // applies R(i-1) (EnvPlan); the state wave publishes each env's decision C (next update) in LDS.
 // Results are bit-identical to pbn_step_wave's settle variants and to oracle/pbn_oracle.c.
 constexpr uint32_t kNoUpd = 0xFFFFFFFFu;
+
+// pbn_rollout_settle's output rows in LDS: every env ends its steps in its
+// own iterations, so the per-env stores of the round-5 kernel were a few lanes wide and went out
+// as partial-line write-backs (2.1x the outputs' bytes at 20 steps, 12.6x at 100).  The block's
+// 64 envs now put step t's outputs into row t mod R of a ring in LDS, and the env-draw wave (the
+// role with the most barrier slack) stores a row with full-line non-temporal stores once every
+// env of the block has ended step t.  An env at most R - 1 steps ahead of the block's slowest
+// waits (its update is produced and not applied), so a row is never reused before it is stored.
+// Row layout (words): final [W][64] | obs [W][64] | flip mask [W][64] | reward [64] | flags
+// [64 bytes] | update counts [64 u16].
+__host__ __device__ constexpr int settle_stage_rows(int W) { return W == 1 ? 16 : (W == 2 ? 8 : 4); }
+__host__ __device__ constexpr int settle_row_words(int W) { return 3 * 64 * W + 64 + 16 + 32; }
+struct StageOut {   // the output pointers the row stores use, copied to LDS at kernel start
+  uint32_t* final_state;
+  uint32_t* obs;
+  uint32_t* flipmask;
+  float* reward;
+  uint8_t* flags;
+  uint16_t* updates;
+};
 constexpr uint32_t kSettleStampIt = 300;   // stamps build: the iteration the settle kernel clocks
 
 // The per-env update plan of pbn_rollout_settle, in that env's lane of every wave (VGPRs; the
@@ -2127,6 +2147,23 @@ pbn_rollout_settle(StepArgs a) {
   if (a.settle_pk) {
     for (int i = (int)threadIdx.x; i < lq * W * 16; i += (int)blockDim.x) thr_l[i] = a.sthr_pk[i];
   }
+  // the output rows [R][settle_row_words(W)] after the thresholds, then the lowest step not yet
+  // stored, by iteration parity (written by the env-draw wave in iteration i, read by the state
+  // wave in iteration i + 1)
+  constexpr int R = settle_stage_rows(W), RW = settle_row_words(W);
+  constexpr int kSF = 0, kSO = 64 * W, kSM = 128 * W, kSR = 192 * W, kSFL = 192 * W + 64, kSU = 192 * W + 80;
+  uint32_t* stg = thr_l + ((lq * W * 16 + 3) & ~3);
+  uint32_t* stg_base = stg + R * RW;
+  uint64_t* stg_out = reinterpret_cast<uint64_t*>(stg_base + 2);   // the row stores' pointers (StageOut)
+  if (threadIdx.x < 2) stg_base[threadIdx.x] = 0u;
+  if (threadIdx.x == 0) {
+    stg_out[0] = reinterpret_cast<uint64_t>(a.final_state);
+    stg_out[1] = reinterpret_cast<uint64_t>(a.obs);
+    stg_out[2] = reinterpret_cast<uint64_t>(a.flipmask);
+    stg_out[3] = reinterpret_cast<uint64_t>(a.reward);
+    stg_out[4] = reinterpret_cast<uint64_t>(a.flags);
+    stg_out[5] = reinterpret_cast<uint64_t>(a.updates);
+  }
                                                          // (0, 0); envs of groups past the end: finished
   uint32_t st[W];
   uint32_t tt0 = 0, tg0 = 0;
@@ -2156,6 +2193,45 @@ pbn_rollout_settle(StepArgs a) {
   // attractors and N <= 31 for single-word states -- every kaban network -- branch-free)
   const bool env_fast = __builtin_amdgcn_readfirstlane((u_fl & 4u) && a.gap_exact == 2 && a.n_attr >= 2 &&
                                                        a.att_single && (W > 1 || N <= 31) ? 1 : 0) != 0;
+  // the env-draw wave's row stores: rows [base, t_lo) once every env of the block has ended those
+  // steps (t_lo = the block's lowest current step, from the decisions C), full-line non-temporal
+  // stores of 64 consecutive envs; at the loop's exit every remaining row
+  uint32_t base = 0;
+  const int nv = (int64_t)blockIdx.x * 2 + 1 < a.n_groups ? 64 : 32;   // envs of this block (an odd group
+                                                                       // count leaves a phantom half)
+  auto flush_rows = [&](uint32_t ct, uint32_t it) __attribute__((always_inline)) {
+    while (base < n_steps && __ballot(valid && ct <= base) == 0) {
+      // the output pointers from their LDS copy, read here on this rare path (taken from the
+      // kernel arguments, the compiler hoisted them out of the step loops, where they held SGPRs
+      // and spilled: 2 -> 25 SGPR spills); stores through VGPR addresses
+      const StageOut* ap = reinterpret_cast<const StageOut*>(stg_out);
+      const uint32_t* row = stg + (size_t)(base % R) * RW;
+      const size_t er = (size_t)base * (size_t)n + (size_t)blockIdx.x * 64 + (size_t)lane;   // [t][n] element
+      const size_t ep = (size_t)base * plane + (size_t)blockIdx.x * 64 + (size_t)lane;      // [t][W][n] element
+      if (valid) {
+        if (u_fl & 2u) {
+#pragma unroll
+          for (int w = 0; w < W; ++w) __builtin_nontemporal_store(row[kSF + w * 64 + lane], ap->final_state + CK(ep + (size_t)w * n, (size_t)n_steps * plane, 10));
+        }
+        if (u_fl & 1u) {
+#pragma unroll
+          for (int w = 0; w < W; ++w) __builtin_nontemporal_store(row[kSO + w * 64 + lane], ap->obs + CK(ep + (size_t)w * n, (size_t)n_steps * plane, 7));
+        }
+        if (u_fl & 4u) {
+#pragma unroll
+          for (int w = 0; w < W; ++w) __builtin_nontemporal_store(row[kSM + w * 64 + lane], ap->flipmask + CK(ep + (size_t)w * n, (size_t)n_steps * plane, 8));
+        }
+        __builtin_nontemporal_store(__uint_as_float(row[kSR + lane]), ap->reward + CK(er, (size_t)n_steps * n, 11));
+      }
+      const size_t eb = (size_t)base * (size_t)n + (size_t)blockIdx.x * 64;   // the row's first env
+      if (lane < nv / 4)   // the flags, four envs per dword
+        __builtin_nontemporal_store(row[kSFL + lane], reinterpret_cast<uint32_t*>(ap->flags) + CK(eb / 4 + lane, (size_t)n_steps * n / 4, 15));
+      if ((u_fl & 32u) && lane < nv / 2)   // the update counts, two envs per dword
+        __builtin_nontemporal_store(row[kSU + lane], reinterpret_cast<uint32_t*>(ap->updates) + CK(eb / 2 + lane, (size_t)n_steps * n / 2, 23));
+      ++base;
+    }
+    if (lane == 0) stg_base[it & 1] = base;
+  };
   if (role == 1 && env_fast) {
     // ---- the draws of each env's update R(i), env `lane`: one Philox call (ENV at k = 0,
     // SETTLE_ENV at k >= 1); the step's draws are computed on every lane and kept where k = 0
@@ -2169,6 +2245,7 @@ pbn_rollout_settle(StepArgs a) {
       uint4 C = ctl[((it + 1) & 1) * 64 + lane];   // {C(i), R(i)}
       // all four words from one read, ahead of the exit test (split, R came in a second round trip)
       asm volatile("" : "+v"(C.x), "+v"(C.y), "+v"(C.z), "+v"(C.w));
+      flush_rows(C.x, it);
       if (__ballot(C.x < n_steps) == 0 || (uint64_t)it > max_it) break;
       const uint32_t t = C.z, k = C.w;
       uint32_t* slot = slots + (size_t)(it & 1) * a.slot_words;
@@ -2236,9 +2313,10 @@ pbn_rollout_settle(StepArgs a) {
           set_bit<W>(gam, pos, N);
         }
       }
-      if (live && first) {
+      if (live && first && t < base + R) {   // (an update past the ring is not applied: no row)
+        uint32_t* row = stg + (size_t)(t % R) * RW;
 #pragma unroll
-        for (int w = 0; w < W; ++w) LANE_STV(a.flipmask, ((size_t)t * plane + (size_t)w * n) + (size_t)le, (size_t)n_steps * plane, 8, m[w]);
+        for (int w = 0; w < W; ++w) row[kSM + w * 64 + lane] = m[w];
       }
       PBN_PSTAMP_AT(it - kSettleStampIt + 10, 17);
 #pragma unroll
@@ -2260,6 +2338,7 @@ pbn_rollout_settle(StepArgs a) {
       uint4 C = ctl[((it + 1) & 1) * 64 + lane];   // {C(i), R(i)}
       // all four words from one read, ahead of the exit test (split, R came in a second round trip)
       asm volatile("" : "+v"(C.x), "+v"(C.y), "+v"(C.z), "+v"(C.w));
+      flush_rows(C.x, it);
       if (__ballot(C.x < n_steps) == 0 || (uint64_t)it > max_it) break;
       const uint32_t t = C.z, k = C.w;
       uint32_t* slot = slots + (size_t)(it & 1) * a.slot_words;
@@ -2314,8 +2393,11 @@ pbn_rollout_settle(StepArgs a) {
           u2 = (uint32_t)(xr >> 32);
           if (u_fl & 4u) {
             actions_from_draw<W>(c_act, N, a.n1_magic, m);
+            if (t < base + R) {   // (an update past the ring is not applied: no row)
+              uint32_t* row = stg + (size_t)(t % R) * RW;
 #pragma unroll
-            for (int w = 0; w < W; ++w) LANE_STV(a.flipmask, ((size_t)t * plane + (size_t)w * n) + (size_t)le, (size_t)n_steps * plane, 8, m[w]);
+              for (int w = 0; w < W; ++w) row[kSM + w * 64 + lane] = m[w];
+            }
           } else {
 #pragma unroll
             for (int w = 0; w < W; ++w)
@@ -2455,18 +2537,6 @@ pbn_rollout_settle(StepArgs a) {
     bool pacc = false;
 #pragma unroll
     for (int w = 0; w < W; ++w) rs[w] = 0;
-    if (valid && (u_fl & 1u)) {
-#pragma unroll
-      for (int w = 0; w < W; ++w) LANE_STV(a.obs, (size_t)w * n + (size_t)le, (size_t)n_steps * plane, 7, st[w]);
-    }
-    // the epilogue's output bases, held in VGPRs (laundered each iteration): as SGPRs they came
-    // from the kernel arguments' 16-dword load tuples, which the allocator spilled and restored
-    // whole (16 v_readlane_b32 per tuple) to use two of them
-    uint32_t* o_final = a.final_state;
-    uint16_t* o_upd = a.updates;
-    float* o_rew = a.reward;
-    uint8_t* o_flags = a.flags;
-    uint32_t* o_obs = a.obs;
     // one loop per function count KF (mnf, at most kNodeRecs): no switch inside the loop
     auto state_loop = [&](auto kf_c) __attribute__((always_inline)) {
     constexpr int KF = decltype(kf_c)::value;
@@ -2482,8 +2552,12 @@ pbn_rollout_settle(StepArgs a) {
       PBN_ISA_LOOP("settle_state", KF);
       PBN_PSTAMP(it - kSettleStampIt + 10, 0);
       if (__ballot(Ct < n_steps) == 0 || (uint64_t)it > max_it) break;
-      const bool proc = p.v && p.Pt < n_steps;
+      // the lowest step whose row is not stored yet, as the env-draw wave left it in the iteration
+      // that produced this update: an update R - 1 or more steps past it waits (no row to write)
+      const uint32_t sbase = stg_base[(it + 1) & 1];
+      const bool proc = p.v && p.Pt < n_steps && p.Pt < sbase + R;
       const uint32_t t = p.Pt, k = p.Pk;
+      uint32_t* row = stg + (size_t)(t % R) * RW;
       const uint32_t* slot = slots + (size_t)((it + 1) & 1) * a.slot_words;
       const uint32_t* lt_in = slot + kLT + half * 32 * W;
       uint32_t s1[W], gam[W];
@@ -2494,7 +2568,9 @@ pbn_rollout_settle(StepArgs a) {
         gam[w] = slot[kGP + w * 64 + lane];
         pk = pk || gam[w] != 0;
       }
-      if (proc && k == 0) {   // the step's reset draw and action count
+      if (proc && k == 0) {   // the step's reset draw and action count; the step's observation
+#pragma unroll
+        for (int w = 0; w < W; ++w) row[kSO + w * 64 + lane] = st[w];
 #pragma unroll
         for (int w = 0; w < W; ++w) rs[w] = slot[kRS + w * 64 + lane];
         const uint32_t info = slot[kIN + lane];
@@ -2562,18 +2638,11 @@ pbn_rollout_settle(StepArgs a) {
       ctl[(it & 1) * 64 + lane] = make_uint4(Ct, Ck, p.Rt, p.Rk);
 #pragma unroll
       for (int w = 0; w < W; ++w) st[w] = cur[w];
-      asm volatile("" : "+v"(o_final), "+v"(o_upd), "+v"(o_rew), "+v"(o_flags), "+v"(o_obs));
       if (end) {
-        // the epilogue of step t: one element index for every output (computed once, ahead of the
-        // stores' uniform branches; n < 2^31, so t * n + le is one v_mad_u64_u32)
-        const size_t tz = t;
-        const size_t er = (uint64_t)t * (uint32_t)n + (uint64_t)(uint32_t)le;    // [t][n] outputs
-        const size_t ep = W == 1 ? er : tz * plane + (size_t)le;                   // [t][W][n] outputs
-        if (u_fl & 2u) {
+        // the epilogue of step t, into the block's row of step t (stored by the env-draw wave)
 #pragma unroll
-          for (int w = 0; w < W; ++w) LANE_STV(o_final, ep + (size_t)w * n, (size_t)n_steps * plane, 10, cur[w]);
-        }
-        if (u_fl & 32u) LANE_STV(o_upd, er, (size_t)n_steps * n, 23, (uint16_t)min(k + 1, 0xFFFFu));
+        for (int w = 0; w < W; ++w) row[kSF + w * 64 + lane] = cur[w];
+        reinterpret_cast<uint16_t*>(row + kSU)[lane] = (uint16_t)min(k + 1, 0xFFFFu);
         const bool in_attr = att >= 0;
         const bool term = in_attr && (uint32_t)att == tg0;
         const bool wrong = in_attr && !term;
@@ -2587,16 +2656,12 @@ pbn_rollout_settle(StepArgs a) {
         // wrong branches, it cost two round trips in the epilogue)
         float4 r4 = reinterpret_cast<const float4*>(rtab)[pcv];
         asm volatile("" : "+v"(r4.x), "+v"(r4.y), "+v"(r4.z));
-        LANE_STV(o_rew, er, (size_t)n_steps * n, 11, term ? r4.z : (wrong ? r4.y : r4.x));
-        LANE_STV(o_flags, er, (size_t)n_steps * n, 15, (uint8_t)fl);
+        row[kSR + lane] = __float_as_uint(term ? r4.z : (wrong ? r4.y : r4.x));
+        reinterpret_cast<uint8_t*>(row + kSFL)[lane] = (uint8_t)fl;
         tg0 = rst ? rtv : tg0;
         tt0 = rst ? 0u : (uint32_t)tt;
 #pragma unroll
         for (int w = 0; w < W; ++w) st[w] = rst ? rs[w] : cur[w];
-        if ((u_fl & 1u) && tz + 1 < n_steps) {
-#pragma unroll
-          for (int w = 0; w < W; ++w) LANE_STV(o_obs, ep + plane + (size_t)w * n, (size_t)n_steps * plane, 7, st[w]);
-        }
       }
       PBN_PSTAMP(it - kSettleStampIt + 10, 1);
       lds_barrier();
