@@ -130,6 +130,7 @@ struct pbn_net {
   int att_off = 0;
   int sel_off = 0;
   int nrec_off = 0;
+  int cm_off = 0;   // the pipelined kernel's threshold digit masks in the image (W == 1)
   int n_cls = 0;
   uint32_t uthr[kNodeRecs] = {0, 0, 0, 0};
   int gap_exact = 1;
@@ -658,6 +659,25 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
       }
     }
   }
+  // the pipelined one-update kernel's threshold digit masks (single-word states), lane-major
+  // [32][sel_mask_stride(B)]: mask (i, q, d) = ~0 if bit B-1-d of node i's threshold q is set.  In
+  // the image, they arrive with the table copy; built by each block from the LDS records, they
+  // cost a second prologue barrier (0.48 us of a 20-step launch, DESIGN.md "Launch anatomy")
+  net->cm_off = 0;
+  if (W == 1) {
+    while (tab.size() & 3) tab.push_back(0u);
+    net->cm_off = (int)tab.size();
+    const int B = d->prob_bits, S = sel_mask_stride(B);
+    std::vector<uint32_t> cmv((size_t)32 * S, 0u);
+    for (int i = 0; i < N; ++i) {
+      const int f0 = d->node_func_start[i], nf = d->node_func_start[i + 1] - f0;
+      for (int q = 0; q < kNodeRecs - 1 && q < nf - 1; ++q) {
+        const uint32_t c = recs[f0 + q].thr;
+        for (int dd = 0; dd < B; ++dd) cmv[(size_t)i * S + q * B + dd] = ((c >> (B - 1 - dd)) & 1u) ? ~0u : 0u;
+      }
+    }
+    tab.insert(tab.end(), cmv.begin(), cmv.end());
+  }
   while (tab.size() & 3) tab.push_back(0u);   // the kernels copy the image as uint4
   net->tab_words = (int)tab.size();
   net->n_funcs = d->n_funcs;
@@ -669,10 +689,8 @@ int pbn_net_create(const pbn_net_desc* d, pbn_net** out) {
   }
   net->lds_wave = ((size_t)net->tab_words + (size_t)kWavesPerBlock * net->wave_words) * 4;
   net->slot_words = (3 * W + 1) * 64 + net->lq * 64 * W;
-  // + the selection wave's threshold digit masks (W == 1): [32][sel_mask_stride(B)], lane-major
-  const size_t cm_words = 32 * (size_t)sel_mask_stride(d->prob_bits);
-  net->lds_pipe = ((size_t)net->tab_words + 64 * (size_t)W + 2 * (size_t)net->slot_words +
-                   (W == 1 ? cm_words : 0)) * 4;
+  // (the selection wave's threshold digit masks are part of the image: cm_off)
+  net->lds_pipe = ((size_t)net->tab_words + 64 * (size_t)W + 2 * (size_t)net->slot_words) * 4;
   // compact records for the wave kernel: {inputs as bytes, 4-input truth table, threshold, 0}
   net->wave1 = pick_wave<1>(W, d->prob_bits);
   net->wave_lean = pick_wave<2>(W, d->prob_bits);
@@ -822,6 +840,7 @@ static void fill_args(const pbn_net* net, StepArgs* p, uint64_t seed, uint64_t s
   a.att_off = net->att_off;
   a.sel_off = net->sel_off;
   a.nrec_off = net->nrec_off;
+  a.cm_off = net->cm_off;
   a.n_cls = net->n_cls;
   a.max_nf = net->max_nf;
   a.lq = net->lq;

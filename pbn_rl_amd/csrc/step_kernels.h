@@ -76,6 +76,8 @@ struct StepArgs {
   int att_off;       // LDS image offset of attractor start[A+1] | states[S][W] (wave kernel)
   int sel_off;       // LDS image offset of the leaf selectors, uint4 [kNodeRecs][2][32W] (wave kernel)
   int nrec_off;      // LDS image offset of the node records, record-major uint4 [kNodeRecs][32W]
+  int cm_off;        // LDS image offset of pbn_rollout_pipe's threshold digit masks (W == 1),
+                     // [32][sel_mask_stride(B)] lane-major
   int n_cls;         // 1..4: the first kNodeRecs thresholds of every node take one of n_cls values
                      // uthr[0..n_cls) (record .y = class index); 0: per-node thresholds
   uint32_t uthr[kNodeRecs];
@@ -1448,33 +1450,13 @@ __global__ void __launch_bounds__(256) PBN_PIPE_ATTR pbn_rollout_pipe(StepArgs a
   uint32_t u_fl = __builtin_amdgcn_readfirstlane((a.obs ? 1u : 0u) | (a.final_state ? 2u : 0u) |
                                                  (random_actions ? 4u : 0u) | ((a.mode & PBN_MODE_AUTORESET) ? 8u : 0u) |
                                                  (a.att_single ? 16u : 0u));
-  // digit masks of the first kNodeRecs - 1 thresholds of every node, [q][d][32W], for the
-  // selection wave's compares, built from the LDS copy of the node records once it has
-  // landed (from the global records this was two dependent L2 round trips per entry, eight
-  // entries per thread: most of the launch's fixed cost)
-  // (single-word states only: for W > 1 the extra LDS costs more occupancy than it saves,
-  // measured -15 % on pbn70 x 1M)
-  uint32_t* cm = slots + 2 * (size_t)a.slot_words;
+  // digit masks of the first kNodeRecs - 1 thresholds of every node, lane-major
+  // [32][sel_mask_stride(B)], for the selection wave's compares: built on the host into the table
+  // image (single-word states only: for W > 1 the extra LDS cost more occupancy than it saved,
+  // measured -15 % on pbn70 x 1M).  Built here from the records, they took a second barrier.
+  const uint32_t* cm = L + a.cm_off;
   __syncthreads();
   PBN_RSTAMP(1);
-  if constexpr (W == 1) {
-    // thread t: record (q, i) = p = t mod 96 and digits [h B/2, (h+1) B/2), h = t / 96 (192
-    // threads = two per record: two LDS reads, then B/2 independent writes)
-    static_assert((kNodeRecs - 1) * 32 * 2 == 192, "cm build assumes 192 threads");
-    if (role < 3) {
-      const int p = (int)threadIdx.x % ((kNodeRecs - 1) * 32), h = (int)threadIdx.x / ((kNodeRecs - 1) * 32);
-      const int i = p & 31, q = p >> 5;
-      uint32_t c = 0;
-      if (i < N && q < (int)recL[i].w - 1) c = recL[q * 32 * W + i].z;
-#pragma unroll
-      for (int dd = 0; dd < B / 2; ++dd) {
-        const int d = h * (B / 2) + dd;
-        const uint32_t v = ((c >> (B - 1 - d)) & 1u) ? ~0u : 0u;
-        cm[i * sel_mask_stride(B) + q * B + d] = v;
-      }
-    }
-    __syncthreads();
-  }
   if (role == 3) {   // (pbn_rollout_copy) past the block's last __syncthreads
     ride_copy_wave(a, lane);
     return;
