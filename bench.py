@@ -890,17 +890,24 @@ def main():
     learn_ms = None
     if args.workload == "bdq-learn" and learner.fused is not None:
         # the fused update (pbn_bdq_learn's three launches) timed alone: 50 back to back on the
-        # frame's batch rows, replayed from one hipGraph (after the timed frames: they train on)
+        # frame's batch rows, replayed from one hipGraph (after the timed frames), with the
+        # learner's parameters, Adam state, tables and loss snapshotted before and restored after,
+        # so that the learner leaves the bench as its last frame left it
+        fu = learner.fused
+        kept = [(t, t.clone()) for t in (fu.q_flat, fu.m, fu.v, fu.step, fu.q_table, fu.loss, fu.grad)
+                if t is not None]
         with torch.cuda.stream(stream):
             rows = learner._idx[:learner.batch_size]
             lg = torch.cuda.CUDAGraph()
             with torch.cuda.graph(lg, stream=stream):
                 for _ in range(50):
-                    learner.fused.update(learner.replay, rows)
+                    fu.update(learner.replay, rows)
             lg.replay()
             learn_ms, _ = timed(lg.replay, stream, dev, world, local)
             learn_ms /= 50
-            learner.fused.mark_updated()
+            for t, c in kept:
+                t.copy_(c)
+            fu.mark_updated()
 
     if rank == 0:
         W = spec.words
@@ -942,6 +949,8 @@ def main():
                             "bound": "mfma", "achieved": ut, "peak": FP32_MATRIX_TFLOPS, "unit": "TFLOP/s",
                             "frac": ut / FP32_MATRIX_TFLOPS, "kernel": "pbn_bdq_learn (forward, backward, apply)",
                             "update_ms": learn_ms, "flops_per_update": uf,
+                            "update_timing_note": "50 updates replayed on the last frame's rows; the learner's "
+                                                  "weights, Adam state and tables restored afterwards",
                             "note": "update_policy's FLOPs in the reference's arithmetic (5B row-forwards: online "
                                     "over states and next states, target over next states, backward over B rows, "
                                     "bench.py update_flops) over the fused update's time, 50 replayed back to back"}

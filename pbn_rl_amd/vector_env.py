@@ -256,6 +256,17 @@ class VectorPBNEnv:
                 if not (dst.is_contiguous() and src.is_contiguous()) or dst.device != src.device or \
                         src.device.type != "cuda":
                     raise ValueError("copy: dst and src must be contiguous tensors on the env's GPU")
+                # the launch writes its outputs and the env's state, t and target while the copy
+                # reads src and writes dst: neither range may overlap them (the kernel cannot check)
+                own = [t for t in (self.state, self.target, self.t, *(v for key, v in out.items()
+                                                                      if key != "_n_steps"))
+                       if isinstance(t, torch.Tensor)]
+                for name, c in (("dst", dst), ("src", src)):
+                    lo, hi = c.data_ptr(), c.data_ptr() + c.numel() * c.element_size()
+                    for t in own:
+                        t_lo = t.data_ptr()
+                        if lo < t_lo + t.numel() * t.element_size() and t_lo < hi:
+                            raise ValueError(f"copy: {name} overlaps a buffer this launch writes")
                 _lib.check(L.pbn_rollout_copy(self.net.handle, self.seed, self.step_index, self.env_offset, n,
                                               n_steps, mode, self.state.data_ptr(), out["flipmask"].data_ptr(),
                                               self.target.data_ptr(), self.t.data_ptr(), ptr(out["obs"]),

@@ -239,3 +239,9 @@ def test_rollout_copy_entry_point(settle):
         envs[0].rollout(steps, copy=(dst[:32], src[:16]))
     with pytest.raises(ValueError):   # a strided view: its bytes are not one range
         envs[0].rollout(steps, copy=(dst[:64:2], src[:32]))
+    out = envs[0].rollout_buffers(steps, keep_obs=True)
+    flat = out["reward"].view(torch.uint8).reshape(-1)
+    with pytest.raises(ValueError, match="overlaps"):   # the copy may not touch the launch's own outputs
+        envs[0].rollout(steps, keep_obs=True, out=out, copy=(flat[:64], src[:64]))
+    with pytest.raises(ValueError, match="overlaps"):
+        envs[0].rollout(steps, copy=(dst[:64], envs[0].state.view(torch.uint8).reshape(-1)[:64]))

@@ -198,3 +198,24 @@ def test_gpu_bb33_one_update_law_fails_reference():
     ref, _ = reference_result()
     assert not np.array_equal(summary(res)[0], ref)
     env.close()
+
+
+def test_settle_unpacked_threshold_compare():
+    """A node whose last function quantises to weight 0 (weights 0.99 / 0.01 at prob_bits = 4): its
+    first threshold is 2^B = 16, which the packed 16-bit compares cannot hold, so the host leaves
+    settle_pk = 0 and pbn_rollout_settle's selection wave takes its unpacked compare
+    (settle_lt_word on the thresholds in global memory).  Rollouts and pbn_step's
+    one-step launches against the oracle."""
+    import json
+    import os
+    from pbn_rl_amd.attractors import find_attractors
+    from pbn_rl_amd.network import Network
+    d = json.load(open(os.path.join(os.path.dirname(__file__), "..", "pbn_rl_amd", "networks", "pbn7.json")))
+    lf = [[(e, w) for e, w in fl] for fl in d["logic_functions"]]
+    lf[0] = [(lf[0][0][0], 0.99), (lf[1][0][0], 0.01)]
+    net = Network.from_logic_functions(d["genes"], lf, name="pbn7_zero_last")
+    assert net.thresholds(4)[0][0] == 16     # == 2^B: not representable in the packed compares
+    spec = EnvSpec(net, find_attractors(net, prob_bits=4), prob_bits=4, perturbation=0.05, horizon=6, settle=6)
+    run_rollout_pair(spec, 2080, 8, 3)
+    run_rollout_pair(spec, 1024, 5, 1)
+    run_pair(spec, 2048, 4, mode=3, env_offset=1024)
