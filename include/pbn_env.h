@@ -491,13 +491,37 @@ int pbn_bdq_td_loss(const float* d_online, const float* d_target, const int64_t*
 int pbn_bdq_layout(int32_t n_nodes, int32_t n_branches, int64_t* offsets);
 int pbn_bdq_learn_workspace(int32_t n_nodes, int32_t n_branches, int64_t batch, int64_t* bytes);
 int pbn_bdq_pack(const pbn_net* net, int32_t n_branches, const float* d_params, float* d_Tq, void* stream);
+/*
+ * The learning frame's counters, advanced by the fused update's last launch (ABI 9): when
+ * pbn_bdq_learn's `advance` is not null, learn_apply runs one more block that does what
+ * pbn_replay_advance does for the frame just stored (position and fill level after n_store rows,
+ * the env step index, epsilon's decay) and then draws the NEXT frame's n_idx rows into d_idx, over
+ * the fill level that frame's store will leave (min(size + n_store, capacity)), with *d_counter,
+ * which then advances.  A captured BDQ frame (pbn_rl_amd/replay.py BDQLearner) so needs no
+ * launch of its own for the counters; its first rows are drawn before the first replay.  The
+ * update itself reads d_idx before this block writes it (an earlier launch of the same call).
+ */
+typedef struct pbn_frame_advance {
+  int64_t n_store, capacity;
+  int64_t* d_pos;
+  int64_t* d_size;
+  int64_t* d_step;      /* nullable */
+  double* d_eps64;      /* nullable */
+  float* d_eps32;       /* nullable */
+  double eps_final, eps_step;
+  int64_t n_idx;
+  uint64_t seed;
+  int64_t* d_counter;
+  int64_t* d_idx;
+} pbn_frame_advance;
+
 int pbn_bdq_learn(const pbn_net* net, int64_t batch, const int64_t* d_idx, int64_t capacity, const uint32_t* d_state,
                   const uint32_t* d_next_state, const uint8_t* d_target, const int32_t* d_action, int32_t n_branches,
                   const float* d_reward, const uint8_t* d_done, float* d_params, float* d_Tq,
                   const float* d_target_params, const float* d_target_Tq, float* d_adam_m, float* d_adam_v,
                   float* d_adam_step, float lr, float beta1, float beta2, float eps, float gamma, float grad_clamp,
                   float slope, void* d_workspace, int64_t workspace_bytes, float* d_loss, float* d_grad,
-                  void* stream);
+                  const pbn_frame_advance* advance, void* stream);
 
 /*
  * pbn_copy_async (ABI 7): d_dst[0 .. bytes) <- d_src[0 .. bytes), device to device on `stream`:

@@ -40,6 +40,16 @@ class PbnError(RuntimeError):
     pass
 
 
+class FrameAdvance(ctypes.Structure):
+    """pbn_frame_advance (include/pbn_env.h, ABI 9): the counters a captured learning frame's fused
+    update advances in its last launch, and the next frame's replay rows it draws."""
+    _fields_ = [("n_store", ctypes.c_int64), ("capacity", ctypes.c_int64), ("d_pos", ctypes.c_void_p),
+                ("d_size", ctypes.c_void_p), ("d_step", ctypes.c_void_p), ("d_eps64", ctypes.c_void_p),
+                ("d_eps32", ctypes.c_void_p), ("eps_final", ctypes.c_double), ("eps_step", ctypes.c_double),
+                ("n_idx", ctypes.c_int64), ("seed", ctypes.c_uint64), ("d_counter", ctypes.c_void_p),
+                ("d_idx", ctypes.c_void_p)]
+
+
 def build(verbose: bool = False, out: str = LIB_PATH, defines=()) -> str:
     """Compile csrc/*.hip for gfx950 into pbn_rl_amd/libpbn_env.so (in-tree): one object per
     source, compiled in parallel, then one link.  ``defines`` builds a diagnostic variant (e.g.
@@ -144,7 +154,7 @@ def load() -> ctypes.CDLL:
         L.pbn_bdq_pack.argtypes = [vp, i32, vp, vp, vp]
         L.pbn_bdq_pack.restype = ctypes.c_int
         L.pbn_bdq_learn.argtypes = ([vp, i64, vp, i64, vp, vp, vp, vp, i32, vp, vp] + [vp] * 7 + [f32] * 7 +
-                                    [vp, i64, vp, vp, vp])
+                                    [vp, i64, vp, vp, vp, vp])
         L.pbn_bdq_learn.restype = ctypes.c_int
     L.pbn_copy_async.argtypes = [vp, vp, i64, vp]
     L.pbn_copy_async.restype = ctypes.c_int

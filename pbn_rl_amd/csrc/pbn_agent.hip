@@ -24,6 +24,7 @@
 #include "../../include/pbn_env.h"
 #include "net_view.h"
 #include "philox.h"
+#include "replay_draw.h"
 
 namespace {
 
@@ -404,34 +405,8 @@ __global__ void __launch_bounds__(256) replay_advance_kernel(int64_t n_store, in
                                                              double eps_final, double eps_step, int64_t n_idx,
                                                              uint64_t seed, int64_t* __restrict__ counter,
                                                              int64_t* __restrict__ idx) {
-  __shared__ int64_t s_size;
-  if (threadIdx.x == 0) {
-    int64_t sz = *size;
-    if (n_store > 0) {
-      *pos = (*pos + n_store) % cap;
-      sz = sz + n_store < cap ? sz + n_store : cap;
-      *size = sz;
-    }
-    if (step) *step += 1;
-    if (eps64) {
-      const double e = *eps64 - eps_step;
-      const double v = isnan(e) ? e : (e > eps_final ? e : eps_final);   // torch.maximum(final, e)
-      *eps64 = v;
-      if (eps32) *eps32 = (float)v;
-    }
-    s_size = sz;
-  }
-  __syncthreads();
-  if (n_idx > 0) {
-    const uint64_t sz = (uint64_t)(s_size > 0 ? s_size : 1);
-    const uint64_t c = (uint64_t)*counter;
-    for (int64_t b = threadIdx.x; b < n_idx; b += blockDim.x) {
-      const pbn::Word4 r = pbn::draw(seed, (uint64_t)b, c, pbn::kStreamReplay, 0);
-      idx[b] = (int64_t)__umul64hi(((uint64_t)r.x << 32) | r.y, sz);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) *counter = (int64_t)(c + 1);
-  }
+  pbn::frame_advance_block(n_store, cap, pos, size, step, eps64, eps32, eps_final, eps_step, n_idx, seed, counter,
+                           idx, 0);
 }
 
 // ---- a replay batch in one pass (pbn_replay_batch): rows idx of the ring unpacked into the

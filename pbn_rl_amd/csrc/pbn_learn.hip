@@ -35,11 +35,13 @@
 
 #include <math.h>
 #include <stdint.h>
+#include <string.h>
 
 #include <algorithm>
 
 #include "../../include/pbn_env.h"
 #include "net_view.h"
+#include "replay_draw.h"
 
 namespace {
 
@@ -111,6 +113,10 @@ struct LearnArgs {
   float* loss;
   float* grad;    // optional: the clamped gradient, parameter layout
   unsigned long long* stamps;   // diagnostic builds (PBN_STAMPS): [kernel][block][wave][32] s_memtime
+  // the frame's counters and the next frame's rows (pbn_frame_advance): learn_apply's extra last
+  // block, when adv_on
+  int adv_on;
+  pbn_frame_advance adv;
 };
 
 // Diagnostic phase clocks (tools/learn_stamps.py): lane 0 of every wave of the first 1,024 blocks
@@ -725,6 +731,12 @@ struct Dense {
 template <int NT>
 __global__ void __launch_bounds__(64 * kApplyWaves) learn_apply_kernel(LearnArgs a) {
   __shared__ float wsc[kApplyWaves][16][kMaxNT * 16 + 1];   // a bilinear tile's new weights, per wave
+  if (a.adv_on && blockIdx.x == gridDim.x - 1) {   // the frame's counters and the next frame's rows
+    const pbn_frame_advance& f = a.adv;             // (this launch reads neither; the earlier ones
+    pbn::frame_advance_block(f.n_store, f.capacity, f.d_pos, f.d_size, f.d_step, f.d_eps64, f.d_eps32,   // of
+                             f.eps_final, f.eps_step, f.n_idx, f.seed, f.d_counter, f.d_idx, f.n_store);   // the
+    return;                                                                                              // call
+  }                                                                                                      // did)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, rr = lane & 15;
   const int B = a.B;
@@ -1021,7 +1033,7 @@ int pbn_bdq_learn(const pbn_net* net, int64_t batch, const int64_t* d_idx, int64
                   const float* d_target_params, const float* d_target_Tq, float* d_adam_m, float* d_adam_v,
                   float* d_adam_step, float lr, float beta1, float beta2, float eps, float gamma, float grad_clamp,
                   float slope, void* d_workspace, int64_t workspace_bytes, float* d_loss, float* d_grad,
-                  void* stream) {
+                  const pbn_frame_advance* advance, void* stream) {
   pbn::NetView nv;
   int rc = pbn::net_view(net, &nv);
   if (rc) return rc;
@@ -1096,6 +1108,18 @@ int pbn_bdq_learn(const pbn_net* net, int64_t batch, const int64_t* d_idx, int64
 #ifdef PBN_STAMPS
   a.stamps = g_lstamps;
 #endif
+  a.adv_on = 0;
+  memset(&a.adv, 0, sizeof a.adv);
+  if (advance) {
+    const pbn_frame_advance& f = *advance;
+    if (f.n_store < 0 || f.capacity < 1 || f.n_idx < 0 || !f.d_size || (f.n_store > 0 && !f.d_pos) ||
+        (f.n_idx > 0 && (!f.d_counter || !f.d_idx)))
+      return pbn::set_error(PBN_EINVAL, "pbn_frame_advance: n_store, n_idx >= 0, capacity >= 1, buffers");
+    if (f.d_idx == d_idx && f.n_idx < batch)
+      return pbn::set_error(PBN_EINVAL, "pbn_frame_advance: d_idx draws fewer rows than the batch");
+    a.adv_on = 1;
+    a.adv = f;
+  }
   const hipStream_t s = (hipStream_t)stream;
   const int tiles = (int)(batch / kRows);
   const size_t lds_f = ((size_t)(kD0 + kD1 + kD2 + kD3 + kDH * H) * kRows + 4 * kRows + 2 * kRows) * sizeof(float) +
@@ -1113,7 +1137,7 @@ int pbn_bdq_learn(const pbn_net* net, int64_t batch, const int64_t* d_idx, int64
   if (hipGetLastError() != hipSuccess) return pbn::set_error(PBN_EDEVICE, "learn_bwd_kernel launch failed");
   const int ntasks = 16 * N + (kD1 / 16) * (kD0 / 16) + (kD2 / 16) * (kD1 / 16) + (kD3 / 16) * (kD2 / 16) +
                      (H * kDH / 16) * (kD3 / 16) + H * (a.Apad / 16) * (kDH / 16);
-  const dim3 grid((ntasks + kApplyWaves - 1) / kApplyWaves), blk(64 * kApplyWaves);
+  const dim3 grid((ntasks + kApplyWaves - 1) / kApplyWaves + (a.adv_on ? 1 : 0)), blk(64 * kApplyWaves);
   switch ((N + 15) / 16) {
     case 1: hipLaunchKernelGGL(learn_apply_kernel<1>, grid, blk, 0, s, a); break;
     case 2: hipLaunchKernelGGL(learn_apply_kernel<2>, grid, blk, 0, s, a); break;

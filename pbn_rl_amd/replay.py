@@ -393,9 +393,11 @@ class FusedBDQUpdate:
         """BatchedBDQ's weight-derived operands as views of the flat buffer (no assembly kernels)."""
         return self._acting
 
-    def update(self, replay: "DeviceReplay", idx: torch.Tensor) -> torch.Tensor:
+    def update(self, replay: "DeviceReplay", idx: torch.Tensor, advance=None) -> torch.Tensor:
         """One update on ring rows ``idx`` (int64, ``batch_size`` of them); returns the loss buffer
-        (overwritten by the next update)."""
+        (overwritten by the next update).  ``advance``: an ``_lib.FrameAdvance`` whose counters
+        the update's last launch advances (and the next frame's rows it draws; BDQLearner's
+        captured frame)."""
         if idx.shape != (self.B,) or idx.dtype != torch.int64:
             raise ValueError(f"idx must be {self.B} int64 ring indices")
         self.sync()
@@ -410,6 +412,7 @@ class FusedBDQUpdate:
                                        self.v.data_ptr(), self.step.data_ptr(), self.lr, b1, b2, self.eps, self.gamma,
                                        self.grad_clamp, self.slope, self.work.data_ptr(), self.work.numel() * 4,
                                        self.loss.data_ptr(), self.grad.data_ptr() if self.grad is not None else None,
+                                       ctypes.byref(advance) if advance is not None else None,
                                        self._stream()), "pbn_bdq_learn")
         if not torch.cuda.is_current_stream_capturing():
             self.mark_updated()   # (a captured update is marked by each replay: BDQLearner._replay_frame)
@@ -595,6 +598,18 @@ class BDQLearner:
         self._size_t = torch.full((1,), self.replay.size, dtype=torch.int64, device=dev)
         self._done_buf = torch.zeros(env.n_alloc, dtype=torch.uint8, device=dev)
         self._tgt_prev = env.target.clone()   # the pre-step targets, carried by the ring store
+        self._adv = None
+        if self.fused is not None:
+            # the fused update's last launch advances the frame's counters and draws the next
+            # frame's rows (pbn_frame_advance): the first replayed frame's rows are drawn now, over
+            # the fill level its store will leave (what pbn_replay_advance drew inside the frame)
+            self._adv = _lib.FrameAdvance(
+                env.n_alloc, self.replay.capacity, self._pos_t.data_ptr(), self._size_t.data_ptr(),
+                self._step_t.data_ptr(), self._eps64.data_ptr(), self._eps32.data_ptr(), float(self.epsilon_final),
+                float(self.epsilon_step), self._idx.numel(), self.seed, self._draw_t.data_ptr(), self._idx.data_ptr())
+            first = torch.full((1,), min(self.replay.size + env.n_alloc, self.replay.capacity), dtype=torch.int64,
+                               device=dev)
+            self.replay.sample_rows(self._idx, self.seed, self._draw_t, first)
         g = torch.cuda.CUDAGraph()
         g.register_generator_state(self.gen)
         if self.opt is not None:
@@ -619,19 +634,21 @@ class BDQLearner:
                              target_copy=(self._tgt_prev, env.target))
         fused = self.fused is not None
         L = _lib.load()
-        with torch.cuda.device(env.device):
-            _lib.check(L.pbn_replay_advance(env.n_alloc, self.replay.capacity, self._pos_t.data_ptr(),
-                                            self._size_t.data_ptr(), self._step_t.data_ptr(), self._eps64.data_ptr(),
-                                            self._eps32.data_ptr(), float(self.epsilon_final), float(self.epsilon_step),
-                                            self._idx.numel() if fused else 0, self.seed,
-                                            self._draw_t.data_ptr() if fused else None,
-                                            self._idx.data_ptr() if fused else None,
-                                            torch.cuda.current_stream(env.device).cuda_stream), "pbn_replay_advance")
+        if not fused:   # (fused: the update's last launch advances them, pbn_frame_advance)
+            with torch.cuda.device(env.device):
+                _lib.check(L.pbn_replay_advance(env.n_alloc, self.replay.capacity, self._pos_t.data_ptr(),
+                                                self._size_t.data_ptr(), self._step_t.data_ptr(),
+                                                self._eps64.data_ptr(), self._eps32.data_ptr(),
+                                                float(self.epsilon_final), float(self.epsilon_step), 0, self.seed,
+                                                None, None, torch.cuda.current_stream(env.device).cuda_stream),
+                           "pbn_replay_advance")
         loss = None
         B = self.batch_size
-        for u in range(self.updates_per_frame):
+        U = self.updates_per_frame
+        for u in range(U):
             if fused:
-                loss = self.fused.update(self.replay, self._idx[u * B:(u + 1) * B])
+                loss = self.fused.update(self.replay, self._idx[u * B:(u + 1) * B],
+                                         advance=self._adv if u == U - 1 else None)
             else:
                 loss = self._update(self.replay.sample_indices(B, self.gen, size_t=self._size_t))
         return env.reward[: env.num_envs], self._done_buf[: env.num_envs].view(torch.bool), loss
