@@ -1,0 +1,5 @@
+cd "$GRAFT_REPO_ROOT" || exit 1
+out=gpurun_out/r06_e; mkdir -p $out; export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_gpu_settle.py tests/test_gpu_configs.py tests/test_gpu_graph.py tests/test_gpu_rccl.py -m gpu -x -q --timeout 180 --timeout-method thread > $out/tests.log 2>&1 || { tail -30 $out/tests.log; exit 4; }
+tail -2 $out/tests.log
+bash tools/gpu_session.sh r06_e absettle
