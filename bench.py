@@ -894,7 +894,7 @@ def main():
         # learner's parameters, Adam state, tables and loss snapshotted before and restored after,
         # so that the learner leaves the bench as its last frame left it
         fu = learner.fused
-        kept = [(t, t.clone()) for t in (fu.q_flat, fu.m, fu.v, fu.step, fu.q_table, fu.loss, fu.grad)
+        kept = [(t, t.clone()) for t in (fu.q_flat, fu.m, fu.v, fu.step, fu.q_image, fu.loss, fu.grad)
                 if t is not None]
         with torch.cuda.stream(stream):
             rows = learner._idx[:learner.batch_size]

@@ -72,7 +72,7 @@
 extern "C" {
 #endif
 
-#define PBN_ABI_VERSION 9
+#define PBN_ABI_VERSION 10
 
 #define PBN_MAX_NODES 128
 #define PBN_MAX_ARITY 4
@@ -477,19 +477,25 @@ int pbn_bdq_td_loss(const float* d_online, const float* d_target, const int64_t*
  *   (K+1, N+1) -- head 0 is the value head, whose rows / biases past output 0 are zero padding;
  *   offsets[12] = the total.  Parameters, Adam's moments and d_grad share this layout.
  * pbn_bdq_learn_workspace: bytes of the update's workspace at batch B (a multiple of 16).
- * pbn_bdq_pack: d_Tq float [n_attr][N][256], the bilinear layer contracted with each attractor's
- *   first state, T[t][i][o] = sum_j x_t[j] W[o][i][j], stored [t][i][j][q] = T[t][i][16 q + j]
- *   (the table pbn_qnet_*_from_state read).  Needed once per parameter version not written by
- *   pbn_bdq_learn (initial weights, a loaded checkpoint, the target network after a soft update).
+ * pbn_bdq_image_floats (ABI 10): floats of a network's image, the d_Tq / d_target_Tq buffers.
+ * pbn_bdq_pack: the image of the weights d_params into d_Tq: first the bilinear layer contracted
+ *   with each attractor's first state, T[t][i][o] = sum_j x_t[j] W[o][i][j], stored
+ *   [t][i][j][q] = T[t][i][16 q + j] (the table pbn_qnet_*_from_state read, n_attr * N * 256
+ *   floats); then (ABI 10) the dense layers' weights as 16 x 16 tiles in the update kernels'
+ *   MFMA-fragment orders (pbn_learn.hip make_image).  Needed once per parameter version not
+ *   written by pbn_bdq_learn (initial weights, a loaded checkpoint, the target network after a
+ *   soft update).
  * pbn_bdq_learn: rows d_idx [B] of the replay ring (the layout of pbn_replay_store);
- *   d_params / d_Tq the online network (updated in place: Adam step, and the table of the new
- *   weights), d_target_params / d_target_Tq the target network (read); d_adam_m / d_adam_v the
+ *   d_params / d_Tq the online network and its image (updated in place: Adam step, and the image
+ *   of the new weights, equal to pbn_bdq_pack's bit for bit), d_target_params / d_target_Tq the
+ *   target network and its image (read; the update reads the dense weights from the images); d_adam_m / d_adam_v the
  *   moments, d_adam_step float [1] Adam's step count (incremented on the device); the loss to
  *   d_loss float [1]; when d_grad is not null, the clamped gradient there.  Same arithmetic as
  *   pbn_rl_amd/replay.py bdq_update + torch.optim.Adam in fp32, to summation order.
  */
 int pbn_bdq_layout(int32_t n_nodes, int32_t n_branches, int64_t* offsets);
 int pbn_bdq_learn_workspace(int32_t n_nodes, int32_t n_branches, int64_t batch, int64_t* bytes);
+int pbn_bdq_image_floats(const pbn_net* net, int32_t n_branches, int64_t* floats);
 int pbn_bdq_pack(const pbn_net* net, int32_t n_branches, const float* d_params, float* d_Tq, void* stream);
 /*
  * The learning frame's counters, advanced by the fused update's last launch (ABI 9): when

@@ -29,7 +29,7 @@ EXPORTS = ["pbn_net_create", "pbn_net_destroy", "pbn_net_words", "pbn_reset", "p
            "pbn_q_to_flipmask_dev",
            "pbn_heads_to_flipmask", "pbn_qnet_heads", "pbn_qnet_flipmask", "pbn_qnet_heads_from_state",
            "pbn_qnet_flipmask_from_state", "pbn_replay_store", "pbn_replay_advance", "pbn_replay_batch", "pbn_bdq_td_loss", "pbn_bdq_layout", "pbn_bdq_learn_workspace",
-           "pbn_bdq_pack", "pbn_bdq_learn", "pbn_copy_async", "pbn_rollout_copy", "pbn_host_buffer", "pbn_host_buffer_free", "pbn_stream_sync",
+           "pbn_bdq_pack", "pbn_bdq_image_floats", "pbn_bdq_learn", "pbn_copy_async", "pbn_rollout_copy", "pbn_host_buffer", "pbn_host_buffer_free", "pbn_stream_sync",
            "pbn_last_error", "pbn_abi_version"]
 SOURCES = ["pbn_env.hip", "pbn_settle.hip", "pbn_agent.hip", "pbn_qnet.hip", "pbn_learn.hip"]
 
@@ -153,6 +153,9 @@ def load() -> ctypes.CDLL:
         L.pbn_bdq_learn_workspace.restype = ctypes.c_int
         L.pbn_bdq_pack.argtypes = [vp, i32, vp, vp, vp]
         L.pbn_bdq_pack.restype = ctypes.c_int
+        if hasattr(L, "pbn_bdq_image_floats"):   # (ABI 10)
+            L.pbn_bdq_image_floats.argtypes = [vp, i32, vp]
+            L.pbn_bdq_image_floats.restype = ctypes.c_int
         L.pbn_bdq_learn.argtypes = ([vp, i64, vp, i64, vp, vp, vp, vp, i32, vp, vp] + [vp] * 7 + [f32] * 7 +
                                     [vp, i64, vp, vp, vp, vp])
         L.pbn_bdq_learn.restype = ctypes.c_int

@@ -70,6 +70,37 @@ void make_layout(int N, int H, int64_t* off) {
   off[TOTAL] = o;
 }
 
+// ---- the network image (pbn_bdq_pack; the online one rewritten by learn_apply): the bilinear
+// target table [n_attr][N][256] (the acting kernels' operand), then the dense layers' weights as
+// 16 x 16 tiles in MFMA-fragment order, so that a wave's fragment of a tile is one 1 KB contiguous
+// load (as 16-row x 64-byte fragment loads of the row-major weights they cost learn_fwd 3.7 of its
+// 22.8 us, profiles/r06_l_learn_fwd_probes.json).  Layer matrix M (rows R, columns C; the second
+// head layers stacked as H x Apad rows, zero past each head's A), tile (ot, kt) at float
+// (ot * C/16 + kt) * 256, twice:
+//   fwd: lane g*16 + r holds M[16 ot + r][16 kt + 4g + v], v = 0..3 (learn_fwd's A operand)
+//   bwd: lane g*16 + r holds M[16 ot + 4g + v][16 kt + r]            (learn_bwd's transposed one)
+enum Lay { LY2, LY3, LY4, LYH1, LYH2, NLAY };
+
+struct ImageLayout {
+  int64_t fwd[NLAY], bwd[NLAY], total;   // float offsets from the image's start
+  int rows[NLAY], cols[NLAY];
+};
+
+void make_image(int N, int H, int n_attr, ImageLayout* im) {
+  const int Apad = 16 * ((N + 1 + 15) / 16);
+  const int R[NLAY] = {kD1, kD2, kD3, H * kDH, H * Apad}, C[NLAY] = {kD0, kD1, kD2, kD3, kDH};
+  int64_t o = (int64_t)n_attr * N * 256;
+  for (int l = 0; l < NLAY; ++l) {
+    im->rows[l] = R[l];
+    im->cols[l] = C[l];
+    im->fwd[l] = o;
+    o += (int64_t)R[l] * C[l];
+    im->bwd[l] = o;
+    o += (int64_t)R[l] * C[l];
+  }
+  im->total = o;
+}
+
 struct LearnArgs {
   // the replay ring and the sampled rows
   const int64_t* idx;
@@ -86,9 +117,10 @@ struct LearnArgs {
   int n_attr, N, W, K, H, A, Apad;
   // parameters (online, updated in place; target, read), their target tables, Adam's state
   float* P;
-  float* Tq;
+  float* Tq;          // the online network's image (its table, then the weight tiles: make_image)
   const float* PT;
-  const float* TqT;
+  const float* TqT;   // the target network's
+  int64_t ifw[NLAY], ibw[NLAY];   // the weight tiles' offsets in the images
   float* m;
   float* v;
   float* step;
@@ -159,18 +191,16 @@ __device__ __forceinline__ int64_t row_index(const LearnArgs& a, int b) {
 // lane l supplies A[o0 + (l & 15)][k] = one float4 of weight row o0 + (l & 15); its accumulator
 // holds D[o0 + 4g + v][r], v = 0..3.
 // The weight fragments come in registers, loaded by wfrag before the layer's inputs are ready
-// (every layer's fragments are requested at kernel entry: one L2 round trip, not one per layer).
+// (every layer's fragments are requested at kernel entry: one L2 round trip, not one per layer):
+// output tile ot of a layer with K inputs, from its fwd tiles in the image (zero past n_ot tiles)
 template <int K>
-__device__ __forceinline__ void wfrag(float4 (&w)[K / 16], const float* __restrict__ W, int ldw, int o0, int o_valid,
-                                      int lane) {
-  const int g = lane >> 4, rr = lane & 15;
-  const int o = o0 + rr;
-  const bool ov = o < o_valid;
-  const float* wrow = W + (size_t)(ov ? o : 0) * ldw + 4 * g;
+__device__ __forceinline__ void wfrag(float4 (&w)[K / 16], const float* __restrict__ tiles, int ot, int n_ot, int lane) {
+  const bool ok = ot < n_ot;
+  const float4* t = reinterpret_cast<const float4*>(tiles) + (size_t)(ok ? ot : 0) * (K / 16) * 64 + lane;
 #pragma unroll
   for (int kb = 0; kb < K / 16; ++kb) {
-    w[kb] = *reinterpret_cast<const float4*>(wrow + kb * 16);
-    if (!ov) w[kb] = make_float4(0.f, 0.f, 0.f, 0.f);
+    w[kb] = t[kb * 64];
+    if (!ok) w[kb] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 
@@ -231,15 +261,12 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
   const int at16 = a.Apad / 16;
   float4 w2[kD0 / 16], w3[kD1 / 16], w4[kD2 / 16], wh1[2][kD3 / 16], wh2[kDH / 16];
   auto fetch_weights = [&]() {
-    wfrag<kD0>(w2, P + a.off[L2_W], kD0, 16 * wave, kD1, lane);
-    if (wave < kD2 / 16) wfrag<kD1>(w3, P + a.off[L3_W], kD1, 16 * wave, kD2, lane);   // (only these waves
-    if (wave < kD3 / 16) wfrag<kD2>(w4, P + a.off[L4_W], kD2, 16 * wave, kD3, lane);   // compute the layers)
+    wfrag<kD0>(w2, Tq + a.ifw[LY2], wave, kD1 / 16, lane);
+    if (wave < kD2 / 16) wfrag<kD1>(w3, Tq + a.ifw[LY3], wave, kD2 / 16, lane);   // (only these waves
+    if (wave < kD3 / 16) wfrag<kD2>(w4, Tq + a.ifw[LY4], wave, kD3 / 16, lane);   // compute the layers)
 #pragma unroll
-    for (int u = 0; u < 2; ++u) wfrag<kD3>(wh1[u], P + a.off[H1_W], kD3, 16 * (wave + kWaves * u), a.H * kDH, lane);
-    {
-      const int tt = wave < a.H * at16 ? wave : 0, h = tt / at16;
-      wfrag<kDH>(wh2, P + a.off[H2_W] + (size_t)h * a.A * kDH, kDH, 16 * (tt - h * at16), a.A, lane);
-    }
+    for (int u = 0; u < 2; ++u) wfrag<kD3>(wh1[u], Tq + a.ifw[LYH1], wave + kWaves * u, a.H * kDH / 16, lane);
+    wfrag<kDH>(wh2, Tq + a.ifw[LYH2], wave < a.H * at16 ? wave : 0, a.H * at16, lane);
   };
   if (wave != 0) fetch_weights();   // (wave 0 loads the rows first: the load counter is in order)
   if (tid < kRows) {   // the rows' targets, state words and the list of their set bits
@@ -346,7 +373,7 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
     }
     for (int tt = wave + 2 * kWaves; tt < n1; tt += kWaves) {
       float4 wl[kD3 / 16];
-      wfrag<kD3>(wl, P + a.off[H1_W], kD3, 16 * tt, a.H * kDH, lane);
+      wfrag<kD3>(wl, Tq + a.ifw[LYH1], tt, n1, lane);
       const f32x4 acc = fwd_tile<kD3>(wl, X4, lane);
       fwd_store(acc, P + a.off[H1_B], 16 * tt, a.slope, XH, set == 0 ? a.hh : nullptr, B, b0, lane);
     }
@@ -367,9 +394,8 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
   };
   if (wave < a.H * at16) head_out(wh2, wave);
   for (int tt = wave + kWaves; tt < a.H * at16; tt += kWaves) {
-    const int h = tt / at16;
     float4 wl[kDH / 16];
-    wfrag<kDH>(wl, P + a.off[H2_W] + (size_t)h * a.A * kDH, kDH, 16 * (tt - h * at16), a.A, lane);
+    wfrag<kDH>(wl, Tq + a.ifw[LYH2], tt, a.H * at16, lane);
     head_out(wl, tt);
   }
   PBN_LSTAMP(0, 9);
@@ -405,18 +431,20 @@ __device__ __forceinline__ void bwd_store(f32x4 acc, f32x4 yv, int kk0, float sl
   if (Ys) *reinterpret_cast<float4*>(Ys + ((kk0 >> 4) * 16 + rr) * 16 + 4 * g) = d;
 }
 
-// a layer's weight fragments for bwd_mma, NOB output blocks from ob0 (0 past n_ob or o_valid)
+// a layer's weight fragments for bwd_mma: input tile kt of a layer with KT input tiles, NOB
+// output blocks from ob0, from its bwd tiles in the image (0 past n_ob)
 template <int NOB>
-__device__ __forceinline__ void bwd_frag(float (&w)[NOB][4], const float* __restrict__ W, int ldw, int k0, int ob0,
-                                         int n_ob, int o_valid, int lane) {
-  const int g = lane >> 4, rr = lane & 15;
+__device__ __forceinline__ void bwd_frag(float (&w)[NOB][4], const float* __restrict__ tiles, int KT, int kt, int ob0,
+                                         int n_ob, int lane) {
 #pragma unroll
-  for (int u = 0; u < NOB; ++u)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int o = 16 * (ob0 + u) + 4 * g + v;
-      w[u][v] = (ob0 + u < n_ob && o < o_valid) ? W[(size_t)o * ldw + k0 + rr] : 0.f;
-    }
+  for (int u = 0; u < NOB; ++u) {
+    const bool ok = ob0 + u < n_ob;
+    const float4 x = reinterpret_cast<const float4*>(tiles)[((size_t)(ok ? ob0 + u : 0) * KT + kt) * 64 + lane];
+    w[u][0] = ok ? x.x : 0.f;
+    w[u][1] = ok ? x.y : 0.f;
+    w[u][2] = ok ? x.z : 0.f;
+    w[u][3] = ok ? x.w : 0.f;
+  }
 }
 
 template <int NOB>
@@ -458,7 +486,7 @@ __global__ void __launch_bounds__(kThreads) learn_bwd_kernel(LearnArgs a) {
   const int tile = blockIdx.x, b0 = tile * kRows;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, rr = lane & 15;
-  const float* P = a.P;
+  const float* Tw = a.Tq;   // the online network's weight tiles
   PBN_LSTAMP(1, 31);
   PBN_LSTAMP(1, 0);
   // weight fragments of the first four backward layers, requested before the TD pass so they
@@ -470,12 +498,12 @@ __global__ void __launch_bounds__(kThreads) learn_bwd_kernel(LearnArgs a) {
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int tt = min(wave + kWaves * u, H * (kDH / 16) - 1), h = tt >> 2;
-    bwd_frag<2>(wh2[u], P + a.off[H2_W] + (size_t)h * A * kDH, kDH, 16 * (tt & 3), 0, at16, A, lane);
+    bwd_frag<2>(wh2[u], Tw + a.ibw[LYH2] + (size_t)h * at16 * (kDH / 16) * 256, kDH / 16, tt & 3, 0, at16, lane);
   }
   const int q1 = wave >> 1;   // quarter of the first head layers' 4 H output blocks: [q H, q H + H)
-  bwd_frag<8>(wh1, P + a.off[H1_W], kD3, 16 * (wave & 1), q1 * H, q1 * H + H, H * kDH, lane);
-  bwd_frag<2>(w4, P + a.off[L4_W], kD2, 16 * (wave & 3), 0, kD3 / 16, kD3, lane);
-  bwd_frag<4>(w3, P + a.off[L3_W], kD1, 16 * wave, 0, kD2 / 16, kD2, lane);
+  bwd_frag<8>(wh1, Tw + a.ibw[LYH1], kD3 / 16, wave & 1, q1 * H, q1 * H + H, lane);
+  bwd_frag<2>(w4, Tw + a.ibw[LY4], kD2 / 16, wave & 3, 0, kD3 / 16, lane);
+  bwd_frag<4>(w3, Tw + a.ibw[LY3], kD1 / 16, wave, 0, kD2 / 16, lane);
   // and the stored activations of the same tiles (the LeakyReLU derivative)
   f32x4 yh2[2], y4 = act_frag(a.h4, 16 * (wave & 1), B, b0, lane), y3 = act_frag(a.h3, 16 * (wave & 3), B, b0, lane),
         y2 = act_frag(a.h2, 16 * wave, B, b0, lane), y1v[2];
@@ -607,7 +635,7 @@ __global__ void __launch_bounds__(kThreads) learn_bwd_kernel(LearnArgs a) {
   // the last layer's fragments (256 inputs: tiles wave, wave + 8), requested now for the end
   float w2[2][8][4];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) bwd_frag<8>(w2[u], P + a.off[L2_W], kD0, 16 * (wave + kWaves * u), 0, kD1 / 16, kD1, lane);
+  for (int u = 0; u < 2; ++u) bwd_frag<8>(w2[u], Tw + a.ibw[LY2], kD0 / 16, wave + kWaves * u, 0, kD1 / 16, lane);
   // second head layers: Apad -> 64 per head
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
@@ -618,7 +646,7 @@ __global__ void __launch_bounds__(kThreads) learn_bwd_kernel(LearnArgs a) {
       acc = bwd_mma<2>(acc, wh2[u], 0, at16, DH + h * Ap * kRows, lane);
       for (int ob0 = 2; ob0 < at16; ob0 += 2) {   // (A > 32)
         float wl[2][4];
-        bwd_frag<2>(wl, P + a.off[H2_W] + (size_t)h * A * kDH, kDH, c0, ob0, at16, A, lane);
+        bwd_frag<2>(wl, Tw + a.ibw[LYH2] + (size_t)h * at16 * (kDH / 16) * 256, kDH / 16, c0 / 16, ob0, at16, lane);
         acc = bwd_mma<2>(acc, wl, ob0, at16, DH + h * Ap * kRows, lane);
       }
       bwd_store(acc, yh2[u], h * kDH + c0, a.slope, DHH, a.dhh, B, b0, lane);
@@ -629,7 +657,7 @@ __global__ void __launch_bounds__(kThreads) learn_bwd_kernel(LearnArgs a) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int ob0 = 0; ob0 < at16; ob0 += 2) {
       float wl[2][4];
-      bwd_frag<2>(wl, P + a.off[H2_W] + (size_t)h * A * kDH, kDH, c0, ob0, at16, A, lane);
+      bwd_frag<2>(wl, Tw + a.ibw[LYH2] + (size_t)h * at16 * (kDH / 16) * 256, kDH / 16, c0 / 16, ob0, at16, lane);
       acc = bwd_mma<2>(acc, wl, ob0, at16, DH + h * Ap * kRows, lane);
     }
     bwd_store(acc, act_frag(a.hh, h * kDH + c0, B, b0, lane), h * kDH + c0, a.slope, DHH, a.dhh, B, b0, lane);
@@ -726,6 +754,7 @@ struct Dense {
   const float* X;
   int64_t w_off, b_off;
   int ldw, o_valid, k_tiles;
+  int lay, ot0;   // the layer's tiles in the image; its first output tile there (head h: h Apad/16)
 };
 
 template <int NT>
@@ -853,20 +882,20 @@ __global__ void __launch_bounds__(64 * kApplyWaves) learn_apply_kernel(LearnArgs
   const int n0 = (kD1 / 16) * (kD0 / 16), n1 = (kD2 / 16) * (kD1 / 16), n2 = (kD3 / 16) * (kD2 / 16),
             n3 = (H * kDH / 16) * (kD3 / 16), n4 = H * at16 * (kDH / 16);
   if (task < n0) {
-    L = Dense{a.dh2, a.y1, a.off[L2_W], a.off[L2_B], kD0, kD1, kD0 / 16};
+    L = Dense{a.dh2, a.y1, a.off[L2_W], a.off[L2_B], kD0, kD1, kD0 / 16, LY2, 0};
   } else if ((task -= n0) < n1) {
-    L = Dense{a.dh3, a.h2, a.off[L3_W], a.off[L3_B], kD1, kD2, kD1 / 16};
+    L = Dense{a.dh3, a.h2, a.off[L3_W], a.off[L3_B], kD1, kD2, kD1 / 16, LY3, 0};
   } else if ((task -= n1) < n2) {
-    L = Dense{a.dh4, a.h3, a.off[L4_W], a.off[L4_B], kD2, kD3, kD2 / 16};
+    L = Dense{a.dh4, a.h3, a.off[L4_W], a.off[L4_B], kD2, kD3, kD2 / 16, LY4, 0};
   } else if ((task -= n2) < n3) {
-    L = Dense{a.dhh, a.h4, a.off[H1_W], a.off[H1_B], kD3, H * kDH, kD3 / 16};
+    L = Dense{a.dhh, a.h4, a.off[H1_W], a.off[H1_B], kD3, H * kDH, kD3 / 16, LYH1, 0};
   } else if ((task -= n3) < n4) {
     const int per = at16 * (kDH / 16);
     const int h = task / per;
     task -= h * per;
     // head h's second layer: rows are its A outputs (the value head has one real output)
     L = Dense{a.dheads + (size_t)h * a.Apad * B, a.hh + (size_t)h * kDH * B, a.off[H2_W] + (int64_t)h * a.A * kDH,
-              a.off[H2_B] + (int64_t)h * a.A, kDH, h == 0 ? 1 : a.A, kDH / 16};
+              a.off[H2_B] + (int64_t)h * a.A, kDH, h == 0 ? 1 : a.A, kDH / 16, LYH2, h * at16};
   } else {
     return;
   }
@@ -904,10 +933,24 @@ __global__ void __launch_bounds__(64 * kApplyWaves) learn_apply_kernel(LearnArgs
     }
   }
   PBN_LSTAMP(2, 4);
+  float nw[4];
 #pragma unroll
   for (int v = 0; v < 4; ++v) {
     const int o = o0 + 4 * g + v;
-    if (o < L.o_valid) adam_apply(a, L.w_off + (int64_t)o * L.ldw + k0 + rr, pre[v], acc[v], bc1, bc2s);
+    nw[v] = o < L.o_valid ? adam_apply(a, L.w_off + (int64_t)o * L.ldw + k0 + rr, pre[v], acc[v], bc1, bc2s) : 0.f;
+  }
+  {   // the tile's new weights into the online image (the learn_fwd / learn_bwd operands of the
+      // next update and pbn_bdq_pack's values; rows past o_valid: the flat buffer's zero padding)
+    const size_t tix = ((size_t)(L.ot0 + ot) * L.k_tiles + kt) * 64 + lane;
+    reinterpret_cast<float4*>(a.Tq + a.ibw[L.lay])[tix] = make_float4(nw[0], nw[1], nw[2], nw[3]);
+    float* sc = &wsc[wave][0][0];   // the fwd order is the tile transposed: through this wave's LDS
+#pragma unroll
+    for (int v = 0; v < 4; ++v) sc[(4 * g + v) * 17 + rr] = nw[v];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    reinterpret_cast<float4*>(a.Tq + a.ifw[L.lay])[tix] =
+        make_float4(sc[rr * 17 + 4 * g], sc[rr * 17 + 4 * g + 1], sc[rr * 17 + 4 * g + 2], sc[rr * 17 + 4 * g + 3]);
   }
   if (kt == 0) {
     bsum += __shfl_xor(bsum, 16);
@@ -930,6 +973,46 @@ __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ P, 
     s += on ? wrow[j] : 0.f;
   }
   Tq[((size_t)t * N + i) * 256 + (o & 15) * 16 + (o >> 4)] = s;
+}
+
+// the weight tiles of one network's image from its flat parameters (make_image's layout): thread =
+// one lane's float4 of one tile of one order
+__global__ void __launch_bounds__(256) pack_tiles_kernel(const float* __restrict__ P, LearnArgs a, int64_t n4) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n4) return;
+  // (layer, order, tile, lane) from the flat float4 index over the tiles region
+  int64_t r = e;
+  int l = 0, bwd = 0;
+  int64_t per = 0;
+  for (l = 0; l < NLAY; ++l) {
+    const int R = l == LY2 ? kD1 : l == LY3 ? kD2 : l == LY4 ? kD3 : l == LYH1 ? a.H * kDH : a.H * a.Apad;
+    const int C = l == LY2 ? kD0 : l == LY3 ? kD1 : l == LY4 ? kD2 : l == LYH1 ? kD3 : kDH;
+    per = (int64_t)R * C / 4;   // float4s of one order of this layer
+    if (r < 2 * per) break;
+    r -= 2 * per;
+  }
+  bwd = r >= per;
+  if (bwd) r -= per;
+  const int C = l == LY2 ? kD0 : l == LY3 ? kD1 : l == LY4 ? kD2 : l == LYH1 ? kD3 : kDH;
+  const int64_t tile = r >> 6;
+  const int lane = (int)(r & 63), g = lane >> 4, rr = lane & 15;
+  const int ot = (int)(tile / (C / 16)), kt = (int)(tile - (int64_t)ot * (C / 16));
+  float x[4];
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int row = bwd ? 16 * ot + 4 * g + v : 16 * ot + rr;
+    const int col = bwd ? 16 * kt + rr : 16 * kt + 4 * g + v;
+    float val;
+    if (l == LYH2) {
+      const int h = row / a.Apad, o = row - h * a.Apad;
+      val = o < a.A ? P[a.off[H2_W] + ((int64_t)h * a.A + o) * kDH + col] : 0.f;
+    } else {
+      const int64_t w_off = l == LY2 ? a.off[L2_W] : l == LY3 ? a.off[L3_W] : l == LY4 ? a.off[L4_W] : a.off[H1_W];
+      val = P[w_off + (int64_t)row * C + col];
+    }
+    x[v] = val;
+  }
+  reinterpret_cast<float4*>(a.Tq + (bwd ? a.ibw[l] : a.ifw[l]))[tile * 64 + lane] = make_float4(x[0], x[1], x[2], x[3]);
 }
 
 struct Work {
@@ -1011,19 +1094,50 @@ int pbn_bdq_learn_workspace(int32_t n_nodes, int32_t n_branches, int64_t batch, 
   return PBN_OK;
 }
 
+int pbn_bdq_image_floats(const pbn_net* net, int32_t n_branches, int64_t* floats) {
+  pbn::NetView v;
+  int rc = pbn::net_view(net, &v);
+  if (rc) return rc;
+  if ((rc = check_shape(v.n_nodes, n_branches))) return rc;
+  if (!floats) return pbn::set_error(PBN_EINVAL, "null floats");
+  ImageLayout im;
+  make_image(v.n_nodes, n_branches + 1, v.n_attr, &im);
+  *floats = im.total;
+  return PBN_OK;
+}
+
 int pbn_bdq_pack(const pbn_net* net, int32_t n_branches, const float* d_params, float* d_Tq, void* stream) {
   pbn::NetView v;
   int rc = pbn::net_view(net, &v);
   if (rc) return rc;
   if ((rc = pbn::check_device(net))) return rc;
   if ((rc = check_shape(v.n_nodes, n_branches))) return rc;
-  if (v.n_attr == 0) return PBN_OK;
   if (!d_params || !d_Tq) return pbn::set_error(PBN_EINVAL, "null buffer");
-  int64_t off[TOTAL + 1];
-  make_layout(v.n_nodes, n_branches + 1, off);
-  hipLaunchKernelGGL(pack_kernel, dim3(v.n_attr * v.n_nodes), dim3(256), 0, (hipStream_t)stream, d_params, off[BIL_W],
-                     v.n_nodes, v.W, v.att_first, d_Tq);
-  if (hipGetLastError() != hipSuccess) return pbn::set_error(PBN_EDEVICE, "pack_kernel launch failed");
+  if (((uintptr_t)d_params | (uintptr_t)d_Tq) & 15u) return pbn::set_error(PBN_EINVAL, "buffers: 16-byte aligned");
+  const int N = v.n_nodes, H = n_branches + 1;
+  LearnArgs a;
+  memset(&a, 0, sizeof a);
+  a.N = N;
+  a.H = H;
+  a.A = N + 1;
+  a.Apad = 16 * ((N + 16) / 16);
+  make_layout(N, H, a.off);
+  ImageLayout im;
+  make_image(N, H, v.n_attr, &im);
+  for (int l = 0; l < NLAY; ++l) {
+    a.ifw[l] = im.fwd[l];
+    a.ibw[l] = im.bwd[l];
+  }
+  a.Tq = d_Tq;
+  const hipStream_t s = (hipStream_t)stream;
+  if (v.n_attr > 0) {
+    hipLaunchKernelGGL(pack_kernel, dim3(v.n_attr * N), dim3(256), 0, s, d_params, a.off[BIL_W], N, v.W, v.att_first,
+                       d_Tq);
+    if (hipGetLastError() != hipSuccess) return pbn::set_error(PBN_EDEVICE, "pack_kernel launch failed");
+  }
+  const int64_t n4 = (im.total - im.fwd[0]) / 4;
+  hipLaunchKernelGGL(pack_tiles_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, d_params, a, n4);
+  if (hipGetLastError() != hipSuccess) return pbn::set_error(PBN_EDEVICE, "pack_tiles_kernel launch failed");
   return PBN_OK;
 }
 
@@ -1047,7 +1161,7 @@ int pbn_bdq_learn(const pbn_net* net, int64_t batch, const int64_t* d_idx, int64
   if (!d_idx || !d_state || !d_next_state || !d_target || !d_action || !d_reward || !d_done || !d_params ||
       !d_target_params || !d_adam_m || !d_adam_v || !d_adam_step || !d_workspace || !d_loss)
     return pbn::set_error(PBN_EINVAL, "null buffer");
-  if (nv.n_attr > 0 && (!d_Tq || !d_target_Tq)) return pbn::set_error(PBN_EINVAL, "null target table");
+  if (!d_Tq || !d_target_Tq) return pbn::set_error(PBN_EINVAL, "null network image");
   for (const void* p : {(const void*)d_params, (const void*)d_target_params, (const void*)d_adam_m,
                         (const void*)d_adam_v, (const void*)d_workspace, (const void*)d_Tq, (const void*)d_target_Tq})
     if ((uintptr_t)p & 15u) return pbn::set_error(PBN_EINVAL, "parameter, table and workspace buffers: 16-byte aligned");
@@ -1078,6 +1192,12 @@ int pbn_bdq_learn(const pbn_net* net, int64_t batch, const int64_t* d_idx, int64
   a.v = d_adam_v;
   a.step = d_adam_step;
   make_layout(N, H, a.off);
+  ImageLayout im;
+  make_image(N, H, nv.n_attr, &im);
+  for (int l = 0; l < NLAY; ++l) {
+    a.ifw[l] = im.fwd[l];
+    a.ibw[l] = im.bwd[l];
+  }
   a.lr = lr;
   a.b1 = beta1;
   a.b2 = beta2;

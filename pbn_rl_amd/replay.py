@@ -281,10 +281,12 @@ class FusedBDQUpdate:
 
     The networks' parameters move into one flat fp32 buffer each (``pbn_bdq_layout``); their
     nn.Parameters become views of it, so ``state_dict``, the PyTorch forward and the acting kernel
-    see the same weights.  The online network's bilinear target table (``Tq``, the acting kernel's
-    operand) is rewritten by every update; ``pack()`` recomputes the tables after weights change
-    any other way (a loaded checkpoint), ``soft_update()`` moves the target network halfway
-    (bdq_model/__init__.py:137-139) and repacks its table.  Adam (torch.optim.Adam's arithmetic,
+    see the same weights.  Each network also has an image (``q_image`` / ``t_image``, pbn_bdq_pack):
+    its bilinear target table (``q_table``, the acting kernel's operand), then its dense weights
+    as 16 x 16 tiles in the update kernels' MFMA-fragment orders.  The online image is rewritten by
+    every update; ``pack()`` recomputes the images after weights change any other way (a loaded
+    checkpoint), ``soft_update()`` moves the target network halfway (bdq_model/__init__.py:137-139)
+    and repacks its image.  Adam (torch.optim.Adam's arithmetic,
     betas (0.9, 0.999), eps 1e-8) keeps its moments in buffers of the same layout and its step
     count on the device (graph-capturable)."""
 
@@ -314,9 +316,16 @@ class FusedBDQUpdate:
         self.v = torch.zeros_like(self.q_flat)
         self.step = torch.zeros(1, dtype=torch.float32, device=dev)
         n_attr = len(spec.attractors)
-        self.q_table = torch.zeros(n_attr, N, 16, 16, dtype=torch.float32, device=dev)
-        self.t_table = torch.zeros_like(self.q_table)
         L = _lib.load()
+        # each network's image (pbn_bdq_pack): the bilinear target table, which the acting kernel
+        # reads (q_table, a view), then the dense weights in the update kernels' fragment orders
+        nimg = ctypes.c_int64()
+        _lib.check(L.pbn_bdq_image_floats(net.handle, self.K, ctypes.byref(nimg)), "pbn_bdq_image_floats")
+        self.q_image = torch.zeros(nimg.value, dtype=torch.float32, device=dev)
+        self.t_image = torch.zeros_like(self.q_image)
+        nt = n_attr * N * 256
+        self.q_table = self.q_image[:nt].view(n_attr, N, 16, 16)
+        self.t_table = self.t_image[:nt].view(n_attr, N, 16, 16)
         nbytes = ctypes.c_int64()
         _lib.check(L.pbn_bdq_learn_workspace(N, self.K, self.B, ctypes.byref(nbytes)), "pbn_bdq_learn_workspace")
         self.work = torch.empty((nbytes.value + 3) // 4, dtype=torch.float32, device=dev)
@@ -356,12 +365,13 @@ class FusedBDQUpdate:
             torch.autograd.graph.increment_version(p)
 
     def pack(self, which: str = "both") -> None:
-        """Recompute the bilinear target tables (pbn_bdq_pack) of the online and/or target network."""
+        """Recompute the images (pbn_bdq_pack: the bilinear target table and the fragment-ordered
+        dense weights) of the online and/or target network."""
         L = _lib.load()
         with torch.cuda.device(self.q_flat.device):
-            for name, flat, table in (("online", self.q_flat, self.q_table), ("target", self.t_flat, self.t_table)):
+            for name, flat, image in (("online", self.q_flat, self.q_image), ("target", self.t_flat, self.t_image)):
                 if which in ("both", name):
-                    _lib.check(L.pbn_bdq_pack(self.net.handle, self.K, flat.data_ptr(), table.data_ptr(),
+                    _lib.check(L.pbn_bdq_pack(self.net.handle, self.K, flat.data_ptr(), image.data_ptr(),
                                               self._stream()), "pbn_bdq_pack")
         if which in ("both", "online"):
             self._qv = self._versions(self._qp)
@@ -407,8 +417,8 @@ class FusedBDQUpdate:
             _lib.check(L.pbn_bdq_learn(self.net.handle, self.B, idx.contiguous().data_ptr(), replay.capacity,
                                        replay.state.data_ptr(), replay.next_state.data_ptr(), replay.target.data_ptr(),
                                        replay.action.data_ptr(), self.K, replay.reward.data_ptr(),
-                                       replay.done.data_ptr(), self.q_flat.data_ptr(), self.q_table.data_ptr(),
-                                       self.t_flat.data_ptr(), self.t_table.data_ptr(), self.m.data_ptr(),
+                                       replay.done.data_ptr(), self.q_flat.data_ptr(), self.q_image.data_ptr(),
+                                       self.t_flat.data_ptr(), self.t_image.data_ptr(), self.m.data_ptr(),
                                        self.v.data_ptr(), self.step.data_ptr(), self.lr, b1, b2, self.eps, self.gamma,
                                        self.grad_clamp, self.slope, self.work.data_ptr(), self.work.numel() * 4,
                                        self.loss.data_ptr(), self.grad.data_ptr() if self.grad is not None else None,

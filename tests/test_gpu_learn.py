@@ -55,6 +55,32 @@ def _nets(N, K, seed):
     return q, tgt
 
 
+def _check_image(fused, q, N, K):
+    """The image's weight tiles (pbn_learn.hip make_image) restated from the module's weights:
+    per dense layer (the three trunk layers, the stacked first head layers, the second head layers
+    as (K + 1) x Apad rows, zero past each head's N + 1), tile (ot, kt) of 256 floats in two
+    orders; fwd lane g*16 + r holds M[16ot + r][16kt + 4g + v], bwd M[16ot + 4g + v][16kt + r]."""
+    A, Ap = N + 1, 16 * ((N + 16) // 16)
+    m = q.model
+    heads = [q.value_head] + list(q.adv_heads)
+    h2 = torch.zeros(len(heads), Ap, 64, device="cuda")
+    for h, hd in enumerate(heads):
+        h2[h, :hd[2].weight.shape[0]] = hd[2].weight.detach()
+    mats = [m[2].weight.detach(), m[4].weight.detach(), m[6].weight.detach(),
+            torch.cat([hd[0].weight.detach() for hd in heads]), h2.reshape(-1, 64)]
+    o = fused.q_table.numel()
+    for M in mats:
+        R, C = M.shape
+        t = M.reshape(R // 16, 16, C // 16, 16).permute(0, 2, 1, 3)          # [ot][kt][row][col]
+        fwd = t.reshape(R // 16, C // 16, 16, 4, 4).permute(0, 1, 3, 2, 4)  # [ot][kt][g][r][v]: M[r][4g + v]
+        bwd = t.reshape(R // 16, C // 16, 4, 4, 16).permute(0, 1, 2, 4, 3)  # [ot][kt][g][r][v]: M[4g + v][r]
+        for want in (fwd, bwd):
+            got = fused.q_image[o:o + R * C]
+            assert torch.equal(got, want.reshape(-1)), (M.shape, o)
+            o += R * C
+    assert o == fused.q_image.numel()
+
+
 @pytest.mark.parametrize("net,B,K", [("pbn28", 256, 3), ("pbn28", 32, 1), ("pbn28", 96, 7), ("pbn70", 64, 3)])
 def test_fused_update_matches_pytorch(net, B, K):
     spec = EnvSpec(load_network(net), load_attractors(net))
@@ -85,11 +111,12 @@ def test_fused_update_matches_pytorch(net, B, K):
     # the value head's padding (outputs past 0) stays zero in the flat buffer
     o, A = fused.off, N + 1
     assert not fused.q_flat[o[10] + 64:o[10] + A * 64].any() and not fused.q_flat[o[11] + 1:o[11] + A].any()
-    # the online table written by the update = pbn_bdq_pack of the new weights, bit for bit, and
-    # equal to the PyTorch contraction to rounding
-    t_upd = fused.q_table.clone()
+    # the online image written by the update (table and fragment-ordered weights) = pbn_bdq_pack
+    # of the new weights, bit for bit, and the table equal to the PyTorch contraction to rounding
+    t_upd = fused.q_image.clone()
     fused.pack("online")
-    assert torch.equal(t_upd, fused.q_table)
+    assert torch.equal(t_upd, fused.q_image)
+    _check_image(fused, q, N, K)
     if len(spec.attractors):
         targets = torch.tensor([list(a[0]) for a in spec.attractors], dtype=torch.float32, device="cuda")
         T = q.model[0].target_table(targets)
@@ -171,7 +198,7 @@ def test_captured_fused_learner_is_bit_exact(upf):
     assert torch.equal(eager.fused.q_flat, graph.fused.q_flat)
     assert torch.equal(eager.fused.t_flat, graph.fused.t_flat)
     assert torch.equal(eager.fused.m, graph.fused.m) and torch.equal(eager.fused.v, graph.fused.v)
-    assert torch.equal(eager.fused.q_table, graph.fused.q_table)
+    assert torch.equal(eager.fused.q_image, graph.fused.q_image)
     assert float(eager.fused.step) == float(graph.fused.step) == eager.updates
 
 
