@@ -72,7 +72,7 @@
 extern "C" {
 #endif
 
-#define PBN_ABI_VERSION 10
+#define PBN_ABI_VERSION 11
 
 #define PBN_MAX_NODES 128
 #define PBN_MAX_ARITY 4
@@ -198,6 +198,36 @@ int pbn_step_dev(pbn_net* net, uint64_t seed, const uint64_t* d_step, uint64_t e
                  uint32_t mode, const uint32_t* d_state, uint32_t* d_flipmask, uint8_t* d_target,
                  uint8_t* d_t, uint32_t* d_state_out, uint32_t* d_final_state, float* d_reward,
                  uint8_t* d_flags, void* stream);
+
+/*
+ * pbn_step_dev_store (ABI 11): pbn_step_dev that also writes the step's transitions into a replay
+ * ring, the layout pbn_replay_store writes (replaces the learning frame's separate ring-store
+ * launch, pbn_rl_amd/replay.py BDQLearner's captured frame).  One-update law only (settle_max < 2;
+ * PBN_EINVAL otherwise).  d_state is updated in place.  Env e's row is (*d_pos + e) mod capacity
+ * (d_pos read when the kernel runs; not advanced): state = s as the step read it (bits past N
+ * cleared), next_state = s' before an autoreset (= d_final_state), target = the target before
+ * the step, action = d_actions_in's n_branches int32 of env e, reward, done = (flags & done_mask)
+ * != 0 (done_mask 0: flags != 0), also into d_done_out[e] when not null.
+ */
+typedef struct pbn_ring_store {
+  int64_t capacity;            /* >= n_envs */
+  const int64_t* d_pos;
+  uint32_t* d_state;           /* [W][capacity] */
+  uint32_t* d_next_state;      /* [W][capacity] */
+  uint8_t* d_target;           /* [capacity] */
+  int32_t* d_action;           /* [capacity][n_branches] */
+  float* d_reward;             /* [capacity] */
+  uint8_t* d_done;             /* [capacity] */
+  const int32_t* d_actions_in; /* [n_envs][n_branches] */
+  int32_t n_branches;
+  uint32_t done_mask;
+  uint8_t* d_done_out;         /* nullable: [n_envs] */
+} pbn_ring_store;
+
+int pbn_step_dev_store(pbn_net* net, uint64_t seed, const uint64_t* d_step, uint64_t env_offset, int64_t n_envs,
+                       uint32_t mode, uint32_t* d_state, uint32_t* d_flipmask, uint8_t* d_target, uint8_t* d_t,
+                       uint32_t* d_final_state, float* d_reward, uint8_t* d_flags, const pbn_ring_store* ring,
+                       void* stream);
 
 /*
  * n_steps synchronous transitions in one launch (steps step .. step+n_steps-1), with the

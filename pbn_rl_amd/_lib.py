@@ -24,7 +24,7 @@ FLAG_PERTURBED = 8
 FLAG_RESET = 16
 FLAG_UNSETTLED = 32
 
-EXPORTS = ["pbn_net_create", "pbn_net_destroy", "pbn_net_words", "pbn_reset", "pbn_step", "pbn_step_dev",
+EXPORTS = ["pbn_net_create", "pbn_net_destroy", "pbn_net_words", "pbn_reset", "pbn_step", "pbn_step_dev", "pbn_step_dev_store",
            "pbn_rollout", "pbn_rollout_ex", "pbn_state_histogram", "pbn_obs_unpack", "pbn_bilinear_targets", "pbn_q_to_flipmask",
            "pbn_q_to_flipmask_dev",
            "pbn_heads_to_flipmask", "pbn_qnet_heads", "pbn_qnet_flipmask", "pbn_qnet_heads_from_state",
@@ -38,6 +38,15 @@ _lib: Optional[ctypes.CDLL] = None
 
 class PbnError(RuntimeError):
     pass
+
+
+class RingStore(ctypes.Structure):
+    """pbn_ring_store (include/pbn_env.h, ABI 11): the replay ring pbn_step_dev_store writes the
+    step's transitions into (pbn_replay_store's layout)."""
+    _fields_ = [("capacity", ctypes.c_int64), ("d_pos", ctypes.c_void_p), ("d_state", ctypes.c_void_p),
+                ("d_next_state", ctypes.c_void_p), ("d_target", ctypes.c_void_p), ("d_action", ctypes.c_void_p),
+                ("d_reward", ctypes.c_void_p), ("d_done", ctypes.c_void_p), ("d_actions_in", ctypes.c_void_p),
+                ("n_branches", ctypes.c_int32), ("done_mask", ctypes.c_uint32), ("d_done_out", ctypes.c_void_p)]
 
 
 class FrameAdvance(ctypes.Structure):
@@ -99,6 +108,9 @@ def load() -> ctypes.CDLL:
     L.pbn_step.restype = ctypes.c_int
     L.pbn_step_dev.argtypes = [vp, u64, vp, u64, i64, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.pbn_step_dev.restype = ctypes.c_int
+    if hasattr(L, "pbn_step_dev_store"):   # (ABI 11)
+        L.pbn_step_dev_store.argtypes = [vp, u64, vp, u64, i64, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.pbn_step_dev_store.restype = ctypes.c_int
     L.pbn_rollout.argtypes = [vp, u64, u64, u64, i64, ctypes.c_int32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.pbn_rollout.restype = ctypes.c_int
     L.pbn_rollout_ex.argtypes = [vp, u64, u64, u64, i64, ctypes.c_int32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp,

@@ -891,14 +891,15 @@ int pbn_reset(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, i
 static int step_impl(pbn_net* net, uint64_t seed, uint64_t step, const uint64_t* d_step, uint64_t env_offset,
                      int64_t n_envs, uint32_t mode, const uint32_t* d_state, uint32_t* d_flipmask,
                      uint8_t* d_target, uint8_t* d_t, uint32_t* d_state_out, uint32_t* d_final_state,
-                     float* d_reward, uint8_t* d_flags, void* stream) {
+                     float* d_reward, uint8_t* d_flags, void* stream, const pbn_ring_store* ring = nullptr) {
   int rc = check_common(net, env_offset, n_envs, true);
   if (rc) return rc;
   if (n_envs == 0) return PBN_OK;
   if (mode & ~(PBN_MODE_AUTORESET | PBN_MODE_RANDOM_ACTIONS)) return fail(PBN_EINVAL, "unknown mode bits");
   if (!d_state || !d_flipmask || !d_target || !d_t || !d_state_out || !d_reward || !d_flags)
     return fail(PBN_EINVAL, "null buffer");
-  if (d_state_out == d_state) return fail(PBN_EINVAL, "d_state_out must not alias d_state");
+  // (the ring form steps in place: the wave kernel's lane reads its env's state once, at entry)
+  if (d_state_out == d_state && !ring) return fail(PBN_EINVAL, "d_state_out must not alias d_state");
   if (!aligned16(d_state) || !aligned16(d_flipmask) || !aligned16(d_target) || !aligned16(d_t) ||
       !aligned16(d_state_out) || !aligned16(d_reward) || !aligned16(d_flags) ||
       (d_final_state && !aligned16(d_final_state)))
@@ -916,6 +917,27 @@ static int step_impl(pbn_net* net, uint64_t seed, uint64_t step, const uint64_t*
   a.flags = d_flags;
   a.mode = (int)mode;
   if (net->lds_wave > 160 * 1024) return fail(PBN_EINVAL, "network too large for the step kernel's LDS");
+  if (ring) {
+    const pbn_ring_store& r = *ring;
+    if (net->settle_max >= 2) return fail(PBN_EINVAL, "pbn_step_dev_store: the one-update law only (settle_max < 2)");
+    if (r.capacity < n_envs) return fail(PBN_EINVAL, "pbn_ring_store: capacity < n_envs");
+    if (r.n_branches < 0 || r.n_branches > 64) return fail(PBN_EINVAL, "pbn_ring_store: n_branches 0..64");
+    if (!r.d_pos || ((uintptr_t)r.d_pos & 7u) || !r.d_state || !r.d_next_state || !r.d_target || !r.d_reward ||
+        !r.d_done || (r.n_branches > 0 && (!r.d_action || !r.d_actions_in)))
+      return fail(PBN_EINVAL, "pbn_ring_store: null or misaligned buffer");
+    a.r_state = r.d_state;
+    a.r_next = r.d_next_state;
+    a.r_target = r.d_target;
+    a.r_action = r.d_action;
+    a.r_reward = r.d_reward;
+    a.r_done = r.d_done;
+    a.r_act_in = r.d_actions_in;
+    a.r_done_out = r.d_done_out;
+    a.r_pos = r.d_pos;
+    a.r_cap = r.capacity;
+    a.r_k = r.n_branches;
+    a.r_done_mask = r.done_mask;
+  }
   // the settle law on whole groups: a one-step launch of the pipelined settle kernel
   // (pbn_rollout_settle; its env-major outputs of one step are pbn_step's), where every env runs
   // its own update sequence and an update is one pipeline iteration, against the wave kernel's
@@ -952,6 +974,17 @@ int pbn_step_dev(pbn_net* net, uint64_t seed, const uint64_t* d_step, uint64_t e
   if (((uintptr_t)d_step & 7u) != 0) return fail(PBN_EINVAL, "d_step must be 8-byte aligned");
   return step_impl(net, seed, 0, d_step, env_offset, n_envs, mode, d_state, d_flipmask, d_target, d_t,
                    d_state_out, d_final_state, d_reward, d_flags, stream);
+}
+
+int pbn_step_dev_store(pbn_net* net, uint64_t seed, const uint64_t* d_step, uint64_t env_offset, int64_t n_envs,
+                       uint32_t mode, uint32_t* d_state, uint32_t* d_flipmask, uint8_t* d_target, uint8_t* d_t,
+                       uint32_t* d_final_state, float* d_reward, uint8_t* d_flags, const pbn_ring_store* ring,
+                       void* stream) {
+  if (!d_step) return fail(PBN_EINVAL, "null d_step");
+  if (((uintptr_t)d_step & 7u) != 0) return fail(PBN_EINVAL, "d_step must be 8-byte aligned");
+  if (!ring) return fail(PBN_EINVAL, "null ring");
+  return step_impl(net, seed, 0, d_step, env_offset, n_envs, mode, d_state, d_flipmask, d_target, d_t, d_state,
+                   d_final_state, d_reward, d_flags, stream, ring);
 }
 
 int pbn_rollout(pbn_net* net, uint64_t seed, uint64_t step, uint64_t env_offset, int64_t n_envs,

@@ -110,6 +110,21 @@ struct StepArgs {
   void* cp_dst;
   int64_t cp_n16;
   int cp_u;
+  // pbn_step_dev_store (ABI 11): the one-update wave kernel also writes the step's transitions into
+  // a replay ring (pbn_replay_store's layout), env le at row (*r_pos + le) mod r_cap; r_state null:
+  // none
+  uint32_t* r_state;
+  uint32_t* r_next;
+  uint8_t* r_target;
+  int32_t* r_action;
+  float* r_reward;
+  uint8_t* r_done;
+  const int32_t* r_act_in;   // [n][r_k] the frame's branch actions
+  uint8_t* r_done_out;       // nullable: [n]
+  const int64_t* r_pos;
+  int64_t r_cap;
+  int r_k;
+  uint32_t r_done_mask;
 };
 
 typedef unsigned int pbn_u32x4 __attribute__((ext_vector_type(4)));
@@ -1026,6 +1041,20 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
     tt0 = a.t[CK(le, n, 2)];
     tg0 = a.target[CK(le, n, 3)];
   }
+  // pbn_step_dev_store: the transition's row, and what the step reads (s, the target, the branch
+  // actions) into it now; s' (before an autoreset), the reward and done after the step
+  int64_t rj = 0;
+  if constexpr (!SETTLE) {
+    if (live && a.r_state) {
+      rj = (int64_t)(((uint64_t)*a.r_pos + (uint64_t)le) % (uint64_t)a.r_cap);
+#pragma unroll
+      for (int w = 0; w < W; ++w) a.r_state[CK((size_t)w * a.r_cap + rj, (size_t)W * a.r_cap, 40)] = st[w];
+      a.r_target[CK(rj, a.r_cap, 41)] = (uint8_t)tg0;
+      for (int k = 0; k < a.r_k; ++k)
+        a.r_action[CK((size_t)rj * a.r_k + k, (size_t)a.r_cap * a.r_k, 42)] =
+            a.r_act_in[CK((size_t)le * a.r_k + k, (size_t)n * a.r_k, 43)];
+    }
+  }
   // node l32 + 32r: its first kNodeRecs compact records {inputs, table, threshold, meta}
   // (node-major, fixed stride: no dependent load); meta of record 0 = nf, of record 1 = f0
   uint4 rec_[W][kNodeRecs];
@@ -1229,13 +1258,20 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
 #pragma unroll
     for (int w = 0; w < W; ++w) a.final_state[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 10)] = sp[w];
   }
+  if constexpr (!SETTLE) {
+    if (a.r_state) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) a.r_next[CK((size_t)w * a.r_cap + rj, (size_t)W * a.r_cap, 44)] = sp[w];
+    }
+  }
   const bool in_attr = att >= 0;
   const bool term = in_attr && (uint32_t)att == tg0;
   const bool wrong = in_attr && !term;
   int tt = (int)tt0 + 1;
   tt = tt > 255 ? 255 : tt;
   const bool trunc = a.horizon > 0 && tt >= a.horizon;
-  a.reward[CK(ks * n + le, n_steps * n, 11)] = rtab[(int)pc * 4 + 2 * (int)term + (int)wrong];
+  const float rwd = rtab[(int)pc * 4 + 2 * (int)term + (int)wrong];
+  a.reward[CK(ks * n + le, n_steps * n, 11)] = rwd;
   uint32_t fl = (uint32_t)term | ((uint32_t)trunc << 1) | ((uint32_t)in_attr << 2) | ((uint32_t)pert << 3) |
                 ((uint32_t)unsettled << 5);
   if ((a.mode & PBN_MODE_AUTORESET) && (term || trunc)) {
@@ -1257,6 +1293,14 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
     fl |= PBN_FLAG_RESET;
   }
   a.flags[CK(ks * n + le, n_steps * n, 15)] = (uint8_t)fl;
+  if constexpr (!SETTLE) {
+    if (a.r_state) {   // done as pbn_replay_store derives it from the flags byte
+      const uint8_t d = a.r_done_mask ? ((fl & a.r_done_mask) ? 1 : 0) : ((uint8_t)fl ? 1 : 0);
+      a.r_reward[CK(rj, a.r_cap, 45)] = rwd;
+      a.r_done[CK(rj, a.r_cap, 46)] = d;
+      if (a.r_done_out) a.r_done_out[CK(le, n, 47)] = d;
+    }
+  }
   tt0 = (uint32_t)tt;
 #pragma unroll
   for (int w = 0; w < W; ++w) st[w] = sp[w];

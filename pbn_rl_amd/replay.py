@@ -608,6 +608,14 @@ class BDQLearner:
         self._size_t = torch.full((1,), self.replay.size, dtype=torch.int64, device=dev)
         self._done_buf = torch.zeros(env.n_alloc, dtype=torch.uint8, device=dev)
         self._tgt_prev = env.target.clone()   # the pre-step targets, carried by the ring store
+        # under the one-update law the step kernel writes the ring rows itself (pbn_step_dev_store)
+        self._ring = None
+        if env.spec.settle < 2:
+            rp = self.replay
+            self._ring = _lib.RingStore(
+                rp.capacity, self._pos_t.data_ptr(), rp.state.data_ptr(), rp.next_state.data_ptr(), rp.target.data_ptr(),
+                rp.action.data_ptr(), rp.reward.data_ptr(), rp.done.data_ptr(), self.agent.actions.data_ptr(),
+                rp.action.shape[1], _lib.FLAG_TERMINATED | _lib.FLAG_TRUNCATED, self._done_buf.data_ptr())
         self._adv = None
         if self.fused is not None:
             # the fused update's last launch advances the frame's counters and draws the next
@@ -633,15 +641,21 @@ class BDQLearner:
     def _graph_body(self):
         env = self.env
         self.agent.act_q(step_t=self._step_t, epsilon_t=self._eps32)
-        env.step_flipmask_dev(self._step_t, copy_back=False)
-        # the ring store reads the pre-step state (still in env.state) and target (carried in
-        # _tgt_prev), derives done from the flags, and in the same pass moves the stepped state into
-        # env.state and the new targets into _tgt_prev; then one launch advances the step index,
-        # the ring position and fill level and epsilon, and (fused) draws the frame's batches
-        self.replay.store_at(self._pos_t, self._size_t, env.state, self._tgt_prev, self.agent.actions, env.reward,
-                             env.final_state, env.flags, done_mask=_lib.FLAG_TERMINATED | _lib.FLAG_TRUNCATED,
-                             done_out=self._done_buf, advance=False, state_copy=(env.state, env._state_next),
-                             target_copy=(self._tgt_prev, env.target))
+        if self._ring is not None:
+            # one launch: the step, in place, writing its transitions into the ring
+            env.step_flipmask_dev_store(self._step_t, self._ring)
+        else:
+            env.step_flipmask_dev(self._step_t, copy_back=False)
+            # the ring store reads the pre-step state (still in env.state) and target (carried in
+            # _tgt_prev), derives done from the flags, and in the same pass moves the stepped state
+            # into env.state and the new targets into _tgt_prev
+            self.replay.store_at(self._pos_t, self._size_t, env.state, self._tgt_prev, self.agent.actions,
+                                 env.reward, env.final_state, env.flags,
+                                 done_mask=_lib.FLAG_TERMINATED | _lib.FLAG_TRUNCATED, done_out=self._done_buf,
+                                 advance=False, state_copy=(env.state, env._state_next),
+                                 target_copy=(self._tgt_prev, env.target))
+        # then the counters: the step index, the ring position and fill level, epsilon (and, fused,
+        # the next frame's rows) advance in the update's last launch or in pbn_replay_advance
         fused = self.fused is not None
         L = _lib.load()
         if not fused:   # (fused: the update's last launch advances them, pbn_frame_advance)

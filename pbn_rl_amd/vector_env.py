@@ -9,6 +9,7 @@ kernel's group size); the padding envs are real envs nobody reads.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Optional, Sequence, Tuple, Union
 
 import torch
@@ -206,6 +207,22 @@ class VectorPBNEnv:
             return self._state_next[:, :k], self.reward[:k], self.flags[:k]
         self.state.copy_(self._state_next)
         return self.state[:, :k], self.reward[:k], self.flags[:k]
+
+    def step_flipmask_dev_store(self, step_t: torch.Tensor, ring) -> None:
+        """``step_flipmask_dev`` that also writes the step's transitions into a replay ring
+        (``pbn_step_dev_store``, one launch where the step and ``pbn_replay_store`` were two; the
+        one-update law only).  ``ring``: an ``_lib.RingStore``.  The state is stepped in place."""
+        if step_t.dtype != torch.int64 or step_t.device != self.device or step_t.numel() != 1:
+            raise ValueError("step_t must be a one-element int64 tensor on the env's device")
+        L = _lib.load()
+        mode = _lib.MODE_AUTORESET if self.autoreset else 0
+        fs = self.final_state.data_ptr() if self.final_state is not None else None
+        with torch.cuda.device(self.device):
+            _lib.check(L.pbn_step_dev_store(self.net.handle, self.seed, step_t.data_ptr(), self.env_offset,
+                                            self.n_alloc, mode, self.state.data_ptr(), self.flipmask.data_ptr(),
+                                            self.target.data_ptr(), self.t.data_ptr(), fs, self.reward.data_ptr(),
+                                            self.flags.data_ptr(), ctypes.byref(ring), self._stream()),
+                       "pbn_step_dev_store")
 
     def rollout_buffers(self, n_steps: int, keep_obs: bool = False, keep_final: bool = True,
                         keep_updates: bool = False) -> dict:

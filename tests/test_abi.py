@@ -41,7 +41,7 @@ def test_library_exports_every_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.pbn_abi_version() == 10
+    assert lib.pbn_abi_version() == 11
 
 
 def test_descriptor_layout_matches_header(tmp_path):

@@ -243,3 +243,82 @@ def test_replay_store_in_pass_copies():
     assert torch.equal(a.state, st0) and torch.equal(a.target, tg0) and torch.equal(a.next_state, nxt)
     assert torch.equal(st, nxt) and torch.equal(tg, tg_new)
     assert int(pos_t) == 0 and int(size_t) == 64
+
+
+@pytest.mark.parametrize("net,n,pos,cap,done_mask", [("pbn28", 4096, 3000, 5000, 3), ("pbn28", 70, 60, 100, 0),
+                                                      ("pbn70", 1024, 0, 1024, 3), ("pbn7", 33, 31, 70, 1)])
+def test_step_dev_store_equals_step_then_ring_store(net, n, pos, cap, done_mask):
+    """pbn_step_dev_store (the step writing its own transitions into the ring) against
+    pbn_step_dev + pbn_replay_store on the same inputs, bit for bit: the stepped env (state in
+    place, target, t, final state, reward, flags), every ring field, done_out, and rows outside the
+    frame untouched; ring wrap-around, ragged env counts, one and two state words."""
+    from pbn_rl_amd import _lib
+    spec = EnvSpec(load_network(net), load_attractors(net), perturbation=0.05, horizon=3)
+    K = 3
+    dev = torch.device("cuda")
+    envs = [VectorPBNEnv(spec, n, seed=9) for _ in range(2)]
+    g = torch.Generator(device=dev).manual_seed(n)
+    for e in envs:
+        e.reset()
+    for _ in range(2):   # some mid-episode t and a horizon truncation next step
+        for e in envs:
+            e.step_flipmask(random_actions=True)
+    acts = torch.randint(0, spec.n + 1, (envs[0].n_alloc, K), device=dev, generator=g, dtype=torch.int32)
+    flip = torch.zeros_like(envs[0].flipmask)
+    for b in range(K):
+        a = acts[:, b].long()
+        on = a > 0
+        bit = torch.where(on, a - 1, torch.zeros_like(a))
+        w, sh = bit // 32, bit % 32
+        for wi in range(envs[0].words):
+            flip[wi] |= torch.where(on & (w == wi), torch.ones_like(a) << sh, torch.zeros_like(a)).to(torch.int32)
+    step_t = torch.tensor([envs[0].step_index], dtype=torch.int64, device=dev)
+    rings = [DeviceReplay(cap, envs[0].words, K, dev) for _ in range(2)]
+    for r in rings:   # canaries: rows outside the frame must stay as they were
+        r.state.fill_(-7)
+        r.next_state.fill_(-7)
+        r.target.fill_(0xEE)
+        r.action.fill_(-7)
+        r.reward.fill_(-7.0)
+        r.done.fill_(0xEE)
+    pos_t = torch.tensor([pos], dtype=torch.int64, device=dev)
+    size_t = torch.tensor([0], dtype=torch.int64, device=dev)
+    outs = [torch.full((envs[0].n_alloc,), 0xAB, dtype=torch.uint8, device=dev) for _ in range(2)]
+    # reference: the step, then the ring store (pre-step state and target kept aside)
+    a = envs[0]
+    a.flipmask.copy_(flip)
+    st0, tg0 = a.state.clone(), a.target.clone()
+    a.step_flipmask_dev(step_t, copy_back=True)
+    rings[0].store_at(pos_t, size_t, st0, tg0, acts, a.reward, a.final_state, a.flags, done_mask=done_mask,
+                      done_out=outs[0], advance=False)
+    # fused
+    b = envs[1]
+    b.flipmask.copy_(flip)
+    r = rings[1]
+    ring = _lib.RingStore(cap, pos_t.data_ptr(), r.state.data_ptr(), r.next_state.data_ptr(), r.target.data_ptr(),
+                          r.action.data_ptr(), r.reward.data_ptr(), r.done.data_ptr(), acts.data_ptr(), K, done_mask,
+                          outs[1].data_ptr())
+    b.step_flipmask_dev_store(step_t, ring)
+    torch.cuda.synchronize()
+    for name in ("state", "target", "t", "final_state", "reward", "flags"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    for name in ("state", "next_state", "target", "action", "reward", "done"):
+        assert torch.equal(getattr(rings[0], name), getattr(rings[1], name)), name
+    assert torch.equal(outs[0], outs[1])
+    assert int((rings[1].done != 0xEE).sum()) == envs[0].n_alloc   # exactly the frame's rows written
+    assert int(pos_t) == pos
+
+
+def test_step_dev_store_refuses_the_settle_law():
+    from pbn_rl_amd import _lib
+    spec = EnvSpec(load_network("pbn7"), load_attractors("pbn7"), settle=8)
+    env = VectorPBNEnv(spec, 64)
+    env.reset()
+    r = DeviceReplay(64, 1, 1, env.device)
+    pos_t = torch.zeros(1, dtype=torch.int64, device=env.device)
+    acts = torch.zeros(64, 1, dtype=torch.int32, device=env.device)
+    ring = _lib.RingStore(64, pos_t.data_ptr(), r.state.data_ptr(), r.next_state.data_ptr(), r.target.data_ptr(),
+                          r.action.data_ptr(), r.reward.data_ptr(), r.done.data_ptr(), acts.data_ptr(), 1, 0, None)
+    step_t = torch.zeros(1, dtype=torch.int64, device=env.device)
+    with pytest.raises(_lib.PbnError, match="one-update law"):
+        env.step_flipmask_dev_store(step_t, ring)

@@ -1,6 +1,6 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
-out=gpurun_out/r06_p; mkdir -p $out; export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests/test_gpu_learn.py tests/test_gpu_graph.py tests/test_gpu_replay.py tests/test_gpu_agent.py -m gpu -x -q --timeout 240 --timeout-method thread > $out/tests.log 2>&1 || { tail -30 $out/tests.log; exit 4; }
+out=gpurun_out/r06_t; mkdir -p $out; export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests/test_gpu_replay.py tests/test_gpu_graph.py tests/test_gpu_learn.py tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_agent.py -m gpu -x -q --timeout 240 --timeout-method thread > $out/tests.log 2>&1 || { tail -30 $out/tests.log; exit 4; }
 tail -1 $out/tests.log
 for rep in 1 2; do
 for side in base tree; do
