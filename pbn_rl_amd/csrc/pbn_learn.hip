@@ -727,7 +727,9 @@ __device__ __forceinline__ float adam_apply(const LearnArgs& a, int64_t i, AdamI
 
 // T[t][i][o] = sum_j target_t[j] W[o][i][j] in j order (pbn_bdq_pack computes the same sums), from
 // the target's first-state words tw and the weight row in LDS (eight reads in flight)
-__device__ __forceinline__ float table_entry(const uint32_t (&tw)[4], int N, const float* __restrict__ wrow) {
+// (the words as a uint4 by value: as an array the run-time word select made it a stack array, and
+// each word's load waited to be stored to scratch)
+__device__ __forceinline__ float table_entry(uint4 tw, int N, const float* __restrict__ wrow) {
   float s = 0.f;
   for (int j0 = 0; j0 < N; j0 += 8) {
     float x[8];
@@ -736,7 +738,7 @@ __device__ __forceinline__ float table_entry(const uint32_t (&tw)[4], int N, con
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int j = j0 + u;
-      const uint32_t word = (j >> 5) == 0 ? tw[0] : (j >> 5) == 1 ? tw[1] : (j >> 5) == 2 ? tw[2] : tw[3];
+      const uint32_t word = (j >> 5) == 0 ? tw.x : (j >> 5) == 1 ? tw.y : (j >> 5) == 2 ? tw.z : tw.w;
       const bool on = j < N && ((word >> (j & 31)) & 1u);
       s += on ? x[u] : 0.f;
     }
@@ -744,9 +746,25 @@ __device__ __forceinline__ float table_entry(const uint32_t (&tw)[4], int N, con
   return s;
 }
 
-__device__ __forceinline__ void target_words(const LearnArgs& a, int t, uint32_t (&tw)[4]) {
+__device__ __forceinline__ uint4 target_words(const LearnArgs& a, int t) {
+  uint32_t tw[4];
 #pragma unroll
   for (int w = 0; w < 4; ++w) tw[w] = (t < a.n_attr && w < a.W) ? a.att_first[(size_t)t * a.W + w] : 0u;
+  return make_uint4(tw[0], tw[1], tw[2], tw[3]);
+}
+
+// Loads issued ahead of their use in straight-line code, without a branch or a select at the
+// load: a guarded load puts its select right behind the load, and that select's s_waitcnt waits
+// out every load issued before it (vmcnt retires in order: learn_apply's ISA had a vmcnt(0)
+// behind each of its 16 target-word loads, and its gradient operands queued behind the Adam
+// state).  Clamped to a valid element; the callers use only the valid lanes' values.
+__device__ __forceinline__ uint4 target_words_ahead(const LearnArgs& a, int t) {
+  const uint32_t* af = a.n_attr > 0 ? a.att_first : reinterpret_cast<const uint32_t*>(a.P);   // (no attractors: unused)
+  const uint32_t* row = af + (size_t)(t < a.n_attr ? t : (a.n_attr > 0 ? a.n_attr - 1 : 0)) * a.W;
+  return make_uint4(row[0], row[a.W > 1 ? 1 : 0], row[a.W > 2 ? 2 : 0], row[a.W > 3 ? 3 : 0]);
+}
+__device__ __forceinline__ AdamIn adam_load_ahead(const LearnArgs& a, int64_t i) {
+  return AdamIn{a.P[i], a.m[i], a.v[i]};
 }
 
 struct Dense {
@@ -786,19 +804,7 @@ __global__ void __launch_bounds__(64 * kApplyWaves) learn_apply_kernel(LearnArgs
   if (task < n_bil) {
     // bilinear weight tile: outputs o0..o0+15 of input i, all j: D[o][j] = sum_r g1[o][r] s_i[r] t_j[r]
     const int ot = task / a.N, i = task - ot * a.N, o0 = 16 * ot;
-    uint32_t tpre[4][4];   // the first four target rows' words of this lane (t = g + 4u), requested now
-#pragma unroll
-    for (int u = 0; u < 4; ++u) target_words(a, g + 4 * u, tpre[u]);
     const int64_t NN = (int64_t)a.N * a.N;
-    AdamIn pre[NT][4];
-#pragma unroll
-    for (int jt = 0; jt < NT; ++jt)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int jj = 16 * jt + rr;
-        pre[jt][v] = adam_load(a, a.off[BIL_W] + (o0 + 4 * g + v) * NN + (int64_t)i * a.N + jj, jj < a.N);
-      }
-    const AdamIn preb = adam_load(a, a.off[BIL_B] + o0 + rr, i == 0 && g == 0);
     const uint32_t* si = a.srow + (size_t)(i >> 5) * B;
     const float* grow = a.g1 + (size_t)(o0 + rr) * B;
     f32x4 acc[NT];
@@ -807,9 +813,9 @@ __global__ void __launch_bounds__(64 * kApplyWaves) learn_apply_kernel(LearnArgs
     float bsum = 0.f;
     constexpr int RC = NT <= 2 ? 8 : 4;   // 16-row steps per round of loads
     const uint32_t sh = i & 31;
-    for (int r0 = 0; r0 < B; r0 += 16 * RC) {
-      float4 y[RC];
-      uint4 sv[RC], tv[RC][NT];
+    float4 y[RC];
+    uint4 sv[RC], tv[RC][NT];
+    auto round_loads = [&](int r0) __attribute__((always_inline)) {
 #pragma unroll
       for (int u = 0; u < RC; ++u) {
         const int rb = min(r0 + 16 * u, B - 16) + 4 * g;
@@ -819,6 +825,26 @@ __global__ void __launch_bounds__(64 * kApplyWaves) learn_apply_kernel(LearnArgs
         for (int jt = 0; jt < NT; ++jt)
           tv[u][jt] = *reinterpret_cast<const uint4*>(a.trow + (size_t)((16 * jt + rr) >> 5) * B + rb);
       }
+    };
+    // the first round's gradient operands, then the tile's Adam state and the first four target
+    // rows' words of this lane (t = g + 4u) behind them (used after the loop), then the rounds
+    round_loads(0);
+    __builtin_amdgcn_sched_barrier(0);
+    AdamIn pre[NT][4];
+#pragma unroll
+    for (int jt = 0; jt < NT; ++jt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int jj = min(16 * jt + rr, a.N - 1);   // (lanes past N: never applied)
+        pre[jt][v] = adam_load_ahead(a, a.off[BIL_W] + (o0 + 4 * g + v) * NN + (int64_t)i * a.N + jj);
+      }
+    const AdamIn preb = adam_load_ahead(a, a.off[BIL_B] + o0 + rr);   // (applied by i == 0, g == 0)
+    uint4 tpre[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) tpre[u] = target_words_ahead(a, g + 4 * u);   // (used for t < n_attr)
+    __builtin_amdgcn_sched_barrier(0);
+    for (int r0 = 0; r0 < B; r0 += 16 * RC) {
+      if (r0 > 0) round_loads(r0);
 #pragma unroll
       for (int u = 0; u < RC; ++u) {
         if (r0 + 16 * u < B) {
@@ -867,9 +893,7 @@ __global__ void __launch_bounds__(64 * kApplyWaves) learn_apply_kernel(LearnArgs
       if (t < a.n_attr) a.Tq[((size_t)t * a.N + i) * 256 + rr * 16 + ot] = table_entry(tpre[u], a.N, &wsc[wave][rr][0]);
     }
     for (int t = g + 16; t < a.n_attr; t += 4) {
-      uint32_t tw[4];
-      target_words(a, t, tw);
-      a.Tq[((size_t)t * a.N + i) * 256 + rr * 16 + ot] = table_entry(tw, a.N, &wsc[wave][rr][0]);
+      a.Tq[((size_t)t * a.N + i) * 256 + rr * 16 + ot] = table_entry(target_words(a, t), a.N, &wsc[wave][rr][0]);
     }
     PBN_LSTAMP(2, 3);
     return;
@@ -902,25 +926,31 @@ __global__ void __launch_bounds__(64 * kApplyWaves) learn_apply_kernel(LearnArgs
   ot = task / L.k_tiles;
   kt = task - ot * L.k_tiles;
   const int o0 = 16 * ot, k0 = 16 * kt;
-  AdamIn pre[4];
-#pragma unroll
-  for (int v = 0; v < 4; ++v) {
-    const int o = o0 + 4 * g + v;
-    pre[v] = adam_load(a, L.w_off + (int64_t)o * L.ldw + k0 + rr, o < L.o_valid);
-  }
-  const AdamIn preb = adam_load(a, L.b_off + o0 + rr, kt == 0 && g == 0 && o0 + rr < L.o_valid);
   const float* yrow = L.dY + (size_t)(o0 + rr) * B;
   const float* xrow = L.X + (size_t)(k0 + rr) * B;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f;
-  for (int r0 = 0; r0 < B; r0 += 128) {   // eight 16-row steps per round of loads
-    float4 y[8], x[8];
+  float4 y[8], x[8];
+  auto round_loads = [&](int r0) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int rb = min(r0 + 16 * u, B - 16) + 4 * g;
       y[u] = *reinterpret_cast<const float4*>(yrow + rb);
       x[u] = *reinterpret_cast<const float4*>(xrow + rb);
     }
+  };
+  round_loads(0);   // then the Adam state behind the first round's operands (the bilinear tiles' order)
+  __builtin_amdgcn_sched_barrier(0);
+  AdamIn pre[4];
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int o = o0 + 4 * g + v;
+    pre[v] = adam_load_ahead(a, L.w_off + (int64_t)(o < L.o_valid ? o : 0) * L.ldw + k0 + rr);   // (o < o_valid only)
+  }
+  const AdamIn preb = adam_load_ahead(a, L.b_off + (o0 + rr < L.o_valid ? o0 + rr : 0));   // (kt, g == 0, valid rows)
+  __builtin_amdgcn_sched_barrier(0);
+  for (int r0 = 0; r0 < B; r0 += 128) {   // eight 16-row steps per round of loads
+    if (r0 > 0) round_loads(r0);
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       if (r0 + 16 * u < B) {
