@@ -235,6 +235,22 @@ __device__ __forceinline__ void fwd_store(f32x4 acc, const float* __restrict__ b
   *reinterpret_cast<float4*>(Ys + ((o0 >> 4) * 16 + rr) * 16 + 4 * g) = y;
 }
 
+// learn_fwd's biases in LDS: [bilinear 256 | 128 | 64 | 32 | H x 64 | H x A] (the layer epilogues
+// read them there: a global load of the bias put its round trip on every layer's path)
+__host__ __device__ inline int fwd_bias_floats(int H, int A) { return kD0 + kD1 + kD2 + kD3 + kDH * H + H * A; }
+__device__ __forceinline__ int64_t fwd_bias_src(const LearnArgs& a, int idx) {
+  if (idx < kD0) return a.off[BIL_B] + idx;
+  idx -= kD0;
+  if (idx < kD1) return a.off[L2_B] + idx;
+  idx -= kD1;
+  if (idx < kD2) return a.off[L3_B] + idx;
+  idx -= kD2;
+  if (idx < kD3) return a.off[L4_B] + idx;
+  idx -= kD3;
+  if (idx < kDH * a.H) return a.off[H1_B] + idx;
+  return a.off[H2_B] + idx - kDH * a.H;
+}
+
 __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* Y1 = lds;                    // [256/16][16][16]
@@ -246,6 +262,7 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
   int* stg = reinterpret_cast<int*>(sw + 4 * kRows);                  // [16]
   int* scnt = stg + kRows;                                            // [16]: set bits per row
   uint8_t* slist = reinterpret_cast<uint8_t*>(scnt + kRows);          // [16][128]: their indices, ascending
+  float* sbias = reinterpret_cast<float*>(slist + kRows * 128);       // fwd_bias_floats
   const int tiles = a.B / kRows;
   const int set = blockIdx.x / tiles;
   const int b0 = (blockIdx.x - set * tiles) * kRows;
@@ -254,6 +271,12 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
   PBN_LSTAMP(0, 31);
   PBN_LSTAMP(0, 0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // the biases, requested first (unguarded: a clamped index) and stored to LDS before the first
+  // barrier
+  const int nbias = fwd_bias_floats(a.H, a.A);
+  float bv[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) bv[k] = P[fwd_bias_src(a, min(tid + kThreads * k, nbias - 1))];
   const int B = a.B;
   float* keep = nullptr;   // the online s rows keep their activations for the backward
   // every layer's weight fragments of this wave, requested at entry (they arrive during the row
@@ -285,6 +308,9 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
     scnt[tid] = c;
   }
   if (wave == 0) fetch_weights();
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (tid + kThreads * k < nbias) sbias[tid + kThreads * k] = bv[k];
   lds_barrier();
   PBN_LSTAMP(0, 1);
   // bilinear layer: y[o] = bias[o] + sum over the set bits i of T[t][i][o] (t = the row's target;
@@ -292,7 +318,7 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
   // lane p reads Tq positions 4p..4p+3 ([t][i][j][q] = T[t][i][16 q + j]: o = 16 q + j): only the
   // table rows of set bits, eight of each row per round trip.
   {
-    const float* bias = P + a.off[BIL_B];
+    const float* bias = sbias;
     const int r0 = 2 * wave;
     const int t0 = stg[r0], t1 = stg[r0 + 1];
     const int c0 = t0 < a.n_attr ? scnt[r0] : 0, c1 = t1 < a.n_attr ? scnt[r0 + 1] : 0;
@@ -344,20 +370,20 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
   if (set == 0) keep = a.h2;
   {   // 256 -> 128: one output tile per wave
     const f32x4 acc = fwd_tile<kD0>(w2, Y1, lane);
-    fwd_store(acc, P + a.off[L2_B], 16 * wave, a.slope, X2, keep, B, b0, lane);
+    fwd_store(acc, sbias + kD0, 16 * wave, a.slope, X2, keep, B, b0, lane);
   }
   PBN_LSTAMP(0, 4);
   lds_barrier();
   PBN_LSTAMP(0, 5);
   if (wave < kD2 / 16) {   // 128 -> 64
     const f32x4 acc = fwd_tile<kD1>(w3, X2, lane);
-    fwd_store(acc, P + a.off[L3_B], 16 * wave, a.slope, X3, set == 0 ? a.h3 : nullptr, B, b0, lane);
+    fwd_store(acc, sbias + kD0 + kD1, 16 * wave, a.slope, X3, set == 0 ? a.h3 : nullptr, B, b0, lane);
   }
   lds_barrier();
   PBN_LSTAMP(0, 6);
   if (wave < kD3 / 16) {   // 64 -> 32
     const f32x4 acc = fwd_tile<kD2>(w4, X3, lane);
-    fwd_store(acc, P + a.off[L4_B], 16 * wave, a.slope, X4, set == 0 ? a.h4 : nullptr, B, b0, lane);
+    fwd_store(acc, sbias + kD0 + kD1 + kD2, 16 * wave, a.slope, X4, set == 0 ? a.h4 : nullptr, B, b0, lane);
   }
   lds_barrier();
   PBN_LSTAMP(0, 7);
@@ -368,14 +394,14 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
       const int tt = wave + kWaves * u;
       if (tt < n1) {
         const f32x4 acc = fwd_tile<kD3>(wh1[u], X4, lane);
-        fwd_store(acc, P + a.off[H1_B], 16 * tt, a.slope, XH, set == 0 ? a.hh : nullptr, B, b0, lane);
+        fwd_store(acc, sbias + kD0 + kD1 + kD2 + kD3, 16 * tt, a.slope, XH, set == 0 ? a.hh : nullptr, B, b0, lane);
       }
     }
     for (int tt = wave + 2 * kWaves; tt < n1; tt += kWaves) {
       float4 wl[kD3 / 16];
       wfrag<kD3>(wl, Tq + a.ifw[LYH1], tt, n1, lane);
       const f32x4 acc = fwd_tile<kD3>(wl, X4, lane);
-      fwd_store(acc, P + a.off[H1_B], 16 * tt, a.slope, XH, set == 0 ? a.hh : nullptr, B, b0, lane);
+      fwd_store(acc, sbias + kD0 + kD1 + kD2 + kD3, 16 * tt, a.slope, XH, set == 0 ? a.hh : nullptr, B, b0, lane);
     }
   }
   lds_barrier();
@@ -385,7 +411,7 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
     const int h = tt / at16, o0 = 16 * (tt - h * at16);
     const f32x4 acc = fwd_tile<kDH>(wl, XH + h * kDH * kRows, lane);
     const int g = lane >> 4, rr = lane & 15;
-    const float* b2 = P + a.off[H2_B] + (size_t)h * a.A;
+    const float* b2 = sbias + kD0 + kD1 + kD2 + kD3 + kDH * a.H + h * a.A;
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int o = o0 + 4 * g + v;
@@ -1273,7 +1299,7 @@ int pbn_bdq_learn(const pbn_net* net, int64_t batch, const int64_t* d_idx, int64
   const hipStream_t s = (hipStream_t)stream;
   const int tiles = (int)(batch / kRows);
   const size_t lds_f = ((size_t)(kD0 + kD1 + kD2 + kD3 + kDH * H) * kRows + 4 * kRows + 2 * kRows) * sizeof(float) +
-                       kRows * 128;
+                       kRows * 128 + (size_t)fwd_bias_floats(H, A) * sizeof(float);
   if (lds_f > 64 * 1024 && hipFuncSetAttribute((const void*)learn_fwd_kernel,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_f) != hipSuccess)
     return pbn::set_error(PBN_EDEVICE, "hipFuncSetAttribute failed");
