@@ -515,10 +515,54 @@ __global__ void __launch_bounds__(kThreads) learn_bwd_kernel(LearnArgs a) {
   const float* Tw = a.Tq;   // the online network's weight tiles
   PBN_LSTAMP(1, 31);
   PBN_LSTAMP(1, 0);
-  // weight fragments of the first four backward layers, requested before the TD pass so they
-  // arrive during it: second head layers (tiles wave, wave + 8 of H x 4), the first head layers
-  // split four ways per output tile (wave & 1 = tile, wave >> 1 = quarter of the 4 H blocks),
-  // 32 -> 64 (waves < 4) and 64 -> 128
+  // Issue order (vmcnt retires in order: a wait for a load waits for every load issued before
+  // it): the TD pass's operands first -- the sampled rows' indices, the block's head rows, then
+  // the rows' actions, rewards and done flags -- and only then the weight fragments and stored
+  // activations the backward layers need after the pass, so that the pass waits for its own loads
+  // alone (it waited for all of them; profiles/r06_ad_bwd_issue_order_ab.json)
+  // [set][h][16][Apad + 4]: the row pitch Apad + 4 puts the 16 rows' lanes on distinct banks
+  float* SH = lds;
+  const int pitch = Ap + 4;
+  const int per4 = kRows * Ap / 4;   // float4s of one (set, head) block of rows
+  const int n4 = 3 * H * per4;
+  int64_t jrow = 0;
+  if (tid < kRows * K) jrow = row_index(a, b0 + (tid & 15));
+  int64_t jw = 0;   // wave 7: the rows' words for learn_apply
+  const bool wrow = tid >= 64 * (kWaves - 1) && tid - 64 * (kWaves - 1) < kRows;
+  if (wrow) jw = row_index(a, b0 + tid - 64 * (kWaves - 1));
+  constexpr int kHeadPre = 4;   // head float4s per thread issued ahead (n4 <= 2048: every K <= 3 shape
+                                // with N <= 31; more in the loop below)
+  float4 hv[kHeadPre];
+  auto head_src = [&](int e) __attribute__((always_inline)) {
+    const int sh = e / per4, f = e - sh * per4;   // sh = set * H + h
+    return reinterpret_cast<const float4*>(a.heads + ((size_t)sh * B + b0) * Ap)[f];
+  };
+  auto head_dst = [&](int e) __attribute__((always_inline)) {
+    const int sh = e / per4, f = e - sh * per4;
+    const int r = f / (Ap / 4), c = f - r * (Ap / 4);
+    return reinterpret_cast<float4*>(SH + ((size_t)sh * kRows + r) * pitch + 4 * c);
+  };
+#pragma unroll
+  for (int k = 0; k < kHeadPre; ++k) hv[k] = head_src(min(tid + kThreads * k, n4 - 1));
+  int ak = 0;
+  float rwj = 0.f, dnj = 0.f;
+  if (tid < kRows * K) {
+    ak = a.act[(size_t)jrow * K + (tid >> 4)];
+    rwj = a.rew[jrow];
+    dnj = (float)a.done[jrow];
+  }
+  if (wrow) {
+    const int b = b0 + tid - 64 * (kWaves - 1);
+    const int tg = a.tgt[jw];
+    for (int w = 0; w < a.W; ++w) {
+      a.srow[(size_t)w * B + b] = a.st[(size_t)w * a.cap + jw];
+      a.trow[(size_t)w * B + b] = tg < a.n_attr ? a.att_first[(size_t)tg * a.W + w] : 0u;
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // the weight fragments of the first four backward layers: second head layers (tiles wave, wave
+  // + 8 of H x 4), the first head layers split four ways per output tile (wave & 1 = tile, wave >> 1
+  // = quarter of the 4 H blocks), 32 -> 64 (waves < 4) and 64 -> 128
   const int at16 = Ap / 16;
   float wh2[2][2][4], wh1[8][4], w4[2][4], w3[4][4];
 #pragma unroll
@@ -539,43 +583,18 @@ __global__ void __launch_bounds__(kThreads) learn_bwd_kernel(LearnArgs a) {
     yh2[u] = act_frag(a.hh, (tt >> 2) * kDH + 16 * (tt & 3), B, b0, lane);
     y1v[u] = act_frag(a.y1, 16 * (wave + kWaves * u), B, b0, lane);
   }
+  __builtin_amdgcn_sched_barrier(0);
   PBN_LSTAMP(1, 1);
 
   // the TD error per (row, branch): bdq_update / update_policy (:111-126) on the raw heads.  The
   // block's head rows of the three sets come into LDS (coalesced; the staging area is the delta
   // planes', written only after this pass), then thread (row r, branch k) runs the duelings and
   // the online argmax over s' as sequential sums (the order of pbn_bdq_td_loss).
-  // [set][h][16][Apad + 4]: the row pitch Apad + 4 puts the 16 rows' lanes on distinct banks
-  float* SH = lds;
-  const int pitch = Ap + 4;
-  {
-    const int per4 = kRows * Ap / 4;   // float4s of one (set, head) block of rows
-    for (int e = tid; e < 3 * H * per4; e += kThreads) {
-      const int sh = e / per4, f = e - sh * per4;   // sh = set * H + h
-      const int r = f / (Ap / 4), c = f - r * (Ap / 4);
-      *reinterpret_cast<float4*>(SH + ((size_t)sh * kRows + r) * pitch + 4 * c) =
-          reinterpret_cast<const float4*>(a.heads + ((size_t)sh * B + b0) * Ap)[f];
-    }
-  }
-  int64_t jrow = 0;
-  int ak = 0;
-  float rwj = 0.f, dnj = 0.f;
-  if (tid < kRows * K) {
-    jrow = row_index(a, b0 + (tid & 15));
-    ak = a.act[(size_t)jrow * K + (tid >> 4)];
-    ak = ak < 0 ? 0 : (ak >= A ? A - 1 : ak);
-    rwj = a.rew[jrow];
-    dnj = (float)a.done[jrow];
-  }
-  if (tid >= 64 * (kWaves - 1) && tid - 64 * (kWaves - 1) < kRows) {   // wave 7: the rows' words for learn_apply
-    const int r = tid - 64 * (kWaves - 1), b = b0 + r;
-    const int64_t j = row_index(a, b);
-    const int tg = a.tgt[j];
-    for (int w = 0; w < a.W; ++w) {
-      a.srow[(size_t)w * B + b] = a.st[(size_t)w * a.cap + j];
-      a.trow[(size_t)w * B + b] = tg < a.n_attr ? a.att_first[(size_t)tg * a.W + w] : 0u;
-    }
-  }
+#pragma unroll
+  for (int k = 0; k < kHeadPre; ++k)
+    if (tid + kThreads * k < n4) *head_dst(tid + kThreads * k) = hv[k];
+  for (int e = tid + kThreads * kHeadPre; e < n4; e += kThreads) *head_dst(e) = head_src(e);
+  ak = ak < 0 ? 0 : (ak >= A ? A - 1 : ak);
   lds_barrier();
   PBN_LSTAMP(1, 2);
   if (tid < kRows * K) {
