@@ -219,7 +219,7 @@ typedef struct pbn_ring_store {
   float* d_reward;             /* [capacity] */
   uint8_t* d_done;             /* [capacity] */
   const int32_t* d_actions_in; /* [n_envs][n_branches] */
-  int32_t n_branches;
+  int32_t n_branches;          /* 1..8 */
   uint32_t done_mask;
   uint8_t* d_done_out;         /* nullable: [n_envs] */
 } pbn_ring_store;

@@ -921,9 +921,9 @@ static int step_impl(pbn_net* net, uint64_t seed, uint64_t step, const uint64_t*
     const pbn_ring_store& r = *ring;
     if (net->settle_max >= 2) return fail(PBN_EINVAL, "pbn_step_dev_store: the one-update law only (settle_max < 2)");
     if (r.capacity < n_envs) return fail(PBN_EINVAL, "pbn_ring_store: capacity < n_envs");
-    if (r.n_branches < 0 || r.n_branches > 64) return fail(PBN_EINVAL, "pbn_ring_store: n_branches 0..64");
+    if (r.n_branches < 1 || r.n_branches > kRingMaxK) return fail(PBN_EINVAL, "pbn_ring_store: n_branches 1..8");
     if (!r.d_pos || ((uintptr_t)r.d_pos & 7u) || !r.d_state || !r.d_next_state || !r.d_target || !r.d_reward ||
-        !r.d_done || (r.n_branches > 0 && (!r.d_action || !r.d_actions_in)))
+        !r.d_done || !r.d_action || !r.d_actions_in)
       return fail(PBN_EINVAL, "pbn_ring_store: null or misaligned buffer");
     a.r_state = r.d_state;
     a.r_next = r.d_next_state;

@@ -129,6 +129,8 @@ struct StepArgs {
 
 typedef unsigned int pbn_u32x4 __attribute__((ext_vector_type(4)));
 
+constexpr int kRingMaxK = 8;   // pbn_step_dev_store: branch actions per env (BDQ: K + 1 <= kMaxHeads)
+
 // In-kernel phase clocks (cdna_hip_programming.md section 7, "In-kernel stamps"):
 // compiled only into the diagnostic library (-DPBN_STAMPS), never the product.
 #ifdef PBN_STAMPS
@@ -1035,24 +1037,36 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   uint32_t tt0 = 0, tg0 = 0;
 #pragma unroll
   for (int w = 0; w < W; ++w) st[w] = 0;
-  if (live) {   // (waves past the end only help copy the tables)
+  if (live) {   // (waves past the end only help copy the tables; the bits past N are cleared after
+                // the barrier: an AND here waited for the load ahead of the records and the image)
 #pragma unroll
-    for (int w = 0; w < W; ++w) st[w] = a.state[CK((size_t)w * n + le, plane, 1)] & valid_word_mask(N, w);
+    for (int w = 0; w < W; ++w) st[w] = a.state[CK((size_t)w * n + le, plane, 1)];
     tt0 = a.t[CK(le, n, 2)];
     tg0 = a.target[CK(le, n, 3)];
   }
-  // pbn_step_dev_store: the transition's row, and what the step reads (s, the target, the branch
-  // actions) into it now; s' (before an autoreset), the reward and done after the step
-  int64_t rj = 0;
-  if constexpr (!SETTLE) {
-    if (live && a.r_state) {
-      rj = (int64_t)(((uint64_t)*a.r_pos + (uint64_t)le) % (uint64_t)a.r_cap);
+  // pbn_step_dev_store: the transition's row, and the env's branch actions requested now
+  // (unguarded, clamped: a guarded load's select would wait for it here, ahead of the node records
+  // and the table image); the row is written after the step (s, the target, the actions, s'
+  // before an autoreset, the reward, done)
+  // one-step launches: the step index (pbn_step_dev) and the env's flip mask requested here too
+  // (after the barrier each was a round trip of its own before the Philox calls and the update)
+  uint64_t step_pre = a.step;
+  uint32_t mpre[W];
+  if constexpr (SINGLE) {
+    if (a.step_ptr) step_pre = *a.step_ptr;
+    const int64_t lc = le < n ? le : n - 1;   // (unguarded; random-action launches ignore it)
 #pragma unroll
-      for (int w = 0; w < W; ++w) a.r_state[CK((size_t)w * a.r_cap + rj, (size_t)W * a.r_cap, 40)] = st[w];
-      a.r_target[CK(rj, a.r_cap, 41)] = (uint8_t)tg0;
-      for (int k = 0; k < a.r_k; ++k)
-        a.r_action[CK((size_t)rj * a.r_k + k, (size_t)a.r_cap * a.r_k, 42)] =
-            a.r_act_in[CK((size_t)le * a.r_k + k, (size_t)n * a.r_k, 43)];
+    for (int w = 0; w < W; ++w) mpre[w] = a.flipmask[CK((size_t)w * n + lc, plane, 6)];
+  }
+  int64_t rj = 0;
+  int32_t rav[kRingMaxK];
+  if constexpr (!SETTLE) {
+    if (a.r_state) {
+      rj = (int64_t)(((uint64_t)*a.r_pos + (uint64_t)le) % (uint64_t)a.r_cap);
+      const int64_t lc = le < n ? le : n - 1;
+#pragma unroll
+      for (int k = 0; k < kRingMaxK; ++k)
+        rav[k] = a.r_act_in[CK((size_t)lc * a.r_k + (k < a.r_k ? k : a.r_k - 1), (size_t)n * a.r_k, 43)];
     }
   }
   // node l32 + 32r: its first kNodeRecs compact records {inputs, table, threshold, meta}
@@ -1068,6 +1082,9 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   copy_image(L, a);
   __syncthreads();   // the kernel's only block barrier
   if (g >= a.n_groups) return;  // whole wave
+#pragma unroll
+  for (int w = 0; w < W; ++w) st[w] &= valid_word_mask(N, w);
+  asm volatile("" : "+v"(tt0), "+v"(tg0));   // (their first uses here, not hoisted above the barrier)
   const uint4* selq = reinterpret_cast<const uint4*>(L + a.sel_off);
 
   const int n_steps = SINGLE ? 1 : a.n_steps;
@@ -1088,9 +1105,7 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
   }
   const uint32_t kk0 = k0, kk1 = k1, ge_lo = (uint32_t)ge, G_lo = (uint32_t)G;
   uint64_t step = a.step + (uint64_t)ks;
-  if constexpr (SINGLE) {
-    if (a.step_ptr) step = *a.step_ptr;   // graph-replayable single step (pbn_step_dev)
-  }
+  if constexpr (SINGLE) step = step_pre;   // (by value, or pbn_step_dev's device step index)
   const uint32_t st_lo = (uint32_t)step;
   const uint32_t st_hi = (uint32_t)((step >> 32) & 0xFFFFu) << 16;
   const uint32_t ge_hi = (uint32_t)((ge >> 32) & 0xFFFFu) | st_hi;
@@ -1178,7 +1193,8 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
     } else if (live) {
 #pragma unroll
       for (int w = 0; w < W; ++w)
-        m[w] = a.flipmask[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 6)] & valid_word_mask(N, w);
+        m[w] = (SINGLE ? mpre[w] : a.flipmask[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 6)]) &
+               valid_word_mask(N, w);
     }
 #pragma unroll
     for (int w = 0; w < W; ++w) {
@@ -1259,9 +1275,16 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) pbn_step_wave(StepArgs a)
     for (int w = 0; w < W; ++w) a.final_state[CK(ks * plane + (size_t)w * n + le, (size_t)n_steps * plane, 10)] = sp[w];
   }
   if constexpr (!SETTLE) {
-    if (a.r_state) {
+    if (a.r_state) {   // (st and tg0 are still the step's inputs here: the autoreset comes below)
 #pragma unroll
-      for (int w = 0; w < W; ++w) a.r_next[CK((size_t)w * a.r_cap + rj, (size_t)W * a.r_cap, 44)] = sp[w];
+      for (int w = 0; w < W; ++w) {
+        a.r_state[CK((size_t)w * a.r_cap + rj, (size_t)W * a.r_cap, 40)] = st[w];
+        a.r_next[CK((size_t)w * a.r_cap + rj, (size_t)W * a.r_cap, 44)] = sp[w];
+      }
+      a.r_target[CK(rj, a.r_cap, 41)] = (uint8_t)tg0;
+#pragma unroll
+      for (int k = 0; k < kRingMaxK; ++k)
+        if (k < a.r_k) a.r_action[CK((size_t)rj * a.r_k + k, (size_t)a.r_cap * a.r_k, 42)] = rav[k];
     }
   }
   const bool in_attr = att >= 0;
