@@ -770,27 +770,6 @@ __device__ __forceinline__ float adam_apply(const LearnArgs& a, int64_t i, AdamI
   return p;
 }
 
-// T[t][i][o] = sum_j target_t[j] W[o][i][j] in j order (pbn_bdq_pack computes the same sums), from
-// the target's first-state words tw and the weight row in LDS (eight reads in flight)
-// (the words as a uint4 by value: as an array the run-time word select made it a stack array, and
-// each word's load waited to be stored to scratch)
-__device__ __forceinline__ float table_entry(uint4 tw, int N, const float* __restrict__ wrow) {
-  float s = 0.f;
-  for (int j0 = 0; j0 < N; j0 += 8) {
-    float x[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) x[u] = wrow[min(j0 + u, N - 1)];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int j = j0 + u;
-      const uint32_t word = (j >> 5) == 0 ? tw.x : (j >> 5) == 1 ? tw.y : (j >> 5) == 2 ? tw.z : tw.w;
-      const bool on = j < N && ((word >> (j & 31)) & 1u);
-      s += on ? x[u] : 0.f;
-    }
-  }
-  return s;
-}
-
 __device__ __forceinline__ uint4 target_words(const LearnArgs& a, int t) {
   uint32_t tw[4];
 #pragma unroll
@@ -884,9 +863,7 @@ __global__ void __launch_bounds__(64 * kApplyWaves) learn_apply_kernel(LearnArgs
         pre[jt][v] = adam_load_ahead(a, a.off[BIL_W] + (o0 + 4 * g + v) * NN + (int64_t)i * a.N + jj);
       }
     const AdamIn preb = adam_load_ahead(a, a.off[BIL_B] + o0 + rr);   // (applied by i == 0, g == 0)
-    uint4 tpre[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) tpre[u] = target_words_ahead(a, g + 4 * u);   // (used for t < n_attr)
+    const uint4 tw0 = target_words_ahead(a, rr);   // target rr's words: the first table tile (t < n_attr)
     __builtin_amdgcn_sched_barrier(0);
     for (int r0 = 0; r0 < B; r0 += 16 * RC) {
       if (r0 > 0) round_loads(r0);
@@ -931,14 +908,24 @@ __global__ void __launch_bounds__(64 * kApplyWaves) learn_apply_kernel(LearnArgs
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // the target-table rows of input i for these 16 outputs, from the weights just written
+    // the target-table rows of input i for these 16 outputs, from the weights just written, 16
+    // targets per MFMA tile: D[o][t] = sum_j W[o][i][j] x_t[j], j ascending through the k-steps
+    // (the f32 MFMA is an fmaf chain, and x_t[j] is 0 or 1: pack_kernel's sequential sums bit for
+    // bit).  A operand lane (g, r): W[o = r][j = s + g] from this wave's LDS rows; B: x_{t0 + r}[s + g]
+    for (int t0 = 0; t0 < a.n_attr; t0 += 16) {
+      const int t = t0 + rr;
+      const uint4 tw = t0 == 0 ? tw0 : target_words(a, t);
+      f32x4 d = {0.f, 0.f, 0.f, 0.f};
+      for (int s4 = 0; s4 < a.N; s4 += 4) {
+        const int j = s4 + g;
+        const uint32_t word = (j >> 5) == 0 ? tw.x : (j >> 5) == 1 ? tw.y : (j >> 5) == 2 ? tw.z : tw.w;
+        const bool in = j < a.N;
+        d = mfma(in ? wsc[wave][rr][j] : 0.f, (in && t < a.n_attr && ((word >> (j & 31)) & 1u)) ? 1.f : 0.f, d);
+      }
+      if (t < a.n_attr) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int t = g + 4 * u;
-      if (t < a.n_attr) a.Tq[((size_t)t * a.N + i) * 256 + rr * 16 + ot] = table_entry(tpre[u], a.N, &wsc[wave][rr][0]);
-    }
-    for (int t = g + 16; t < a.n_attr; t += 4) {
-      a.Tq[((size_t)t * a.N + i) * 256 + rr * 16 + ot] = table_entry(target_words(a, t), a.N, &wsc[wave][rr][0]);
+        for (int v = 0; v < 4; ++v) a.Tq[((size_t)t * a.N + i) * 256 + (4 * g + v) * 16 + ot] = d[v];
+      }
     }
     PBN_LSTAMP(2, 3);
     return;
