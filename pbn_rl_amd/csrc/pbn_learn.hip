@@ -525,8 +525,11 @@ __global__ void __launch_bounds__(kThreads) learn_bwd_kernel(LearnArgs a) {
   const int pitch = Ap + 4;
   const int per4 = kRows * Ap / 4;   // float4s of one (set, head) block of rows
   const int n4 = 3 * H * per4;
+  // the TD pass: four lanes per (row r, branch k) pair p = tid >> 2 (r = p & 15, k = p >> 4)
+  const bool tdl = tid < 4 * kRows * K;
+  const int tp = tid >> 2, tq = tid & 3;
   int64_t jrow = 0;
-  if (tid < kRows * K) jrow = row_index(a, b0 + (tid & 15));
+  if (tdl) jrow = row_index(a, b0 + (tp & 15));
   int64_t jw = 0;   // wave 7: the rows' words for learn_apply
   const bool wrow = tid >= 64 * (kWaves - 1) && tid - 64 * (kWaves - 1) < kRows;
   if (wrow) jw = row_index(a, b0 + tid - 64 * (kWaves - 1));
@@ -546,8 +549,8 @@ __global__ void __launch_bounds__(kThreads) learn_bwd_kernel(LearnArgs a) {
   for (int k = 0; k < kHeadPre; ++k) hv[k] = head_src(min(tid + kThreads * k, n4 - 1));
   int ak = 0;
   float rwj = 0.f, dnj = 0.f;
-  if (tid < kRows * K) {
-    ak = a.act[(size_t)jrow * K + (tid >> 4)];
+  if (tdl) {
+    ak = a.act[(size_t)jrow * K + (tp >> 4)];
     rwj = a.rew[jrow];
     dnj = (float)a.done[jrow];
   }
@@ -597,54 +600,70 @@ __global__ void __launch_bounds__(kThreads) learn_bwd_kernel(LearnArgs a) {
   ak = ak < 0 ? 0 : (ak >= A ? A - 1 : ak);
   lds_barrier();
   PBN_LSTAMP(1, 2);
-  if (tid < kRows * K) {
-    const int r = tid & 15, k = tid >> 4;
+  if (tdl) {
+    const int r = tp & 15, k = tp >> 4;
     auto hrow = [&](int set, int h) { return SH + ((size_t)(set * H + h) * kRows + r) * pitch; };
     const float* adv0 = hrow(0, k + 1);
     const float* adv1 = hrow(1, k + 1);
     const float* adv2 = hrow(2, k + 1);
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-    for (int o0 = 0; o0 < A; o0 += 8) {   // eight LDS reads of each row in flight, added in order
-      float x0[8], x1[8], x2[8];
+    // the three duelings' means: lane tq < 3 sums set tq's row in order (eight LDS reads in
+    // flight, the next eight requested before these are added); the means to every lane of the pair
+    const float* mine = tq == 0 ? adv0 : (tq == 1 ? adv1 : adv2);
+    float ssum = 0.f;
+    float xc[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int o = min(o0 + u, A - 1);
-        x0[u] = adv0[o];
-        x1[u] = adv1[o];
-        x2[u] = adv2[o];
-      }
+    for (int u = 0; u < 8; ++u) xc[u] = mine[min(u, A - 1)];
+    for (int o0 = 0; o0 < A; o0 += 8) {
+      float xn[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (o0 + u < A) {
-          s0 += x0[u];
-          s1 += x1[u];
-          s2 += x2[u];
-        }
-      }
+      for (int u = 0; u < 8; ++u) xn[u] = mine[min(o0 + 8 + u, A - 1)];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (o0 + u < A) ssum += xc[u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) xc[u] = xn[u];
     }
-    const float m0 = s0 / (float)A, m1 = s1 / (float)A, m2 = s2 / (float)A;
+    const float mq = ssum / (float)A;   // (lane 3: a fourth copy of set 2's, unused)
+    const int l0 = lane & ~3;
+    const float m0 = __shfl(mq, l0), m1 = __shfl(mq, l0 + 1), m2 = __shfl(mq, l0 + 2);
+    // the online argmax over s' (torch.argmax: first maximum, NaN is the maximum): each lane scans
+    // a quarter of actions 1 .. A-1 with the sequential rule, then the quarters are combined in
+    // order with the same rule (which makes the combination the sequential scan's result)
     const float v1 = hrow(1, 0)[0];
-    float best = (v1 + adv1[0]) - m1;
+    const int seg = (A - 1 + 3) / 4, lo = 1 + tq * seg, hi = min(lo + seg, A);
+    bool have = lo < hi;
+    float best = 0.f;
     int am = 0;
-    for (int o0 = 1; o0 < A; o0 += 8) {   // torch.argmax: first maximum, NaN is the maximum
-      float x1[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) x1[u] = adv1[min(o0 + u, A - 1)];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const float qo = (v1 + x1[u]) - m1;
-        const bool take = o0 + u < A && !isnan(best) && (isnan(qo) || qo > best);
+    if (have) {
+      best = (v1 + adv1[lo]) - m1;
+      am = lo;
+      for (int o = lo + 1; o < hi; ++o) {
+        const float qo = (v1 + adv1[o]) - m1;
+        const bool take = !isnan(best) && (isnan(qo) || qo > best);
         best = take ? qo : best;
-        am = take ? o0 + u : am;
+        am = take ? o : am;
       }
     }
-    const float current = (hrow(0, 0)[0] + adv0[ak]) - m0;
-    const float tnext = (hrow(2, 0)[0] + adv2[am]) - m2;
-    const float expected = rwj + (tnext * a.gamma) * dnj;
-    const float d = expected - current;
-    sd[r * K + k] = d * d;
-    sg[r * K + k] = 2.f * (current - expected) / (float)(B * K);
-    sact[r * K + k] = ak;
+    float gbest = (v1 + adv1[0]) - m1;
+    int gam = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float b = __shfl(best, l0 + q);
+      const int ai = __shfl(am, l0 + q);
+      const bool h = __shfl((int)have, l0 + q) != 0;
+      const bool take = h && !isnan(gbest) && (isnan(b) || b > gbest);
+      gbest = take ? b : gbest;
+      gam = take ? ai : gam;
+    }
+    if (tq == 0) {
+      const float current = (hrow(0, 0)[0] + adv0[ak]) - m0;
+      const float tnext = (hrow(2, 0)[0] + adv2[gam]) - m2;
+      const float expected = rwj + (tnext * a.gamma) * dnj;
+      const float d = expected - current;
+      sd[r * K + k] = d * d;
+      sg[r * K + k] = 2.f * (current - expected) / (float)(B * K);
+      sact[r * K + k] = ak;
+    }
   }
   PBN_LSTAMP(1, 3);
   lds_barrier();

@@ -21,7 +21,8 @@ STAMP_LIB = os.path.join(ROOT, "pbn_rl_amd", "libpbn_env_stamps.so")
 ROW, BLOCKS, WAVES = 32, 1024, 8
 POINTS = {
     "fwd": ["entry", "rows", "bilinear", "bilinear_sync", "L2", "L2_sync", "L3_sync", "L4_sync", "H1_sync", "end"],
-    "bwd": ["entry", "frags_issued", "td_loaded", "td_done", "td_sync", "H2", "H2_sync", "H1_sync", "L3_sync", "end"],
+    "bwd": ["entry", "frags_issued", "td_loaded", "td_done", "td_sync", "H2", "H2_sync", "H1_sync", "L3_sync", "end",
+            "td_sums", "td_argmax"],
     "apply": ["entry", "bil_loop", "bil_adam", "bil_table", "dense_loop", "dense_end"],
 }
 
