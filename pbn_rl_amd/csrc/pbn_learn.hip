@@ -308,9 +308,10 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
     scnt[tid] = c;
   }
   if (wave == 0) fetch_weights();
+  // (unconditional: past the biases into a spare slot; a branch here made the wait counter's merge
+  // hold the first barrier for every weight fragment)
 #pragma unroll
-  for (int k = 0; k < 4; ++k)
-    if (tid + kThreads * k < nbias) sbias[tid + kThreads * k] = bv[k];
+  for (int k = 0; k < 4; ++k) sbias[min(tid + kThreads * k, nbias)] = bv[k];
   lds_barrier();
   PBN_LSTAMP(0, 1);
   // bilinear layer: y[o] = bias[o] + sum over the set bits i of T[t][i][o] (t = the row's target;
@@ -325,17 +326,26 @@ __global__ void __launch_bounds__(kThreads) learn_fwd_kernel(LearnArgs a) {
     float4 acc[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
     const int cm = max(c0, c1);
     if (cm > 0) {
-      const float* T0 = Tq + (size_t)(c0 ? t0 : 0) * a.N * 256 + 4 * lane;
-      const float* T1 = Tq + (size_t)(c1 ? t1 : 0) * a.N * 256 + 4 * lane;
       const uint8_t* l0 = slist + r0 * 128;
       const uint8_t* l1 = l0 + 128;
+      // buffer loads: a lane past its row's count gets an out-of-range offset, whose load returns
+      // zeros without memory traffic (it read table row 0 before: ~35 % of the reads at 14-17 bits)
+      const int tb0 = __builtin_amdgcn_readfirstlane(c0 ? t0 : 0), tb1 = __builtin_amdgcn_readfirstlane(c1 ? t1 : 0);
+      const int nrec = a.N * 256 * 4;
+      __amdgpu_buffer_rsrc_t R0 = __builtin_amdgcn_make_buffer_rsrc((void*)(Tq + (size_t)tb0 * a.N * 256), (short)0, nrec, 0x00020000);
+      __amdgpu_buffer_rsrc_t R1 = __builtin_amdgcn_make_buffer_rsrc((void*)(Tq + (size_t)tb1 * a.N * 256), (short)0, nrec, 0x00020000);
       for (int p0 = 0; p0 < cm; p0 += 8) {
         float4 x0[8], x1[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int p = p0 + u;
-          x0[u] = *reinterpret_cast<const float4*>(T0 + (size_t)(p < c0 ? l0[p] : 0) * 256);
-          x1[u] = *reinterpret_cast<const float4*>(T1 + (size_t)(p < c1 ? l1[p] : 0) * 256);
+          const int i0 = l0[min(p, 127)], i1 = l1[min(p, 127)];
+          const int o0 = p < c0 ? (i0 * 256 + 4 * lane) * 4 : 0x40000000;
+          const int o1 = p < c1 ? (i1 * 256 + 4 * lane) * 4 : 0x40000000;
+          auto v0 = __builtin_amdgcn_raw_buffer_load_b128(R0, o0, 0, 0);
+          auto v1 = __builtin_amdgcn_raw_buffer_load_b128(R1, o1, 0, 0);
+          x0[u] = *reinterpret_cast<float4*>(&v0);
+          x1[u] = *reinterpret_cast<float4*>(&v1);
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
@@ -1324,7 +1334,7 @@ int pbn_bdq_learn(const pbn_net* net, int64_t batch, const int64_t* d_idx, int64
   const hipStream_t s = (hipStream_t)stream;
   const int tiles = (int)(batch / kRows);
   const size_t lds_f = ((size_t)(kD0 + kD1 + kD2 + kD3 + kDH * H) * kRows + 4 * kRows + 2 * kRows) * sizeof(float) +
-                       kRows * 128 + (size_t)fwd_bias_floats(H, A) * sizeof(float);
+                       kRows * 128 + (size_t)(fwd_bias_floats(H, A) + 1) * sizeof(float);
   if (lds_f > 64 * 1024 && hipFuncSetAttribute((const void*)learn_fwd_kernel,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_f) != hipSuccess)
     return pbn::set_error(PBN_EDEVICE, "hipFuncSetAttribute failed");
